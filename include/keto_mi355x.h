@@ -1,0 +1,207 @@
+/*
+ * keto_mi355x.h -- C-ABI of the MI355X batched check / expand engine.
+ *
+ * This is the drop-in boundary for Keto's read hot path.  Each entry point replaces one
+ * reference interface (paths relative to the reference tree, icyphox/keto = ory/keto v0.8.1):
+ *
+ *   keto_snapshot_build      replaces the per-node SQL reads the engines issue through
+ *                            relationtuple.Manager.GetRelationTuples
+ *                            (internal/relationtuple/definitions.go:29;
+ *                             internal/persistence/sql/relationtuples.go:238-277) with one
+ *                            immutable CSR snapshot built from a full scan of keto_relation_tuples
+ *                            in the same ORDER BY (relationtuples.go:250).
+ *   keto_check_batch         replaces check.(*Engine).SubjectIsAllowed
+ *                            (internal/check/engine.go:116-123), batched.
+ *   keto_expand_batch        replaces expand.(*Engine).BuildTree
+ *                            (internal/expand/engine.go:33-102), batched.
+ *   keto_tree_*              replace the expand.Tree value and its JSON codec
+ *                            (internal/expand/tree.go:26-30,156-163).
+ *
+ * All strings are borrowed (keto_str = pointer + length, not NUL-terminated) and only read
+ * during the call.  The library keeps no caller pointers after a call returns.  A snapshot is
+ * immutable after keto_snapshot_build and may be shared by concurrent *_batch calls.
+ * Every call returns KETO_OK (0) or a negative KETO_E_* code; keto_last_error() then holds a
+ * thread-local message.  There is no CPU fallback inside the library: when the HIP runtime or a
+ * device is missing, compute calls fail with KETO_E_HIP.
+ */
+#ifndef KETO_MI355X_H
+#define KETO_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KETO_ABI_VERSION 1
+
+/* return codes */
+#define KETO_OK 0
+#define KETO_E_INVALID (-1)     /* bad argument */
+#define KETO_E_HIP (-2)         /* HIP runtime / device error, or no device */
+#define KETO_E_NOMEM (-3)       /* host or device allocation failed */
+#define KETO_E_CONFIG (-4)      /* namespace config not supported (duplicate ids or names) */
+#define KETO_E_RANGE (-5)       /* a size limit of the snapshot format was exceeded */
+
+/* per-query status of keto_check_batch (allowed_out is always valid) */
+#define KETO_CHECK_OK 0                 /* decision equals the reference engine's */
+#define KETO_CHECK_UNKNOWN_NAMESPACE 1  /* request namespace unknown: reference returns false (engine.go:98-100) */
+
+/* per-root status of keto_expand_batch */
+#define KETO_EXPAND_TREE 0              /* a tree (BuildTree returned a non-nil *Tree) */
+#define KETO_EXPAND_NIL 1               /* BuildTree returned nil, nil (JSON null) */
+#define KETO_EXPAND_NOT_FOUND 2         /* BuildTree returned herodot.ErrNotFound (unknown namespace, A.Q8/Q9) */
+
+/* node types of an expand tree (internal/expand/tree.go:16-23; only union and leaf are produced) */
+#define KETO_NODE_UNION 0
+#define KETO_NODE_LEAF 1
+
+typedef struct {
+    const char* p;
+    uint32_t n;
+} keto_str;
+
+/* namespace.Namespace{ID, Name} (internal/namespace/definitions.go:9-13), in config order */
+typedef struct {
+    int32_t id;
+    keto_str name;
+} keto_namespace;
+
+/* one row of keto_relation_tuples (internal/persistence/sql/relationtuples.go:19-31).
+ * Array order = commit order (commit_time ties are broken by position). */
+typedef struct {
+    int32_t namespace_id;
+    keto_str object;
+    keto_str relation;
+    uint8_t subject_kind;       /* 0 = subject_id, 1 = subject set */
+    keto_str subject_id;        /* kind 0 */
+    int32_t set_namespace_id;   /* kind 1 */
+    keto_str set_object;        /* kind 1 */
+    keto_str set_relation;      /* kind 1 */
+} keto_tuple;
+
+/* a Subject by name (internal/relationtuple/definitions.go:77-117) */
+typedef struct {
+    uint8_t kind;               /* 0 = SubjectID, 1 = SubjectSet */
+    keto_str id;                /* kind 0 */
+    keto_str set_namespace;     /* kind 1 */
+    keto_str set_object;
+    keto_str set_relation;
+} keto_subject;
+
+/* check request = InternalRelationTuple + request max-depth (CheckRequest, check_service.proto) */
+typedef struct {
+    keto_str namespace_;
+    keto_str object;
+    keto_str relation;
+    keto_subject subject;
+    int32_t max_depth;          /* <= 0 or > global -> global (engine.go:118-120) */
+} keto_check_req;
+
+/* pre-resolved check request (keto_resolve_checks), 16 bytes; the form the device consumes */
+typedef struct {
+    uint32_t row;               /* top-level row, or KETO_NO_ROW */
+    uint32_t target;            /* subject: ID string id, or row id of a subject set, or KETO_NO_TARGET */
+    uint32_t flags;             /* bit0: target is a subject set */
+    int32_t max_depth;          /* request max-depth (clamped on the device) */
+} keto_check_ids;
+#define KETO_NO_ROW 0xFFFFFFFFu
+#define KETO_NO_TARGET 0xFFFFFFFFu
+
+/* expand request (ExpandRequest, expand_service.proto) */
+typedef struct {
+    keto_subject subject;
+    int32_t max_depth;
+} keto_expand_req;
+
+/* one node of an expand tree in pre-order.  subject: bit31 set -> subject set (bits 0..30 = row
+ * id), else subject id (bits 0..30 = string id).  info: bit31 set -> leaf, bits 0..30 = number of
+ * children (all children follow in pre-order). */
+typedef struct {
+    uint32_t subject;
+    uint32_t info;
+} keto_tree_node;
+
+typedef struct {
+    uint32_t page_size;         /* 0 -> 100 (internal/persistence/sql/persister.go:46) */
+    int32_t device;             /* HIP device ordinal; -1 = host-only snapshot (no compute) */
+    uint32_t flags;             /* reserved, 0 */
+} keto_snapshot_opts;
+
+typedef struct keto_snapshot keto_snapshot;
+typedef struct keto_tree_arena keto_tree_arena;
+
+typedef struct {
+    uint64_t n_tuples;
+    uint64_t n_edges;           /* including materialized wildcard rows */
+    uint32_t n_rows;            /* real + empty + wildcard rows */
+    uint32_t n_real_rows;
+    uint32_t n_wildcard_rows;
+    uint32_t n_seq_rows;        /* rows on the ordered (collision / wildcard) path */
+    uint32_t n_poisoned_rows;
+    uint32_t n_strings;
+    uint32_t n_collision_keys;
+    uint64_t device_bytes;
+} keto_snapshot_stats;
+
+int keto_abi_version(void);
+const char* keto_last_error(void);
+
+/* Build a snapshot from the tuple table; sorts with the reference ORDER BY itself. */
+int keto_snapshot_build(const keto_namespace* namespaces, uint32_t n_namespaces, const keto_tuple* tuples,
+                        uint64_t n_tuples, const keto_snapshot_opts* opts, keto_snapshot** out);
+
+/* Bulk loader for pre-interned, pre-ordered data (synthetic / exported snapshots).
+ * row_ns/row_obj/row_rel: per row, namespace id and string ids; rows must be in
+ * (namespace_id, object bytes, relation bytes) order.  row_ptr: n_rows+1 offsets into edges.
+ * edges: per row, subject sets first (bit31 set, bits 0..30 = target row) in reference order, then
+ * subject ids (bits 0..30 = string id) in byte order.  strings: n_strings strings in byte order
+ * (string id = index).  The caller guarantees that no Subject.String() of two different subjects
+ * coincide and that every subject set resolves to a row (pass empty rows for dangling sets). */
+int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespaces, uint32_t n_rows,
+                           const int32_t* row_ns, const uint32_t* row_obj, const uint32_t* row_rel,
+                           const uint64_t* row_ptr, const uint32_t* edges, const keto_str* strings,
+                           uint32_t n_strings, const keto_snapshot_opts* opts, keto_snapshot** out);
+
+void keto_snapshot_release(keto_snapshot* s);
+int keto_snapshot_get_stats(const keto_snapshot* s, keto_snapshot_stats* out);
+
+/* Resolve named requests to device form; status_out gets KETO_CHECK_* (may be NULL). */
+int keto_resolve_checks(const keto_snapshot* s, const keto_check_req* reqs, uint32_t n, keto_check_ids* out,
+                        uint8_t* status_out);
+
+/* Batched SubjectIsAllowed.  allowed_out[i] = 0/1, status_out[i] = KETO_CHECK_* (may be NULL). */
+int keto_check_batch(keto_snapshot* s, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth,
+                     uint8_t* allowed_out, uint8_t* status_out);
+
+/* Same with pre-resolved requests in host memory. */
+int keto_check_batch_ids(keto_snapshot* s, const keto_check_ids* reqs, uint32_t n, int32_t global_max_depth,
+                         uint8_t* allowed_out);
+
+/* Same with requests and results resident in device memory of the snapshot's device; enqueued on
+ * `stream` (a hipStream_t, NULL = default stream).  Returns after enqueueing; results are ready
+ * when the stream is synchronized. */
+int keto_check_batch_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                            uint8_t* d_allowed_out, void* stream);
+
+/* Batched BuildTree.  The arena owns all trees; free it with keto_tree_arena_free. */
+int keto_expand_batch(keto_snapshot* s, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
+                      keto_tree_arena** out);
+void keto_tree_arena_free(keto_tree_arena* a);
+uint32_t keto_tree_count(const keto_tree_arena* a);
+int keto_tree_status(const keto_tree_arena* a, uint32_t i);
+/* pre-order nodes of tree i (NULL, *n = 0 for nil / error) */
+const keto_tree_node* keto_tree_nodes(const keto_tree_arena* a, uint32_t i, uint64_t* n_nodes);
+/* JSON of tree i exactly as Tree.MarshalJSON (internal/expand/tree.go:156-163); "null" for nil.
+ * Writes at most cap bytes (NUL-terminated) and returns the full length, or a negative code. */
+int64_t keto_tree_json(const keto_snapshot* s, const keto_tree_arena* a, uint32_t i, char* buf, uint64_t cap);
+
+/* String of a subject reference used in keto_tree_node.subject (Subject.String(), definitions.go:163-169). */
+int64_t keto_subject_string(const keto_snapshot* s, uint32_t subject, char* buf, uint64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KETO_MI355X_H */

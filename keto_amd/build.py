@@ -1,0 +1,48 @@
+"""Build recipe for the in-tree HIP library keto_amd/libketo_mi355x.so (gfx950 only)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libketo_mi355x.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+SOURCES = ["snapshot.cpp", "capi.cpp", "engine.hip"]
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, force=False):
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "snapshot.hpp"),
+                                                        os.path.join(HERE, "..", "include", "keto_mi355x.h")]
+    if not force and not _stale(OUT, deps):
+        return OUT
+    objs = []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(CSRC, src + ".o")
+        objs.append(obj)
+        if not force and not _stale(obj, [path, deps[-2], deps[-1]]):
+            continue
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, "-c", path, "-o", obj]
+        if src.endswith(".cpp"):
+            cmd = [HIPCC, *CXXFLAGS, "-x", "c++", "-c", path, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(verbose=True, force="--force" in sys.argv)

@@ -1,0 +1,281 @@
+"""ctypes binding of libketo_mi355x.so (include/keto_mi355x.h).
+
+Plumbing for tests and bench.py.  Loading fails loudly when the library is missing: there is no
+Python or CPU fallback of the engine anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libketo_mi355x.so")
+
+KETO_OK = 0
+CHECK_OK, CHECK_UNKNOWN_NAMESPACE = 0, 1
+EXPAND_TREE, EXPAND_NIL, EXPAND_NOT_FOUND = 0, 1, 2
+NO_ROW = 0xFFFFFFFF
+NO_TARGET = 0xFFFFFFFF
+
+EXPORTS = [
+    "keto_abi_version", "keto_last_error", "keto_snapshot_build", "keto_snapshot_from_csr",
+    "keto_snapshot_release", "keto_snapshot_get_stats", "keto_resolve_checks", "keto_check_batch",
+    "keto_check_batch_ids", "keto_check_batch_device", "keto_expand_batch", "keto_tree_arena_free",
+    "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
+]
+
+
+class KetoError(RuntimeError):
+    pass
+
+
+class KStr(C.Structure):
+    _fields_ = [("p", C.c_char_p), ("n", C.c_uint32)]
+
+
+class KNamespace(C.Structure):
+    _fields_ = [("id", C.c_int32), ("name", KStr)]
+
+
+class KTuple(C.Structure):
+    _fields_ = [("namespace_id", C.c_int32), ("object", KStr), ("relation", KStr), ("subject_kind", C.c_uint8),
+                ("subject_id", KStr), ("set_namespace_id", C.c_int32), ("set_object", KStr),
+                ("set_relation", KStr)]
+
+
+class KSubject(C.Structure):
+    _fields_ = [("kind", C.c_uint8), ("id", KStr), ("set_namespace", KStr), ("set_object", KStr),
+                ("set_relation", KStr)]
+
+
+class KCheckReq(C.Structure):
+    _fields_ = [("namespace_", KStr), ("object", KStr), ("relation", KStr), ("subject", KSubject),
+                ("max_depth", C.c_int32)]
+
+
+class KCheckIds(C.Structure):
+    _fields_ = [("row", C.c_uint32), ("target", C.c_uint32), ("flags", C.c_uint32), ("max_depth", C.c_int32)]
+
+
+CHECK_IDS_DTYPE = np.dtype([("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
+
+
+class KExpandReq(C.Structure):
+    _fields_ = [("subject", KSubject), ("max_depth", C.c_int32)]
+
+
+class KTreeNode(C.Structure):
+    _fields_ = [("subject", C.c_uint32), ("info", C.c_uint32)]
+
+
+class KOpts(C.Structure):
+    _fields_ = [("page_size", C.c_uint32), ("device", C.c_int32), ("flags", C.c_uint32)]
+
+
+class KStats(C.Structure):
+    _fields_ = [("n_tuples", C.c_uint64), ("n_edges", C.c_uint64), ("n_rows", C.c_uint32),
+                ("n_real_rows", C.c_uint32), ("n_wildcard_rows", C.c_uint32), ("n_seq_rows", C.c_uint32),
+                ("n_poisoned_rows", C.c_uint32), ("n_strings", C.c_uint32), ("n_collision_keys", C.c_uint32),
+                ("device_bytes", C.c_uint64)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KetoError(f"{LIB_PATH} is missing: build it with `python keto_amd/build.py` "
+                        "(the engine has no non-HIP implementation)")
+    lib = C.CDLL(LIB_PATH)
+    for name in EXPORTS:
+        if not hasattr(lib, name):
+            raise KetoError(f"{LIB_PATH} does not export {name}")
+    lib.keto_last_error.restype = C.c_char_p
+    lib.keto_tree_count.restype = C.c_uint32
+    lib.keto_tree_nodes.restype = C.POINTER(KTreeNode)
+    lib.keto_tree_json.restype = C.c_int64
+    lib.keto_subject_string.restype = C.c_int64
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != KETO_OK:
+        raise KetoError(f"keto error {rc}: {load().keto_last_error().decode(errors='replace')}")
+
+
+class _Keep:
+    """Keeps encoded strings alive while a call borrows them."""
+
+    def __init__(self):
+        self.items = []
+
+    def s(self, x: str) -> KStr:
+        b = x.encode()
+        self.items.append(b)
+        return KStr(b, len(b))
+
+
+def subject_struct(keep: _Keep, sub) -> KSubject:
+    """sub: ("id", str) or ("set", ns, obj, rel), or any object with .id / .namespace fields."""
+    if isinstance(sub, tuple):
+        if sub[0] == "id":
+            return KSubject(0, keep.s(sub[1]), KStr(None, 0), KStr(None, 0), KStr(None, 0))
+        return KSubject(1, KStr(None, 0), keep.s(sub[1]), keep.s(sub[2]), keep.s(sub[3]))
+    if hasattr(sub, "id"):
+        return KSubject(0, keep.s(sub.id), KStr(None, 0), KStr(None, 0), KStr(None, 0))
+    return KSubject(1, KStr(None, 0), keep.s(sub.namespace), keep.s(sub.object), keep.s(sub.relation))
+
+
+class Snapshot:
+    def __init__(self, handle, lib):
+        self.h = handle
+        self.lib = lib
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.keto_snapshot_release(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ builders
+    @classmethod
+    def build(cls, namespaces: Sequence[Tuple[int, str]], rows: Iterable[tuple], page_size=100, device=0):
+        """rows: (ns_id, obj, rel, sid) for subject ids, (ns_id, obj, rel, None, sns_id, sobj, srel) for sets,
+        in commit order."""
+        lib = load()
+        keep = _Keep()
+        ns = (KNamespace * max(1, len(namespaces)))(*[KNamespace(i, keep.s(n)) for i, n in namespaces])
+        rows = list(rows)
+        tt = (KTuple * max(1, len(rows)))()
+        for k, r in enumerate(rows):
+            t = tt[k]
+            t.namespace_id = r[0]
+            t.object = keep.s(r[1])
+            t.relation = keep.s(r[2])
+            if r[3] is not None:
+                t.subject_kind = 0
+                t.subject_id = keep.s(r[3])
+            else:
+                t.subject_kind = 1
+                t.set_namespace_id = r[4]
+                t.set_object = keep.s(r[5])
+                t.set_relation = keep.s(r[6])
+        h = C.c_void_p()
+        opts = KOpts(page_size, device, 0)
+        _check(lib.keto_snapshot_build(ns, len(namespaces), tt, C.c_uint64(len(rows)), C.byref(opts), C.byref(h)))
+        return cls(h, lib)
+
+    @classmethod
+    def from_csr(cls, namespaces, row_ns, row_obj, row_rel, row_ptr, edges, strings=None, page_size=100, device=0):
+        lib = load()
+        keep = _Keep()
+        ns = (KNamespace * max(1, len(namespaces)))(*[KNamespace(i, keep.s(n)) for i, n in namespaces])
+        row_ns = np.ascontiguousarray(row_ns, dtype=np.int32)
+        row_obj = np.ascontiguousarray(row_obj, dtype=np.uint32)
+        row_rel = np.ascontiguousarray(row_rel, dtype=np.uint32)
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        edges = np.ascontiguousarray(edges, dtype=np.uint32)
+        strs = None
+        n_str = 0
+        if strings is not None:
+            strs = (KStr * max(1, len(strings)))(*[keep.s(x) for x in strings])
+            n_str = len(strings)
+        h = C.c_void_p()
+        opts = KOpts(page_size, device, 0)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        _check(lib.keto_snapshot_from_csr(ns, len(namespaces), C.c_uint32(len(row_ns)), p(row_ns), p(row_obj),
+                                          p(row_rel), p(row_ptr), p(edges), strs, C.c_uint32(n_str),
+                                          C.byref(opts), C.byref(h)))
+        return cls(h, lib)
+
+    def stats(self) -> dict:
+        st = KStats()
+        _check(self.lib.keto_snapshot_get_stats(self.h, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in KStats._fields_}
+
+    # ------------------------------------------------------------------ check
+    def _check_reqs(self, keep, reqs):
+        arr = (KCheckReq * max(1, len(reqs)))()
+        for k, (ns, obj, rel, sub, depth) in enumerate(reqs):
+            arr[k].namespace_ = keep.s(ns)
+            arr[k].object = keep.s(obj)
+            arr[k].relation = keep.s(rel)
+            arr[k].subject = subject_struct(keep, sub)
+            arr[k].max_depth = depth
+        return arr
+
+    def check_batch(self, reqs, global_max_depth=5):
+        """reqs: list of (namespace, object, relation, subject, max_depth). Returns (allowed, status)."""
+        keep = _Keep()
+        arr = self._check_reqs(keep, reqs)
+        n = len(reqs)
+        allowed = np.zeros(max(1, n), dtype=np.uint8)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth),
+                                         allowed.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
+        return allowed[:n], status[:n]
+
+    def resolve_checks(self, reqs):
+        keep = _Keep()
+        arr = self._check_reqs(keep, reqs)
+        n = len(reqs)
+        out = np.zeros(max(1, n), dtype=CHECK_IDS_DTYPE)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_resolve_checks(self.h, arr, C.c_uint32(n), out.ctypes.data_as(C.c_void_p),
+                                            status.ctypes.data_as(C.c_void_p)))
+        return out[:n], status[:n]
+
+    def check_batch_ids(self, ids: np.ndarray, global_max_depth=5):
+        ids = np.ascontiguousarray(ids, dtype=CHECK_IDS_DTYPE)
+        n = len(ids)
+        allowed = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch_ids(self.h, ids.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                             C.c_int32(global_max_depth), allowed.ctypes.data_as(C.c_void_p)))
+        return allowed[:n]
+
+    def check_batch_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, global_max_depth=5, stream=0):
+        _check(self.lib.keto_check_batch_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
+                                                C.c_int32(global_max_depth), C.c_void_p(d_out_ptr),
+                                                C.c_void_p(stream)))
+
+    # ------------------------------------------------------------------ expand
+    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False):
+        """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes])."""
+        keep = _Keep()
+        n = len(reqs)
+        arr = (KExpandReq * max(1, n))()
+        for k, (sub, depth) in enumerate(reqs):
+            arr[k].subject = subject_struct(keep, sub)
+            arr[k].max_depth = depth
+        a = C.c_void_p()
+        _check(self.lib.keto_expand_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth), C.byref(a)))
+        out = []
+        try:
+            for i in range(n):
+                st = self.lib.keto_tree_status(a, C.c_uint32(i))
+                js = None
+                if st == EXPAND_TREE:
+                    ln = self.lib.keto_tree_json(self.h, a, C.c_uint32(i), None, C.c_uint64(0))
+                    buf = C.create_string_buffer(ln + 1)
+                    self.lib.keto_tree_json(self.h, a, C.c_uint32(i), buf, C.c_uint64(ln + 1))
+                    js = json.loads(buf.raw[:ln].decode())
+                item = (st, js)
+                if want_nodes:
+                    nn = C.c_uint64()
+                    ptr = self.lib.keto_tree_nodes(a, C.c_uint32(i), C.byref(nn))
+                    nodes = [(ptr[j].subject, ptr[j].info) for j in range(nn.value)] if nn.value else []
+                    item = (st, js, nodes)
+                out.append(item)
+        finally:
+            self.lib.keto_tree_arena_free(a)
+        return out

@@ -1,0 +1,403 @@
+// C-ABI of the engine (include/keto_mi355x.h): request resolution (names -> snapshot ids, the
+// role of whereQuery in internal/persistence/sql/relationtuples.go:178-198), batch dispatch to the
+// device engine, and the expand tree arena with its JSON codec (internal/expand/tree.go:85-163).
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "snapshot.hpp"
+
+using namespace keto;
+
+struct keto_snapshot {
+    std::unique_ptr<Snapshot> s;
+};
+
+struct keto_tree_arena {
+    ExpandResult r;
+    uint32_t ov_base = 0xFFFFFFFFu;
+    std::vector<RowKey> ov_keys;           // overlay roots (wildcard queries)
+    uint32_t extra_base = 0;               // subject-id strings not in the snapshot
+    std::vector<std::string> extra;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        g_err.clear();
+        return f();
+    } catch (const Error& e) {
+        g_err = e.msg;
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return KETO_E_NOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return KETO_E_INVALID;
+    }
+}
+
+void json_escape(std::string& o, std::string_view s) {
+    // encoding/json's HTMLEscape-compatible string encoding
+    static const char* hex = "0123456789abcdef";
+    o.push_back('"');
+    for (size_t i = 0; i < s.size();) {
+        unsigned char c = (unsigned char)s[i];
+        if (c < 0x80) {
+            if (c == '"' || c == '\\') {
+                o.push_back('\\');
+                o.push_back((char)c);
+            } else if (c == '\n') {
+                o += "\\n";
+            } else if (c == '\r') {
+                o += "\\r";
+            } else if (c == '\t') {
+                o += "\\t";
+            } else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+                o += "\\u00";
+                o.push_back(hex[c >> 4]);
+                o.push_back(hex[c & 15]);
+            } else {
+                o.push_back((char)c);
+            }
+            ++i;
+            continue;
+        }
+        // multi-byte UTF-8; invalid sequences become U+FFFD like encoding/json
+        int len = (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+        bool ok = len && i + len <= s.size();
+        uint32_t cp = 0;
+        if (ok) {
+            cp = c & (0x7F >> len);
+            for (int k = 1; k < len; ++k) {
+                unsigned char cc = (unsigned char)s[i + k];
+                if ((cc >> 6) != 2) { ok = false; break; }
+                cp = (cp << 6) | (cc & 0x3F);
+            }
+            if (ok && ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && (cp < 0x10000 || cp > 0x10FFFF)) ||
+                       (cp >= 0xD800 && cp <= 0xDFFF)))
+                ok = false;
+        }
+        if (!ok) {
+            o += "\\ufffd";
+            ++i;
+            continue;
+        }
+        if (cp == 0x2028 || cp == 0x2029) {
+            o += cp == 0x2028 ? "\\u2028" : "\\u2029";
+        } else {
+            o.append(s.substr(i, len));
+        }
+        i += len;
+    }
+    o.push_back('"');
+}
+
+struct SubjectFields {
+    bool set;
+    std::string id, ns, obj, rel;
+};
+
+SubjectFields fields_of(const Snapshot& S, const keto_tree_arena* a, uint32_t ref) {
+    SubjectFields f;
+    f.set = (ref & EDGE_SET) != 0;
+    uint32_t v = ref & EDGE_VAL;
+    if (!f.set) {
+        if (a && v >= a->extra_base && v - a->extra_base < a->extra.size()) f.id = a->extra[v - a->extra_base];
+        else if (v < S.strs.size()) f.id = S.strs[v];
+        return f;
+    }
+    if (a && v >= a->ov_base && v - a->ov_base < a->ov_keys.size()) {
+        const RowKey& k = a->ov_keys[v - a->ov_base];
+        if (k.ns != ANY_NS) {
+            auto it = S.ns_by_id.find((int32_t)k.ns);
+            if (it != S.ns_by_id.end()) f.ns = S.ns_names[it->second];
+        }
+        if (k.obj != ANY) f.obj = S.strs[k.obj];
+        if (k.rel != ANY) f.rel = S.strs[k.rel];
+        return f;
+    }
+    f.ns = S.row_field_ns(v);
+    f.obj = S.row_field(v, 1);
+    f.rel = S.row_field(v, 2);
+    return f;
+}
+
+void tree_json(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node* nd, uint64_t n, uint64_t& pos,
+               std::string& o) {
+    const keto_tree_node x = nd[pos++];
+    const bool leaf = (x.info & 0x80000000u) != 0;
+    const uint32_t nc = x.info & 0x7FFFFFFFu;
+    o += leaf ? "{\"type\":\"leaf\"" : "{\"type\":\"union\"";
+    if (!leaf && nc) {
+        o += ",\"children\":[";
+        for (uint32_t c = 0; c < nc && pos < n; ++c) {
+            if (c) o.push_back(',');
+            tree_json(S, a, nd, n, pos, o);
+        }
+        o.push_back(']');
+    }
+    SubjectFields f = fields_of(S, a, x.subject);
+    if (!f.set) {
+        o += ",\"subject_id\":";
+        json_escape(o, f.id);
+    } else {
+        o += ",\"subject_set\":{\"namespace\":";
+        json_escape(o, f.ns);
+        o += ",\"object\":";
+        json_escape(o, f.obj);
+        o += ",\"relation\":";
+        json_escape(o, f.rel);
+        o.push_back('}');
+    }
+    o.push_back('}');
+}
+
+int64_t copy_out(const std::string& s, char* buf, uint64_t cap) {
+    if (buf && cap) {
+        uint64_t k = std::min<uint64_t>(cap - 1, s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (int64_t)s.size();
+}
+
+// RelationQuery of a check request / of a subject set; see Snapshot::resolve_query
+keto_check_ids resolve_one(const Snapshot& S, const keto_check_req& q, uint8_t& status, bool& wild, RowKey& wkey) {
+    keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0, q.max_depth};
+    status = KETO_CHECK_OK;
+    wild = false;
+    int64_t row = S.resolve_query(sv(q.namespace_), sv(q.object), sv(q.relation), &wkey);
+    if (row == -2) status = KETO_CHECK_UNKNOWN_NAMESPACE;
+    else if (row == -3) wild = true;
+    else if (row >= 0) r.row = (uint32_t)row;
+    if (q.subject.kind == 0) {
+        int64_t sid = S.lookup_str(sv(q.subject.id));
+        if (sid >= 0) r.target = (uint32_t)sid;
+    } else {
+        int64_t t = S.resolve_query(sv(q.subject.set_namespace), sv(q.subject.set_object), sv(q.subject.set_relation));
+        if (t >= 0) {
+            r.target = (uint32_t)t;
+            r.flags = 1;
+        }
+    }
+    return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int keto_abi_version(void) { return KETO_ABI_VERSION; }
+
+const char* keto_last_error(void) { return g_err.c_str(); }
+
+int keto_snapshot_build(const keto_namespace* namespaces, uint32_t n_namespaces, const keto_tuple* tuples,
+                        uint64_t n_tuples, const keto_snapshot_opts* opts, keto_snapshot** out) {
+    return guarded([&] {
+        if (!out) throw Error{KETO_E_INVALID, "out == NULL"};
+        *out = nullptr;
+        keto_snapshot_opts o = opts ? *opts : keto_snapshot_opts{100, 0, 0};
+        auto h = std::make_unique<keto_snapshot>();
+        h->s = build_snapshot(namespaces, n_namespaces, tuples, n_tuples, o.page_size);
+        if (o.device >= 0) device_upload(*h->s, o.device);
+        *out = h.release();
+        return KETO_OK;
+    });
+}
+
+int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespaces, uint32_t n_rows,
+                           const int32_t* row_ns, const uint32_t* row_obj, const uint32_t* row_rel,
+                           const uint64_t* row_ptr, const uint32_t* edges, const keto_str* strings,
+                           uint32_t n_strings, const keto_snapshot_opts* opts, keto_snapshot** out) {
+    return guarded([&] {
+        if (!out) throw Error{KETO_E_INVALID, "out == NULL"};
+        *out = nullptr;
+        keto_snapshot_opts o = opts ? *opts : keto_snapshot_opts{100, 0, 0};
+        auto h = std::make_unique<keto_snapshot>();
+        h->s = build_snapshot_csr(namespaces, n_namespaces, n_rows, row_ns, row_obj, row_rel, row_ptr, edges, strings,
+                                  n_strings, o.page_size);
+        if (o.device >= 0) device_upload(*h->s, o.device);
+        *out = h.release();
+        return KETO_OK;
+    });
+}
+
+void keto_snapshot_release(keto_snapshot* s) { delete s; }
+
+int keto_snapshot_get_stats(const keto_snapshot* h, keto_snapshot_stats* out) {
+    return guarded([&] {
+        if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        const Snapshot& S = *h->s;
+        out->n_tuples = S.n_tuples;
+        out->n_edges = S.edges.size();
+        out->n_rows = S.n_rows();
+        out->n_real_rows = S.n_real_rows;
+        out->n_wildcard_rows = S.n_wild_rows;
+        out->n_seq_rows = S.n_seq_rows;
+        out->n_poisoned_rows = S.n_poisoned_rows;
+        out->n_strings = (uint32_t)S.strs.size();
+        out->n_collision_keys = S.n_coll_keys;
+        out->device_bytes = device_bytes(S);
+        return KETO_OK;
+    });
+}
+
+int keto_resolve_checks(const keto_snapshot* h, const keto_check_req* reqs, uint32_t n, keto_check_ids* out,
+                        uint8_t* status_out) {
+    return guarded([&] {
+        if (!h || (n && (!reqs || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        for (uint32_t i = 0; i < n; ++i) {
+            uint8_t st;
+            bool wild;
+            RowKey k;
+            out[i] = resolve_one(*h->s, reqs[i], st, wild, k);
+            if (wild) throw Error{KETO_E_INVALID, "request " + std::to_string(i) +
+                                                      " is a wildcard query that no stored subject set uses; "
+                                                      "pass it to keto_check_batch"};
+            if (status_out) status_out[i] = st;
+        }
+        return KETO_OK;
+    });
+}
+
+int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth,
+                     uint8_t* allowed_out, uint8_t* status_out) {
+    return guarded([&] {
+        if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        Snapshot& S = *h->s;
+        std::vector<keto_check_ids> ids(n);
+        Overlay ov;
+        ov.base = S.n_rows();
+        for (uint32_t i = 0; i < n; ++i) {
+            uint8_t st;
+            bool wild;
+            RowKey k;
+            ids[i] = resolve_one(S, reqs[i], st, wild, k);
+            if (wild) ids[i].row = overlay_row(S, ov, k);
+            if (status_out) status_out[i] = st;
+        }
+        device_check(S, ids.data(), n, global_max_depth, allowed_out, true, nullptr, &ov);
+        return KETO_OK;
+    });
+}
+
+int keto_check_batch_ids(keto_snapshot* h, const keto_check_ids* reqs, uint32_t n, int32_t global_max_depth,
+                         uint8_t* allowed_out) {
+    return guarded([&] {
+        if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_check(*h->s, reqs, n, global_max_depth, allowed_out, true, nullptr, nullptr);
+        return KETO_OK;
+    });
+}
+
+int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                            uint8_t* d_allowed_out, void* stream) {
+    return guarded([&] {
+        if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, false, stream, nullptr);
+        return KETO_OK;
+    });
+}
+
+int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
+                      keto_tree_arena** out) {
+    return guarded([&] {
+        if (!h || !out || (n && !reqs)) throw Error{KETO_E_INVALID, "NULL argument"};
+        *out = nullptr;
+        Snapshot& S = *h->s;
+        auto a = std::make_unique<keto_tree_arena>();
+        Overlay ov;
+        ov.base = S.n_rows();
+        a->ov_base = ov.base;
+        a->extra_base = (uint32_t)S.strs.size();
+        std::vector<uint32_t> root(n), flags(n), vid(n, 0);
+        std::vector<int32_t> depth(n);
+        std::vector<uint8_t> not_found(n, 0);
+        for (uint32_t i = 0; i < n; ++i) {
+            const keto_subject& sj = reqs[i].subject;
+            depth[i] = reqs[i].max_depth;
+            if (sj.kind == 0) {                                             // SubjectID -> Leaf
+                int64_t sid = S.lookup_str(sv(sj.id));
+                if (sid < 0) {
+                    sid = a->extra_base + a->extra.size();
+                    a->extra.emplace_back(sv(sj.id));
+                }
+                root[i] = (uint32_t)sid;
+                flags[i] = 0;
+                continue;
+            }
+            flags[i] = 1;
+            RowKey k;
+            int64_t r = S.resolve_query(sv(sj.set_namespace), sv(sj.set_object), sv(sj.set_relation), &k);
+            if (r == -2) {
+                not_found[i] = 1;
+                root[i] = KETO_NO_ROW;
+            } else if (r == -1) {
+                root[i] = KETO_NO_ROW;
+            } else if (r == -3) {
+                root[i] = overlay_row(S, ov, k);
+                std::string key = std::string(sv(sj.set_namespace)) + ":" + std::string(sv(sj.set_object)) + "#" +
+                                  std::string(sv(sj.set_relation));
+                vid[i] = S.vid_of_key(key);
+            } else {
+                root[i] = (uint32_t)r;
+                vid[i] = S.vid_of_row((uint32_t)r);
+            }
+        }
+        a->ov_keys = ov.keys;
+        device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r);
+        for (uint32_t i = 0; i < n; ++i)
+            if (not_found[i]) a->r.status[i] = KETO_EXPAND_NOT_FOUND;
+        *out = a.release();
+        return KETO_OK;
+    });
+}
+
+void keto_tree_arena_free(keto_tree_arena* a) { delete a; }
+
+uint32_t keto_tree_count(const keto_tree_arena* a) { return a ? (uint32_t)a->r.status.size() : 0; }
+
+int keto_tree_status(const keto_tree_arena* a, uint32_t i) {
+    if (!a || i >= a->r.status.size()) return KETO_E_INVALID;
+    return a->r.status[i];
+}
+
+const keto_tree_node* keto_tree_nodes(const keto_tree_arena* a, uint32_t i, uint64_t* n_nodes) {
+    if (n_nodes) *n_nodes = 0;
+    if (!a || i >= a->r.status.size() || a->r.status[i] != KETO_EXPAND_TREE) return nullptr;
+    uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+    if (n_nodes) *n_nodes = e - b;
+    return a->r.nodes.data() + b;
+}
+
+int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_t i, char* buf, uint64_t cap) {
+    if (!h || !a || i >= a->r.status.size()) return KETO_E_INVALID;
+    std::string o;
+    if (a->r.status[i] == KETO_EXPAND_NOT_FOUND) {
+        g_err = "Unknown namespace";
+        return KETO_E_INVALID;
+    }
+    if (a->r.status[i] != KETO_EXPAND_TREE) {
+        o = "null";
+    } else {
+        uint64_t b = a->r.offset[i], e = a->r.offset[i + 1], pos = 0;
+        tree_json(*h->s, a, a->r.nodes.data() + b, e - b, pos, o);
+    }
+    return copy_out(o, buf, cap);
+}
+
+int64_t keto_subject_string(const keto_snapshot* h, uint32_t subject, char* buf, uint64_t cap) {
+    if (!h) return KETO_E_INVALID;
+    SubjectFields f = fields_of(*h->s, nullptr, subject);
+    return copy_out(f.set ? f.ns + ":" + f.obj + "#" + f.rel : f.id, buf, cap);
+}
+
+}  // extern "C"

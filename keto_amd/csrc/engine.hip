@@ -1,0 +1,824 @@
+// MI355X (gfx950) device engine for batched check and expand.
+//
+// Kernels
+//   check_kernel<Stack>   exact, order-faithful depth-bounded DFS per request, one lane per
+//                         request (grid-stride over a persistent grid).  Reproduces
+//                         check.(*Engine).SubjectIsAllowed / checkOneIndirectionFurther /
+//                         subjectIsAllowed (internal/check/engine.go:36-123) including the
+//                         first-encounter visited map keyed by Subject.String()
+//                         (internal/x/graph/graph_utils.go:13-35) that is fresh for every
+//                         top-level tuple and shared below it.
+//   expand_kernel<FILL>   the same traversal for expand.(*Engine).BuildTree
+//                         (internal/expand/engine.go:33-102): one visited map per tree, counted
+//                         first (FILL=false) then written in pre-order (FILL=true).
+//
+// Memory traffic per row visit: one 16-B RowRec (dwordx4), the subject-set region scanned in
+// order, and for a requested subject id a binary search of the row's byte-ordered id region
+// (an id never changes the visited map unless its key collides, so only membership matters:
+// that is what makes the search exact).  Visited maps are per-lane open-addressing tables in HBM
+// tagged with an epoch, so starting a fresh map is one register increment, never a clear.
+// Tables that fill past 1/2 abort the request, which is re-run on a tier with larger tables;
+// the last tier is sized so it cannot overflow.  No request ever leaves the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+#include "snapshot.hpp"
+
+namespace keto {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t err__ = (x);                                                                     \
+        if (err__ != hipSuccess)                                                                    \
+            throw Error{KETO_E_HIP, std::string(#x) + ": " + hipGetErrorString(err__)};             \
+    } while (0)
+
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_OVERFLOW = 2;
+constexpr int EXP_TREE = 0, EXP_NIL = 1, EXP_ERROR = 2, EXP_OVERFLOW = 3;
+
+struct DevSnap {
+    const uint4* rows;
+    const uint32_t* edges;
+    const uint32_t* row_pp;
+    const uint64_t* coll;     // (key << 32) | vid ; empty = ~0
+    uint32_t coll_mask;       // 0 = no collisions
+};
+
+struct DevOverlay {           // batch-local wildcard rows (top-level / root only), ids >= base
+    const uint4* rows;
+    const uint32_t* edges;
+    const uint32_t* pp;
+    uint32_t base;            // 0xFFFFFFFF = none
+};
+
+__host__ __device__ inline uint32_t mix32(uint32_t k) {
+    k ^= k >> 16;
+    k *= 0x7feb352dU;
+    k ^= k >> 15;
+    k *= 0x846ca68bU;
+    k ^= k >> 16;
+    return k;
+}
+
+__device__ inline uint32_t coll_lookup(const DevSnap& s, uint32_t key) {
+    if (s.coll_mask == 0) return NONE32;
+    uint32_t i = mix32(key) & s.coll_mask;
+    for (;;) {
+        uint64_t e = s.coll[i];
+        if (e == ~0ull) return NONE32;
+        if ((uint32_t)(e >> 32) == key) return (uint32_t)e;
+        i = (i + 1) & s.coll_mask;
+    }
+}
+
+struct RowView {
+    uint64_t beg;
+    uint32_t n_sets, n_ids;
+    bool seq;
+};
+
+__device__ inline RowView load_row(const DevSnap& s, uint32_t r) {
+    uint4 v = s.rows[r];
+    RowView rv;
+    rv.beg = (uint64_t)v.x | ((uint64_t)(v.y & 0xFFu) << 32);
+    rv.seq = ((v.y >> 8) & ROW_SEQ) != 0;
+    rv.n_sets = v.z;
+    rv.n_ids = v.w;
+    return rv;
+}
+
+// lower_bound over the byte-ordered subject-id region
+__device__ inline bool find_id(const uint32_t* __restrict__ e, uint64_t b, uint32_t n, uint32_t t) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 8) {
+        uint32_t m = (lo + hi) >> 1;
+        if (e[b + m] < t) lo = m + 1; else hi = m;
+    }
+    for (uint32_t i = lo; i < hi; ++i) {
+        uint32_t v = e[b + i];
+        if (v >= t) return v == t;
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------ visited maps
+struct Visited {
+    uint64_t* tab;
+    uint32_t mask;
+    uint32_t epoch;
+    uint32_t count;
+    __device__ inline void fresh() {
+        if (epoch >= 0xFFFFFFFEu) {        // epoch wrap: clear this lane's table once
+            for (uint32_t i = 0; i <= mask; ++i) tab[i] = 0;
+            epoch = 0;
+        }
+        ++epoch;
+        count = 0;
+    }
+    // 0 = newly added, 1 = already present, 2 = table too full (request must move up a tier)
+    __device__ inline int test_add(uint32_t vid) {
+        uint32_t i = mix32(vid) & mask;
+        const uint64_t want = ((uint64_t)epoch << 32) | vid;
+        for (;;) {
+            uint64_t e = tab[i];
+            if ((uint32_t)(e >> 32) != epoch) {
+                if ((++count) * 2u > mask + 1u) return 2;
+                tab[i] = want;
+                return 0;
+            }
+            if (e == want) return 1;
+            i = (i + 1) & mask;
+        }
+    }
+};
+
+struct Frame {
+    uint64_t pos;
+    uint32_t left;
+    uint16_t k;
+    uint16_t seq;
+};
+
+template <int N>
+struct LocalStack {
+    Frame f[N];
+    __device__ inline Frame& operator[](int i) { return f[i]; }
+    __device__ static constexpr int cap() { return N; }
+};
+struct GlobalStack {
+    Frame* f;           // this lane's frames, stride 1
+    int n;
+    __device__ inline Frame& operator[](int i) { return f[i]; }
+    __device__ inline int cap() const { return n; }
+};
+
+// ------------------------------------------------------------------ check
+// Further(r0, k0) below a top-level tuple (engine.go:82-114 + :36-80), V already holds the
+// top-level subject.  Returns RES_TRUE / RES_FALSE / RES_OVERFLOW.
+template <class Stack>
+__device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool tset, Visited& V, Stack& st) {
+    const uint32_t tval = tset ? (EDGE_SET | T) : T;
+    int sp = 0;
+    {
+        RowView rv = load_row(s, r0);
+        if (!rv.seq) {
+            if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T)) return RES_TRUE;
+            st[0] = Frame{rv.beg, rv.n_sets, (uint16_t)k0, 0};
+        } else {
+            st[0] = Frame{rv.beg, rv.n_sets, (uint16_t)k0, 1};
+        }
+        sp = 1;
+    }
+    while (sp > 0) {
+        Frame& f = st[sp - 1];
+        if (f.left == 0) {
+            --sp;
+            continue;
+        }
+        const uint32_t e = s.edges[f.pos];
+        f.pos++;
+        f.left--;
+        if (e & EDGE_SET) {
+            uint32_t vid = e & EDGE_VAL;
+            if (f.seq) {
+                uint32_t c = coll_lookup(s, e);
+                if (c != NONE32) vid = c;
+            }
+            int t = V.test_add(vid);
+            if (t == 1) continue;
+            if (t == 2) return RES_OVERFLOW;
+            if (tset && e == tval) return RES_TRUE;
+            if (f.k >= 2) {
+                if (sp == st.cap()) return RES_OVERFLOW;
+                const uint16_t k = f.k - 1;
+                RowView rv = load_row(s, e & EDGE_VAL);
+                if (!rv.seq) {
+                    if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T)) return RES_TRUE;
+                    st[sp] = Frame{rv.beg, rv.n_sets, k, 0};
+                } else {
+                    st[sp] = Frame{rv.beg, rv.n_sets, k, 1};
+                }
+                ++sp;
+            }
+        } else {
+            // subject id inside an ordered (ROW_SEQ) row
+            uint32_t c = coll_lookup(s, e);
+            if (c != NONE32) {
+                int t = V.test_add(c);
+                if (t == 1) continue;
+                if (t == 2) return RES_OVERFLOW;
+            }
+            if (!tset && e == tval) return RES_TRUE;
+        }
+    }
+    return RES_FALSE;
+}
+
+// SubjectIsAllowed for one request (engine.go:116-123): depth clamp, then the top-level row
+// whose tuples each start a fresh visited map (shadowed ctx at engine.go:48).
+template <class Stack>
+__device__ int check_one(const DevSnap& s, const DevOverlay& ov, const keto_check_ids& q, int gmd, Visited& V,
+                         Stack& st) {
+    int d = q.max_depth;
+    if (d <= 0 || gmd < d) d = gmd;
+    if (q.row == KETO_NO_ROW || d <= 0 || q.target == KETO_NO_TARGET) return RES_FALSE;
+    const bool tset = (q.flags & 1u) != 0;
+    const uint32_t T = q.target;
+    const uint32_t tval = tset ? (EDGE_SET | T) : T;
+    const uint32_t* te = s.edges;
+    RowView rv;
+    if (q.row >= ov.base) {
+        DevSnap o{ov.rows, ov.edges, ov.pp, nullptr, 0};
+        rv = load_row(o, q.row - ov.base);
+        te = ov.edges;
+    } else {
+        rv = load_row(s, q.row);
+    }
+    if (!rv.seq) {
+        if (!tset && rv.n_ids && find_id(te, rv.beg + rv.n_sets, rv.n_ids, T)) return RES_TRUE;
+        for (uint32_t i = 0; i < rv.n_sets; ++i) {
+            const uint32_t e = te[rv.beg + i];
+            if (tset && e == tval) return RES_TRUE;
+            if (d >= 2) {
+                V.fresh();
+                V.test_add(e & EDGE_VAL);
+                int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st);
+                if (r != RES_FALSE) return r;
+            }
+        }
+    } else {
+        for (uint32_t i = 0; i < rv.n_sets; ++i) {
+            const uint32_t e = te[rv.beg + i];
+            if (e & EDGE_SET) {
+                if (tset && e == tval) return RES_TRUE;
+                if (d >= 2) {
+                    uint32_t vid = coll_lookup(s, e);
+                    if (vid == NONE32) vid = e & EDGE_VAL;
+                    V.fresh();
+                    V.test_add(vid);
+                    int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st);
+                    if (r != RES_FALSE) return r;
+                }
+            } else if (!tset && e == tval) {
+                return RES_TRUE;
+            }
+        }
+    }
+    return RES_FALSE;
+}
+
+struct TierArgs {
+    uint64_t* vtab;          // n_slots * (mask+1) entries
+    uint32_t mask;
+    uint32_t* slot_epoch;    // n_slots
+    Frame* gstack;           // n_slots * gstack_n (GlobalStack tiers only)
+    int gstack_n;
+    const uint32_t* in_list; // NULL = all requests [0, n)
+    const uint32_t* in_count;
+    uint32_t* out_list;      // overflowed requests
+    uint32_t* out_count;
+};
+
+template <class Stack>
+__global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
+                                                    uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    Visited V;
+    V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
+    V.mask = ta.mask;
+    V.epoch = ta.slot_epoch[slot];
+    V.count = 0;
+    Stack st;
+    if constexpr (std::is_same<Stack, GlobalStack>::value) {
+        st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
+        st.n = ta.gstack_n;
+    }
+    const uint32_t total = ta.in_list ? *ta.in_count : n;
+    for (uint32_t j = slot; j < total; j += stride) {
+        const uint32_t i = ta.in_list ? ta.in_list[j] : j;
+        const keto_check_ids qq = q[i];
+        int r = check_one(s, ov, qq, gmd, V, st);
+        if (r == RES_OVERFLOW) {
+            uint32_t at = atomicAdd(ta.out_count, 1u);
+            ta.out_list[at] = i;
+        } else {
+            allowed[i] = (uint8_t)r;
+        }
+    }
+    ta.slot_epoch[slot] = V.epoch;
+}
+
+// ------------------------------------------------------------------ expand
+struct ExpandOut {
+    keto_tree_node* nodes;   // FILL only
+    const uint64_t* offset;  // FILL only
+    uint64_t* count;         // count pass: nodes per root
+    uint8_t* status;
+};
+
+__device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint32_t subject, uint32_t info) {
+    if (fill) out[cnt] = keto_tree_node{subject, info};
+    ++cnt;
+}
+
+// BuildTree for one root (engine.go:33-102).  root: row id (root_flags bit0 = set) or string id.
+template <bool FILL, class Stack>
+__device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
+                          uint32_t root_vid, int d, Visited& V, keto_tree_node* out, uint64_t& cnt, Stack& st) {
+    if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
+        emit(out, cnt, FILL, root, 0x80000000u);
+        return EXP_TREE;
+    }
+    if (root == KETO_NO_ROW) return EXP_NIL;                // no tuples at all (:68-70)
+    V.fresh();
+    V.test_add(root_vid);
+    int sp = 0;
+    // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union pushed
+    auto open = [&](uint32_t r, int k) -> int {
+        const bool in_ov = r >= ov.base;     // only the root can live in the overlay
+        RowView rv;
+        uint32_t pp;
+        if (in_ov) {
+            DevSnap o{ov.rows, ov.edges, ov.pp, nullptr, 0};
+            rv = load_row(o, r - ov.base);
+            pp = ov.pp[r - ov.base];
+        } else {
+            rv = load_row(s, r);
+            pp = s.row_pp[r];
+        }
+        const uint32_t n_all = rv.n_sets + rv.n_ids;
+        if (pp == NO_PAGE && n_all == 0) return EXP_NIL;
+        if (pp == 0) return EXP_ERROR;                      // first page fails toInternal
+        if (k <= 1) {                                       // :72-75
+            emit(out, cnt, FILL, EDGE_SET | r, 0x80000000u);
+            return EXP_TREE;
+        }
+        if (pp != NO_PAGE) return EXP_ERROR;                // a later page fails
+        if (sp == st.cap()) return EXP_OVERFLOW;
+        emit(out, cnt, FILL, EDGE_SET | r, n_all);
+        st[sp] = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? 1 : 0) | (in_ov ? 2 : 0))};
+        ++sp;
+        return EXP_TREE;
+    };
+    int r0 = open(root, d);
+    if (r0 != EXP_TREE) return r0;
+    while (sp > 0) {
+        Frame& f = st[sp - 1];
+        if (f.left == 0) {
+            --sp;
+            continue;
+        }
+        const uint32_t e = (f.seq & 2) ? ov.edges[f.pos] : s.edges[f.pos];
+        f.pos++;
+        f.left--;
+        if (!(e & EDGE_SET)) {
+            emit(out, cnt, FILL, e, 0x80000000u);          // subject id child -> Leaf
+            continue;
+        }
+        const uint32_t c = e & EDGE_VAL;
+        uint32_t vid = c;
+        if (f.seq & 1) {
+            uint32_t cv = coll_lookup(s, e);
+            if (cv != NONE32) vid = cv;
+        }
+        const uint16_t k = f.k - 1;
+        int t = V.test_add(vid);
+        if (t == 2) return EXP_OVERFLOW;
+        if (t == 1) {                                       // visited -> nil -> Leaf(set)
+            emit(out, cnt, FILL, e, 0x80000000u);
+            continue;
+        }
+        int r = open(c, k);
+        if (r == EXP_NIL) emit(out, cnt, FILL, e, 0x80000000u);
+        else if (r != EXP_TREE) return r;
+    }
+    return EXP_TREE;
+}
+
+struct ExpandReq {
+    uint32_t root;
+    uint32_t flags;
+    uint32_t vid;
+    int32_t depth;
+};
+
+template <bool FILL, class Stack>
+__global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, const ExpandReq* __restrict__ q,
+                                                     uint32_t n, int gmd, ExpandOut o, TierArgs ta) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    Visited V;
+    V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
+    V.mask = ta.mask;
+    V.epoch = ta.slot_epoch[slot];
+    V.count = 0;
+    Stack st;
+    if constexpr (std::is_same<Stack, GlobalStack>::value) {
+        st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
+        st.n = ta.gstack_n;
+    }
+    const uint32_t total = ta.in_list ? *ta.in_count : n;
+    for (uint32_t j = slot; j < total; j += stride) {
+        const uint32_t i = ta.in_list ? ta.in_list[j] : j;
+        if (FILL && o.status[i] != EXP_TREE) continue;   // nil / error roots own no output
+        const ExpandReq rq = q[i];
+        int d = rq.depth;
+        if (d <= 0 || gmd < d) d = gmd;
+        uint64_t cnt = 0;
+        keto_tree_node* out = FILL ? o.nodes + o.offset[i] : nullptr;
+        int r = expand_one<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, st);
+        if (r == EXP_OVERFLOW) {
+            uint32_t at = atomicAdd(ta.out_count, 1u);
+            ta.out_list[at] = i;
+        } else if (!FILL) {
+            o.count[i] = r == EXP_TREE ? cnt : 0;
+            o.status[i] = (uint8_t)r;
+        }
+    }
+    ta.slot_epoch[slot] = V.epoch;
+}
+
+// ------------------------------------------------------------------ host side
+struct Tier {
+    uint32_t n_slots = 0;
+    uint32_t cap = 0;             // visited entries per slot (power of two)
+    int gstack_n = 0;             // 0 = local stack
+    uint64_t* vtab = nullptr;
+    uint32_t* slot_epoch = nullptr;
+    Frame* gstack = nullptr;
+};
+
+struct DeviceState {
+    int device = 0;
+    uint4* rows = nullptr;
+    uint32_t* edges = nullptr;
+    uint32_t* row_pp = nullptr;
+    uint64_t* coll = nullptr;
+    uint32_t coll_mask = 0;
+    uint64_t bytes = 0;
+    uint32_t vid_bound = 0;       // distinct visit ids that can exist (rows + collision classes)
+    std::mutex mu;                // one batch at a time per snapshot (workspaces are shared)
+    Tier tiers[3];
+    uint32_t* lists = nullptr;    // 2 overflow lists, capacity list_cap each
+    uint32_t* counters = nullptr; // 2 counters
+    uint64_t list_cap = 0;
+    hipStream_t stream = nullptr;
+
+    DevSnap view() const { return DevSnap{rows, edges, row_pp, coll, coll_mask}; }
+};
+
+namespace {
+
+template <class T>
+T* dmalloc(uint64_t n, uint64_t& acc) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&p, n * sizeof(T));
+    if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+    acc += n * sizeof(T);
+    return (T*)p;
+}
+
+uint32_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return (uint32_t)std::min<uint64_t>(p, 1ull << 31);
+}
+
+void free_tier(Tier& t) {
+    if (t.vtab) (void)hipFree(t.vtab);
+    if (t.slot_epoch) (void)hipFree(t.slot_epoch);
+    if (t.gstack) (void)hipFree(t.gstack);
+    t = Tier{};
+}
+
+void ensure_tier(DeviceState& D, int level, uint32_t n_slots, uint32_t cap, int gstack_n) {
+    Tier& t = D.tiers[level];
+    if (t.n_slots == n_slots && t.cap == cap && t.gstack_n == gstack_n) return;
+    free_tier(t);
+    uint64_t acc = 0;
+    t.n_slots = n_slots;
+    t.cap = cap;
+    t.gstack_n = gstack_n;
+    t.vtab = dmalloc<uint64_t>((uint64_t)n_slots * cap, acc);
+    HIP_OK(hipMemset(t.vtab, 0, (uint64_t)n_slots * cap * sizeof(uint64_t)));
+    t.slot_epoch = dmalloc<uint32_t>(n_slots, acc);
+    std::vector<uint32_t> ones(n_slots, 1u);
+    HIP_OK(hipMemcpy(t.slot_epoch, ones.data(), n_slots * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (gstack_n) t.gstack = dmalloc<Frame>((uint64_t)n_slots * gstack_n, acc);
+}
+
+void ensure_lists(DeviceState& D, uint64_t n) {
+    if (D.list_cap >= n && D.lists) return;
+    if (D.lists) (void)hipFree(D.lists);
+    if (!D.counters) {
+        uint64_t acc = 0;
+        D.counters = dmalloc<uint32_t>(4, acc);
+    }
+    uint64_t acc = 0;
+    D.list_cap = std::max<uint64_t>(n, 1024);
+    D.lists = dmalloc<uint32_t>(2 * D.list_cap, acc);
+}
+
+int hw_slots() {
+    // persistent grid: 256 CUs x 8 waves of 64 lanes; every lane owns one visited table
+    return 256 * 8 * 64;
+}
+
+TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, uint32_t* out_list,
+                   uint32_t* out_count) {
+    TierArgs a;
+    a.vtab = t.vtab;
+    a.mask = t.cap - 1;
+    a.slot_epoch = t.slot_epoch;
+    a.gstack = t.gstack;
+    a.gstack_n = t.gstack_n;
+    a.in_list = in_list;
+    a.in_count = in_count;
+    a.out_list = out_list;
+    a.out_count = out_count;
+    return a;
+}
+
+// stack depth needed for a global max-depth (check recursion holds <= d-1 frames, expand <= d)
+int needed_frames(int gmd) { return std::max(1, gmd); }
+
+}  // namespace
+
+void device_upload(Snapshot& S, int device) {
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev <= 0) throw Error{KETO_E_HIP, "no HIP device"};
+    if (device < 0 || device >= n_dev) throw Error{KETO_E_INVALID, "bad device ordinal"};
+    HIP_OK(hipSetDevice(device));
+    auto D = std::make_unique<DeviceState>();
+    D->device = device;
+    uint64_t acc = 0;
+    D->rows = dmalloc<uint4>(S.rows.size(), acc);
+    D->edges = dmalloc<uint32_t>(S.edges.size(), acc);
+    D->row_pp = dmalloc<uint32_t>(S.row_pp.size(), acc);
+    if (!S.rows.empty())
+        HIP_OK(hipMemcpy(D->rows, S.rows.data(), S.rows.size() * sizeof(RowRec), hipMemcpyHostToDevice));
+    if (!S.edges.empty())
+        HIP_OK(hipMemcpy(D->edges, S.edges.data(), S.edges.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (!S.row_pp.empty())
+        HIP_OK(hipMemcpy(D->row_pp, S.row_pp.data(), S.row_pp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (!S.coll.empty()) {
+        uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
+        std::vector<uint64_t> tab(cap, ~0ull);
+        for (auto& kv : S.coll) {
+            uint32_t i = mix32(kv.first) & (cap - 1);
+            while (tab[i] != ~0ull) i = (i + 1) & (cap - 1);
+            tab[i] = ((uint64_t)kv.first << 32) | kv.second;
+        }
+        D->coll = dmalloc<uint64_t>(cap, acc);
+        HIP_OK(hipMemcpy(D->coll, tab.data(), cap * sizeof(uint64_t), hipMemcpyHostToDevice));
+        D->coll_mask = cap - 1;
+    }
+    D->bytes = acc;
+    D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.rows.size() + S.n_coll_keys + 1);
+    HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+    S.device = device;
+    S.dev.reset(D.release());
+}
+
+void device_release(Snapshot& S) {
+    if (!S.dev) return;
+    DeviceState& D = *S.dev;
+    (void)hipSetDevice(D.device);
+    for (auto& t : D.tiers) free_tier(t);
+    if (D.rows) (void)hipFree(D.rows);
+    if (D.edges) (void)hipFree(D.edges);
+    if (D.row_pp) (void)hipFree(D.row_pp);
+    if (D.coll) (void)hipFree(D.coll);
+    if (D.lists) (void)hipFree(D.lists);
+    if (D.counters) (void)hipFree(D.counters);
+    if (D.stream) (void)hipStreamDestroy(D.stream);
+    S.dev.reset();
+}
+
+uint64_t device_bytes(const Snapshot& S) { return S.dev ? S.dev->bytes : 0; }
+
+Snapshot::~Snapshot() {
+    if (dev) device_release(*this);
+}
+
+void DeviceStateDeleter::operator()(DeviceState* d) const { delete d; }
+
+namespace {
+
+// Tier plan: 0 = every lane of a full persistent grid, small tables; 1 = fewer lanes, large
+// tables; 2 = a handful of lanes with tables that hold every visit id of the snapshot.
+struct Plan {
+    uint32_t slots[3];
+    uint32_t cap[3];
+    int frames[3];
+};
+
+Plan make_plan(const DeviceState& D, uint32_t n, int gmd) {
+    Plan p;
+    uint32_t full = pow2_at_least(2ull * D.vid_bound + 2);
+    p.slots[0] = (uint32_t)std::min<uint64_t>((uint64_t)hw_slots(), ((uint64_t)n + 255) / 256 * 256);
+    if (p.slots[0] == 0) p.slots[0] = 256;
+    p.cap[0] = std::min<uint32_t>(256, full);
+    p.slots[1] = 4096;
+    p.cap[1] = std::min<uint32_t>(1u << 15, full);
+    p.slots[2] = 64;
+    p.cap[2] = full;
+    int fr = needed_frames(gmd);
+    p.frames[0] = fr <= 16 ? 0 : std::min(fr, 64);   // 0 = LocalStack; deeper paths overflow upward
+    p.frames[1] = fr <= 16 ? 0 : std::min(fr, 256);
+    p.frames[2] = std::min<int>(fr, (int)std::min<uint64_t>(D.vid_bound + 2ull, 1u << 20));
+    if (p.frames[2] < 17) p.frames[2] = 17;
+    return p;
+}
+
+template <class Launch>
+void run_tiers(DeviceState& D, uint32_t n, const Plan& p, hipStream_t st, Launch launch) {
+    ensure_lists(D, n);
+    uint32_t* list0 = D.lists;
+    uint32_t* list1 = D.lists + D.list_cap;
+    uint32_t* c0 = D.counters;
+    uint32_t* c1 = D.counters + 1;
+    HIP_OK(hipMemsetAsync(D.counters, 0, 4 * sizeof(uint32_t), st));
+    // tier 0 over all requests
+    ensure_tier(D, 0, p.slots[0], p.cap[0], p.frames[0]);
+    launch(0, D.tiers[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
+    // tier 1 over tier-0 overflows (count read on the device)
+    ensure_tier(D, 1, p.slots[1], p.cap[1], p.frames[1]);
+    launch(1, D.tiers[1], list0, c0, list1, c1, p.slots[1]);
+    uint32_t left = 0;
+    HIP_OK(hipMemcpyAsync(&left, c1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (left) {
+        ensure_tier(D, 2, p.slots[2], p.cap[2], p.frames[2]);
+        HIP_OK(hipMemsetAsync(c0, 0, sizeof(uint32_t), st));
+        launch(2, D.tiers[2], list1, c1, list0, c0, p.slots[2]);
+        uint32_t still = 0;
+        HIP_OK(hipMemcpyAsync(&still, c0, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (still) throw Error{KETO_E_RANGE, "visited table overflow on the final tier"};
+    }
+}
+
+}  // namespace
+
+namespace {
+
+// batch-local overlay rows on the device (freed when the batch returns)
+struct OverlayBuf {
+    DevOverlay v{nullptr, nullptr, nullptr, 0xFFFFFFFFu};
+    void* p[3] = {nullptr, nullptr, nullptr};
+    OverlayBuf(const Overlay* ov) {
+        if (!ov || ov->empty()) return;
+        uint64_t acc = 0;
+        uint4* r = dmalloc<uint4>(ov->rows.size(), acc);
+        p[0] = r;
+        uint32_t* e = dmalloc<uint32_t>(ov->edges.size(), acc);
+        p[1] = e;
+        uint32_t* pp = dmalloc<uint32_t>(ov->pp.size(), acc);
+        p[2] = pp;
+        HIP_OK(hipMemcpy(r, ov->rows.data(), ov->rows.size() * sizeof(RowRec), hipMemcpyHostToDevice));
+        if (!ov->edges.empty())
+            HIP_OK(hipMemcpy(e, ov->edges.data(), ov->edges.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(pp, ov->pp.data(), ov->pp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        v = DevOverlay{r, e, pp, ov->base};
+    }
+    ~OverlayBuf() {
+        for (void* q : p)
+            if (q) (void)hipFree(q);
+    }
+};
+
+struct DevFree {
+    std::vector<void*> p;
+    ~DevFree() {
+        for (void* q : p)
+            if (q) (void)hipFree(q);
+    }
+};
+
+}  // namespace
+
+void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
+                  bool host_buffers, void* stream, const Overlay* ovh) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    if (n == 0) return;
+    if (gmd > 65535) gmd = 65535;
+    hipStream_t st = stream ? (hipStream_t)stream : D.stream;
+    OverlayBuf ov(ovh);
+    const keto_check_ids* dq = reqs;
+    uint8_t* da = allowed;
+    DevFree tmp;
+    if (host_buffers) {
+        uint64_t acc = 0;
+        keto_check_ids* tq = dmalloc<keto_check_ids>(n, acc);
+        tmp.p.push_back(tq);
+        uint8_t* ta8 = dmalloc<uint8_t>(n, acc);
+        tmp.p.push_back(ta8);
+        HIP_OK(hipMemcpyAsync(tq, reqs, (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice, st));
+        dq = tq;
+        da = ta8;
+    }
+    Plan p = make_plan(D, n, gmd);
+    DevSnap sv = D.view();
+    DevOverlay dov = ov.v;
+    run_tiers(D, n, p, st,
+              [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
+                  uint32_t slots) {
+                  TierArgs a = tier_args(t, il, ic, ol, oc);
+                  dim3 grid(slots / 256), block(256);
+                  if (p.frames[level] == 0)
+                      hipLaunchKernelGGL(check_kernel<LocalStack<16>>, grid, block, 0, st, sv, dov, dq, n, gmd, da,
+                                         a);
+                  else
+                      hipLaunchKernelGGL(check_kernel<GlobalStack>, grid, block, 0, st, sv, dov, dq, n, gmd, da, a);
+                  HIP_OK(hipGetLastError());
+              });
+    if (host_buffers) {
+        HIP_OK(hipMemcpyAsync(allowed, da, n, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
+}
+
+void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
+                   const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
+                   const Overlay* ovh, ExpandResult& out) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    const uint32_t n = (uint32_t)root.size();
+    out.status.assign(n, EXP_NIL);
+    out.offset.assign(n + 1, 0);
+    out.nodes.clear();
+    if (n == 0) return;
+    if (gmd > 65535) gmd = 65535;
+    hipStream_t st = D.stream;
+    OverlayBuf ov(ovh);
+    std::vector<ExpandReq> hq(n);
+    for (uint32_t i = 0; i < n; ++i) hq[i] = ExpandReq{root[i], root_flags[i], root_vid[i], depth[i]};
+    DevFree tmp;
+    uint64_t acc = 0;
+    ExpandReq* dq = dmalloc<ExpandReq>(n, acc);
+    tmp.p.push_back(dq);
+    uint64_t* dcount = dmalloc<uint64_t>(n + 1, acc);
+    tmp.p.push_back(dcount);
+    uint8_t* dstatus = dmalloc<uint8_t>(n, acc);
+    tmp.p.push_back(dstatus);
+    HIP_OK(hipMemcpy(dq, hq.data(), n * sizeof(ExpandReq), hipMemcpyHostToDevice));
+    Plan p = make_plan(D, n, gmd + 1);
+    DevSnap sv = D.view();
+    DevOverlay dov = ov.v;
+    ExpandOut o{nullptr, nullptr, dcount, dstatus};
+    auto launch_pass = [&](bool fill, const ExpandOut& eo) {
+        run_tiers(D, n, p, st,
+                  [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
+                      uint32_t slots) {
+                      TierArgs a = tier_args(t, il, ic, ol, oc);
+                      dim3 grid(slots / 256), block(256);
+                      const bool local = p.frames[level] == 0;
+                      if (!fill && local)
+                          hipLaunchKernelGGL((expand_kernel<false, LocalStack<17>>), grid, block, 0, st, sv, dov, dq,
+                                             n, gmd, eo, a);
+                      else if (!fill)
+                          hipLaunchKernelGGL((expand_kernel<false, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
+                                             gmd, eo, a);
+                      else if (local)
+                          hipLaunchKernelGGL((expand_kernel<true, LocalStack<17>>), grid, block, 0, st, sv, dov, dq,
+                                             n, gmd, eo, a);
+                      else
+                          hipLaunchKernelGGL((expand_kernel<true, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
+                                             gmd, eo, a);
+                      HIP_OK(hipGetLastError());
+                  });
+    };
+    // count pass, then exclusive scan on the host, then the fill pass (same tier plan: a root
+    // overflows on exactly the same tiers both times, and a partial pre-order is a prefix)
+    launch_pass(false, o);
+    std::vector<uint64_t> cnt(n);
+    HIP_OK(hipMemcpy(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(out.status.data(), dstatus, n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) out.offset[i + 1] = out.offset[i] + cnt[i];
+    const uint64_t total = out.offset[n];
+    out.nodes.resize(total);
+    if (total == 0) return;
+    keto_tree_node* dnodes = dmalloc<keto_tree_node>(total, acc);
+    tmp.p.push_back(dnodes);
+    uint64_t* doff = dmalloc<uint64_t>(n + 1, acc);
+    tmp.p.push_back(doff);
+    HIP_OK(hipMemcpy(doff, out.offset.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+    launch_pass(true, ExpandOut{dnodes, doff, dcount, dstatus});
+    HIP_OK(hipMemcpy(out.nodes.data(), dnodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost));
+}
+
+}  // namespace keto

@@ -1,0 +1,471 @@
+// Host-side snapshot builder: interning, reference ORDER BY, CSR, wildcard materialization,
+// poisoned-page detection and visit-key collision classes.
+//
+// What it reproduces (paths relative to the reference tree):
+//   * row order and edge order = ORDER BY nid, namespace_id, object, relation, subject_id,
+//     subject_set_namespace_id, subject_set_object, subject_set_relation, commit_time
+//     (internal/persistence/sql/relationtuples.go:250) under SQLite semantics: NULL first, so
+//     subject sets precede subject ids; TEXT compared byte-wise (BINARY collation).
+//   * whereQuery (relationtuples.go:178-198): an empty namespace/object/relation is no filter.
+//     Stored subject sets with empty fields become materialized "wildcard rows" whose edges
+//     are the concatenation of all matching rows in ORDER BY order.
+//   * toInternal (relationtuples.go:43-80): a row whose namespace id, or whose subject-set
+//     namespace id, is not configured fails its whole page with ErrNotFound.  check turns that
+//     into `false` for the node (internal/check/engine.go:98-100) -> the row is truncated at the
+//     first poisoned page; expand returns the error (internal/expand/engine.go:63-66).
+//   * visited identity is Subject.String() (internal/x/graph/graph_utils.go:13-35;
+//     internal/relationtuple/definitions.go:163-169): keys shared by two different subjects get
+//     a shared visit id ("collision class") and their rows take the ordered ROW_SEQ path.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <unordered_set>
+
+#include "snapshot.hpp"
+
+namespace keto {
+
+namespace {
+
+inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
+
+void load_namespaces(Snapshot& S, const keto_namespace* ns, uint32_t n_ns) {
+    if (n_ns && !ns) throw Error{KETO_E_INVALID, "namespaces == NULL"};
+    for (uint32_t i = 0; i < n_ns; ++i) {
+        std::string name(sv(ns[i].name));
+        if (S.ns_by_id.count(ns[i].id) || S.ns_by_name.count(name))
+            throw Error{KETO_E_CONFIG, "duplicate namespace id or name in config: " + name};
+        S.ns_by_id[ns[i].id] = (int)i;
+        S.ns_by_name[name] = (int)i;
+        S.ns_ids.push_back(ns[i].id);
+        S.ns_names.push_back(std::move(name));
+    }
+}
+
+struct Interner {
+    std::unordered_map<std::string_view, uint32_t> tmp;
+    std::vector<std::string_view> views;
+    uint32_t add(std::string_view s) {
+        auto it = tmp.find(s);
+        if (it != tmp.end()) return it->second;
+        uint32_t id = (uint32_t)views.size();
+        tmp.emplace(s, id);
+        views.push_back(s);
+        return id;
+    }
+    // sorts byte-wise; fills S.strs and returns remap old id -> rank
+    std::vector<uint32_t> finish(Snapshot& S) {
+        std::vector<uint32_t> order(views.size());
+        std::iota(order.begin(), order.end(), 0u);
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return views[a] < views[b]; });
+        std::vector<uint32_t> rank(views.size());
+        S.strs.resize(views.size());
+        for (uint32_t r = 0; r < order.size(); ++r) {
+            rank[order[r]] = r;
+            S.strs[r] = std::string(views[order[r]]);
+        }
+        return rank;
+    }
+};
+
+struct T {                    // one interned tuple
+    int32_t ns;
+    uint32_t obj, rel;
+    uint8_t kind;
+    uint32_t a;               // kind 0: sid ; kind 1: sobj
+    int32_t sns;
+    uint32_t srel;
+    uint64_t seq;             // commit order
+};
+
+bool tuple_less(const T& x, const T& y) {
+    if (x.ns != y.ns) return x.ns < y.ns;
+    if (x.obj != y.obj) return x.obj < y.obj;
+    if (x.rel != y.rel) return x.rel < y.rel;
+    // subject_id: NULL (sets) first
+    if (x.kind != y.kind) return x.kind == 1;
+    if (x.kind == 0) {
+        if (x.a != y.a) return x.a < y.a;
+    } else {
+        if (x.sns != y.sns) return x.sns < y.sns;
+        if (x.a != y.a) return x.a < y.a;
+        if (x.srel != y.srel) return x.srel < y.srel;
+    }
+    return x.seq < y.seq;
+}
+
+int64_t key_cmp(const RowKey& a, const RowKey& b) {
+    if (a.ns != b.ns) return a.ns < b.ns ? -1 : 1;
+    if (a.obj != b.obj) return a.obj < b.obj ? -1 : 1;
+    if (a.rel != b.rel) return a.rel < b.rel ? -1 : 1;
+    return 0;
+}
+
+// row flags + effective counts, once edges, poison pages and collision classes are known
+void finalize_rows(Snapshot& S, const std::vector<uint64_t>& row_ptr, const std::vector<uint8_t>& is_wild) {
+    uint32_t R = (uint32_t)row_ptr.size() - 1;
+    S.rows.resize(R);
+    S.n_seq_rows = 0;
+    S.n_poisoned_rows = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        uint64_t b = row_ptr[r], e = row_ptr[r + 1], n = e - b;
+        if (b >= (1ull << 40)) throw Error{KETO_E_RANGE, "more than 2^40 edges"};
+        uint32_t pp = S.row_pp[r];
+        uint64_t L = pp == NO_PAGE ? n : std::min<uint64_t>(n, (uint64_t)pp * S.page_size);
+        if (pp != NO_PAGE) S.n_poisoned_rows++;
+        bool seq = is_wild[r] != 0;
+        if (!seq && !S.coll.empty()) {
+            for (uint64_t k = b; k < b + L; ++k)
+                if (S.coll.count(S.edges[k])) { seq = true; break; }
+        }
+        RowRec rec;
+        rec.edge_lo = (uint32_t)b;
+        rec.hi_flags = (uint32_t)(b >> 32) | ((seq ? ROW_SEQ : 0u) << 8);
+        if (L > 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "row with more than 2^32 edges"};
+        if (seq) {
+            rec.n_sets = (uint32_t)L;
+            rec.n_ids = 0;
+            S.n_seq_rows++;
+        } else {
+            uint64_t ns = 0;
+            while (ns < L && (S.edges[b + ns] & EDGE_SET)) ++ns;
+            rec.n_sets = (uint32_t)ns;
+            rec.n_ids = (uint32_t)(L - ns);
+        }
+        S.rows[r] = rec;
+    }
+}
+
+}  // namespace
+
+int64_t Snapshot::lookup_str(std::string_view s) const {
+    auto it = std::lower_bound(strs.begin(), strs.end(), s,
+                               [](const std::string& a, std::string_view b) { return std::string_view(a) < b; });
+    if (it == strs.end() || std::string_view(*it) != s) return -1;
+    return it - strs.begin();
+}
+
+int64_t Snapshot::resolve_query(std::string_view ns, std::string_view obj, std::string_view rel,
+                                RowKey* key_out) const {
+    RowKey k;
+    if (ns.empty()) {
+        k.ns = ANY_NS;
+    } else {
+        auto it = ns_by_name.find(std::string(ns));
+        if (it == ns_by_name.end()) return -2;                                   // ErrNotFound
+        k.ns = ns_ids[it->second];
+    }
+    if (obj.empty()) k.obj = ANY;
+    else {
+        int64_t o = lookup_str(obj);
+        if (o < 0) return -1;          // no row can match an unknown string
+        k.obj = (uint32_t)o;
+    }
+    if (rel.empty()) k.rel = ANY;
+    else {
+        int64_t r = lookup_str(rel);
+        if (r < 0) return -1;
+        k.rel = (uint32_t)r;
+    }
+    if (key_out) *key_out = k;
+    if (k.ns != ANY_NS && k.obj != ANY && k.rel != ANY) {
+        // real rows are sorted: binary search
+        uint32_t lo = 0, hi = n_real_rows;
+        while (lo < hi) {
+            uint32_t m = lo + (hi - lo) / 2;
+            int64_t c = key_cmp(row_key[m], k);
+            if (c == 0) return m;
+            if (c < 0) lo = m + 1; else hi = m;
+        }
+    }
+    auto it = row_of.find(k);
+    if (it != row_of.end()) return it->second;
+    if (k.ns == ANY_NS || k.obj == ANY || k.rel == ANY) return -3;
+    return -1;
+}
+
+uint32_t Snapshot::vid_of_key(const std::string& key) const {
+    std::lock_guard<std::mutex> lk(key_mu);
+    if (!key_index) {
+        key_index = std::make_unique<std::unordered_map<std::string, uint32_t>>();
+        for (uint32_t r = 0; r < rows.size(); ++r) {
+            const RowKey& k = row_key[r];
+            if (k.ns != ANY_NS && !ns_by_id.count((int32_t)k.ns)) continue;
+            key_index->emplace(subject_string(EDGE_SET | r), vid_of_row(r));
+        }
+    }
+    auto it = key_index->find(key);
+    return it == key_index->end() ? 0xFFFFFFF0u : it->second;   // 0xFFFFFFF0: no snapshot subject
+}
+
+uint32_t overlay_row(const Snapshot& S, Overlay& ov, const RowKey& k) {
+    auto f = ov.map.find(k);
+    if (f != ov.map.end()) return f->second;
+    uint32_t id = ov.base + (uint32_t)ov.rows.size();
+    uint64_t b = ov.edges.size(), pos = 0;
+    uint32_t pp = NO_PAGE;
+    for (uint32_t q = 0; q < S.n_real_rows; ++q) {          // matching real rows in ORDER BY order
+        const RowKey& rk = S.row_key[q];
+        if ((k.ns != ANY_NS && rk.ns != k.ns) || (k.obj != ANY && rk.obj != k.obj) || (k.rel != ANY && rk.rel != k.rel))
+            continue;
+        uint64_t rb = S.row_begin(q);
+        uint64_t re = q + 1 < S.rows.size() ? S.row_begin(q + 1) : S.edges.size();
+        for (uint64_t i = rb; i < re; ++i, ++pos) {
+            if (S.edges[i] == EDGE_POISON && pp == NO_PAGE) pp = (uint32_t)(pos / S.page_size);
+            ov.edges.push_back(S.edges[i]);
+        }
+    }
+    uint64_t n = ov.edges.size() - b;
+    uint64_t L = pp == NO_PAGE ? n : std::min<uint64_t>(n, (uint64_t)pp * S.page_size);
+    RowRec rec;
+    rec.edge_lo = (uint32_t)b;
+    rec.hi_flags = (uint32_t)(b >> 32) | (ROW_SEQ << 8);
+    rec.n_sets = (uint32_t)L;
+    rec.n_ids = 0;
+    ov.rows.push_back(rec);
+    ov.pp.push_back(pp);
+    ov.keys.push_back(k);
+    ov.map.emplace(k, id);
+    return id;
+}
+
+uint32_t Snapshot::vid_of_row(uint32_t row) const {
+    if (coll.empty()) return row;
+    auto it = coll.find(EDGE_SET | row);
+    return it == coll.end() ? row : it->second;
+}
+
+std::string Snapshot::row_field_ns(uint32_t row) const {
+    const RowKey& k = row_key[row];
+    if (k.ns == ANY_NS) return "";
+    auto it = ns_by_id.find((int32_t)k.ns);
+    return it == ns_by_id.end() ? std::string() : ns_names[it->second];
+}
+
+std::string Snapshot::row_field(uint32_t row, int which) const {
+    uint32_t v = which == 1 ? row_key[row].obj : row_key[row].rel;
+    if (v == ANY || v >= strs.size()) return "";
+    return strs[v];
+}
+
+std::string Snapshot::subject_string(uint32_t ref) const {
+    if (ref & EDGE_SET) {
+        uint32_t r = ref & EDGE_VAL;
+        return row_field_ns(r) + ":" + row_field(r, 1) + "#" + row_field(r, 2);
+    }
+    return ref < strs.size() ? strs[ref] : std::string();
+}
+
+std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns, const keto_tuple* tup, uint64_t n,
+                                         uint32_t page_size) {
+    auto Sp = std::make_unique<Snapshot>();
+    Snapshot& S = *Sp;
+    S.page_size = page_size ? page_size : 100;
+    S.n_tuples = n;
+    load_namespaces(S, ns, n_ns);
+    if (n && !tup) throw Error{KETO_E_INVALID, "tuples == NULL"};
+
+    // ---- intern strings
+    Interner in;
+    uint32_t e_id = in.add("");
+    for (const auto& nm : S.ns_names) in.add(nm);
+    std::vector<T> ts(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        const keto_tuple& t = tup[i];
+        T& x = ts[i];
+        x.ns = t.namespace_id;
+        x.obj = in.add(sv(t.object));
+        x.rel = in.add(sv(t.relation));
+        x.kind = t.subject_kind ? 1 : 0;
+        x.seq = i;
+        if (x.kind == 0) {
+            x.a = in.add(sv(t.subject_id));
+            x.sns = 0;
+            x.srel = 0;
+        } else {
+            x.a = in.add(sv(t.set_object));
+            x.sns = t.set_namespace_id;
+            x.srel = in.add(sv(t.set_relation));
+        }
+    }
+    std::vector<uint32_t> rank = in.finish(S);
+    S.empty_str = rank[e_id];
+    for (auto& x : ts) {
+        x.obj = rank[x.obj];
+        x.rel = rank[x.rel];
+        x.a = rank[x.a];
+        if (x.kind == 1) x.srel = rank[x.srel];
+    }
+    in.tmp.clear();
+    in.views.clear();
+
+    // ---- reference ORDER BY
+    std::sort(ts.begin(), ts.end(), tuple_less);
+
+    // ---- real rows
+    std::vector<uint64_t> real_ptr;   // per real row begin (in tuple index space)
+    for (uint64_t i = 0; i < n; ++i) {
+        if (i == 0 || ts[i].ns != ts[i - 1].ns || ts[i].obj != ts[i - 1].obj || ts[i].rel != ts[i - 1].rel) {
+            real_ptr.push_back(i);
+            S.row_key.push_back(RowKey{ts[i].ns, ts[i].obj, ts[i].rel});
+        }
+    }
+    real_ptr.push_back(n);
+    if (real_ptr.size() - 1 >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "more than 2^31-1 rows"};
+    S.n_real_rows = (uint32_t)(real_ptr.size() - 1);
+
+    // ---- subject sets -> target rows (real, empty or wildcard)
+    std::vector<RowKey> wild_keys;          // wildcard rows, in creation order
+    std::vector<uint8_t> extra_is_wild;     // for rows >= n_real_rows
+    auto target_row = [&](int32_t sns, uint32_t sobj, uint32_t srel, bool& poison) -> uint32_t {
+        auto it = S.ns_by_id.find(sns);
+        if (it == S.ns_by_id.end()) { poison = true; return EDGE_POISON; }
+        poison = false;
+        const std::string& name = S.ns_names[it->second];
+        RowKey k{name.empty() ? ANY_NS : (int64_t)sns, sobj == S.empty_str ? ANY : sobj,
+                 srel == S.empty_str ? ANY : srel};
+        bool wild = k.ns == ANY_NS || k.obj == ANY || k.rel == ANY;
+        if (!wild) {
+            uint32_t lo = 0, hi = S.n_real_rows;
+            while (lo < hi) {
+                uint32_t m = lo + (hi - lo) / 2;
+                int64_t c = key_cmp(S.row_key[m], k);
+                if (c == 0) return m;
+                if (c < 0) lo = m + 1; else hi = m;
+            }
+        }
+        auto f = S.row_of.find(k);
+        if (f != S.row_of.end()) return f->second;
+        uint32_t id = (uint32_t)S.row_key.size();
+        if (id >= EDGE_VAL) throw Error{KETO_E_RANGE, "more than 2^31-1 rows"};
+        S.row_key.push_back(k);
+        S.row_of.emplace(k, id);
+        extra_is_wild.push_back(wild ? 1 : 0);
+        if (wild) wild_keys.push_back(k);
+        return id;
+    };
+
+    // ---- real-row edges
+    std::vector<uint32_t> real_edges(n);
+    std::vector<uint8_t> poison(n, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        const T& x = ts[i];
+        bool own_unknown = !S.ns_by_id.count(x.ns);
+        if (x.kind == 0) {
+            real_edges[i] = x.a;
+            poison[i] = own_unknown;
+        } else {
+            bool p;
+            uint32_t r = target_row(x.sns, x.a, x.srel, p);
+            real_edges[i] = p ? EDGE_POISON : (EDGE_SET | r);
+            poison[i] = p || own_unknown;
+        }
+        if (poison[i]) real_edges[i] = EDGE_POISON;
+    }
+    uint32_t R = (uint32_t)S.row_key.size();
+    S.n_wild_rows = (uint32_t)wild_keys.size();
+
+    // ---- assemble edges: real rows, then empty rows (no edges), then wildcard rows
+    std::vector<uint64_t> row_ptr(R + 1, 0);
+    S.row_pp.assign(R, NO_PAGE);
+    S.edges.reserve(n);
+    for (uint32_t r = 0; r < S.n_real_rows; ++r) {
+        row_ptr[r] = S.edges.size();
+        for (uint64_t i = real_ptr[r]; i < real_ptr[r + 1]; ++i) {
+            if (poison[i] && S.row_pp[r] == NO_PAGE) S.row_pp[r] = (uint32_t)((i - real_ptr[r]) / S.page_size);
+            S.edges.push_back(real_edges[i]);
+        }
+    }
+    std::vector<uint8_t> is_wild(R, 0);
+    for (uint32_t r = S.n_real_rows; r < R; ++r) {
+        row_ptr[r] = S.edges.size();
+        if (!extra_is_wild[r - S.n_real_rows]) continue;
+        is_wild[r] = 1;
+        const RowKey& k = S.row_key[r];
+        uint64_t pos = 0;
+        for (uint32_t q = 0; q < S.n_real_rows; ++q) {          // matching real rows in ORDER BY order
+            const RowKey& rk = S.row_key[q];
+            if ((k.ns != ANY_NS && rk.ns != k.ns) || (k.obj != ANY && rk.obj != k.obj) ||
+                (k.rel != ANY && rk.rel != k.rel))
+                continue;
+            for (uint64_t i = real_ptr[q]; i < real_ptr[q + 1]; ++i, ++pos) {
+                if (poison[i] && S.row_pp[r] == NO_PAGE) S.row_pp[r] = (uint32_t)(pos / S.page_size);
+                S.edges.push_back(real_edges[i]);
+            }
+        }
+    }
+    row_ptr[R] = S.edges.size();
+
+    // ---- visit-key collision classes over every typed subject: rows (sets) and subject ids
+    {
+        std::unordered_map<std::string, uint32_t> owners;   // key -> number of distinct typed subjects
+        std::vector<std::string> row_keys(R);
+        for (uint32_t r = 0; r < R; ++r) {
+            const RowKey& k = S.row_key[r];
+            if (k.ns != ANY_NS && !S.ns_by_id.count((int32_t)k.ns)) continue;   // unknown-ns rows are never subjects
+            row_keys[r] = S.subject_string(EDGE_SET | r);
+            owners[row_keys[r]]++;
+        }
+        std::vector<uint8_t> id_used(S.strs.size(), 0);
+        for (uint32_t e : S.edges)
+            if (!(e & EDGE_SET) && e != EDGE_POISON) id_used[e] = 1;
+        for (uint32_t s = 0; s < S.strs.size(); ++s)
+            if (id_used[s]) owners[S.strs[s]]++;
+        std::unordered_map<std::string, uint32_t> cls;
+        for (auto& kv : owners)
+            if (kv.second >= 2) cls.emplace(kv.first, (uint32_t)cls.size());
+        S.n_coll_keys = (uint32_t)cls.size();
+        if (!cls.empty()) {
+            for (uint32_t r = 0; r < R; ++r) {
+                if (row_keys[r].empty() && S.row_key[r].ns != ANY_NS) continue;
+                auto it = cls.find(row_keys[r]);
+                if (it != cls.end()) S.coll[EDGE_SET | r] = VID_CLASS | it->second;
+            }
+            for (uint32_t s = 0; s < S.strs.size(); ++s) {
+                if (!id_used[s]) continue;
+                auto it = cls.find(S.strs[s]);
+                if (it != cls.end()) S.coll[s] = VID_CLASS | it->second;
+            }
+        }
+    }
+
+    finalize_rows(S, row_ptr, is_wild);
+    return Sp;
+}
+
+std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t n_ns, uint32_t n_rows,
+                                             const int32_t* row_ns, const uint32_t* row_obj,
+                                             const uint32_t* row_rel, const uint64_t* row_ptr,
+                                             const uint32_t* edges, const keto_str* strings, uint32_t n_strings,
+                                             uint32_t page_size) {
+    auto Sp = std::make_unique<Snapshot>();
+    Snapshot& S = *Sp;
+    S.page_size = page_size ? page_size : 100;
+    load_namespaces(S, ns, n_ns);
+    if (!row_ns || !row_obj || !row_rel || !row_ptr || (row_ptr[n_rows] && !edges))
+        throw Error{KETO_E_INVALID, "NULL array"};
+    if (n_rows >= EDGE_VAL) throw Error{KETO_E_RANGE, "more than 2^31-1 rows"};
+    if (strings) {
+        S.strs.resize(n_strings);
+        for (uint32_t i = 0; i < n_strings; ++i) S.strs[i] = std::string(sv(strings[i]));
+        int64_t e = S.lookup_str("");
+        S.empty_str = e < 0 ? ANY : (uint32_t)e;
+    }
+    S.row_key.resize(n_rows);
+    for (uint32_t r = 0; r < n_rows; ++r) {
+        S.row_key[r] = RowKey{row_ns[r], row_obj[r], row_rel[r]};
+        if (r && key_cmp(S.row_key[r - 1], S.row_key[r]) >= 0)
+            throw Error{KETO_E_INVALID, "rows not in (namespace_id, object, relation) order"};
+    }
+    S.n_real_rows = n_rows;
+    uint64_t E = row_ptr[n_rows];
+    S.n_tuples = E;
+    S.edges.assign(edges, edges + E);
+    S.row_pp.assign(n_rows, NO_PAGE);
+    std::vector<uint64_t> rp(row_ptr, row_ptr + n_rows + 1);
+    std::vector<uint8_t> is_wild(n_rows, 0);
+    finalize_rows(S, rp, is_wild);
+    return Sp;
+}
+
+}  // namespace keto

@@ -1,0 +1,172 @@
+// Internal snapshot representation shared by the host builder (snapshot.cpp), the device
+// engine (engine.hip) and the C-ABI (capi.cpp).
+//
+// HBM layout (one copy per device, read-only after upload):
+//   rows   : RowRec[n_rows], 16 B each, one aligned dwordx4 load per row visit
+//   edges  : u32[n_edges]; bit31 = subject set (bits 0..30 = target row id),
+//            else subject id (bits 0..30 = string id)
+//   row_pp : u32[n_rows], first poisoned page (0-based) or NO_PAGE -- read by expand only
+//   coll   : u64 open-addressing table {edge value -> visit id} for colliding visit keys,
+//            consulted only on rows flagged ROW_SEQ
+//
+// A "normal" row stores its effective (check) edges as [subject sets in ORDER BY order]
+// [subject ids sorted by string id == byte order], so a check finds the requested subject id by
+// binary search.  A ROW_SEQ row (materialized wildcard query, or a row holding an edge whose
+// Subject.String() collides with another subject's) keeps the exact ORDER BY sequence and is
+// walked edge by edge with full visited semantics.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/keto_mi355x.h"
+
+namespace keto {
+
+constexpr uint32_t EDGE_SET = 0x80000000u;
+constexpr uint32_t EDGE_VAL = 0x7FFFFFFFu;
+constexpr uint32_t EDGE_POISON = 0x7FFFFFFFu;   // a row whose toInternal fails; never traversed
+constexpr uint32_t NO_PAGE = 0xFFFFFFFFu;
+constexpr uint32_t ANY = 0xFFFFFFFFu;           // wildcard field of a row key
+constexpr int64_t ANY_NS = INT64_MIN;
+constexpr uint32_t ROW_SEQ = 1u;                // flag bit (in RowRec.y bits 8..15)
+constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys live above all row ids
+
+struct RowRec {          // 16 B
+    uint32_t edge_lo;    // edge begin, low 32 bits
+    uint32_t hi_flags;   // bits 0..7 edge begin bits 32..39; bits 8..15 flags
+    uint32_t n_sets;     // normal: effective subject sets; ROW_SEQ: effective edge count
+    uint32_t n_ids;      // normal: effective subject ids;  ROW_SEQ: 0
+};
+static_assert(sizeof(RowRec) == 16, "RowRec must be 16 bytes");
+
+struct RowKey {          // (namespace id | ANY, object string | ANY, relation string | ANY)
+    int64_t ns;
+    uint32_t obj, rel;
+    bool operator==(const RowKey& o) const { return ns == o.ns && obj == o.obj && rel == o.rel; }
+};
+struct RowKeyHash {
+    size_t operator()(const RowKey& k) const {
+        uint64_t h = (uint64_t)k.ns * 0x9E3779B97F4A7C15ull;
+        h ^= (uint64_t)k.obj * 0xC2B2AE3D27D4EB4Full + (h << 6) + (h >> 2);
+        h ^= (uint64_t)k.rel * 0x165667B19E3779F9ull + (h << 6) + (h >> 2);
+        return (size_t)h;
+    }
+};
+
+struct DeviceState;      // engine.hip
+struct DeviceStateDeleter {
+    void operator()(DeviceState* d) const;   // engine.hip
+};
+
+struct Snapshot {
+    // ---- config
+    std::vector<int32_t> ns_ids;
+    std::vector<std::string> ns_names;
+    std::unordered_map<std::string, int> ns_by_name;   // name -> config index
+    std::unordered_map<int32_t, int> ns_by_id;         // id   -> config index
+    uint32_t page_size = 100;
+
+    // ---- strings (byte order == id order)
+    std::vector<std::string> strs;
+    std::unordered_map<std::string_view, uint32_t> str_id;   // views into strs
+    uint32_t empty_str = ANY;                                // id of "" if present
+
+    // ---- rows
+    uint32_t n_real_rows = 0;
+    uint32_t n_wild_rows = 0;
+    std::vector<RowKey> row_key;                             // per row
+    std::unordered_map<RowKey, uint32_t, RowKeyHash> row_of; // real + empty + wildcard rows
+    std::vector<RowRec> rows;
+    std::vector<uint32_t> row_pp;
+    std::vector<uint32_t> edges;
+    std::vector<uint8_t> row_has_coll;
+
+    // ---- visit-key collisions
+    std::unordered_map<uint32_t, uint32_t> coll;             // edge value -> visit id
+    uint32_t n_coll_keys = 0;
+
+    uint64_t n_tuples = 0;
+    uint32_t n_poisoned_rows = 0;
+    uint32_t n_seq_rows = 0;
+
+    // ---- device
+    int device = -1;
+    std::unique_ptr<DeviceState, DeviceStateDeleter> dev;
+    std::mutex mu;
+
+    ~Snapshot();
+
+    uint64_t row_begin(uint32_t r) const {
+        return (uint64_t)rows[r].edge_lo | ((uint64_t)(rows[r].hi_flags & 0xFFu) << 32);
+    }
+    uint32_t row_flags(uint32_t r) const { return (rows[r].hi_flags >> 8) & 0xFFu; }
+    uint32_t n_rows() const { return (uint32_t)rows.size(); }
+
+    // lookups used by request resolution
+    int64_t lookup_str(std::string_view s) const;                      // -1 if absent
+    // RelationQuery (namespace name, object, relation) -> row, per whereQuery; returns
+    //  >=0 row id, -1 no such row (empty result), -2 unknown namespace (NotFound),
+    //  -3 a wildcard query no stored subject set materialized (*key_out is set)
+    int64_t resolve_query(std::string_view ns, std::string_view obj, std::string_view rel,
+                          RowKey* key_out = nullptr) const;
+    // visit id of a Subject.String() key that names no snapshot row: the row sharing the key
+    // (if any), else a fresh id (lazy key index, built on first use)
+    uint32_t vid_of_key(const std::string& key) const;
+    mutable std::unique_ptr<std::unordered_map<std::string, uint32_t>> key_index;
+    mutable std::mutex key_mu;
+    uint32_t vid_of_row(uint32_t row) const;
+    std::string subject_string(uint32_t subject_ref) const;
+    std::string row_field_ns(uint32_t row) const;
+    std::string row_field(uint32_t row, int which) const;               // 1 obj, 2 rel
+};
+
+// builders (snapshot.cpp); throw keto::Error
+struct Error {
+    int code;
+    std::string msg;
+};
+
+std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns, const keto_tuple* t, uint64_t n,
+                                         uint32_t page_size);
+std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t n_ns, uint32_t n_rows,
+                                             const int32_t* row_ns, const uint32_t* row_obj,
+                                             const uint32_t* row_rel, const uint64_t* row_ptr,
+                                             const uint32_t* edges, const keto_str* strings, uint32_t n_strings,
+                                             uint32_t page_size);
+
+// Batch-local rows for wildcard requests that no stored subject set materialized: they can only
+// be top-level (check) or root (expand) rows, never edge targets.  Row ids >= base.
+struct Overlay {
+    uint32_t base = 0;
+    std::vector<RowRec> rows;
+    std::vector<uint32_t> pp;
+    std::vector<uint32_t> edges;
+    std::vector<RowKey> keys;
+    std::unordered_map<RowKey, uint32_t, RowKeyHash> map;
+    bool empty() const { return rows.empty(); }
+};
+// materialize the wildcard query k (ns ANY / obj ANY / rel ANY) into the overlay; returns row id
+uint32_t overlay_row(const Snapshot& s, Overlay& ov, const RowKey& k);
+
+// device engine (engine.hip)
+void device_upload(Snapshot& s, int device);
+void device_release(Snapshot& s);
+uint64_t device_bytes(const Snapshot& s);
+void device_check(Snapshot& s, const keto_check_ids* d_or_h_reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
+                  bool host_buffers, void* stream, const Overlay* ov);
+struct ExpandResult {
+    std::vector<uint8_t> status;
+    std::vector<uint64_t> offset;          // n+1
+    std::vector<keto_tree_node> nodes;
+};
+void device_expand(Snapshot& s, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
+                   const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
+                   const Overlay* ov, ExpandResult& out);
+
+}  // namespace keto

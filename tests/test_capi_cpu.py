@@ -1,0 +1,59 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/keto_mi355x.h
+declares, builds host-only snapshots (device = -1) with the reference ordering / poisoning /
+collision bookkeeping, and refuses compute without a device."""
+import os
+import re
+
+import pytest
+
+import keto_amd
+from keto_amd import capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_exports_match_header():
+    hdr = open(os.path.join(ROOT, "include", "keto_mi355x.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(keto_[a-z_]+)\(", hdr, re.M))
+    lib = keto_amd.load()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(capi.EXPORTS) == declared
+
+
+def test_abi_version():
+    assert keto_amd.load().keto_abi_version() == 1
+
+
+def test_host_snapshot_stats():
+    ns = [(1, "n")]
+    rows = [(1, "a", "r", "u"), (1, "a", "r", None, 1, "b", "r"), (1, "b", "r", "v"),
+            (1, "c", "r", None, 1, "", "r"),        # wildcard subject set -> materialized row
+            (1, "d", "r", None, 99, "x", "y"),      # unknown subject-set namespace -> poisoned row
+            (1, "e", "r", "n:b#r")]                 # subject id colliding with set n:b#r
+    s = keto_amd.Snapshot.build(ns, rows, device=-1)
+    st = s.stats()
+    assert st["n_tuples"] == 6
+    assert st["n_real_rows"] == 5
+    assert st["n_wildcard_rows"] == 1
+    assert st["n_poisoned_rows"] == 2      # the row itself and the wildcard row (n, *, r) that includes it
+    assert st["n_collision_keys"] == 1
+    assert st["device_bytes"] == 0
+
+
+def test_duplicate_namespace_rejected():
+    with pytest.raises(keto_amd.KetoError, match="-4"):
+        keto_amd.Snapshot.build([(1, "n"), (2, "n")], [], device=-1)
+
+
+def test_compute_without_device_fails_loudly():
+    s = keto_amd.Snapshot.build([(1, "n")], [(1, "a", "r", "u")], device=-1)
+    with pytest.raises(keto_amd.KetoError):
+        s.check_batch([("n", "a", "r", ("id", "u"), 0)])
+
+
+def test_csr_bulk_loader_validates_order():
+    import numpy as np
+    with pytest.raises(keto_amd.KetoError):
+        keto_amd.Snapshot.from_csr([(1, "n")], np.array([1, 1]), np.array([2, 1]), np.array([0, 0]),
+                                   np.array([0, 0, 0], dtype=np.uint64), np.zeros(0, np.uint32), device=-1)

@@ -1,0 +1,297 @@
+// Synthetic ACL graphs and request batches for bench.py and the large-size tests (tooling, not
+// part of the engine).  Graphs come out already interned and in the reference ORDER BY, ready for
+// keto_snapshot_from_csr; names are fixed-width lowercase hex ("d%08x", "f%08x", "g%08x",
+// "u%08x"), so numeric id order equals byte order and no Subject.String() can collide.
+//
+// "power-law ACL" graph (BASELINE config #4):
+//   namespaces docs(1) / folders(2) / groups(3); rows docs:d#view, folders:f#view, groups:g#member
+//   docs:d#view    -> (folders:f#view) parent, f ~ power law over folders; 0-2 x (groups:g#member),
+//                     g ~ power law; Pareto(1.8) direct user shares
+//   folders:f#view -> (folders:p#view) parent (random recursive forest, p < f; 1/64 are roots);
+//                     0-3 x (groups:g#member); Pareto(1.6) users
+//   groups:g#member-> (groups:h#member) nested, h < g with p = 0.5, h > g (cycles) with p = 0.001;
+//                     Pareto(1.3) users, capped at 2^21 (heavy-tailed group sizes)
+//   users drawn with a power law (popular users are in many groups); total edges adjusted to
+//   exactly `target_edges` by adding / removing direct user shares on documents.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../include/keto_mi355x.h"
+
+namespace {
+
+inline uint64_t splitmix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct Rng {
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(splitmix(seed)) {}
+    uint64_t next() { return s = splitmix(s); }
+    double u01() { return ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
+};
+
+// P(x < k) = (k/n)^(1/3): heavy preference for low indices
+inline uint64_t skewed(Rng& r, uint64_t n, double power = 3.0) {
+    uint64_t x = (uint64_t)(std::pow(r.u01(), power) * (double)n);
+    return x >= n ? n - 1 : x;
+}
+inline uint64_t pareto(Rng& r, double xm, double a, uint64_t cap) {
+    double v = xm / std::pow(r.u01(), 1.0 / a) - xm;   // starts at 0
+    uint64_t k = (uint64_t)v;
+    return k > cap ? cap : k;
+}
+
+template <class F>
+void parallel_for(uint64_t n, int threads, F f) {
+    if (threads < 1) threads = 1;
+    std::atomic<uint64_t> next{0};
+    const uint64_t chunk = 1 << 14;
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&] {
+            for (;;) {
+                uint64_t b = next.fetch_add(chunk);
+                if (b >= n) break;
+                uint64_t e = std::min(n, b + chunk);
+                for (uint64_t i = b; i < e; ++i) f(i);
+            }
+        });
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+typedef struct {
+    uint64_t n_docs, n_folders, n_groups, n_users, target_edges, seed;
+} synth_params;
+
+typedef struct {
+    uint32_t n_rows;
+    int32_t* row_ns;
+    uint32_t* row_obj;
+    uint32_t* row_rel;
+    uint64_t* row_ptr;
+    uint32_t* edges;
+    uint64_t n_edges;
+    uint64_t n_set_edges;
+} synth_graph;
+
+enum { REL_MEMBER = 0, REL_VIEW = 1 };
+
+static void row_degrees(const synth_params* p, uint64_t r, uint32_t& ns, uint32_t& ni) {
+    const uint64_t F0 = p->n_docs, G0 = p->n_docs + p->n_folders;
+    Rng g(p->seed * 0x100000001B3ull ^ (r * 0x9E3779B97F4A7C15ull));
+    if (r < F0) {
+        uint64_t u = g.next() % 5;
+        ns = 1 + (u < 2 ? 0 : u < 4 ? 1 : 2);
+        ni = (uint32_t)pareto(g, 1.0, 1.8, 64);
+    } else if (r < G0) {
+        uint64_t f = r - F0;
+        bool root = f < p->n_folders / 64;
+        ns = (root ? 0 : 1) + (uint32_t)(g.next() % 4);
+        ni = (uint32_t)pareto(g, 3.0, 1.6, 10000);
+    } else {
+        uint64_t x = g.next() % 1000;
+        ns = x < 500 ? 1 : 0;
+        if (x == 999) ns++;
+        ni = (uint32_t)pareto(g, 16.0, 1.3, 1u << 21);
+    }
+}
+
+int synth_generate(const synth_params* p, int threads, synth_graph* out) {
+    const uint64_t R = p->n_docs + p->n_folders + p->n_groups;
+    if (R >= 0x7FFFFFFFull || p->n_users >= 0x7FFFFFFFull) return -1;
+    const uint64_t F0 = p->n_docs, G0 = p->n_docs + p->n_folders;
+    std::vector<uint32_t> nset(R), nid(R);
+    parallel_for(R, threads, [&](uint64_t r) { row_degrees(p, r, nset[r], nid[r]); });
+    uint64_t tot = 0;
+    for (uint64_t r = 0; r < R; ++r) tot += nset[r] + nid[r];
+    // hit target_edges exactly by adjusting document shares
+    if (p->target_edges) {
+        int64_t diff = (int64_t)p->target_edges - (int64_t)tot;
+        uint64_t r = 0, guard = 0;
+        while (diff != 0 && p->n_docs && guard < 64 * p->n_docs) {
+            if (diff > 0) { nid[r]++; diff--; }
+            else if (nid[r] > 0) { nid[r]--; diff++; }
+            r = (r + 7919) % p->n_docs;
+            ++guard;
+        }
+    }
+    out->n_rows = (uint32_t)R;
+    out->row_ns = (int32_t*)malloc(R * sizeof(int32_t));
+    out->row_obj = (uint32_t*)malloc(R * sizeof(uint32_t));
+    out->row_rel = (uint32_t*)malloc(R * sizeof(uint32_t));
+    out->row_ptr = (uint64_t*)malloc((R + 1) * sizeof(uint64_t));
+    uint64_t acc = 0, sets = 0;
+    for (uint64_t r = 0; r < R; ++r) {
+        out->row_ptr[r] = acc;
+        acc += nset[r] + nid[r];
+        sets += nset[r];
+    }
+    out->row_ptr[R] = acc;
+    out->n_edges = acc;
+    out->n_set_edges = sets;
+    out->edges = (uint32_t*)malloc(std::max<uint64_t>(acc, 1) * sizeof(uint32_t));
+    if (!out->row_ns || !out->row_obj || !out->row_rel || !out->row_ptr || !out->edges) return -2;
+    parallel_for(R, threads, [&](uint64_t r) {
+        if (r < F0) { out->row_ns[r] = 1; out->row_obj[r] = (uint32_t)r; out->row_rel[r] = REL_VIEW; }
+        else if (r < G0) { out->row_ns[r] = 2; out->row_obj[r] = (uint32_t)(r - F0); out->row_rel[r] = REL_VIEW; }
+        else { out->row_ns[r] = 3; out->row_obj[r] = (uint32_t)(r - G0); out->row_rel[r] = REL_MEMBER; }
+        Rng g(p->seed * 0xC2B2AE3D27D4EB4Full ^ (r * 0xD6E8FEB86659FD93ull) ^ 0x5555);
+        uint32_t* e = out->edges + out->row_ptr[r];
+        uint32_t k = 0;
+        const uint32_t ns = nset[r], ni = nid[r];
+        if (r < F0) {
+            e[k++] = 0x80000000u | (uint32_t)(F0 + skewed(g, p->n_folders));
+            while (k < ns) e[k++] = 0x80000000u | (uint32_t)(G0 + skewed(g, p->n_groups));
+        } else if (r < G0) {
+            uint64_t f = r - F0;
+            bool root = f < p->n_folders / 64;
+            if (!root) e[k++] = 0x80000000u | (uint32_t)(F0 + g.next() % f);
+            while (k < ns) e[k++] = 0x80000000u | (uint32_t)(G0 + skewed(g, p->n_groups));
+        } else {
+            uint64_t gi = r - G0;
+            while (k < ns) {
+                uint64_t h;
+                if (k == 0 && gi > 0) h = g.next() % gi;                       // nested, acyclic
+                else h = gi + 1 + g.next() % std::max<uint64_t>(1, p->n_groups - gi - 1);   // back-edge
+                if (h >= p->n_groups) h = g.next() % p->n_groups;
+                e[k++] = 0x80000000u | (uint32_t)(G0 + h);
+            }
+        }
+        std::sort(e, e + ns);                     // subject sets by (namespace id, object, relation)
+        for (uint32_t j = 0; j < ni; ++j) e[ns + j] = (uint32_t)skewed(g, p->n_users, 1.5);
+        std::sort(e + ns, e + ns + ni);           // subject ids by bytes
+    });
+    return 0;
+}
+
+void synth_free(synth_graph* g) {
+    free(g->row_ns);
+    free(g->row_obj);
+    free(g->row_rel);
+    free(g->row_ptr);
+    free(g->edges);
+    memset(g, 0, sizeof(*g));
+}
+
+// Requests docs:d#view@u: half sampled along a real path (a random walk of 0..depth-1 subject-set
+// hops from d, then one of the reached row's users), half uniformly random users.
+int synth_queries(const synth_graph* g, const synth_params* p, uint64_t n, uint64_t seed, int32_t depth,
+                  keto_check_ids* out, int threads) {
+    parallel_for(n, threads, [&](uint64_t i) {
+        Rng r(seed * 0xA24BAED4963EE407ull ^ (i * 0x9FB21C651E98DF25ull));
+        uint32_t doc = (uint32_t)(r.next() % p->n_docs);
+        keto_check_ids q{doc, 0, 0, depth};
+        if (r.next() & 1) {
+            uint32_t cur = doc;
+            int hops = (int)(r.next() % (uint64_t)std::max(1, depth));
+            for (int h = 0; h < hops; ++h) {
+                uint64_t b = g->row_ptr[cur], e = g->row_ptr[cur + 1];
+                uint64_t ns = 0;
+                while (b + ns < e && (g->edges[b + ns] & 0x80000000u)) ++ns;
+                if (!ns) break;
+                cur = g->edges[b + r.next() % ns] & 0x7FFFFFFFu;
+            }
+            uint64_t b = g->row_ptr[cur], e = g->row_ptr[cur + 1];
+            uint64_t ns = 0;
+            while (b + ns < e && (g->edges[b + ns] & 0x80000000u)) ++ns;
+            if (e - b > ns) q.target = g->edges[b + ns + r.next() % (e - b - ns)];
+            else q.target = (uint32_t)(r.next() % p->n_users);
+        } else {
+            q.target = (uint32_t)(r.next() % p->n_users);
+        }
+        out[i] = q;
+    });
+    return 0;
+}
+
+// ---- oracle table extraction (cpu_baseline sample): every row a depth-bounded check from the
+// sample's rows can query (subject-set hops 0..depth-1), as tuples in ORDER BY order.
+typedef struct {
+    uint64_t n;
+    int32_t* ns;
+    uint32_t *obj, *rel;
+    uint8_t* kind;
+    uint32_t* sid;
+    int32_t* sns;
+    uint32_t *sobj, *srel, *key;
+} synth_table;
+
+int synth_extract(const synth_graph* g, const synth_params* p, const keto_check_ids* q, uint64_t nq, int32_t depth,
+                  synth_table* out) {
+    std::vector<uint8_t> seen(g->n_rows, 0);
+    std::vector<uint32_t> frontier, next, rows;
+    for (uint64_t i = 0; i < nq; ++i)
+        if (q[i].row < g->n_rows && !seen[q[i].row]) { seen[q[i].row] = 1; frontier.push_back(q[i].row); }
+    rows = frontier;
+    for (int h = 1; h < depth && !frontier.empty(); ++h) {
+        next.clear();
+        for (uint32_t r : frontier)
+            for (uint64_t k = g->row_ptr[r]; k < g->row_ptr[r + 1]; ++k) {
+                uint32_t e = g->edges[k];
+                if (!(e & 0x80000000u)) break;
+                uint32_t t = e & 0x7FFFFFFFu;
+                if (!seen[t]) { seen[t] = 1; next.push_back(t); rows.push_back(t); }
+            }
+        frontier.swap(next);
+    }
+    std::sort(rows.begin(), rows.end());
+    uint64_t n = 0;
+    for (uint32_t r : rows) n += g->row_ptr[r + 1] - g->row_ptr[r];
+    out->n = n;
+    out->ns = (int32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->obj = (uint32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->rel = (uint32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->kind = (uint8_t*)malloc(std::max<uint64_t>(n, 1));
+    out->sid = (uint32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->sns = (int32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->sobj = (uint32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->srel = (uint32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    out->key = (uint32_t*)malloc(std::max<uint64_t>(n, 1) * 4);
+    uint64_t k = 0;
+    for (uint32_t r : rows) {
+        for (uint64_t i = g->row_ptr[r]; i < g->row_ptr[r + 1]; ++i, ++k) {
+            uint32_t e = g->edges[i];
+            out->ns[k] = g->row_ns[r];
+            out->obj[k] = g->row_obj[r];
+            out->rel[k] = g->row_rel[r];
+            if (e & 0x80000000u) {
+                uint32_t t = e & 0x7FFFFFFFu;
+                out->kind[k] = 1;
+                out->sid[k] = 0;
+                out->sns[k] = g->row_ns[t];
+                out->sobj[k] = g->row_obj[t];
+                out->srel[k] = g->row_rel[t];
+                out->key[k] = (uint32_t)(p->n_users + t);
+            } else {
+                out->kind[k] = 0;
+                out->sid[k] = e;
+                out->sns[k] = 0;
+                out->sobj[k] = out->srel[k] = 0;
+                out->key[k] = e;
+            }
+        }
+    }
+    return 0;
+}
+
+void synth_table_free(synth_table* t) {
+    free(t->ns); free(t->obj); free(t->rel); free(t->kind); free(t->sid);
+    free(t->sns); free(t->sobj); free(t->srel); free(t->key);
+    memset(t, 0, sizeof(*t));
+}
+
+}  // extern "C"
