@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched Keto checks on the 1B-tuple power-law ACL graph at max-depth 5.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 the driver starts one
+rank per GPU with torch.distributed.run.  A step = one keto_check_batch_device call over a
+resident batch of synthetic docs:d#view@u requests (16M per GPU by default).  The path shards by
+request with no data-path collective: every rank holds the whole snapshot (the 1B-tuple CSR is
+~6.4 GB of a 288 GB HBM3E) and checks its own batch ("weak" scaling).  Rank 0 prints one JSON line.
+
+Extras on the same line:
+  roofline      algorithmic bytes of the dominant kernel (tier-0 check_kernel) per launch, from the
+                instrumented work counters of one extra (untimed) pass over the same batch, divided
+                by its average HIP-event duration over the timed steps; peak = 8 TB/s HBM3E.
+  cpu_baseline  the C restatement of the reference engine (oracle/keto_oracle.c) on the box's host
+                cores over a bounded sample of the same requests; its decisions are also compared
+                with the GPU's for that sample ("parity").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=16 * 1024 * 1024, help="checks per GPU per step")
+    ap.add_argument("--scale", type=float, default=1.0, help="graph scale (1.0 = 1B tuples)")
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--threads", type=int, default=16, help="host threads (generator, cpu baseline)")
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="requests in the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-work", action="store_true", help="skip the instrumented work-count pass")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from tools import synth
+
+    params = synth.scaled(synth.POWERLAW_1B, a.scale) if a.scale != 1.0 else dict(synth.POWERLAW_1B)
+    t0 = time.time()
+    g = synth.SynthGraph(params, threads=a.threads)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    snap = g.snapshot(device=dev)
+    t_snap = time.time() - t0
+    q = g.queries(a.batch, seed=1000 + rank, depth=a.depth, threads=a.threads)
+    d_q = torch.from_numpy(q.view(np.uint8)).to(f"cuda:{dev}")
+    d_out = torch.empty(a.batch, dtype=torch.uint8, device=f"cuda:{dev}")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    tier_ms, tier_n = [], []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        ms, n = snap.last_timing()
+        tier_ms.append(ms)
+        tier_n.append(n)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total = world * a.batch * a.steps
+    value = total / elapsed
+
+    # ---- roofline of the dominant kernel (tier-0 check_kernel)
+    tier0_ms = float(np.mean([m[0] for m in tier_ms]))
+    tier1_ms = float(np.mean([m[1] for m in tier_ms]))
+    overflow = int(np.mean([n[1] for n in tier_n]))
+    roofline = None
+    work = None
+    allowed_rate = float(d_out.float().mean().item())
+    if not a.no_work:
+        w = snap.check_work_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth)
+        rows, edges, idreads, vprobes, vinserts, items = w[:6]
+        # bytes the exact traversal must move: 16-B row records, 4-B subject-set edges, 4-B words
+        # of the id-membership searches, 8-B visited-table probes and inserts, 16-B requests in,
+        # 1-B decisions out
+        alg = 16 * rows + 4 * edges + 4 * idreads + 8 * vprobes + 8 * vinserts + 17 * a.batch
+        achieved = alg / (tier0_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "alg_bytes_per_launch": int(alg), "kernel": "check_kernel<LocalStack<16>> (tier 0)",
+                    "kernel_ms": round(tier0_ms, 3)}
+        work = {"rows_per_check": rows / a.batch, "set_edges_per_check": edges / a.batch,
+                "id_words_per_check": idreads / a.batch, "visited_probes_per_check": vprobes / a.batch,
+                "top_level_items_per_check": items / a.batch}
+
+    # ---- CPU baseline (rank 0, N = 1): oracle restatement on a bounded sample of the same batch
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        ns = min(a.cpu_sample, a.batch)
+        sample = q[:ns]
+        tab = g.oracle_table(sample, a.depth)
+        reqs = g.oracle_requests(tab, sample)
+        threads = a.threads
+        t0 = time.perf_counter()
+        ref = tab.check_batch_reqs(reqs, a.depth, threads=threads)
+        t_cpu = time.perf_counter() - t0
+        gpu = d_out[:ns].cpu().numpy()
+        parity = {"sample": int(ns), "mismatches": int((ref != gpu).sum())}
+        cpu = {"value": round(ns / t_cpu, 1), "unit": "checks/s", "cores": threads, "kind": "port",
+               "sample": f"first {ns} requests of the rank-0 batch; oracle/keto_oracle.c over the "
+                         f"{tab.t.n} tuples those requests can reach, {threads} host threads, {t_cpu:.2f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": "checks/sec (whole node) on 1B-tuple graph, max-depth 5; % of HBM roofline",
+            "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "powerlaw-acl-1B (BASELINE config #4) on one GPU per rank, replicated snapshot",
+                       "tuples": int(g.n_edges), "set_edge_fraction": round(g.n_set_edges / max(1, g.n_edges), 4),
+                       "rows": int(g.n_rows), "checks_per_gpu_per_step": a.batch, "max_depth": a.depth,
+                       "global_batch": a.batch * world, "parallelism": f"replicated-dp{world}",
+                       "scale": a.scale},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "detail": {"tier0_ms": round(tier0_ms, 3), "tier1_ms": round(tier1_ms, 3),
+                       "tier0_overflow_requests": overflow, "allowed_fraction": round(allowed_rate, 4),
+                       "gen_s": round(t_gen, 1), "snapshot_upload_s": round(t_snap, 1), "work": work},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -185,9 +185,29 @@ int keto_check_batch_ids(keto_snapshot* s, const keto_check_ids* reqs, uint32_t 
 int keto_check_batch_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                             uint8_t* d_allowed_out, void* stream);
 
+/* Device time of the last keto_check_* call on this snapshot, per tier (tier 0 = every request,
+ * tiers 1/2 = requests whose visited map outgrew the previous tier's table), from HIP events on
+ * the call's stream. */
+typedef struct {
+    float tier_ms[3];
+    uint32_t requests[3];
+} keto_batch_timing;
+int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
+
+/* Work counters of the traversal for a device-resident batch (instrumented kernels; same results):
+ * out[0] row records read, out[1] subject-set edges scanned, out[2] subject-id words read by the
+ * membership searches, out[3] visited-table probes, out[4] visited-table inserts, out[5] top-level
+ * subject sets expanded (fresh visited maps).  Used for the roofline's algorithmic bytes. */
+int keto_check_work_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                           uint8_t* d_allowed_out, uint64_t out[8]);
+
 /* Batched BuildTree.  The arena owns all trees; free it with keto_tree_arena_free. */
 int keto_expand_batch(keto_snapshot* s, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
                       keto_tree_arena** out);
+/* Same with pre-resolved roots: roots[i] bit31 set -> subject set (bits 0..30 = row id), else a
+ * subject id (bits 0..30 = string id). */
+int keto_expand_batch_ids(keto_snapshot* s, const uint32_t* roots, const int32_t* max_depth, uint32_t n,
+                          int32_t global_max_depth, keto_tree_arena** out);
 void keto_tree_arena_free(keto_tree_arena* a);
 uint32_t keto_tree_count(const keto_tree_arena* a);
 int keto_tree_status(const keto_tree_arena* a, uint32_t i);

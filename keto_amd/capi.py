@@ -26,6 +26,7 @@ EXPORTS = [
     "keto_snapshot_release", "keto_snapshot_get_stats", "keto_resolve_checks", "keto_check_batch",
     "keto_check_batch_ids", "keto_check_batch_device", "keto_expand_batch", "keto_tree_arena_free",
     "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
+    "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids",
 ]
 
 
@@ -74,6 +75,10 @@ class KTreeNode(C.Structure):
 
 class KOpts(C.Structure):
     _fields_ = [("page_size", C.c_uint32), ("device", C.c_int32), ("flags", C.c_uint32)]
+
+
+class KTiming(C.Structure):
+    _fields_ = [("tier_ms", C.c_float * 3), ("requests", C.c_uint32 * 3)]
 
 
 class KStats(C.Structure):
@@ -248,7 +253,43 @@ class Snapshot:
                                                 C.c_int32(global_max_depth), C.c_void_p(d_out_ptr),
                                                 C.c_void_p(stream)))
 
+    def last_timing(self):
+        t = KTiming()
+        _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
+        return list(t.tier_ms), list(t.requests)
+
+    def check_work_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, global_max_depth=5):
+        out = (C.c_uint64 * 8)()
+        _check(self.lib.keto_check_work_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
+                                               C.c_int32(global_max_depth), C.c_void_p(d_out_ptr), out))
+        return list(out)
+
     # ------------------------------------------------------------------ expand
+    def expand_batch_ids(self, roots: np.ndarray, depths: np.ndarray, global_max_depth=5):
+        """Pre-resolved roots (bit31 = subject set row). Returns (status[n], offsets[n+1], nodes[m,2])."""
+        roots = np.ascontiguousarray(roots, dtype=np.uint32)
+        depths = np.ascontiguousarray(depths, dtype=np.int32)
+        n = len(roots)
+        a = C.c_void_p()
+        _check(self.lib.keto_expand_batch_ids(self.h, roots.ctypes.data_as(C.c_void_p),
+                                              depths.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                              C.c_int32(global_max_depth), C.byref(a)))
+        try:
+            status = np.array([self.lib.keto_tree_status(a, C.c_uint32(i)) for i in range(n)], dtype=np.int32)
+            offs = np.zeros(n + 1, dtype=np.int64)
+            chunks = []
+            for i in range(n):
+                nn = C.c_uint64()
+                ptr = self.lib.keto_tree_nodes(a, C.c_uint32(i), C.byref(nn))
+                offs[i + 1] = offs[i] + nn.value
+                if nn.value:
+                    buf = (C.c_uint32 * (2 * nn.value)).from_address(C.cast(ptr, C.c_void_p).value)
+                    chunks.append(np.frombuffer(buf, dtype=np.uint32).copy().reshape(-1, 2))
+            nodes = np.concatenate(chunks) if chunks else np.zeros((0, 2), dtype=np.uint32)
+        finally:
+            self.lib.keto_tree_arena_free(a)
+        return status, offs, nodes
+
     def expand_batch(self, reqs, global_max_depth=5, want_nodes=False):
         """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes])."""
         keep = _Keep()

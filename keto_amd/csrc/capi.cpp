@@ -307,6 +307,23 @@ int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
     });
 }
 
+int keto_last_batch_timing(const keto_snapshot* h, keto_batch_timing* out) {
+    return guarded([&] {
+        if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        *out = device_last_timing(*h->s);
+        return KETO_OK;
+    });
+}
+
+int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                           uint8_t* d_allowed_out, uint64_t out[8]) {
+    return guarded([&] {
+        if (!h || !out || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, false, nullptr, nullptr, out);
+        return KETO_OK;
+    });
+}
+
 int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
                       keto_tree_arena** out) {
     return guarded([&] {
@@ -356,6 +373,31 @@ int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n,
         device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r);
         for (uint32_t i = 0; i < n; ++i)
             if (not_found[i]) a->r.status[i] = KETO_EXPAND_NOT_FOUND;
+        *out = a.release();
+        return KETO_OK;
+    });
+}
+
+int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t* max_depth, uint32_t n,
+                          int32_t global_max_depth, keto_tree_arena** out) {
+    return guarded([&] {
+        if (!h || !out || (n && (!roots || !max_depth))) throw Error{KETO_E_INVALID, "NULL argument"};
+        *out = nullptr;
+        Snapshot& S = *h->s;
+        auto a = std::make_unique<keto_tree_arena>();
+        a->extra_base = (uint32_t)S.strs.size();
+        std::vector<uint32_t> root(n), flags(n), vid(n, 0);
+        std::vector<int32_t> depth(max_depth, max_depth + n);
+        for (uint32_t i = 0; i < n; ++i) {
+            const bool set = (roots[i] & EDGE_SET) != 0;
+            root[i] = roots[i] & EDGE_VAL;
+            flags[i] = set ? 1u : 0u;
+            if (set) {
+                if (root[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "root row out of range"};
+                vid[i] = S.vid_of_row(root[i]);
+            }
+        }
+        device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, a->r);
         *out = a.release();
         return KETO_OK;
     });

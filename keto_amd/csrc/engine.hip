@@ -93,15 +93,41 @@ __device__ inline RowView load_row(const DevSnap& s, uint32_t r) {
     return rv;
 }
 
+// Algorithmic-work counters (bench.py's roofline): compiled out of the production kernels.
+template <bool ON>
+struct Work {
+    __device__ inline void row() {}
+    __device__ inline void edge() {}
+    __device__ inline void idread(uint32_t) {}
+    __device__ inline void vprobe() {}
+    __device__ inline void vinsert() {}
+    __device__ inline void item() {}
+};
+template <>
+struct Work<true> {
+    uint64_t rows = 0, edges = 0, idreads = 0, vprobes = 0, vinserts = 0, items = 0;
+    __device__ inline void row() { ++rows; }
+    __device__ inline void edge() { ++edges; }
+    __device__ inline void idread(uint32_t k) { idreads += k; }
+    __device__ inline void vprobe() { ++vprobes; }
+    __device__ inline void vinsert() { ++vinserts; }
+    __device__ inline void item() { ++items; }
+};
+
 // lower_bound over the byte-ordered subject-id region
-__device__ inline bool find_id(const uint32_t* __restrict__ e, uint64_t b, uint32_t n, uint32_t t) {
+template <class W>
+__device__ inline bool find_id(const uint32_t* __restrict__ e, uint64_t b, uint32_t n, uint32_t t, W& w) {
+    // invariant: the first element >= t lies in [lo, hi]  (hi itself included)
     uint32_t lo = 0, hi = n;
     while (hi - lo > 8) {
         uint32_t m = (lo + hi) >> 1;
+        w.idread(1);
         if (e[b + m] < t) lo = m + 1; else hi = m;
     }
-    for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t end = hi < n ? hi + 1 : n;
+    for (uint32_t i = lo; i < end; ++i) {
         uint32_t v = e[b + i];
+        w.idread(1);
         if (v >= t) return v == t;
     }
     return false;
@@ -122,14 +148,17 @@ struct Visited {
         count = 0;
     }
     // 0 = newly added, 1 = already present, 2 = table too full (request must move up a tier)
-    __device__ inline int test_add(uint32_t vid) {
+    template <class W>
+    __device__ inline int test_add(uint32_t vid, W& w) {
         uint32_t i = mix32(vid) & mask;
         const uint64_t want = ((uint64_t)epoch << 32) | vid;
         for (;;) {
             uint64_t e = tab[i];
+            w.vprobe();
             if ((uint32_t)(e >> 32) != epoch) {
                 if ((++count) * 2u > mask + 1u) return 2;
                 tab[i] = want;
+                w.vinsert();
                 return 0;
             }
             if (e == want) return 1;
@@ -161,14 +190,15 @@ struct GlobalStack {
 // ------------------------------------------------------------------ check
 // Further(r0, k0) below a top-level tuple (engine.go:82-114 + :36-80), V already holds the
 // top-level subject.  Returns RES_TRUE / RES_FALSE / RES_OVERFLOW.
-template <class Stack>
-__device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool tset, Visited& V, Stack& st) {
+template <class Stack, class W>
+__device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool tset, Visited& V, Stack& st, W& w) {
     const uint32_t tval = tset ? (EDGE_SET | T) : T;
     int sp = 0;
     {
         RowView rv = load_row(s, r0);
+        w.row();
         if (!rv.seq) {
-            if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T)) return RES_TRUE;
+            if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T, w)) return RES_TRUE;
             st[0] = Frame{rv.beg, rv.n_sets, (uint16_t)k0, 0};
         } else {
             st[0] = Frame{rv.beg, rv.n_sets, (uint16_t)k0, 1};
@@ -182,6 +212,7 @@ __device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool
             continue;
         }
         const uint32_t e = s.edges[f.pos];
+        w.edge();
         f.pos++;
         f.left--;
         if (e & EDGE_SET) {
@@ -190,7 +221,7 @@ __device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool
                 uint32_t c = coll_lookup(s, e);
                 if (c != NONE32) vid = c;
             }
-            int t = V.test_add(vid);
+            int t = V.test_add(vid, w);
             if (t == 1) continue;
             if (t == 2) return RES_OVERFLOW;
             if (tset && e == tval) return RES_TRUE;
@@ -198,8 +229,9 @@ __device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool
                 if (sp == st.cap()) return RES_OVERFLOW;
                 const uint16_t k = f.k - 1;
                 RowView rv = load_row(s, e & EDGE_VAL);
+                w.row();
                 if (!rv.seq) {
-                    if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T)) return RES_TRUE;
+                    if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T, w)) return RES_TRUE;
                     st[sp] = Frame{rv.beg, rv.n_sets, k, 0};
                 } else {
                     st[sp] = Frame{rv.beg, rv.n_sets, k, 1};
@@ -210,7 +242,7 @@ __device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool
             // subject id inside an ordered (ROW_SEQ) row
             uint32_t c = coll_lookup(s, e);
             if (c != NONE32) {
-                int t = V.test_add(c);
+                int t = V.test_add(c, w);
                 if (t == 1) continue;
                 if (t == 2) return RES_OVERFLOW;
             }
@@ -222,9 +254,9 @@ __device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool
 
 // SubjectIsAllowed for one request (engine.go:116-123): depth clamp, then the top-level row
 // whose tuples each start a fresh visited map (shadowed ctx at engine.go:48).
-template <class Stack>
+template <class Stack, class W>
 __device__ int check_one(const DevSnap& s, const DevOverlay& ov, const keto_check_ids& q, int gmd, Visited& V,
-                         Stack& st) {
+                         Stack& st, W& w) {
     int d = q.max_depth;
     if (d <= 0 || gmd < d) d = gmd;
     if (q.row == KETO_NO_ROW || d <= 0 || q.target == KETO_NO_TARGET) return RES_FALSE;
@@ -240,29 +272,34 @@ __device__ int check_one(const DevSnap& s, const DevOverlay& ov, const keto_chec
     } else {
         rv = load_row(s, q.row);
     }
+    w.row();
     if (!rv.seq) {
-        if (!tset && rv.n_ids && find_id(te, rv.beg + rv.n_sets, rv.n_ids, T)) return RES_TRUE;
+        if (!tset && rv.n_ids && find_id(te, rv.beg + rv.n_sets, rv.n_ids, T, w)) return RES_TRUE;
         for (uint32_t i = 0; i < rv.n_sets; ++i) {
             const uint32_t e = te[rv.beg + i];
+            w.edge();
             if (tset && e == tval) return RES_TRUE;
             if (d >= 2) {
                 V.fresh();
-                V.test_add(e & EDGE_VAL);
-                int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st);
+                w.item();
+                V.test_add(e & EDGE_VAL, w);
+                int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st, w);
                 if (r != RES_FALSE) return r;
             }
         }
     } else {
         for (uint32_t i = 0; i < rv.n_sets; ++i) {
             const uint32_t e = te[rv.beg + i];
+            w.edge();
             if (e & EDGE_SET) {
                 if (tset && e == tval) return RES_TRUE;
                 if (d >= 2) {
                     uint32_t vid = coll_lookup(s, e);
                     if (vid == NONE32) vid = e & EDGE_VAL;
                     V.fresh();
-                    V.test_add(vid);
-                    int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st);
+                    w.item();
+                    V.test_add(vid, w);
+                    int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st, w);
                     if (r != RES_FALSE) return r;
                 }
             } else if (!tset && e == tval) {
@@ -285,9 +322,10 @@ struct TierArgs {
     uint32_t* out_count;
 };
 
-template <class Stack>
+template <class Stack, bool COUNT = false>
 __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
-                                                    uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta) {
+                                                    uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
+                                                    unsigned long long* __restrict__ work) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     Visited V;
@@ -300,11 +338,12 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
         st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
         st.n = ta.gstack_n;
     }
+    Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
     for (uint32_t j = slot; j < total; j += stride) {
         const uint32_t i = ta.in_list ? ta.in_list[j] : j;
         const keto_check_ids qq = q[i];
-        int r = check_one(s, ov, qq, gmd, V, st);
+        int r = check_one(s, ov, qq, gmd, V, st, w);
         if (r == RES_OVERFLOW) {
             uint32_t at = atomicAdd(ta.out_count, 1u);
             ta.out_list[at] = i;
@@ -313,6 +352,14 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
         }
     }
     ta.slot_epoch[slot] = V.epoch;
+    if constexpr (COUNT) {
+        atomicAdd(work + 0, (unsigned long long)w.rows);
+        atomicAdd(work + 1, (unsigned long long)w.edges);
+        atomicAdd(work + 2, (unsigned long long)w.idreads);
+        atomicAdd(work + 3, (unsigned long long)w.vprobes);
+        atomicAdd(work + 4, (unsigned long long)w.vinserts);
+        atomicAdd(work + 5, (unsigned long long)w.items);
+    }
 }
 
 // ------------------------------------------------------------------ expand
@@ -338,7 +385,8 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     }
     if (root == KETO_NO_ROW) return EXP_NIL;                // no tuples at all (:68-70)
     V.fresh();
-    V.test_add(root_vid);
+    Work<false> nw;
+    V.test_add(root_vid, nw);
     int sp = 0;
     // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union pushed
     auto open = [&](uint32_t r, int k) -> int {
@@ -389,7 +437,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             if (cv != NONE32) vid = cv;
         }
         const uint16_t k = f.k - 1;
-        int t = V.test_add(vid);
+        int t = V.test_add(vid, nw);
         if (t == 2) return EXP_OVERFLOW;
         if (t == 1) {                                       // visited -> nil -> Leaf(set)
             emit(out, cnt, FILL, e, 0x80000000u);
@@ -470,6 +518,8 @@ struct DeviceState {
     uint32_t* counters = nullptr; // 2 counters
     uint64_t list_cap = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    keto_batch_timing last{};
 
     DevSnap view() const { return DevSnap{rows, edges, row_pp, coll, coll_mask}; }
 };
@@ -528,8 +578,15 @@ void ensure_lists(DeviceState& D, uint64_t n) {
 }
 
 int hw_slots() {
-    // persistent grid: 256 CUs x 8 waves of 64 lanes; every lane owns one visited table
-    return 256 * 8 * 64;
+    // persistent grid sized to residency: 256 CUs x 28 waves (7 per SIMD at the kernel's SGPR
+    // budget) x 64 lanes; every lane owns one visited table.  KETO_SLOTS overrides (tuning).
+    static int v = [] {
+        const char* e = getenv("KETO_SLOTS");
+        int s = e ? atoi(e) : 256 * 28 * 64;
+        s = (s + 255) / 256 * 256;
+        return s < 256 ? 256 : s;
+    }();
+    return v;
 }
 
 TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, uint32_t* out_list,
@@ -584,6 +641,7 @@ void device_upload(Snapshot& S, int device) {
     D->bytes = acc;
     D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.rows.size() + S.n_coll_keys + 1);
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+    for (auto& e : D->ev) HIP_OK(hipEventCreate(&e));
     S.device = device;
     S.dev.reset(D.release());
 }
@@ -600,10 +658,14 @@ void device_release(Snapshot& S) {
     if (D.lists) (void)hipFree(D.lists);
     if (D.counters) (void)hipFree(D.counters);
     if (D.stream) (void)hipStreamDestroy(D.stream);
+    for (auto& e : D.ev)
+        if (e) (void)hipEventDestroy(e);
     S.dev.reset();
 }
 
 uint64_t device_bytes(const Snapshot& S) { return S.dev ? S.dev->bytes : 0; }
+
+keto_batch_timing device_last_timing(const Snapshot& S) { return S.dev ? S.dev->last : keto_batch_timing{}; }
 
 Snapshot::~Snapshot() {
     if (dev) device_release(*this);
@@ -646,23 +708,36 @@ void run_tiers(DeviceState& D, uint32_t n, const Plan& p, hipStream_t st, Launch
     uint32_t* list1 = D.lists + D.list_cap;
     uint32_t* c0 = D.counters;
     uint32_t* c1 = D.counters + 1;
+    ensure_tier(D, 0, p.slots[0], p.cap[0], p.frames[0]);
+    ensure_tier(D, 1, p.slots[1], p.cap[1], p.frames[1]);
     HIP_OK(hipMemsetAsync(D.counters, 0, 4 * sizeof(uint32_t), st));
     // tier 0 over all requests
-    ensure_tier(D, 0, p.slots[0], p.cap[0], p.frames[0]);
+    HIP_OK(hipEventRecord(D.ev[0], st));
     launch(0, D.tiers[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
+    HIP_OK(hipEventRecord(D.ev[1], st));
     // tier 1 over tier-0 overflows (count read on the device)
-    ensure_tier(D, 1, p.slots[1], p.cap[1], p.frames[1]);
     launch(1, D.tiers[1], list0, c0, list1, c1, p.slots[1]);
-    uint32_t left = 0;
-    HIP_OK(hipMemcpyAsync(&left, c1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipEventRecord(D.ev[2], st));
+    uint32_t cnt[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(cnt, c0, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (left) {
+    keto_batch_timing& T = D.last;
+    T = keto_batch_timing{};
+    T.requests[0] = n;
+    T.requests[1] = cnt[0];
+    T.requests[2] = cnt[1];
+    HIP_OK(hipEventElapsedTime(&T.tier_ms[0], D.ev[0], D.ev[1]));
+    HIP_OK(hipEventElapsedTime(&T.tier_ms[1], D.ev[1], D.ev[2]));
+    if (cnt[1]) {
         ensure_tier(D, 2, p.slots[2], p.cap[2], p.frames[2]);
         HIP_OK(hipMemsetAsync(c0, 0, sizeof(uint32_t), st));
+        HIP_OK(hipEventRecord(D.ev[3], st));
         launch(2, D.tiers[2], list1, c1, list0, c0, p.slots[2]);
+        HIP_OK(hipEventRecord(D.ev[4], st));
         uint32_t still = 0;
         HIP_OK(hipMemcpyAsync(&still, c0, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipEventElapsedTime(&T.tier_ms[2], D.ev[3], D.ev[4]));
         if (still) throw Error{KETO_E_RANGE, "visited table overflow on the final tier"};
     }
 }
@@ -707,7 +782,7 @@ struct DevFree {
 }  // namespace
 
 void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
-                  bool host_buffers, void* stream, const Overlay* ovh) {
+                  bool host_buffers, void* stream, const Overlay* ovh, uint64_t* work_out) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
@@ -732,18 +807,39 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     Plan p = make_plan(D, n, gmd);
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
+    unsigned long long* dwork = nullptr;
+    if (work_out) {
+        uint64_t acc = 0;
+        dwork = dmalloc<unsigned long long>(8, acc);
+        tmp.p.push_back(dwork);
+        HIP_OK(hipMemsetAsync(dwork, 0, 8 * sizeof(unsigned long long), st));
+    }
     run_tiers(D, n, p, st,
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
                   dim3 grid(slots / 256), block(256);
-                  if (p.frames[level] == 0)
-                      hipLaunchKernelGGL(check_kernel<LocalStack<16>>, grid, block, 0, st, sv, dov, dq, n, gmd, da,
-                                         a);
+                  const bool local = p.frames[level] == 0;
+                  if (local && !dwork)
+                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, false>), grid, block, 0, st, sv, dov, dq, n,
+                                         gmd, da, a, dwork);
+                  else if (!dwork)
+                      hipLaunchKernelGGL((check_kernel<GlobalStack, false>), grid, block, 0, st, sv, dov, dq, n, gmd,
+                                         da, a, dwork);
+                  else if (local)
+                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, true>), grid, block, 0, st, sv, dov, dq, n, gmd,
+                                         da, a, dwork);
                   else
-                      hipLaunchKernelGGL(check_kernel<GlobalStack>, grid, block, 0, st, sv, dov, dq, n, gmd, da, a);
+                      hipLaunchKernelGGL((check_kernel<GlobalStack, true>), grid, block, 0, st, sv, dov, dq, n, gmd,
+                                         da, a, dwork);
                   HIP_OK(hipGetLastError());
               });
+    if (work_out) {
+        unsigned long long h[8];
+        HIP_OK(hipMemcpyAsync(h, dwork, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        for (int i = 0; i < 8; ++i) work_out[i] = h[i];
+    }
     if (host_buffers) {
         HIP_OK(hipMemcpyAsync(allowed, da, n, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));

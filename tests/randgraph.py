@@ -8,7 +8,7 @@ from oracle.oracle_sql import RelationTuple, SQLStore, SubjectID, SubjectSet
 
 
 def random_graph(seed, n_tuples=None, page_size=None, allow_wildcards=True, allow_poison=True,
-                 allow_collisions=True):
+                 allow_collisions=True, wide=False):
     rng = random.Random(seed)
     n_ns = rng.randint(1, 3)
     ids = rng.sample([0, 1, 2, 5, 7, 10], n_ns)
@@ -19,17 +19,20 @@ def random_graph(seed, n_tuples=None, page_size=None, allow_wildcards=True, allo
     objs = ["a", "b", "c", "d", "a#b", "B", "é"][: rng.randint(2, 7)]
     rels = ["r", "s", "b#c", "t"][: rng.randint(1, 4)]
     users = ["u", "v", "w", "U"][: rng.randint(1, 4)]
+    if wide:  # few rows with long, byte-ordered subject-id regions (binary-search paths)
+        objs = objs[:2]
+        users = [f"u{i:03d}" for i in rng.sample(range(1000), 80)]
     if allow_collisions:
         # an id whose text equals a set's String() (SURVEY A.Q4 / DF3)
         for _ in range(rng.randint(0, 2)):
             ns = rng.choice(names)
             users.append(f"{ns}:{rng.choice(objs)}#{rng.choice(rels)}")
-    n = n_tuples if n_tuples is not None else rng.randint(0, 40)
+    n = n_tuples if n_tuples is not None else (rng.randint(100, 400) if wide else rng.randint(0, 40))
     tuples, raw = [], []
     for _ in range(n):
         ns = rng.choice(names)
         o, r = rng.choice(objs), rng.choice(rels)
-        if rng.random() < 0.45:
+        if rng.random() < (0.85 if wide else 0.45):
             sub = SubjectID(rng.choice(users))
         else:
             so, sr = rng.choice(objs), rng.choice(rels)

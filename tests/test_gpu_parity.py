@@ -43,10 +43,10 @@ def test_golden_on_gpu(case):
             assert st == EXPAND_TREE and js == ex["expected"]
 
 
-@pytest.mark.parametrize("seed", range(300))
-def test_random_graphs_match_oracle(seed):
+@pytest.mark.parametrize("seed,wide", [(s, False) for s in range(300)] + [(s, True) for s in range(1000, 1060)])
+def test_random_graphs_match_oracle(seed, wide):
     from keto_amd.capi import EXPAND_NIL, EXPAND_NOT_FOUND, EXPAND_TREE
-    store, ns, tuples, raw, ps, alph = random_store(seed)
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=wide)
     snap = _snapshot(ns, rows_from_tuples(ns, tuples, raw), ps)
     checks = random_checks(seed, alph, k=24)
     # the engine takes one global max-depth per batch: group by it

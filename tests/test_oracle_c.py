@@ -32,9 +32,9 @@ def _sql_expand(store, sub, d, g):
     return ("nil", None) if t is None else ("tree", t.to_json())
 
 
-@pytest.mark.parametrize("seed", range(400))
-def test_c_oracle_matches_sql_oracle(seed):
-    store, _ns, _t, _raw, _ps, alph = random_store(seed)
+@pytest.mark.parametrize("seed,wide", [(s, False) for s in range(400)] + [(s, True) for s in range(1000, 1040)])
+def test_c_oracle_matches_sql_oracle(seed, wide):
+    store, _ns, _t, _raw, _ps, alph = random_store(seed, wide=wide)
     tab = OracleTable.from_store(store)
     for tup, d, g in random_checks(seed, alph):
         want = CheckEngine(store, g).subject_is_allowed(tup, d)

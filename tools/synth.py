@@ -1,0 +1,142 @@
+"""ctypes front-end of tools/synth.cpp: synthetic ACL graphs / request batches (bench tooling)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "synth.cpp")
+LIB = os.path.join(HERE, "libketo_synth.so")
+
+NAMESPACES = [(1, "docs"), (2, "folders"), (3, "groups")]
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", SRC, "-o", LIB])
+    return LIB
+
+
+class Params(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("n_folders", C.c_uint64), ("n_groups", C.c_uint64),
+                ("n_users", C.c_uint64), ("target_edges", C.c_uint64), ("seed", C.c_uint64)]
+
+
+class Graph(C.Structure):
+    _fields_ = [("n_rows", C.c_uint32), ("row_ns", C.POINTER(C.c_int32)), ("row_obj", C.POINTER(C.c_uint32)),
+                ("row_rel", C.POINTER(C.c_uint32)), ("row_ptr", C.POINTER(C.c_uint64)),
+                ("edges", C.POINTER(C.c_uint32)), ("n_edges", C.c_uint64), ("n_set_edges", C.c_uint64)]
+
+
+class Table(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("ns", C.c_void_p), ("obj", C.c_void_p), ("rel", C.c_void_p),
+                ("kind", C.c_void_p), ("sid", C.c_void_p), ("sns", C.c_void_p), ("sobj", C.c_void_p),
+                ("srel", C.c_void_p), ("key", C.c_void_p)]
+
+
+# BASELINE.json config #4: 1,000,000,000 tuples, ~30 % subject-set edges (seed 4)
+POWERLAW_1B = dict(n_docs=1 << 27, n_folders=1 << 24, n_groups=1 << 22, n_users=1 << 26,
+                   target_edges=1_000_000_000, seed=4)
+
+
+def scaled(params: dict, scale: float) -> dict:
+    p = dict(params)
+    for k in ("n_docs", "n_folders", "n_groups", "n_users"):
+        p[k] = max(64, int(p[k] * scale))
+    p["target_edges"] = int(p["target_edges"] * scale)
+    return p
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = C.CDLL(LIB)
+    return _lib
+
+
+class SynthGraph:
+    def __init__(self, params: dict, threads: int = 16):
+        self.params = params
+        self.p = Params(**{k: params[k] for k, _ in Params._fields_})
+        self.g = Graph()
+        rc = lib().synth_generate(C.byref(self.p), C.c_int(threads), C.byref(self.g))
+        if rc != 0:
+            raise RuntimeError(f"synth_generate failed: {rc}")
+        R, E = self.g.n_rows, self.g.n_edges
+        self.row_ns = np.ctypeslib.as_array(self.g.row_ns, shape=(R,))
+        self.row_obj = np.ctypeslib.as_array(self.g.row_obj, shape=(R,))
+        self.row_rel = np.ctypeslib.as_array(self.g.row_rel, shape=(R,))
+        self.row_ptr = np.ctypeslib.as_array(self.g.row_ptr, shape=(R + 1,))
+        self.edges = np.ctypeslib.as_array(self.g.edges, shape=(max(E, 1),))[:E]
+
+    @property
+    def n_rows(self):
+        return self.g.n_rows
+
+    @property
+    def n_edges(self):
+        return self.g.n_edges
+
+    @property
+    def n_set_edges(self):
+        return self.g.n_set_edges
+
+    def close(self):
+        if self.g.row_ptr:
+            lib().synth_free(C.byref(self.g))
+
+    def queries(self, n: int, seed: int, depth: int = 5, threads: int = 16) -> np.ndarray:
+        from keto_amd.capi import CHECK_IDS_DTYPE
+        out = np.zeros(n, dtype=CHECK_IDS_DTYPE)
+        lib().synth_queries(C.byref(self.g), C.byref(self.p), C.c_uint64(n), C.c_uint64(seed), C.c_int32(depth),
+                            out.ctypes.data_as(C.c_void_p), C.c_int(threads))
+        return out
+
+    def snapshot(self, device=0):
+        from keto_amd.capi import Snapshot
+        return Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
+                                 device=device)
+
+    def oracle_table(self, q: np.ndarray, depth: int):
+        """OracleTable over every row a depth-bounded check of the sample can query."""
+        from oracle.oracle_c import OracleTable
+        t = Table()
+        lib().synth_extract(C.byref(self.g), C.byref(self.p), q.ctypes.data_as(C.c_void_p), C.c_uint64(len(q)),
+                            C.c_int32(depth), C.byref(t))
+        n = t.n
+
+        def arr(ptr, dt):
+            buf = (C.c_char * (max(n, 1) * np.dtype(dt).itemsize)).from_address(ptr)
+            return np.frombuffer(buf, dtype=dt, count=n).copy()
+
+        arrays = dict(ns=arr(t.ns, np.int32), obj=arr(t.obj, np.uint32), rel=arr(t.rel, np.uint32),
+                      kind=arr(t.kind, np.uint8), sid=arr(t.sid, np.uint32), sns=arr(t.sns, np.int32),
+                      sobj=arr(t.sobj, np.uint32), srel=arr(t.srel, np.uint32), key=arr(t.key, np.uint32))
+        lib().synth_table_free(C.byref(t))
+        # string space: objects / relations are per-row ids; namespace names and "" get ids above them
+        strings = {"": 0xFFFFFFF0, "docs": 0xFFFF0001, "folders": 0xFFFF0002, "groups": 0xFFFF0003}
+        return OracleTable(NAMESPACES, arrays, strings, {}, page_size=100)
+
+    def oracle_requests(self, tab, q: np.ndarray):
+        """keto_check_ids -> oracle requests (docs:d#view@u, request max-depth kept)."""
+        from oracle.oracle_c import OraCheckReq
+        reqs = []
+        for r in q:
+            x = OraCheckReq()
+            x.q.ns = int(self.row_ns[r["row"]])
+            x.q.obj = int(self.row_obj[r["row"]])
+            x.q.rel = int(self.row_rel[r["row"]])
+            x.q_ns_unknown = 0
+            x.t.kind = 0
+            x.t.sid = int(r["target"])
+            x.t.key = int(r["target"])
+            x.max_depth = int(r["max_depth"])
+            reqs.append(x)
+        return reqs
