@@ -188,127 +188,36 @@ struct GlobalStack {
 };
 
 // ------------------------------------------------------------------ check
-// Further(r0, k0) below a top-level tuple (engine.go:82-114 + :36-80), V already holds the
-// top-level subject.  Returns RES_TRUE / RES_FALSE / RES_OVERFLOW.
-template <class Stack, class W>
-__device__ int check_dfs(const DevSnap& s, uint32_t r0, int k0, uint32_t T, bool tset, Visited& V, Stack& st, W& w) {
-    const uint32_t tval = tset ? (EDGE_SET | T) : T;
-    int sp = 0;
-    {
-        RowView rv = load_row(s, r0);
-        w.row();
-        if (!rv.seq) {
-            if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T, w)) return RES_TRUE;
-            st[0] = Frame{rv.beg, rv.n_sets, (uint16_t)k0, 0};
-        } else {
-            st[0] = Frame{rv.beg, rv.n_sets, (uint16_t)k0, 1};
+// Visited map with the first REG_VIDS visit ids in registers; a map that grows past them spills
+// into the lane's epoch-tagged HBM table (Visited).  Typical check items mark a handful of sets.
+constexpr int REG_VIDS = 16;
+struct VisitedRS {
+    uint32_t r[REG_VIDS];
+    uint32_t n;          // entries in r; REG_VIDS + 1 = spilled to V
+    Visited V;
+    __device__ inline void fresh() { n = 0; }
+    template <class W>
+    __device__ inline int test_add(uint32_t vid, W& w) {
+        if (n <= (uint32_t)REG_VIDS) {
+            bool hit = false;
+#pragma unroll
+            for (int i = 0; i < REG_VIDS; ++i) hit |= ((uint32_t)i < n) & (r[i] == vid);
+            if (hit) return 1;
+            if (n < (uint32_t)REG_VIDS) {
+#pragma unroll
+                for (int i = 0; i < REG_VIDS; ++i)
+                    if ((uint32_t)i == n) r[i] = vid;
+                ++n;
+                return 0;
+            }
+            V.fresh();                                  // spill
+#pragma unroll
+            for (int i = 0; i < REG_VIDS; ++i) V.test_add(r[i], w);
+            n = REG_VIDS + 1;
         }
-        sp = 1;
+        return V.test_add(vid, w);
     }
-    while (sp > 0) {
-        Frame& f = st[sp - 1];
-        if (f.left == 0) {
-            --sp;
-            continue;
-        }
-        const uint32_t e = s.edges[f.pos];
-        w.edge();
-        f.pos++;
-        f.left--;
-        if (e & EDGE_SET) {
-            uint32_t vid = e & EDGE_VAL;
-            if (f.seq) {
-                uint32_t c = coll_lookup(s, e);
-                if (c != NONE32) vid = c;
-            }
-            int t = V.test_add(vid, w);
-            if (t == 1) continue;
-            if (t == 2) return RES_OVERFLOW;
-            if (tset && e == tval) return RES_TRUE;
-            if (f.k >= 2) {
-                if (sp == st.cap()) return RES_OVERFLOW;
-                const uint16_t k = f.k - 1;
-                RowView rv = load_row(s, e & EDGE_VAL);
-                w.row();
-                if (!rv.seq) {
-                    if (!tset && rv.n_ids && find_id(s.edges, rv.beg + rv.n_sets, rv.n_ids, T, w)) return RES_TRUE;
-                    st[sp] = Frame{rv.beg, rv.n_sets, k, 0};
-                } else {
-                    st[sp] = Frame{rv.beg, rv.n_sets, k, 1};
-                }
-                ++sp;
-            }
-        } else {
-            // subject id inside an ordered (ROW_SEQ) row
-            uint32_t c = coll_lookup(s, e);
-            if (c != NONE32) {
-                int t = V.test_add(c, w);
-                if (t == 1) continue;
-                if (t == 2) return RES_OVERFLOW;
-            }
-            if (!tset && e == tval) return RES_TRUE;
-        }
-    }
-    return RES_FALSE;
-}
-
-// SubjectIsAllowed for one request (engine.go:116-123): depth clamp, then the top-level row
-// whose tuples each start a fresh visited map (shadowed ctx at engine.go:48).
-template <class Stack, class W>
-__device__ int check_one(const DevSnap& s, const DevOverlay& ov, const keto_check_ids& q, int gmd, Visited& V,
-                         Stack& st, W& w) {
-    int d = q.max_depth;
-    if (d <= 0 || gmd < d) d = gmd;
-    if (q.row == KETO_NO_ROW || d <= 0 || q.target == KETO_NO_TARGET) return RES_FALSE;
-    const bool tset = (q.flags & 1u) != 0;
-    const uint32_t T = q.target;
-    const uint32_t tval = tset ? (EDGE_SET | T) : T;
-    const uint32_t* te = s.edges;
-    RowView rv;
-    if (q.row >= ov.base) {
-        DevSnap o{ov.rows, ov.edges, ov.pp, nullptr, 0};
-        rv = load_row(o, q.row - ov.base);
-        te = ov.edges;
-    } else {
-        rv = load_row(s, q.row);
-    }
-    w.row();
-    if (!rv.seq) {
-        if (!tset && rv.n_ids && find_id(te, rv.beg + rv.n_sets, rv.n_ids, T, w)) return RES_TRUE;
-        for (uint32_t i = 0; i < rv.n_sets; ++i) {
-            const uint32_t e = te[rv.beg + i];
-            w.edge();
-            if (tset && e == tval) return RES_TRUE;
-            if (d >= 2) {
-                V.fresh();
-                w.item();
-                V.test_add(e & EDGE_VAL, w);
-                int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st, w);
-                if (r != RES_FALSE) return r;
-            }
-        }
-    } else {
-        for (uint32_t i = 0; i < rv.n_sets; ++i) {
-            const uint32_t e = te[rv.beg + i];
-            w.edge();
-            if (e & EDGE_SET) {
-                if (tset && e == tval) return RES_TRUE;
-                if (d >= 2) {
-                    uint32_t vid = coll_lookup(s, e);
-                    if (vid == NONE32) vid = e & EDGE_VAL;
-                    V.fresh();
-                    w.item();
-                    V.test_add(vid, w);
-                    int r = check_dfs(s, e & EDGE_VAL, d - 1, T, tset, V, st, w);
-                    if (r != RES_FALSE) return r;
-                }
-            } else if (!tset && e == tval) {
-                return RES_TRUE;
-            }
-        }
-    }
-    return RES_FALSE;
-}
+};
 
 struct TierArgs {
     uint64_t* vtab;          // n_slots * (mask+1) entries
@@ -322,17 +231,31 @@ struct TierArgs {
     uint32_t* out_count;
 };
 
-template <class Stack, bool COUNT = false>
+
+constexpr uint16_t FR_SEQ = 1, FR_TOP = 2, FR_OV = 4;
+
+// Batched SubjectIsAllowed (internal/check/engine.go:36-123) as a per-lane state machine.
+// A lane owns one request at a time; each loop iteration does ONE of
+//   (a) fetch the next request of this lane, or
+//   (b) one edge of the current row: the top-level row (frame flag FR_TOP) starts a fresh visited
+//       map per subject set (the shadowed ctx at engine.go:48), deeper rows test-and-set it
+//       (graph_utils.go:13-35), in ORDER BY order,
+// then, if (a) or (b) produced one, enters a row: loads its 16-B record, searches its byte-ordered
+// subject-id region for the requested id, and pushes it as the current frame.  Lanes that finish
+// a request take the next one on the following iteration, so a wave never waits for its slowest
+// request.  Only a set reached with remaining depth >= 2 is entered (engine.go:65-69,88-91).
+template <class Stack, bool COUNT, int TIER>
 __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
                                                     uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
                                                     unsigned long long* __restrict__ work) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
-    Visited V;
-    V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
-    V.mask = ta.mask;
-    V.epoch = ta.slot_epoch[slot];
-    V.count = 0;
+    VisitedRS V;
+    V.n = 0;
+    V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
+    V.V.mask = ta.mask;
+    V.V.epoch = ta.slot_epoch[slot];
+    V.V.count = 0;
     Stack st;
     if constexpr (std::is_same<Stack, GlobalStack>::value) {
         st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
@@ -340,18 +263,107 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
     }
     Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
-    for (uint32_t j = slot; j < total; j += stride) {
-        const uint32_t i = ta.in_list ? ta.in_list[j] : j;
-        const keto_check_ids qq = q[i];
-        int r = check_one(s, ov, qq, gmd, V, st, w);
-        if (r == RES_OVERFLOW) {
-            uint32_t at = atomicAdd(ta.out_count, 1u);
-            ta.out_list[at] = i;
+    uint32_t j = slot;
+    bool busy = false;           // a request is in flight on this lane
+    uint32_t qi = 0, T = 0, tval = 0;
+    bool tset = false;
+    Frame cur{0, 0, 0, 0};
+    int sp = 0;
+    for (;;) {
+        uint32_t enter = NONE32;     // row to enter this iteration
+        uint16_t enter_k = 0, enter_fl = 0;
+        int res = -1;                // >= 0: request decided (RES_*)
+        if (!busy) {
+            if (j >= total) break;
+            qi = ta.in_list ? ta.in_list[j] : j;
+            j += stride;
+            const keto_check_ids qq = q[qi];
+            int d = qq.max_depth;
+            if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
+            if (qq.row == KETO_NO_ROW || d <= 0 || qq.target == KETO_NO_TARGET) {
+                allowed[qi] = 0;
+                continue;
+            }
+            busy = true;
+            tset = (qq.flags & 1u) != 0;
+            T = qq.target;
+            tval = tset ? (EDGE_SET | T) : T;
+            sp = 0;
+            enter = qq.row;
+            enter_k = (uint16_t)d;
+            enter_fl = FR_TOP | (qq.row >= ov.base ? FR_OV : 0);
+        } else if (cur.left == 0) {                               // row exhausted: pop
+            if (--sp == 0) res = RES_FALSE;
+            else cur = st[sp - 1];
         } else {
-            allowed[i] = (uint8_t)r;
+            const uint32_t e = (cur.seq & FR_OV) ? ov.edges[cur.pos] : s.edges[cur.pos];
+            ++cur.pos;
+            --cur.left;
+            w.edge();
+            if (e & EDGE_SET) {
+                uint32_t vid = e & EDGE_VAL;
+                if (cur.seq & FR_SEQ) {
+                    uint32_t c = coll_lookup(s, e);
+                    if (c != NONE32) vid = c;
+                }
+                int t;
+                if (cur.seq & FR_TOP) {                           // fresh map per top-level tuple
+                    V.fresh();
+                    w.item();
+                    t = V.test_add(vid, w);
+                } else {
+                    t = V.test_add(vid, w);
+                }
+                if (t == 2) res = RES_OVERFLOW;
+                else if (t == 0) {
+                    if (tset && e == tval) res = RES_TRUE;        // engine.go:54-57
+                    else if (cur.k >= 2) {                        // remaining depth after the hop >= 1
+                        enter = e & EDGE_VAL;
+                        enter_k = cur.k - 1;
+                        enter_fl = 0;
+                    }
+                }
+            } else {                                              // subject id in an ordered row
+                int t = 0;
+                if (!(cur.seq & FR_TOP)) {
+                    uint32_t c = coll_lookup(s, e);
+                    if (c != NONE32) t = V.test_add(c, w);
+                }
+                if (t == 2) res = RES_OVERFLOW;
+                else if (t == 0 && !tset && e == tval) res = RES_TRUE;
+            }
+        }
+        if (enter != NONE32) {
+            RowView rv;
+            if (enter_fl & FR_OV) {
+                DevSnap o{ov.rows, ov.edges, ov.pp, nullptr, 0};
+                rv = load_row(o, enter - ov.base);
+            } else {
+                rv = load_row(s, enter);
+            }
+            w.row();
+            const uint32_t* eb = (enter_fl & FR_OV) ? ov.edges : s.edges;
+            if (!rv.seq && !tset && rv.n_ids && find_id(eb, rv.beg + rv.n_sets, rv.n_ids, T, w)) {
+                res = RES_TRUE;
+            } else if (sp >= st.cap()) {
+                res = RES_OVERFLOW;
+            } else {
+                if (sp > 0) st[sp - 1] = cur;
+                cur = Frame{rv.beg, rv.n_sets, enter_k, (uint16_t)(enter_fl | (rv.seq ? FR_SEQ : 0))};
+                ++sp;
+            }
+        }
+        if (res >= 0) {
+            if (res == RES_OVERFLOW) {
+                uint32_t at = atomicAdd(ta.out_count, 1u);
+                ta.out_list[at] = qi;
+            } else {
+                allowed[qi] = (uint8_t)res;
+            }
+            busy = false;
         }
     }
-    ta.slot_epoch[slot] = V.epoch;
+    ta.slot_epoch[slot] = V.V.epoch;
     if constexpr (COUNT) {
         atomicAdd(work + 0, (unsigned long long)w.rows);
         atomicAdd(work + 1, (unsigned long long)w.edges);
@@ -820,17 +832,21 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
                   TierArgs a = tier_args(t, il, ic, ol, oc);
                   dim3 grid(slots / 256), block(256);
                   const bool local = p.frames[level] == 0;
-                  if (local && !dwork)
-                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, false>), grid, block, 0, st, sv, dov, dq, n,
+                  // TIER is only a name tag: tier-0 launches are their own symbol in rocprof traces
+                  if (local && !dwork && level == 0)
+                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, false, 0>), grid, block, 0, st, sv, dov, dq, n,
+                                         gmd, da, a, dwork);
+                  else if (local && !dwork)
+                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, false, 1>), grid, block, 0, st, sv, dov, dq, n,
                                          gmd, da, a, dwork);
                   else if (!dwork)
-                      hipLaunchKernelGGL((check_kernel<GlobalStack, false>), grid, block, 0, st, sv, dov, dq, n, gmd,
-                                         da, a, dwork);
+                      hipLaunchKernelGGL((check_kernel<GlobalStack, false, 1>), grid, block, 0, st, sv, dov, dq, n,
+                                         gmd, da, a, dwork);
                   else if (local)
-                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, true>), grid, block, 0, st, sv, dov, dq, n, gmd,
-                                         da, a, dwork);
+                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, true, 1>), grid, block, 0, st, sv, dov, dq, n,
+                                         gmd, da, a, dwork);
                   else
-                      hipLaunchKernelGGL((check_kernel<GlobalStack, true>), grid, block, 0, st, sv, dov, dq, n, gmd,
+                      hipLaunchKernelGGL((check_kernel<GlobalStack, true, 1>), grid, block, 0, st, sv, dov, dq, n, gmd,
                                          da, a, dwork);
                   HIP_OK(hipGetLastError());
               });
