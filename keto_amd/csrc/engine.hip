@@ -1,30 +1,32 @@
 // MI355X (gfx950) device engine for batched check and expand.
 //
 // Kernels
-//   check_kernel<Stack>   exact, order-faithful depth-bounded DFS per request, one lane per
-//                         request (grid-stride over a persistent grid).  Reproduces
-//                         check.(*Engine).SubjectIsAllowed / checkOneIndirectionFurther /
-//                         subjectIsAllowed (internal/check/engine.go:36-123) including the
-//                         first-encounter visited map keyed by Subject.String()
-//                         (internal/x/graph/graph_utils.go:13-35) that is fresh for every
-//                         top-level tuple and shared below it.
-//   expand_kernel<FILL>   the same traversal for expand.(*Engine).BuildTree
-//                         (internal/expand/engine.go:33-102): one visited map per tree, counted
-//                         first (FILL=false) then written in pre-order (FILL=true).
+//   check_kernel   exact, order-faithful, depth-bounded DFS per request as a per-lane state machine
+//                  over a persistent grid.  Reproduces check.(*Engine).SubjectIsAllowed /
+//                  checkOneIndirectionFurther / subjectIsAllowed (internal/check/engine.go:36-123),
+//                  including the first-encounter visited map keyed by Subject.String()
+//                  (internal/x/graph/graph_utils.go:13-35) that is fresh for every top-level tuple
+//                  and shared below it.
+//   expand_kernel  the same traversal for expand.(*Engine).BuildTree (internal/expand/engine.go:
+//                  33-102): one visited map per tree, counted first (FILL=false), then written in
+//                  pre-order (FILL=true).
 //
-// Memory traffic per row visit: one 16-B RowRec (dwordx4), the subject-set region scanned in
-// order, and for a requested subject id a binary search of the row's byte-ordered id region
-// (an id never changes the visited map unless its key collides, so only membership matters:
-// that is what makes the search exact).  Visited maps are per-lane open-addressing tables in HBM
-// tagged with an epoch, so starting a fresh map is one register increment, never a clear.
-// Tables that fill past 1/2 abort the request, which is re-run on a tier with larger tables;
-// the last tier is sized so it cannot overflow.  No request ever leaves the GPU.
+// Data: the snapshot is one u32 arena per device (layout in snapshot.hpp).  A row visit reads the
+// row's 16-B header, which sits right in front of its edges, so the header line usually also holds
+// the subject sets and a short id region.  A requested subject id is looked up in the row's
+// byte-ordered id region (binary search, <= HASH_MIN ids) or in the open-addressing id table stored
+// in front of the header: an id never changes the visited map unless its key collides, so only
+// membership matters, which is what makes looking it up (instead of walking to it) exact.
+// Visited maps keep their first REG_VIDS visit ids in registers and spill into a per-lane,
+// epoch-tagged table in HBM; a table filling past 1/2 aborts the request, which is re-run on a
+// tier with larger tables; the last tier is sized so it cannot overflow.  No request leaves the GPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
-#include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "snapshot.hpp"
@@ -43,18 +45,14 @@ constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_OVERFLOW = 2;
 constexpr int EXP_TREE = 0, EXP_NIL = 1, EXP_ERROR = 2, EXP_OVERFLOW = 3;
 
 struct DevSnap {
-    const uint4* rows;
-    const uint32_t* edges;
-    const uint32_t* row_pp;
-    const uint64_t* coll;     // (key << 32) | vid ; empty = ~0
+    const uint32_t* arena;    // main arena (u32 words)
+    const uint64_t* coll;     // (edge value << 32) | visit id ; empty = ~0
     uint32_t coll_mask;       // 0 = no collisions
 };
 
-struct DevOverlay {           // batch-local wildcard rows (top-level / root only), ids >= base
-    const uint4* rows;
-    const uint32_t* edges;
-    const uint32_t* pp;
-    uint32_t base;            // 0xFFFFFFFF = none
+struct DevOverlay {           // batch-local wildcard rows (top-level / root only)
+    const uint32_t* arena;
+    uint32_t base;            // handles >= base live in this arena (unit = handle - base)
 };
 
 __host__ __device__ inline uint32_t mix32(uint32_t k) {
@@ -78,18 +76,31 @@ __device__ inline uint32_t coll_lookup(const DevSnap& s, uint32_t key) {
 }
 
 struct RowView {
-    uint64_t beg;
-    uint32_t n_sets, n_ids;
+    const uint32_t* a;        // arena holding the row
+    uint64_t beg;             // word index of the first edge
+    uint32_t n_sets, n_ids;   // effective counts (ROW_SEQ: n_sets = all edges, in order)
+    uint32_t hlog2;           // id table size (0 = none), table ends at beg - HDR_WORDS
+    uint32_t pp;              // first poisoned page (expand)
     bool seq;
 };
 
-__device__ inline RowView load_row(const DevSnap& s, uint32_t r) {
-    uint4 v = s.rows[r];
+__device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint32_t h) {
     RowView rv;
-    rv.beg = (uint64_t)v.x | ((uint64_t)(v.y & 0xFFu) << 32);
-    rv.seq = ((v.y >> 8) & ROW_SEQ) != 0;
-    rv.n_sets = v.z;
-    rv.n_ids = v.w;
+    uint64_t w;
+    if (h >= ov.base) {
+        rv.a = ov.arena;
+        w = (uint64_t)(h - ov.base) * HDR_WORDS;
+    } else {
+        rv.a = s.arena;
+        w = (uint64_t)h * HDR_WORDS;
+    }
+    const uint4 v = *reinterpret_cast<const uint4*>(rv.a + w);
+    rv.beg = w + HDR_WORDS;
+    rv.n_sets = v.x;
+    rv.n_ids = v.y;
+    rv.seq = (v.z & HDR_SEQ) != 0;
+    rv.hlog2 = (v.z >> 8) & 31u;
+    rv.pp = v.w;
     return rv;
 }
 
@@ -114,10 +125,27 @@ struct Work<true> {
     __device__ inline void item() { ++items; }
 };
 
-// lower_bound over the byte-ordered subject-id region
+// Is subject id t in the row's (effective) id region?
 template <class W>
-__device__ inline bool find_id(const uint32_t* __restrict__ e, uint64_t b, uint32_t n, uint32_t t, W& w) {
-    // invariant: the first element >= t lies in [lo, hi]  (hi itself included)
+__device__ inline bool row_has_id(const RowView& rv, uint32_t t, W& w) {
+    if (rv.n_ids == 0) return false;
+    const uint32_t* __restrict__ e = rv.a;
+    if (rv.hlog2) {
+        // open-addressing table in front of the header: [beg - HDR_WORDS - 2^hlog2, beg - HDR_WORDS)
+        const uint32_t mask = (1u << rv.hlog2) - 1u;
+        const uint64_t tb = rv.beg - HDR_WORDS - (1ull << rv.hlog2);
+        uint32_t i = mix32(t) & mask;
+        for (;;) {
+            const uint32_t v = e[tb + i];
+            w.idread(1);
+            if (v == t) return true;
+            if (v == NONE32) return false;
+            i = (i + 1) & mask;
+        }
+    }
+    // lower_bound over the byte-ordered id region; invariant: answer in [lo, hi] (hi included)
+    const uint64_t b = rv.beg + rv.n_sets;
+    const uint32_t n = rv.n_ids;
     uint32_t lo = 0, hi = n;
     while (hi - lo > 8) {
         uint32_t m = (lo + hi) >> 1;
@@ -167,30 +195,9 @@ struct Visited {
     }
 };
 
-struct Frame {
-    uint64_t pos;
-    uint32_t left;
-    uint16_t k;
-    uint16_t seq;
-};
-
-template <int N>
-struct LocalStack {
-    Frame f[N];
-    __device__ inline Frame& operator[](int i) { return f[i]; }
-    __device__ static constexpr int cap() { return N; }
-};
-struct GlobalStack {
-    Frame* f;           // this lane's frames, stride 1
-    int n;
-    __device__ inline Frame& operator[](int i) { return f[i]; }
-    __device__ inline int cap() const { return n; }
-};
-
-// ------------------------------------------------------------------ check
-// Visited map with the first REG_VIDS visit ids in registers; a map that grows past them spills
-// into the lane's epoch-tagged HBM table (Visited).  Typical check items mark a handful of sets.
-constexpr int REG_VIDS = 16;
+// The first REG_VIDS visit ids of a map live in registers; a map that grows past them spills into
+// the lane's HBM table.  Typical check items mark a handful of subject sets.
+constexpr int REG_VIDS = 12;
 struct VisitedRS {
     uint32_t r[REG_VIDS];
     uint32_t n;          // entries in r; REG_VIDS + 1 = spilled to V
@@ -219,6 +226,27 @@ struct VisitedRS {
     }
 };
 
+struct Frame {
+    uint64_t pos;      // word index of the next edge
+    uint32_t left;
+    uint16_t k;        // remaining depth of the row
+    uint16_t fl;       // FR_* flags
+};
+constexpr uint16_t FR_SEQ = 1, FR_TOP = 2, FR_OV = 4;
+
+template <int N>
+struct LocalStack {
+    Frame f[N];
+    __device__ inline Frame& operator[](int i) { return f[i]; }
+    __device__ static constexpr int cap() { return N; }
+};
+struct GlobalStack {
+    Frame* f;           // this lane's frames
+    int n;
+    __device__ inline Frame& operator[](int i) { return f[i]; }
+    __device__ inline int cap() const { return n; }
+};
+
 struct TierArgs {
     uint64_t* vtab;          // n_slots * (mask+1) entries
     uint32_t mask;
@@ -231,19 +259,17 @@ struct TierArgs {
     uint32_t* out_count;
 };
 
-
-constexpr uint16_t FR_SEQ = 1, FR_TOP = 2, FR_OV = 4;
-
+// ------------------------------------------------------------------ check
 // Batched SubjectIsAllowed (internal/check/engine.go:36-123) as a per-lane state machine.
 // A lane owns one request at a time; each loop iteration does ONE of
-//   (a) fetch the next request of this lane, or
-//   (b) one edge of the current row: the top-level row (frame flag FR_TOP) starts a fresh visited
-//       map per subject set (the shadowed ctx at engine.go:48), deeper rows test-and-set it
+//   (a) fetch the lane's next request, or
+//   (b) one edge of the current row: the top-level row (FR_TOP) starts a fresh visited map per
+//       subject set (the shadowed ctx at engine.go:48), deeper rows test-and-set it
 //       (graph_utils.go:13-35), in ORDER BY order,
-// then, if (a) or (b) produced one, enters a row: loads its 16-B record, searches its byte-ordered
-// subject-id region for the requested id, and pushes it as the current frame.  Lanes that finish
-// a request take the next one on the following iteration, so a wave never waits for its slowest
-// request.  Only a set reached with remaining depth >= 2 is entered (engine.go:65-69,88-91).
+// then, if (a) or (b) produced one, enters a row: reads its header, looks the requested id up in
+// it, and pushes it as the current frame.  A lane that decides a request takes the next one on the
+// following iteration, so a wave never waits for its slowest request.  Only a subject set reached
+// with remaining depth >= 2 is entered (engine.go:65-69,88-91).
 template <class Stack, bool COUNT, int TIER>
 __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
                                                     uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
@@ -268,9 +294,10 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
     uint32_t qi = 0, T = 0, tval = 0;
     bool tset = false;
     Frame cur{0, 0, 0, 0};
+    const uint32_t* ce = s.arena;   // arena of the current frame
     int sp = 0;
     for (;;) {
-        uint32_t enter = NONE32;     // row to enter this iteration
+        uint32_t enter = NONE32;     // row handle to enter this iteration
         uint16_t enter_k = 0, enter_fl = 0;
         int res = -1;                // >= 0: request decided (RES_*)
         if (!busy) {
@@ -291,29 +318,31 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
             sp = 0;
             enter = qq.row;
             enter_k = (uint16_t)d;
-            enter_fl = FR_TOP | (qq.row >= ov.base ? FR_OV : 0);
+            enter_fl = FR_TOP;
         } else if (cur.left == 0) {                               // row exhausted: pop
-            if (--sp == 0) res = RES_FALSE;
-            else cur = st[sp - 1];
+            if (--sp == 0) {
+                res = RES_FALSE;
+            } else {
+                cur = st[sp - 1];
+                ce = (cur.fl & FR_OV) ? ov.arena : s.arena;
+            }
         } else {
-            const uint32_t e = (cur.seq & FR_OV) ? ov.edges[cur.pos] : s.edges[cur.pos];
+            const uint32_t e = ce[cur.pos];
             ++cur.pos;
             --cur.left;
             w.edge();
             if (e & EDGE_SET) {
                 uint32_t vid = e & EDGE_VAL;
-                if (cur.seq & FR_SEQ) {
+                if (cur.fl & FR_SEQ) {
                     uint32_t c = coll_lookup(s, e);
                     if (c != NONE32) vid = c;
                 }
                 int t;
-                if (cur.seq & FR_TOP) {                           // fresh map per top-level tuple
+                if (cur.fl & FR_TOP) {                            // fresh map per top-level tuple
                     V.fresh();
                     w.item();
-                    t = V.test_add(vid, w);
-                } else {
-                    t = V.test_add(vid, w);
                 }
+                t = V.test_add(vid, w);
                 if (t == 2) res = RES_OVERFLOW;
                 else if (t == 0) {
                     if (tset && e == tval) res = RES_TRUE;        // engine.go:54-57
@@ -325,7 +354,7 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
                 }
             } else {                                              // subject id in an ordered row
                 int t = 0;
-                if (!(cur.seq & FR_TOP)) {
+                if (!(cur.fl & FR_TOP)) {
                     uint32_t c = coll_lookup(s, e);
                     if (c != NONE32) t = V.test_add(c, w);
                 }
@@ -334,22 +363,17 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
             }
         }
         if (enter != NONE32) {
-            RowView rv;
-            if (enter_fl & FR_OV) {
-                DevSnap o{ov.rows, ov.edges, ov.pp, nullptr, 0};
-                rv = load_row(o, enter - ov.base);
-            } else {
-                rv = load_row(s, enter);
-            }
+            const RowView rv = load_row(s, ov, enter);
             w.row();
-            const uint32_t* eb = (enter_fl & FR_OV) ? ov.edges : s.edges;
-            if (!rv.seq && !tset && rv.n_ids && find_id(eb, rv.beg + rv.n_sets, rv.n_ids, T, w)) {
+            if (!rv.seq && !tset && row_has_id(rv, T, w)) {
                 res = RES_TRUE;
             } else if (sp >= st.cap()) {
                 res = RES_OVERFLOW;
             } else {
                 if (sp > 0) st[sp - 1] = cur;
-                cur = Frame{rv.beg, rv.n_sets, enter_k, (uint16_t)(enter_fl | (rv.seq ? FR_SEQ : 0))};
+                cur = Frame{rv.beg, rv.n_sets, enter_k,
+                            (uint16_t)(enter_fl | (rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
+                ce = rv.a;
                 ++sp;
             }
         }
@@ -387,7 +411,8 @@ __device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint3
     ++cnt;
 }
 
-// BuildTree for one root (engine.go:33-102).  root: row id (root_flags bit0 = set) or string id.
+// BuildTree for one root (engine.go:33-102).  root: row handle (root_flags bit0 = subject set) or
+// a string id.  Set nodes are emitted with their row handle (the host maps handles to row ids).
 template <bool FILL, class Stack>
 __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
                           uint32_t root_vid, int d, Visited& V, keto_tree_node* out, uint64_t& cnt, Stack& st) {
@@ -398,32 +423,23 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     if (root == KETO_NO_ROW) return EXP_NIL;                // no tuples at all (:68-70)
     V.fresh();
     Work<false> nw;
-    V.test_add(root_vid, nw);
+    V.test_add(root_vid, nw);                               // :40-43 (root marked too)
     int sp = 0;
     // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union pushed
-    auto open = [&](uint32_t r, int k) -> int {
-        const bool in_ov = r >= ov.base;     // only the root can live in the overlay
-        RowView rv;
-        uint32_t pp;
-        if (in_ov) {
-            DevSnap o{ov.rows, ov.edges, ov.pp, nullptr, 0};
-            rv = load_row(o, r - ov.base);
-            pp = ov.pp[r - ov.base];
-        } else {
-            rv = load_row(s, r);
-            pp = s.row_pp[r];
-        }
+    auto open = [&](uint32_t h, int k) -> int {
+        const RowView rv = load_row(s, ov, h);
         const uint32_t n_all = rv.n_sets + rv.n_ids;
-        if (pp == NO_PAGE && n_all == 0) return EXP_NIL;
-        if (pp == 0) return EXP_ERROR;                      // first page fails toInternal
+        if (rv.pp == NO_PAGE && n_all == 0) return EXP_NIL;
+        if (rv.pp == 0) return EXP_ERROR;                   // the first page fails toInternal
         if (k <= 1) {                                       // :72-75
-            emit(out, cnt, FILL, EDGE_SET | r, 0x80000000u);
+            emit(out, cnt, FILL, EDGE_SET | h, 0x80000000u);
             return EXP_TREE;
         }
-        if (pp != NO_PAGE) return EXP_ERROR;                // a later page fails
+        if (rv.pp != NO_PAGE) return EXP_ERROR;             // a later page fails
         if (sp == st.cap()) return EXP_OVERFLOW;
-        emit(out, cnt, FILL, EDGE_SET | r, n_all);
-        st[sp] = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? 1 : 0) | (in_ov ? 2 : 0))};
+        emit(out, cnt, FILL, EDGE_SET | h, n_all);
+        st[sp] = Frame{rv.beg, n_all, (uint16_t)k,
+                       (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
         ++sp;
         return EXP_TREE;
     };
@@ -435,7 +451,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             --sp;
             continue;
         }
-        const uint32_t e = (f.seq & 2) ? ov.edges[f.pos] : s.edges[f.pos];
+        const uint32_t e = (f.fl & FR_OV) ? ov.arena[f.pos] : s.arena[f.pos];
         f.pos++;
         f.left--;
         if (!(e & EDGE_SET)) {
@@ -444,7 +460,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         }
         const uint32_t c = e & EDGE_VAL;
         uint32_t vid = c;
-        if (f.seq & 1) {
+        if (f.fl & FR_SEQ) {
             uint32_t cv = coll_lookup(s, e);
             if (cv != NONE32) vid = cv;
         }
@@ -517,9 +533,7 @@ struct Tier {
 
 struct DeviceState {
     int device = 0;
-    uint4* rows = nullptr;
-    uint32_t* edges = nullptr;
-    uint32_t* row_pp = nullptr;
+    uint32_t* arena = nullptr;
     uint64_t* coll = nullptr;
     uint32_t coll_mask = 0;
     uint64_t bytes = 0;
@@ -533,7 +547,7 @@ struct DeviceState {
     hipEvent_t ev[6] = {};
     keto_batch_timing last{};
 
-    DevSnap view() const { return DevSnap{rows, edges, row_pp, coll, coll_mask}; }
+    DevSnap view() const { return DevSnap{arena, coll, coll_mask}; }
 };
 
 namespace {
@@ -580,17 +594,14 @@ void ensure_tier(DeviceState& D, int level, uint32_t n_slots, uint32_t cap, int 
 void ensure_lists(DeviceState& D, uint64_t n) {
     if (D.list_cap >= n && D.lists) return;
     if (D.lists) (void)hipFree(D.lists);
-    if (!D.counters) {
-        uint64_t acc = 0;
-        D.counters = dmalloc<uint32_t>(4, acc);
-    }
     uint64_t acc = 0;
+    if (!D.counters) D.counters = dmalloc<uint32_t>(4, acc);
     D.list_cap = std::max<uint64_t>(n, 1024);
     D.lists = dmalloc<uint32_t>(2 * D.list_cap, acc);
 }
 
 int hw_slots() {
-    // persistent grid sized to residency: 256 CUs x 28 waves (7 per SIMD at the kernel's SGPR
+    // persistent grid sized to residency: 256 CUs x 28 waves (7 per SIMD at the kernel's register
     // budget) x 64 lanes; every lane owns one visited table.  KETO_SLOTS overrides (tuning).
     static int v = [] {
         const char* e = getenv("KETO_SLOTS");
@@ -616,8 +627,48 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     return a;
 }
 
-// stack depth needed for a global max-depth (check recursion holds <= d-1 frames, expand <= d)
-int needed_frames(int gmd) { return std::max(1, gmd); }
+template <class F>
+void host_parallel_for(uint64_t n, F f) {
+    unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 100000) th = 1;
+    std::vector<std::thread> ts;
+    const uint64_t chunk = (n + th - 1) / th;
+    for (unsigned t = 0; t < th; ++t)
+        ts.emplace_back([&, t] {
+            uint64_t b = t * chunk, e = std::min(n, b + chunk);
+            for (uint64_t i = b; i < e; ++i) f(i);
+        });
+    for (auto& x : ts) x.join();
+}
+
+// Write one row (table, header, edges) into an arena at its handle.
+void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uint32_t hlog2, const uint32_t* edges,
+             uint64_t n_stored, const std::vector<uint32_t>& unit_of_row) {
+    uint64_t h = (uint64_t)unit * HDR_WORDS;
+    const bool seq = ((rec.hi_flags >> 8) & ROW_SEQ) != 0;
+    arena[h + 0] = rec.n_sets;
+    arena[h + 1] = rec.n_ids;
+    arena[h + 2] = (seq ? HDR_SEQ : 0u) | (hlog2 << 8);
+    arena[h + 3] = pp;
+    uint32_t* e = arena + h + HDR_WORDS;
+    for (uint64_t i = 0; i < n_stored; ++i) {
+        uint32_t v = edges[i];
+        if ((v & EDGE_SET) && v != EDGE_POISON) v = EDGE_SET | unit_of_row[v & EDGE_VAL];
+        e[i] = v;
+    }
+    for (uint64_t i = n_stored; i < ((n_stored + 3) & ~3ull); ++i) e[i] = NONE32;
+    if (hlog2) {
+        const uint32_t mask = (1u << hlog2) - 1u;
+        uint32_t* tab = arena + h - (1ull << hlog2);
+        for (uint32_t i = 0; i <= mask; ++i) tab[i] = NONE32;
+        for (uint32_t k = 0; k < rec.n_ids; ++k) {
+            const uint32_t id = edges[rec.n_sets + k];
+            uint32_t i = mix32(id) & mask;
+            while (tab[i] != NONE32 && tab[i] != id) i = (i + 1) & mask;
+            tab[i] = id;
+        }
+    }
+}
 
 }  // namespace
 
@@ -629,29 +680,34 @@ void device_upload(Snapshot& S, int device) {
     auto D = std::make_unique<DeviceState>();
     D->device = device;
     uint64_t acc = 0;
-    D->rows = dmalloc<uint4>(S.rows.size(), acc);
-    D->edges = dmalloc<uint32_t>(S.edges.size(), acc);
-    D->row_pp = dmalloc<uint32_t>(S.row_pp.size(), acc);
-    if (!S.rows.empty())
-        HIP_OK(hipMemcpy(D->rows, S.rows.data(), S.rows.size() * sizeof(RowRec), hipMemcpyHostToDevice));
-    if (!S.edges.empty())
-        HIP_OK(hipMemcpy(D->edges, S.edges.data(), S.edges.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    if (!S.row_pp.empty())
-        HIP_OK(hipMemcpy(D->row_pp, S.row_pp.data(), S.row_pp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const uint64_t words = S.n_units * HDR_WORDS;
+    std::vector<uint32_t> arena(std::max<uint64_t>(words, 4));
+    const uint32_t R = S.n_rows();
+    host_parallel_for(R, [&](uint64_t r) {
+        const uint64_t b = S.row_begin((uint32_t)r);
+        const uint64_t e = r + 1 < R ? S.row_begin((uint32_t)r + 1) : S.edges.size();
+        put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), S.edges.data() + b,
+                e - b, S.unit_of_row);
+    });
+    D->arena = dmalloc<uint32_t>(arena.size(), acc);
+    HIP_OK(hipMemcpy(D->arena, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     if (!S.coll.empty()) {
         uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
         std::vector<uint64_t> tab(cap, ~0ull);
         for (auto& kv : S.coll) {
-            uint32_t i = mix32(kv.first) & (cap - 1);
+            uint32_t key = kv.first;
+            if (key & EDGE_SET) key = EDGE_SET | S.unit_of_row[key & EDGE_VAL];   // row -> handle
+            uint32_t vid = kv.second;
+            uint32_t i = mix32(key) & (cap - 1);
             while (tab[i] != ~0ull) i = (i + 1) & (cap - 1);
-            tab[i] = ((uint64_t)kv.first << 32) | kv.second;
+            tab[i] = ((uint64_t)key << 32) | vid;
         }
         D->coll = dmalloc<uint64_t>(cap, acc);
         HIP_OK(hipMemcpy(D->coll, tab.data(), cap * sizeof(uint64_t), hipMemcpyHostToDevice));
         D->coll_mask = cap - 1;
     }
     D->bytes = acc;
-    D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.rows.size() + S.n_coll_keys + 1);
+    D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_units + S.n_coll_keys + 1);
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     for (auto& e : D->ev) HIP_OK(hipEventCreate(&e));
     S.device = device;
@@ -663,9 +719,7 @@ void device_release(Snapshot& S) {
     DeviceState& D = *S.dev;
     (void)hipSetDevice(D.device);
     for (auto& t : D.tiers) free_tier(t);
-    if (D.rows) (void)hipFree(D.rows);
-    if (D.edges) (void)hipFree(D.edges);
-    if (D.row_pp) (void)hipFree(D.row_pp);
+    if (D.arena) (void)hipFree(D.arena);
     if (D.coll) (void)hipFree(D.coll);
     if (D.lists) (void)hipFree(D.lists);
     if (D.counters) (void)hipFree(D.counters);
@@ -695,17 +749,17 @@ struct Plan {
     int frames[3];
 };
 
-Plan make_plan(const DeviceState& D, uint32_t n, int gmd) {
+Plan make_plan(const DeviceState& D, uint32_t n, int frames_needed) {
     Plan p;
     uint32_t full = pow2_at_least(2ull * D.vid_bound + 2);
     p.slots[0] = (uint32_t)std::min<uint64_t>((uint64_t)hw_slots(), ((uint64_t)n + 255) / 256 * 256);
     if (p.slots[0] == 0) p.slots[0] = 256;
     p.cap[0] = std::min<uint32_t>(256, full);
-    p.slots[1] = 4096;
+    p.slots[1] = (uint32_t)std::min<uint64_t>(4096, ((uint64_t)n + 255) / 256 * 256);
     p.cap[1] = std::min<uint32_t>(1u << 15, full);
     p.slots[2] = 64;
     p.cap[2] = full;
-    int fr = needed_frames(gmd);
+    const int fr = std::max(1, frames_needed);
     p.frames[0] = fr <= 16 ? 0 : std::min(fr, 64);   // 0 = LocalStack; deeper paths overflow upward
     p.frames[1] = fr <= 16 ? 0 : std::min(fr, 256);
     p.frames[2] = std::min<int>(fr, (int)std::min<uint64_t>(D.vid_bound + 2ull, 1u << 20));
@@ -754,32 +808,29 @@ void run_tiers(DeviceState& D, uint32_t n, const Plan& p, hipStream_t st, Launch
     }
 }
 
-}  // namespace
-
-namespace {
-
-// batch-local overlay rows on the device (freed when the batch returns)
+// batch-local overlay arena on the device (freed when the batch returns)
 struct OverlayBuf {
-    DevOverlay v{nullptr, nullptr, nullptr, 0xFFFFFFFFu};
-    void* p[3] = {nullptr, nullptr, nullptr};
-    OverlayBuf(const Overlay* ov) {
+    DevOverlay v{nullptr, 0xFFFFFFFFu};
+    void* p = nullptr;
+    OverlayBuf(const Snapshot& S, const Overlay* ov) {
         if (!ov || ov->empty()) return;
+        std::vector<uint32_t> arena(std::max<uint64_t>(ov->n_units * HDR_WORDS, 4));
+        for (size_t i = 0; i < ov->rows.size(); ++i) {
+            const RowRec& rec = ov->rows[i];
+            const uint64_t b = (uint64_t)rec.edge_lo | ((uint64_t)(rec.hi_flags & 0xFFu) << 32);
+            const uint64_t e = i + 1 < ov->rows.size()
+                                   ? ((uint64_t)ov->rows[i + 1].edge_lo | ((uint64_t)(ov->rows[i + 1].hi_flags & 0xFFu) << 32))
+                                   : ov->edges.size();
+            put_row(arena.data(), ov->unit[i], rec, ov->pp[i], 0, ov->edges.data() + b, e - b, S.unit_of_row);
+        }
         uint64_t acc = 0;
-        uint4* r = dmalloc<uint4>(ov->rows.size(), acc);
-        p[0] = r;
-        uint32_t* e = dmalloc<uint32_t>(ov->edges.size(), acc);
-        p[1] = e;
-        uint32_t* pp = dmalloc<uint32_t>(ov->pp.size(), acc);
-        p[2] = pp;
-        HIP_OK(hipMemcpy(r, ov->rows.data(), ov->rows.size() * sizeof(RowRec), hipMemcpyHostToDevice));
-        if (!ov->edges.empty())
-            HIP_OK(hipMemcpy(e, ov->edges.data(), ov->edges.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        HIP_OK(hipMemcpy(pp, ov->pp.data(), ov->pp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        v = DevOverlay{r, e, pp, ov->base};
+        uint32_t* a = dmalloc<uint32_t>(arena.size(), acc);
+        p = a;
+        HIP_OK(hipMemcpy(a, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        v = DevOverlay{a, (uint32_t)S.n_units};
     }
     ~OverlayBuf() {
-        for (void* q : p)
-            if (q) (void)hipFree(q);
+        if (p) (void)hipFree(p);
     }
 };
 
@@ -802,7 +853,7 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     if (n == 0) return;
     if (gmd > 65535) gmd = 65535;
     hipStream_t st = stream ? (hipStream_t)stream : D.stream;
-    OverlayBuf ov(ovh);
+    OverlayBuf ov(S, ovh);
     const keto_check_ids* dq = reqs;
     uint8_t* da = allowed;
     DevFree tmp;
@@ -816,7 +867,8 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
         dq = tq;
         da = ta8;
     }
-    Plan p = make_plan(D, n, gmd);
+    // check recursion holds at most gmd - 1 frames
+    Plan p = make_plan(D, n, std::max(1, gmd - 1));
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
     unsigned long long* dwork = nullptr;
@@ -876,7 +928,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (n == 0) return;
     if (gmd > 65535) gmd = 65535;
     hipStream_t st = D.stream;
-    OverlayBuf ov(ovh);
+    OverlayBuf ov(S, ovh);
     std::vector<ExpandReq> hq(n);
     for (uint32_t i = 0; i < n; ++i) hq[i] = ExpandReq{root[i], root_flags[i], root_vid[i], depth[i]};
     DevFree tmp;
@@ -888,7 +940,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     uint8_t* dstatus = dmalloc<uint8_t>(n, acc);
     tmp.p.push_back(dstatus);
     HIP_OK(hipMemcpy(dq, hq.data(), n * sizeof(ExpandReq), hipMemcpyHostToDevice));
-    Plan p = make_plan(D, n, gmd + 1);
+    Plan p = make_plan(D, n, gmd);            // expand holds at most gmd frames
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
     ExpandOut o{nullptr, nullptr, dcount, dstatus};
@@ -900,13 +952,13 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                       dim3 grid(slots / 256), block(256);
                       const bool local = p.frames[level] == 0;
                       if (!fill && local)
-                          hipLaunchKernelGGL((expand_kernel<false, LocalStack<17>>), grid, block, 0, st, sv, dov, dq,
+                          hipLaunchKernelGGL((expand_kernel<false, LocalStack<16>>), grid, block, 0, st, sv, dov, dq,
                                              n, gmd, eo, a);
                       else if (!fill)
                           hipLaunchKernelGGL((expand_kernel<false, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
                                              gmd, eo, a);
                       else if (local)
-                          hipLaunchKernelGGL((expand_kernel<true, LocalStack<17>>), grid, block, 0, st, sv, dov, dq,
+                          hipLaunchKernelGGL((expand_kernel<true, LocalStack<16>>), grid, block, 0, st, sv, dov, dq,
                                              n, gmd, eo, a);
                       else
                           hipLaunchKernelGGL((expand_kernel<true, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
@@ -914,8 +966,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                       HIP_OK(hipGetLastError());
                   });
     };
-    // count pass, then exclusive scan on the host, then the fill pass (same tier plan: a root
-    // overflows on exactly the same tiers both times, and a partial pre-order is a prefix)
+    // count pass, exclusive scan on the host, fill pass (same tier plan: a root overflows on the
+    // same tiers both times, and a partial pre-order is a prefix of the full one)
     launch_pass(false, o);
     std::vector<uint64_t> cnt(n);
     HIP_OK(hipMemcpy(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -931,6 +983,19 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     HIP_OK(hipMemcpy(doff, out.offset.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
     launch_pass(true, ExpandOut{dnodes, doff, dcount, dstatus});
     HIP_OK(hipMemcpy(out.nodes.data(), dnodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost));
+    // handles -> row ids (overlay handles -> ovh->base + overlay index)
+    host_parallel_for(total, [&](uint64_t i) {
+        keto_tree_node& x = out.nodes[i];
+        if (!(x.subject & EDGE_SET)) return;
+        const uint32_t h = x.subject & EDGE_VAL;
+        if (h >= S.n_units && ovh) {
+            const uint32_t u = (uint32_t)(h - S.n_units);
+            auto it = std::lower_bound(ovh->unit.begin(), ovh->unit.end(), u);
+            x.subject = EDGE_SET | (ovh->base + (uint32_t)(it - ovh->unit.begin()));
+        } else {
+            x.subject = EDGE_SET | (uint32_t)S.row_of_handle(h);
+        }
+    });
 }
 
 }  // namespace keto

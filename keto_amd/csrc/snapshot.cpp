@@ -226,13 +226,59 @@ uint32_t overlay_row(const Snapshot& S, Overlay& ov, const RowKey& k) {
     ov.pp.push_back(pp);
     ov.keys.push_back(k);
     ov.map.emplace(k, id);
+    ov.unit.push_back((uint32_t)ov.n_units);                  // overlay rows: header + edges, no table
+    ov.n_units += 1 + (n + 3) / 4;
+    if (S.n_units + ov.n_units >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "overlay exceeds the handle space"};
     return id;
 }
 
+namespace {
+uint64_t row_end_of(const Snapshot& S, uint32_t r) {
+    return r + 1 < S.rows.size() ? S.row_begin(r + 1) : S.edges.size();
+}
+uint32_t ceil_log2(uint64_t x) {
+    uint32_t k = 0;
+    while ((1ull << k) < x) ++k;
+    return k;
+}
+}  // namespace
+
+uint32_t Snapshot::row_hlog2(uint32_t r) const {
+    if (row_flags(r) & ROW_SEQ) return 0;
+    return rows[r].n_ids > HASH_MIN ? ceil_log2(2ull * rows[r].n_ids) : 0;
+}
+
+void compute_layout(Snapshot& S) {
+    const uint32_t R = S.n_rows();
+    S.unit_of_row.resize(R);
+    uint64_t w = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t h = S.row_hlog2(r);
+        const uint64_t table = h ? (1ull << h) : 0;
+        const uint64_t n = row_end_of(S, r) - S.row_begin(r);
+        const uint64_t unit = (w + table) / HDR_WORDS;
+        if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
+        S.unit_of_row[r] = (uint32_t)unit;
+        w += table + HDR_WORDS + ((n + 3) & ~3ull);
+    }
+    S.n_units = w / HDR_WORDS;
+}
+
+int64_t Snapshot::row_of_handle(uint32_t unit) const {
+    auto it = std::lower_bound(unit_of_row.begin(), unit_of_row.end(), unit);
+    if (it == unit_of_row.end() || *it != unit) return -1;
+    return it - unit_of_row.begin();
+}
+
+uint32_t handle_of(const Snapshot& S, const Overlay* ov, uint32_t row) {
+    if (ov && row >= ov->base) return (uint32_t)(S.n_units + ov->unit[row - ov->base]);
+    return S.unit_of_row[row];
+}
+
 uint32_t Snapshot::vid_of_row(uint32_t row) const {
-    if (coll.empty()) return row;
+    if (coll.empty()) return unit_of_row[row];
     auto it = coll.find(EDGE_SET | row);
-    return it == coll.end() ? row : it->second;
+    return it == coll.end() ? unit_of_row[row] : it->second;
 }
 
 std::string Snapshot::row_field_ns(uint32_t row) const {
@@ -430,6 +476,7 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
     }
 
     finalize_rows(S, row_ptr, is_wild);
+    compute_layout(S);
     return Sp;
 }
 
@@ -465,6 +512,7 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
     std::vector<uint64_t> rp(row_ptr, row_ptr + n_rows + 1);
     std::vector<uint8_t> is_wild(n_rows, 0);
     finalize_rows(S, rp, is_wild);
+    compute_layout(S);
     return Sp;
 }
 

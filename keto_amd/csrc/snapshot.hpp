@@ -37,6 +37,16 @@ constexpr int64_t ANY_NS = INT64_MIN;
 constexpr uint32_t ROW_SEQ = 1u;                // flag bit (in RowRec.y bits 8..15)
 constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys live above all row ids
 
+// Device arena (one u32 array per device).  Row r occupies
+//   [open-addressing subject-id table, 2^hlog2 words, only for rows with > HASH_MIN ids]
+//   [16-B header: n_sets, n_ids, flags | hlog2 << 8, first poisoned page]   <- handle = word / 4
+//   [edges in ORDER BY order; subject sets hold the target's handle]        padded to 16 B
+// so one row visit reads one header line that usually also holds the subject sets and a short
+// id region, and a long id region is probed in the table right in front of the header.
+constexpr uint32_t HASH_MIN = 16;               // id regions longer than this get a table
+constexpr uint32_t HDR_WORDS = 4;
+constexpr uint32_t HDR_SEQ = 1u;                // flags bit (header word 2, bits 0..7)
+
 struct RowRec {          // 16 B
     uint32_t edge_lo;    // edge begin, low 32 bits
     uint32_t hi_flags;   // bits 0..7 edge begin bits 32..39; bits 8..15 flags
@@ -95,6 +105,13 @@ struct Snapshot {
     uint32_t n_poisoned_rows = 0;
     uint32_t n_seq_rows = 0;
 
+    // ---- device arena layout (compute_layout): handle of each row, total arena units (16 B)
+    std::vector<uint32_t> unit_of_row;
+    uint64_t n_units = 0;
+    uint32_t handle(uint32_t row) const { return unit_of_row[row]; }
+    int64_t row_of_handle(uint32_t unit) const;   // -1 if not a row header
+    uint32_t row_hlog2(uint32_t r) const;         // 0 = no id table
+
     // ---- device
     int device = -1;
     std::unique_ptr<DeviceState, DeviceStateDeleter> dev;
@@ -143,16 +160,22 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
 // Batch-local rows for wildcard requests that no stored subject set materialized: they can only
 // be top-level (check) or root (expand) rows, never edge targets.  Row ids >= base.
 struct Overlay {
-    uint32_t base = 0;
+    uint32_t base = 0;                 // row ids >= base are overlay rows (host side)
     std::vector<RowRec> rows;
     std::vector<uint32_t> pp;
-    std::vector<uint32_t> edges;
+    std::vector<uint32_t> edges;       // row-id encoded like Snapshot::edges
     std::vector<RowKey> keys;
     std::unordered_map<RowKey, uint32_t, RowKeyHash> map;
+    std::vector<uint32_t> unit;        // overlay-local arena unit of each overlay row
+    uint64_t n_units = 0;
     bool empty() const { return rows.empty(); }
 };
 // materialize the wildcard query k (ns ANY / obj ANY / rel ANY) into the overlay; returns row id
 uint32_t overlay_row(const Snapshot& s, Overlay& ov, const RowKey& k);
+// device handle of a row id that may be an overlay row (handles >= s.n_units are overlay rows)
+uint32_t handle_of(const Snapshot& s, const Overlay* ov, uint32_t row);
+// arena layout of every row (called by the builders)
+void compute_layout(Snapshot& s);
 
 // device engine (engine.hip)
 void device_upload(Snapshot& s, int device);
@@ -166,6 +189,7 @@ struct ExpandResult {
     std::vector<uint64_t> offset;          // n+1
     std::vector<keto_tree_node> nodes;
 };
+// roots: row handles (root_flags bit0 = subject set) or string ids; out.nodes carry row ids
 void device_expand(Snapshot& s, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
                    const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
                    const Overlay* ov, ExpandResult& out);

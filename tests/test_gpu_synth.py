@@ -28,7 +28,7 @@ def test_powerlaw_checks_match_oracle(powerlaw, gmd):
     q = g.queries(40000, seed=11 + gmd, depth=gmd)
     rng = np.random.default_rng(gmd)
     q["max_depth"] = rng.integers(-1, gmd + 2, size=len(q))      # exercise the depth clamp
-    gpu = _gpu_check(snap, q, gmd)
+    gpu = _gpu_check(snap, snap.with_handles(q), gmd)
     tab = g.oracle_table(q, gmd)
     ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
     assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
