@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, co
             w.row();
             if (!rv.seq && !tset && row_has_id(rv, T, w)) {
                 res = RES_TRUE;
-            } else if (sp >= st.cap()) {
+            } else if (sp > st.cap()) {        // saved frames live in st[0 .. sp-1)
                 res = RES_OVERFLOW;
             } else {
                 if (sp > 0) st[sp - 1] = cur;
@@ -757,8 +757,15 @@ Plan make_plan(const DeviceState& D, uint32_t n, int frames_needed) {
     p.cap[0] = std::min<uint32_t>(256, full);
     p.slots[1] = (uint32_t)std::min<uint64_t>(4096, ((uint64_t)n + 255) / 256 * 256);
     p.cap[1] = std::min<uint32_t>(1u << 15, full);
-    p.slots[2] = 64;
+    // tier 2: tables that hold every visit id of the snapshot, as many lanes as 8 GiB allows (>= 1)
     p.cap[2] = full;
+    {
+        const uint64_t per = (uint64_t)full * sizeof(uint64_t);
+        uint64_t sl = std::max<uint64_t>(1, (8ull << 30) / per);
+        uint32_t s2 = 1;
+        while (s2 * 2 <= std::min<uint64_t>(sl, 256)) s2 *= 2;
+        p.slots[2] = s2;
+    }
     const int fr = std::max(1, frames_needed);
     p.frames[0] = fr <= 16 ? 0 : std::min(fr, 64);   // 0 = LocalStack; deeper paths overflow upward
     p.frames[1] = fr <= 16 ? 0 : std::min(fr, 256);
@@ -882,7 +889,8 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
-                  dim3 grid(slots / 256), block(256);
+                  const uint32_t bs = std::min<uint32_t>(256, slots);
+                  dim3 grid(slots / bs), block(bs);
                   const bool local = p.frames[level] == 0;
                   // TIER is only a name tag: tier-0 launches are their own symbol in rocprof traces
                   if (local && !dwork && level == 0)
@@ -949,7 +957,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                   [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                       uint32_t slots) {
                       TierArgs a = tier_args(t, il, ic, ol, oc);
-                      dim3 grid(slots / 256), block(256);
+                      const uint32_t bs = std::min<uint32_t>(256, slots);
+                  dim3 grid(slots / bs), block(bs);
                       const bool local = p.frames[level] == 0;
                       if (!fill && local)
                           hipLaunchKernelGGL((expand_kernel<false, LocalStack<16>>), grid, block, 0, st, sv, dov, dq,

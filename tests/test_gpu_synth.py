@@ -18,6 +18,54 @@ def powerlaw():
     g.close()
 
 
+@pytest.fixture(scope="module")
+def nested():
+    from tools import synth
+    g = synth.SynthGraph(dict(n_docs=0, n_folders=0, n_groups=1 << 15, n_users=1 << 15, target_edges=0, seed=3),
+                         threads=16, kind="nested", chain=32)
+    snap = g.snapshot(device=0)
+    yield g, snap
+    g.close()
+
+
+@pytest.mark.parametrize("gmd", [32, 16, 40, 7])
+def test_nested_deep_checks_match_oracle(nested, gmd):
+    """Config #3 shape: chains of 32 nested groups with cycles; global max-depth up to 40 takes the
+    deep (global-stack) kernel tiers."""
+    g, snap = nested
+    q = g.queries_nested(12000, seed=100 + gmd, depths=(5, 16, 32, 0, -1, 40))
+    gpu = snap.check_batch_ids(snap.with_handles(q), gmd)
+    tab = g.oracle_table(q, max(gmd, 1))
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+
+
+def test_nested_expand_matches_oracle(nested):
+    g, snap = nested
+    rng = np.random.default_rng(9)
+    rows = rng.integers(0, g.n_rows, size=120).astype(np.uint32)
+    depths = rng.choice([2, 5, 12, 20], size=120).astype(np.int32)
+    status, offs, nodes = snap.expand_batch_ids(rows | np.uint32(0x80000000), depths, 20)
+    q = np.zeros(len(rows), dtype=[("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
+    q["row"] = rows
+    tab = g.oracle_table(q, 20)
+    for i, (row, d) in enumerate(zip(rows, depths)):
+        r, want = _oracle_expand_nodes(g, tab, int(row), int(d), 20)
+        if r == 0:
+            assert status[i] == 1
+            continue
+        assert r == 1 and status[i] == 0
+        have = []
+        for subj, info in nodes[offs[i]:offs[i + 1]]:
+            leaf, nc = int(info >> 31), int(info & 0x7FFFFFFF)
+            if subj >> 31:
+                t = int(subj & 0x7FFFFFFF)
+                have.append((leaf, 1, 0, 0xFFFF0000 + int(g.row_ns[t]), int(g.row_obj[t]), int(g.row_rel[t]), nc))
+            else:
+                have.append((leaf, 0, int(subj), 0, 0, 0, nc))
+        assert have == want, f"root row {row} depth {d}"
+
+
 def _gpu_check(snap, q, gmd):
     return snap.check_batch_ids(q, gmd)
 

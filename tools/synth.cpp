@@ -178,6 +178,88 @@ int synth_generate(const synth_params* p, int threads, synth_graph* out) {
     return 0;
 }
 
+// "nested groups" graph (BASELINE config #3): groups:g#member only.  Groups form chains of
+// `chain` groups (g -> g+1 inside a chain, so membership nests up to `chain` levels), with a
+// 0.3-probability cross edge to a random later group and a 0.01-probability back-edge to an earlier
+// group (cycles).  Users per group ~ Pareto(1.5); users drawn with a power law.
+int synth_generate_nested(const synth_params* p, uint32_t chain, int threads, synth_graph* out) {
+    const uint64_t R = p->n_groups;
+    if (R >= 0x7FFFFFFFull || chain == 0) return -1;
+    std::vector<uint32_t> nset(R), nid(R);
+    parallel_for(R, threads, [&](uint64_t r) {
+        Rng g(p->seed * 0x2545F4914F6CDD1Dull ^ (r * 0x9E3779B97F4A7C15ull));
+        uint32_t k = (r % chain != chain - 1 && r + 1 < R) ? 1 : 0;
+        if (g.u01() < 0.3) ++k;
+        if (g.u01() < 0.01) ++k;
+        nset[r] = k;
+        nid[r] = (uint32_t)pareto(g, 2.0, 1.5, 1u << 16);
+    });
+    out->n_rows = (uint32_t)R;
+    out->row_ns = (int32_t*)malloc(R * sizeof(int32_t));
+    out->row_obj = (uint32_t*)malloc(R * sizeof(uint32_t));
+    out->row_rel = (uint32_t*)malloc(R * sizeof(uint32_t));
+    out->row_ptr = (uint64_t*)malloc((R + 1) * sizeof(uint64_t));
+    uint64_t acc = 0, sets = 0;
+    for (uint64_t r = 0; r < R; ++r) {
+        out->row_ptr[r] = acc;
+        acc += nset[r] + nid[r];
+        sets += nset[r];
+    }
+    out->row_ptr[R] = acc;
+    out->n_edges = acc;
+    out->n_set_edges = sets;
+    out->edges = (uint32_t*)malloc(std::max<uint64_t>(acc, 1) * sizeof(uint32_t));
+    if (!out->row_ns || !out->row_obj || !out->row_rel || !out->row_ptr || !out->edges) return -2;
+    parallel_for(R, threads, [&](uint64_t r) {
+        out->row_ns[r] = 3;
+        out->row_obj[r] = (uint32_t)r;
+        out->row_rel[r] = REL_MEMBER;
+        Rng g(p->seed * 0x2545F4914F6CDD1Dull ^ (r * 0x9E3779B97F4A7C15ull));
+        const bool in_chain = r % chain != chain - 1 && r + 1 < R;
+        const bool cross = g.u01() < 0.3;
+        const bool back = g.u01() < 0.01;
+        uint32_t* e = out->edges + out->row_ptr[r];
+        uint32_t k = 0;
+        Rng h(p->seed ^ (r * 0xD1B54A32D192ED03ull));
+        if (in_chain) e[k++] = 0x80000000u | (uint32_t)(r + 1);
+        if (cross) e[k++] = 0x80000000u | (uint32_t)(r + 1 + h.next() % std::max<uint64_t>(1, R - r - 1)) % (uint32_t)R;
+        if (back) e[k++] = 0x80000000u | (uint32_t)(r ? h.next() % r : 0);
+        std::sort(e, e + nset[r]);
+        for (uint32_t j = 0; j < nid[r]; ++j) e[nset[r] + j] = (uint32_t)skewed(h, p->n_users, 1.5);
+        std::sort(e + nset[r], e + nset[r] + nid[r]);
+    });
+    return 0;
+}
+
+// Requests groups:g#member@u for the nested graph: half a user of a group reached by walking
+// 0..depth-1 nesting edges, half random users; request depth cycles through `depths`.
+int synth_queries_nested(const synth_graph* g, const synth_params* p, uint64_t n, uint64_t seed,
+                         const int32_t* depths, uint32_t n_depths, keto_check_ids* out, int threads) {
+    parallel_for(n, threads, [&](uint64_t i) {
+        Rng r(seed * 0xA24BAED4963EE407ull ^ (i * 0x9FB21C651E98DF25ull));
+        uint32_t row = (uint32_t)(r.next() % g->n_rows);
+        int32_t d = depths[i % n_depths];
+        keto_check_ids q{row, 0, 0, d};
+        if (r.next() & 1) {
+            uint32_t cur = row;
+            int hops = (int)(r.next() % (uint64_t)std::max(1, d));
+            for (int h = 0; h < hops; ++h) {
+                uint64_t b = g->row_ptr[cur], e = g->row_ptr[cur + 1], ns = 0;
+                while (b + ns < e && (g->edges[b + ns] & 0x80000000u)) ++ns;
+                if (!ns) break;
+                cur = g->edges[b + r.next() % ns] & 0x7FFFFFFFu;
+            }
+            uint64_t b = g->row_ptr[cur], e = g->row_ptr[cur + 1], ns = 0;
+            while (b + ns < e && (g->edges[b + ns] & 0x80000000u)) ++ns;
+            q.target = e - b > ns ? g->edges[b + ns + r.next() % (e - b - ns)] : (uint32_t)(r.next() % p->n_users);
+        } else {
+            q.target = (uint32_t)(r.next() % p->n_users);
+        }
+        out[i] = q;
+    });
+    return 0;
+}
+
 void synth_free(synth_graph* g) {
     free(g->row_ns);
     free(g->row_obj);

@@ -61,12 +61,20 @@ def lib():
     return _lib
 
 
+# BASELINE.json config #3: nested group membership, chains up to 32, cycles (seed 3)
+NESTED_100M = dict(n_docs=0, n_folders=0, n_groups=1 << 24, n_users=1 << 24, target_edges=0, seed=3)
+
+
 class SynthGraph:
-    def __init__(self, params: dict, threads: int = 16):
+    def __init__(self, params: dict, threads: int = 16, kind: str = "powerlaw", chain: int = 32):
         self.params = params
+        self.kind = kind
         self.p = Params(**{k: params[k] for k, _ in Params._fields_})
         self.g = Graph()
-        rc = lib().synth_generate(C.byref(self.p), C.c_int(threads), C.byref(self.g))
+        if kind == "nested":
+            rc = lib().synth_generate_nested(C.byref(self.p), C.c_uint32(chain), C.c_int(threads), C.byref(self.g))
+        else:
+            rc = lib().synth_generate(C.byref(self.p), C.c_int(threads), C.byref(self.g))
         if rc != 0:
             raise RuntimeError(f"synth_generate failed: {rc}")
         R, E = self.g.n_rows, self.g.n_edges
@@ -97,6 +105,15 @@ class SynthGraph:
         out = np.zeros(n, dtype=CHECK_IDS_DTYPE)
         lib().synth_queries(C.byref(self.g), C.byref(self.p), C.c_uint64(n), C.c_uint64(seed), C.c_int32(depth),
                             out.ctypes.data_as(C.c_void_p), C.c_int(threads))
+        return out
+
+    def queries_nested(self, n: int, seed: int, depths=(5, 16, 32), threads: int = 16) -> np.ndarray:
+        from keto_amd.capi import CHECK_IDS_DTYPE
+        out = np.zeros(n, dtype=CHECK_IDS_DTYPE)
+        d = np.ascontiguousarray(depths, dtype=np.int32)
+        lib().synth_queries_nested(C.byref(self.g), C.byref(self.p), C.c_uint64(n), C.c_uint64(seed),
+                                   d.ctypes.data_as(C.c_void_p), C.c_uint32(len(d)), out.ctypes.data_as(C.c_void_p),
+                                   C.c_int(threads))
         return out
 
     def snapshot(self, device=0):
