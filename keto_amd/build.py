@@ -46,3 +46,23 @@ def build(verbose=False, force=False):
 
 if __name__ == "__main__":
     build(verbose=True, force="--force" in sys.argv)
+
+
+def build_variant(name, defines):
+    """Tuning build with -D defines into keto_amd/variants/lib_<name>.so (select with KETO_LIB)."""
+    vdir = os.path.join(HERE, "variants")
+    os.makedirs(vdir, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(vdir, f"{name}_{src}.o")
+        flags = [f"-D{d}" for d in defines]
+        if src.endswith(".cpp"):
+            cmd = [HIPCC, *CXXFLAGS, *flags, "-x", "c++", "-c", path, "-o", obj]
+        else:
+            cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, *flags, "-c", path, "-o", obj]
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    out = os.path.join(vdir, f"lib_{name}.so")
+    subprocess.check_call([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs])
+    return out

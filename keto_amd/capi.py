@@ -13,7 +13,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libketo_mi355x.so")
+LIB_PATH = os.environ.get("KETO_LIB") or os.path.join(HERE, "libketo_mi355x.so")   # KETO_LIB: tuning builds
 
 KETO_OK = 0
 CHECK_OK, CHECK_UNKNOWN_NAMESPACE = 0, 1

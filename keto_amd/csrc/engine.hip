@@ -40,6 +40,10 @@ namespace keto {
             throw Error{KETO_E_HIP, std::string(#x) + ": " + hipGetErrorString(err__)};             \
     } while (0)
 
+#ifndef KETO_CHECK_WAVES
+#define KETO_CHECK_WAVES 8      // check_kernel: ask for 8 waves per SIMD (register budget 64 VGPRs)
+#endif
+
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_OVERFLOW = 2;
 constexpr int EXP_TREE = 0, EXP_NIL = 1, EXP_ERROR = 2, EXP_OVERFLOW = 3;
@@ -197,18 +201,30 @@ struct Visited {
 
 // The first REG_VIDS visit ids of a map live in registers; a map that grows past them spills into
 // the lane's HBM table.  Typical check items mark a handful of subject sets.
-constexpr int REG_VIDS = 12;
+#ifndef KETO_REG_VIDS
+#define KETO_REG_VIDS 8
+#endif
+constexpr int REG_VIDS = KETO_REG_VIDS;
+// ...then the next LDS_VIDS in a per-lane LDS column ([slot][lane], conflict-free), then HBM.
+#ifndef KETO_LDS_VIDS
+#define KETO_LDS_VIDS 16
+#endif
+constexpr int LDS_VIDS = KETO_LDS_VIDS;
+constexpr int LDS_STRIDE = 256;          // lanes per block
 struct VisitedRS {
     uint32_t r[REG_VIDS];
-    uint32_t n;          // entries in r; REG_VIDS + 1 = spilled to V
+    uint32_t n;          // entries held: r, then lds; REG_VIDS + LDS_VIDS + 1 = spilled to V
+    uint32_t* lds;       // this lane's LDS column (stride LDS_STRIDE), or nullptr
     Visited V;
     __device__ inline void fresh() { n = 0; }
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
-        if (n <= (uint32_t)REG_VIDS) {
+        const uint32_t lcap = lds ? (uint32_t)LDS_VIDS : 0u;
+        if (n <= (uint32_t)REG_VIDS + lcap) {
             bool hit = false;
 #pragma unroll
             for (int i = 0; i < REG_VIDS; ++i) hit |= ((uint32_t)i < n) & (r[i] == vid);
+            for (uint32_t i = REG_VIDS; i < n && !hit; ++i) hit = lds[(i - REG_VIDS) * LDS_STRIDE] == vid;
             if (hit) return 1;
             if (n < (uint32_t)REG_VIDS) {
 #pragma unroll
@@ -217,10 +233,16 @@ struct VisitedRS {
                 ++n;
                 return 0;
             }
-            V.fresh();                                  // spill
+            if (n < (uint32_t)REG_VIDS + lcap) {
+                lds[(n - REG_VIDS) * LDS_STRIDE] = vid;
+                ++n;
+                return 0;
+            }
+            V.fresh();                                  // spill everything into the HBM table
 #pragma unroll
             for (int i = 0; i < REG_VIDS; ++i) V.test_add(r[i], w);
-            n = REG_VIDS + 1;
+            for (uint32_t i = 0; i < lcap; ++i) V.test_add(lds[i * LDS_STRIDE], w);
+            n = REG_VIDS + lcap + 1;
         }
         return V.test_add(vid, w);
     }
@@ -271,13 +293,15 @@ struct TierArgs {
 // following iteration, so a wave never waits for its slowest request.  Only a subject set reached
 // with remaining depth >= 2 is entered (engine.go:65-69,88-91).
 template <class Stack, bool COUNT, int TIER>
-__global__ void __launch_bounds__(256) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
+__global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
                                                     uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
                                                     unsigned long long* __restrict__ work) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
+    __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
     VisitedRS V;
     V.n = 0;
+    V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
@@ -539,7 +563,9 @@ struct DeviceState {
     uint64_t bytes = 0;
     uint32_t vid_bound = 0;       // distinct visit ids that can exist (rows + collision classes)
     std::mutex mu;                // one batch at a time per snapshot (workspaces are shared)
-    Tier tiers[3];
+    Tier tiers[3];                // check workspaces
+    Tier etiers[3];               // expand workspaces
+    uint32_t v1_lanes = 0;        // resident lanes of check_kernel (tier 0)
     uint32_t* lists = nullptr;    // 2 overflow lists, capacity list_cap each
     uint32_t* counters = nullptr; // 2 counters
     uint64_t list_cap = 0;
@@ -575,8 +601,8 @@ void free_tier(Tier& t) {
     t = Tier{};
 }
 
-void ensure_tier(DeviceState& D, int level, uint32_t n_slots, uint32_t cap, int gstack_n) {
-    Tier& t = D.tiers[level];
+void ensure_tier(Tier* set, int level, uint32_t n_slots, uint32_t cap, int gstack_n) {
+    Tier& t = set[level];
     if (t.n_slots == n_slots && t.cap == cap && t.gstack_n == gstack_n) return;
     free_tier(t);
     uint64_t acc = 0;
@@ -681,6 +707,7 @@ void device_upload(Snapshot& S, int device) {
     D->device = device;
     uint64_t acc = 0;
     const uint64_t words = S.n_units * HDR_WORDS;
+    if (words >= (1ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^32 words (16 GiB)"};
     std::vector<uint32_t> arena(std::max<uint64_t>(words, 4));
     const uint32_t R = S.n_rows();
     host_parallel_for(R, [&](uint64_t r) {
@@ -719,6 +746,7 @@ void device_release(Snapshot& S) {
     DeviceState& D = *S.dev;
     (void)hipSetDevice(D.device);
     for (auto& t : D.tiers) free_tier(t);
+    for (auto& t : D.etiers) free_tier(t);
     if (D.arena) (void)hipFree(D.arena);
     if (D.coll) (void)hipFree(D.coll);
     if (D.lists) (void)hipFree(D.lists);
@@ -775,21 +803,21 @@ Plan make_plan(const DeviceState& D, uint32_t n, int frames_needed) {
 }
 
 template <class Launch>
-void run_tiers(DeviceState& D, uint32_t n, const Plan& p, hipStream_t st, Launch launch) {
+void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t st, Launch launch) {
     ensure_lists(D, n);
     uint32_t* list0 = D.lists;
     uint32_t* list1 = D.lists + D.list_cap;
     uint32_t* c0 = D.counters;
     uint32_t* c1 = D.counters + 1;
-    ensure_tier(D, 0, p.slots[0], p.cap[0], p.frames[0]);
-    ensure_tier(D, 1, p.slots[1], p.cap[1], p.frames[1]);
+    ensure_tier(set, 0, p.slots[0], p.cap[0], p.frames[0]);
+    ensure_tier(set, 1, p.slots[1], p.cap[1], p.frames[1]);
     HIP_OK(hipMemsetAsync(D.counters, 0, 4 * sizeof(uint32_t), st));
     // tier 0 over all requests
     HIP_OK(hipEventRecord(D.ev[0], st));
-    launch(0, D.tiers[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
+    launch(0, set[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
     HIP_OK(hipEventRecord(D.ev[1], st));
     // tier 1 over tier-0 overflows (count read on the device)
-    launch(1, D.tiers[1], list0, c0, list1, c1, p.slots[1]);
+    launch(1, set[1], list0, c0, list1, c1, p.slots[1]);
     HIP_OK(hipEventRecord(D.ev[2], st));
     uint32_t cnt[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(cnt, c0, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -802,10 +830,10 @@ void run_tiers(DeviceState& D, uint32_t n, const Plan& p, hipStream_t st, Launch
     HIP_OK(hipEventElapsedTime(&T.tier_ms[0], D.ev[0], D.ev[1]));
     HIP_OK(hipEventElapsedTime(&T.tier_ms[1], D.ev[1], D.ev[2]));
     if (cnt[1]) {
-        ensure_tier(D, 2, p.slots[2], p.cap[2], p.frames[2]);
+        ensure_tier(set, 2, p.slots[2], p.cap[2], p.frames[2]);
         HIP_OK(hipMemsetAsync(c0, 0, sizeof(uint32_t), st));
         HIP_OK(hipEventRecord(D.ev[3], st));
-        launch(2, D.tiers[2], list1, c1, list0, c0, p.slots[2]);
+        launch(2, set[2], list1, c1, list0, c0, p.slots[2]);
         HIP_OK(hipEventRecord(D.ev[4], st));
         uint32_t still = 0;
         HIP_OK(hipMemcpyAsync(&still, c0, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -876,6 +904,16 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     }
     // check recursion holds at most gmd - 1 frames
     Plan p = make_plan(D, n, std::max(1, gmd - 1));
+    p.frames[0] = std::max(1, std::min(gmd - 1, 64));   // tier 0: frames in HBM (GlobalStack)
+    if (!D.v1_lanes) {
+        // persistent grid = what is resident at the kernel's register budget (KETO_SLOTS overrides)
+        int per_cu = 0, cus = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_kernel<GlobalStack, false, 0>, 256, 0));
+        HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
+        D.v1_lanes = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
+        if (getenv("KETO_SLOTS")) D.v1_lanes = (uint32_t)hw_slots();
+    }
+    p.slots[0] = (uint32_t)std::min<uint64_t>(D.v1_lanes, ((uint64_t)n + 255) / 256 * 256);
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
     unsigned long long* dwork = nullptr;
@@ -885,16 +923,18 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
         tmp.p.push_back(dwork);
         HIP_OK(hipMemsetAsync(dwork, 0, 8 * sizeof(unsigned long long), st));
     }
-    run_tiers(D, n, p, st,
+    run_tiers(D, D.tiers, n, p, st,
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
                   const uint32_t bs = std::min<uint32_t>(256, slots);
                   dim3 grid(slots / bs), block(bs);
                   const bool local = p.frames[level] == 0;
-                  // TIER is only a name tag: tier-0 launches are their own symbol in rocprof traces
-                  if (local && !dwork && level == 0)
-                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, false, 0>), grid, block, 0, st, sv, dov, dq, n,
+                  if (level == 0 && !dwork)
+                      hipLaunchKernelGGL((check_kernel<GlobalStack, false, 0>), grid, block, 0, st, sv, dov, dq, n,
+                                         gmd, da, a, dwork);
+                  else if (level == 0)
+                      hipLaunchKernelGGL((check_kernel<GlobalStack, true, 1>), grid, block, 0, st, sv, dov, dq, n,
                                          gmd, da, a, dwork);
                   else if (local && !dwork)
                       hipLaunchKernelGGL((check_kernel<LocalStack<16>, false, 1>), grid, block, 0, st, sv, dov, dq, n,
@@ -953,7 +993,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     DevOverlay dov = ov.v;
     ExpandOut o{nullptr, nullptr, dcount, dstatus};
     auto launch_pass = [&](bool fill, const ExpandOut& eo) {
-        run_tiers(D, n, p, st,
+        run_tiers(D, D.etiers, n, p, st,
                   [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                       uint32_t slots) {
                       TierArgs a = tier_args(t, il, ic, ol, oc);
