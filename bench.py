@@ -29,6 +29,24 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 
 
+def pmc_traffic(kernel_name, workload):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/*_traffic.json, written by tools/traffic.py from tools/gpu_round.sh), used only when
+    they were measured on this engine.hip and this workload; else None."""
+    import glob
+    import hashlib
+    with open(os.path.join(ROOT, "keto_amd", "csrc", "engine.hip"), "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            j = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if j.get("engine_sha256") == sha and j.get("kernel") in kernel_name and j.get("workload") == workload:
+            return j["traffic_bytes"], os.path.relpath(p, ROOT)
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,10 +135,15 @@ def main():
         # Visited-map state is scratch (registers first, HBM spill) and is not counted.
         alg = 16 * rows + 4 * edges + 4 * idreads + 17 * a.batch
         achieved = alg / (tier0_ms * 1e-3) / 1e9
+        kname = "keto::check_kernel<keto::GlobalStack, false, 0> (tier 0)"
+        traffic, tsrc = pmc_traffic(kname, {"tuples": int(g.n_edges), "checks_per_gpu_per_step": a.batch,
+                                            "max_depth": a.depth, "scale": a.scale})
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "alg_bytes_per_launch": int(alg), "kernel": "check_kernel<LocalStack<16>, false, 0> (tier 0)",
-                    "kernel_ms": round(tier0_ms, 3)}
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None if traffic is None else int(traffic),
+                    "traffic_GBps": None if traffic is None else round(traffic / (tier0_ms * 1e-3) / 1e9, 1),
+                    "traffic_source": tsrc,
+                    "alg_bytes_per_launch": int(alg), "kernel": kname, "kernel_ms": round(tier0_ms, 3)}
         work = {"rows_per_check": rows / a.batch, "set_edges_per_check": edges / a.batch,
                 "id_words_per_check": idreads / a.batch, "visited_hbm_probes_per_check": vprobes / a.batch,
                 "top_level_items_per_check": items / a.batch}
