@@ -146,7 +146,9 @@ def main():
                     "alg_bytes_per_launch": int(alg), "kernel": kname, "kernel_ms": round(tier0_ms, 3)}
         work = {"rows_per_check": rows / a.batch, "set_edges_per_check": edges / a.batch,
                 "id_words_per_check": idreads / a.batch, "visited_hbm_probes_per_check": vprobes / a.batch,
-                "top_level_items_per_check": items / a.batch}
+                "top_level_items_per_check": items / a.batch,
+                "line_touches_per_check": {k: round(v / a.batch, 3) for k, v in zip(
+                    ("request", "header", "edge", "id_table", "id_search", "frame_push", "frame_pop"), w[6:13])}}
 
     # ---- CPU baseline (rank 0, N = 1): oracle restatement on a bounded sample of the same batch
     cpu = None

@@ -202,9 +202,12 @@ int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
 /* Work counters of the traversal for a device-resident batch (instrumented kernels; same results):
  * out[0] row records read, out[1] subject-set edges scanned, out[2] subject-id words read by the
  * membership searches, out[3] visited-table probes, out[4] visited-table inserts, out[5] top-level
- * subject sets expanded (fresh visited maps).  Used for the roofline's algorithmic bytes. */
+ * subject sets expanded (fresh visited maps).  Used for the roofline's algorithmic bytes.
+ * out[6..12] are 128-B line touches per access stream (requests, row headers, edges, id tables,
+ * id searches, frame pushes, frame pops): an upper bound of the kernel's L2 line traffic. */
+#define KETO_WORK_SLOTS 16
 int keto_check_work_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
-                           uint8_t* d_allowed_out, uint64_t out[8]);
+                           uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]);
 
 /* Batched BuildTree.  The arena owns all trees; free it with keto_tree_arena_free. */
 int keto_expand_batch(keto_snapshot* s, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,

@@ -272,7 +272,7 @@ class Snapshot:
         return list(t.tier_ms), list(t.requests)
 
     def check_work_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, global_max_depth=5):
-        out = (C.c_uint64 * 8)()
+        out = (C.c_uint64 * 16)()
         _check(self.lib.keto_check_work_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
                                                C.c_int32(global_max_depth), C.c_void_p(d_out_ptr), out))
         return list(out)

@@ -329,7 +329,7 @@ int keto_last_batch_timing(const keto_snapshot* h, keto_batch_timing* out) {
 }
 
 int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
-                           uint8_t* d_allowed_out, uint64_t out[8]) {
+                           uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]) {
     return guarded([&] {
         if (!h || !out || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, false, nullptr, nullptr, out);

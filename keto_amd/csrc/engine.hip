@@ -14,7 +14,7 @@
 // Data: the snapshot is one u32 arena per device (layout in snapshot.hpp).  A row visit reads the
 // row's 16-B header, which sits right in front of its edges, so the header line usually also holds
 // the subject sets and a short id region.  A requested subject id is looked up in the row's
-// byte-ordered id region (binary search, <= HASH_MIN ids) or in the open-addressing id table stored
+// id window (binary search, <= WINDOW_WORDS edges) or in the bucketed id table stored
 // in front of the header: an id never changes the visited map unless its key collides, so only
 // membership matters, which is what makes looking it up (instead of walking to it) exact.
 // Visited maps keep their first REG_VIDS visit ids in registers and spill into a per-lane,
@@ -117,34 +117,59 @@ struct Work {
     __device__ inline void vprobe() {}
     __device__ inline void vinsert() {}
     __device__ inline void item() {}
+    __device__ inline void request() {}
+    __device__ inline void header(const void*) {}
+    __device__ inline void edge_at(const void*) {}
+    __device__ inline void id_at(const void*, bool) {}
+    __device__ inline void push() {}
+    __device__ inline void pop() {}
 };
 template <>
 struct Work<true> {
-    uint64_t rows = 0, edges = 0, idreads = 0, vprobes = 0, vinserts = 0, items = 0;
-    __device__ inline void row() { ++rows; }
-    __device__ inline void edge() { ++edges; }
-    __device__ inline void idread(uint32_t k) { idreads += k; }
-    __device__ inline void vprobe() { ++vprobes; }
-    __device__ inline void vinsert() { ++vinserts; }
-    __device__ inline void item() { ++items; }
+    // 0 rows, 1 set edges, 2 id words, 3 visited HBM probes, 4 visited inserts, 5 top-level items,
+    // line touches (a 128-B line different from the lane's previous access in that stream):
+    // 6 requests, 7 row headers, 8 edges, 9 id table, 10 id search, 11 frame pushes, 12 frame pops
+    uint64_t c[16] = {};
+    uint64_t edge_line = ~0ull, id_line = ~0ull;
+    __device__ inline void row() { ++c[0]; }
+    __device__ inline void edge() { ++c[1]; }
+    __device__ inline void idread(uint32_t k) { c[2] += k; }
+    __device__ inline void vprobe() { ++c[3]; }
+    __device__ inline void vinsert() { ++c[4]; }
+    __device__ inline void item() { ++c[5]; }
+    __device__ inline void request() { ++c[6]; }
+    __device__ inline void header(const void* p) {
+        ++c[7];
+        edge_line = id_line = (uint64_t)p >> 7;
+    }
+    __device__ inline void edge_at(const void* p) {
+        const uint64_t l = (uint64_t)p >> 7;
+        if (l != edge_line) ++c[8];
+        edge_line = l;
+    }
+    __device__ inline void id_at(const void* p, bool table) {
+        const uint64_t l = (uint64_t)p >> 7;
+        if (l != id_line) ++c[table ? 9 : 10];
+        id_line = l;
+    }
+    __device__ inline void push() { ++c[11]; }
+    __device__ inline void pop() { ++c[12]; }
 };
-
 // Is subject id t in the row's (effective) id region?
 template <class W>
 __device__ inline bool row_has_id(const RowView& rv, uint32_t t, W& w) {
     if (rv.n_ids == 0) return false;
     const uint32_t* __restrict__ e = rv.a;
     if (rv.hlog2) {
-        // open-addressing table in front of the header: [beg - HDR_WORDS - 2^hlog2, beg - HDR_WORDS)
-        const uint32_t mask = (1u << rv.hlog2) - 1u;
+        // bucketed table in front of the header: [beg - HDR_WORDS - 2^hlog2, beg - HDR_WORDS)
+        const uint32_t nb = (1u << rv.hlog2) / BUCKET_WORDS;
         const uint64_t tb = rv.beg - HDR_WORDS - (1ull << rv.hlog2);
-        uint32_t i = mix32(t) & mask;
-        for (;;) {
-            const uint32_t v = e[tb + i];
-            w.idread(1);
-            if (v == t) return true;
-            if (v == NONE32) return false;
-            i = (i + 1) & mask;
+        for (uint32_t b = mix32(t) & (nb - 1);; b = (b + 1) & (nb - 1)) {
+            const uint4 v = *reinterpret_cast<const uint4*>(e + tb + (uint64_t)b * BUCKET_WORDS);
+            w.idread(BUCKET_WORDS);
+            w.id_at(e + tb + (uint64_t)b * BUCKET_WORDS, true);
+            if (v.x == t || v.y == t || v.z == t || v.w == t) return true;
+            if (v.x == NONE32 || v.y == NONE32 || v.z == NONE32 || v.w == NONE32) return false;
         }
     }
     // lower_bound over the byte-ordered id region; invariant: answer in [lo, hi] (hi included)
@@ -154,12 +179,14 @@ __device__ inline bool row_has_id(const RowView& rv, uint32_t t, W& w) {
     while (hi - lo > 8) {
         uint32_t m = (lo + hi) >> 1;
         w.idread(1);
+        w.id_at(e + b + m, false);
         if (e[b + m] < t) lo = m + 1; else hi = m;
     }
     const uint32_t end = hi < n ? hi + 1 : n;
     for (uint32_t i = lo; i < end; ++i) {
         uint32_t v = e[b + i];
         w.idread(1);
+        w.id_at(e + b + i, false);
         if (v >= t) return v == t;
     }
     return false;
@@ -207,42 +234,44 @@ struct Visited {
 constexpr int REG_VIDS = KETO_REG_VIDS;
 // ...then the next LDS_VIDS in a per-lane LDS column ([slot][lane], conflict-free), then HBM.
 #ifndef KETO_LDS_VIDS
-#define KETO_LDS_VIDS 16
+#define KETO_LDS_VIDS 8
 #endif
 constexpr int LDS_VIDS = KETO_LDS_VIDS;
 constexpr int LDS_STRIDE = 256;          // lanes per block
+// A visited map of one lane: the first REG_VIDS ids in registers, the next LV in the lane's LDS
+// column, and only the ids beyond those in the lane's HBM table (started fresh on the first
+// overflow), so a test probes HBM only when a map has outgrown registers + LDS.
+template <int LV>
 struct VisitedRS {
     uint32_t r[REG_VIDS];
-    uint32_t n;          // entries held: r, then lds; REG_VIDS + LDS_VIDS + 1 = spilled to V
+    uint32_t n;          // ids held in r + lds; REG_VIDS + LV + 1 = the HBM table holds the rest
     uint32_t* lds;       // this lane's LDS column (stride LDS_STRIDE), or nullptr
     Visited V;
     __device__ inline void fresh() { n = 0; }
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
-        const uint32_t lcap = lds ? (uint32_t)LDS_VIDS : 0u;
-        if (n <= (uint32_t)REG_VIDS + lcap) {
-            bool hit = false;
+        const uint32_t lcap = lds ? (uint32_t)LV : 0u;
+        const uint32_t m = min(n, (uint32_t)REG_VIDS + lcap);
+        bool hit = false;
 #pragma unroll
-            for (int i = 0; i < REG_VIDS; ++i) hit |= ((uint32_t)i < n) & (r[i] == vid);
-            for (uint32_t i = REG_VIDS; i < n && !hit; ++i) hit = lds[(i - REG_VIDS) * LDS_STRIDE] == vid;
-            if (hit) return 1;
-            if (n < (uint32_t)REG_VIDS) {
+        for (int i = 0; i < REG_VIDS; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
+        for (uint32_t i = REG_VIDS; i < m && !hit; ++i) hit = lds[(i - REG_VIDS) * LDS_STRIDE] == vid;
+        if (hit) return 1;
+        if (n < (uint32_t)REG_VIDS) {
 #pragma unroll
-                for (int i = 0; i < REG_VIDS; ++i)
-                    if ((uint32_t)i == n) r[i] = vid;
-                ++n;
-                return 0;
-            }
-            if (n < (uint32_t)REG_VIDS + lcap) {
-                lds[(n - REG_VIDS) * LDS_STRIDE] = vid;
-                ++n;
-                return 0;
-            }
-            V.fresh();                                  // spill everything into the HBM table
-#pragma unroll
-            for (int i = 0; i < REG_VIDS; ++i) V.test_add(r[i], w);
-            for (uint32_t i = 0; i < lcap; ++i) V.test_add(lds[i * LDS_STRIDE], w);
-            n = REG_VIDS + lcap + 1;
+            for (int i = 0; i < REG_VIDS; ++i)
+                if ((uint32_t)i == n) r[i] = vid;
+            ++n;
+            return 0;
+        }
+        if (n < (uint32_t)REG_VIDS + lcap) {
+            lds[(n - REG_VIDS) * LDS_STRIDE] = vid;
+            ++n;
+            return 0;
+        }
+        if (n == (uint32_t)REG_VIDS + lcap) {            // first overflow of this map
+            V.fresh();
+            ++n;
         }
         return V.test_add(vid, w);
     }
@@ -260,13 +289,43 @@ template <int N>
 struct LocalStack {
     Frame f[N];
     __device__ inline Frame& operator[](int i) { return f[i]; }
+    __device__ inline void save(int i, const Frame& x) { f[i] = x; }
+    __device__ inline Frame load(int i) { return f[i]; }
     __device__ static constexpr int cap() { return N; }
 };
 struct GlobalStack {
     Frame* f;           // this lane's frames
     int n;
     __device__ inline Frame& operator[](int i) { return f[i]; }
+    __device__ inline void save(int i, const Frame& x) { f[i] = x; }
+    __device__ inline Frame load(int i) { return f[i]; }
     __device__ inline int cap() const { return n; }
+};
+// Saved check frames in a per-lane LDS column ([frame][lane], 8 B each): the word position and
+// the edges left, with the frame flags in the top bits of `left`.  A frame's remaining depth is
+// not stored: a parent's is always its child's + 1 (the caller restores it).  Check only: a row
+// with >= 2^29 edges left cannot be saved here and sends its request up a tier (LFULL).
+constexpr uint32_t LDS_LEFT_MAX = (1u << 29) - 1u;
+template <int N>
+struct LdsStack {
+    uint2* col;         // this lane's column: col[i * LDS_STRIDE]
+    __device__ inline bool fits(const Frame& x) const { return x.left <= LDS_LEFT_MAX; }
+    __device__ inline void save(int i, const Frame& x) {
+        col[i * LDS_STRIDE] = make_uint2((uint32_t)x.pos, x.left | ((uint32_t)x.fl << 29));
+    }
+    __device__ inline Frame load(int i) {
+        const uint2 v = col[i * LDS_STRIDE];
+        return Frame{v.x, v.y & LDS_LEFT_MAX, 0, (uint16_t)(v.y >> 29)};
+    }
+    __device__ static constexpr int cap() { return N; }
+};
+template <class S>
+struct is_lds_stack : std::false_type {
+    static constexpr int frames = 1;
+};
+template <int N>
+struct is_lds_stack<LdsStack<N>> : std::true_type {
+    static constexpr int frames = N;
 };
 
 struct TierArgs {
@@ -299,7 +358,9 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
-    VisitedRS V;
+    constexpr int LDS_FRAMES = is_lds_stack<Stack>::frames;
+    __shared__ uint2 lds_frames[LDS_FRAMES * LDS_STRIDE];
+    VisitedRS<LDS_VIDS> V;
     V.n = 0;
     V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
@@ -311,9 +372,13 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
         st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
         st.n = ta.gstack_n;
     }
+    if constexpr (is_lds_stack<Stack>::value) st.col = lds_frames + threadIdx.x;
     Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
-    uint32_t j = slot;
+    // each lane owns a contiguous run of requests, so consecutive fetches share request lines
+    const uint32_t per = (total + stride - 1) / stride;
+    uint32_t j = slot * per;
+    const uint32_t j_end = min(total, j + per);
     bool busy = false;           // a request is in flight on this lane
     uint32_t qi = 0, T = 0, tval = 0;
     bool tset = false;
@@ -325,10 +390,11 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
         uint16_t enter_k = 0, enter_fl = 0;
         int res = -1;                // >= 0: request decided (RES_*)
         if (!busy) {
-            if (j >= total) break;
+            if (j >= j_end) break;
             qi = ta.in_list ? ta.in_list[j] : j;
-            j += stride;
+            ++j;
             const keto_check_ids qq = q[qi];
+            w.request();
             int d = qq.max_depth;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
             if (qq.row == KETO_NO_ROW || d <= 0 || qq.target == KETO_NO_TARGET) {
@@ -347,11 +413,15 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             if (--sp == 0) {
                 res = RES_FALSE;
             } else {
-                cur = st[sp - 1];
+                const uint16_t k = cur.k + 1;
+                cur = st.load(sp - 1);
+                cur.k = k;
+                w.pop();
                 ce = (cur.fl & FR_OV) ? ov.arena : s.arena;
             }
         } else {
             const uint32_t e = ce[cur.pos];
+            w.edge_at(ce + cur.pos);
             ++cur.pos;
             --cur.left;
             w.edge();
@@ -389,12 +459,19 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
         if (enter != NONE32) {
             const RowView rv = load_row(s, ov, enter);
             w.row();
+            w.header(rv.a + rv.beg - HDR_WORDS);
             if (!rv.seq && !tset && row_has_id(rv, T, w)) {
                 res = RES_TRUE;
             } else if (sp > st.cap()) {        // saved frames live in st[0 .. sp-1)
                 res = RES_OVERFLOW;
-            } else {
-                if (sp > 0) st[sp - 1] = cur;
+            } else if constexpr (is_lds_stack<Stack>::value) {
+                if (sp > 0 && !st.fits(cur)) res = RES_OVERFLOW;
+            }
+            if (enter != NONE32 && res < 0) {
+                if (sp > 0) {
+                    st.save(sp - 1, cur);
+                    w.push();
+                }
                 cur = Frame{rv.beg, rv.n_sets, enter_k,
                             (uint16_t)(enter_fl | (rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
                 ce = rv.a;
@@ -413,12 +490,235 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     }
     ta.slot_epoch[slot] = V.V.epoch;
     if constexpr (COUNT) {
-        atomicAdd(work + 0, (unsigned long long)w.rows);
-        atomicAdd(work + 1, (unsigned long long)w.edges);
-        atomicAdd(work + 2, (unsigned long long)w.idreads);
-        atomicAdd(work + 3, (unsigned long long)w.vprobes);
-        atomicAdd(work + 4, (unsigned long long)w.vinserts);
-        atomicAdd(work + 5, (unsigned long long)w.items);
+        for (int i = 0; i < 13; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
+    }
+}
+
+// ------------------------------------------------------------------ check, tier 0
+// The same traversal as check_kernel, restructured so that every loop iteration issues at most
+// ONE global access per lane, and every lane issues it from the same instruction: the next
+// request (16 B), a row's header together with its window of the first four edge words (2 x 16 B
+// from one 32-B line-aligned slot), one 16-B bucket of a row's id table, or the next 16-B block of
+// a long row's edges.  Everything else -- walking the window, the visited maps, saving and
+// restoring frames -- runs on registers and LDS, so a wave waits once per iteration and all of its
+// lanes' accesses are in flight together.  Saved frames (position, edges left | depth | flags,
+// and the unread window) live in LDS; a frame with no edges left is not saved (the child returns
+// straight to the grandparent).  Requests needing more than F saved frames, or a row with more
+// than WF_LEFT_MAX edges left when saved, overflow to the next tier (check_kernel).
+constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
+constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // lkf = left | k << 23 | fl << 28
+constexpr uint16_t FR_WV = 8;                        // the window holds the block of `pos`
+
+__device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
+    return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
+}
+__device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
+
+#ifndef KETO_WAVE_WAVES
+#define KETO_WAVE_WAVES 6
+#endif
+
+template <int F, bool WIN, int LV, bool COUNT>
+__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
+    check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                      uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
+    __shared__ uint2 sf_pk[F * LDS_STRIDE];
+    __shared__ uint4 sf_win[(WIN ? F : 1) * LDS_STRIDE];
+    VisitedRS<LV> V;
+    V.n = 0;
+    V.lds = LV > 0 ? lds_vis + threadIdx.x : nullptr;
+    V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
+    V.V.mask = ta.mask;
+    V.V.epoch = ta.slot_epoch[slot];
+    V.V.count = 0;
+    Work<COUNT> w;
+    // each lane owns a contiguous run of requests, so consecutive fetches share request lines
+    const uint32_t per = (n + stride - 1) / stride;
+    uint32_t j = slot * per;
+    const uint32_t j_end = min(n, j + per);
+
+    uint32_t phase = P_REQ;
+    uint32_t qi = 0, T = 0, tval = 0;
+    bool tset = false;
+    uint32_t pos = 0, left = 0, k = 0, fl = 0;     // current frame
+    uint4 win = make_uint4(0, 0, 0, 0);
+    const uint32_t* ce = s.arena;
+    int sp = 0;                                    // saved frames
+    bool have = false;                             // a current frame exists
+    uint32_t enter_h = 0, enter_k = 0, enter_fl = 0;
+    uint32_t tb = 0, nbm = 0, bk = 0;              // id table probe
+    for (;;) {
+        // ---- the iteration's one global access
+        const uint4* a0 = nullptr;
+        const uint4* a1 = nullptr;
+        if (phase == P_REQ) {
+            if (j >= j_end) break;
+            qi = j++;
+            a0 = reinterpret_cast<const uint4*>(q + qi);
+            w.request();
+        } else if (phase == P_HDR) {
+            const bool is_ov = enter_h >= ov.base;
+            const uint32_t* ar = is_ov ? ov.arena : s.arena;
+            a0 = reinterpret_cast<const uint4*>(ar + (uint64_t)(is_ov ? enter_h - ov.base : enter_h) * HDR_WORDS);
+            a1 = a0 + 1;
+            w.header(a0);
+        } else if (phase == P_IDQ) {
+            a0 = reinterpret_cast<const uint4*>(ce + tb + bk * BUCKET_WORDS);
+            w.idread(BUCKET_WORDS);
+            w.id_at(a0, true);
+        } else if (phase == P_EDGE) {
+            a0 = reinterpret_cast<const uint4*>(ce + (pos & ~3u));
+            w.edge_at(a0);
+        }
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+        if (a0) v0 = *a0;
+        if (a1) v1 = *a1;
+
+        int res = -1;
+        if (phase == P_REQ) {
+            int d = (int)v0.w;
+            if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
+            if (v0.x == KETO_NO_ROW || d <= 0 || v0.y == KETO_NO_TARGET) {
+                allowed[qi] = 0;
+                continue;
+            }
+            tset = (v0.z & 1u) != 0;
+            T = v0.y;
+            tval = tset ? (EDGE_SET | T) : T;
+            sp = 0;
+            have = false;
+            enter_h = v0.x;
+            enter_k = (uint32_t)d;
+            enter_fl = FR_TOP;
+            phase = P_HDR;
+            continue;
+        }
+        if (phase == P_HDR) {
+            // entering a row (engine.go:82-114): save the parent if it still has edges
+            w.row();
+            if (have && left > 0) {
+                if (sp == F || left > WF_LEFT_MAX) {
+                    res = RES_OVERFLOW;
+                } else {
+                    const uint32_t sfl = WIN ? fl : (fl & ~(uint32_t)FR_WV);   // no saved window: reload it
+                    sf_pk[sp * LDS_STRIDE + threadIdx.x] = make_uint2(pos, left | (k << 23) | (sfl << 28));
+                    if constexpr (WIN) sf_win[sp * LDS_STRIDE + threadIdx.x] = win;
+                    ++sp;
+                    w.push();
+                }
+            }
+            if (res < 0) {
+                const bool is_ov = enter_h >= ov.base;
+                const bool seq = (v0.z & HDR_SEQ) != 0;
+                const uint32_t hl = (v0.z >> 8) & 31u;
+                ce = is_ov ? ov.arena : s.arena;
+                pos = (is_ov ? enter_h - ov.base : enter_h) * HDR_WORDS + HDR_WORDS;
+                left = v0.x;
+                k = enter_k;
+                fl = enter_fl | (seq ? FR_SEQ : 0) | (is_ov ? FR_OV : 0) | FR_WV;
+                win = v1;
+                have = true;
+                phase = P_WALK;
+                const uint32_t n_sets = v0.x, n_ids = v0.y;
+                if (!seq && !tset && n_ids > 0) {                 // is the requested id in the row?
+                    if (hl == 0) {                                // all ids are in the window
+                        bool hit = false;
+#pragma unroll
+                        for (uint32_t i = 0; i < WINDOW_WORDS; ++i)
+                            hit |= (i >= n_sets) & (i < n_sets + n_ids) & (win_at(win, i) == T);
+                        w.idread(n_ids);
+                        if (hit) res = RES_TRUE;
+                    } else {
+                        tb = pos - HDR_WORDS - (1u << hl);
+                        nbm = (1u << hl) / BUCKET_WORDS - 1u;
+                        bk = mix32(T) & nbm;
+                        phase = P_IDQ;
+                    }
+                }
+            }
+        } else if (phase == P_IDQ) {
+            if (has4(v0, T)) res = RES_TRUE;
+            else if (has4(v0, NONE32)) phase = P_WALK;
+            else bk = (bk + 1u) & nbm;
+        } else if (phase == P_EDGE) {
+            win = v0;
+            fl |= FR_WV;
+            phase = P_WALK;
+        }
+        // ---- walk the window (registers, LDS; HBM only for visited spills and collisions)
+        while (res < 0 && phase == P_WALK) {
+            if (left == 0) {                                      // row exhausted: pop
+                if (sp == 0) {
+                    res = RES_FALSE;
+                    break;
+                }
+                --sp;
+                const uint2 pk = sf_pk[sp * LDS_STRIDE + threadIdx.x];
+                if constexpr (WIN) win = sf_win[sp * LDS_STRIDE + threadIdx.x];
+                pos = pk.x;
+                left = pk.y & WF_LEFT_MAX;
+                k = (pk.y >> 23) & 31u;
+                fl = pk.y >> 28;
+                ce = (fl & FR_OV) ? ov.arena : s.arena;
+                w.pop();
+                continue;
+            }
+            if (!(fl & FR_WV)) {
+                phase = P_EDGE;
+                break;
+            }
+            const uint32_t e = win_at(win, pos & 3u);
+            ++pos;
+            --left;
+            if ((pos & 3u) == 0) fl &= ~(uint32_t)FR_WV;
+            w.edge();
+            if (e & EDGE_SET) {
+                uint32_t vid = e & EDGE_VAL;
+                if (fl & FR_SEQ) {
+                    const uint32_t c = coll_lookup(s, e);
+                    if (c != NONE32) vid = c;
+                }
+                if (fl & FR_TOP) {                                // fresh map per top-level tuple
+                    V.fresh();
+                    w.item();
+                }
+                const int t = V.test_add(vid, w);
+                if (t == 2) res = RES_OVERFLOW;
+                else if (t == 0) {
+                    if (tset && e == tval) res = RES_TRUE;        // engine.go:54-57
+                    else if (k >= 2) {                            // remaining depth after the hop >= 1
+                        enter_h = e & EDGE_VAL;
+                        enter_k = k - 1;
+                        enter_fl = 0;
+                        phase = P_HDR;
+                    }
+                }
+            } else {                                              // subject id in an ordered row
+                int t = 0;
+                if (!(fl & FR_TOP)) {
+                    const uint32_t c = coll_lookup(s, e);
+                    if (c != NONE32) t = V.test_add(c, w);
+                }
+                if (t == 2) res = RES_OVERFLOW;
+                else if (t == 0 && !tset && e == tval) res = RES_TRUE;
+            }
+        }
+        if (res >= 0) {
+            if (res == RES_OVERFLOW) {
+                const uint32_t at = atomicAdd(ta.out_count, 1u);
+                ta.out_list[at] = qi;
+            } else {
+                allowed[qi] = (uint8_t)res;
+            }
+            phase = P_REQ;
+        }
+    }
+    ta.slot_epoch[slot] = V.V.epoch;
+    if constexpr (COUNT) {
+        for (int i = 0; i < 13; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
     }
 }
 
@@ -565,7 +865,7 @@ struct DeviceState {
     std::mutex mu;                // one batch at a time per snapshot (workspaces are shared)
     Tier tiers[3];                // check workspaces
     Tier etiers[3];               // expand workspaces
-    uint32_t v1_lanes = 0;        // resident lanes of check_kernel (tier 0)
+    uint32_t v1_lanes[16] = {};   // resident lanes of the tier-0 check kernel, per variant
     uint32_t* lists = nullptr;    // 2 overflow lists, capacity list_cap each
     uint32_t* counters = nullptr; // 2 counters
     uint64_t list_cap = 0;
@@ -684,14 +984,20 @@ void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uin
     }
     for (uint64_t i = n_stored; i < ((n_stored + 3) & ~3ull); ++i) e[i] = NONE32;
     if (hlog2) {
-        const uint32_t mask = (1u << hlog2) - 1u;
+        const uint32_t nb = (1u << hlog2) / BUCKET_WORDS;
         uint32_t* tab = arena + h - (1ull << hlog2);
-        for (uint32_t i = 0; i <= mask; ++i) tab[i] = NONE32;
+        for (uint32_t i = 0; i < (1u << hlog2); ++i) tab[i] = NONE32;
         for (uint32_t k = 0; k < rec.n_ids; ++k) {
             const uint32_t id = edges[rec.n_sets + k];
-            uint32_t i = mix32(id) & mask;
-            while (tab[i] != NONE32 && tab[i] != id) i = (i + 1) & mask;
-            tab[i] = id;
+            for (uint32_t b = mix32(id) & (nb - 1);; b = (b + 1) & (nb - 1)) {
+                uint32_t* q = tab + (uint64_t)b * BUCKET_WORDS;
+                uint32_t i = 0;
+                while (i < BUCKET_WORDS && q[i] != NONE32 && q[i] != id) ++i;
+                if (i < BUCKET_WORDS) {
+                    q[i] = id;
+                    break;
+                }
+            }
         }
     }
 }
@@ -879,6 +1185,28 @@ struct DevFree {
 
 }  // namespace
 
+namespace {
+using CheckKernelFn = void (*)(DevSnap, DevOverlay, const keto_check_ids*, uint32_t, int, uint8_t*, TierArgs,
+                               unsigned long long*);
+// tier-0 variants for max-depth <= 5 (4 saved frames): {save windows, LDS visit ids}; then the
+// max-depth <= 9 kernel (8 frames).  KETO_T0 picks a variant (tuning); 0 is the default.
+constexpr int T0_VARIANTS = 4;
+int t0_variant() {
+    const char* e = getenv("KETO_T0");
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v < T0_VARIANTS ? v : 0;
+}
+CheckKernelFn t0_kernel(int var, bool count) {
+    switch (var) {
+        case 0: return count ? check_wave_kernel<4, false, 16, true> : check_wave_kernel<4, false, 16, false>;
+        case 1: return count ? check_wave_kernel<4, true, 16, true> : check_wave_kernel<4, true, 16, false>;
+        case 2: return count ? check_wave_kernel<4, true, 8, true> : check_wave_kernel<4, true, 8, false>;
+        case 3: return count ? check_wave_kernel<4, false, 8, true> : check_wave_kernel<4, false, 8, false>;
+        default: return count ? check_wave_kernel<8, false, 8, true> : check_wave_kernel<8, false, 8, false>;
+    }
+}
+}  // namespace
+
 void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
                   bool host_buffers, void* stream, const Overlay* ovh, uint64_t* work_out) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
@@ -902,59 +1230,56 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
         dq = tq;
         da = ta8;
     }
-    // check recursion holds at most gmd - 1 frames
+    // check recursion holds at most gmd - 1 frames.  Tier 0 keeps them in LDS when they fit
+    // (LdsStack<4> covers the default max-depth 5), else in HBM (GlobalStack).
     Plan p = make_plan(D, n, std::max(1, gmd - 1));
-    p.frames[0] = std::max(1, std::min(gmd - 1, 64));   // tier 0: frames in HBM (GlobalStack)
-    if (!D.v1_lanes) {
-        // persistent grid = what is resident at the kernel's register budget (KETO_SLOTS overrides)
+    const int fr = std::max(1, gmd - 1);
+    const int kind = fr <= 4 ? 0 : fr <= 8 ? 1 : 2;
+    p.frames[0] = kind == 2 ? std::min(fr, 64) : 0;
+    const int var = kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : T0_VARIANTS + 1;
+    if (!D.v1_lanes[var]) {
+        // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_kernel<GlobalStack, false, 0>, 256, 0));
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_kernel(var, false), 256, 0));
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
-        D.v1_lanes = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
-        if (getenv("KETO_SLOTS")) D.v1_lanes = (uint32_t)hw_slots();
+        D.v1_lanes[var] = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
+        if (getenv("KETO_SLOTS")) D.v1_lanes[var] = (uint32_t)hw_slots();
     }
-    p.slots[0] = (uint32_t)std::min<uint64_t>(D.v1_lanes, ((uint64_t)n + 255) / 256 * 256);
+    p.slots[0] = (uint32_t)std::min<uint64_t>(D.v1_lanes[var], ((uint64_t)n + 255) / 256 * 256);
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
     unsigned long long* dwork = nullptr;
     if (work_out) {
         uint64_t acc = 0;
-        dwork = dmalloc<unsigned long long>(8, acc);
+        dwork = dmalloc<unsigned long long>(KETO_WORK_SLOTS, acc);
         tmp.p.push_back(dwork);
-        HIP_OK(hipMemsetAsync(dwork, 0, 8 * sizeof(unsigned long long), st));
+        HIP_OK(hipMemsetAsync(dwork, 0, KETO_WORK_SLOTS * sizeof(unsigned long long), st));
     }
     run_tiers(D, D.tiers, n, p, st,
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
                   const uint32_t bs = std::min<uint32_t>(256, slots);
-                  dim3 grid(slots / bs), block(bs);
+                  const dim3 grid(slots / bs), block(bs);
+                  auto go = [&](auto kern) {
+                      hipLaunchKernelGGL(kern, grid, block, 0, st, sv, dov, dq, n, gmd, da, a, dwork);
+                  };
                   const bool local = p.frames[level] == 0;
-                  if (level == 0 && !dwork)
-                      hipLaunchKernelGGL((check_kernel<GlobalStack, false, 0>), grid, block, 0, st, sv, dov, dq, n,
-                                         gmd, da, a, dwork);
+                  if (level == 0 && kind < 2)
+                      go(t0_kernel(var, dwork != nullptr));
                   else if (level == 0)
-                      hipLaunchKernelGGL((check_kernel<GlobalStack, true, 1>), grid, block, 0, st, sv, dov, dq, n,
-                                         gmd, da, a, dwork);
-                  else if (local && !dwork)
-                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, false, 1>), grid, block, 0, st, sv, dov, dq, n,
-                                         gmd, da, a, dwork);
-                  else if (!dwork)
-                      hipLaunchKernelGGL((check_kernel<GlobalStack, false, 1>), grid, block, 0, st, sv, dov, dq, n,
-                                         gmd, da, a, dwork);
+                      dwork ? go(check_kernel<GlobalStack, true, 0>) : go(check_kernel<GlobalStack, false, 0>);
                   else if (local)
-                      hipLaunchKernelGGL((check_kernel<LocalStack<16>, true, 1>), grid, block, 0, st, sv, dov, dq, n,
-                                         gmd, da, a, dwork);
+                      dwork ? go(check_kernel<LocalStack<16>, true, 1>) : go(check_kernel<LocalStack<16>, false, 1>);
                   else
-                      hipLaunchKernelGGL((check_kernel<GlobalStack, true, 1>), grid, block, 0, st, sv, dov, dq, n, gmd,
-                                         da, a, dwork);
+                      dwork ? go(check_kernel<GlobalStack, true, 1>) : go(check_kernel<GlobalStack, false, 1>);
                   HIP_OK(hipGetLastError());
               });
     if (work_out) {
-        unsigned long long h[8];
+        unsigned long long h[KETO_WORK_SLOTS];
         HIP_OK(hipMemcpyAsync(h, dwork, sizeof(h), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        for (int i = 0; i < 8; ++i) work_out[i] = h[i];
+        for (int i = 0; i < KETO_WORK_SLOTS; ++i) work_out[i] = h[i];
     }
     if (host_buffers) {
         HIP_OK(hipMemcpyAsync(allowed, da, n, hipMemcpyDeviceToHost, st));

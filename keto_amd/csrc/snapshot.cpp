@@ -245,7 +245,9 @@ uint32_t ceil_log2(uint64_t x) {
 
 uint32_t Snapshot::row_hlog2(uint32_t r) const {
     if (row_flags(r) & ROW_SEQ) return 0;
-    return rows[r].n_ids > HASH_MIN ? ceil_log2(2ull * rows[r].n_ids) : 0;
+    const RowRec& x = rows[r];
+    if (x.n_ids == 0 || (uint64_t)x.n_sets + x.n_ids <= WINDOW_WORDS) return 0;   // ids sit in the window
+    return std::max<uint32_t>(2, ceil_log2(2ull * x.n_ids));                      // load <= 1/2, >= 1 bucket
 }
 
 void compute_layout(Snapshot& S) {
@@ -256,6 +258,14 @@ void compute_layout(Snapshot& S) {
         const uint32_t h = S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
         const uint64_t n = row_end_of(S, r) - S.row_begin(r);
+        // line placement: a row that fits one 128-B line gets one line to itself (header, window
+        // and id table come in with one miss); a bigger row keeps header + window in one line
+        const uint64_t total = table + HDR_WORDS + ((n + 3) & ~3ull);
+        if (total <= LINE_WORDS) {
+            if (w % LINE_WORDS + total > LINE_WORDS) w = (w + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
+        } else if ((w + table) % LINE_WORDS == LINE_WORDS - HDR_WORDS) {
+            w += HDR_WORDS;
+        }
         const uint64_t unit = (w + table) / HDR_WORDS;
         if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
         S.unit_of_row[r] = (uint32_t)unit;

@@ -38,13 +38,17 @@ constexpr uint32_t ROW_SEQ = 1u;                // flag bit (in RowRec.y bits 8.
 constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys live above all row ids
 
 // Device arena (one u32 array per device).  Row r occupies
-//   [open-addressing subject-id table, 2^hlog2 words, only for rows with > HASH_MIN ids]
+//   [subject-id table, 2^hlog2 words of 16-B buckets, for rows whose ids do not all fit in the
+//    window (n_ids > 0 and n_sets + n_ids > WINDOW_WORDS)]
 //   [16-B header: n_sets, n_ids, flags | hlog2 << 8, first poisoned page]   <- handle = word / 4
 //   [edges in ORDER BY order; subject sets hold the target's handle]        padded to 16 B
-// so one row visit reads one header line that usually also holds the subject sets and a short
-// id region, and a long id region is probed in the table right in front of the header.
-constexpr uint32_t HASH_MIN = 16;               // id regions longer than this get a table
+// A row visit reads the header and the window (the first 4 edge words) with one 32-B access
+// that never straddles a 128-B line; a row that fits in a line is placed in a single line, so
+// its id table is in the line the header came in with.
 constexpr uint32_t HDR_WORDS = 4;
+constexpr uint32_t WINDOW_WORDS = 4;            // edge words read together with the header
+constexpr uint32_t LINE_WORDS = 32;             // 128-B cache line
+constexpr uint32_t BUCKET_WORDS = 4;            // id tables are probed one 16-B bucket at a time
 constexpr uint32_t HDR_SEQ = 1u;                // flags bit (header word 2, bits 0..7)
 
 struct RowRec {          // 16 B
