@@ -84,7 +84,7 @@ struct RowView {
     uint64_t beg;             // word index of the first edge
     uint32_t n_sets, n_ids;   // effective counts (ROW_SEQ: n_sets = all edges, in order)
     uint32_t hlog2;           // id table size (0 = none), table ends at beg - HDR_WORDS
-    uint32_t pp;              // first poisoned page (expand)
+    bool poison, poison0;     // some page / the first page fails toInternal (expand)
     bool seq;
 };
 
@@ -104,7 +104,8 @@ __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint3
     rv.n_ids = v.y;
     rv.seq = (v.z & HDR_SEQ) != 0;
     rv.hlog2 = (v.z >> 8) & 31u;
-    rv.pp = v.w;
+    rv.poison = (v.z & HDR_POISON) != 0;
+    rv.poison0 = (v.z & HDR_POISON0) != 0;
     return rv;
 }
 
@@ -550,14 +551,38 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     bool have = false;                             // a current frame exists
     uint32_t enter_h = 0, enter_k = 0, enter_fl = 0;
     uint32_t tb = 0, nbm = 0, bk = 0;              // id table probe
+    uint32_t tb1 = 0, tb2 = 0;                     // bloom bits of the requested id
+    uint4 nq = make_uint4(0, 0, 0, 0);             // prefetched request j
+    bool nq_ok = false;
     for (;;) {
-        // ---- the iteration's one global access
+        // ---- start the next request from its prefetched copy (no iteration spent on fetching it)
+        while (phase == P_REQ && nq_ok) {
+            nq_ok = false;
+            qi = j++;
+            int d = (int)nq.w;
+            if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
+            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
+                allowed[qi] = 0;
+                continue;
+            }
+            tset = (nq.z & 1u) != 0;
+            T = nq.y;
+            tval = tset ? (EDGE_SET | T) : T;
+            bloom_bits(T, tb1, tb2);
+            sp = 0;
+            have = false;
+            enter_h = nq.x;
+            enter_k = (uint32_t)d;
+            enter_fl = FR_TOP;
+            phase = P_HDR;
+        }
+        if (phase == P_REQ && j >= j_end) break;
+        // ---- the iteration's global accesses: one per lane (plus the next request's prefetch)
         const uint4* a0 = nullptr;
         const uint4* a1 = nullptr;
-        if (phase == P_REQ) {
-            if (j >= j_end) break;
-            qi = j++;
-            a0 = reinterpret_cast<const uint4*>(q + qi);
+        const uint4* a2 = nullptr;
+        if (phase == P_REQ) {                                     // not prefetched: fetch it now
+            a0 = reinterpret_cast<const uint4*>(q + j);
             w.request();
         } else if (phase == P_HDR) {
             const bool is_ov = enter_h >= ov.base;
@@ -573,27 +598,22 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             a0 = reinterpret_cast<const uint4*>(ce + (pos & ~3u));
             w.edge_at(a0);
         }
-        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+        if (!nq_ok && phase != P_REQ && j < j_end) {
+            a2 = reinterpret_cast<const uint4*>(q + j);
+            w.request();
+        }
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
         if (a0) v0 = *a0;
         if (a1) v1 = *a1;
-
+        if (a2) v2 = *a2;
+        if (a2) {
+            nq = v2;
+            nq_ok = true;
+        }
         int res = -1;
         if (phase == P_REQ) {
-            int d = (int)v0.w;
-            if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            if (v0.x == KETO_NO_ROW || d <= 0 || v0.y == KETO_NO_TARGET) {
-                allowed[qi] = 0;
-                continue;
-            }
-            tset = (v0.z & 1u) != 0;
-            T = v0.y;
-            tval = tset ? (EDGE_SET | T) : T;
-            sp = 0;
-            have = false;
-            enter_h = v0.x;
-            enter_k = (uint32_t)d;
-            enter_fl = FR_TOP;
-            phase = P_HDR;
+            nq = v0;
+            nq_ok = true;
             continue;
         }
         if (phase == P_HDR) {
@@ -631,8 +651,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                             hit |= (i >= n_sets) & (i < n_sets + n_ids) & (win_at(win, i) == T);
                         w.idread(n_ids);
                         if (hit) res = RES_TRUE;
-                    } else {
-                        tb = pos - HDR_WORDS - (1u << hl);
+                    } else if (bloom_has(v0.z, v0.w, tb1) && bloom_has(v0.z, v0.w, tb2)) {
+                        tb = pos - HDR_WORDS - (1u << hl);        // the bloom filter cannot rule it out
                         nbm = (1u << hl) / BUCKET_WORDS - 1u;
                         bk = mix32(T) & nbm;
                         phase = P_IDQ;
@@ -753,13 +773,13 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     auto open = [&](uint32_t h, int k) -> int {
         const RowView rv = load_row(s, ov, h);
         const uint32_t n_all = rv.n_sets + rv.n_ids;
-        if (rv.pp == NO_PAGE && n_all == 0) return EXP_NIL;
-        if (rv.pp == 0) return EXP_ERROR;                   // the first page fails toInternal
+        if (!rv.poison && n_all == 0) return EXP_NIL;
+        if (rv.poison0) return EXP_ERROR;                   // the first page fails toInternal
         if (k <= 1) {                                       // :72-75
             emit(out, cnt, FILL, EDGE_SET | h, 0x80000000u);
             return EXP_TREE;
         }
-        if (rv.pp != NO_PAGE) return EXP_ERROR;             // a later page fails
+        if (rv.poison) return EXP_ERROR;                    // a later page fails
         if (sp == st.cap()) return EXP_OVERFLOW;
         emit(out, cnt, FILL, EDGE_SET | h, n_all);
         st[sp] = Frame{rv.beg, n_all, (uint16_t)k,
@@ -974,8 +994,20 @@ void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uin
     const bool seq = ((rec.hi_flags >> 8) & ROW_SEQ) != 0;
     arena[h + 0] = rec.n_sets;
     arena[h + 1] = rec.n_ids;
-    arena[h + 2] = (seq ? HDR_SEQ : 0u) | (hlog2 << 8);
-    arena[h + 3] = pp;
+    uint32_t w2 = (seq ? HDR_SEQ : 0u) | (pp != NO_PAGE ? HDR_POISON : 0u) | (pp == 0 ? HDR_POISON0 : 0u) | (hlog2 << 8);
+    uint32_t w3 = 0;
+    if (hlog2) {
+        for (uint32_t k = 0; k < rec.n_ids; ++k) {
+            uint32_t b[2];
+            bloom_bits(edges[rec.n_sets + k], b[0], b[1]);
+            for (uint32_t x : b) {
+                if (x < 32) w3 |= 1u << x;
+                else w2 |= 1u << (x - 32 + 13);
+            }
+        }
+    }
+    arena[h + 2] = w2;
+    arena[h + 3] = w3;
     uint32_t* e = arena + h + HDR_WORDS;
     for (uint64_t i = 0; i < n_stored; ++i) {
         uint32_t v = edges[i];

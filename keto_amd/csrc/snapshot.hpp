@@ -26,6 +26,12 @@
 
 #include "../../include/keto_mi355x.h"
 
+#if defined(__HIP__)
+#define KETO_HD __host__ __device__
+#else
+#define KETO_HD
+#endif
+
 namespace keto {
 
 constexpr uint32_t EDGE_SET = 0x80000000u;
@@ -49,7 +55,27 @@ constexpr uint32_t HDR_WORDS = 4;
 constexpr uint32_t WINDOW_WORDS = 4;            // edge words read together with the header
 constexpr uint32_t LINE_WORDS = 32;             // 128-B cache line
 constexpr uint32_t BUCKET_WORDS = 4;            // id tables are probed one 16-B bucket at a time
-constexpr uint32_t HDR_SEQ = 1u;                // flags bit (header word 2, bits 0..7)
+// header word 2: bits 0..7 flags, 8..12 hlog2, 13..31 bloom bits 32..50; word 3: bloom bits 0..31.
+// The 51-bit bloom filter (2 bits per subject id) summarizes the ids of a row with an id table,
+// so most absent ids are rejected with the header and the table is never probed for them.
+constexpr uint32_t HDR_SEQ = 1u;                // walked edge by edge (ROW_SEQ)
+constexpr uint32_t HDR_POISON = 2u;             // some page fails toInternal (expand: error)
+constexpr uint32_t HDR_POISON0 = 4u;            // the first page fails (check: empty row)
+constexpr uint32_t BLOOM_BITS = 51;
+KETO_HD inline void bloom_bits(uint32_t id, uint32_t& b1, uint32_t& b2) {
+    uint32_t h = id * 0x9E3779B1u + 0x7F4A7C15u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    h *= 0x297A2D39u;
+    h ^= h >> 15;
+    b1 = (h & 0xFFFFu) % BLOOM_BITS;
+    b2 = (h >> 16) % BLOOM_BITS;
+}
+// is bit b of the (word2, word3) bloom set?
+KETO_HD inline bool bloom_has(uint32_t w2, uint32_t w3, uint32_t b) {
+    return b < 32 ? ((w3 >> b) & 1u) : ((w2 >> (b - 32 + 13)) & 1u);
+}
 
 struct RowRec {          // 16 B
     uint32_t edge_lo;    // edge begin, low 32 bits
