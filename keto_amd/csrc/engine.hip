@@ -497,108 +497,144 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
 
 // ------------------------------------------------------------------ check, tier 0
 // The same traversal as check_kernel, restructured so that every loop iteration issues at most
-// ONE global access per lane, and every lane issues it from the same instruction: the next
-// request (16 B), a row's header together with its window of the first four edge words (2 x 16 B
-// from one 32-B line-aligned slot), one 16-B bucket of a row's id table, or the next 16-B block of
-// a long row's edges.  Everything else -- walking the window, the visited maps, saving and
-// restoring frames -- runs on registers and LDS, so a wave waits once per iteration and all of its
-// lanes' accesses are in flight together.  Saved frames (position, edges left | depth | flags,
-// and the unread window) live in LDS; a frame with no edges left is not saved (the child returns
-// straight to the grandparent).  Requests needing more than F saved frames, or a row with more
-// than WF_LEFT_MAX edges left when saved, overflow to the next tier (check_kernel).
+// ONE global access per lane, and every lane issues it from the same instruction: a row's header
+// together with its window of the first four edge words (2 x 16 B from one 32-B slot that never
+// straddles a line), one 16-B bucket of a row's id table, or the next 16-B block of a long row's
+// edges.  The lane's next request is prefetched alongside (into LDS), so starting a request costs
+// no iteration.  Everything else -- walking the window, the visited maps, saving and restoring
+// frames -- runs on registers and LDS, so a wave waits once per iteration with all of its lanes'
+// accesses in flight together.  The header's bloom filter rules most absent ids out without the
+// table.  Saved frames (position, edges left | depth | flags, optionally the unread window) live
+// in LDS; a frame with no edges left is not saved (the child returns straight to the grandparent).
+// A request needing more than F saved frames, or a row with more than WF_LEFT_MAX edges left when
+// saved, overflows to the next tier (check_kernel).  Lane control state is one packed word.
 constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
-constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // lkf = left | k << 23 | fl << 28
+constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // saved lkf = left | k << 23 | fl << 28
 constexpr uint16_t FR_WV = 8;                        // the window holds the block of `pos`
+// control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23
+constexpr uint32_t C_PH = 0, C_K = 3, C_FL = 8, C_SP = 12, C_HL = 19;
+constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18;
+__device__ inline uint32_t bf(uint32_t c, uint32_t off, uint32_t wd) { return (c >> off) & ((1u << wd) - 1u); }
+__device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_t v) {
+    const uint32_t m = ((1u << wd) - 1u) << off;
+    return (c & ~m) | ((v << off) & m);
+}
 
 __device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
     return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
 }
 __device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
 
+// visited map of a tier-0 lane: registers, then the lane's LDS column, then its HBM table
+template <int RV, int LV>
+struct LaneVisited {
+    uint32_t r[RV];
+    uint32_t n, epoch, count;
+    template <class W>
+    __device__ inline int test_add(uint32_t vid, uint32_t* lds, uint64_t* tab, uint32_t mask, W& w) {
+        const uint32_t m = min(n, (uint32_t)(RV + LV));
+        bool hit = false;
+#pragma unroll
+        for (int i = 0; i < RV; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
+        for (uint32_t i = RV; i < m && !hit; ++i) hit = lds[(i - RV) * LDS_STRIDE] == vid;
+        if (hit) return 1;
+        if (n < (uint32_t)RV) {
+#pragma unroll
+            for (int i = 0; i < RV; ++i)
+                if ((uint32_t)i == n) r[i] = vid;
+            ++n;
+            return 0;
+        }
+        if (n < (uint32_t)(RV + LV)) {
+            lds[(n - RV) * LDS_STRIDE] = vid;
+            ++n;
+            return 0;
+        }
+        Visited H{tab, mask, epoch, count};
+        if (n == (uint32_t)(RV + LV)) {                 // first overflow of this map
+            H.fresh();
+            ++n;
+        }
+        const int t = H.test_add(vid, w);
+        epoch = H.epoch;
+        count = H.count;
+        return t;
+    }
+};
+
 #ifndef KETO_WAVE_WAVES
-#define KETO_WAVE_WAVES 6
+#define KETO_WAVE_WAVES 8
 #endif
 
-template <int F, bool WIN, int LV, bool COUNT>
+template <int F, bool WIN, int LV, int RV, bool COUNT>
 __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
                       uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t slot = blockIdx.x * blockDim.x + tid;
     const uint32_t stride = gridDim.x * blockDim.x;
     __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
     __shared__ uint2 sf_pk[F * LDS_STRIDE];
     __shared__ uint4 sf_win[(WIN ? F : 1) * LDS_STRIDE];
-    VisitedRS<LV> V;
+    __shared__ uint4 lds_nq[LDS_STRIDE];                       // the lane's prefetched request
+    uint32_t* const vcol = lds_vis + tid;
+    LaneVisited<RV, LV> V;
     V.n = 0;
-    V.lds = LV > 0 ? lds_vis + threadIdx.x : nullptr;
-    V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
-    V.V.mask = ta.mask;
-    V.V.epoch = ta.slot_epoch[slot];
-    V.V.count = 0;
+    V.epoch = ta.slot_epoch[slot];
+    V.count = 0;
     Work<COUNT> w;
     // each lane owns a contiguous run of requests, so consecutive fetches share request lines
     const uint32_t per = (n + stride - 1) / stride;
-    uint32_t j = slot * per;
+    uint32_t j = slot * per;                                   // next request to start
     const uint32_t j_end = min(n, j + per);
 
-    uint32_t phase = P_REQ;
-    uint32_t qi = 0, T = 0, tval = 0;
-    bool tset = false;
-    uint32_t pos = 0, left = 0, k = 0, fl = 0;     // current frame
+    uint32_t c = P_REQ;                                        // control word
+    uint32_t T = 0;                                            // requested subject
+    uint32_t pos = 0, left = 0;                                // current frame (k, fl in c)
     uint4 win = make_uint4(0, 0, 0, 0);
-    const uint32_t* ce = s.arena;
-    int sp = 0;                                    // saved frames
-    bool have = false;                             // a current frame exists
-    uint32_t enter_h = 0, enter_k = 0, enter_fl = 0;
-    uint32_t tb = 0, nbm = 0, bk = 0;              // id table probe
-    uint32_t tb1 = 0, tb2 = 0;                     // bloom bits of the requested id
-    uint4 nq = make_uint4(0, 0, 0, 0);             // prefetched request j
-    bool nq_ok = false;
+    uint32_t eh = 0;                                           // row to enter (P_HDR) / bucket (P_IDQ)
     for (;;) {
         // ---- start the next request from its prefetched copy (no iteration spent on fetching it)
-        while (phase == P_REQ && nq_ok) {
-            nq_ok = false;
-            qi = j++;
+        while (bf(c, C_PH, 3) == P_REQ && (c & C_NQ)) {
+            const uint4 nq = lds_nq[tid];
+            const uint32_t qi = j++;
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
             if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
                 allowed[qi] = 0;
+                c &= ~C_NQ;
                 continue;
             }
-            tset = (nq.z & 1u) != 0;
             T = nq.y;
-            tval = tset ? (EDGE_SET | T) : T;
-            bloom_bits(T, tb1, tb2);
-            sp = 0;
-            have = false;
-            enter_h = nq.x;
-            enter_k = (uint32_t)d;
-            enter_fl = FR_TOP;
-            phase = P_HDR;
+            eh = nq.x;
+            c = P_HDR | ((uint32_t)d << C_K) | ((nq.z & 1u) ? C_TSET : 0u);   // sp 0, no frame, nq taken
         }
-        if (phase == P_REQ && j >= j_end) break;
-        // ---- the iteration's global accesses: one per lane (plus the next request's prefetch)
+        const uint32_t ph = bf(c, C_PH, 3);
+        if (ph == P_REQ && j >= j_end) break;
+        // ---- the iteration's global accesses: one per lane, plus the next request's prefetch
+        const uint32_t* const ce = (bf(c, C_FL, 4) & FR_OV) ? ov.arena : s.arena;
         const uint4* a0 = nullptr;
         const uint4* a1 = nullptr;
         const uint4* a2 = nullptr;
-        if (phase == P_REQ) {                                     // not prefetched: fetch it now
+        if (ph == P_REQ) {                                        // not prefetched: fetch it now
             a0 = reinterpret_cast<const uint4*>(q + j);
             w.request();
-        } else if (phase == P_HDR) {
-            const bool is_ov = enter_h >= ov.base;
+        } else if (ph == P_HDR) {
+            const bool is_ov = eh >= ov.base;
             const uint32_t* ar = is_ov ? ov.arena : s.arena;
-            a0 = reinterpret_cast<const uint4*>(ar + (uint64_t)(is_ov ? enter_h - ov.base : enter_h) * HDR_WORDS);
+            a0 = reinterpret_cast<const uint4*>(ar + (uint64_t)(is_ov ? eh - ov.base : eh) * HDR_WORDS);
             a1 = a0 + 1;
             w.header(a0);
-        } else if (phase == P_IDQ) {
-            a0 = reinterpret_cast<const uint4*>(ce + tb + bk * BUCKET_WORDS);
+        } else if (ph == P_IDQ) {
+            const uint32_t hl = bf(c, C_HL, 5);
+            a0 = reinterpret_cast<const uint4*>(ce + (pos - HDR_WORDS - (1u << hl)) + eh * BUCKET_WORDS);
             w.idread(BUCKET_WORDS);
             w.id_at(a0, true);
-        } else if (phase == P_EDGE) {
+        } else if (ph == P_EDGE) {
             a0 = reinterpret_cast<const uint4*>(ce + (pos & ~3u));
             w.edge_at(a0);
         }
-        if (!nq_ok && phase != P_REQ && j < j_end) {
+        if (!(c & C_NQ) && ph != P_REQ && j < j_end) {
             a2 = reinterpret_cast<const uint4*>(q + j);
             w.request();
         }
@@ -607,41 +643,42 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         if (a1) v1 = *a1;
         if (a2) v2 = *a2;
         if (a2) {
-            nq = v2;
-            nq_ok = true;
+            lds_nq[tid] = v2;
+            c |= C_NQ;
         }
-        int res = -1;
-        if (phase == P_REQ) {
-            nq = v0;
-            nq_ok = true;
+        if (ph == P_REQ) {
+            lds_nq[tid] = v0;
+            c |= C_NQ;
             continue;
         }
-        if (phase == P_HDR) {
+        int res = -1;
+        const bool tset = (c & C_TSET) != 0;
+        if (ph == P_HDR) {
             // entering a row (engine.go:82-114): save the parent if it still has edges
             w.row();
+            const bool have = (c & C_HAVE) != 0;
             if (have && left > 0) {
+                const uint32_t sp = bf(c, C_SP, 4);
                 if (sp == F || left > WF_LEFT_MAX) {
                     res = RES_OVERFLOW;
                 } else {
-                    const uint32_t sfl = WIN ? fl : (fl & ~(uint32_t)FR_WV);   // no saved window: reload it
-                    sf_pk[sp * LDS_STRIDE + threadIdx.x] = make_uint2(pos, left | (k << 23) | (sfl << 28));
-                    if constexpr (WIN) sf_win[sp * LDS_STRIDE + threadIdx.x] = win;
-                    ++sp;
+                    const uint32_t fl = WIN ? bf(c, C_FL, 4) : (bf(c, C_FL, 4) & ~(uint32_t)FR_WV);
+                    sf_pk[sp * LDS_STRIDE + tid] = make_uint2(pos, left | (bf(c, C_K, 5) << 23) | (fl << 28));
+                    if constexpr (WIN) sf_win[sp * LDS_STRIDE + tid] = win;
+                    c = bf_set(c, C_SP, 4, sp + 1);
                     w.push();
                 }
             }
             if (res < 0) {
-                const bool is_ov = enter_h >= ov.base;
+                const bool is_ov = eh >= ov.base;
                 const bool seq = (v0.z & HDR_SEQ) != 0;
                 const uint32_t hl = (v0.z >> 8) & 31u;
-                ce = is_ov ? ov.arena : s.arena;
-                pos = (is_ov ? enter_h - ov.base : enter_h) * HDR_WORDS + HDR_WORDS;
+                const uint32_t k = have ? bf(c, C_K, 5) - 1u : bf(c, C_K, 5);
+                const uint32_t fl = (have ? 0u : (uint32_t)FR_TOP) | (seq ? FR_SEQ : 0u) | (is_ov ? FR_OV : 0u) | FR_WV;
+                pos = (is_ov ? eh - ov.base : eh) * HDR_WORDS + HDR_WORDS;
                 left = v0.x;
-                k = enter_k;
-                fl = enter_fl | (seq ? FR_SEQ : 0) | (is_ov ? FR_OV : 0) | FR_WV;
                 win = v1;
-                have = true;
-                phase = P_WALK;
+                c = bf_set(bf_set(bf_set(bf_set(c, C_K, 5, k), C_FL, 4, fl), C_HL, 5, hl), C_PH, 3, P_WALK) | C_HAVE;
                 const uint32_t n_sets = v0.x, n_ids = v0.y;
                 if (!seq && !tset && n_ids > 0) {                 // is the requested id in the row?
                     if (hl == 0) {                                // all ids are in the window
@@ -651,92 +688,93 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                             hit |= (i >= n_sets) & (i < n_sets + n_ids) & (win_at(win, i) == T);
                         w.idread(n_ids);
                         if (hit) res = RES_TRUE;
-                    } else if (bloom_has(v0.z, v0.w, tb1) && bloom_has(v0.z, v0.w, tb2)) {
-                        tb = pos - HDR_WORDS - (1u << hl);        // the bloom filter cannot rule it out
-                        nbm = (1u << hl) / BUCKET_WORDS - 1u;
-                        bk = mix32(T) & nbm;
-                        phase = P_IDQ;
+                    } else {
+                        uint32_t b1, b2;
+                        bloom_bits(T, b1, b2);
+                        if (bloom_has(v0.z, v0.w, b1) && bloom_has(v0.z, v0.w, b2)) {
+                            eh = mix32(T) & ((1u << hl) / BUCKET_WORDS - 1u);   // probe the table
+                            c = bf_set(c, C_PH, 3, P_IDQ);
+                        }
                     }
                 }
             }
-        } else if (phase == P_IDQ) {
+        } else if (ph == P_IDQ) {
             if (has4(v0, T)) res = RES_TRUE;
-            else if (has4(v0, NONE32)) phase = P_WALK;
-            else bk = (bk + 1u) & nbm;
-        } else if (phase == P_EDGE) {
+            else if (has4(v0, NONE32)) c = bf_set(c, C_PH, 3, P_WALK);
+            else eh = (eh + 1u) & ((1u << bf(c, C_HL, 5)) / BUCKET_WORDS - 1u);
+        } else if (ph == P_EDGE) {
             win = v0;
-            fl |= FR_WV;
-            phase = P_WALK;
+            c = bf_set(c, C_PH, 3, P_WALK) | ((uint32_t)FR_WV << C_FL);
         }
         // ---- walk the window (registers, LDS; HBM only for visited spills and collisions)
-        while (res < 0 && phase == P_WALK) {
+        while (res < 0 && bf(c, C_PH, 3) == P_WALK) {
             if (left == 0) {                                      // row exhausted: pop
+                uint32_t sp = bf(c, C_SP, 4);
                 if (sp == 0) {
                     res = RES_FALSE;
                     break;
                 }
                 --sp;
-                const uint2 pk = sf_pk[sp * LDS_STRIDE + threadIdx.x];
-                if constexpr (WIN) win = sf_win[sp * LDS_STRIDE + threadIdx.x];
+                const uint2 pk = sf_pk[sp * LDS_STRIDE + tid];
+                if constexpr (WIN) win = sf_win[sp * LDS_STRIDE + tid];
                 pos = pk.x;
                 left = pk.y & WF_LEFT_MAX;
-                k = (pk.y >> 23) & 31u;
-                fl = pk.y >> 28;
-                ce = (fl & FR_OV) ? ov.arena : s.arena;
+                c = bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 31u), C_FL, 4, pk.y >> 28);
                 w.pop();
                 continue;
             }
+            const uint32_t fl = bf(c, C_FL, 4);
             if (!(fl & FR_WV)) {
-                phase = P_EDGE;
+                c = bf_set(c, C_PH, 3, P_EDGE);
                 break;
             }
             const uint32_t e = win_at(win, pos & 3u);
             ++pos;
             --left;
-            if ((pos & 3u) == 0) fl &= ~(uint32_t)FR_WV;
+            if ((pos & 3u) == 0) c &= ~((uint32_t)FR_WV << C_FL);
             w.edge();
+            const uint32_t tval = tset ? (EDGE_SET | T) : T;
             if (e & EDGE_SET) {
                 uint32_t vid = e & EDGE_VAL;
                 if (fl & FR_SEQ) {
-                    const uint32_t c = coll_lookup(s, e);
-                    if (c != NONE32) vid = c;
+                    const uint32_t cv = coll_lookup(s, e);
+                    if (cv != NONE32) vid = cv;
                 }
                 if (fl & FR_TOP) {                                // fresh map per top-level tuple
-                    V.fresh();
+                    V.n = 0;
                     w.item();
                 }
-                const int t = V.test_add(vid, w);
+                const int t = V.test_add(vid, vcol, ta.vtab + (uint64_t)slot * (ta.mask + 1u), ta.mask, w);
                 if (t == 2) res = RES_OVERFLOW;
                 else if (t == 0) {
                     if (tset && e == tval) res = RES_TRUE;        // engine.go:54-57
-                    else if (k >= 2) {                            // remaining depth after the hop >= 1
-                        enter_h = e & EDGE_VAL;
-                        enter_k = k - 1;
-                        enter_fl = 0;
-                        phase = P_HDR;
+                    else if (bf(c, C_K, 5) >= 2) {                // remaining depth after the hop >= 1
+                        eh = e & EDGE_VAL;
+                        c = bf_set(c, C_PH, 3, P_HDR);
                     }
                 }
             } else {                                              // subject id in an ordered row
                 int t = 0;
                 if (!(fl & FR_TOP)) {
-                    const uint32_t c = coll_lookup(s, e);
-                    if (c != NONE32) t = V.test_add(c, w);
+                    const uint32_t cv = coll_lookup(s, e);
+                    if (cv != NONE32) t = V.test_add(cv, vcol, ta.vtab + (uint64_t)slot * (ta.mask + 1u), ta.mask, w);
                 }
                 if (t == 2) res = RES_OVERFLOW;
                 else if (t == 0 && !tset && e == tval) res = RES_TRUE;
             }
         }
         if (res >= 0) {
+            const uint32_t qi = j - 1;
             if (res == RES_OVERFLOW) {
                 const uint32_t at = atomicAdd(ta.out_count, 1u);
                 ta.out_list[at] = qi;
             } else {
                 allowed[qi] = (uint8_t)res;
             }
-            phase = P_REQ;
+            c = bf_set(c, C_PH, 3, P_REQ);
         }
     }
-    ta.slot_epoch[slot] = V.V.epoch;
+    ta.slot_epoch[slot] = V.epoch;
     if constexpr (COUNT) {
         for (int i = 0; i < 13; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
     }
@@ -1229,12 +1267,13 @@ int t0_variant() {
     return v >= 0 && v < T0_VARIANTS ? v : 0;
 }
 CheckKernelFn t0_kernel(int var, bool count) {
+    // <saved frames, save windows, LDS visit ids, register visit ids>
     switch (var) {
-        case 0: return count ? check_wave_kernel<4, false, 16, true> : check_wave_kernel<4, false, 16, false>;
-        case 1: return count ? check_wave_kernel<4, true, 16, true> : check_wave_kernel<4, true, 16, false>;
-        case 2: return count ? check_wave_kernel<4, true, 8, true> : check_wave_kernel<4, true, 8, false>;
-        case 3: return count ? check_wave_kernel<4, false, 8, true> : check_wave_kernel<4, false, 8, false>;
-        default: return count ? check_wave_kernel<8, false, 8, true> : check_wave_kernel<8, false, 8, false>;
+        case 0: return count ? check_wave_kernel<4, false, 8, 16, true> : check_wave_kernel<4, false, 8, 16, false>;
+        case 1: return count ? check_wave_kernel<4, false, 16, 8, true> : check_wave_kernel<4, false, 16, 8, false>;
+        case 2: return count ? check_wave_kernel<4, true, 8, 16, true> : check_wave_kernel<4, true, 8, 16, false>;
+        case 3: return count ? check_wave_kernel<4, false, 8, 8, true> : check_wave_kernel<4, false, 8, 8, false>;
+        default: return count ? check_wave_kernel<8, false, 8, 8, true> : check_wave_kernel<8, false, 8, 8, false>;
     }
 }
 }  // namespace
