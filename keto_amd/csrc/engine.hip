@@ -511,9 +511,9 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
 constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
 constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // saved lkf = left | k << 23 | fl << 28
 constexpr uint16_t FR_WV = 8;                        // the window holds the block of `pos`
-// control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23
+// control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23 | nq2 24
 constexpr uint32_t C_PH = 0, C_K = 3, C_FL = 8, C_SP = 12, C_HL = 19;
-constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18;
+constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18, C_NQ2 = 1u << 24;
 __device__ inline uint32_t bf(uint32_t c, uint32_t off, uint32_t wd) { return (c >> off) & ((1u << wd) - 1u); }
 __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_t v) {
     const uint32_t m = ((1u << wd) - 1u) << off;
@@ -525,40 +525,67 @@ __device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
 }
 __device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
 
-// visited map of a tier-0 lane: registers, then the lane's LDS column, then its HBM table
+// requests j and j + 1 (if in the run) straight into the wave's LDS prefetch slots (global_load_lds:
+// no VGPR destination; lane L's 16 B land at wave_base + 16 L, i.e. lds_nq[tid] and
+// lds_nq[LDS_STRIDE + tid]); retired by the iteration's vmcnt(0)
+__device__ inline void prefetch_pair(const keto_check_ids* q, uint32_t j, uint32_t j_end, uint4* wave_base) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q + j), reinterpret_cast<void*>(wave_base), 16, 0, 0);
+    if (j + 1u < j_end)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q + j + 1u),
+                                         reinterpret_cast<void*>(wave_base + LDS_STRIDE), 16, 0, 0);
+}
+
+// visited map of a tier-0 lane.  A 64-bit filter of hashed ids answers "new" for most tests with
+// no scan; ids are kept newest-first in RV registers (inserting shifts the oldest out), then the
+// lane's LDS column (LV slots), then the lane's HBM table (started fresh on the first overflow).
 template <int RV, int LV>
 struct LaneVisited {
     uint32_t r[RV];
+    uint32_t f0, f1;             // filter bits 0..31, 32..63
     uint32_t n, epoch, count;
+    __device__ inline void fresh() {
+        n = 0;
+        f0 = f1 = 0;
+    }
     template <class W>
     __device__ inline int test_add(uint32_t vid, uint32_t* lds, uint64_t* tab, uint32_t mask, W& w) {
-        const uint32_t m = min(n, (uint32_t)(RV + LV));
-        bool hit = false;
+        const uint32_t b = (vid * 0x9E3779B1u) >> 26;
+        const uint32_t bit = 1u << (b & 31u);
+        const bool maybe = ((b < 32 ? f0 : f1) & bit) != 0;
+        if (maybe) {                                         // the filter cannot rule it out: scan
+            const uint32_t m = min(n, (uint32_t)(RV + LV));
+            bool hit = false;
 #pragma unroll
-        for (int i = 0; i < RV; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
-        for (uint32_t i = RV; i < m && !hit; ++i) hit = lds[(i - RV) * LDS_STRIDE] == vid;
-        if (hit) return 1;
-        if (n < (uint32_t)RV) {
-#pragma unroll
-            for (int i = 0; i < RV; ++i)
-                if ((uint32_t)i == n) r[i] = vid;
-            ++n;
-            return 0;
+            for (int i = 0; i < RV; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
+            for (uint32_t i = RV; i < m && !hit; ++i) hit = lds[(i - RV) * LDS_STRIDE] == vid;
+            if (hit) return 1;
+            if (n > (uint32_t)(RV + LV)) {                   // the rest is in the HBM table
+                Visited H{tab, mask, epoch, count};
+                const int t = H.test_add(vid, w);
+                epoch = H.epoch;
+                count = H.count;
+                return t;
+            }
         }
-        if (n < (uint32_t)(RV + LV)) {
-            lds[(n - RV) * LDS_STRIDE] = vid;
-            ++n;
+        if (b < 32) f0 |= bit;
+        else f1 |= bit;
+        // insert newest-first; the oldest register entry moves out to LDS / HBM
+        const uint32_t out = r[RV - 1];
+#pragma unroll
+        for (int i = RV - 1; i > 0; --i) r[i] = r[i - 1];
+        r[0] = vid;
+        ++n;
+        if (n <= (uint32_t)RV) return 0;
+        if (n <= (uint32_t)(RV + LV)) {
+            lds[(n - 1 - RV) * LDS_STRIDE] = out;
             return 0;
         }
         Visited H{tab, mask, epoch, count};
-        if (n == (uint32_t)(RV + LV)) {                 // first overflow of this map
-            H.fresh();
-            ++n;
-        }
-        const int t = H.test_add(vid, w);
+        if (n == (uint32_t)(RV + LV) + 1u) H.fresh();       // first overflow of this map
+        const int t = H.test_add(out, w);                   // `out` cannot be present yet
         epoch = H.epoch;
         count = H.count;
-        return t;
+        return t == 2 ? 2 : 0;
     }
 };
 
@@ -576,38 +603,59 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
     __shared__ uint2 sf_pk[F * LDS_STRIDE];
     __shared__ uint4 sf_win[(WIN ? F : 1) * LDS_STRIDE];
-    __shared__ uint4 lds_nq[LDS_STRIDE];                       // the lane's prefetched request
+    __shared__ uint4 lds_nq[2 * LDS_STRIDE];                   // the lane's prefetched request pair
     uint32_t* const vcol = lds_vis + tid;
     LaneVisited<RV, LV> V;
-    V.n = 0;
+    V.fresh();
     V.epoch = ta.slot_epoch[slot];
     V.count = 0;
     Work<COUNT> w;
-    // each lane owns a contiguous run of requests, so consecutive fetches share request lines
-    const uint32_t per = (n + stride - 1) / stride;
-    uint32_t j = slot * per;                                   // next request to start
+    // each lane owns a contiguous run of requests (a multiple of 4 long): requests are fetched two
+    // at a time and decisions are stored four at a time
+    const uint32_t per = ((n + stride - 1) / stride + 3u) & ~3u;
+    uint32_t j = min(n, slot * per);                           // next request to start
     const uint32_t j_end = min(n, j + per);
+    const bool packed = ((uintptr_t)allowed & 3u) == 0;
+    uint32_t acc = 0;                                          // decisions of the current group of 4
 
     uint32_t c = P_REQ;                                        // control word
     uint32_t T = 0;                                            // requested subject
     uint32_t pos = 0, left = 0;                                // current frame (k, fl in c)
     uint4 win = make_uint4(0, 0, 0, 0);
     uint32_t eh = 0;                                           // row to enter (P_HDR) / bucket (P_IDQ)
+    // record request qi's decision: whole groups of 4 are stored as one word, a run's partial last
+    // group byte by byte
+    auto decide = [&](uint32_t qi, uint32_t r) {
+        if (!packed || (qi | 3u) >= j_end) {
+            allowed[qi] = (uint8_t)r;
+            return;
+        }
+        acc |= r << ((qi & 3u) * 8u);
+        if ((qi & 3u) == 3u) {
+            *reinterpret_cast<uint32_t*>(allowed + (qi & ~3u)) = acc;
+            acc = 0;
+        }
+    };
     for (;;) {
         // ---- start the next request from its prefetched copy (no iteration spent on fetching it)
         while (bf(c, C_PH, 3) == P_REQ && (c & C_NQ)) {
             const uint4 nq = lds_nq[tid];
             const uint32_t qi = j++;
+            uint32_t keep = 0;                                    // the pair's second request moves up
+            if (c & C_NQ2) {
+                lds_nq[tid] = lds_nq[LDS_STRIDE + tid];
+                keep = C_NQ;
+            }
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
             if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
-                allowed[qi] = 0;
-                c &= ~C_NQ;
+                decide(qi, 0);
+                c = (c & ~(C_NQ | C_NQ2)) | keep;
                 continue;
             }
             T = nq.y;
             eh = nq.x;
-            c = P_HDR | ((uint32_t)d << C_K) | ((nq.z & 1u) ? C_TSET : 0u);   // sp 0, no frame, nq taken
+            c = P_HDR | ((uint32_t)d << C_K) | ((nq.z & 1u) ? C_TSET : 0u) | keep;   // sp 0, no frame
         }
         const uint32_t ph = bf(c, C_PH, 3);
         if (ph == P_REQ && j >= j_end) break;
@@ -615,9 +663,9 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         const uint32_t* const ce = (bf(c, C_FL, 4) & FR_OV) ? ov.arena : s.arena;
         const uint4* a0 = nullptr;
         const uint4* a1 = nullptr;
-        const uint4* a2 = nullptr;
         if (ph == P_REQ) {                                        // not prefetched: fetch it now
-            a0 = reinterpret_cast<const uint4*>(q + j);
+            prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
+            c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
             w.request();
         } else if (ph == P_HDR) {
             const bool is_ov = eh >= ov.base;
@@ -634,23 +682,16 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             a0 = reinterpret_cast<const uint4*>(ce + (pos & ~3u));
             w.edge_at(a0);
         }
-        if (!(c & C_NQ) && ph != P_REQ && j < j_end) {
-            a2 = reinterpret_cast<const uint4*>(q + j);
+        if (!(c & C_NQ) && ph != P_REQ && j < j_end) {            // prefetch the next pair alongside
+            prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
+            c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
             w.request();
         }
-        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
         if (a0) v0 = *a0;
         if (a1) v1 = *a1;
-        if (a2) v2 = *a2;
-        if (a2) {
-            lds_nq[tid] = v2;
-            c |= C_NQ;
-        }
-        if (ph == P_REQ) {
-            lds_nq[tid] = v0;
-            c |= C_NQ;
-            continue;
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // also retires the LDS-direct prefetch
+        if (ph == P_REQ) continue;
         int res = -1;
         const bool tset = (c & C_TSET) != 0;
         if (ph == P_HDR) {
@@ -741,7 +782,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                     if (cv != NONE32) vid = cv;
                 }
                 if (fl & FR_TOP) {                                // fresh map per top-level tuple
-                    V.n = 0;
+                    V.fresh();
                     w.item();
                 }
                 const int t = V.test_add(vid, vcol, ta.vtab + (uint64_t)slot * (ta.mask + 1u), ta.mask, w);
@@ -765,11 +806,12 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         }
         if (res >= 0) {
             const uint32_t qi = j - 1;
-            if (res == RES_OVERFLOW) {
+            if (res == RES_OVERFLOW) {                            // decided by the next tier
                 const uint32_t at = atomicAdd(ta.out_count, 1u);
                 ta.out_list[at] = qi;
+                decide(qi, 0);
             } else {
-                allowed[qi] = (uint8_t)res;
+                decide(qi, (uint32_t)res);
             }
             c = bf_set(c, C_PH, 3, P_REQ);
         }
@@ -1269,8 +1311,8 @@ int t0_variant() {
 CheckKernelFn t0_kernel(int var, bool count) {
     // <saved frames, save windows, LDS visit ids, register visit ids>
     switch (var) {
-        case 0: return count ? check_wave_kernel<4, false, 8, 16, true> : check_wave_kernel<4, false, 8, 16, false>;
-        case 1: return count ? check_wave_kernel<4, false, 16, 8, true> : check_wave_kernel<4, false, 16, 8, false>;
+        case 0: return count ? check_wave_kernel<4, false, 4, 16, true> : check_wave_kernel<4, false, 4, 16, false>;
+        case 1: return count ? check_wave_kernel<4, false, 8, 16, true> : check_wave_kernel<4, false, 8, 16, false>;
         case 2: return count ? check_wave_kernel<4, true, 8, 16, true> : check_wave_kernel<4, true, 8, 16, false>;
         case 3: return count ? check_wave_kernel<4, false, 8, 8, true> : check_wave_kernel<4, false, 8, 8, false>;
         default: return count ? check_wave_kernel<8, false, 8, 8, true> : check_wave_kernel<8, false, 8, 8, false>;
