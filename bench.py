@@ -8,9 +8,13 @@ request with no data-path collective: every rank holds the whole snapshot (the 1
 ~6.4 GB of a 288 GB HBM3E) and checks its own batch ("weak" scaling).  Rank 0 prints one JSON line.
 
 Extras on the same line:
-  roofline      algorithmic bytes of the dominant kernel (tier-0 check_kernel) per launch, from the
-                instrumented work counters of one extra (untimed) pass over the same batch, divided
-                by its average HIP-event duration over the timed steps; peak = 8 TB/s HBM3E.
+  roofline      SURVEY.md 8(d) algorithmic bytes of the dominant kernel (the tier-0 check kernel)
+                per launch -- B_check(q) = 14 + sum over the BFS rows (8 + 4 deg), priced by the
+                oracle's BFS-count mode on a 1 % sample of the batch and scaled -- divided by the
+                kernel's average HIP-event duration over the timed steps (events recorded on the
+                launch stream); peak = 8 TB/s HBM3E.  `traffic` = HBM bytes per launch from the
+                committed rocprofv3 PMC passes of this same engine build (profiles/*_traffic.json);
+                `traversal_bytes_per_launch` = what the kernel's own traversal requests.
   cpu_baseline  the C restatement of the reference engine (oracle/keto_oracle.c) on the box's host
                 cores over a bounded sample of the same requests; its decisions are also compared
                 with the GPU's for that sample ("parity").
@@ -27,6 +31,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def pmc_traffic(kernel_name, workload):
@@ -56,9 +64,11 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale (1.0 = 1B tuples)")
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16, help="host threads (generator, cpu baseline)")
-    ap.add_argument("--cpu-sample", type=int, default=200_000, help="requests in the cpu_baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="requests in the cpu_baseline sample")
+    ap.add_argument("--bytes-sample", type=float, default=0.01,
+                    help="fraction of the batch priced in the oracle's BFS-count mode (roofline bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-work", action="store_true", help="skip the instrumented work-count pass")
+    ap.add_argument("--no-work", action="store_true", help="skip the roofline / cpu_baseline legs (profiling runs)")
     return ap.parse_args()
 
 
@@ -80,9 +90,11 @@ def main():
     from tools import synth
 
     params = synth.scaled(synth.POWERLAW_1B, a.scale) if a.scale != 1.0 else dict(synth.POWERLAW_1B)
+    log(f"rank {rank}/{world}: generating the graph (scale {a.scale})")
     t0 = time.time()
     g = synth.SynthGraph(params, threads=a.threads)
     t_gen = time.time() - t0
+    log(f"rank {rank}: {g.n_edges} tuples, {g.n_rows} rows; building + uploading the snapshot")
     t0 = time.time()
     snap = g.snapshot(device=dev)
     t_snap = time.time() - t0
@@ -96,6 +108,7 @@ def main():
     def step():
         snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
 
+    log(f"rank {rank}: warmup {a.warmup}, timed {a.steps} steps of {a.batch} checks")
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -120,53 +133,69 @@ def main():
     total = world * a.batch * a.steps
     value = total / elapsed
 
-    # ---- roofline of the dominant kernel (tier-0 check_kernel)
+    # ---- roofline of the dominant kernel (tier-0 check kernel)
     tier0_ms = float(np.mean([m[0] for m in tier_ms]))
     tier1_ms = float(np.mean([m[1] for m in tier_ms]))
     overflow = int(np.mean([n[1] for n in tier_n]))
     roofline = None
     work = None
     allowed_rate = float(d_out.float().mean().item())
-    if not a.no_work:
+    gpu_out = d_out.cpu().numpy()
+    cpu = None
+    parity = None
+    if rank == 0 and not a.no_work:
+        # oracle table over a bounded sample of the batch: every tuple those requests can reach
+        ns = min(a.cpu_sample, a.batch)
+        sample = q[:ns]
+        log(f"oracle table over the first {ns} requests")
+        t0 = time.perf_counter()
+        tab = g.oracle_table(sample, a.depth)
+        reqs = g.oracle_requests(tab, sample)
+        t_tab = time.perf_counter() - t0
+        # SURVEY.md 8(d) algorithmic bytes: B_check(q) = 14 + sum over BFS rows (8 + 4 deg), from the
+        # oracle's BFS-count mode on a 1 % sample of the batch, scaled to the launch
+        nb = min(ns, max(1, int(a.batch * a.bytes_sample)))
+        log(f"{tab.t.n} tuples; pricing {nb} requests in BFS-count mode")
+        t0 = time.perf_counter()
+        bq = tab.bfs_bytes_reqs(tab.prefix(reqs, nb), a.depth, threads=a.threads)
+        t_bfs = time.perf_counter() - t0
+        alg = float(bq.mean()) * a.batch
+        achieved = alg / (tier0_ms * 1e-3) / 1e9
+        # bytes the tier-0 kernel's own traversal requests (instrumented pass, same decisions):
+        # 32 B header + window per row visit, 16 B per id-table bucket, 16 B per edge-block reload,
+        # 16 B per request in, 1 B per decision out
         w = snap.check_work_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth)
         rows, edges, idreads, vprobes, vinserts, items = w[:6]
-        # graph bytes the exact traversal must read: 16-B row records, 4-B subject-set edges, 4-B
-        # words of the subject-id membership searches; plus 16-B requests in and 1-B decisions out.
-        # Visited-map state is scratch (registers first, HBM spill) and is not counted.
-        alg = 16 * rows + 4 * edges + 4 * idreads + 17 * a.batch
-        achieved = alg / (tier0_ms * 1e-3) / 1e9
-        kname = "keto::check_kernel<keto::GlobalStack, false, 0> (tier 0)"
+        touched = 32 * w[0] + 16 * w[9] + 16 * w[8] + 17 * a.batch
+        kname = snap.check_kernel_name(a.depth)
         traffic, tsrc = pmc_traffic(kname, {"tuples": int(g.n_edges), "checks_per_gpu_per_step": a.batch,
                                             "max_depth": a.depth, "scale": a.scale})
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else int(traffic),
                     "traffic_GBps": None if traffic is None else round(traffic / (tier0_ms * 1e-3) / 1e9, 1),
-                    "traffic_source": tsrc,
-                    "alg_bytes_per_launch": int(alg), "kernel": kname, "kernel_ms": round(tier0_ms, 3)}
+                    "traffic_source": tsrc, "kernel": kname, "kernel_ms": round(tier0_ms, 3),
+                    "alg_bytes_per_launch": int(alg), "alg_bytes_per_check": round(float(bq.mean()), 1),
+                    "alg_bytes_sample": f"SURVEY 8(d) B_check over the first {nb} requests (oracle BFS-count mode, "
+                                        f"{a.threads} threads, {t_bfs:.1f} s)",
+                    "traversal_bytes_per_launch": int(touched),
+                    "traversal_GBps": round(touched / (tier0_ms * 1e-3) / 1e9, 1)}
         work = {"rows_per_check": rows / a.batch, "set_edges_per_check": edges / a.batch,
                 "id_words_per_check": idreads / a.batch, "visited_hbm_probes_per_check": vprobes / a.batch,
                 "top_level_items_per_check": items / a.batch,
                 "line_touches_per_check": {k: round(v / a.batch, 3) for k, v in zip(
                     ("request", "header", "edge", "id_table", "id_search", "frame_push", "frame_pop"), w[6:13])}}
-
-    # ---- CPU baseline (rank 0, N = 1): oracle restatement on a bounded sample of the same batch
-    cpu = None
-    parity = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        ns = min(a.cpu_sample, a.batch)
-        sample = q[:ns]
-        tab = g.oracle_table(sample, a.depth)
-        reqs = g.oracle_requests(tab, sample)
-        threads = a.threads
-        t0 = time.perf_counter()
-        ref = tab.check_batch_reqs(reqs, a.depth, threads=threads)
-        t_cpu = time.perf_counter() - t0
-        gpu = d_out[:ns].cpu().numpy()
-        parity = {"sample": int(ns), "mismatches": int((ref != gpu).sum())}
-        cpu = {"value": round(ns / t_cpu, 1), "unit": "checks/s", "cores": threads, "kind": "port",
-               "sample": f"first {ns} requests of the rank-0 batch; oracle/keto_oracle.c over the "
-                         f"{tab.t.n} tuples those requests can reach, {threads} host threads, {t_cpu:.2f} s"}
+        # ---- CPU baseline (N = 1): the oracle restatement timed on the sample, decisions compared
+        if world == 1 and not a.no_cpu_baseline:
+            log(f"cpu baseline over {ns} requests, {a.threads} threads")
+            t0 = time.perf_counter()
+            ref = tab.check_batch_reqs(reqs, a.depth, threads=a.threads)
+            t_cpu = time.perf_counter() - t0
+            parity = {"sample": int(ns), "mismatches": int((ref != gpu_out[:ns]).sum())}
+            cpu = {"value": round(ns / t_cpu, 1), "unit": "checks/s", "cores": a.threads, "kind": "port",
+                   "sample": f"first {ns} requests of the rank-0 batch; oracle/keto_oracle.c over the "
+                             f"{tab.t.n} tuples those requests can reach (extracted in {t_tab:.1f} s), "
+                             f"{a.threads} host threads, {t_cpu:.2f} s"}
 
     if rank == 0:
         line = {

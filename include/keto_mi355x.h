@@ -206,6 +206,9 @@ int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
  * out[6..12] are 128-B line touches per access stream (requests, row headers, edges, id tables,
  * id searches, frame pushes, frame pops): an upper bound of the kernel's L2 line traffic. */
 #define KETO_WORK_SLOTS 16
+/* Name of the tier-0 check kernel a batch at this global max-depth launches (as rocprofv3 prints
+ * it, without the argument list), for matching profiles to bench lines.  Static storage. */
+const char* keto_check_kernel_name(int32_t global_max_depth);
 int keto_check_work_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]);
 

@@ -27,6 +27,7 @@ EXPORTS = [
     "keto_check_batch_ids", "keto_check_batch_device", "keto_expand_batch", "keto_tree_arena_free",
     "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
     "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids", "keto_row_handles",
+    "keto_check_kernel_name",
 ]
 
 
@@ -103,6 +104,7 @@ def load():
         if not hasattr(lib, name):
             raise KetoError(f"{LIB_PATH} does not export {name}")
     lib.keto_last_error.restype = C.c_char_p
+    lib.keto_check_kernel_name.restype = C.c_char_p
     lib.keto_tree_count.restype = C.c_uint32
     lib.keto_tree_nodes.restype = C.POINTER(KTreeNode)
     lib.keto_tree_json.restype = C.c_int64
@@ -270,6 +272,11 @@ class Snapshot:
         t = KTiming()
         _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
         return list(t.tier_ms), list(t.requests)
+
+    @staticmethod
+    def check_kernel_name(global_max_depth=5) -> str:
+        """Tier-0 check kernel a batch at this global max-depth launches (profile matching)."""
+        return load().keto_check_kernel_name(C.c_int32(global_max_depth)).decode()
 
     def check_work_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, global_max_depth=5):
         out = (C.c_uint64 * 16)()

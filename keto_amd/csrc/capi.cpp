@@ -328,6 +328,8 @@ int keto_last_batch_timing(const keto_snapshot* h, keto_batch_timing* out) {
     });
 }
 
+const char* keto_check_kernel_name(int32_t global_max_depth) { return device_check_kernel_name(global_max_depth); }
+
 int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]) {
     return guarded([&] {

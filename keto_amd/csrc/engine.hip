@@ -1308,6 +1308,15 @@ int t0_variant() {
     const int v = e ? atoi(e) : 0;
     return v >= 0 && v < T0_VARIANTS ? v : 0;
 }
+const char* t0_kernel_name(int var) {
+    switch (var) {
+        case 0: return "keto::check_wave_kernel<4, false, 4, 16, false>";
+        case 1: return "keto::check_wave_kernel<4, false, 8, 16, false>";
+        case 2: return "keto::check_wave_kernel<4, true, 8, 16, false>";
+        case 3: return "keto::check_wave_kernel<4, false, 8, 8, false>";
+        default: return "keto::check_wave_kernel<8, false, 8, 8, false>";
+    }
+}
 CheckKernelFn t0_kernel(int var, bool count) {
     // <saved frames, save windows, LDS visit ids, register visit ids>
     switch (var) {
@@ -1319,6 +1328,12 @@ CheckKernelFn t0_kernel(int var, bool count) {
     }
 }
 }  // namespace
+
+const char* device_check_kernel_name(int32_t gmd) {
+    const int fr = std::max(1, std::min<int32_t>(gmd, 65535) - 1);
+    if (fr > 8) return "keto::check_kernel<keto::GlobalStack, false, 0>";
+    return t0_kernel_name(fr <= 4 ? t0_variant() : T0_VARIANTS);
+}
 
 void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
                   bool host_buffers, void* stream, const Overlay* ovh, uint64_t* work_out) {

@@ -214,6 +214,7 @@ uint64_t device_bytes(const Snapshot& s);
 void device_check(Snapshot& s, const keto_check_ids* d_or_h_reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
                   bool host_buffers, void* stream, const Overlay* ov, uint64_t* work_out = nullptr);
 keto_batch_timing device_last_timing(const Snapshot& s);
+const char* device_check_kernel_name(int32_t gmd);
 struct ExpandResult {
     std::vector<uint8_t> status;
     std::vector<uint64_t> offset;          // n+1

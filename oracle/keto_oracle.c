@@ -262,6 +262,79 @@ int ora_check_batch(const ora_table* t, const ora_check_req* rq, uint64_t n, int
     return 0;
 }
 
+/* ------------------------------------------------------------------ BFS-count mode (measurement)
+ * Algorithmic bytes of one check as SURVEY.md section 8(d) defines them:
+ *   B_check(q) = 12 + 2 + sum over rows r in Rows(q) of (8 + 4 deg(r))
+ * Rows(q) = the distinct subject-set rows at BFS levels 0 .. L(q)-1 from the request row (one
+ * visited set per request), L(q) = the BFS level of the first tuple equal to the requested subject
+ * (1 .. D), or D if there is none.  deg(r) = tuples in the row.  This is the traffic of a CSR scan
+ * that reads each row it expands in full; bench.py prices its roofline with it. */
+uint64_t ora_bfs_bytes(const ora_table* t, const ora_check_req* rq, int32_t global_max_depth) {
+    int d = rq->max_depth;
+    if (d <= 0 || global_max_depth < d) d = global_max_depth;
+    uint64_t bytes = 14;
+    if (rq->q_ns_unknown) return bytes;
+    vmap V; vm_init(&V);
+    ora_query* cur = (ora_query*)malloc(sizeof(ora_query)); uint64_t nc = 1, capc = 1;
+    cur[0] = rq->q;
+    ora_query* nxt = NULL; uint64_t nn = 0, capn = 0;
+    for (int level = 0; level < d && nc > 0; ++level) {
+        int hit = 0;
+        nn = 0;
+        for (uint64_t x = 0; x < nc; ++x) {
+            rset r; query_rows(t, &cur[x], &r);
+            bytes += 8 + 4 * r.n;
+            for (uint64_t k = 0; k < r.n; ++k) {
+                ora_subject s; subject_of(t, rs_at(&r, k), &s);
+                if (subj_equals(&rq->t, &s)) hit = 1;
+                if (s.kind == 1 && !vm_test_and_add(&V, s.key)) {
+                    ora_query q2;
+                    if (set_query(t, &s, &q2) == 0) {
+                        if (nn == capn) { capn = capn ? 2 * capn : 16; nxt = (ora_query*)realloc(nxt, capn * sizeof(ora_query)); }
+                        nxt[nn++] = q2;
+                    }
+                }
+            }
+            rs_free(&r);
+        }
+        if (hit) break;                                   /* L(q) = level + 1: rows 0 .. level counted */
+        ora_query* tq = cur; cur = nxt; nxt = tq;
+        uint64_t tc = capc; capc = capn; capn = tc;
+        nc = nn;
+    }
+    free(cur); free(nxt); vm_free(&V);
+    return bytes;
+}
+
+typedef struct {
+    const ora_table* t; const ora_check_req* rq; uint64_t n; int32_t g; uint64_t* out;
+    uint64_t* next; pthread_mutex_t* mu;
+} bjob;
+
+static void* bworker(void* p) {
+    bjob* j = (bjob*)p;
+    for (;;) {
+        pthread_mutex_lock(j->mu);
+        uint64_t s = *j->next; *j->next += 64;
+        pthread_mutex_unlock(j->mu);
+        if (s >= j->n) break;
+        uint64_t e = s + 64 < j->n ? s + 64 : j->n;
+        for (uint64_t i = s; i < e; ++i) j->out[i] = ora_bfs_bytes(j->t, &j->rq[i], j->g);
+    }
+    return NULL;
+}
+
+int ora_bfs_bytes_batch(const ora_table* t, const ora_check_req* rq, uint64_t n, int32_t g, uint64_t* out, int n_threads) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256]; bjob jb; uint64_t next = 0; pthread_mutex_t mu; pthread_mutex_init(&mu, NULL);
+    jb.t = t; jb.rq = rq; jb.n = n; jb.g = g; jb.out = out; jb.next = &next; jb.mu = &mu;
+    for (int i = 0; i < n_threads; ++i) pthread_create(&th[i], NULL, bworker, &jb);
+    for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&mu);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ expand */
 typedef struct {                 /* pre-order tree node */
     uint8_t type;                /* 0 union, 1 leaf */

@@ -38,6 +38,8 @@ def lib():
         _lib.ora_check.restype = C.c_int
         _lib.ora_check_batch.restype = C.c_int
         _lib.ora_expand.restype = C.c_int
+        _lib.ora_bfs_bytes.restype = C.c_uint64
+        _lib.ora_bfs_bytes_batch.restype = C.c_int
     return _lib
 
 
@@ -169,12 +171,32 @@ class OracleTable:
         r = self.check_req(tup, max_depth)
         return bool(lib().ora_check(C.byref(self.t), C.byref(r), C.c_int32(global_max_depth)))
 
+    @staticmethod
+    def prefix(reqs, n):
+        """The first n requests of a ctypes request array, as a view (no copy)."""
+        return (OraCheckReq * n).from_address(C.addressof(reqs))
+
+    @staticmethod
+    def _req_array(reqs):
+        if isinstance(reqs, C.Array):
+            return reqs
+        return (OraCheckReq * len(reqs))(*reqs)
+
     def check_batch_reqs(self, reqs, global_max_depth=5, threads=1):
         n = len(reqs)
-        arr = (OraCheckReq * n)(*reqs)
+        arr = self._req_array(reqs)
         out = np.zeros(n, dtype=np.uint8)
         lib().ora_check_batch(C.byref(self.t), arr, C.c_uint64(n), C.c_int32(global_max_depth), _p(out),
                               C.c_int(threads))
+        return out
+
+    def bfs_bytes_reqs(self, reqs, global_max_depth=5, threads=1):
+        """SURVEY.md 8(d) algorithmic bytes of each check (BFS-count mode; measurement only)."""
+        n = len(reqs)
+        arr = self._req_array(reqs)
+        out = np.zeros(n, dtype=np.uint64)
+        lib().ora_bfs_bytes_batch(C.byref(self.t), arr, C.c_uint64(n), C.c_int32(global_max_depth), _p(out),
+                                  C.c_int(threads))
         return out
 
     def expand(self, subject, max_depth, global_max_depth=5):

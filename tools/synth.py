@@ -142,18 +142,17 @@ class SynthGraph:
         return OracleTable(NAMESPACES, arrays, strings, {}, page_size=100)
 
     def oracle_requests(self, tab, q: np.ndarray):
-        """keto_check_ids -> oracle requests (docs:d#view@u, request max-depth kept)."""
+        """keto_check_ids -> oracle requests (docs:d#view@u, request max-depth kept), as one ctypes array."""
         from oracle.oracle_c import OraCheckReq
-        reqs = []
-        for r in q:
-            x = OraCheckReq()
-            x.q.ns = int(self.row_ns[r["row"]])
-            x.q.obj = int(self.row_obj[r["row"]])
-            x.q.rel = int(self.row_rel[r["row"]])
-            x.q_ns_unknown = 0
-            x.t.kind = 0
-            x.t.sid = int(r["target"])
-            x.t.key = int(r["target"])
-            x.max_depth = int(r["max_depth"])
-            reqs.append(x)
-        return reqs
+        arr = (OraCheckReq * len(q))()
+        v = np.frombuffer(arr, dtype=np.dtype(OraCheckReq))
+        rows = q["row"].astype(np.int64)
+        v["q"]["ns"] = self.row_ns[rows]
+        v["q"]["obj"] = self.row_obj[rows]
+        v["q"]["rel"] = self.row_rel[rows]
+        v["q_ns_unknown"] = 0
+        v["t"]["kind"] = 0
+        v["t"]["sid"] = q["target"]
+        v["t"]["key"] = q["target"]
+        v["max_depth"] = q["max_depth"]
+        return arr

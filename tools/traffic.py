@@ -6,8 +6,9 @@ reads (tooling).
 writes <out>_kernel_stats.txt (rocprofv3 --kernel-trace --stats summary of the bench command) and
 <out>_traffic.json (per-launch HBM bytes of the dominant kernel from the FETCH_SIZE / WRITE_SIZE
 PMC passes).  Correction (calibrated with tools/calib.hip on an MI355X, profiles/r01_calib.txt):
-FETCH_SIZE tallies 64 B per L2 miss while a miss moves a 128-B line, for streaming reads and for
-random 4-16 B gathers alike, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 is taken as is.
+FETCH_SIZE tallies 64 B per L2 miss while every miss is a 128-B DRAM read (TCC_EA0_RDREQ_128B =
+TCC_EA0_RDREQ), for streaming reads and for random 4-16 B gathers alike, so read bytes =
+2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 is taken as is.
 The json carries the sha256 of engine.hip, so bench.py only uses it for the kernel it was measured on.
 """
 import collections
@@ -18,7 +19,6 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "check_kernel<keto::GlobalStack, false, 0>"
 
 
 def engine_sha():
@@ -26,7 +26,7 @@ def engine_sha():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc(path, counter, kernel=KERNEL):
+def pmc(path, counter, kernel):
     vals = []
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
@@ -34,7 +34,7 @@ def pmc(path, counter, kernel=KERNEL):
     return sum(vals) / len(vals), len(vals)
 
 
-def stats(path, kernel=KERNEL):
+def stats(path, kernel):
     out, avg = ["kernel | calls | avg_us | total_ms | pct"], None
     for r in csv.DictReader(open(path)):
         out.append(f"{r['Name'][:110]} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
@@ -45,17 +45,19 @@ def stats(path, kernel=KERNEL):
 
 
 def main(src, dst):
-    txt, avg_ms = stats(os.path.join(src, "kt", "kt_kernel_stats.csv"))
-    fetch, nf = pmc(os.path.join(src, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE")
-    write, nw = pmc(os.path.join(src, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE")
+    line = [l for l in open(os.path.join(src, "bench.log")) if l.startswith("{")][-1]
+    bench = json.loads(line)
+    cfg = bench["config"]
+    kernel = bench["roofline"]["kernel"]
+    txt, avg_ms = stats(os.path.join(src, "kt", "kt_kernel_stats.csv"), kernel)
+    fetch, nf = pmc(os.path.join(src, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE", kernel)
+    write, nw = pmc(os.path.join(src, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE", kernel)
     with open(dst + "_kernel_stats.txt", "w") as f:
-        f.write(f"# rocprofv3 --kernel-trace --stats -- python bench.py --no-cpu-baseline  ({src})\n")
+        f.write(f"# rocprofv3 --kernel-trace --stats -- python bench.py --no-work  ({src})\n")
         f.write(txt + "\n")
-    line = [l for l in open(os.path.join(src, "kt.log")) if l.startswith("{")][-1]
-    cfg = json.loads(line)["config"]
     rd = 2.0 * fetch * 1024
     wr = write * 1024
-    j = {"kernel": KERNEL, "engine_sha256": engine_sha(), "launches": [nf, nw],
+    j = {"kernel": kernel, "engine_sha256": engine_sha(), "launches": [nf, nw],
          "workload": {k: cfg[k] for k in ("tuples", "checks_per_gpu_per_step", "max_depth", "scale")},
          "FETCH_SIZE_kb": fetch, "WRITE_SIZE_kb": write, "read_bytes": rd, "write_bytes": wr,
          "traffic_bytes": rd + wr, "kernel_trace_avg_ms": avg_ms,
