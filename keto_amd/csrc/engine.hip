@@ -703,8 +703,15 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 if (sp == F || left > WF_LEFT_MAX) {
                     res = RES_OVERFLOW;
                 } else {
-                    const uint32_t fl = WIN ? bf(c, C_FL, 4) : (bf(c, C_FL, 4) & ~(uint32_t)FR_WV);
-                    sf_pk[sp * LDS_STRIDE + tid] = make_uint2(pos, left | (bf(c, C_K, 5) << 23) | (fl << 28));
+                    const uint32_t fl0 = bf(c, C_FL, 4);
+                    uint32_t fl = fl0, px = pos;
+                    if constexpr (!WIN) {
+                        // one edge left and it is in the window: save the edge itself (WV marks
+                        // it), so the pop needs no reload; otherwise the pop reloads the block
+                        if (left == 1 && (fl0 & FR_WV)) px = win_at(win, pos & 3u);
+                        else fl = fl0 & ~(uint32_t)FR_WV;
+                    }
+                    sf_pk[sp * LDS_STRIDE + tid] = make_uint2(px, left | (bf(c, C_K, 5) << 23) | (fl << 28));
                     if constexpr (WIN) sf_win[sp * LDS_STRIDE + tid] = win;
                     c = bf_set(c, C_SP, 4, sp + 1);
                     w.push();
@@ -757,8 +764,15 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 }
                 --sp;
                 const uint2 pk = sf_pk[sp * LDS_STRIDE + tid];
-                if constexpr (WIN) win = sf_win[sp * LDS_STRIDE + tid];
-                pos = pk.x;
+                if constexpr (WIN) {
+                    win = sf_win[sp * LDS_STRIDE + tid];
+                    pos = pk.x;
+                } else if ((pk.y >> 28) & FR_WV) {               // a saved single edge
+                    win = make_uint4(pk.x, pk.x, pk.x, pk.x);
+                    pos = 0;
+                } else {
+                    pos = pk.x;
+                }
                 left = pk.y & WF_LEFT_MAX;
                 c = bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 31u), C_FL, 4, pk.y >> 28);
                 w.pop();
