@@ -1166,7 +1166,8 @@ void device_upload(Snapshot& S, int device) {
         D->coll_mask = cap - 1;
     }
     D->bytes = acc;
-    D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_units + S.n_coll_keys + 1);
+    // a map holds at most one id per row / collision class (+ an expand root outside the rows)
+    D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     for (auto& e : D->ev) HIP_OK(hipEventCreate(&e));
     S.device = device;
@@ -1382,12 +1383,33 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_kernel(var, false), 256, 0));
+        if (kind == 2)
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_kernel<GlobalStack, false, 0>, 256, 0));
+        else
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_kernel(var, false), 256, 0));
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
         D.v1_lanes[var] = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
         if (getenv("KETO_SLOTS")) D.v1_lanes[var] = (uint32_t)hw_slots();
     }
     p.slots[0] = (uint32_t)std::min<uint64_t>(D.v1_lanes[var], ((uint64_t)n + 255) / 256 * 256);
+    if (kind == 2) {
+        // deep requests (nested groups) visit thousands of sets: give every tier-0 lane a table
+        // of up to 8K ids and tier 1 32K lanes of up to 64K ids, within 1/4 of device memory
+        size_t free_b = 0, total_b = 0;
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        uint64_t held = 0;
+        for (int l = 0; l < 2; ++l) held += (uint64_t)D.tiers[l].n_slots * D.tiers[l].cap * sizeof(uint64_t);
+        const uint64_t budget = std::min<uint64_t>(total_b / 4, (free_b + held) / 2) / 2;
+        const uint32_t full = pow2_at_least(2ull * D.vid_bound + 2);
+        auto fit = [&](uint32_t slots, uint32_t lo, uint32_t hi) {
+            uint32_t c = lo;
+            while (c < hi && (uint64_t)slots * (2ull * c) * sizeof(uint64_t) <= budget) c *= 2;
+            return std::min(c, full);
+        };
+        p.cap[0] = fit(p.slots[0], 256, 8192);
+        p.slots[1] = (uint32_t)std::min<uint64_t>(32768, ((uint64_t)n + 255) / 256 * 256);
+        p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, 65536));
+    }
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
     unsigned long long* dwork = nullptr;

@@ -1,0 +1,209 @@
+"""BASELINE.json configs #1, #2, #3 and #5 on one MI355X (config #4 is bench.py's headline line).
+
+Each config prints one JSON line: GPU throughput with inputs resident in HBM (tier timings from the
+engine's HIP events), the bit-exactness of a sample against the oracle, and the CPU reference
+restatement timed on the same sample and host cores.
+
+  #1 cat-videos: the reference's contrib/cat-videos-example tuples (7), 10,000 seeded checks;
+     CPU: the SQL-level restatement of the reference engine over in-memory SQLite (ref-sql) and
+     the C restatement; GPU: the same 10,000 checks.
+  #2 Drive-like: the power-law docs/folders/groups generator at 10,000,000 tuples, 1,000,000
+     checks, max-depth 5.
+  #3 nested groups: chains of up to 32 nested groups with back-edges (cycles), ~100M tuples,
+     1,000,000 checks with request depths {5, 16, 32}, global max-depth 32.
+  #5 expand: 100,000 roots sampled from #3's rows, global max-depth 5; trees/s for count + fill
+     passes; a sample of trees compared node by node (pre-order, child order included) with the
+     oracle.
+
+  python tools/bench_configs.py [--configs 1,2,3,5] [--threads 16]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def log(msg):
+    print(f"[configs {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def timed_checks(snap, qd, n, gmd, reps=3):
+    import torch
+    d_q = torch.from_numpy(qd.view(np.uint8)).to("cuda:0")
+    d_out = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    sp = torch.cuda.current_stream().cuda_stream
+    w = min(n, 65536)                                        # warm-up: workspaces, code objects
+    snap.check_batch_device(d_q.data_ptr(), w, d_out.data_ptr(), gmd, sp)
+    torch.cuda.synchronize()
+    best, tiers = None, None
+    for r in range(reps):
+        log(f"  timed run {r + 1}/{reps} of {n} checks")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        snap.check_batch_device(d_q.data_ptr(), n, d_out.data_ptr(), gmd, sp)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ms, cnt = snap.last_timing()
+        if best is None or dt < best:
+            best, tiers = dt, (ms, cnt)
+    return best, tiers, d_out.cpu().numpy()
+
+
+def config1(a):
+    from keto_amd.capi import Snapshot
+    from oracle.oracle_sql import CheckEngine, RelationTuple, SQLStore, SubjectID, SubjectSet
+    from tests.engine_util import rows_from_tuples
+    from tests.golden_util import case_namespaces, case_tuples, load_cases
+    case = next(c for c in load_cases() if c["name"] == "contrib/cat-videos-example")
+    ns = case_namespaces(case)
+    tuples = case_tuples(case)
+    rng = np.random.default_rng(1)
+    users = [("id", "*"), ("id", "cat lady"), ("id", "dog guy"), ("set", "videos", "/cats", "owner")]
+    objs = ["/cats", "/cats/1.mp4", "/cats/2.mp4"]
+    rels = ["owner", "view"]
+    reqs = [("videos", objs[rng.integers(3)], rels[rng.integers(2)], users[rng.integers(4)], int(rng.integers(4)))
+            for _ in range(10_000)]
+    store = SQLStore(ns, tuples)
+    eng = CheckEngine(store, 5)
+    t0 = time.perf_counter()
+    ref = []
+    for (n_, o, r, u, d) in reqs:
+        sub = SubjectID(u[1]) if u[0] == "id" else SubjectSet(*u[1:])
+        ref.append(eng.subject_is_allowed(RelationTuple(n_, o, r, sub), d))
+    t_sql = time.perf_counter() - t0
+    snap = Snapshot.build(ns, rows_from_tuples(ns, tuples), device=0)
+    t0 = time.perf_counter()
+    allowed, _ = snap.check_batch(reqs, 5)
+    t_gpu = time.perf_counter() - t0
+    mism = int(sum(bool(x) != y for x, y in zip(allowed, ref)))
+    return {"config": "#1 cat-videos", "tuples": len(tuples), "checks": len(reqs),
+            "ref_sql": {"checks_per_s": round(len(reqs) / t_sql, 1), "cores": 1,
+                        "what": "oracle/oracle_sql.py: the reference engine's recursion issuing its SQL "
+                                "(ORDER BY, LIMIT 100 OFFSET, page count) against in-memory SQLite"},
+            "gpu_host_api": {"checks_per_s": round(len(reqs) / t_gpu, 1),
+                             "what": "keto_check_batch with string requests (resolution + H2D + kernel + D2H)"},
+            "mismatches": mism}
+
+
+def checks_config(a, name, g, q, gmd, sample, reps=3):
+    log(f"{name}: {g.n_edges} tuples; snapshot")
+    snap = g.snapshot(device=0)
+    qd = snap.with_handles(q)
+    n = len(q)
+    dt, (ms, cnt), out = timed_checks(snap, qd, n, gmd, reps)
+    s = q[:sample]
+    log(f"{name}: oracle table over {sample} requests")
+    tab = g.oracle_table(s, gmd)
+    reqs = g.oracle_requests(tab, s)
+    t0 = time.perf_counter()
+    ref = tab.check_batch_reqs(reqs, gmd, threads=a.threads)
+    t_cpu = time.perf_counter() - t0
+    return {"config": name, "tuples": int(g.n_edges), "rows": int(g.n_rows), "checks": n, "global_max_depth": gmd,
+            "gpu": {"checks_per_s": round(n / dt, 1), "wall_ms": round(dt * 1e3, 3),
+                    "tier_ms": [round(x, 3) for x in ms], "tier_requests": [int(x) for x in cnt],
+                    "kernel": snap.check_kernel_name(gmd)},
+            "allowed_fraction": round(float(out.mean()), 4),
+            "parity": {"sample": sample, "mismatches": int((ref != out[:sample]).sum())},
+            "cpu_port": {"checks_per_s": round(sample / t_cpu, 1), "cores": a.threads,
+                         "what": f"oracle/keto_oracle.c over the {tab.t.n} tuples the sample can reach"}}
+
+
+def config2(a):
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 0.01), threads=a.threads)
+    q = g.queries(1_000_000, seed=2, depth=5, threads=a.threads)
+    return checks_config(a, "#2 Drive-like (power-law docs/folders/groups, 10M tuples)", g, q, 5, 200_000)
+
+
+def config3(a):
+    from tools import synth
+    g = synth.SynthGraph(dict(synth.NESTED_100M), threads=a.threads, kind="nested", chain=32)
+    q = g.queries_nested(1_000_000, seed=3, depths=(5, 16, 32), threads=a.threads)
+    return checks_config(a, "#3 nested groups (chains <= 32, cycles)", g, q, 32, 20_000, reps=1), g
+
+
+def config5(a, g=None):
+    from tools import synth
+    from keto_amd.capi import load
+    if g is None:
+        g = synth.SynthGraph(dict(synth.NESTED_100M), threads=a.threads, kind="nested", chain=32)
+    snap = g.snapshot(device=0)
+    rng = np.random.default_rng(5)
+    n = 100_000
+    rows = rng.integers(0, g.n_rows, size=n).astype(np.uint32)
+    roots = rows | np.uint32(0x80000000)
+    depths = np.zeros(n, dtype=np.int32)          # request depth 0 -> global max-depth 5
+    lib = load()
+    best = None
+    for _ in range(3):
+        arena = C.c_void_p()
+        t0 = time.perf_counter()
+        rc = lib.keto_expand_batch_ids(snap.h, roots.ctypes.data_as(C.c_void_p), depths.ctypes.data_as(C.c_void_p),
+                                       C.c_uint32(n), C.c_int32(5), C.byref(arena))
+        dt = time.perf_counter() - t0
+        assert rc == 0
+        lib.keto_tree_arena_free(arena)
+        best = dt if best is None else min(best, dt)
+    # node-by-node comparison of a sample of trees with the oracle
+    from tests.test_gpu_synth import _oracle_expand_nodes
+    k = 300
+    status, offs, nodes = snap.expand_batch_ids(roots[:k], depths[:k], 5)
+    q = np.zeros(k, dtype=[("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
+    q["row"] = rows[:k]
+    tab = g.oracle_table(q, 5)
+    bad = 0
+    n_nodes = 0
+    for i in range(k):
+        r, want = _oracle_expand_nodes(g, tab, int(rows[i]), 5, 5)
+        if r == 0:
+            bad += int(status[i] != 1)
+            continue
+        have = []
+        for subj, info in nodes[offs[i]:offs[i + 1]]:
+            leaf, nc = int(info >> 31), int(info & 0x7FFFFFFF)
+            if subj >> 31:
+                t = int(subj & 0x7FFFFFFF)
+                have.append((leaf, 1, 0, 0xFFFF0000 + int(g.row_ns[t]), int(g.row_obj[t]), int(g.row_rel[t]), nc))
+            else:
+                have.append((leaf, 0, int(subj), 0, 0, 0, nc))
+        n_nodes += len(have)
+        bad += int(have != want or status[i] != 0)
+    return {"config": "#5 expand (100k roots on the #3 graph, max-depth 5)", "tuples": int(g.n_edges), "roots": n,
+            "gpu": {"trees_per_s": round(n / best, 1), "wall_ms": round(best * 1e3, 3),
+                    "what": "keto_expand_batch_ids: H2D roots, count pass, host scan, fill pass, D2H tree arena"},
+            "parity": {"sample_trees": k, "sample_nodes": n_nodes, "mismatched_trees": bad}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,2,3,5")
+    ap.add_argument("--threads", type=int, default=16)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    want = set(a.configs.split(","))
+    g3 = None
+    if "1" in want:
+        log("config #1")
+        print(json.dumps(config1(a)), flush=True)
+    if "2" in want:
+        log("config #2")
+        print(json.dumps(config2(a)), flush=True)
+    if "3" in want:
+        log("config #3")
+        r, g3 = config3(a)
+        print(json.dumps(r), flush=True)
+    if "5" in want:
+        log("config #5")
+        print(json.dumps(config5(a, g3)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
