@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16, help="host threads (generator, cpu baseline)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="requests in the cpu_baseline sample")
+    ap.add_argument("--sql-sample", type=int, default=300, help="requests in the ref_sql (SQLite) sample")
     ap.add_argument("--bytes-sample", type=float, default=0.01,
                     help="fraction of the batch priced in the oracle's BFS-count mode (roofline bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -143,6 +144,7 @@ def main():
     gpu_out = d_out.cpu().numpy()
     cpu = None
     parity = None
+    ref_sql = None
     if rank == 0 and not a.no_work:
         # oracle table over a bounded sample of the batch: every tuple those requests can reach
         ns = min(a.cpu_sample, a.batch)
@@ -196,6 +198,25 @@ def main():
                    "sample": f"first {ns} requests of the rank-0 batch; oracle/keto_oracle.c over the "
                              f"{tab.t.n} tuples those requests can reach (extracted in {t_tab:.1f} s), "
                              f"{a.threads} host threads, {t_cpu:.2f} s"}
+            # the reference engine's algorithm issuing its own SQL against in-memory SQLite
+            # (oracle/oracle_sql.py), one core, on a small sample
+            if a.sql_sample > 0:
+                from oracle.oracle_sql import CheckEngine
+                k = min(a.sql_sample, ns)
+                log(f"ref_sql over {k} requests (SQLite, 1 core)")
+                stab = g.oracle_table(q[:k], a.depth)
+                store = g.sql_store(stab)
+                eng = CheckEngine(store, a.depth)
+                rq = g.sql_requests(q[:k])
+                t0 = time.perf_counter()
+                sql = np.array([eng.subject_is_allowed(r, d) for r, d in rq], dtype=np.uint8)
+                t_sql = time.perf_counter() - t0
+                ref_sql = {"value": round(k / t_sql, 1), "unit": "checks/s", "cores": 1,
+                           "mismatches_vs_gpu": int((sql != gpu_out[:k]).sum()),
+                           "sample": f"first {k} requests; oracle/oracle_sql.py (the reference check engine's "
+                                     f"recursion issuing its SELECT ... ORDER BY ... LIMIT 100 OFFSET and page "
+                                     f"count per node) over the {stab.t.n} tuples they reach in in-memory "
+                                     f"SQLite, {t_sql:.2f} s"}
 
     if rank == 0:
         line = {
@@ -210,6 +231,7 @@ def main():
                        "scale": a.scale},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "ref_sql": ref_sql,
             "parity": parity,
             "detail": {"tier0_ms": round(tier0_ms, 3), "tier1_ms": round(tier1_ms, 3),
                        "tier0_overflow_requests": overflow, "allowed_fraction": round(allowed_rate, 4),

@@ -253,13 +253,30 @@ uint32_t Snapshot::row_hlog2(uint32_t r) const {
 void compute_layout(Snapshot& S) {
     const uint32_t R = S.n_rows();
     S.unit_of_row.resize(R);
+    // Hot rows first: rows that many subject sets point at (popular folders, groups) are laid out
+    // densely at the front of the arena, most-referenced first, so the lines most traversals touch
+    // stay in L2 and the Infinity Cache.  A stable counting sort by floor(log2(in-degree)).
+    std::vector<uint8_t> band(R, 0);
+    {
+        std::vector<uint32_t> indeg(R, 0);
+        for (uint32_t e : S.edges)
+            if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
+        for (uint32_t r = 0; r < R; ++r) band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
+    }
+    std::vector<uint64_t> start(35, 0);                  // key = 33 - band: hottest first
+    for (uint32_t r = 0; r < R; ++r) ++start[33 - band[r] + 1];
+    for (int b = 1; b < 35; ++b) start[b] += start[b - 1];
+    S.rows_by_unit.assign(R, 0);
+    for (uint32_t r = 0; r < R; ++r) S.rows_by_unit[start[33 - band[r]]++] = r;
+    S.layout_units.assign(R, 0);
     uint64_t w = 0;
-    for (uint32_t r = 0; r < R; ++r) {
+    for (uint32_t x = 0; x < R; ++x) {
+        const uint32_t r = S.rows_by_unit[x];
         const uint32_t h = S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
         const uint64_t n = row_end_of(S, r) - S.row_begin(r);
-        // line placement: a row that fits one 128-B line gets one line to itself (header, window
-        // and id table come in with one miss); a bigger row keeps header + window in one line
+        // line placement: a row that fits in a 128-B line never straddles one (header, window and
+        // id table come in with one miss); a bigger row keeps header + window in one line
         const uint64_t total = table + HDR_WORDS + ((n + 3) & ~3ull);
         if (total <= LINE_WORDS) {
             if (w % LINE_WORDS + total > LINE_WORDS) w = (w + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
@@ -269,15 +286,16 @@ void compute_layout(Snapshot& S) {
         const uint64_t unit = (w + table) / HDR_WORDS;
         if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
         S.unit_of_row[r] = (uint32_t)unit;
+        S.layout_units[x] = (uint32_t)unit;
         w += table + HDR_WORDS + ((n + 3) & ~3ull);
     }
     S.n_units = w / HDR_WORDS;
 }
 
 int64_t Snapshot::row_of_handle(uint32_t unit) const {
-    auto it = std::lower_bound(unit_of_row.begin(), unit_of_row.end(), unit);
-    if (it == unit_of_row.end() || *it != unit) return -1;
-    return it - unit_of_row.begin();
+    auto it = std::lower_bound(layout_units.begin(), layout_units.end(), unit);   // increasing
+    if (it == layout_units.end() || *it != unit) return -1;
+    return rows_by_unit[it - layout_units.begin()];
 }
 
 uint32_t handle_of(const Snapshot& S, const Overlay* ov, uint32_t row) {

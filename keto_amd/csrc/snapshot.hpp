@@ -137,6 +137,8 @@ struct Snapshot {
 
     // ---- device arena layout (compute_layout): handle of each row, total arena units (16 B)
     std::vector<uint32_t> unit_of_row;
+    std::vector<uint32_t> rows_by_unit;   // rows in arena order (most-referenced first)
+    std::vector<uint32_t> layout_units;   // their units, increasing
     uint64_t n_units = 0;
     uint32_t handle(uint32_t row) const { return unit_of_row[row]; }
     int64_t row_of_handle(uint32_t unit) const;   // -1 if not a row header

@@ -141,6 +141,33 @@ class SynthGraph:
         strings = {"": 0xFFFFFFF0, "docs": 0xFFFF0001, "folders": 0xFFFF0002, "groups": 0xFFFF0003}
         return OracleTable(NAMESPACES, arrays, strings, {}, page_size=100)
 
+    def sql_store(self, tab):
+        """The oracle table's tuples in an in-memory SQLite store with the reference schema
+        (oracle/oracle_sql.py's SQLStore; strings are the ids as 8-digit hex, so byte order = id order)."""
+        from oracle.oracle_sql import SQLStore, _NID
+        st = SQLStore(NAMESPACES)
+        n = tab.t.n
+        a = tab.arr
+        hx = lambda v: f"{int(v):08x}"
+        rows = []
+        for i in range(n):
+            if a["kind"][i]:
+                rows.append((f"s{i}", _NID, int(a["ns"][i]), hx(a["obj"][i]), hx(a["rel"][i]), None,
+                             int(a["sns"][i]), hx(a["sobj"][i]), hx(a["srel"][i]), i))
+            else:
+                rows.append((f"s{i}", _NID, int(a["ns"][i]), hx(a["obj"][i]), hx(a["rel"][i]), hx(a["sid"][i]),
+                             None, None, None, i))
+        st.conn.executemany("INSERT INTO keto_relation_tuples VALUES (?,?,?,?,?,?,?,?,?,?)", rows)
+        return st
+
+    def sql_requests(self, q: np.ndarray):
+        """keto_check_ids -> (RelationTuple, request max-depth) for oracle_sql.CheckEngine."""
+        from oracle.oracle_sql import RelationTuple, SubjectID
+        names = dict(NAMESPACES)
+        return [(RelationTuple(names[int(self.row_ns[r["row"]])], f"{int(self.row_obj[r['row']]):08x}",
+                               f"{int(self.row_rel[r['row']]):08x}", SubjectID(f"{int(r['target']):08x}")),
+                 int(r["max_depth"])) for r in q]
+
     def oracle_requests(self, tab, q: np.ndarray):
         """keto_check_ids -> oracle requests (docs:d#view@u, request max-depth kept), as one ctypes array."""
         from oracle.oracle_c import OraCheckReq
