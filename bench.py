@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--bytes-sample", type=float, default=0.01,
                     help="fraction of the batch priced in the oracle's BFS-count mode (roofline bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--partitioned", action="store_true",
+                    help="edge-partitioned snapshot (root rows split by hash(ns, object)); each step routes the "
+                         "batch to the owners with RCCL all-to-all, checks, and returns the decisions")
     ap.add_argument("--no-work", action="store_true", help="skip the roofline / cpu_baseline legs (profiling runs)")
     return ap.parse_args()
 
@@ -97,17 +100,32 @@ def main():
     t_gen = time.time() - t0
     log(f"rank {rank}: {g.n_edges} tuples, {g.n_rows} rows; building + uploading the snapshot")
     t0 = time.time()
-    snap = g.snapshot(device=dev)
+    snap = g.snapshot_part(rank, world, dev) if a.partitioned else g.snapshot(device=dev)
     t_snap = time.time() - t0
     q = g.queries(a.batch, seed=1000 + rank, depth=a.depth, threads=a.threads)
-    qd = snap.with_handles(q)            # request resolution (row ids -> row handles), untimed
-    d_q = torch.from_numpy(qd.view(np.uint8)).to(f"cuda:{dev}")
     d_out = torch.empty(a.batch, dtype=torch.uint8, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
+    if a.partitioned:
+        from keto_amd.multi import route_device, send_back
+        # requests travel as row ids; the owner table routes them (root rows to their part)
+        d_q = torch.from_numpy(q.view(np.int32).reshape(-1, 4).copy()).to(f"cuda:{dev}")
+        owner_dev = torch.from_numpy(snap.row_owner(np.arange(g.n_rows, dtype=np.uint32), world).astype(np.int16)
+                                     ).to(f"cuda:{dev}")
+        routed = [0]
 
-    def step():
-        snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
+        def step():
+            recv, state = route_device(d_q, owner_dev, rank, world)
+            dec = torch.empty(len(recv), dtype=torch.uint8, device=d_q.device)
+            snap.check_batch_rows_device(recv.data_ptr(), len(recv), dec.data_ptr(), a.depth, sp)
+            send_back(dec, state, d_out, world)
+            routed[0] = len(recv)
+    else:
+        qd = snap.with_handles(q)        # request resolution (row ids -> row handles), untimed
+        d_q = torch.from_numpy(qd.view(np.uint8)).to(f"cuda:{dev}")
+
+        def step():
+            snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
 
     log(f"rank {rank}: warmup {a.warmup}, timed {a.steps} steps of {a.batch} checks")
     for _ in range(a.warmup):
@@ -166,7 +184,10 @@ def main():
         # bytes the tier-0 kernel's own traversal requests (instrumented pass, same decisions):
         # 32 B header + window per row visit, 16 B per id-table bucket, 16 B per edge-block reload,
         # 16 B per request in, 1 B per decision out
-        w = snap.check_work_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth)
+        if a.partitioned:                # the instrumented pass takes handle-form requests
+            w = [0] * 16
+        else:
+            w = snap.check_work_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth)
         rows, edges, idreads, vprobes, vinserts, items = w[:6]
         touched = 32 * w[0] + 16 * w[9] + 16 * w[8] + 17 * a.batch
         kname = snap.check_kernel_name(a.depth)
@@ -224,10 +245,12 @@ def main():
             "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": "powerlaw-acl-1B (BASELINE config #4) on one GPU per rank, replicated snapshot",
+            "config": {"workload": "powerlaw-acl-1B (BASELINE config #4) on one GPU per rank, " +
+                                   ("edge-partitioned snapshot, requests routed by all-to-all" if a.partitioned
+                                    else "replicated snapshot"),
                        "tuples": int(g.n_edges), "set_edge_fraction": round(g.n_set_edges / max(1, g.n_edges), 4),
                        "rows": int(g.n_rows), "checks_per_gpu_per_step": a.batch, "max_depth": a.depth,
-                       "global_batch": a.batch * world, "parallelism": f"replicated-dp{world}",
+                       "global_batch": a.batch * world, "parallelism": f"partitioned-{world}" if a.partitioned else f"replicated-dp{world}",
                        "scale": a.scale},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -167,6 +167,24 @@ int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespac
                            uint32_t n_strings, const keto_snapshot_opts* opts, keto_snapshot** out);
 
 void keto_snapshot_release(keto_snapshot* s);
+
+/* Edge-partitioned upload, for graphs larger than one GPU (one process per GPU, n_parts parts).
+ * Takes a host-only snapshot (built with device = -1) and uploads to `device` only
+ *   - every row that is the target of some subject set (these are kept on all parts), and
+ *   - the root rows (rows no subject set points at) whose hash(namespace_id, object) % n_parts
+ *     == part.
+ * A check or expand whose top-level row is a root row must run on the part keto_row_owner names
+ * (requests are routed with one all-to-all; see keto_amd/multi.py); the traversal below the top
+ * level only visits rows every part holds, so each part answers exactly.  Calls naming another
+ * part's root row fail with KETO_E_INVALID.  Replaces nothing in the reference. */
+int keto_snapshot_upload_part(keto_snapshot* s, uint32_t part, uint32_t n_parts, int32_t device);
+/* keto_check_batch_device on requests that name rows by row id (row and subject-set target), the
+ * form requests travel in between parts: each is translated to this device's handles first.  A
+ * request for another part's root row fails the call with KETO_E_INVALID. */
+int keto_check_batch_rows_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                                 uint8_t* d_allowed_out, void* stream);
+/* Owner part of each row id for n_parts parts: -1 = a row every part holds (route anywhere). */
+int keto_row_owner(const keto_snapshot* s, const uint32_t* rows, uint64_t n, uint32_t n_parts, int32_t* out);
 int keto_snapshot_get_stats(const keto_snapshot* s, keto_snapshot_stats* out);
 
 /* Row ids (snapshot row order; KETO_NO_ROW passes through) -> row handles for keto_check_ids. */

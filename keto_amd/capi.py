@@ -27,7 +27,7 @@ EXPORTS = [
     "keto_check_batch_ids", "keto_check_batch_device", "keto_expand_batch", "keto_tree_arena_free",
     "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
     "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids", "keto_row_handles",
-    "keto_check_kernel_name",
+    "keto_check_kernel_name", "keto_snapshot_upload_part", "keto_row_owner", "keto_check_batch_rows_device",
 ]
 
 
@@ -182,6 +182,19 @@ class Snapshot:
         _check(lib.keto_snapshot_build(ns, len(namespaces), tt, C.c_uint64(len(rows)), C.byref(opts), C.byref(h)))
         return cls(h, lib)
 
+    def upload_part(self, part: int, n_parts: int, device: int = 0):
+        """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part)."""
+        _check(self.lib.keto_snapshot_upload_part(self.h, C.c_uint32(part), C.c_uint32(n_parts), C.c_int32(device)))
+        return self
+
+    def row_owner(self, rows: np.ndarray, n_parts: int) -> np.ndarray:
+        """Owner part of each row id (-1: held by every part)."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        out = np.empty(len(rows), dtype=np.int32)
+        _check(self.lib.keto_row_owner(self.h, rows.ctypes.data_as(C.c_void_p), C.c_uint64(len(rows)),
+                                       C.c_uint32(n_parts), out.ctypes.data_as(C.c_void_p)))
+        return out
+
     @classmethod
     def from_csr(cls, namespaces, row_ns, row_obj, row_rel, row_ptr, edges, strings=None, page_size=100, device=0):
         lib = load()
@@ -267,6 +280,12 @@ class Snapshot:
         _check(self.lib.keto_check_batch_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
                                                 C.c_int32(global_max_depth), C.c_void_p(d_out_ptr),
                                                 C.c_void_p(stream)))
+
+    def check_batch_rows_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, global_max_depth=5, stream=0):
+        """Device-resident requests naming rows by row id (partitioned mode)."""
+        _check(self.lib.keto_check_batch_rows_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
+                                                     C.c_int32(global_max_depth), C.c_void_p(d_out_ptr),
+                                                     C.c_void_p(stream)))
 
     def last_timing(self):
         t = KTiming()

@@ -177,7 +177,12 @@ keto_check_ids resolve_one(const Snapshot& S, const keto_check_req& q, uint8_t& 
     int64_t row = S.resolve_query(sv(q.namespace_), sv(q.object), sv(q.relation), &wkey);
     if (row == -2) status = KETO_CHECK_UNKNOWN_NAMESPACE;
     else if (row == -3) wild = true;
-    else if (row >= 0) r.row = S.handle((uint32_t)row);
+    else if (row >= 0) {
+        if (!S.present((uint32_t)row))
+            throw Error{KETO_E_INVALID, "the request's row is a root row owned by part " +
+                                            std::to_string(S.root_owner((uint32_t)row, S.n_parts)) + " (keto_row_owner)"};
+        r.row = S.handle((uint32_t)row);
+    }
     if (q.subject.kind == 0) {
         int64_t sid = S.lookup_str(sv(q.subject.id));
         if (sid >= 0) r.target = (uint32_t)sid;
@@ -314,6 +319,7 @@ int keto_row_handles(const keto_snapshot* h, const uint32_t* rows, uint64_t n, u
         for (uint64_t i = 0; i < n; ++i) {
             if (rows[i] == KETO_NO_ROW) { out[i] = KETO_NO_ROW; continue; }
             if (rows[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "row id out of range"};
+            if (!S.present(rows[i])) throw Error{KETO_E_INVALID, "row " + std::to_string(rows[i]) + " is owned by another part"};
             out[i] = S.handle(rows[i]);
         }
         return KETO_OK;
@@ -329,6 +335,42 @@ int keto_last_batch_timing(const keto_snapshot* h, keto_batch_timing* out) {
 }
 
 const char* keto_check_kernel_name(int32_t global_max_depth) { return device_check_kernel_name(global_max_depth); }
+
+int keto_check_batch_rows_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                                 uint8_t* d_allowed_out, void* stream) {
+    return guarded([&] {
+        if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_check_rows(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream);
+        return KETO_OK;
+    });
+}
+
+int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device) {
+    return guarded([&] {
+        if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        Snapshot& S = *h->s;
+        if (S.dev) throw Error{KETO_E_INVALID, "snapshot is already on a device (build it with device = -1)"};
+        if (n_parts == 0 || part >= n_parts) throw Error{KETO_E_INVALID, "bad part"};
+        S.part = part;
+        S.n_parts = n_parts;
+        compute_layout(S);
+        device_upload(S, device);
+        return KETO_OK;
+    });
+}
+
+int keto_row_owner(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t n_parts, int32_t* out) {
+    return guarded([&] {
+        if (!h || (n && (!rows || !out)) || n_parts == 0) throw Error{KETO_E_INVALID, "bad argument"};
+        const Snapshot& S = *h->s;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (rows[i] == KETO_NO_ROW) { out[i] = -1; continue; }
+            if (rows[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "row id out of range"};
+            out[i] = S.is_root[rows[i]] ? (int32_t)S.root_owner(rows[i], n_parts) : -1;
+        }
+        return KETO_OK;
+    });
+}
 
 int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]) {
@@ -380,6 +422,7 @@ int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n,
                                   std::string(sv(sj.set_relation));
                 vid[i] = S.vid_of_key(key);
             } else {
+                if (!S.present((uint32_t)r)) throw Error{KETO_E_INVALID, "expand root is owned by another part"};
                 root[i] = S.handle((uint32_t)r);
                 vid[i] = S.vid_of_row((uint32_t)r);
             }
@@ -409,6 +452,7 @@ int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t
             flags[i] = set ? 1u : 0u;
             if (set) {
                 if (root[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "root row out of range"};
+                if (!S.present(root[i])) throw Error{KETO_E_INVALID, "expand root is owned by another part"};
                 vid[i] = S.vid_of_row(root[i]);
                 root[i] = S.handle(root[i]);
             }

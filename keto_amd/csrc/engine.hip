@@ -124,6 +124,7 @@ struct Work {
     __device__ inline void id_at(const void*, bool) {}
     __device__ inline void push() {}
     __device__ inline void pop() {}
+    __device__ inline void leaf(bool, uint32_t) {}
 };
 template <>
 struct Work<true> {
@@ -155,6 +156,15 @@ struct Work<true> {
     }
     __device__ inline void push() { ++c[11]; }
     __device__ inline void pop() { ++c[12]; }
+    // 13 leaf rows entered (no subject sets), 14 of them without the requested id, 15 of those
+    // with <= 8 ids
+    __device__ inline void leaf(bool miss, uint32_t n_ids) {
+        ++c[13];
+        if (miss) {
+            ++c[14];
+            if (n_ids <= 8) ++c[15];
+        }
+    }
 };
 // Is subject id t in the row's (effective) id region?
 template <class W>
@@ -524,6 +534,9 @@ __device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
     return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
 }
 __device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
+__device__ inline const uint32_t* ce0(const DevSnap& s, const DevOverlay& ov, uint32_t h) {
+    return h >= ov.base ? ov.arena : s.arena;
+}
 
 // requests j and j + 1 (if in the run) straight into the wave's LDS prefetch slots (global_load_lds:
 // no VGPR destination; lane L's 16 B land at wave_base + 16 L, i.e. lds_nq[tid] and
@@ -728,6 +741,23 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 win = v1;
                 c = bf_set(bf_set(bf_set(bf_set(c, C_K, 5, k), C_FL, 4, fl), C_HL, 5, hl), C_PH, 3, P_WALK) | C_HAVE;
                 const uint32_t n_sets = v0.x, n_ids = v0.y;
+                if constexpr (COUNT) {
+                    if (!seq && n_sets == 0 && !tset) {
+                        bool in = false;
+                        if (hl == 0) {
+                            for (uint32_t i = 0; i < WINDOW_WORDS; ++i) in |= (i < n_ids) & (win_at(win, i) == T);
+                        } else {
+                            const uint32_t nb = (1u << hl) / BUCKET_WORDS;
+                            const uint32_t* tab = ce0(s, ov, eh) + pos - HDR_WORDS - (1u << hl);
+                            for (uint32_t b = mix32(T) & (nb - 1);; b = (b + 1) & (nb - 1)) {
+                                const uint4 v = *reinterpret_cast<const uint4*>(tab + b * BUCKET_WORDS);
+                                if (has4(v, T)) { in = true; break; }
+                                if (has4(v, NONE32)) break;
+                            }
+                        }
+                        w.leaf(!in, n_ids);
+                    }
+                }
                 if (!seq && !tset && n_ids > 0) {                 // is the requested id in the row?
                     if (hl == 0) {                                // all ids are in the window
                         bool hit = false;
@@ -832,7 +862,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     }
     ta.slot_epoch[slot] = V.epoch;
     if constexpr (COUNT) {
-        for (int i = 0; i < 13; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
+        for (int i = 0; i < 16; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
     }
 }
 
@@ -986,6 +1016,9 @@ struct DeviceState {
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
     keto_batch_timing last{};
+    uint32_t* row_handle = nullptr;   // row id -> handle (NO_UNIT: another part's root row), lazily
+    keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
+    uint64_t xlate_cap = 0;
 
     DevSnap view() const { return DevSnap{arena, coll, coll_mask}; }
 };
@@ -1143,6 +1176,7 @@ void device_upload(Snapshot& S, int device) {
     std::vector<uint32_t> arena(std::max<uint64_t>(words, 4));
     const uint32_t R = S.n_rows();
     host_parallel_for(R, [&](uint64_t r) {
+        if (!S.present((uint32_t)r)) return;                 // another part's root row
         const uint64_t b = S.row_begin((uint32_t)r);
         const uint64_t e = r + 1 < R ? S.row_begin((uint32_t)r + 1) : S.edges.size();
         put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), S.edges.data() + b,
@@ -1155,7 +1189,10 @@ void device_upload(Snapshot& S, int device) {
         std::vector<uint64_t> tab(cap, ~0ull);
         for (auto& kv : S.coll) {
             uint32_t key = kv.first;
-            if (key & EDGE_SET) key = EDGE_SET | S.unit_of_row[key & EDGE_VAL];   // row -> handle
+            if (key & EDGE_SET) {
+                if (!S.present(key & EDGE_VAL)) continue;    // another part's root row
+                key = EDGE_SET | S.unit_of_row[key & EDGE_VAL];   // row -> handle
+            }
             uint32_t vid = kv.second;
             uint32_t i = mix32(key) & (cap - 1);
             while (tab[i] != ~0ull) i = (i + 1) & (cap - 1);
@@ -1184,6 +1221,8 @@ void device_release(Snapshot& S) {
     if (D.coll) (void)hipFree(D.coll);
     if (D.lists) (void)hipFree(D.lists);
     if (D.counters) (void)hipFree(D.counters);
+    if (D.row_handle) (void)hipFree(D.row_handle);
+    if (D.xlate) (void)hipFree(D.xlate);
     if (D.stream) (void)hipStreamDestroy(D.stream);
     for (auto& e : D.ev)
         if (e) (void)hipEventDestroy(e);
@@ -1449,6 +1488,62 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
         HIP_OK(hipMemcpyAsync(allowed, da, n, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
     }
+}
+
+// Requests naming rows by row id (as they travel between parts) -> row handles of this device.
+// A top-level row another part owns becomes KETO_NO_ROW and is counted in *misrouted; a subject-set
+// target that is another part's root row becomes KETO_NO_TARGET (no tuple has it as subject, so
+// the reference answers false for it too).
+__global__ void __launch_bounds__(256) rows_to_handles(const keto_check_ids* __restrict__ in, keto_check_ids* __restrict__ out,
+                                                       uint32_t n, const uint32_t* __restrict__ table, uint32_t n_rows,
+                                                       uint32_t* misrouted) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keto_check_ids q = in[i];
+    if (q.row != KETO_NO_ROW) {
+        const uint32_t h = q.row < n_rows ? table[q.row] : NO_UNIT;
+        if (h == NO_UNIT) atomicAdd(misrouted, 1u);
+        q.row = h == NO_UNIT ? KETO_NO_ROW : h;
+    }
+    if ((q.flags & 1u) && q.target != KETO_NO_TARGET) {
+        const uint32_t h = q.target < n_rows ? table[q.target] : NO_UNIT;
+        q.target = h == NO_UNIT ? KETO_NO_TARGET : h;
+    }
+    out[i] = q;
+}
+
+void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
+                       void* stream) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    hipStream_t st = stream ? (hipStream_t)stream : D.stream;
+    {
+        std::lock_guard<std::mutex> lk(D.mu);
+        HIP_OK(hipSetDevice(D.device));
+        uint64_t acc = 0;
+        if (!D.row_handle) {
+            D.row_handle = dmalloc<uint32_t>(S.n_rows(), acc);
+            HIP_OK(hipMemcpy(D.row_handle, S.unit_of_row.data(), (uint64_t)S.n_rows() * sizeof(uint32_t),
+                             hipMemcpyHostToDevice));
+        }
+        if (D.xlate_cap < n) {
+            if (D.xlate) (void)hipFree(D.xlate);
+            D.xlate_cap = std::max<uint64_t>(n, 1024);
+            D.xlate = dmalloc<keto_check_ids>(D.xlate_cap, acc);
+        }
+        ensure_lists(D, n);
+        HIP_OK(hipMemsetAsync(D.counters + 2, 0, sizeof(uint32_t), st));
+        if (n) {
+            hipLaunchKernelGGL(rows_to_handles, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, D.xlate, n,
+                               D.row_handle, S.n_rows(), D.counters + 2);
+            HIP_OK(hipGetLastError());
+        }
+        uint32_t bad = 0;
+        HIP_OK(hipMemcpyAsync(&bad, D.counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
+    }
+    device_check(S, D.xlate, n, gmd, d_allowed, false, stream, nullptr);
 }
 
 void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,

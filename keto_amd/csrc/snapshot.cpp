@@ -261,16 +261,32 @@ void compute_layout(Snapshot& S) {
         std::vector<uint32_t> indeg(R, 0);
         for (uint32_t e : S.edges)
             if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
-        for (uint32_t r = 0; r < R; ++r) band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
+        S.is_root.assign(R, 0);
+        for (uint32_t r = 0; r < R; ++r) {
+            band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
+            S.is_root[r] = indeg[r] == 0;
+        }
     }
+    // edge partitioning: root rows of other parts are left out of this device's arena
+    std::vector<uint8_t> keep(R, 1);
+    uint32_t kept = R;
+    if (S.n_parts > 1)
+        for (uint32_t r = 0; r < R; ++r)
+            if (S.is_root[r] && S.root_owner(r, S.n_parts) != S.part) {
+                keep[r] = 0;
+                --kept;
+            }
     std::vector<uint64_t> start(35, 0);                  // key = 33 - band: hottest first
-    for (uint32_t r = 0; r < R; ++r) ++start[33 - band[r] + 1];
+    for (uint32_t r = 0; r < R; ++r) start[33 - band[r] + 1] += keep[r];
     for (int b = 1; b < 35; ++b) start[b] += start[b - 1];
-    S.rows_by_unit.assign(R, 0);
-    for (uint32_t r = 0; r < R; ++r) S.rows_by_unit[start[33 - band[r]]++] = r;
-    S.layout_units.assign(R, 0);
+    S.rows_by_unit.assign(kept, 0);
+    for (uint32_t r = 0; r < R; ++r) {
+        S.unit_of_row[r] = NO_UNIT;
+        if (keep[r]) S.rows_by_unit[start[33 - band[r]]++] = r;
+    }
+    S.layout_units.assign(kept, 0);
     uint64_t w = 0;
-    for (uint32_t x = 0; x < R; ++x) {
+    for (uint32_t x = 0; x < kept; ++x) {
         const uint32_t r = S.rows_by_unit[x];
         const uint32_t h = S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
@@ -290,6 +306,15 @@ void compute_layout(Snapshot& S) {
         w += table + HDR_WORDS + ((n + 3) & ~3ull);
     }
     S.n_units = w / HDR_WORDS;
+}
+
+uint32_t Snapshot::root_owner(uint32_t r, uint32_t parts) const {
+    // hash(namespace id, object): every relation of one object lives on one part
+    uint64_t h = (uint64_t)(uint32_t)row_key[r].ns * 0x9E3779B97F4A7C15ull ^ (uint64_t)row_key[r].obj * 0xC2B2AE3D27D4EB4Full;
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 32;
+    return parts ? (uint32_t)(h % parts) : 0;
 }
 
 int64_t Snapshot::row_of_handle(uint32_t unit) const {

@@ -38,6 +38,7 @@ constexpr uint32_t EDGE_SET = 0x80000000u;
 constexpr uint32_t EDGE_VAL = 0x7FFFFFFFu;
 constexpr uint32_t EDGE_POISON = 0x7FFFFFFFu;   // a row whose toInternal fails; never traversed
 constexpr uint32_t NO_PAGE = 0xFFFFFFFFu;
+constexpr uint32_t NO_UNIT = 0xFFFFFFFFu;         // row not on this device (edge partitioning)
 constexpr uint32_t ANY = 0xFFFFFFFFu;           // wildcard field of a row key
 constexpr int64_t ANY_NS = INT64_MIN;
 constexpr uint32_t ROW_SEQ = 1u;                // flag bit (in RowRec.y bits 8..15)
@@ -136,9 +137,15 @@ struct Snapshot {
     uint32_t n_seq_rows = 0;
 
     // ---- device arena layout (compute_layout): handle of each row, total arena units (16 B)
-    std::vector<uint32_t> unit_of_row;
+    std::vector<uint32_t> unit_of_row;    // NO_UNIT: a root row another part owns (not on this device)
     std::vector<uint32_t> rows_by_unit;   // rows in arena order (most-referenced first)
     std::vector<uint32_t> layout_units;   // their units, increasing
+    // edge partitioning (keto_snapshot_upload_part): rows that are some subject set's target are
+    // kept on every part; root rows (never a subject set) only on part hash(ns, object) % n_parts
+    std::vector<uint8_t> is_root;
+    uint32_t part = 0, n_parts = 1;
+    uint32_t root_owner(uint32_t r, uint32_t parts) const;   // part owning root row r
+    bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT; }
     uint64_t n_units = 0;
     uint32_t handle(uint32_t row) const { return unit_of_row[row]; }
     int64_t row_of_handle(uint32_t unit) const;   // -1 if not a row header
@@ -216,6 +223,9 @@ uint64_t device_bytes(const Snapshot& s);
 void device_check(Snapshot& s, const keto_check_ids* d_or_h_reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
                   bool host_buffers, void* stream, const Overlay* ov, uint64_t* work_out = nullptr);
 keto_batch_timing device_last_timing(const Snapshot& s);
+// requests with row ids (not handles) resident on the device: translated, then checked
+void device_check_rows(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
+                       void* stream);
 const char* device_check_kernel_name(int32_t gmd);
 struct ExpandResult {
     std::vector<uint8_t> status;

@@ -58,3 +58,98 @@ class ShardedChecker:
             a, b = shard_bounds(n, r, self.world)
             res[a:b] = out[r * width: r * width + (b - a)]
         return res
+
+
+class PartitionedChecker:
+    """Edge-partitioned mode, for graphs larger than one GPU (keto_snapshot_upload_part).
+
+    Every part holds the rows that some subject set points at; the root rows (rows no subject set
+    points at -- in an ACL graph the documents, which are most rows) are split by
+    hash(namespace_id, object) over the parts.  A check below its top-level row only visits rows
+    every part holds, so the only exchange is routing: one all-to-all sends each request to the
+    owner of its top-level row (requests on shared rows stay where they are), the owner runs its
+    engine, and a second all-to-all returns the decisions.  Both go over RCCL (xGMI) with the nccl
+    backend.  The reference's DFS cannot be cut into level-synchronous frontier exchanges without
+    changing its answers, so the partitioning keeps every traversal on one GPU.
+
+    owner(rows) -> int32 part per row id (-1 = held by every part), e.g. Snapshot.row_owner;
+    local_check(requests) -> uint8 decisions for the requests routed to this rank."""
+
+    def __init__(self, owner: Callable[[np.ndarray], np.ndarray], local_check: Callable[[np.ndarray], np.ndarray],
+                 group=None, device: str = "cpu"):
+        import torch.distributed as dist
+        self.owner = owner
+        self.local_check = local_check
+        self.group = group
+        self.device = device
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.last_routed = 0            # requests this rank received in the last call
+
+    def __call__(self, requests: np.ndarray) -> np.ndarray:
+        import torch
+        import torch.distributed as dist
+        n = len(requests)
+        own = np.asarray(self.owner(requests["row"]), dtype=np.int64)
+        dest = np.where(own < 0, self.rank, own)
+        order = np.argsort(dest, kind="stable")
+        send = np.ascontiguousarray(requests[order])
+        counts = np.bincount(dest, minlength=self.world).astype(np.int64)
+        c_out = torch.from_numpy(counts).to(self.device)
+        c_in = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(c_in, c_out, group=self.group)
+        in_counts = c_in.cpu().numpy()
+        item = requests.dtype.itemsize
+        sb = torch.from_numpy(send.view(np.uint8).copy()).to(self.device)
+        rb = torch.empty(int(in_counts.sum()) * item, dtype=torch.uint8, device=self.device)
+        dist.all_to_all_single(rb, sb, output_split_sizes=(in_counts * item).tolist(),
+                               input_split_sizes=(counts * item).tolist(), group=self.group)
+        mine = np.frombuffer(rb.cpu().numpy().tobytes(), dtype=requests.dtype)
+        self.last_routed = len(mine)
+        dec = np.asarray(self.local_check(mine), dtype=np.uint8)
+        if len(dec) != len(mine):
+            raise RuntimeError(f"local engine returned {len(dec)} decisions for {len(mine)} requests")
+        db = torch.from_numpy(dec.copy()).to(self.device)
+        back = torch.empty(n, dtype=torch.uint8, device=self.device)
+        dist.all_to_all_single(back, db, output_split_sizes=counts.tolist(),
+                               input_split_sizes=in_counts.tolist(), group=self.group)
+        res = np.empty(n, dtype=np.uint8)
+        res[order] = back.cpu().numpy()
+        return res
+
+
+def route_device(d_reqs, owner_dev, rank: int, world: int, group=None):
+    """Device-side routing of a partitioned check batch (all tensors on this rank's GPU).
+
+    d_reqs: int32 [n, 4] keto_check_ids naming rows by row id; owner_dev: int16/int32 [n_rows]
+    owner part per row (-1 = every part).  Returns (received requests [m, 4], state) where `state`
+    carries what send_back() needs to return the m decisions to their origins."""
+    import torch
+    import torch.distributed as dist
+    own = owner_dev[d_reqs[:, 0].long()].long()
+    dest = torch.where(own < 0, torch.full_like(own, rank), own)
+    order = torch.argsort(dest, stable=True)
+    send = d_reqs[order]
+    counts = torch.bincount(dest, minlength=world)
+    if world == 1:
+        return send, (order, counts.cpu().tolist(), counts.cpu().tolist())
+    in_counts = torch.empty_like(counts)
+    dist.all_to_all_single(in_counts, counts, group=group)
+    cs, ics = counts.cpu().tolist(), in_counts.cpu().tolist()
+    recv = torch.empty((sum(ics), 4), dtype=d_reqs.dtype, device=d_reqs.device)
+    dist.all_to_all_single(recv, send, output_split_sizes=ics, input_split_sizes=cs, group=group)
+    return recv, (order, cs, ics)
+
+
+def send_back(decisions, state, out, world: int, group=None):
+    """Return the decisions of route_device()'s received requests to their origins, in the
+    origin's order, into `out` (uint8 [n] on the device)."""
+    import torch
+    import torch.distributed as dist
+    order, cs, ics = state
+    if world == 1:
+        back = decisions
+    else:
+        back = torch.empty(sum(cs), dtype=torch.uint8, device=decisions.device)
+        dist.all_to_all_single(back, decisions, output_split_sizes=cs, input_split_sizes=ics, group=group)
+    out[order] = back

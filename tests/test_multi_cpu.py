@@ -70,3 +70,53 @@ def test_sharded_checker_gloo_world2(tmp_path, n):
     got = np.load(out)
     assert got.shape == want.shape and (got == want).all()
     assert 0.05 < want.mean() < 0.95
+
+
+def _part_worker(rank, world, port, q_bytes, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from keto_amd.multi import PartitionedChecker
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    host = g.host_snapshot()                       # row owners come from the C-ABI (no device)
+    q = np.frombuffer(q_bytes, dtype=g.queries(1, seed=0).dtype)
+    seen = []
+
+    def local(part):
+        own = host.row_owner(part["row"], world)
+        assert ((own == rank) | (own < 0)).all(), "a request reached a part that does not own its row"
+        seen.append(int((own == rank).sum()))
+        if len(part) == 0:
+            return np.zeros(0, dtype=np.uint8)
+        tab = g.oracle_table(part, 5)
+        return tab.check_batch_reqs(g.oracle_requests(tab, part), 5, threads=1)
+
+    lo, hi = (0, len(q) // 2) if rank == 0 else (len(q) // 2, len(q))
+    res = PartitionedChecker(lambda rows: host.row_owner(rows, world), local)(q[lo:hi])
+    np.save(out_path + f".{rank}.npy", res)
+    np.save(out_path + f".{rank}.seen.npy", np.array(seen))
+    dist.destroy_process_group()
+
+
+def test_partitioned_routing_gloo_world2(tmp_path):
+    """Requests whose top-level row is a root row travel to the part that owns it and come back in
+    order; the decisions equal a single-process oracle run."""
+    import torch.multiprocessing as mp
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    q = g.queries(3000, seed=31, depth=5)
+    host = g.host_snapshot()
+    own = host.row_owner(q["row"], 2)
+    assert (own >= 0).mean() > 0.9                # the docs:d#view rows of the requests are root rows
+    assert 0.3 < (own == 0).mean() < 0.7
+    tab = g.oracle_table(q, 5)
+    want = tab.check_batch_reqs(g.oracle_requests(tab, q), 5, threads=2)
+    out = str(tmp_path / "res")
+    mp.start_processes(_part_worker, args=(2, _free_port(), q.tobytes(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.concatenate([np.load(out + ".0.npy"), np.load(out + ".1.npy")])
+    assert (got == want).all()
+    routed = int(np.load(out + ".0.seen.npy").sum() + np.load(out + ".1.seen.npy").sum())
+    assert routed == int((own >= 0).sum())

@@ -121,6 +121,19 @@ class SynthGraph:
         return Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                                  device=device)
 
+    def snapshot_part(self, part: int, n_parts: int, device=0):
+        """This part's share of the edge-partitioned snapshot (keto_snapshot_upload_part)."""
+        from keto_amd.capi import Snapshot
+        s = Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
+                              device=-1)
+        return s.upload_part(part, n_parts, device)
+
+    def host_snapshot(self):
+        """Host-only snapshot (no device): resolution, row owners."""
+        from keto_amd.capi import Snapshot
+        return Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
+                                 device=-1)
+
     def oracle_table(self, q: np.ndarray, depth: int):
         """OracleTable over every row a depth-bounded check of the sample can query."""
         from oracle.oracle_c import OracleTable
