@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import sys
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -93,9 +94,19 @@ _lib = None
 
 
 def load():
+    """Load the engine.  In a process that also uses PyTorch-ROCm (which ships its own HIP runtime),
+    torch's runtime must be initialized before the engine's: if torch is already imported, this
+    initializes it first."""
     global _lib
     if _lib is not None:
         return _lib
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
     if not os.path.exists(LIB_PATH):
         raise KetoError(f"{LIB_PATH} is missing: build it with `python keto_amd/build.py` "
                         "(the engine has no non-HIP implementation)")

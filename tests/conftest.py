@@ -11,3 +11,17 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_runtime_first():
+    """PyTorch-ROCm ships its own HIP runtime next to the system one the engine links; in one
+    process the two coexist only if torch's initializes first (the bench does the same).  GPU tests
+    that hand torch device buffers to the engine rely on this."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+    yield
