@@ -649,9 +649,11 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             acc = 0;
         }
     };
-    for (;;) {
-        // ---- start the next request from its prefetched copy (no iteration spent on fetching it)
-        while (bf(c, C_PH, 3) == P_REQ && (c & C_NQ)) {
+    // start the lane's next request from its LDS prefetch slots (no iteration spent on fetching
+    // it); requests that need no traversal are decided on the spot.  Leaves the phase at P_HDR, or
+    // at P_REQ when no prefetched request is left (the next iteration fetches one or the lane ends)
+    auto start_next = [&]() {
+        while (c & C_NQ) {
             const uint4 nq = lds_nq[tid];
             const uint32_t qi = j++;
             uint32_t keep = 0;                                    // the pair's second request moves up
@@ -663,48 +665,48 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
             if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
                 decide(qi, 0);
-                c = (c & ~(C_NQ | C_NQ2)) | keep;
+                c = keep;
                 continue;
             }
             T = nq.y;
             eh = nq.x;
             c = P_HDR | ((uint32_t)d << C_K) | ((nq.z & 1u) ? C_TSET : 0u) | keep;   // sp 0, no frame
+            return;
         }
+        c = (c & ~7u) | P_REQ;
+    };
+    for (;;) {
         const uint32_t ph = bf(c, C_PH, 3);
         if (ph == P_REQ && j >= j_end) break;
-        // ---- the iteration's global accesses: one per lane, plus the next request's prefetch
-        const uint32_t* const ce = (bf(c, C_FL, 4) & FR_OV) ? ov.arena : s.arena;
-        const uint4* a0 = nullptr;
-        const uint4* a1 = nullptr;
-        if (ph == P_REQ) {                                        // not prefetched: fetch it now
-            prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
-            c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
-            w.request();
-        } else if (ph == P_HDR) {
-            const bool is_ov = eh >= ov.base;
-            const uint32_t* ar = is_ov ? ov.arena : s.arena;
-            a0 = reinterpret_cast<const uint4*>(ar + (uint64_t)(is_ov ? eh - ov.base : eh) * HDR_WORDS);
-            a1 = a0 + 1;
-            w.header(a0);
-        } else if (ph == P_IDQ) {
-            const uint32_t hl = bf(c, C_HL, 5);
-            a0 = reinterpret_cast<const uint4*>(ce + (pos - HDR_WORDS - (1u << hl)) + eh * BUCKET_WORDS);
+        // ---- the iteration's global accesses: one per lane (selected without branches), plus the
+        // next request pair's prefetch
+        const bool hdr = ph == P_HDR;
+        const bool in_ov = hdr ? eh >= ov.base : (bf(c, C_FL, 4) & FR_OV) != 0;
+        const uint32_t* const ar = in_ov ? ov.arena : s.arena;
+        const uint32_t hl = bf(c, C_HL, 5);
+        const uint32_t word = hdr ? (in_ov ? eh - ov.base : eh) * HDR_WORDS
+                                  : ph == P_IDQ ? pos - HDR_WORDS - (1u << hl) + eh * BUCKET_WORDS : (pos & ~3u);
+        const uint4* const a0 = reinterpret_cast<const uint4*>(ar + word);
+        if (hdr) w.header(a0);
+        else if (ph == P_IDQ) {
             w.idread(BUCKET_WORDS);
             w.id_at(a0, true);
         } else if (ph == P_EDGE) {
-            a0 = reinterpret_cast<const uint4*>(ce + (pos & ~3u));
             w.edge_at(a0);
         }
-        if (!(c & C_NQ) && ph != P_REQ && j < j_end) {            // prefetch the next pair alongside
+        if (!(c & C_NQ) && j < j_end) {                           // prefetch the next pair
             prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
             c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
             w.request();
         }
         uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-        if (a0) v0 = *a0;
-        if (a1) v1 = *a1;
+        if (ph != P_REQ) v0 = a0[0];
+        if (hdr) v1 = a0[1];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // also retires the LDS-direct prefetch
-        if (ph == P_REQ) continue;
+        if (ph == P_REQ) {
+            start_next();
+            continue;
+        }
         int res = -1;
         const bool tset = (c & C_TSET) != 0;
         if (ph == P_HDR) {
@@ -857,7 +859,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             } else {
                 decide(qi, (uint32_t)res);
             }
-            c = bf_set(c, C_PH, 3, P_REQ);
+            start_next();
         }
     }
     ta.slot_epoch[slot] = V.epoch;
