@@ -1019,6 +1019,12 @@ struct DeviceState {
     hipEvent_t ev[6] = {};
     keto_batch_timing last{};
     uint32_t* row_handle = nullptr;   // row id -> handle (NO_UNIT: another part's root row), lazily
+    uint32_t* layout_units = nullptr; // handles in arena order (increasing) and their rows, lazily:
+    uint32_t* rows_by_unit = nullptr; //   expand output handle -> row id on the device
+    void* ex_buf = nullptr;           // expand workspace (requests, counts, statuses, offsets)
+    uint64_t ex_cap = 0;
+    keto_tree_node* ex_nodes = nullptr;
+    uint64_t ex_nodes_cap = 0;
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
 
@@ -1224,6 +1230,10 @@ void device_release(Snapshot& S) {
     if (D.lists) (void)hipFree(D.lists);
     if (D.counters) (void)hipFree(D.counters);
     if (D.row_handle) (void)hipFree(D.row_handle);
+    if (D.layout_units) (void)hipFree(D.layout_units);
+    if (D.rows_by_unit) (void)hipFree(D.rows_by_unit);
+    if (D.ex_buf) (void)hipFree(D.ex_buf);
+    if (D.ex_nodes) (void)hipFree(D.ex_nodes);
     if (D.xlate) (void)hipFree(D.xlate);
     if (D.stream) (void)hipStreamDestroy(D.stream);
     for (auto& e : D.ev)
@@ -1548,6 +1558,26 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
     device_check(S, D.xlate, n, gmd, d_allowed, false, stream, nullptr);
 }
 
+// Expand output: set nodes carry row handles; map them to row ids on the device (binary search in
+// the arena-order handle list; overlay handles >= ov_units_base are left for the host).
+__global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restrict__ nodes, uint64_t n,
+                                                       const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
+                                                       uint32_t n_rows, uint32_t ov_units_base) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = nodes[i].subject;
+    if (!(x & EDGE_SET)) return;
+    const uint32_t h = x & EDGE_VAL;
+    if (h >= ov_units_base) return;
+    uint32_t lo = 0, hi = n_rows;                  // first unit >= h
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (units[m] < h) lo = m + 1;
+        else hi = m;
+    }
+    nodes[i].subject = EDGE_SET | rows[lo];
+}
+
 void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
                    const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
                    const Overlay* ovh, ExpandResult& out) {
@@ -1563,17 +1593,25 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (gmd > 65535) gmd = 65535;
     hipStream_t st = D.stream;
     OverlayBuf ov(S, ovh);
-    std::vector<ExpandReq> hq(n);
-    for (uint32_t i = 0; i < n; ++i) hq[i] = ExpandReq{root[i], root_flags[i], root_vid[i], depth[i]};
-    DevFree tmp;
     uint64_t acc = 0;
-    ExpandReq* dq = dmalloc<ExpandReq>(n, acc);
-    tmp.p.push_back(dq);
-    uint64_t* dcount = dmalloc<uint64_t>(n + 1, acc);
-    tmp.p.push_back(dcount);
-    uint8_t* dstatus = dmalloc<uint8_t>(n, acc);
-    tmp.p.push_back(dstatus);
-    HIP_OK(hipMemcpy(dq, hq.data(), n * sizeof(ExpandReq), hipMemcpyHostToDevice));
+    // workspace, reused across calls: requests | counts (n + 1) | offsets (n + 1) | statuses
+    const uint64_t need = (uint64_t)n * sizeof(ExpandReq) + 2ull * (n + 1) * sizeof(uint64_t) + n + 64;
+    if (D.ex_cap < need) {
+        if (D.ex_buf) (void)hipFree(D.ex_buf);
+        D.ex_cap = std::max<uint64_t>(need, 1 << 20);
+        D.ex_buf = dmalloc<uint8_t>(D.ex_cap, acc);
+    }
+    uint8_t* base = (uint8_t*)D.ex_buf;
+    uint64_t* dcount = reinterpret_cast<uint64_t*>(base);
+    uint64_t* doff = dcount + (n + 1);
+    ExpandReq* dq = reinterpret_cast<ExpandReq*>(doff + (n + 1));
+    uint8_t* dstatus = reinterpret_cast<uint8_t*>(dq + n);
+    {
+        std::vector<ExpandReq> hq(n);
+        for (uint32_t i = 0; i < n; ++i) hq[i] = ExpandReq{root[i], root_flags[i], root_vid[i], depth[i]};
+        HIP_OK(hipMemcpyAsync(dq, hq.data(), n * sizeof(ExpandReq), hipMemcpyHostToDevice, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
     Plan p = make_plan(D, n, gmd);            // expand holds at most gmd frames
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
@@ -1584,7 +1622,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                       uint32_t slots) {
                       TierArgs a = tier_args(t, il, ic, ol, oc);
                       const uint32_t bs = std::min<uint32_t>(256, slots);
-                  dim3 grid(slots / bs), block(bs);
+                      dim3 grid(slots / bs), block(bs);
                       const bool local = p.frames[level] == 0;
                       if (!fill && local)
                           hipLaunchKernelGGL((expand_kernel<false, LocalStack<16>>), grid, block, 0, st, sv, dov, dq,
@@ -1605,32 +1643,45 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     // same tiers both times, and a partial pre-order is a prefix of the full one)
     launch_pass(false, o);
     std::vector<uint64_t> cnt(n);
-    HIP_OK(hipMemcpy(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(out.status.data(), dstatus, n, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpyAsync(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(out.status.data(), dstatus, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
     for (uint32_t i = 0; i < n; ++i) out.offset[i + 1] = out.offset[i] + cnt[i];
     const uint64_t total = out.offset[n];
     out.nodes.resize(total);
     if (total == 0) return;
-    keto_tree_node* dnodes = dmalloc<keto_tree_node>(total, acc);
-    tmp.p.push_back(dnodes);
-    uint64_t* doff = dmalloc<uint64_t>(n + 1, acc);
-    tmp.p.push_back(doff);
-    HIP_OK(hipMemcpy(doff, out.offset.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
-    launch_pass(true, ExpandOut{dnodes, doff, dcount, dstatus});
-    HIP_OK(hipMemcpy(out.nodes.data(), dnodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost));
-    // handles -> row ids (overlay handles -> ovh->base + overlay index)
-    host_parallel_for(total, [&](uint64_t i) {
-        keto_tree_node& x = out.nodes[i];
-        if (!(x.subject & EDGE_SET)) return;
-        const uint32_t h = x.subject & EDGE_VAL;
-        if (h >= S.n_units && ovh) {
+    if (D.ex_nodes_cap < total) {
+        if (D.ex_nodes) (void)hipFree(D.ex_nodes);
+        D.ex_nodes_cap = std::max<uint64_t>(total, 1 << 16);
+        D.ex_nodes = dmalloc<keto_tree_node>(D.ex_nodes_cap, acc);
+    }
+    if (!D.layout_units) {
+        const uint64_t m = std::max<uint64_t>(1, S.layout_units.size());
+        D.layout_units = dmalloc<uint32_t>(m, acc);
+        D.rows_by_unit = dmalloc<uint32_t>(m, acc);
+        HIP_OK(hipMemcpy(D.layout_units, S.layout_units.data(), S.layout_units.size() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(D.rows_by_unit, S.rows_by_unit.data(), S.rows_by_unit.size() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice));
+    }
+    HIP_OK(hipMemcpyAsync(doff, out.offset.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus});
+    hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
+                       D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    // overlay handles -> ovh->base + overlay index (batch-local wildcard roots only)
+    if (ovh && !ovh->empty())
+        host_parallel_for(total, [&](uint64_t i) {
+            keto_tree_node& x = out.nodes[i];
+            if (!(x.subject & EDGE_SET)) return;
+            const uint32_t h = x.subject & EDGE_VAL;
+            if (h < S.n_units) return;
             const uint32_t u = (uint32_t)(h - S.n_units);
             auto it = std::lower_bound(ovh->unit.begin(), ovh->unit.end(), u);
             x.subject = EDGE_SET | (ovh->base + (uint32_t)(it - ovh->unit.begin()));
-        } else {
-            x.subject = EDGE_SET | (uint32_t)S.row_of_handle(h);
-        }
-    });
+        });
 }
 
 }  // namespace keto
