@@ -49,7 +49,7 @@ constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_OVERFLOW = 2;
 constexpr int EXP_TREE = 0, EXP_NIL = 1, EXP_ERROR = 2, EXP_OVERFLOW = 3;
 
 struct DevSnap {
-    const uint32_t* arena;    // main arena (u32 words)
+    const uint32_t* arena;    // main arena (u32 words; tier 0 adds 2^32 words for segment 1)
     const uint64_t* coll;     // (edge value << 32) | visit id ; empty = ~0
     uint32_t coll_mask;       // 0 = no collisions
 };
@@ -86,6 +86,7 @@ struct RowView {
     uint32_t hlog2;           // id table size (0 = none), table ends at beg - HDR_WORDS
     bool poison, poison0;     // some page / the first page fails toInternal (expand)
     bool seq;
+    bool closure;             // a closure filter precedes the header (the id table precedes that)
 };
 
 __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint32_t h) {
@@ -106,6 +107,7 @@ __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint3
     rv.hlog2 = (v.z >> 8) & 31u;
     rv.poison = (v.z & HDR_POISON) != 0;
     rv.poison0 = (v.z & HDR_POISON0) != 0;
+    rv.closure = (v.z & HDR_CLOSURE) != 0;
     return rv;
 }
 
@@ -125,6 +127,7 @@ struct Work {
     __device__ inline void push() {}
     __device__ inline void pop() {}
     __device__ inline void leaf(bool, uint32_t) {}
+    __device__ inline void pruned() {}
 };
 template <>
 struct Work<true> {
@@ -156,25 +159,30 @@ struct Work<true> {
     }
     __device__ inline void push() { ++c[11]; }
     __device__ inline void pop() { ++c[12]; }
-    // 13 leaf rows entered (no subject sets), 14 of them without the requested id, 15 of those
-    // with <= 8 ids
-    __device__ inline void leaf(bool miss, uint32_t n_ids) {
+    // 13 leaf rows entered (no subject sets), 14 of them without the requested id; 15 subject
+    // sets skipped by their closure filter
+    __device__ inline void leaf(bool miss, uint32_t) {
         ++c[13];
-        if (miss) {
-            ++c[14];
-            if (n_ids <= 8) ++c[15];
-        }
+        if (miss) ++c[14];
     }
+    __device__ inline void pruned() { ++c[15]; }
 };
+// Can subject id t be reached from the row at all (closure filter; rv.closure only)?
+__device__ inline bool closure_has(const RowView& rv, uint32_t t) {
+    uint32_t wd, bit;
+    closure_bit(t, wd, bit);
+    return (rv.a[rv.beg - HDR_WORDS - CB_WORDS + wd] >> bit) & 1u;
+}
+
 // Is subject id t in the row's (effective) id region?
 template <class W>
 __device__ inline bool row_has_id(const RowView& rv, uint32_t t, W& w) {
     if (rv.n_ids == 0) return false;
     const uint32_t* __restrict__ e = rv.a;
     if (rv.hlog2) {
-        // bucketed table in front of the header: [beg - HDR_WORDS - 2^hlog2, beg - HDR_WORDS)
+        // bucketed table in front of the header (and its closure filter)
         const uint32_t nb = (1u << rv.hlog2) / BUCKET_WORDS;
-        const uint64_t tb = rv.beg - HDR_WORDS - (1ull << rv.hlog2);
+        const uint64_t tb = rv.beg - HDR_WORDS - (rv.closure ? CB_WORDS : 0u) - (1ull << rv.hlog2);
         for (uint32_t b = mix32(t) & (nb - 1);; b = (b + 1) & (nb - 1)) {
             const uint4 v = *reinterpret_cast<const uint4*>(e + tb + (uint64_t)b * BUCKET_WORDS);
             w.idread(BUCKET_WORDS);
@@ -471,7 +479,10 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             const RowView rv = load_row(s, ov, enter);
             w.row();
             w.header(rv.a + rv.beg - HDR_WORDS);
-            if (!rv.seq && !tset && row_has_id(rv, T, w)) {
+            if (rv.closure && !tset && !(enter_fl & FR_TOP) && !closure_has(rv, T)) {
+                enter = NONE32;                                   // T is not below this set: skip it
+                w.pruned();
+            } else if (!rv.seq && !tset && row_has_id(rv, T, w)) {
                 res = RES_TRUE;
             } else if (sp > st.cap()) {        // saved frames live in st[0 .. sp-1)
                 res = RES_OVERFLOW;
@@ -522,8 +533,12 @@ constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
 constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // saved lkf = left | k << 23 | fl << 28
 constexpr uint16_t FR_WV = 8;                        // the window holds the block of `pos`
 // control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23 | nq2 24
+// | cb 25 (the current row has a closure filter, so its id table starts CB_WORDS further down)
+// | seg 26 (the current row lies in arena segment 1: positions are 32-bit words within a segment)
 constexpr uint32_t C_PH = 0, C_K = 3, C_FL = 8, C_SP = 12, C_HL = 19;
-constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18, C_NQ2 = 1u << 24;
+constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18, C_NQ2 = 1u << 24, C_CB = 1u << 25;
+constexpr uint32_t C_SEG = 1u << 26;
+// saved frame word: left 0..22 | k 23..26 (tier 0 runs max-depth <= 9) | seg 27 | fl 28..31
 __device__ inline uint32_t bf(uint32_t c, uint32_t off, uint32_t wd) { return (c >> off) & ((1u << wd) - 1u); }
 __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_t v) {
     const uint32_t m = ((1u << wd) - 1u) << off;
@@ -534,9 +549,6 @@ __device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
     return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
 }
 __device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
-__device__ inline const uint32_t* ce0(const DevSnap& s, const DevOverlay& ov, uint32_t h) {
-    return h >= ov.base ? ov.arena : s.arena;
-}
 
 // requests j and j + 1 (if in the run) straight into the wave's LDS prefetch slots (global_load_lds:
 // no VGPR destination; lane L's 16 B land at wave_base + 16 L, i.e. lds_nq[tid] and
@@ -682,11 +694,19 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         // next request pair's prefetch
         const bool hdr = ph == P_HDR;
         const bool in_ov = hdr ? eh >= ov.base : (bf(c, C_FL, 4) & FR_OV) != 0;
-        const uint32_t* const ar = in_ov ? ov.arena : s.arena;
+        const bool hi = hdr ? ((eh >> SEG_SHIFT) & 1u) != 0 : (c & C_SEG) != 0;
+        const uint32_t* const ar = (in_ov ? ov.arena : s.arena) + ((hi && !in_ov) ? (1ull << 32) : 0ull);
         const uint32_t hl = bf(c, C_HL, 5);
-        const uint32_t word = hdr ? (in_ov ? eh - ov.base : eh) * HDR_WORDS
-                                  : ph == P_IDQ ? pos - HDR_WORDS - (1u << hl) + eh * BUCKET_WORDS : (pos & ~3u);
+        const uint32_t word = hdr ? (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS
+                                  : ph == P_IDQ ? pos - HDR_WORDS - ((c & C_CB) ? CB_WORDS : 0u) - (1u << hl) +
+                                                      eh * BUCKET_WORDS
+                                                : (pos & ~3u);
         const uint4* const a0 = reinterpret_cast<const uint4*>(ar + word);
+        // entering a subject set (always a row some set points at, so it has a closure filter):
+        // the filter word of T, from the line the header comes in with
+        const bool cbq = hdr && (c & (C_HAVE | C_TSET)) == C_HAVE;
+        uint32_t cwd, cbit;
+        closure_bit(T, cwd, cbit);
         if (hdr) w.header(a0);
         else if (ph == P_IDQ) {
             w.idread(BUCKET_WORDS);
@@ -700,8 +720,10 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             w.request();
         }
         uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+        uint32_t cbw = NONE32;
         if (ph != P_REQ) v0 = a0[0];
         if (hdr) v1 = a0[1];
+        if (cbq) cbw = reinterpret_cast<const uint32_t*>(a0)[(int)cwd - (int)CB_WORDS];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // also retires the LDS-direct prefetch
         if (ph == P_REQ) {
             start_next();
@@ -709,7 +731,13 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         }
         int res = -1;
         const bool tset = (c & C_TSET) != 0;
-        if (ph == P_HDR) {
+        if (ph == P_HDR && cbq && (v0.z & HDR_CLOSURE) && !((cbw >> cbit) & 1u)) {
+            // T is not below this subject set: skip it, the parent's walk goes on (the set stays
+            // marked visited, as in the reference; see HDR_CLOSURE)
+            w.row();
+            w.pruned();
+            c = bf_set(c, C_PH, 3, P_WALK);
+        } else if (ph == P_HDR) {
             // entering a row (engine.go:82-114): save the parent if it still has edges
             w.row();
             const bool have = (c & C_HAVE) != 0;
@@ -726,7 +754,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                         if (left == 1 && (fl0 & FR_WV)) px = win_at(win, pos & 3u);
                         else fl = fl0 & ~(uint32_t)FR_WV;
                     }
-                    sf_pk[sp * LDS_STRIDE + tid] = make_uint2(px, left | (bf(c, C_K, 5) << 23) | (fl << 28));
+                    sf_pk[sp * LDS_STRIDE + tid] =
+                        make_uint2(px, left | (bf(c, C_K, 5) << 23) | ((c & C_SEG) ? (1u << 27) : 0u) | (fl << 28));
                     if constexpr (WIN) sf_win[sp * LDS_STRIDE + tid] = win;
                     c = bf_set(c, C_SP, 4, sp + 1);
                     w.push();
@@ -738,10 +767,12 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 const uint32_t hl = (v0.z >> 8) & 31u;
                 const uint32_t k = have ? bf(c, C_K, 5) - 1u : bf(c, C_K, 5);
                 const uint32_t fl = (have ? 0u : (uint32_t)FR_TOP) | (seq ? FR_SEQ : 0u) | (is_ov ? FR_OV : 0u) | FR_WV;
-                pos = (is_ov ? eh - ov.base : eh) * HDR_WORDS + HDR_WORDS;
+                pos = (is_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS + HDR_WORDS;
                 left = v0.x;
                 win = v1;
                 c = bf_set(bf_set(bf_set(bf_set(c, C_K, 5, k), C_FL, 4, fl), C_HL, 5, hl), C_PH, 3, P_WALK) | C_HAVE;
+                c = (v0.z & HDR_CLOSURE) ? (c | C_CB) : (c & ~C_CB);
+                c = (!is_ov && ((eh >> SEG_SHIFT) & 1u)) ? (c | C_SEG) : (c & ~C_SEG);
                 const uint32_t n_sets = v0.x, n_ids = v0.y;
                 if constexpr (COUNT) {
                     if (!seq && n_sets == 0 && !tset) {
@@ -750,7 +781,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                             for (uint32_t i = 0; i < WINDOW_WORDS; ++i) in |= (i < n_ids) & (win_at(win, i) == T);
                         } else {
                             const uint32_t nb = (1u << hl) / BUCKET_WORDS;
-                            const uint32_t* tab = ce0(s, ov, eh) + pos - HDR_WORDS - (1u << hl);
+                            const uint32_t* tab = ar + pos - HDR_WORDS -
+                                                  ((v0.z & HDR_CLOSURE) ? CB_WORDS : 0u) - (1u << hl);
                             for (uint32_t b = mix32(T) & (nb - 1);; b = (b + 1) & (nb - 1)) {
                                 const uint4 v = *reinterpret_cast<const uint4*>(tab + b * BUCKET_WORDS);
                                 if (has4(v, T)) { in = true; break; }
@@ -806,7 +838,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                     pos = pk.x;
                 }
                 left = pk.y & WF_LEFT_MAX;
-                c = bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 31u), C_FL, 4, pk.y >> 28);
+                c = bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 15u), C_FL, 4, pk.y >> 28);
+                c = ((pk.y >> 27) & 1u) ? (c | C_SEG) : (c & ~C_SEG);
                 w.pop();
                 continue;
             }
@@ -1122,14 +1155,30 @@ void host_parallel_for(uint64_t n, F f) {
     for (auto& x : ts) x.join();
 }
 
-// Write one row (table, header, edges) into an arena at its handle.
+// Write one row (table, closure filter seed, header, edges) into an arena at its handle.  The
+// closure filter starts as the row's own ids (all bits for a ROW_SEQ row); closure_pass adds the
+// closures of its subject sets on the device.
 void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uint32_t hlog2, const uint32_t* edges,
-             uint64_t n_stored, const std::vector<uint32_t>& unit_of_row) {
+             uint64_t n_stored, const std::vector<uint32_t>& unit_of_row, bool closure) {
     uint64_t h = (uint64_t)unit * HDR_WORDS;
     const bool seq = ((rec.hi_flags >> 8) & ROW_SEQ) != 0;
     arena[h + 0] = rec.n_sets;
     arena[h + 1] = rec.n_ids;
-    uint32_t w2 = (seq ? HDR_SEQ : 0u) | (pp != NO_PAGE ? HDR_POISON : 0u) | (pp == 0 ? HDR_POISON0 : 0u) | (hlog2 << 8);
+    uint32_t w2 = (seq ? HDR_SEQ : 0u) | (pp != NO_PAGE ? HDR_POISON : 0u) | (pp == 0 ? HDR_POISON0 : 0u) |
+                  (closure ? HDR_CLOSURE : 0u) | (hlog2 << 8);
+    if (closure) {
+        uint32_t* cf = arena + h - CB_WORDS;
+        for (uint32_t i = 0; i < CB_WORDS; ++i) cf[i] = seq ? NONE32 : 0u;
+        if (!seq)
+            for (uint64_t i = 0; i < n_stored; ++i) {
+                const uint32_t v = edges[i];
+                if (v & EDGE_SET) continue;                     // subject sets: closure_pass
+                if (v == EDGE_POISON) continue;
+                uint32_t wd, bit;
+                closure_bit(v, wd, bit);
+                cf[wd] |= 1u << bit;
+            }
+    }
     uint32_t w3 = 0;
     if (hlog2) {
         for (uint32_t k = 0; k < rec.n_ids; ++k) {
@@ -1152,7 +1201,7 @@ void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uin
     for (uint64_t i = n_stored; i < ((n_stored + 3) & ~3ull); ++i) e[i] = NONE32;
     if (hlog2) {
         const uint32_t nb = (1u << hlog2) / BUCKET_WORDS;
-        uint32_t* tab = arena + h - (1ull << hlog2);
+        uint32_t* tab = arena + h - (closure ? CB_WORDS : 0u) - (1ull << hlog2);
         for (uint32_t i = 0; i < (1u << hlog2); ++i) tab[i] = NONE32;
         for (uint32_t k = 0; k < rec.n_ids; ++k) {
             const uint32_t id = edges[rec.n_sets + k];
@@ -1169,6 +1218,103 @@ void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uin
     }
 }
 
+// One round of closure propagation: each listed row ORs the closure filters of its subject sets
+// into its own.  Filters only gain bits that are in the true closures, so rounds may overlap with
+// one another's writes (reads of a half-updated filter are still subsets); a round that changes
+// nothing means every filter is closed.  One lane per row.
+__global__ void __launch_bounds__(256) closure_pass(uint32_t* __restrict__ arena, const uint32_t* __restrict__ rows,
+                                                   uint32_t n, uint32_t* __restrict__ changed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = (uint64_t)rows[i] * HDR_WORDS;
+    uint4* const cf = reinterpret_cast<uint4*>(arena + h - CB_WORDS);
+    uint4 acc[CB_WORDS / 4];
+#pragma unroll
+    for (int k = 0; k < (int)(CB_WORDS / 4); ++k) acc[k] = cf[k];
+    const uint4 v = *reinterpret_cast<const uint4*>(arena + h);
+    const uint32_t n_sets = v.x;
+    uint32_t more = 0;
+    for (uint32_t e = 0; e < n_sets; ++e) {
+        const uint32_t x = arena[h + HDR_WORDS + e];
+        if (!(x & EDGE_SET)) continue;
+        const uint64_t ch = (uint64_t)(x & EDGE_VAL) * HDR_WORDS;
+        const uint32_t cz = arena[ch + 2];
+        if (!(cz & HDR_CLOSURE)) {                    // cannot happen: a set's target has a filter
+            more = NONE32;
+            continue;
+        }
+        const uint4* const cc = reinterpret_cast<const uint4*>(arena + ch - CB_WORDS);
+#pragma unroll
+        for (int k = 0; k < (int)(CB_WORDS / 4); ++k) {
+            const uint4 y = cc[k];
+            acc[k].x |= y.x;
+            acc[k].y |= y.y;
+            acc[k].z |= y.z;
+            acc[k].w |= y.w;
+        }
+    }
+    if (more) {
+#pragma unroll
+        for (int k = 0; k < (int)(CB_WORDS / 4); ++k) acc[k] = make_uint4(NONE32, NONE32, NONE32, NONE32);
+    }
+    bool diff = false;
+#pragma unroll
+    for (int k = 0; k < (int)(CB_WORDS / 4); ++k) {
+        const uint4 o = cf[k];
+        if (o.x != acc[k].x || o.y != acc[k].y || o.z != acc[k].z || o.w != acc[k].w) {
+            cf[k] = acc[k];
+            diff = true;
+        }
+    }
+    if (diff) atomicAdd(changed, 1u);
+}
+
+__global__ void __launch_bounds__(256) closure_fill(uint32_t* __restrict__ arena, const uint32_t* __restrict__ rows,
+                                                   uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t* const cf = arena + (uint64_t)rows[i] * HDR_WORDS - CB_WORDS;
+    for (uint32_t k = 0; k < CB_WORDS; ++k) cf[k] = NONE32;
+}
+
+// Close every row's closure filter on the device: rounds of closure_pass over the rows that have
+// a filter and subject sets, until a round changes nothing.  A graph that has not converged after
+// CLOSURE_MAX_ROUNDS rounds gets full filters (no pruning) instead.
+constexpr int CLOSURE_MAX_ROUNDS = 2048;
+void build_closures(const Snapshot& S, uint32_t* d_arena, const std::vector<uint32_t>& host_arena) {
+    std::vector<uint32_t> list, all;
+    for (uint32_t r = 0; r < S.n_rows(); ++r) {
+        if (S.is_root[r] || !S.present(r)) continue;
+        all.push_back(S.unit_of_row[r]);
+        const uint64_t h = (uint64_t)S.unit_of_row[r] * HDR_WORDS;
+        if (host_arena[h] > 0 && !(host_arena[h + 2] & HDR_SEQ)) list.push_back(S.unit_of_row[r]);
+    }
+    if (list.empty()) return;
+    uint32_t *d_rows = nullptr, *d_changed = nullptr;
+    HIP_OK(hipMalloc(&d_rows, std::max(list.size(), all.size()) * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_changed, sizeof(uint32_t)));
+    HIP_OK(hipMemcpy(d_rows, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const uint32_t n = (uint32_t)list.size();
+    bool done = false;
+    for (int round = 0; round < CLOSURE_MAX_ROUNDS && !done; ++round) {
+        HIP_OK(hipMemset(d_changed, 0, sizeof(uint32_t)));
+        hipLaunchKernelGGL(closure_pass, dim3((n + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, n, d_changed);
+        HIP_OK(hipGetLastError());
+        uint32_t ch = 0;
+        HIP_OK(hipMemcpy(&ch, d_changed, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        done = ch == 0;
+    }
+    if (!done) {
+        HIP_OK(hipMemcpy(d_rows, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        const uint32_t m = (uint32_t)all.size();
+        hipLaunchKernelGGL(closure_fill, dim3((m + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, m);
+        HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipDeviceSynchronize());
+    (void)hipFree(d_rows);
+    (void)hipFree(d_changed);
+}
+
 }  // namespace
 
 void device_upload(Snapshot& S, int device) {
@@ -1180,7 +1326,7 @@ void device_upload(Snapshot& S, int device) {
     D->device = device;
     uint64_t acc = 0;
     const uint64_t words = S.n_units * HDR_WORDS;
-    if (words >= (1ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^32 words (16 GiB)"};
+    if (words > (2ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^33 words (32 GiB)"};
     std::vector<uint32_t> arena(std::max<uint64_t>(words, 4));
     const uint32_t R = S.n_rows();
     host_parallel_for(R, [&](uint64_t r) {
@@ -1188,10 +1334,11 @@ void device_upload(Snapshot& S, int device) {
         const uint64_t b = S.row_begin((uint32_t)r);
         const uint64_t e = r + 1 < R ? S.row_begin((uint32_t)r + 1) : S.edges.size();
         put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), S.edges.data() + b,
-                e - b, S.unit_of_row);
+                e - b, S.unit_of_row, !S.is_root[r]);
     });
     D->arena = dmalloc<uint32_t>(arena.size(), acc);
     HIP_OK(hipMemcpy(D->arena, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    build_closures(S, D->arena, arena);
     if (!S.coll.empty()) {
         uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
         std::vector<uint64_t> tab(cap, ~0ull);
@@ -1340,7 +1487,7 @@ struct OverlayBuf {
             const uint64_t e = i + 1 < ov->rows.size()
                                    ? ((uint64_t)ov->rows[i + 1].edge_lo | ((uint64_t)(ov->rows[i + 1].hi_flags & 0xFFu) << 32))
                                    : ov->edges.size();
-            put_row(arena.data(), ov->unit[i], rec, ov->pp[i], 0, ov->edges.data() + b, e - b, S.unit_of_row);
+            put_row(arena.data(), ov->unit[i], rec, ov->pp[i], 0, ov->edges.data() + b, e - b, S.unit_of_row, false);
         }
         uint64_t acc = 0;
         uint32_t* a = dmalloc<uint32_t>(arena.size(), acc);

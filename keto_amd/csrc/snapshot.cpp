@@ -291,19 +291,29 @@ void compute_layout(Snapshot& S) {
         const uint32_t h = S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
         const uint64_t n = row_end_of(S, r) - S.row_begin(r);
-        // line placement: a row that fits in a 128-B line never straddles one (header, window and
-        // id table come in with one miss); a bigger row keeps header + window in one line
-        const uint64_t total = table + HDR_WORDS + ((n + 3) & ~3ull);
-        if (total <= LINE_WORDS) {
-            if (w % LINE_WORDS + total > LINE_WORDS) w = (w + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
-        } else if ((w + table) % LINE_WORDS == LINE_WORDS - HDR_WORDS) {
-            w += HDR_WORDS;
-        }
-        const uint64_t unit = (w + table) / HDR_WORDS;
+        // line placement: a row that fits in a 128-B line never straddles one (closure filter,
+        // header, window and id table come in with one miss); a bigger row keeps closure filter +
+        // header + window in one line
+        const uint64_t cb = S.is_root[r] ? 0 : CB_WORDS;          // closure filter
+        const uint64_t slot = cb + HDR_WORDS + WINDOW_WORDS;         // read together on a visit
+        const uint64_t total = table + cb + HDR_WORDS + ((n + 3) & ~3ull);
+        const uint64_t fit = std::max(total, table + slot);          // a short row's window included
+        auto align = [&](uint64_t x) {
+            if (fit <= LINE_WORDS) {
+                if (x % LINE_WORDS + fit > LINE_WORDS) x = (x + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
+            } else {
+                const uint64_t o = (x + table) % LINE_WORDS;         // closure filter + header + window
+                if (o + slot > LINE_WORDS) x += LINE_WORDS - o;
+            }
+            return x;
+        };
+        w = align(w);
+        if (w < (1ull << 32) && w + fit > (1ull << 32)) w = align(1ull << 32);   // rows stay in a segment
+        const uint64_t unit = (w + table + cb) / HDR_WORDS;
         if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
         S.unit_of_row[r] = (uint32_t)unit;
         S.layout_units[x] = (uint32_t)unit;
-        w += table + HDR_WORDS + ((n + 3) & ~3ull);
+        w += total;
     }
     S.n_units = w / HDR_WORDS;
 }

@@ -1,17 +1,14 @@
 // Internal snapshot representation shared by the host builder (snapshot.cpp), the device
 // engine (engine.hip) and the C-ABI (capi.cpp).
 //
-// HBM layout (one copy per device, read-only after upload):
-//   rows   : RowRec[n_rows], 16 B each, one aligned dwordx4 load per row visit
-//   edges  : u32[n_edges]; bit31 = subject set (bits 0..30 = target row id),
-//            else subject id (bits 0..30 = string id)
-//   row_pp : u32[n_rows], first poisoned page (0-based) or NO_PAGE -- read by expand only
-//   coll   : u64 open-addressing table {edge value -> visit id} for colliding visit keys,
-//            consulted only on rows flagged ROW_SEQ
+// Host tables: rows (RowRec: edge range, flags, effective set / id counts), edges (bit31 = subject
+// set, bits 0..30 = target row id; else a subject id = string id), row_pp (first poisoned page,
+// expand only) and coll (visit ids of colliding Subject.String() keys).  The device arena built
+// from them is described at HDR_WORDS below.
 //
 // A "normal" row stores its effective (check) edges as [subject sets in ORDER BY order]
 // [subject ids sorted by string id == byte order], so a check finds the requested subject id by
-// binary search.  A ROW_SEQ row (materialized wildcard query, or a row holding an edge whose
+// membership.  A ROW_SEQ row (materialized wildcard query, or a row holding an edge whose
 // Subject.String() collides with another subject's) keeps the exact ORDER BY sequence and is
 // walked edge by edge with full visited semantics.
 #pragma once
@@ -47,21 +44,45 @@ constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys l
 // Device arena (one u32 array per device).  Row r occupies
 //   [subject-id table, 2^hlog2 words of 16-B buckets, for rows whose ids do not all fit in the
 //    window (n_ids > 0 and n_sets + n_ids > WINDOW_WORDS)]
-//   [16-B header: n_sets, n_ids, flags | hlog2 << 8, first poisoned page]   <- handle = word / 4
-//   [edges in ORDER BY order; subject sets hold the target's handle]        padded to 16 B
-// A row visit reads the header and the window (the first 4 edge words) with one 32-B access
-// that never straddles a 128-B line; a row that fits in a line is placed in a single line, so
-// its id table is in the line the header came in with.
+//   [closure filter, CB_WORDS words, only for rows some subject set points at (HDR_CLOSURE)]
+//   [16-B header: n_sets, n_ids, flags | hlog2 << 8 | bloom, bloom]   <- handle = word / 4
+//   [edges in ORDER BY order; subject sets hold the target's handle]  padded to 16 B
+// A row visit reads the header and the window (the first 4 edge words) -- and, entering a subject
+// set, one word of its closure filter -- from one 128-B line: closure filter, header and window
+// never straddle a line, and a row that fits in a line is placed in a single line, so its id table
+// is in the line the header came in with.
 constexpr uint32_t HDR_WORDS = 4;
 constexpr uint32_t WINDOW_WORDS = 4;            // edge words read together with the header
 constexpr uint32_t LINE_WORDS = 32;             // 128-B cache line
 constexpr uint32_t BUCKET_WORDS = 4;            // id tables are probed one 16-B bucket at a time
+// The arena is two segments of 2^32 words (16 GiB); no row (id table to last edge) crosses from one
+// to the other, so a position inside a row is a 32-bit word index within its segment.  Handles
+// (31-bit 16-B units) with bit SEG_SHIFT set lie in segment 1.
+constexpr uint32_t SEG_SHIFT = 30;
+constexpr uint32_t SEG_MASK = (1u << SEG_SHIFT) - 1u;
 // header word 2: bits 0..7 flags, 8..12 hlog2, 13..31 bloom bits 32..50; word 3: bloom bits 0..31.
 // The 51-bit bloom filter (2 bits per subject id) summarizes the ids of a row with an id table,
 // so most absent ids are rejected with the header and the table is never probed for them.
 constexpr uint32_t HDR_SEQ = 1u;                // walked edge by edge (ROW_SEQ)
 constexpr uint32_t HDR_POISON = 2u;             // some page fails toInternal (expand: error)
 constexpr uint32_t HDR_POISON0 = 4u;            // the first page fails (check: empty row)
+constexpr uint32_t HDR_CLOSURE = 8u;            // a closure filter precedes the header
+// Closure filter of a row some subject set points at: a 768-bit, one-hash bloom filter of every
+// subject id reachable from the row through any number of subject sets (its own ids included).  A
+// check entering such a row for a requested id the filter rules out skips the row: every node the
+// skipped search would have marked visited lies inside that closure, which never reaches the
+// requested id, so no answer changes (rows whose closure holds a colliding visit key, ROW_SEQ,
+// have all bits set).  Built on the device at upload (closure_pass).
+constexpr uint32_t CB_WORDS = 24;
+KETO_HD inline void closure_bit(uint32_t id, uint32_t& word, uint32_t& bit) {
+    uint32_t h = id * 0x85EBCA77u + 0x165667B1u;
+    h ^= h >> 13;
+    h *= 0xC2B2AE3Du;
+    h ^= h >> 16;
+    const uint32_t p = (uint32_t)(((uint64_t)h * (CB_WORDS * 32u)) >> 32);
+    word = p >> 5;
+    bit = p & 31u;
+}
 constexpr uint32_t BLOOM_BITS = 51;
 KETO_HD inline void bloom_bits(uint32_t id, uint32_t& b1, uint32_t& b2) {
     uint32_t h = id * 0x9E3779B1u + 0x7F4A7C15u;

@@ -57,3 +57,23 @@ def test_csr_bulk_loader_validates_order():
     with pytest.raises(keto_amd.KetoError):
         keto_amd.Snapshot.from_csr([(1, "n")], np.array([1, 1]), np.array([2, 1]), np.array([0, 0]),
                                    np.array([0, 0, 0], dtype=np.uint64), np.zeros(0, np.uint32), device=-1)
+
+
+def test_arena_layout_lines():
+    """compute_layout on the power-law generator: rows some subject set points at carry a closure
+    filter, and filter + header + window (CB + 8 words) fill exactly one 128-B line; every other
+    row's header + window (8 words) never straddles a line; handles are distinct and increasing in
+    arena order."""
+    import numpy as np
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    s = g.host_snapshot()
+    h = s.row_handles(np.arange(g.n_rows, dtype=np.uint32)).astype(np.int64)
+    sets = g.edges[(g.edges & 0x80000000) != 0] & 0x7FFFFFFF
+    target = np.zeros(g.n_rows, dtype=bool)
+    target[sets.astype(np.int64)] = True
+    assert target.any() and (~target).any()
+    word = h * 4
+    assert ((word[target] - 24) % 32 == 0).all()              # filter at a line start, header at +96 B
+    assert (word[~target] % 32 <= 24).all()
+    assert len(np.unique(h)) == len(h)

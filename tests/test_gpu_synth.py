@@ -83,6 +83,24 @@ def test_powerlaw_checks_match_oracle(powerlaw, gmd):
     assert 0.05 < gpu.mean() < 0.95
 
 
+def test_powerlaw_closure_filters_prune(powerlaw):
+    """Subject sets whose closure filter rules the requested id out are skipped (work slot 15) --
+    a large share of the row visits -- and every decision stays the oracle's."""
+    import torch
+    g, snap = powerlaw
+    q = g.queries(20000, seed=77, depth=5)
+    d = torch.from_numpy(snap.with_handles(q).view(np.int32).reshape(-1, 4).copy()).to("cuda:0")
+    out = torch.empty(len(q), dtype=torch.uint8, device="cuda:0")
+    w = snap.check_work_device(d.data_ptr(), len(q), out.data_ptr(), 5)
+    torch.cuda.synchronize()
+    gpu = out.cpu().numpy()
+    tab = g.oracle_table(q, 5)
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), 5, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+    rows, pruned = w[0], w[15]
+    assert pruned > 0.15 * rows, (rows, pruned)
+
+
 def _oracle_expand_nodes(g, tab, row, depth, gmd):
     from oracle.oracle_c import OraNode, OraSubject, lib
     ns = int(g.row_ns[row])
