@@ -157,11 +157,15 @@ class Snapshot:
         self.h = handle
         self.lib = lib
 
+    def close(self):
+        """Release the snapshot (host tables and device arena) now."""
+        if self.h:
+            self.lib.keto_snapshot_release(self.h)
+            self.h = None
+
     def __del__(self):
         try:
-            if self.h:
-                self.lib.keto_snapshot_release(self.h)
-                self.h = None
+            self.close()
         except Exception:
             pass
 

@@ -1524,8 +1524,8 @@ int t0_variant() {
 const char* t0_kernel_name(int var) {
     switch (var) {
         case 0: return "keto::check_wave_kernel<4, false, 4, 16, false>";
-        case 1: return "keto::check_wave_kernel<4, false, 8, 16, false>";
-        case 2: return "keto::check_wave_kernel<4, true, 8, 16, false>";
+        case 1: return "keto::check_wave_kernel<4, false, 4, 8, false>";
+        case 2: return "keto::check_wave_kernel<4, false, 12, 4, false>";
         case 3: return "keto::check_wave_kernel<4, false, 8, 8, false>";
         default: return "keto::check_wave_kernel<8, false, 8, 8, false>";
     }
@@ -1534,8 +1534,8 @@ CheckKernelFn t0_kernel(int var, bool count) {
     // <saved frames, save windows, LDS visit ids, register visit ids>
     switch (var) {
         case 0: return count ? check_wave_kernel<4, false, 4, 16, true> : check_wave_kernel<4, false, 4, 16, false>;
-        case 1: return count ? check_wave_kernel<4, false, 8, 16, true> : check_wave_kernel<4, false, 8, 16, false>;
-        case 2: return count ? check_wave_kernel<4, true, 8, 16, true> : check_wave_kernel<4, true, 8, 16, false>;
+        case 1: return count ? check_wave_kernel<4, false, 4, 8, true> : check_wave_kernel<4, false, 4, 8, false>;
+        case 2: return count ? check_wave_kernel<4, false, 12, 4, true> : check_wave_kernel<4, false, 12, 4, false>;
         case 3: return count ? check_wave_kernel<4, false, 8, 8, true> : check_wave_kernel<4, false, 8, 8, false>;
         default: return count ? check_wave_kernel<8, false, 8, 8, true> : check_wave_kernel<8, false, 8, 8, false>;
     }

@@ -17,6 +17,7 @@
 //     internal/relationtuple/definitions.go:163-169): keys shared by two different subjects get
 //     a shared visit id ("collision class") and their rows take the ordered ROW_SEQ path.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <unordered_set>
@@ -285,7 +286,10 @@ void compute_layout(Snapshot& S) {
         if (keep[r]) S.rows_by_unit[start[33 - band[r]]++] = r;
     }
     S.layout_units.assign(kept, 0);
+    // test hook: start the layout this many words into the arena, so a small graph straddles the
+    // segment boundary at 2^32 words (tests/test_gpu_synth.py)
     uint64_t w = 0;
+    if (const char* base = getenv("KETO_TEST_ARENA_BASE")) w = strtoull(base, nullptr, 0) & ~(uint64_t)(LINE_WORDS - 1);
     for (uint32_t x = 0; x < kept; ++x) {
         const uint32_t r = S.rows_by_unit[x];
         const uint32_t h = S.row_hlog2(r);

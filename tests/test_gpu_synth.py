@@ -118,7 +118,10 @@ def _oracle_expand_nodes(g, tab, row, depth, gmd):
 
 
 def test_powerlaw_expand_matches_oracle(powerlaw):
-    g, snap = powerlaw
+    _expand_matches_oracle(*powerlaw)
+
+
+def _expand_matches_oracle(g, snap):
     rng = np.random.default_rng(5)
     rows = rng.integers(0, g.n_rows, size=300).astype(np.uint32)
     depths = rng.integers(1, 5, size=300).astype(np.int32)
@@ -142,3 +145,37 @@ def test_powerlaw_expand_matches_oracle(powerlaw):
             else:
                 have.append((leaf, 0, int(subj), 0, 0, 0, nc))
         assert have == want, f"root row {row} depth {d}"
+
+
+@pytest.fixture(scope="module")
+def powerlaw_seg1():
+    """The power-law graph laid out from 2^32 - 64K words on: rows in both arena segments and rows
+    bumped past the boundary (a 16 GiB arena on the device)."""
+    import os
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 4096), threads=16)
+    os.environ["KETO_TEST_ARENA_BASE"] = str((1 << 32) - (1 << 16))
+    try:
+        snap = g.snapshot(device=0)
+    finally:
+        del os.environ["KETO_TEST_ARENA_BASE"]
+    yield g, snap
+    snap.close()
+    g.close()
+
+
+@pytest.mark.parametrize("gmd", [5, 9, 16])
+def test_segment1_checks_match_oracle(powerlaw_seg1, gmd):
+    g, snap = powerlaw_seg1
+    h = snap.row_handles(np.arange(g.n_rows, dtype=np.uint32)).astype(np.int64)
+    assert (h < (1 << 30)).any() and (h >= (1 << 30)).mean() > 0.5
+    q = g.queries(20000, seed=300 + gmd, depth=gmd)
+    gpu = _gpu_check(snap, snap.with_handles(q), gmd)
+    tab = g.oracle_table(q, gmd)
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+    assert 0.05 < gpu.mean() < 0.95
+
+
+def test_segment1_expand_matches_oracle(powerlaw_seg1):
+    _expand_matches_oracle(*powerlaw_seg1)

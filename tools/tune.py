@@ -60,7 +60,7 @@ def main():
         w = snap.check_work_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth)
         per = {k: round(x / a.batch, 3) for k, x in zip(
             ("rows", "set_edges", "id_words", "vprobes", "vinserts", "items", "L_req", "L_hdr", "L_edge",
-             "L_idtab", "L_idsearch", "push", "pop", "leaf", "leaf_miss", "leaf_miss_le8"), w[:16])}
+             "L_idtab", "L_idsearch", "push", "pop", "leaf", "leaf_miss", "pruned"), w[:16])}
         best = min(ms)
         print(json.dumps({"variant": v, "ms": [round(x, 3) for x in ms], "checks_per_s": round(a.batch / best * 1e3),
                           "overflow": int(n[1]), "mismatch_vs_first": mism, "work": per}), flush=True)
