@@ -546,7 +546,9 @@ __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_
 }
 
 __device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
-    return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
+    const uint32_t lo = (i & 1u) ? w.y : w.x;              // two-level select: no branches
+    const uint32_t hi = (i & 1u) ? w.w : w.z;
+    return (i & 2u) ? hi : lo;
 }
 __device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
 
@@ -571,6 +573,8 @@ struct LaneVisited {
     __device__ inline void fresh() {
         n = 0;
         f0 = f1 = 0;
+#pragma unroll
+        for (int i = 0; i < RV; ++i) r[i] = NONE32;          // no visit id is NONE32: no count test
     }
     template <class W>
     __device__ inline int test_add(uint32_t vid, uint32_t* lds, uint64_t* tab, uint32_t mask, W& w) {
@@ -581,7 +585,7 @@ struct LaneVisited {
             const uint32_t m = min(n, (uint32_t)(RV + LV));
             bool hit = false;
 #pragma unroll
-            for (int i = 0; i < RV; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
+            for (int i = 0; i < RV; ++i) hit |= r[i] == vid;
             for (uint32_t i = RV; i < m && !hit; ++i) hit = lds[(i - RV) * LDS_STRIDE] == vid;
             if (hit) return 1;
             if (n > (uint32_t)(RV + LV)) {                   // the rest is in the HBM table
