@@ -41,7 +41,7 @@ namespace keto {
     } while (0)
 
 #ifndef KETO_CHECK_WAVES
-#define KETO_CHECK_WAVES 8      // check_kernel: ask for 8 waves per SIMD (register budget 64 VGPRs)
+#define KETO_CHECK_WAVES 7      // check_kernel: ask for 7 waves per SIMD (register budget 72 VGPRs, no spills)
 #endif
 
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
@@ -245,6 +245,35 @@ struct Visited {
     }
 };
 
+// Tier 2 (the few requests whose maps outgrow every hashed table): one 16-bit epoch per visit id
+// of the snapshot, indexed directly.  A test is one 2-B load with no probe chain over a table of
+// 2 x vid_bound bytes (33 MB for 16.7M rows) instead of a hash table of 2^26 entries; a fresh map
+// is one increment, and the table is cleared once every 65535 maps.
+struct DirectVisited {
+    uint64_t* tab;       // the lane's tier-2 table, used as uint16_t[mask + 1 >= 2 * vid_bound + 2]
+    uint32_t mask;
+    uint32_t epoch;
+    uint32_t count;
+    __device__ inline void fresh() {
+        epoch = (epoch & 0xFFFFu) + 1u;
+        if (epoch == 0x10000u) {                   // epoch wrap: clear this lane's table once
+            uint16_t* t = reinterpret_cast<uint16_t*>(tab);
+            for (uint64_t i = 0; i <= (uint64_t)mask; ++i) t[i] = 0;
+            epoch = 1;
+        }
+        count = 0;
+    }
+    template <class W>
+    __device__ inline int test_add(uint32_t vid, W& w) {
+        uint16_t* t = reinterpret_cast<uint16_t*>(tab) + vid;
+        w.vprobe();
+        if (*t == (uint16_t)epoch) return 1;
+        *t = (uint16_t)epoch;
+        w.vinsert();
+        return 0;
+    }
+};
+
 // The first REG_VIDS visit ids of a map live in registers; a map that grows past them spills into
 // the lane's HBM table.  Typical check items mark a handful of subject sets.
 #ifndef KETO_REG_VIDS
@@ -260,12 +289,12 @@ constexpr int LDS_STRIDE = 256;          // lanes per block
 // A visited map of one lane: the first REG_VIDS ids in registers, the next LV in the lane's LDS
 // column, and only the ids beyond those in the lane's HBM table (started fresh on the first
 // overflow), so a test probes HBM only when a map has outgrown registers + LDS.
-template <int LV>
+template <int LV, class VT = Visited>
 struct VisitedRS {
     uint32_t r[REG_VIDS];
     uint32_t n;          // ids held in r + lds; REG_VIDS + LV + 1 = the HBM table holds the rest
     uint32_t* lds;       // this lane's LDS column (stride LDS_STRIDE), or nullptr
-    Visited V;
+    VT V;
     __device__ inline void fresh() { n = 0; }
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
@@ -303,6 +332,7 @@ struct Frame {
     uint16_t fl;       // FR_* flags
 };
 constexpr uint16_t FR_SEQ = 1, FR_TOP = 2, FR_OV = 4;
+constexpr uint16_t FR_WV = 8;   // the frame's edge block (tier 0: window) holds the block of `pos`
 
 template <int N>
 struct LocalStack {
@@ -360,16 +390,66 @@ struct TierArgs {
 };
 
 // ------------------------------------------------------------------ check
-// Batched SubjectIsAllowed (internal/check/engine.go:36-123) as a per-lane state machine.
-// A lane owns one request at a time; each loop iteration does ONE of
+__device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
+    const uint32_t lo = (i & 1u) ? w.y : w.x;              // two-level select: no branches
+    const uint32_t hi = (i & 1u) ? w.w : w.z;
+    return (i & 2u) ? hi : lo;
+}
+__device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
+
+// Saved frames of check_kernel carry the 16-B edge block of their position (when the frame had it),
+// so the walk resumes after a pop without reloading it.  GlobalStack tiers give each lane
+// 2 x frames entries (frame, block, frame, block, ...); LocalStack tiers keep both in scratch.
+template <class Stack>
+struct CheckStack;
+template <int N>
+struct CheckStack<LocalStack<N>> {
+    Frame f[N];
+    uint4 b[N];
+    __device__ inline CheckStack(const TierArgs&, uint32_t) {}
+    __device__ static constexpr int cap() { return N; }
+    __device__ inline void save(int i, const Frame& x, const uint4& blk) {
+        f[i] = x;
+        b[i] = blk;
+    }
+    __device__ inline Frame load(int i, uint4& blk) {
+        blk = b[i];
+        return f[i];
+    }
+};
+template <>
+struct CheckStack<GlobalStack> {
+    uint4* p;           // this lane's frames: p[2i] = frame i, p[2i + 1] = its edge block
+    int n;
+    __device__ inline CheckStack(const TierArgs& ta, uint32_t slot)
+        : p(reinterpret_cast<uint4*>(ta.gstack + (uint64_t)slot * ta.gstack_n)), n(ta.gstack_n / 2) {}
+    __device__ inline int cap() const { return n; }
+    __device__ inline void save(int i, const Frame& x, const uint4& blk) {
+        reinterpret_cast<Frame*>(p)[2 * i] = x;
+        p[2 * i + 1] = blk;
+    }
+    __device__ inline Frame load(int i, uint4& blk) {
+        const uint4 a = p[2 * i];
+        blk = p[2 * i + 1];
+        return Frame{(uint64_t)a.x | ((uint64_t)a.y << 32), a.z, (uint16_t)(a.w & 0xFFFFu), (uint16_t)(a.w >> 16)};
+    }
+};
+
+// Batched SubjectIsAllowed (internal/check/engine.go:36-123) as a per-lane state machine; the
+// deep-request tier 0 (max-depth > 9) and the overflow tiers 1 and 2 of every depth.  A lane owns
+// one request at a time; each loop iteration does ONE of
 //   (a) fetch the lane's next request, or
-//   (b) one edge of the current row: the top-level row (FR_TOP) starts a fresh visited map per
+//   (b) pop a finished row, or
+//   (c) one edge of the current row: the top-level row (FR_TOP) starts a fresh visited map per
 //       subject set (the shadowed ctx at engine.go:48), deeper rows test-and-set it
 //       (graph_utils.go:13-35), in ORDER BY order,
-// then, if (a) or (b) produced one, enters a row: reads its header, looks the requested id up in
-// it, and pushes it as the current frame.  A lane that decides a request takes the next one on the
-// following iteration, so a wave never waits for its slowest request.  Only a subject set reached
-// with remaining depth >= 2 is entered (engine.go:65-69,88-91).
+// then, if (a) or (c) produced one, enters a row.  Long searches here are latency-bound chains of
+// dependent accesses, so the kernel keeps them short: a row's header comes with its window (the
+// first 16-B edge block) and, for a subject set, the requested id's closure-filter word, all from
+// one line; that load is issued for a candidate child BEFORE its visited test, so the header and
+// the HBM visited probe are in flight together; edges are read a 16-B block at a time and saved
+// frames keep their block; the header bloom filter rules most absent ids out without the id table.
+// Only a subject set reached with remaining depth >= 2 is entered (engine.go:65-69,88-91).
 template <class Stack, bool COUNT, int TIER>
 __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
                                                     uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
@@ -377,21 +457,14 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
-    constexpr int LDS_FRAMES = is_lds_stack<Stack>::frames;
-    __shared__ uint2 lds_frames[LDS_FRAMES * LDS_STRIDE];
-    VisitedRS<LDS_VIDS> V;
+    VisitedRS<LDS_VIDS, typename std::conditional<TIER == 2, DirectVisited, Visited>::type> V;
     V.n = 0;
     V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
     V.V.count = 0;
-    Stack st;
-    if constexpr (std::is_same<Stack, GlobalStack>::value) {
-        st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
-        st.n = ta.gstack_n;
-    }
-    if constexpr (is_lds_stack<Stack>::value) st.col = lds_frames + threadIdx.x;
+    CheckStack<Stack> st(ta, slot);
     Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
     // each lane owns a contiguous run of requests, so consecutive fetches share request lines
@@ -399,14 +472,20 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     uint32_t j = slot * per;
     const uint32_t j_end = min(total, j + per);
     bool busy = false;           // a request is in flight on this lane
-    uint32_t qi = 0, T = 0, tval = 0;
+    uint32_t qi = 0, T = 0;
     bool tset = false;
+    uint32_t cwb = 0;            // T's closure-filter word << 5 | bit
     Frame cur{0, 0, 0, 0};
     const uint32_t* ce = s.arena;   // arena of the current frame
+    uint4 blk = make_uint4(0, 0, 0, 0);
+    uint64_t blk_at = ~0ull;        // word index of the 16-B edge block held in blk
     int sp = 0;
     for (;;) {
         uint32_t enter = NONE32;     // row handle to enter this iteration
         uint16_t enter_k = 0, enter_fl = 0;
+        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);   // its header and window
+        uint32_t cbw = NONE32;       // its closure-filter word of T (subject sets only)
+        const uint32_t* ea = s.arena;   // its arena
         int res = -1;                // >= 0: request decided (RES_*)
         if (!busy) {
             if (j >= j_end) break;
@@ -423,44 +502,70 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             busy = true;
             tset = (qq.flags & 1u) != 0;
             T = qq.target;
-            tval = tset ? (EDGE_SET | T) : T;
+            {
+                uint32_t cwd, cbit;
+                closure_bit(T, cwd, cbit);
+                cwb = cwd << 5 | cbit;
+            }
             sp = 0;
             enter = qq.row;
             enter_k = (uint16_t)d;
             enter_fl = FR_TOP;
+            uint64_t hw;
+            if (enter >= ov.base) {
+                ea = ov.arena;
+                hw = (uint64_t)(enter - ov.base) * HDR_WORDS;
+            } else {
+                hw = (uint64_t)enter * HDR_WORDS;
+            }
+            h0 = *reinterpret_cast<const uint4*>(ea + hw);
+            h1 = *reinterpret_cast<const uint4*>(ea + hw + HDR_WORDS);
         } else if (cur.left == 0) {                               // row exhausted: pop
             if (--sp == 0) {
                 res = RES_FALSE;
             } else {
-                const uint16_t k = cur.k + 1;
-                cur = st.load(sp - 1);
-                cur.k = k;
+                cur = st.load(sp - 1, blk);                       // with its own remaining depth
+                blk_at = (cur.fl & FR_WV) ? (cur.pos & ~3ull) : ~0ull;
                 w.pop();
                 ce = (cur.fl & FR_OV) ? ov.arena : s.arena;
             }
         } else {
-            const uint32_t e = ce[cur.pos];
-            w.edge_at(ce + cur.pos);
+            const uint64_t bw = cur.pos & ~3ull;
+            if (bw != blk_at) {                                   // next 16-B block of the row
+                blk = *reinterpret_cast<const uint4*>(ce + bw);
+                blk_at = bw;
+                w.edge_at(ce + bw);
+            }
+            const uint32_t e = win_at(blk, (uint32_t)cur.pos & 3u);
+            const uint32_t tval = tset ? (EDGE_SET | T) : T;
             ++cur.pos;
             --cur.left;
             w.edge();
             if (e & EDGE_SET) {
-                uint32_t vid = e & EDGE_VAL;
+                const uint32_t child = e & EDGE_VAL;
+                uint32_t vid = child;
                 if (cur.fl & FR_SEQ) {
                     uint32_t c = coll_lookup(s, e);
                     if (c != NONE32) vid = c;
                 }
-                int t;
+                // a child that would be entered if new: its header, window and filter word are
+                // loaded now, in flight together with the visited probe below
+                if (cur.k >= 2 && !(tset && e == tval)) {
+                    const uint64_t hw = (uint64_t)child * HDR_WORDS;
+                    h0 = *reinterpret_cast<const uint4*>(s.arena + hw);
+                    h1 = *reinterpret_cast<const uint4*>(s.arena + hw + HDR_WORDS);
+                    if (!tset) cbw = s.arena[hw - CB_WORDS + (cwb >> 5)];     // every set target has a filter
+                }
                 if (cur.fl & FR_TOP) {                            // fresh map per top-level tuple
                     V.fresh();
                     w.item();
                 }
-                t = V.test_add(vid, w);
+                const int t = V.test_add(vid, w);
                 if (t == 2) res = RES_OVERFLOW;
                 else if (t == 0) {
                     if (tset && e == tval) res = RES_TRUE;        // engine.go:54-57
                     else if (cur.k >= 2) {                        // remaining depth after the hop >= 1
-                        enter = e & EDGE_VAL;
+                        enter = child;
                         enter_k = cur.k - 1;
                         enter_fl = 0;
                     }
@@ -476,28 +581,60 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             }
         }
         if (enter != NONE32) {
-            const RowView rv = load_row(s, ov, enter);
+            const uint32_t n_sets = h0.x, n_ids = h0.y;
+            const bool seq = (h0.z & HDR_SEQ) != 0;
+            const uint32_t hl = (h0.z >> 8) & 31u;
+            const bool cb = (h0.z & HDR_CLOSURE) != 0;
+            const uint64_t beg = (enter >= ov.base ? (uint64_t)(enter - ov.base) : (uint64_t)enter) * HDR_WORDS + HDR_WORDS;
             w.row();
-            w.header(rv.a + rv.beg - HDR_WORDS);
-            if (rv.closure && !tset && !(enter_fl & FR_TOP) && !closure_has(rv, T)) {
+            w.header(ea + beg - HDR_WORDS);
+            if (cb && !tset && !(enter_fl & FR_TOP) && !((cbw >> (cwb & 31u)) & 1u)) {
                 enter = NONE32;                                   // T is not below this set: skip it
                 w.pruned();
-            } else if (!rv.seq && !tset && row_has_id(rv, T, w)) {
-                res = RES_TRUE;
-            } else if (sp > st.cap()) {        // saved frames live in st[0 .. sp-1)
-                res = RES_OVERFLOW;
-            } else if constexpr (is_lds_stack<Stack>::value) {
-                if (sp > 0 && !st.fits(cur)) res = RES_OVERFLOW;
+            } else if (!seq && !tset && n_ids > 0) {              // is the requested id in the row?
+                bool hit = false;
+                if (hl == 0) {                                    // all ids are in the window
+#pragma unroll
+                    for (uint32_t i = 0; i < WINDOW_WORDS; ++i)
+                        hit |= (i >= n_sets) & (i < n_sets + n_ids) & (win_at(h1, i) == T);
+                    w.idread(n_ids);
+                } else {
+                    uint32_t b1, b2;
+                    bloom_bits(T, b1, b2);
+                    if (bloom_has(h0.z, h0.w, b1) && bloom_has(h0.z, h0.w, b2)) {
+                        const uint32_t nb = (1u << hl) / BUCKET_WORDS;
+                        const uint64_t tb = beg - HDR_WORDS - (cb ? CB_WORDS : 0u) - (1ull << hl);
+                        for (uint32_t b = mix32(T) & (nb - 1);; b = (b + 1) & (nb - 1)) {
+                            const uint4 v = *reinterpret_cast<const uint4*>(ea + tb + (uint64_t)b * BUCKET_WORDS);
+                            w.idread(BUCKET_WORDS);
+                            w.id_at(ea + tb + (uint64_t)b * BUCKET_WORDS, true);
+                            if (has4(v, T)) {
+                                hit = true;
+                                break;
+                            }
+                            if (has4(v, NONE32)) break;
+                        }
+                    }
+                }
+                if (hit) res = RES_TRUE;
             }
+            // the parent is saved only if it has edges left (saved frames: st[0 .. sp-1)); an
+            // exhausted one is replaced, and the child returns straight to the grandparent
+            const bool save = sp > 0 && cur.left > 0;
+            if (enter != NONE32 && res < 0 && save && sp > st.cap()) res = RES_OVERFLOW;
             if (enter != NONE32 && res < 0) {
-                if (sp > 0) {
-                    st.save(sp - 1, cur);
+                if (save) {
+                    Frame sv = cur;
+                    sv.fl = (blk_at == (cur.pos & ~3ull)) ? (uint16_t)(cur.fl | FR_WV) : (uint16_t)(cur.fl & ~FR_WV);
+                    st.save(sp - 1, sv, blk);
                     w.push();
                 }
-                cur = Frame{rv.beg, rv.n_sets, enter_k,
-                            (uint16_t)(enter_fl | (rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
-                ce = rv.a;
-                ++sp;
+                cur = Frame{beg, n_sets, enter_k,
+                            (uint16_t)(enter_fl | (seq ? FR_SEQ : 0) | (ea != s.arena ? FR_OV : 0))};
+                ce = ea;
+                blk = h1;
+                blk_at = beg;
+                if (save || sp == 0) ++sp;
             }
         }
         if (res >= 0) {
@@ -512,7 +649,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     }
     ta.slot_epoch[slot] = V.V.epoch;
     if constexpr (COUNT) {
-        for (int i = 0; i < 13; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
+        for (int i = 0; i < 16; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
     }
 }
 
@@ -531,7 +668,6 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
 // saved, overflows to the next tier (check_kernel).  Lane control state is one packed word.
 constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
 constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // saved lkf = left | k << 23 | fl << 28
-constexpr uint16_t FR_WV = 8;                        // the window holds the block of `pos`
 // control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23 | nq2 24
 // | cb 25 (the current row has a closure filter, so its id table starts CB_WORDS further down)
 // | seg 26 (the current row lies in arena segment 1: positions are 32-bit words within a segment)
@@ -544,13 +680,6 @@ __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_
     const uint32_t m = ((1u << wd) - 1u) << off;
     return (c & ~m) | ((v << off) & m);
 }
-
-__device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
-    const uint32_t lo = (i & 1u) ? w.y : w.x;              // two-level select: no branches
-    const uint32_t hi = (i & 1u) ? w.w : w.z;
-    return (i & 2u) ? hi : lo;
-}
-__device__ inline bool has4(const uint4& v, uint32_t t) { return v.x == t || v.y == t || v.z == t || v.w == t; }
 
 // requests j and j + 1 (if in the run) straight into the wave's LDS prefetch slots (global_load_lds:
 // no VGPR destination; lane L's 16 B land at wave_base + 16 L, i.e. lds_nq[tid] and
@@ -1095,7 +1224,9 @@ void free_tier(Tier& t) {
 
 void ensure_tier(Tier* set, int level, uint32_t n_slots, uint32_t cap, int gstack_n) {
     Tier& t = set[level];
-    if (t.n_slots == n_slots && t.cap == cap && t.gstack_n == gstack_n) return;
+    // a workspace with at least as many slots of the same shape is reused (kernels index slots only
+    // below their grid size), so batches of changing sizes do not reallocate
+    if (t.n_slots >= n_slots && t.cap == cap && t.gstack_n == gstack_n && t.vtab) return;
     free_tier(t);
     uint64_t acc = 0;
     t.n_slots = n_slots;
@@ -1581,6 +1712,7 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     const int fr = std::max(1, gmd - 1);
     const int kind = fr <= 4 ? 0 : fr <= 8 ? 1 : 2;
     p.frames[0] = kind == 2 ? std::min(fr, 64) : 0;
+    for (int l = 0; l < 3; ++l) p.frames[l] *= 2;   // check frames on GlobalStack carry their edge block
     const int var = kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : T0_VARIANTS + 1;
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
@@ -1596,21 +1728,27 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     p.slots[0] = (uint32_t)std::min<uint64_t>(D.v1_lanes[var], ((uint64_t)n + 255) / 256 * 256);
     if (kind == 2) {
         // deep requests (nested groups) visit thousands of sets: give every tier-0 lane a table
-        // of up to 8K ids and tier 1 32K lanes of up to 64K ids, within 1/4 of device memory
+        // of up to 16K entries and tier 1 128K lanes of up to 64K entries, within half of device
+        // memory (tables are reused across batches; ~137 GB on a 288 GB MI355X)
         size_t free_b = 0, total_b = 0;
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
         uint64_t held = 0;
         for (int l = 0; l < 2; ++l) held += (uint64_t)D.tiers[l].n_slots * D.tiers[l].cap * sizeof(uint64_t);
-        const uint64_t budget = std::min<uint64_t>(total_b / 4, (free_b + held) / 2) / 2;
+        uint64_t budget = std::min<uint64_t>(total_b / 2, (free_b + held) * 6 / 10);
+        if (const char* eb = getenv("KETO_DEEP_BUDGET_GB"))
+            budget = std::min<uint64_t>((uint64_t)atoi(eb) << 30, (free_b + held) * 3 / 4);
         const uint32_t full = pow2_at_least(2ull * D.vid_bound + 2);
         auto fit = [&](uint32_t slots, uint32_t lo, uint32_t hi) {
             uint32_t c = lo;
             while (c < hi && (uint64_t)slots * (2ull * c) * sizeof(uint64_t) <= budget) c *= 2;
             return std::min(c, full);
         };
-        p.cap[0] = fit(p.slots[0], 256, 8192);
-        p.slots[1] = (uint32_t)std::min<uint64_t>(32768, ((uint64_t)n + 255) / 256 * 256);
-        p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, 65536));
+        const char* e0 = getenv("KETO_T0_CAP");
+        const char* e1 = getenv("KETO_T1_SLOTS");
+        const char* e2 = getenv("KETO_T1_CAP");
+        p.cap[0] = fit(p.slots[0], 256, e0 ? (uint32_t)atoi(e0) : 16384u);
+        p.slots[1] = (uint32_t)std::min<uint64_t>(e1 ? (uint32_t)atoi(e1) : 131072u, ((uint64_t)n + 255) / 256 * 256);
+        p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, e2 ? (uint32_t)atoi(e2) : 65536u));
     }
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
@@ -1635,6 +1773,8 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
                       go(t0_kernel(var, dwork != nullptr));
                   else if (level == 0)
                       dwork ? go(check_kernel<GlobalStack, true, 0>) : go(check_kernel<GlobalStack, false, 0>);
+                  else if (level == 2)         // direct-indexed visited tables (DirectVisited)
+                      dwork ? go(check_kernel<GlobalStack, true, 2>) : go(check_kernel<GlobalStack, false, 2>);
                   else if (local)
                       dwork ? go(check_kernel<LocalStack<16>, true, 1>) : go(check_kernel<LocalStack<16>, false, 1>);
                   else

@@ -9,7 +9,7 @@ restatement timed on the same sample and host cores.
      the C restatement; GPU: the same 10,000 checks.
   #2 Drive-like: the power-law docs/folders/groups generator at 10,000,000 tuples, 1,000,000
      checks, max-depth 5.
-  #3 nested groups: chains of up to 32 nested groups with back-edges (cycles), ~100M tuples,
+  #3 nested groups: chains of up to 32 nested groups with back-edges (cycles), 100M tuples,
      1,000,000 checks with request depths {5, 16, 32}, global max-depth 32.
   #5 expand: 100,000 roots sampled from #3's rows, global max-depth 5; trees/s for count + fill
      passes; a sample of trees compared node by node (pre-order, child order included) with the
@@ -39,8 +39,7 @@ def timed_checks(snap, qd, n, gmd, reps=3):
     d_q = torch.from_numpy(qd.view(np.uint8)).to("cuda:0")
     d_out = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     sp = torch.cuda.current_stream().cuda_stream
-    w = min(n, 65536)                                        # warm-up: workspaces, code objects
-    snap.check_batch_device(d_q.data_ptr(), w, d_out.data_ptr(), gmd, sp)
+    snap.check_batch_device(d_q.data_ptr(), n, d_out.data_ptr(), gmd, sp)   # warm-up: workspaces, code objects
     torch.cuda.synchronize()
     best, tiers = None, None
     for r in range(reps):
@@ -92,12 +91,31 @@ def config1(a):
             "mismatches": mism}
 
 
+WORK_KEYS = ("rows", "set_edges", "id_words", "vprobes", "vinserts", "items", "L_req", "L_hdr", "L_edge",
+             "L_idtab", "L_idsearch", "push", "pop", "leaf", "leaf_miss", "pruned")
+
+
+def work_counters(snap, qd, n, gmd):
+    """Per-check traversal counters of the same batch (instrumented kernels, all tiers)."""
+    import torch
+    d_q = torch.from_numpy(qd.view(np.uint8)).to("cuda:0")
+    d_out = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    w = snap.check_work_device(d_q.data_ptr(), n, d_out.data_ptr(), gmd)
+    return {k: round(v / n, 3) for k, v in zip(WORK_KEYS, w)}
+
+
 def checks_config(a, name, g, q, gmd, sample, reps=3):
     log(f"{name}: {g.n_edges} tuples; snapshot")
     snap = g.snapshot(device=0)
     qd = snap.with_handles(q)
     n = len(q)
     dt, (ms, cnt), out = timed_checks(snap, qd, n, gmd, reps)
+    work = work_counters(snap, qd, n, gmd) if a.work else None
+    if a.no_parity:
+        return {"config": name, "tuples": int(g.n_edges), "rows": int(g.n_rows), "checks": n,
+                "gpu": {"checks_per_s": round(n / dt, 1), "wall_ms": round(dt * 1e3, 3),
+                        "tier_ms": [round(x, 3) for x in ms], "tier_requests": [int(x) for x in cnt]},
+                "work": work}
     s = q[:sample]
     log(f"{name}: oracle table over {sample} requests")
     tab = g.oracle_table(s, gmd)
@@ -109,6 +127,7 @@ def checks_config(a, name, g, q, gmd, sample, reps=3):
             "gpu": {"checks_per_s": round(n / dt, 1), "wall_ms": round(dt * 1e3, 3),
                     "tier_ms": [round(x, 3) for x in ms], "tier_requests": [int(x) for x in cnt],
                     "kernel": snap.check_kernel_name(gmd)},
+            "work": work,
             "allowed_fraction": round(float(out.mean()), 4),
             "parity": {"sample": sample, "mismatches": int((ref != out[:sample]).sum())},
             "cpu_port": {"checks_per_s": round(sample / t_cpu, 1), "cores": a.threads,
@@ -185,6 +204,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,3,5")
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--work", action="store_true", help="add per-check traversal counters (instrumented run)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle legs (tuning sweeps)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)

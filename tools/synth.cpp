@@ -194,6 +194,23 @@ int synth_generate_nested(const synth_params* p, uint32_t chain, int threads, sy
         nset[r] = k;
         nid[r] = (uint32_t)pareto(g, 2.0, 1.5, 1u << 16);
     });
+    // hit target_edges exactly (when set) by spreading extra / fewer direct members over groups
+    if (p->target_edges) {
+        int64_t diff = (int64_t)p->target_edges;
+        for (uint64_t r = 0; r < R; ++r) diff -= (int64_t)nset[r] + nid[r];
+        const uint64_t stride = 0x9E3779B1ull % R | 1;   // odd: a permutation of the rows when R is 2^k
+        for (uint64_t i = 0; diff != 0 && i < 64 * R; ++i) {
+            const uint64_t r = (i * stride) % R;
+            if (diff > 0) {
+                ++nid[r];
+                --diff;
+            } else if (nid[r] > 0) {
+                --nid[r];
+                ++diff;
+            }
+        }
+        if (diff != 0) return -3;
+    }
     out->n_rows = (uint32_t)R;
     out->row_ns = (int32_t*)malloc(R * sizeof(int32_t));
     out->row_obj = (uint32_t*)malloc(R * sizeof(uint32_t));

@@ -62,7 +62,7 @@ def lib():
 
 
 # BASELINE.json config #3: nested group membership, chains up to 32, cycles (seed 3)
-NESTED_100M = dict(n_docs=0, n_folders=0, n_groups=1 << 24, n_users=1 << 24, target_edges=0, seed=3)
+NESTED_100M = dict(n_docs=0, n_folders=0, n_groups=1 << 24, n_users=1 << 24, target_edges=100_000_000, seed=3)
 
 
 class SynthGraph:
