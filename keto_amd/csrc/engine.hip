@@ -52,6 +52,7 @@ struct DevSnap {
     const uint32_t* arena;    // main arena (u32 words; tier 0 adds 2^32 words for segment 1)
     const uint64_t* coll;     // (edge value << 32) | visit id ; empty = ~0
     uint32_t coll_mask;       // 0 = no collisions
+    uint32_t n_units;         // handles of the main arena are < n_units (DirectVisited's class base)
 };
 
 struct DevOverlay {           // batch-local wildcard rows (top-level / root only)
@@ -245,19 +246,23 @@ struct Visited {
     }
 };
 
-// Tier 2 (the few requests whose maps outgrow every hashed table): one 16-bit epoch per visit id
-// of the snapshot, indexed directly.  A test is one 2-B load with no probe chain over a table of
-// 2 x vid_bound bytes (33 MB for 16.7M rows) instead of a hash table of 2^26 entries; a fresh map
-// is one increment, and the table is cleared once every 65535 maps.
+// Tier 2 (the few requests whose maps outgrow every hashed table): one 16-bit epoch per possible
+// visit id (main-arena handle or collision class), indexed directly.  A test is one 2-B load with
+// no probe chain, over 2 B per arena unit instead of a hash table of 2^(log2(2 x rows) + 1) 8-B
+// entries; a fresh map is one increment, and the table is cleared once every 65535 maps.
 struct DirectVisited {
-    uint64_t* tab;       // the lane's tier-2 table, used as uint16_t[mask + 1 >= 2 * vid_bound + 2]
+    uint64_t* tab;       // the lane's tier-2 table (mask + 1 words), used as uint16_t[4 (mask + 1)]
     uint32_t mask;
     uint32_t epoch;
     uint32_t count;
+    uint32_t base;       // n_units: collision class c has index base + c
+    // visit ids are main-arena handles (< n_units; set edges never point into a batch overlay)
+    // or VID_CLASS | class; both map to one dense index below 4 (mask + 1)
+    __device__ inline uint32_t index(uint32_t vid) const { return (vid & VID_CLASS) ? base + (vid & ~VID_CLASS) : vid; }
     __device__ inline void fresh() {
         epoch = (epoch & 0xFFFFu) + 1u;
         if (epoch == 0x10000u) {                   // epoch wrap: clear this lane's table once
-            uint16_t* t = reinterpret_cast<uint16_t*>(tab);
+            uint64_t* t = tab;
             for (uint64_t i = 0; i <= (uint64_t)mask; ++i) t[i] = 0;
             epoch = 1;
         }
@@ -265,7 +270,7 @@ struct DirectVisited {
     }
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
-        uint16_t* t = reinterpret_cast<uint16_t*>(tab) + vid;
+        uint16_t* t = reinterpret_cast<uint16_t*>(tab) + index(vid);
         w.vprobe();
         if (*t == (uint16_t)epoch) return 1;
         *t = (uint16_t)epoch;
@@ -464,6 +469,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
     V.V.count = 0;
+    if constexpr (TIER == 2) V.V.base = s.n_units;
     CheckStack<Stack> st(ta, slot);
     Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
@@ -1174,6 +1180,8 @@ struct DeviceState {
     uint32_t coll_mask = 0;
     uint64_t bytes = 0;
     uint32_t vid_bound = 0;       // distinct visit ids that can exist (rows + collision classes)
+    uint32_t n_units = 0;         // main-arena handles are < n_units
+    uint32_t n_coll = 0;          // collision classes
     std::mutex mu;                // one batch at a time per snapshot (workspaces are shared)
     Tier tiers[3];                // check workspaces
     Tier etiers[3];               // expand workspaces
@@ -1194,7 +1202,7 @@ struct DeviceState {
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
 
-    DevSnap view() const { return DevSnap{arena, coll, coll_mask}; }
+    DevSnap view() const { return DevSnap{arena, coll, coll_mask, n_units}; }
 };
 
 namespace {
@@ -1495,6 +1503,8 @@ void device_upload(Snapshot& S, int device) {
     D->bytes = acc;
     // a map holds at most one id per row / collision class (+ an expand root outside the rows)
     D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
+    D->n_units = (uint32_t)S.n_units;
+    D->n_coll = S.n_coll_keys;
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     for (auto& e : D->ev) HIP_OK(hipEventCreate(&e));
     S.device = device;
@@ -1713,6 +1723,19 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
     const int kind = fr <= 4 ? 0 : fr <= 8 ? 1 : 2;
     p.frames[0] = kind == 2 ? std::min(fr, 64) : 0;
     for (int l = 0; l < 3; ++l) p.frames[l] *= 2;   // check frames on GlobalStack carry their edge block
+    {
+        // tier 2 keeps one 16-bit epoch per possible visit id (DirectVisited): 2 B per arena unit
+        // and collision class, as many lanes (<= 256, a power of two) as 16 GiB allows
+        const uint64_t ids = (uint64_t)D.n_units + D.n_coll + 1;
+        if ((ids + 3) / 4 > 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "tier-2 visited table exceeds 2^32 words"};
+        p.cap[2] = (uint32_t)((ids + 3) / 4);
+        const uint64_t per = (uint64_t)p.cap[2] * sizeof(uint64_t);
+        const char* es = getenv("KETO_T2_SLOTS");
+        const uint64_t want = std::min<uint64_t>(es ? (uint64_t)atoi(es) : 256u, std::max<uint64_t>(1, (16ull << 30) / per));
+        uint32_t s2 = 1;
+        while (s2 * 2 <= want) s2 *= 2;
+        p.slots[2] = s2;
+    }
     const int var = kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : T0_VARIANTS + 1;
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
