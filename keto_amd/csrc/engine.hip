@@ -244,6 +244,7 @@ struct Visited {
             i = (i + 1) & mask;
         }
     }
+    __device__ inline void release() {}
 };
 
 // Tier 2 (the few requests whose maps outgrow every hashed table): one 16-bit epoch per possible
@@ -276,6 +277,96 @@ struct DirectVisited {
         *t = (uint16_t)epoch;
         w.vinsert();
         return 0;
+    }
+    __device__ inline void release() {}
+};
+
+// Tier 1 of deep batches: a hashed map (Visited) that, when it outgrows the lane's table, borrows
+// one of tier 2's direct tables (DirectVisited) for the rest of the request instead of sending the
+// request up a tier, where it would restart from scratch and run after every tier-1 request.  The
+// hashed table keeps the map's earlier ids (read-only from then on); new ids go to the direct
+// table.  Tier 2 runs after tier 1 on the same stream and its lanes own the same tables, so the
+// per-table 16-bit epoch lives in tier 2's slot_epoch and is handed over on release.  With every
+// table borrowed, a map that overflows moves up a tier as before.
+struct PromoVisited {
+    uint64_t* tab;       // hashed: the lane's tier-1 table
+    uint32_t mask;
+    uint32_t epoch;
+    uint32_t count;
+    uint32_t base;       // n_units (DirectVisited::index)
+    uint64_t* pool;      // tier 2's tables, pool_n x (pool_mask + 1) words
+    uint32_t pool_mask, pool_n;
+    uint32_t* pool_epoch;
+    uint32_t* pool_busy; // bitmap of borrowed tables
+    int d;               // borrowed table, -1 = none
+    uint32_t depoch;     // its epoch for the current map
+    bool live;           // the hashed table holds ids of the current map
+    __device__ inline Visited hashed() { return Visited{tab, mask, epoch, count}; }
+    __device__ inline DirectVisited direct() {
+        return DirectVisited{pool + (uint64_t)d * (pool_mask + 1ull), pool_mask, depoch, 0, base};
+    }
+    __device__ inline void fresh() {
+        Visited H = hashed();
+        H.fresh();
+        epoch = H.epoch;
+        count = H.count;
+        if (d >= 0) {
+            DirectVisited D = direct();
+            D.fresh();
+            depoch = D.epoch;
+            live = false;
+        }
+    }
+    __device__ inline bool borrow() {
+        for (uint32_t wi = 0; wi * 32u < pool_n; ++wi) {
+            const uint32_t valid = pool_n - wi * 32u >= 32u ? NONE32 : (1u << (pool_n - wi * 32u)) - 1u;
+            uint32_t cur = __hip_atomic_load(pool_busy + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (~cur & valid) {
+                const uint32_t b = __ffs(~cur & valid) - 1u;
+                const uint32_t old = atomicOr(pool_busy + wi, 1u << b);
+                if (!(old & (1u << b))) {
+                    __threadfence();                 // acquire: the last owner's epoch and marks
+                    d = (int)(wi * 32u + b);
+                    depoch = pool_epoch[d];
+                    DirectVisited D = direct();
+                    D.fresh();                       // a new map on the borrowed table
+                    depoch = D.epoch;
+                    return true;
+                }
+                cur = old | (1u << b);
+            }
+        }
+        return false;
+    }
+    __device__ inline void release() {
+        if (d < 0) return;
+        pool_epoch[d] = depoch;
+        __threadfence();                             // release: marks and epoch before the bit
+        atomicAnd(pool_busy + (d >> 5), ~(1u << (d & 31)));
+        d = -1;
+    }
+    template <class W>
+    __device__ inline int test_add(uint32_t vid, W& w) {
+        if (d < 0) {
+            Visited H = hashed();
+            const int t = H.test_add(vid, w);
+            epoch = H.epoch;
+            count = H.count;
+            if (t != 2 || pool_n == 0 || !borrow()) return t;
+            live = true;                             // vid is in neither table: add it below
+        } else if (live) {
+            uint32_t i = mix32(vid) & mask;          // earlier ids of this map (table <= half full)
+            const uint64_t want = ((uint64_t)epoch << 32) | vid;
+            for (;;) {
+                const uint64_t e = tab[i];
+                w.vprobe();
+                if ((uint32_t)(e >> 32) != epoch) break;
+                if (e == want) return 1;
+                i = (i + 1) & mask;
+            }
+        }
+        DirectVisited D = direct();
+        return D.test_add(vid, w);
     }
 };
 
@@ -392,6 +483,11 @@ struct TierArgs {
     const uint32_t* in_count;
     uint32_t* out_list;      // overflowed requests
     uint32_t* out_count;
+    // tier 1 of deep batches: tier 2's direct tables, borrowed on overflow (PromoVisited)
+    uint64_t* pool;
+    uint32_t pool_mask, pool_n;
+    uint32_t* pool_epoch;
+    uint32_t* pool_busy;
 };
 
 // ------------------------------------------------------------------ check
@@ -462,7 +558,8 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
-    VisitedRS<LDS_VIDS, typename std::conditional<TIER == 2, DirectVisited, Visited>::type> V;
+    VisitedRS<LDS_VIDS, typename std::conditional<TIER == 2, DirectVisited,
+                                                  typename std::conditional<TIER == 1, PromoVisited, Visited>::type>::type> V;
     V.n = 0;
     V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
@@ -470,6 +567,17 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     V.V.epoch = ta.slot_epoch[slot];
     V.V.count = 0;
     if constexpr (TIER == 2) V.V.base = s.n_units;
+    if constexpr (TIER == 1) {
+        V.V.base = s.n_units;
+        V.V.pool = ta.pool;
+        V.V.pool_mask = ta.pool_mask;
+        V.V.pool_n = ta.pool_n;
+        V.V.pool_epoch = ta.pool_epoch;
+        V.V.pool_busy = ta.pool_busy;
+        V.V.d = -1;
+        V.V.depoch = 0;
+        V.V.live = false;
+    }
     CheckStack<Stack> st(ta, slot);
     Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
@@ -650,6 +758,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             } else {
                 allowed[qi] = (uint8_t)res;
             }
+            V.V.release();                                        // a borrowed tier-2 table (tier 1)
             busy = false;
         }
     }
@@ -1187,6 +1296,7 @@ struct DeviceState {
     Tier etiers[3];               // expand workspaces
     uint32_t v1_lanes[16] = {};   // resident lanes of the tier-0 check kernel, per variant
     uint32_t* lists = nullptr;    // 2 overflow lists, capacity list_cap each
+    uint32_t* pool_busy = nullptr; // tier 1's borrowed-table bitmap (256 tables)
     uint32_t* counters = nullptr; // 2 counters
     uint64_t list_cap = 0;
     hipStream_t stream = nullptr;
@@ -1277,6 +1387,11 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     a.slot_epoch = t.slot_epoch;
     a.gstack = t.gstack;
     a.gstack_n = t.gstack_n;
+    a.pool = nullptr;
+    a.pool_mask = 0;
+    a.pool_n = 0;
+    a.pool_epoch = nullptr;
+    a.pool_busy = nullptr;
     a.in_list = in_list;
     a.in_count = in_count;
     a.out_list = out_list;
@@ -1520,6 +1635,7 @@ void device_release(Snapshot& S) {
     if (D.arena) (void)hipFree(D.arena);
     if (D.coll) (void)hipFree(D.coll);
     if (D.lists) (void)hipFree(D.lists);
+    if (D.pool_busy) (void)hipFree(D.pool_busy);
     if (D.counters) (void)hipFree(D.counters);
     if (D.row_handle) (void)hipFree(D.row_handle);
     if (D.layout_units) (void)hipFree(D.layout_units);
@@ -1551,6 +1667,7 @@ struct Plan {
     uint32_t slots[3];
     uint32_t cap[3];
     int frames[3];
+    bool pool = false;   // tier 1 borrows tier 2's tables on overflow (deep batches)
 };
 
 Plan make_plan(const DeviceState& D, uint32_t n, int frames_needed) {
@@ -1587,6 +1704,12 @@ void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t
     uint32_t* c1 = D.counters + 1;
     ensure_tier(set, 0, p.slots[0], p.cap[0], p.frames[0]);
     ensure_tier(set, 1, p.slots[1], p.cap[1], p.frames[1]);
+    if (p.pool) {
+        ensure_tier(set, 2, p.slots[2], p.cap[2], p.frames[2]);
+        uint64_t acc = 0;
+        if (!D.pool_busy) D.pool_busy = dmalloc<uint32_t>(8, acc);
+        HIP_OK(hipMemsetAsync(D.pool_busy, 0, 8 * sizeof(uint32_t), st));
+    }
     HIP_OK(hipMemsetAsync(D.counters, 0, 4 * sizeof(uint32_t), st));
     // tier 0 over all requests
     HIP_OK(hipEventRecord(D.ev[0], st));
@@ -1772,6 +1895,7 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
         p.cap[0] = fit(p.slots[0], 256, e0 ? (uint32_t)atoi(e0) : 16384u);
         p.slots[1] = (uint32_t)std::min<uint64_t>(e1 ? (uint32_t)atoi(e1) : 131072u, ((uint64_t)n + 255) / 256 * 256);
         p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, e2 ? (uint32_t)atoi(e2) : 65536u));
+        p.pool = getenv("KETO_NO_POOL") == nullptr;
     }
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
@@ -1786,6 +1910,14 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
+                  if (level == 1 && p.pool) {
+                      const Tier& t2 = D.tiers[2];
+                      a.pool = t2.vtab;
+                      a.pool_mask = t2.cap - 1;
+                      a.pool_n = std::min<uint32_t>(t2.n_slots, 256);
+                      a.pool_epoch = t2.slot_epoch;
+                      a.pool_busy = D.pool_busy;
+                  }
                   const uint32_t bs = std::min<uint32_t>(256, slots);
                   const dim3 grid(slots / bs), block(bs);
                   auto go = [&](auto kern) {

@@ -2,6 +2,7 @@
 nested-groups graph with cycles and depth up to 32 (config #3 shape), GPU vs the C oracle,
 bit-exact decisions and exact expand trees."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -38,6 +39,36 @@ def test_nested_deep_checks_match_oracle(nested, gmd):
     tab = g.oracle_table(q, max(gmd, 1))
     ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
     assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+
+
+@pytest.mark.parametrize("pool", [True, False])
+def test_nested_tier1_borrowed_tables_match_oracle(nested, pool):
+    """Tiny tier-0/1 visited tables (KETO_T0_CAP / KETO_T1_CAP) make thousands of deep requests
+    outgrow tier 1: with the pool, a tier-1 lane borrows one of tier 2's direct tables and finishes
+    the request itself (PromoVisited); requests that find every table borrowed, or all of them
+    without the pool, restart on tier 2.  Every decision must equal the oracle's either way."""
+    g, snap = nested
+    q = g.queries_nested(12000, seed=77, depths=(16, 32, 0, 40))
+    env = {"KETO_T0_CAP": "256", "KETO_T1_CAP": "1024"}
+    if not pool:
+        env["KETO_NO_POOL"] = "1"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        gpu = snap.check_batch_ids(snap.with_handles(q), 40)
+        _, n = snap.last_timing()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    tab = g.oracle_table(q, 40)
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), 40, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)} (pool {pool}, tiers {n})"
+    assert n[1] > 0, f"no request reached tier 1: {n}"
+    if not pool:
+        assert n[2] > 0, f"no request reached tier 2 without the pool: {n}"
 
 
 def test_nested_expand_matches_oracle(nested):
