@@ -281,13 +281,16 @@ struct DirectVisited {
     __device__ inline void release() {}
 };
 
-// Tier 1 of deep batches: a hashed map (Visited) that, when it outgrows the lane's table, borrows
-// one of tier 2's direct tables (DirectVisited) for the rest of the request instead of sending the
-// request up a tier, where it would restart from scratch and run after every tier-1 request.  The
-// hashed table keeps the map's earlier ids (read-only from then on); new ids go to the direct
-// table.  Tier 2 runs after tier 1 on the same stream and its lanes own the same tables, so the
-// per-table 16-bit epoch lives in tier 2's slot_epoch and is handed over on release.  With every
-// table borrowed, a map that overflows moves up a tier as before.
+// Tiers 0 and 1 of deep batches: a hashed map (Visited) that, when it outgrows the lane's table,
+// borrows a bigger table of the NEXT tier for the rest of the request instead of sending the
+// request up a tier, where it would restart from scratch and run after every request of this tier:
+// tier 0 borrows one of tier 1's hashed tables (Visited, DIRECT = false), tier 1 one of tier 2's
+// direct tables (DirectVisited, DIRECT = true).  The lane's own table keeps the map's earlier ids
+// (read-only from then on); new ids go to the borrowed table.  The next tier runs after this one
+// on the same stream and its lanes own the same tables, so a table's epoch lives in the next
+// tier's slot_epoch and is handed over on release.  With every table borrowed, or the borrowed
+// one full too, the request moves up a tier as before.
+template <bool DIRECT>
 struct PromoVisited {
     uint64_t* tab;       // hashed: the lane's tier-1 table
     uint32_t mask;
@@ -300,10 +303,15 @@ struct PromoVisited {
     uint32_t* pool_busy; // bitmap of borrowed tables
     int d;               // borrowed table, -1 = none
     uint32_t depoch;     // its epoch for the current map
+    uint32_t dcount;     // ids in it (hashed tables)
+    uint32_t hint;       // first bitmap word to try
     bool live;           // the hashed table holds ids of the current map
+    using BT = typename std::conditional<DIRECT, DirectVisited, Visited>::type;
     __device__ inline Visited hashed() { return Visited{tab, mask, epoch, count}; }
-    __device__ inline DirectVisited direct() {
-        return DirectVisited{pool + (uint64_t)d * (pool_mask + 1ull), pool_mask, depoch, 0, base};
+    __device__ inline BT borrowed() {
+        uint64_t* const t = pool + (uint64_t)d * (pool_mask + 1ull);
+        if constexpr (DIRECT) return DirectVisited{t, pool_mask, depoch, dcount, base};
+        else return Visited{t, pool_mask, depoch, dcount};
     }
     __device__ inline void fresh() {
         Visited H = hashed();
@@ -311,14 +319,17 @@ struct PromoVisited {
         epoch = H.epoch;
         count = H.count;
         if (d >= 0) {
-            DirectVisited D = direct();
-            D.fresh();
-            depoch = D.epoch;
+            BT B = borrowed();
+            B.fresh();
+            depoch = B.epoch;
+            dcount = B.count;
             live = false;
         }
     }
     __device__ inline bool borrow() {
-        for (uint32_t wi = 0; wi * 32u < pool_n; ++wi) {
+        const uint32_t nw = (pool_n + 31u) / 32u;
+        for (uint32_t k = 0; k < nw; ++k) {
+            const uint32_t wi = (hint + k) % nw;
             const uint32_t valid = pool_n - wi * 32u >= 32u ? NONE32 : (1u << (pool_n - wi * 32u)) - 1u;
             uint32_t cur = __hip_atomic_load(pool_busy + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             while (~cur & valid) {
@@ -328,9 +339,11 @@ struct PromoVisited {
                     __threadfence();                 // acquire: the last owner's epoch and marks
                     d = (int)(wi * 32u + b);
                     depoch = pool_epoch[d];
-                    DirectVisited D = direct();
-                    D.fresh();                       // a new map on the borrowed table
-                    depoch = D.epoch;
+                    dcount = 0;
+                    BT B = borrowed();
+                    B.fresh();                       // a new map on the borrowed table
+                    depoch = B.epoch;
+                    dcount = B.count;
                     return true;
                 }
                 cur = old | (1u << b);
@@ -365,8 +378,11 @@ struct PromoVisited {
                 i = (i + 1) & mask;
             }
         }
-        DirectVisited D = direct();
-        return D.test_add(vid, w);
+        BT B = borrowed();
+        const int t = B.test_add(vid, w);
+        depoch = B.epoch;
+        dcount = B.count;
+        return t;
     }
 };
 
@@ -483,7 +499,7 @@ struct TierArgs {
     const uint32_t* in_count;
     uint32_t* out_list;      // overflowed requests
     uint32_t* out_count;
-    // tier 1 of deep batches: tier 2's direct tables, borrowed on overflow (PromoVisited)
+    // tiers 0 / 1 of deep batches: the next tier's tables, borrowed on overflow (PromoVisited)
     uint64_t* pool;
     uint32_t pool_mask, pool_n;
     uint32_t* pool_epoch;
@@ -559,7 +575,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     const uint32_t stride = gridDim.x * blockDim.x;
     __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
     VisitedRS<LDS_VIDS, typename std::conditional<TIER == 2, DirectVisited,
-                                                  typename std::conditional<TIER == 1, PromoVisited, Visited>::type>::type> V;
+                                                  PromoVisited<TIER == 1>>::type> V;
     V.n = 0;
     V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
@@ -567,8 +583,10 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     V.V.epoch = ta.slot_epoch[slot];
     V.V.count = 0;
     if constexpr (TIER == 2) V.V.base = s.n_units;
-    if constexpr (TIER == 1) {
+    if constexpr (TIER < 2) {
         V.V.base = s.n_units;
+        V.V.hint = slot;
+        V.V.dcount = 0;
         V.V.pool = ta.pool;
         V.V.pool_mask = ta.pool_mask;
         V.V.pool_n = ta.pool_n;
@@ -1296,7 +1314,8 @@ struct DeviceState {
     Tier etiers[3];               // expand workspaces
     uint32_t v1_lanes[16] = {};   // resident lanes of the tier-0 check kernel, per variant
     uint32_t* lists = nullptr;    // 2 overflow lists, capacity list_cap each
-    uint32_t* pool_busy = nullptr; // tier 1's borrowed-table bitmap (256 tables)
+    uint32_t* pool_busy = nullptr; // borrowed-table bitmaps: tier 2's tables (8 words), tier 1's
+    uint64_t pool_words = 0;
     uint32_t* counters = nullptr; // 2 counters
     uint64_t list_cap = 0;
     hipStream_t stream = nullptr;
@@ -1707,8 +1726,13 @@ void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t
     if (p.pool) {
         ensure_tier(set, 2, p.slots[2], p.cap[2], p.frames[2]);
         uint64_t acc = 0;
-        if (!D.pool_busy) D.pool_busy = dmalloc<uint32_t>(8, acc);
-        HIP_OK(hipMemsetAsync(D.pool_busy, 0, 8 * sizeof(uint32_t), st));
+        const uint64_t words = 8 + ((uint64_t)set[1].n_slots + 31) / 32;   // tier 2's tables, then tier 1's
+        if (D.pool_words < words) {
+            if (D.pool_busy) (void)hipFree(D.pool_busy);
+            D.pool_busy = dmalloc<uint32_t>(words, acc);
+            D.pool_words = words;
+        }
+        HIP_OK(hipMemsetAsync(D.pool_busy, 0, words * sizeof(uint32_t), st));
     }
     HIP_OK(hipMemsetAsync(D.counters, 0, 4 * sizeof(uint32_t), st));
     // tier 0 over all requests
@@ -1910,13 +1934,13 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
-                  if (level == 1 && p.pool) {
-                      const Tier& t2 = D.tiers[2];
-                      a.pool = t2.vtab;
-                      a.pool_mask = t2.cap - 1;
-                      a.pool_n = std::min<uint32_t>(t2.n_slots, 256);
-                      a.pool_epoch = t2.slot_epoch;
-                      a.pool_busy = D.pool_busy;
+                  if (level < 2 && p.pool) {
+                      const Tier& tn = D.tiers[level + 1];
+                      a.pool = tn.vtab;
+                      a.pool_mask = tn.cap - 1;
+                      a.pool_n = level == 1 ? std::min<uint32_t>(tn.n_slots, 256) : tn.n_slots;
+                      a.pool_epoch = tn.slot_epoch;
+                      a.pool_busy = D.pool_busy + (level == 1 ? 0 : 8);
                   }
                   const uint32_t bs = std::min<uint32_t>(256, slots);
                   const dim3 grid(slots / bs), block(bs);
