@@ -58,8 +58,8 @@ def pmc_traffic(kernel_name, workload):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=16 * 1024 * 1024, help="checks per GPU per step")
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale (1.0 = 1B tuples)")
     ap.add_argument("--depth", type=int, default=5)
