@@ -185,6 +185,21 @@ int keto_check_batch_rows_device(keto_snapshot* s, const keto_check_ids* d_reqs,
                                  uint8_t* d_allowed_out, void* stream);
 /* Owner part of each row id for n_parts parts: -1 = a row every part holds (route anywhere). */
 int keto_row_owner(const keto_snapshot* s, const uint32_t* rows, uint64_t n, uint32_t n_parts, int32_t* out);
+/* Device-side routing of a row-id batch over n_parts (<= 64) parts, all buffers on one device:
+ * a stable counting sort by destination part = d_owner[row] (keto_row_owner's output as int16,
+ * n_rows entries), or self_part for rows every part holds, KETO_NO_ROW and out-of-range rows (the
+ * destination's keto_check_batch_rows_device then rejects the latter).  Writes d_send (the n
+ * requests grouped by part, batch order kept inside each part), d_order (batch index of each
+ * d_send entry) and counts_out[n_parts] (host: requests per part, the all-to-all split sizes).
+ * d_work: keto_route_work_bytes(n, n_parts) bytes of device scratch.  Synchronizes `stream`.
+ * Replaces the host-side grouping of a partitioned batch (repo:keto_amd/multi.py). */
+uint64_t keto_route_work_bytes(uint32_t n, uint32_t n_parts);
+int keto_route_rows_device(const keto_check_ids* d_reqs, uint32_t n, const int16_t* d_owner, uint32_t n_rows,
+                           uint32_t self_part, uint32_t n_parts, void* d_work, uint64_t work_bytes,
+                           keto_check_ids* d_send, uint32_t* d_order, uint32_t* counts_out, void* stream);
+/* Inverse of the routing for the decisions: d_out[d_order[j]] = d_back[j] for j < n (enqueued on
+ * `stream`). */
+int keto_unroute_device(const uint8_t* d_back, const uint32_t* d_order, uint32_t n, uint8_t* d_out, void* stream);
 int keto_snapshot_get_stats(const keto_snapshot* s, keto_snapshot_stats* out);
 
 /* Row ids (snapshot row order; KETO_NO_ROW passes through) -> row handles for keto_check_ids. */

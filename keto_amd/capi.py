@@ -29,6 +29,7 @@ EXPORTS = [
     "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
     "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids", "keto_row_handles",
     "keto_check_kernel_name", "keto_snapshot_upload_part", "keto_row_owner", "keto_check_batch_rows_device",
+    "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device",
 ]
 
 
@@ -120,6 +121,8 @@ def load():
     lib.keto_tree_nodes.restype = C.POINTER(KTreeNode)
     lib.keto_tree_json.restype = C.c_int64
     lib.keto_subject_string.restype = C.c_int64
+    lib.keto_route_work_bytes.restype = C.c_uint64
+    lib.keto_route_work_bytes.argtypes = [C.c_uint32, C.c_uint32]
     _lib = lib
     return lib
 
@@ -127,6 +130,29 @@ def load():
 def _check(rc):
     if rc != KETO_OK:
         raise KetoError(f"keto error {rc}: {load().keto_last_error().decode(errors='replace')}")
+
+
+def route_work_bytes(n: int, n_parts: int) -> int:
+    """Device scratch bytes keto_route_rows_device needs for n requests over n_parts parts."""
+    return int(load().keto_route_work_bytes(n, n_parts))
+
+
+def route_rows_device(d_reqs_ptr: int, n: int, d_owner_ptr: int, n_rows: int, self_part: int, n_parts: int,
+                      d_work_ptr: int, work_bytes: int, d_send_ptr: int, d_order_ptr: int, stream=0) -> list:
+    """keto_route_rows_device: group n row-id requests by owner part on the device (stable);
+    returns the per-part counts (the all-to-all split sizes)."""
+    counts = (C.c_uint32 * n_parts)()
+    _check(load().keto_route_rows_device(C.c_void_p(d_reqs_ptr), C.c_uint32(n), C.c_void_p(d_owner_ptr),
+                                         C.c_uint32(n_rows), C.c_uint32(self_part), C.c_uint32(n_parts),
+                                         C.c_void_p(d_work_ptr), C.c_uint64(work_bytes), C.c_void_p(d_send_ptr),
+                                         C.c_void_p(d_order_ptr), counts, C.c_void_p(stream)))
+    return list(counts)
+
+
+def unroute_device(d_back_ptr: int, d_order_ptr: int, n: int, d_out_ptr: int, stream=0) -> None:
+    """keto_unroute_device: d_out[d_order[j]] = d_back[j]."""
+    _check(load().keto_unroute_device(C.c_void_p(d_back_ptr), C.c_void_p(d_order_ptr), C.c_uint32(n),
+                                      C.c_void_p(d_out_ptr), C.c_void_p(stream)))
 
 
 class _Keep:

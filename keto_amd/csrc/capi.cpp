@@ -359,6 +359,28 @@ int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts,
     });
 }
 
+uint64_t keto_route_work_bytes(uint32_t n, uint32_t n_parts) { return route_work_bytes(n, n_parts); }
+
+int keto_route_rows_device(const keto_check_ids* d_reqs, uint32_t n, const int16_t* d_owner, uint32_t n_rows,
+                           uint32_t self_part, uint32_t n_parts, void* d_work, uint64_t work_bytes,
+                           keto_check_ids* d_send, uint32_t* d_order, uint32_t* counts_out, void* stream) {
+    return guarded([&] {
+        if (!counts_out || (n && (!d_reqs || !d_owner || !d_work || !d_send || !d_order)))
+            throw Error{KETO_E_INVALID, "NULL argument"};
+        route_rows(d_reqs, n, d_owner, n_rows, self_part, n_parts, d_work, work_bytes, d_send, d_order, counts_out,
+                   stream);
+        return KETO_OK;
+    });
+}
+
+int keto_unroute_device(const uint8_t* d_back, const uint32_t* d_order, uint32_t n, uint8_t* d_out, void* stream) {
+    return guarded([&] {
+        if (n && (!d_back || !d_order || !d_out)) throw Error{KETO_E_INVALID, "NULL argument"};
+        unroute_rows(d_back, d_order, n, d_out, stream);
+        return KETO_OK;
+    });
+}
+
 int keto_row_owner(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t n_parts, int32_t* out) {
     return guarded([&] {
         if (!h || (n && (!rows || !out)) || n_parts == 0) throw Error{KETO_E_INVALID, "bad argument"};

@@ -248,6 +248,12 @@ keto_batch_timing device_last_timing(const Snapshot& s);
 void device_check_rows(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
                        void* stream);
 const char* device_check_kernel_name(int32_t gmd);
+// partitioned-batch routing (route.hip): stable counting sort of row-id requests by owner part
+uint64_t route_work_bytes(uint32_t n, uint32_t n_parts);
+void route_rows(const keto_check_ids* d_reqs, uint32_t n, const int16_t* d_owner, uint32_t n_rows, uint32_t self_part,
+                uint32_t n_parts, void* d_work, uint64_t work_len, keto_check_ids* d_send, uint32_t* d_order,
+                uint32_t* counts_out, void* stream);
+void unroute_rows(const uint8_t* d_back, const uint32_t* d_order, uint32_t n, uint8_t* d_out, void* stream);
 struct ExpandResult {
     std::vector<uint8_t> status;
     std::vector<uint64_t> offset;          // n+1

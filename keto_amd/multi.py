@@ -121,21 +121,31 @@ class PartitionedChecker:
 def route_device(d_reqs, owner_dev, rank: int, world: int, group=None):
     """Device-side routing of a partitioned check batch (all tensors on this rank's GPU).
 
-    d_reqs: int32 [n, 4] keto_check_ids naming rows by row id; owner_dev: int16/int32 [n_rows]
-    owner part per row (-1 = every part).  Returns (received requests [m, 4], state) where `state`
-    carries what send_back() needs to return the m decisions to their origins."""
+    d_reqs: int32 [n, 4] keto_check_ids naming rows by row id; owner_dev: int16 [n_rows] owner part
+    per row (-1 = every part).  The grouping by destination is the engine's stable counting sort
+    (keto_route_rows_device, repo:keto_amd/csrc/route.hip); the exchange is one RCCL all-to-all.
+    Returns (received requests [m, 4], state) where `state` carries what send_back() needs to
+    return the m decisions to their origins."""
     import torch
     import torch.distributed as dist
-    own = owner_dev[d_reqs[:, 0].long()].long()
-    dest = torch.where(own < 0, torch.full_like(own, rank), own)
-    order = torch.argsort(dest, stable=True)
-    send = d_reqs[order]
-    counts = torch.bincount(dest, minlength=world)
+    from . import capi
+    if owner_dev.dtype != torch.int16 or not owner_dev.is_contiguous():
+        raise ValueError("owner_dev must be a contiguous int16 tensor (keto_row_owner output)")
+    d_reqs = d_reqs.contiguous()
+    n = len(d_reqs)
+    stream = torch.cuda.current_stream(d_reqs.device).cuda_stream
+    wb = capi.route_work_bytes(n, world)
+    work = torch.empty(max(wb, 1), dtype=torch.uint8, device=d_reqs.device)
+    send = torch.empty_like(d_reqs)
+    order = torch.empty(max(n, 1), dtype=torch.int32, device=d_reqs.device)
+    cs = capi.route_rows_device(d_reqs.data_ptr(), n, owner_dev.data_ptr(), len(owner_dev), rank, world,
+                                work.data_ptr(), wb, send.data_ptr(), order.data_ptr(), stream)
     if world == 1:
-        return send, (order, counts.cpu().tolist(), counts.cpu().tolist())
+        return send, (order, cs, cs)
+    counts = torch.tensor(cs, dtype=torch.int64, device=d_reqs.device)
     in_counts = torch.empty_like(counts)
     dist.all_to_all_single(in_counts, counts, group=group)
-    cs, ics = counts.cpu().tolist(), in_counts.cpu().tolist()
+    ics = in_counts.cpu().tolist()
     recv = torch.empty((sum(ics), 4), dtype=d_reqs.dtype, device=d_reqs.device)
     dist.all_to_all_single(recv, send, output_split_sizes=ics, input_split_sizes=cs, group=group)
     return recv, (order, cs, ics)
@@ -143,13 +153,15 @@ def route_device(d_reqs, owner_dev, rank: int, world: int, group=None):
 
 def send_back(decisions, state, out, world: int, group=None):
     """Return the decisions of route_device()'s received requests to their origins, in the
-    origin's order, into `out` (uint8 [n] on the device)."""
+    origin's order, into `out` (uint8 [n] on the device; keto_unroute_device)."""
     import torch
     import torch.distributed as dist
+    from . import capi
     order, cs, ics = state
     if world == 1:
         back = decisions
     else:
         back = torch.empty(sum(cs), dtype=torch.uint8, device=decisions.device)
-        dist.all_to_all_single(back, decisions, output_split_sizes=cs, input_split_sizes=ics, group=group)
-    out[order] = back
+        dist.all_to_all_single(back, decisions.contiguous(), output_split_sizes=cs, input_split_sizes=ics, group=group)
+    capi.unroute_device(back.data_ptr(), order.data_ptr(), sum(cs), out.data_ptr(),
+                        torch.cuda.current_stream(out.device).cuda_stream)
