@@ -504,6 +504,11 @@ struct TierArgs {
     uint32_t pool_mask, pool_n;
     uint32_t* pool_epoch;
     uint32_t* pool_busy;
+    // tier-0 wave kernel: dyn bits 0..15 > 0 hand out request runs of that many requests from 8
+    // per-XCD heads (heads[32 x]) once a lane's static first run (its share of dyn bits 16..19
+    // eighths of the XCD's range) is done; 0 = static runs only
+    uint32_t* heads;
+    uint32_t dyn;
 };
 
 // ------------------------------------------------------------------ check
@@ -901,11 +906,32 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     V.epoch = ta.slot_epoch[slot];
     V.count = 0;
     Work<COUNT> w;
-    // each lane owns a contiguous run of requests (a multiple of 4 long): requests are fetched two
-    // at a time and decisions are stored four at a time
-    const uint32_t per = ((n + stride - 1) / stride + 3u) & ~3u;
-    uint32_t j = min(n, slot * per);                           // next request to start
-    const uint32_t j_end = min(n, j + per);
+    // each lane works through contiguous runs of requests (multiples of 4 long, 4-aligned):
+    // requests are fetched two at a time and decisions are stored four at a time.  Static mode: one
+    // run per lane.  Dynamic mode (ta.dyn): the batch is split into 8 per-XCD ranges (workgroup b
+    // runs on XCD b % 8); a lane's first run covers its share of part of its XCD's range, then it takes
+    // runs of ta.dyn requests from its XCD's head (one returning atomic per wave and grab), so lanes
+    // that drew long searches do not hold up the end of the launch
+    const uint32_t R = ta.dyn & 0xFFFFu;
+    uint32_t j, j_end, xe = n, dyn_base = 0;
+    uint32_t* head = nullptr;
+    if (R == 0) {
+        const uint32_t per = ((n + stride - 1) / stride + 3u) & ~3u;
+        j = min(n, slot * per);                                // next request to start
+        j_end = min(n, j + per);
+    } else {
+        const uint32_t nx = min(8u, gridDim.x);                // ranges: one per XCD that has workgroups
+        const uint32_t xcd = blockIdx.x % nx;
+        const uint32_t lanes_x = (gridDim.x - xcd + nx - 1u) / nx * blockDim.x;
+        const uint32_t lx = (blockIdx.x / nx) * blockDim.x + tid;
+        const uint32_t xs = (uint32_t)(((uint64_t)n * xcd / nx) & ~3ull);
+        xe = xcd == nx - 1u ? n : (uint32_t)(((uint64_t)n * (xcd + 1u) / nx) & ~3ull);
+        const uint32_t r0 = (uint32_t)((uint64_t)(xe - xs) * (ta.dyn >> 16) / 8u / lanes_x) & ~3u;
+        j = min(xe, xs + lx * r0);
+        j_end = min(xe, j + r0);
+        dyn_base = xs + lanes_x * r0;
+        head = ta.heads + 32u * xcd;
+    }
     const bool packed = ((uintptr_t)allowed & 3u) == 0;
     uint32_t acc = 0;                                          // decisions of the current group of 4
 
@@ -955,7 +981,20 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     };
     for (;;) {
         const uint32_t ph = bf(c, C_PH, 3);
-        if (ph == P_REQ && j >= j_end) break;
+        if (ph == P_REQ && j >= j_end) {
+            if (R == 0) break;
+            // the lanes that finished their run take the next runs of their XCD's range together
+            const uint64_t m = __ballot(1);
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            uint32_t base = 0;
+            if ((tid & 63u) == leader) base = atomicAdd(head, (uint32_t)__popcll(m));
+            base = __shfl(base, (int)leader);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint64_t st = (uint64_t)dyn_base + (uint64_t)(base + below) * R;
+            if (st >= xe) break;
+            j = (uint32_t)st;
+            j_end = (uint32_t)min<uint64_t>(xe, st + R);
+        }
         // ---- the iteration's global accesses: one per lane (selected without branches), plus the
         // next request pair's prefetch
         const bool hdr = ph == P_HDR;
@@ -1317,6 +1356,7 @@ struct DeviceState {
     uint32_t* pool_busy = nullptr; // borrowed-table bitmaps: tier 2's tables (8 words), tier 1's
     uint64_t pool_words = 0;
     uint32_t* counters = nullptr; // 2 counters
+    uint32_t* heads = nullptr;    // tier-0 per-XCD run heads (8 x 128 B)
     uint64_t list_cap = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
@@ -1407,6 +1447,8 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     a.gstack = t.gstack;
     a.gstack_n = t.gstack_n;
     a.pool = nullptr;
+    a.heads = nullptr;
+    a.dyn = 0;
     a.pool_mask = 0;
     a.pool_n = 0;
     a.pool_epoch = nullptr;
@@ -1656,6 +1698,7 @@ void device_release(Snapshot& S) {
     if (D.lists) (void)hipFree(D.lists);
     if (D.pool_busy) (void)hipFree(D.pool_busy);
     if (D.counters) (void)hipFree(D.counters);
+    if (D.heads) (void)hipFree(D.heads);
     if (D.row_handle) (void)hipFree(D.row_handle);
     if (D.layout_units) (void)hipFree(D.layout_units);
     if (D.rows_by_unit) (void)hipFree(D.rows_by_unit);
@@ -1813,6 +1856,21 @@ int t0_variant() {
     const int v = e ? atoi(e) : 0;
     return v >= 0 && v < T0_VARIANTS ? v : 0;
 }
+// request runs handed out per grab by the tier-0 wave kernel (TierArgs::dyn) for a batch of n
+// requests over `lanes` lanes: runs of 32 after a static first half (profiles/r01v_dyn_runs_tune.log:
+// 2.73 ms vs 2.90 ms static on the 1B graph), used once every lane has at least 16 requests (with
+// fewer, one static run per lane keeps more lanes busy than runs of 32 would).  KETO_T0_DYN
+// overrides the run size (0 = static runs), KETO_T0_DYN_STATIC the static eighths,
+// KETO_T0_DYN_FORCE=1 drops the batch-size condition (tests).
+uint32_t t0_dyn(uint64_t n, uint64_t lanes) {
+    const char* e = getenv("KETO_T0_DYN");
+    const char* f = getenv("KETO_T0_DYN_STATIC");       // eighths of a range handed out statically
+    const char* force = getenv("KETO_T0_DYN_FORCE");
+    if (!(force && atoi(force) == 1) && n < 16 * lanes) return 0u;
+    const int v = e ? atoi(e) : 32;
+    const int st = f ? std::min(7, std::max(0, atoi(f))) : 4;
+    return v > 0 ? (std::min<uint32_t>((uint32_t)v + 3u, 0xFFFCu) & ~3u) | ((uint32_t)st << 16) : 0u;
+}
 const char* t0_kernel_name(int var) {
     switch (var) {
         case 0: return "keto::check_wave_kernel<4, false, 4, 16, false>";
@@ -1948,8 +2006,18 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
                       hipLaunchKernelGGL(kern, grid, block, 0, st, sv, dov, dq, n, gmd, da, a, dwork);
                   };
                   const bool local = p.frames[level] == 0;
-                  if (level == 0 && kind < 2)
+                  if (level == 0 && kind < 2) {
+                      a.dyn = t0_dyn(n, slots);
+                      if (a.dyn) {
+                          if (!D.heads) {
+                              uint64_t acc = 0;
+                              D.heads = dmalloc<uint32_t>(8 * 32, acc);
+                          }
+                          HIP_OK(hipMemsetAsync(D.heads, 0, 8 * 32 * sizeof(uint32_t), st));
+                          a.heads = D.heads;
+                      }
                       go(t0_kernel(var, dwork != nullptr));
+                  }
                   else if (level == 0)
                       dwork ? go(check_kernel<GlobalStack, true, 0>) : go(check_kernel<GlobalStack, false, 0>);
                   else if (level == 2)         // direct-indexed visited tables (DirectVisited)

@@ -210,3 +210,25 @@ def test_segment1_checks_match_oracle(powerlaw_seg1, gmd):
 
 def test_segment1_expand_matches_oracle(powerlaw_seg1):
     _expand_matches_oracle(*powerlaw_seg1)
+
+
+@pytest.mark.parametrize("dyn,static8,gmd", [("32", "4", 5), ("4", "0", 5), ("16", "7", 8), ("100", "2", 5),
+                                              ("0", "4", 5)])
+def test_powerlaw_dynamic_runs_match_oracle(powerlaw, monkeypatch, dyn, static8, gmd):
+    """Tier 0 with dynamic per-XCD request runs (TierArgs::dyn; forced on a batch far below the
+    16-requests-per-lane threshold, so most lanes grab runs, several lanes find their XCD's range
+    exhausted and a run ends at the batch end; grids of 4 and 20 workgroups split the batch into
+    fewer or uneven XCD ranges): every decision equals the oracle's.  Batch sizes
+    that are not multiples of 4 exercise the byte-wise decision stores of a run's last group."""
+    g, snap = powerlaw
+    monkeypatch.setenv("KETO_T0_DYN_FORCE", "1")
+    monkeypatch.setenv("KETO_T0_DYN", dyn)
+    monkeypatch.setenv("KETO_T0_DYN_STATIC", static8)
+    for n, seed in ((300_001, 70), (1_003, 71), (5_001, 72)):
+        q = g.queries(n, seed=seed + gmd, depth=gmd)
+        rng = np.random.default_rng(seed)
+        q["max_depth"] = rng.integers(-1, gmd + 2, size=len(q))
+        gpu = _gpu_check(snap, snap.with_handles(q), gmd)
+        tab = g.oracle_table(q, gmd)
+        ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
+        assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"

@@ -3,6 +3,7 @@ KETO_T0 variant on the same resident batch, checks that all variants agree bit f
 the work / line-touch counters of each.
 
   python tools/tune.py [--scale 1.0] [--batch 16777216] [--depth 5] [--variants 0,1,2,3] [--reps 3]
+  (a variant may carry a dynamic run size: --variants 0:0,0:16 sets KETO_T0_DYN)
 """
 import argparse
 import json
@@ -43,8 +44,13 @@ def main():
     sp = torch.cuda.current_stream().cuda_stream
     ref = None
     print(f"graph: {g.n_edges} tuples, {g.n_rows} rows", flush=True)
-    for v in [int(x) for x in a.variants.split(",")]:
+    for tok in a.variants.split(","):
+        # "variant[:run size[:static eighths]]" (KETO_T0_DYN, KETO_T0_DYN_STATIC; run size 0 = static runs)
+        v, dyn, st = (tok.split(":") + ["", ""])[:3]
+        v = int(v)
         os.environ["KETO_T0"] = str(v)
+        os.environ["KETO_T0_DYN"] = dyn or "0"
+        os.environ["KETO_T0_DYN_STATIC"] = st or "4"
         snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
         torch.cuda.synchronize()
         ms = []
@@ -62,7 +68,7 @@ def main():
             ("rows", "set_edges", "id_words", "vprobes", "vinserts", "items", "L_req", "L_hdr", "L_edge",
              "L_idtab", "L_idsearch", "push", "pop", "leaf", "leaf_miss", "pruned"), w[:16])}
         best = min(ms)
-        print(json.dumps({"variant": v, "ms": [round(x, 3) for x in ms], "checks_per_s": round(a.batch / best * 1e3),
+        print(json.dumps({"variant": tok, "mean_ms": round(sum(ms) / len(ms), 3), "ms": [round(x, 3) for x in ms], "checks_per_s": round(a.batch / best * 1e3),
                           "overflow": int(n[1]), "mismatch_vs_first": mism, "work": per}), flush=True)
 
 
