@@ -21,11 +21,12 @@ def test_host_library_under_asan(tmp_path):
         o = str(tmp_path / (f + ".o"))
         subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *san, "-c", os.path.join(csrc, f), "-o", o])
         objs.append(o)
-    o = str(tmp_path / "engine.o")
-    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-Xarch_host",
-                           "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-fno-omit-frame-pointer",
-                           "-w", "-c", os.path.join(csrc, "engine.hip"), "-o", o])
-    objs.append(o)
+    for f in ("engine.hip", "route.hip"):
+        o = str(tmp_path / (f + ".o"))
+        subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-Xarch_host",
+                               "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-fno-omit-frame-pointer",
+                               "-w", "-c", os.path.join(csrc, f), "-o", o])
+        objs.append(o)
     d = str(tmp_path / "drv.o")
     subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *san, "-c",
                            os.path.join(ROOT, "tests", "asan", "snapshot_asan.cpp"), "-o", d])

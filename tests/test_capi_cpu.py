@@ -77,3 +77,21 @@ def test_arena_layout_lines():
     assert ((word[target] - 24) % 32 == 0).all()              # filter at a line start, header at +96 B
     assert (word[~target] % 32 <= 24).all()
     assert len(np.unique(h)) == len(h)
+
+
+def test_route_argument_checks_need_no_gpu():
+    """keto_route_work_bytes is host arithmetic (destination bytes + per-(part, 2048-request tile)
+    counts + part starts, each 256-B aligned); keto_route_rows_device rejects bad part counts and a
+    short workspace before touching the device."""
+    import ctypes as C
+    from keto_amd import capi
+    lib = capi.load()
+    assert capi.route_work_bytes(0, 1) == 0 + 0 + 256
+    assert capi.route_work_bytes(4096, 3) == 4096 + 256 + 256
+    assert capi.route_work_bytes(4097, 8) == 4352 + 256 + 256
+    counts = (C.c_uint32 * 65)()
+    for n_parts, self_part, wb in ((0, 0, 1 << 20), (65, 0, 1 << 20), (4, 4, 1 << 20), (4, 0, 10)):
+        rc = lib.keto_route_rows_device(C.c_void_p(8), C.c_uint32(100), C.c_void_p(8), C.c_uint32(10),
+                                        C.c_uint32(self_part), C.c_uint32(n_parts), C.c_void_p(8), C.c_uint64(wb),
+                                        C.c_void_p(8), C.c_void_p(8), counts, None)
+        assert rc == -1, (n_parts, self_part, wb)                 # KETO_E_INVALID
