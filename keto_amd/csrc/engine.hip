@@ -915,8 +915,13 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     const uint32_t R = ta.dyn & 0xFFFFu;
     uint32_t j, j_end, xe = n, dyn_base = 0;
     uint32_t* head = nullptr;
+    bool whole_groups = true;                                  // runs are 4-aligned multiples of 4
     if (R == 0) {
-        const uint32_t per = ((n + stride - 1) / stride + 3u) & ~3u;
+        // batches under 4 requests per lane: runs of 1-3 requests (every lane busy; decisions are
+        // then stored byte by byte); otherwise runs rounded up to a multiple of 4
+        uint32_t per = (n + stride - 1) / stride;
+        if (per >= 4u) per = (per + 3u) & ~3u;
+        whole_groups = (per & 3u) == 0;
         j = min(n, slot * per);                                // next request to start
         j_end = min(n, j + per);
     } else {
@@ -932,7 +937,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         dyn_base = xs + lanes_x * r0;
         head = ta.heads + 32u * xcd;
     }
-    const bool packed = ((uintptr_t)allowed & 3u) == 0;
+    const bool packed = ((uintptr_t)allowed & 3u) == 0 && whole_groups;
     uint32_t acc = 0;                                          // decisions of the current group of 4
 
     uint32_t c = P_REQ;                                        // control word
