@@ -73,7 +73,52 @@ def parse():
                     help="edge-partitioned snapshot (root rows split by hash(ns, object)); each step routes the "
                          "batch to the owners with RCCL all-to-all, checks, and returns the decisions")
     ap.add_argument("--no-work", action="store_true", help="skip the roofline / cpu_baseline legs (profiling runs)")
+    ap.add_argument("--e2e-steps", type=int, default=5,
+                    help="batches timed end to end through the host API (keto_check_batch_rows, pinned buffers); 0 = skip")
+    ap.add_argument("--e2e-only", action="store_true", help="time only the end-to-end leg (profiling runs)")
     return ap.parse_args()
+
+
+def end_to_end(snap, q, a, d_out):
+    """SURVEY.md 8(d) t_batch: host entry to decisions on the host, for the same batch through
+    keto_check_batch_rows -- requests by row id in pinned host memory (keto_host_alloc), H2D,
+    row id -> handle translation on the device, the check, D2H, pipelined in chunks."""
+    from keto_amd.capi import CHECK_IDS_DTYPE, CHECK_PAIR_DTYPE, HostBuffer, pairs_of
+    n = len(q)
+    if not (q["max_depth"] == q["max_depth"][0]).all():
+        raise ValueError("the pair form needs one request depth per batch")
+    legs = {}
+    outs = []
+    for form, dt, size in (("pairs", CHECK_PAIR_DTYPE, 8), ("rows", CHECK_IDS_DTYPE, 16)):
+        hq, ho = HostBuffer(n, dt), HostBuffer(n, np.uint8)
+        hq.array[:] = pairs_of(q) if form == "pairs" else q
+        if form == "pairs":
+            call = lambda: snap.check_batch_pairs(hq.array, int(q["max_depth"][0]), a.depth, out=ho.array)
+        else:
+            call = lambda: snap.check_batch_rows(hq.array, a.depth, out=ho.array)
+        log(f"end-to-end leg ({form}): {a.e2e_steps} batches of {n} through the host API (pinned buffers)")
+        call()                                                     # warm-up (slots, staging)
+        ts, walls, tiers = [], [], []
+        for _ in range(a.e2e_steps):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+            t = snap.last_timing_full()
+            walls.append(t["wall_ms"])
+            tiers.append(t["tier_ms"][0])
+        ms = float(np.median(ts)) * 1e3
+        pcie = n * (size + 1)
+        legs[form] = {"value": round(n / (ms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(ms, 3),
+                      "library_wall_ms": round(float(np.median(walls)), 3),
+                      "tier0_ms_sum": round(float(np.median(tiers)), 3), "chunks": t["chunks"],
+                      "request_bytes": size, "pcie_bytes_per_batch": pcie,
+                      "pcie_GBps": round(pcie / (ms * 1e-3) / 1e9, 1)}
+        outs.append(ho.array.copy())
+    best = legs["pairs"]
+    return {**best, "form": "keto_check_batch_pairs (8-B row-id requests, batch depth)", "rows_form": legs["rows"],
+            "what": "host entry to decisions on the host: requests by row id in pinned host memory -> H2D -> "
+                    "device row-id translation -> check -> 1-B decisions D2H, chunks pipelined over copy / compute "
+                    "streams; median of the timed batches", "_out": outs}
 
 
 def main():
@@ -127,6 +172,13 @@ def main():
         def step():
             snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
 
+    e2e = None
+    if not a.partitioned and a.e2e_steps > 0:
+        e2e = end_to_end(snap, q, a, d_out)
+        if a.e2e_only:
+            if rank == 0:
+                print(json.dumps({"end_to_end": e2e}), flush=True)
+            return
     log(f"rank {rank}: warmup {a.warmup}, timed {a.steps} steps of {a.batch} checks")
     for _ in range(a.warmup):
         step()
@@ -239,6 +291,10 @@ def main():
                                      f"count per node) over the {stab.t.n} tuples they reach in in-memory "
                                      f"SQLite, {t_sql:.2f} s"}
 
+    if e2e is not None and roofline is not None:
+        e2e["frac"] = round(roofline["alg_bytes_per_launch"] / (e2e["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if e2e is not None:
+        e2e["decisions_equal_device_resident"] = all(bool((o == gpu_out).all()) for o in e2e.pop("_out"))
     if rank == 0:
         line = {
             "metric": "checks/sec (whole node) on 1B-tuple graph, max-depth 5; % of HBM roofline",
@@ -253,6 +309,7 @@ def main():
                        "global_batch": a.batch * world, "parallelism": f"partitioned-{world}" if a.partitioned else f"replicated-dp{world}",
                        "scale": a.scale},
             "roofline": roofline,
+            "end_to_end": e2e,
             "cpu_baseline": cpu,
             "ref_sql": ref_sql,
             "parity": parity,

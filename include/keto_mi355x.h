@@ -18,8 +18,10 @@
  *                            (internal/expand/tree.go:26-30,156-163).
  *
  * All strings are borrowed (keto_str = pointer + length, not NUL-terminated) and only read
- * during the call.  The library keeps no caller pointers after a call returns.  A snapshot is
- * immutable after keto_snapshot_build and may be shared by concurrent *_batch calls.
+ * during the call.  The library keeps no caller pointers after a call returns.  A snapshot may be
+ * shared by concurrent *_batch calls from any threads; calls on one snapshot run one at a time on its
+ * device (a batch's persistent grid fills the whole GPU, so overlapping two would not finish either
+ * sooner), each call's host-side work (resolution, staging) runs in the calling thread.
  * Every call returns KETO_OK (0) or a negative KETO_E_* code; keto_last_error() then holds a
  * thread-local message.  There is no CPU fallback inside the library: when the HIP runtime or a
  * device is missing, compute calls fail with KETO_E_HIP.
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 1
+#define KETO_ABI_VERSION 2
 
 /* return codes */
 #define KETO_OK 0
@@ -47,11 +49,19 @@ extern "C" {
 /* per-query status of keto_check_batch (allowed_out is always valid) */
 #define KETO_CHECK_OK 0                 /* decision equals the reference engine's */
 #define KETO_CHECK_UNKNOWN_NAMESPACE 1  /* request namespace unknown: reference returns false (engine.go:98-100) */
+#define KETO_CHECK_UNDECIDED 2          /* no tier could decide it within the engine's limits (allowed_out = 0):
+                                           ask the reference engine; the other requests of
+                                           the batch are decided as usual */
+
+/* decision byte of the ids / device entry points: 0 = denied, 1 = allowed, KETO_UNDECIDED = the
+ * request exceeded the engine's limits on its final tier (per request, never the whole batch) */
+#define KETO_UNDECIDED 2
 
 /* per-root status of keto_expand_batch */
 #define KETO_EXPAND_TREE 0              /* a tree (BuildTree returned a non-nil *Tree) */
 #define KETO_EXPAND_NIL 1               /* BuildTree returned nil, nil (JSON null) */
 #define KETO_EXPAND_NOT_FOUND 2         /* BuildTree returned herodot.ErrNotFound (unknown namespace, A.Q8/Q9) */
+#define KETO_EXPAND_UNDECIDED 3         /* the tree exceeded the engine's limits: ask the reference engine */
 
 /* node types of an expand tree (internal/expand/tree.go:16-23; only union and leaf are produced) */
 #define KETO_NODE_UNION 0
@@ -213,9 +223,35 @@ int keto_resolve_checks(const keto_snapshot* s, const keto_check_req* reqs, uint
 int keto_check_batch(keto_snapshot* s, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth,
                      uint8_t* allowed_out, uint8_t* status_out);
 
-/* Same with pre-resolved requests in host memory. */
+/* Same with pre-resolved requests in host memory (decision bytes as above, KETO_UNDECIDED
+ * included).  Host-buffer calls run as a pipeline of chunks: the H2D copy of the next chunk and the
+ * D2H copy of the previous one overlap the check of the current one.  Buffers from keto_host_alloc
+ * (pinned) are copied directly; pageable ones go through the library's pinned staging. */
 int keto_check_batch_ids(keto_snapshot* s, const keto_check_ids* reqs, uint32_t n, int32_t global_max_depth,
                          uint8_t* allowed_out);
+
+/* Same with requests that name rows by row id (row, and subject-set targets): the form a caller
+ * that interned names once keeps (snapshot row order, keto_row_handles' input).  Translated to
+ * device handles on the device, inside the pipeline. */
+int keto_check_batch_rows(keto_snapshot* s, const keto_check_ids* reqs, uint32_t n, int32_t global_max_depth,
+                          uint8_t* allowed_out);
+
+/* Compact 8-byte request of keto_check_batch_pairs: the top-level row by row id, and the subject:
+ * bit31 set -> a subject set (bits 0..30 = its row id), else a subject-id string id;
+ * KETO_NO_TARGET = a subject the snapshot does not know. */
+typedef struct {
+    uint32_t row;
+    uint32_t subject;
+} keto_check_pair;
+
+/* keto_check_batch_rows for batches whose requests share one request max-depth (the usual case:
+ * CheckRequest.max_depth unset -> 0 -> the global maximum): half the PCIe bytes per request. */
+int keto_check_batch_pairs(keto_snapshot* s, const keto_check_pair* reqs, uint32_t n, int32_t max_depth,
+                           int32_t global_max_depth, uint8_t* allowed_out);
+
+/* Pinned (page-locked) host memory for request / decision buffers of the host-buffer calls. */
+int keto_host_alloc(uint64_t bytes, void** out);
+void keto_host_free(void* p);
 
 /* Same with requests and results resident in device memory of the snapshot's device; enqueued on
  * `stream` (a hipStream_t, NULL = default stream).  Returns after enqueueing; results are ready
@@ -225,10 +261,13 @@ int keto_check_batch_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint
 
 /* Device time of the last keto_check_* call on this snapshot, per tier (tier 0 = every request,
  * tiers 1/2 = requests whose visited map outgrew the previous tier's table), from HIP events on
- * the call's stream. */
+ * the call's stream; summed over the chunks of a host-buffer call. */
 typedef struct {
     float tier_ms[3];
     uint32_t requests[3];
+    uint32_t undecided;         /* requests left KETO_UNDECIDED */
+    uint32_t chunks;            /* host-buffer calls: pipeline chunks (0 for device calls) */
+    float wall_ms;              /* host-buffer calls: entry to return, H2D + checks + D2H */
 } keto_batch_timing;
 int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
 

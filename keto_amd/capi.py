@@ -17,8 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KETO_LIB") or os.path.join(HERE, "libketo_mi355x.so")   # KETO_LIB: tuning builds
 
 KETO_OK = 0
-CHECK_OK, CHECK_UNKNOWN_NAMESPACE = 0, 1
-EXPAND_TREE, EXPAND_NIL, EXPAND_NOT_FOUND = 0, 1, 2
+CHECK_OK, CHECK_UNKNOWN_NAMESPACE, CHECK_UNDECIDED = 0, 1, 2
+UNDECIDED = 2                 # decision byte of the ids / device entry points
+EXPAND_TREE, EXPAND_NIL, EXPAND_NOT_FOUND, EXPAND_UNDECIDED = 0, 1, 2, 3
 NO_ROW = 0xFFFFFFFF
 NO_TARGET = 0xFFFFFFFF
 
@@ -29,7 +30,8 @@ EXPORTS = [
     "keto_tree_count", "keto_tree_status", "keto_tree_nodes", "keto_tree_json", "keto_subject_string",
     "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids", "keto_row_handles",
     "keto_check_kernel_name", "keto_snapshot_upload_part", "keto_row_owner", "keto_check_batch_rows_device",
-    "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device",
+    "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device", "keto_check_batch_rows",
+    "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs",
 ]
 
 
@@ -66,6 +68,16 @@ class KCheckIds(C.Structure):
 
 
 CHECK_IDS_DTYPE = np.dtype([("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
+CHECK_PAIR_DTYPE = np.dtype([("row", "<u4"), ("subject", "<u4")])
+
+
+def pairs_of(q: np.ndarray) -> np.ndarray:
+    """keto_check_ids by row id (subject sets flagged) -> 8-B keto_check_pair."""
+    p = np.empty(len(q), dtype=CHECK_PAIR_DTYPE)
+    p["row"] = q["row"]
+    sets = (q["flags"] & 1) != 0
+    p["subject"] = np.where(sets & (q["target"] != NO_TARGET), q["target"] | np.uint32(0x80000000), q["target"])
+    return p
 
 
 class KExpandReq(C.Structure):
@@ -81,7 +93,8 @@ class KOpts(C.Structure):
 
 
 class KTiming(C.Structure):
-    _fields_ = [("tier_ms", C.c_float * 3), ("requests", C.c_uint32 * 3)]
+    _fields_ = [("tier_ms", C.c_float * 3), ("requests", C.c_uint32 * 3), ("undecided", C.c_uint32),
+                ("chunks", C.c_uint32), ("wall_ms", C.c_float)]
 
 
 class KStats(C.Structure):
@@ -153,6 +166,27 @@ def unroute_device(d_back_ptr: int, d_order_ptr: int, n: int, d_out_ptr: int, st
     """keto_unroute_device: d_out[d_order[j]] = d_back[j]."""
     _check(load().keto_unroute_device(C.c_void_p(d_back_ptr), C.c_void_p(d_order_ptr), C.c_uint32(n),
                                       C.c_void_p(d_out_ptr), C.c_void_p(stream)))
+
+
+class HostBuffer:
+    """Pinned host memory from keto_host_alloc, viewed as a numpy array (freed with the object)."""
+
+    def __init__(self, n: int, dtype):
+        lib = load()
+        self.dtype = np.dtype(dtype)
+        self.n = n
+        self.p = C.c_void_p()
+        _check(lib.keto_host_alloc(C.c_uint64(max(1, n) * self.dtype.itemsize), C.byref(self.p)))
+        buf = (C.c_char * (max(1, n) * self.dtype.itemsize)).from_address(self.p.value)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=n)
+
+    def __del__(self):
+        try:
+            if self.p:
+                load().keto_host_free(self.p)
+                self.p = None
+        except Exception:
+            pass
 
 
 class _Keep:
@@ -317,6 +351,28 @@ class Snapshot:
                                              C.c_int32(global_max_depth), allowed.ctypes.data_as(C.c_void_p)))
         return allowed[:n]
 
+    def check_batch_rows(self, ids: np.ndarray, global_max_depth=5, out: Optional[np.ndarray] = None):
+        """keto_check_batch_rows: host requests naming rows by row id (translated on the device),
+        pipelined H2D / check / D2H.  `ids` / `out` may live in pinned memory (HostBuffer)."""
+        ids = np.ascontiguousarray(ids, dtype=CHECK_IDS_DTYPE)
+        n = len(ids)
+        if out is None:
+            out = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch_rows(self.h, ids.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                              C.c_int32(global_max_depth), out.ctypes.data_as(C.c_void_p)))
+        return out[:n]
+
+    def check_batch_pairs(self, pairs: np.ndarray, max_depth=0, global_max_depth=5, out: Optional[np.ndarray] = None):
+        """keto_check_batch_pairs: 8-B requests by row id, one request max-depth for the batch."""
+        pairs = np.ascontiguousarray(pairs, dtype=CHECK_PAIR_DTYPE)
+        n = len(pairs)
+        if out is None:
+            out = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch_pairs(self.h, pairs.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                               C.c_int32(max_depth), C.c_int32(global_max_depth),
+                                               out.ctypes.data_as(C.c_void_p)))
+        return out[:n]
+
     def check_batch_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, global_max_depth=5, stream=0):
         _check(self.lib.keto_check_batch_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
                                                 C.c_int32(global_max_depth), C.c_void_p(d_out_ptr),
@@ -332,6 +388,12 @@ class Snapshot:
         t = KTiming()
         _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
         return list(t.tier_ms), list(t.requests)
+
+    def last_timing_full(self) -> dict:
+        t = KTiming()
+        _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
+        return {"tier_ms": list(t.tier_ms), "requests": list(t.requests), "undecided": t.undecided,
+                "chunks": t.chunks, "wall_ms": t.wall_ms}
 
     @staticmethod
     def check_kernel_name(global_max_depth=5) -> str:

@@ -289,7 +289,13 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
             if (wild) ids[i].row = handle_of(S, &ov, overlay_row(S, ov, k));
             if (status_out) status_out[i] = st;
         }
-        device_check(S, ids.data(), n, global_max_depth, allowed_out, true, nullptr, &ov);
+        device_check_host(S, ids.data(), n, global_max_depth, allowed_out, FORM_HANDLES, 0, &ov);
+        if (status_out)
+            for (uint32_t i = 0; i < n; ++i)
+                if (allowed_out[i] == KETO_UNDECIDED) {
+                    allowed_out[i] = 0;
+                    status_out[i] = KETO_CHECK_UNDECIDED;
+                }
         return KETO_OK;
     });
 }
@@ -298,16 +304,44 @@ int keto_check_batch_ids(keto_snapshot* h, const keto_check_ids* reqs, uint32_t 
                          uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        device_check(*h->s, reqs, n, global_max_depth, allowed_out, true, nullptr, nullptr);
+        device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_HANDLES, 0, nullptr);
         return KETO_OK;
     });
 }
+
+int keto_check_batch_rows(keto_snapshot* h, const keto_check_ids* reqs, uint32_t n, int32_t global_max_depth,
+                          uint8_t* allowed_out) {
+    return guarded([&] {
+        if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_ROWS, 0, nullptr);
+        return KETO_OK;
+    });
+}
+
+int keto_check_batch_pairs(keto_snapshot* h, const keto_check_pair* reqs, uint32_t n, int32_t max_depth,
+                           int32_t global_max_depth, uint8_t* allowed_out) {
+    return guarded([&] {
+        if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_PAIRS, max_depth, nullptr);
+        return KETO_OK;
+    });
+}
+
+int keto_host_alloc(uint64_t bytes, void** out) {
+    return guarded([&] {
+        if (!out) throw Error{KETO_E_INVALID, "NULL argument"};
+        *out = host_alloc(bytes);
+        return KETO_OK;
+    });
+}
+
+void keto_host_free(void* p) { host_free(p); }
 
 int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                             uint8_t* d_allowed_out, void* stream) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, false, stream, nullptr);
+        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream);
         return KETO_OK;
     });
 }
@@ -398,7 +432,7 @@ int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint3
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]) {
     return guarded([&] {
         if (!h || !out || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, false, nullptr, nullptr, out);
+        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, nullptr, out);
         return KETO_OK;
     });
 }
@@ -508,6 +542,10 @@ int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_
     if (a->r.status[i] == KETO_EXPAND_NOT_FOUND) {
         g_err = "Unknown namespace";
         return KETO_E_INVALID;
+    }
+    if (a->r.status[i] == KETO_EXPAND_UNDECIDED) {
+        g_err = "the tree exceeds the engine's limits (KETO_EXPAND_UNDECIDED)";
+        return KETO_E_RANGE;
     }
     if (a->r.status[i] != KETO_EXPAND_TREE) {
         o = "null";

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -1375,6 +1376,18 @@ struct DeviceState {
     uint64_t ex_nodes_cap = 0;
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
+    // host-buffer calls (device_check_host): a pipeline of chunks over two device slots, H2D on
+    // copy_in, the check on `stream`, D2H on copy_out; pinned staging when the caller's buffers
+    // are pageable.  Kept across calls (no per-call allocation).
+    hipStream_t copy_in = nullptr, copy_out = nullptr;
+    keto_check_ids* slot_q[2] = {};   // raw requests of a chunk (handles or row ids)
+    keto_check_ids* slot_x[2] = {};   // translated requests (row-id form)
+    uint8_t* slot_a[2] = {};          // decisions of a chunk
+    uint64_t slot_cap = 0;
+    keto_check_ids* pin_q[2] = {};    // pinned staging (pageable callers)
+    uint8_t* pin_a[2] = {};
+    uint64_t pin_cap = 0;
+    hipEvent_t pev[8] = {};           // pipeline events: in_done[2], kern_done[2], out_done[2]
 
     DevSnap view() const { return DevSnap{arena, coll, coll_mask, n_units}; }
 };
@@ -1426,21 +1439,19 @@ void ensure_lists(DeviceState& D, uint64_t n) {
     if (D.list_cap >= n && D.lists) return;
     if (D.lists) (void)hipFree(D.lists);
     uint64_t acc = 0;
-    if (!D.counters) D.counters = dmalloc<uint32_t>(4, acc);
+    if (!D.counters) D.counters = dmalloc<uint32_t>(8, acc);   // [0..3] tiers (cleared per batch), [4] misrouted
     D.list_cap = std::max<uint64_t>(n, 1024);
     D.lists = dmalloc<uint32_t>(2 * D.list_cap, acc);
 }
 
 int hw_slots() {
     // persistent grid sized to residency: 256 CUs x 28 waves (7 per SIMD at the kernel's register
-    // budget) x 64 lanes; every lane owns one visited table.  KETO_SLOTS overrides (tuning).
-    static int v = [] {
-        const char* e = getenv("KETO_SLOTS");
-        int s = e ? atoi(e) : 256 * 28 * 64;
-        s = (s + 255) / 256 * 256;
-        return s < 256 ? 256 : s;
-    }();
-    return v;
+    // budget) x 64 lanes; every lane owns one visited table.  KETO_SLOTS overrides (tuning, tests;
+    // read on every batch).
+    const char* e = getenv("KETO_SLOTS");
+    int s = e ? atoi(e) : 256 * 28 * 64;
+    s = (s + 255) / 256 * 256;
+    return s < 256 ? 256 : s;
 }
 
 TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, uint32_t* out_list,
@@ -1687,7 +1698,10 @@ void device_upload(Snapshot& S, int device) {
     D->n_units = (uint32_t)S.n_units;
     D->n_coll = S.n_coll_keys;
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&D->copy_in, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&D->copy_out, hipStreamNonBlocking));
     for (auto& e : D->ev) HIP_OK(hipEventCreate(&e));
+    for (auto& e : D->pev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     S.device = device;
     S.dev.reset(D.release());
 }
@@ -1710,8 +1724,19 @@ void device_release(Snapshot& S) {
     if (D.ex_buf) (void)hipFree(D.ex_buf);
     if (D.ex_nodes) (void)hipFree(D.ex_nodes);
     if (D.xlate) (void)hipFree(D.xlate);
+    for (int i = 0; i < 2; ++i) {
+        if (D.slot_q[i]) (void)hipFree(D.slot_q[i]);
+        if (D.slot_x[i]) (void)hipFree(D.slot_x[i]);
+        if (D.slot_a[i]) (void)hipFree(D.slot_a[i]);
+        if (D.pin_q[i]) (void)hipHostFree(D.pin_q[i]);
+        if (D.pin_a[i]) (void)hipHostFree(D.pin_a[i]);
+    }
     if (D.stream) (void)hipStreamDestroy(D.stream);
+    if (D.copy_in) (void)hipStreamDestroy(D.copy_in);
+    if (D.copy_out) (void)hipStreamDestroy(D.copy_out);
     for (auto& e : D.ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : D.pev)
         if (e) (void)hipEventDestroy(e);
     S.dev.reset();
 }
@@ -1762,8 +1787,29 @@ Plan make_plan(const DeviceState& D, uint32_t n, int frames_needed) {
     return p;
 }
 
+// Requests (or expand roots) still on the final tier's overflow list: no tier could decide them
+// within its limits.  They get a per-request status instead of failing the batch: check decisions
+// become KETO_UNDECIDED, expand roots EXP_OVERFLOW with no nodes.
+__global__ void __launch_bounds__(256) mark_undecided(uint8_t* __restrict__ dst, uint64_t* __restrict__ cnt,
+                                                     const uint32_t* __restrict__ list, uint32_t n, uint8_t value) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = list[i];
+    dst[k] = value;
+    if (cnt) cnt[k] = 0;
+}
+
+struct Undecided {
+    uint8_t* dst = nullptr;       // decisions / statuses
+    uint64_t* cnt = nullptr;      // expand count pass: node counts zeroed
+    uint8_t value = 0;
+};
+
+// Runs tiers 0..2 over a batch of n; the batch's timing goes to D.last (added to it when
+// `accumulate`, for the chunks of one host-buffer call).
 template <class Launch>
-void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t st, Launch launch) {
+void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t st, Launch launch,
+               const Undecided& und, bool accumulate = false) {
     ensure_lists(D, n);
     uint32_t* list0 = D.lists;
     uint32_t* list1 = D.lists + D.list_cap;
@@ -1793,8 +1839,7 @@ void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t
     uint32_t cnt[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(cnt, c0, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    keto_batch_timing& T = D.last;
-    T = keto_batch_timing{};
+    keto_batch_timing T{};
     T.requests[0] = n;
     T.requests[1] = cnt[0];
     T.requests[2] = cnt[1];
@@ -1810,8 +1855,23 @@ void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t
         HIP_OK(hipMemcpyAsync(&still, c0, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         HIP_OK(hipEventElapsedTime(&T.tier_ms[2], D.ev[3], D.ev[4]));
-        if (still) throw Error{KETO_E_RANGE, "visited table overflow on the final tier"};
+        if (still) {
+            hipLaunchKernelGGL(mark_undecided, dim3((still + 255) / 256), dim3(256), 0, st, und.dst, und.cnt, list0, still,
+                               und.value);
+            HIP_OK(hipGetLastError());
+            T.undecided = still;
+        }
     }
+    keto_batch_timing& L = D.last;
+    if (!accumulate) {
+        L = T;
+        return;
+    }
+    for (int i = 0; i < 3; ++i) {
+        L.tier_ms[i] += T.tier_ms[i];
+        L.requests[i] += T.requests[i];
+    }
+    L.undecided += T.undecided;
 }
 
 // batch-local overlay arena on the device (freed when the batch returns)
@@ -1903,29 +1963,18 @@ const char* device_check_kernel_name(int32_t gmd) {
     return t0_kernel_name(fr <= 4 ? t0_variant() : T0_VARIANTS);
 }
 
-void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
-                  bool host_buffers, void* stream, const Overlay* ovh, uint64_t* work_out) {
-    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
-    DeviceState& D = *S.dev;
-    std::lock_guard<std::mutex> lk(D.mu);
-    HIP_OK(hipSetDevice(D.device));
-    if (n == 0) return;
-    if (gmd > 65535) gmd = 65535;
-    hipStream_t st = stream ? (hipStream_t)stream : D.stream;
-    OverlayBuf ov(S, ovh);
-    const keto_check_ids* dq = reqs;
-    uint8_t* da = allowed;
-    DevFree tmp;
-    if (host_buffers) {
-        uint64_t acc = 0;
-        keto_check_ids* tq = dmalloc<keto_check_ids>(n, acc);
-        tmp.p.push_back(tq);
-        uint8_t* ta8 = dmalloc<uint8_t>(n, acc);
-        tmp.p.push_back(ta8);
-        HIP_OK(hipMemcpyAsync(tq, reqs, (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice, st));
-        dq = tq;
-        da = ta8;
+namespace {
+
+// The check of one device-resident batch: the tier plan and the kernel launches.  The caller holds
+// D.mu and has set the device; `dq` / `da` are device buffers.
+void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
+                  hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate) {
+    if (n == 0) {
+        if (!accumulate) D.last = keto_batch_timing{};
+        return;
     }
+    if (gmd > 65535) gmd = 65535;
+    DevFree tmp;
     // check recursion holds at most gmd - 1 frames.  Tier 0 keeps them in LDS when they fit
     // (LdsStack<4> covers the default max-depth 5), else in HBM (GlobalStack).
     Plan p = make_plan(D, n, std::max(1, gmd - 1));
@@ -1956,9 +2005,9 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_kernel(var, false), 256, 0));
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
         D.v1_lanes[var] = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
-        if (getenv("KETO_SLOTS")) D.v1_lanes[var] = (uint32_t)hw_slots();
     }
-    p.slots[0] = (uint32_t)std::min<uint64_t>(D.v1_lanes[var], ((uint64_t)n + 255) / 256 * 256);
+    const uint32_t lanes = getenv("KETO_SLOTS") ? (uint32_t)hw_slots() : D.v1_lanes[var];
+    p.slots[0] = (uint32_t)std::min<uint64_t>(lanes, ((uint64_t)n + 255) / 256 * 256);
     if (kind == 2) {
         // deep requests (nested groups) visit thousands of sets: give every tier-0 lane a table
         // of up to 16K entries and tier 1 128K lanes of up to 64K entries, within half of device
@@ -1984,8 +2033,8 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
         p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, e2 ? (uint32_t)atoi(e2) : 65536u));
         p.pool = getenv("KETO_NO_POOL") == nullptr;
     }
+    if (const char* e = getenv("KETO_TEST_T2_FRAMES")) p.frames[2] = 2 * std::max(1, atoi(e));   // test hook
     DevSnap sv = D.view();
-    DevOverlay dov = ov.v;
     unsigned long long* dwork = nullptr;
     if (work_out) {
         uint64_t acc = 0;
@@ -2032,16 +2081,13 @@ void device_check(Snapshot& S, const keto_check_ids* reqs, uint32_t n, int32_t g
                   else
                       dwork ? go(check_kernel<GlobalStack, true, 1>) : go(check_kernel<GlobalStack, false, 1>);
                   HIP_OK(hipGetLastError());
-              });
+              },
+              Undecided{da, nullptr, (uint8_t)KETO_UNDECIDED}, accumulate);
     if (work_out) {
         unsigned long long h[KETO_WORK_SLOTS];
         HIP_OK(hipMemcpyAsync(h, dwork, sizeof(h), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         for (int i = 0; i < KETO_WORK_SLOTS; ++i) work_out[i] = h[i];
-    }
-    if (host_buffers) {
-        HIP_OK(hipMemcpyAsync(allowed, da, n, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
     }
 }
 
@@ -2067,38 +2113,243 @@ __global__ void __launch_bounds__(256) rows_to_handles(const keto_check_ids* __r
     out[i] = q;
 }
 
+void translate_rows_locked(Snapshot& S, DeviceState& D, const keto_check_ids* d_reqs, keto_check_ids* d_out, uint32_t n,
+                           hipStream_t st, uint32_t* d_bad) {
+    uint64_t acc = 0;
+    if (!D.row_handle) {
+        D.row_handle = dmalloc<uint32_t>(S.n_rows(), acc);
+        HIP_OK(hipMemcpy(D.row_handle, S.unit_of_row.data(), (uint64_t)S.n_rows() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice));
+    }
+    if (n) {
+        hipLaunchKernelGGL(rows_to_handles, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, d_out, n, D.row_handle,
+                           S.n_rows(), d_bad);
+        HIP_OK(hipGetLastError());
+    }
+}
+
+// 8-B requests (row id, subject: bit31 = subject-set row id, else subject-id string id) -> the
+// 16-B handle form, with the batch's request depth.  Misrouted rows are counted like above.
+__global__ void __launch_bounds__(256) pairs_to_handles(const keto_check_pair* __restrict__ in, keto_check_ids* __restrict__ out,
+                                                        uint32_t n, int32_t depth, const uint32_t* __restrict__ table,
+                                                        uint32_t n_rows, uint32_t* misrouted) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const keto_check_pair p = in[i];
+    keto_check_ids q{KETO_NO_ROW, KETO_NO_TARGET, 0u, depth};
+    if (p.row != KETO_NO_ROW) {
+        const uint32_t h = p.row < n_rows ? table[p.row] : NO_UNIT;
+        if (h == NO_UNIT) atomicAdd(misrouted, 1u);
+        q.row = h == NO_UNIT ? KETO_NO_ROW : h;
+    }
+    if (p.subject != KETO_NO_TARGET) {
+        if (p.subject & EDGE_SET) {
+            const uint32_t r = p.subject & EDGE_VAL;
+            const uint32_t h = r < n_rows ? table[r] : NO_UNIT;
+            q.target = h == NO_UNIT ? KETO_NO_TARGET : h;
+            q.flags = 1u;
+        } else {
+            q.target = p.subject;
+        }
+    }
+    out[i] = q;
+}
+
+void translate_pairs_locked(Snapshot& S, DeviceState& D, const keto_check_pair* d_reqs, keto_check_ids* d_out, uint32_t n,
+                            int32_t depth, hipStream_t st, uint32_t* d_bad) {
+    translate_rows_locked(S, D, nullptr, nullptr, 0, st, d_bad);          // the row -> handle table
+    if (n) {
+        hipLaunchKernelGGL(pairs_to_handles, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, d_out, n, depth,
+                           D.row_handle, S.n_rows(), d_bad);
+        HIP_OK(hipGetLastError());
+    }
+}
+
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+uint64_t chunk_requests() {
+    const char* e = getenv("KETO_CHUNK");               // tuning / tests
+    const long long v = e ? atoll(e) : (4ll << 20);
+    return (uint64_t)std::max<long long>(256, v);
+}
+
+}  // namespace
+
+void device_check(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
+                  uint64_t* work_out) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    hipStream_t st = stream ? (hipStream_t)stream : D.stream;
+    check_locked(S, D, d_reqs, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, work_out, false);
+}
+
+// Host-buffer batches: the requests go to the device in chunks of KETO_CHUNK (default 4M), so the
+// H2D copy of chunk c + 1 (copy_in stream) and the D2H copy of chunk c - 1 (copy_out) overlap the
+// check of chunk c (the check stream).  Two device slots alternate.  Pinned caller buffers
+// (keto_host_alloc / hipHostRegister) are copied directly; pageable ones through pinned staging.
+// form: FORM_HANDLES (keto_check_ids with handles), FORM_ROWS (keto_check_ids naming rows by row
+// id, translated on the device) or FORM_PAIRS (8-B keto_check_pair by row id, one request depth for
+// the batch, expanded and translated on the device).
+void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd, uint8_t* allowed, int form,
+                       int32_t pair_depth, const Overlay* ovh) {
+    const uint64_t esz = form == FORM_PAIRS ? sizeof(keto_check_pair) : sizeof(keto_check_ids);
+    const uint8_t* reqs = static_cast<const uint8_t*>(reqs_v);
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    const auto t_start = std::chrono::steady_clock::now();
+    D.last = keto_batch_timing{};
+    if (n == 0) return;
+    OverlayBuf ov(S, ovh);
+    const uint64_t C = std::min<uint64_t>(n, chunk_requests());
+    const uint32_t chunks = (uint32_t)((n + C - 1) / C);
+    uint64_t acc = 0;
+    if (D.slot_cap < C) {
+        for (int i = 0; i < 2; ++i) {
+            if (D.slot_q[i]) (void)hipFree(D.slot_q[i]);
+            if (D.slot_x[i]) (void)hipFree(D.slot_x[i]);
+            if (D.slot_a[i]) (void)hipFree(D.slot_a[i]);
+            D.slot_q[i] = D.slot_x[i] = nullptr;
+            D.slot_a[i] = nullptr;
+        }
+        D.slot_cap = 0;
+        for (int i = 0; i < 2; ++i) {
+            D.slot_q[i] = dmalloc<keto_check_ids>(C, acc);
+            D.slot_x[i] = dmalloc<keto_check_ids>(C, acc);
+            D.slot_a[i] = dmalloc<uint8_t>((C + 3) & ~3ull, acc);
+        }
+        D.slot_cap = C;
+    }
+    const bool pinned = host_pinned(reqs) && host_pinned(allowed);
+    if (!pinned && D.pin_cap < C) {
+        for (int i = 0; i < 2; ++i) {
+            if (D.pin_q[i]) (void)hipHostFree(D.pin_q[i]);
+            if (D.pin_a[i]) (void)hipHostFree(D.pin_a[i]);
+            D.pin_q[i] = nullptr;
+            D.pin_a[i] = nullptr;
+        }
+        D.pin_cap = 0;
+        for (int i = 0; i < 2; ++i) {
+            HIP_OK(hipHostMalloc((void**)&D.pin_q[i], C * sizeof(keto_check_ids), hipHostMallocDefault));
+            HIP_OK(hipHostMalloc((void**)&D.pin_a[i], C, hipHostMallocDefault));
+        }
+        D.pin_cap = C;
+    }
+    ensure_lists(D, C);
+    hipEvent_t* in_done = D.pev;
+    hipEvent_t* kern_done = D.pev + 2;
+    hipEvent_t* out_done = D.pev + 4;
+    uint32_t* d_bad = D.counters + 4;
+    HIP_OK(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), D.stream));
+    auto lo = [&](uint32_t c) { return (uint64_t)c * C; };
+    auto len = [&](uint32_t c) { return (uint32_t)(std::min<uint64_t>(n, lo(c) + C) - lo(c)); };
+    // stage chunk c's requests and enqueue its H2D into slot c % 2 (slot reuse waits for chunk
+    // c - 2's check, which read it, through kern_done)
+    auto put = [&](uint32_t c) {
+        const int k = c & 1;
+        if (c >= 2) HIP_OK(hipStreamWaitEvent(D.copy_in, kern_done[k], 0));
+        const uint8_t* src = reqs + lo(c) * esz;
+        if (!pinned) {
+            if (c >= 2) HIP_OK(hipEventSynchronize(in_done[k]));   // staging k free again
+            uint8_t* dst = reinterpret_cast<uint8_t*>(D.pin_q[k]);
+            const uint64_t bytes = (uint64_t)len(c) * esz, part = 1 << 20;
+            host_parallel_for((bytes + part - 1) / part, [&](uint64_t i) {
+                std::memcpy(dst + i * part, src + i * part, std::min(part, bytes - i * part));
+            });
+            src = dst;
+        }
+        HIP_OK(hipMemcpyAsync(D.slot_q[k], src, (uint64_t)len(c) * esz, hipMemcpyHostToDevice, D.copy_in));
+        HIP_OK(hipEventRecord(in_done[k], D.copy_in));
+    };
+    // bring chunk c's decisions home (pageable: via staging, copied out once the D2H is done)
+    auto drain = [&](uint32_t c) {
+        const int k = c & 1;
+        if (!pinned) {
+            HIP_OK(hipEventSynchronize(out_done[k]));
+            std::memcpy(allowed + lo(c), D.pin_a[k], len(c));
+        }
+    };
+    put(0);
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const int k = c & 1;
+        if (c + 1 < chunks) put(c + 1);
+        HIP_OK(hipStreamWaitEvent(D.stream, in_done[k], 0));
+        if (c >= 2) HIP_OK(hipStreamWaitEvent(D.stream, out_done[k], 0));   // slot_a[k] drained
+        const keto_check_ids* dq = D.slot_q[k];
+        if (form == FORM_ROWS) {
+            translate_rows_locked(S, D, dq, D.slot_x[k], len(c), D.stream, d_bad);
+            dq = D.slot_x[k];
+        } else if (form == FORM_PAIRS) {
+            translate_pairs_locked(S, D, reinterpret_cast<const keto_check_pair*>(dq), D.slot_x[k], len(c), pair_depth,
+                                   D.stream, d_bad);
+            dq = D.slot_x[k];
+        }
+        check_locked(S, D, dq, len(c), gmd, D.slot_a[k], D.stream, ov.v, nullptr, true);
+        HIP_OK(hipEventRecord(kern_done[k], D.stream));
+        HIP_OK(hipStreamWaitEvent(D.copy_out, kern_done[k], 0));
+        if (!pinned && c >= 2) drain(c - 2);
+        HIP_OK(hipMemcpyAsync(pinned ? allowed + lo(c) : D.pin_a[k], D.slot_a[k], len(c), hipMemcpyDeviceToHost,
+                              D.copy_out));
+        HIP_OK(hipEventRecord(out_done[k], D.copy_out));
+    }
+    for (uint32_t c = chunks >= 2 ? chunks - 2 : 0; c < chunks; ++c)
+        if (!pinned) drain(c);
+    HIP_OK(hipStreamSynchronize(D.copy_out));
+    uint32_t bad = 0;
+    if (form != FORM_HANDLES) {
+        HIP_OK(hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, D.stream));
+        HIP_OK(hipStreamSynchronize(D.stream));
+    }
+    D.last.chunks = chunks;
+    D.last.wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
+}
+
+void* host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e)};
+    return p;
+}
+
+void host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
                        void* stream) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     DeviceState& D = *S.dev;
     hipStream_t st = stream ? (hipStream_t)stream : D.stream;
-    {
-        std::lock_guard<std::mutex> lk(D.mu);
-        HIP_OK(hipSetDevice(D.device));
-        uint64_t acc = 0;
-        if (!D.row_handle) {
-            D.row_handle = dmalloc<uint32_t>(S.n_rows(), acc);
-            HIP_OK(hipMemcpy(D.row_handle, S.unit_of_row.data(), (uint64_t)S.n_rows() * sizeof(uint32_t),
-                             hipMemcpyHostToDevice));
-        }
-        if (D.xlate_cap < n) {
-            if (D.xlate) (void)hipFree(D.xlate);
-            D.xlate_cap = std::max<uint64_t>(n, 1024);
-            D.xlate = dmalloc<keto_check_ids>(D.xlate_cap, acc);
-        }
-        ensure_lists(D, n);
-        HIP_OK(hipMemsetAsync(D.counters + 2, 0, sizeof(uint32_t), st));
-        if (n) {
-            hipLaunchKernelGGL(rows_to_handles, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, D.xlate, n,
-                               D.row_handle, S.n_rows(), D.counters + 2);
-            HIP_OK(hipGetLastError());
-        }
-        uint32_t bad = 0;
-        HIP_OK(hipMemcpyAsync(&bad, D.counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
-        if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
+    // the lock is held from the translation through the check: D.xlate is shared by all callers
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    uint64_t acc = 0;
+    if (D.xlate_cap < n) {
+        if (D.xlate) (void)hipFree(D.xlate);
+        D.xlate = nullptr;
+        D.xlate_cap = 0;
+        D.xlate = dmalloc<keto_check_ids>(std::max<uint64_t>(n, 1024), acc);
+        D.xlate_cap = std::max<uint64_t>(n, 1024);
     }
-    device_check(S, D.xlate, n, gmd, d_allowed, false, stream, nullptr);
+    ensure_lists(D, n);
+    HIP_OK(hipMemsetAsync(D.counters + 4, 0, sizeof(uint32_t), st));
+    translate_rows_locked(S, D, d_reqs, D.xlate, n, st, D.counters + 4);
+    uint32_t bad = 0;
+    HIP_OK(hipMemcpyAsync(&bad, D.counters + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
+    check_locked(S, D, D.xlate, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, false);
 }
 
 // Expand output: set nodes carry row handles; map them to row ids on the device (binary search in
@@ -2180,7 +2431,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                           hipLaunchKernelGGL((expand_kernel<true, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
                                              gmd, eo, a);
                       HIP_OK(hipGetLastError());
-                  });
+                  },
+                  Undecided{dstatus, fill ? nullptr : dcount, (uint8_t)EXP_OVERFLOW});
     };
     // count pass, exclusive scan on the host, fill pass (same tier plan: a root overflows on the
     // same tiers both times, and a partial pre-order is a prefix of the full one)

@@ -241,13 +241,22 @@ void compute_layout(Snapshot& s);
 void device_upload(Snapshot& s, int device);
 void device_release(Snapshot& s);
 uint64_t device_bytes(const Snapshot& s);
-void device_check(Snapshot& s, const keto_check_ids* d_or_h_reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
-                  bool host_buffers, void* stream, const Overlay* ov, uint64_t* work_out = nullptr);
+// device-resident requests and decisions, enqueued on `stream` (NULL: the snapshot's own)
+void device_check(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
+                  uint64_t* work_out = nullptr);
+// host buffers: pipelined chunks (H2D / check / D2H overlapped); form FORM_* (keto_check_ids by
+// handle or by row id, 8-B keto_check_pair by row id with one request depth); ov = batch-local
+// wildcard rows
+constexpr int FORM_HANDLES = 0, FORM_ROWS = 1, FORM_PAIRS = 2;
+void device_check_host(Snapshot& s, const void* reqs, uint32_t n, int32_t gmd, uint8_t* allowed, int form,
+                       int32_t pair_depth, const Overlay* ov);
 keto_batch_timing device_last_timing(const Snapshot& s);
 // requests with row ids (not handles) resident on the device: translated, then checked
 void device_check_rows(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
                        void* stream);
 const char* device_check_kernel_name(int32_t gmd);
+void* host_alloc(uint64_t bytes);    // pinned host memory (hipHostMalloc)
+void host_free(void* p);
 // partitioned-batch routing (route.hip): stable counting sort of row-id requests by owner part
 uint64_t route_work_bytes(uint32_t n, uint32_t n_parts);
 void route_rows(const keto_check_ids* d_reqs, uint32_t n, const int16_t* d_owner, uint32_t n_rows, uint32_t self_part,

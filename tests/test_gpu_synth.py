@@ -232,3 +232,85 @@ def test_powerlaw_dynamic_runs_match_oracle(powerlaw, monkeypatch, dyn, static8,
         tab = g.oracle_table(q, gmd)
         ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
         assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+
+
+@pytest.fixture(scope="module")
+def drive():
+    """BASELINE config #2 at 1/16 scale: files whose view row holds the file's own
+    owner set (another relation of the same object, namespace 1 sorts first) before its folder; an
+    8-ary folder tree of depth <= 6 with group grants; Zipf(1.1) group sizes."""
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.DRIVE_10M, 1 / 16), threads=16, kind="drive")
+    snap = g.snapshot(device=0)
+    yield g, snap
+    snap.close()
+    g.close()
+
+
+@pytest.mark.parametrize("gmd", [5, 2, 3, 7])
+def test_drive_checks_match_oracle(drive, gmd):
+    g, snap = drive
+    q = g.queries(40000, seed=20 + gmd, depth=gmd)
+    rng = np.random.default_rng(gmd)
+    q["max_depth"] = rng.integers(-1, gmd + 2, size=len(q))      # exercise the depth clamp
+    gpu = _gpu_check(snap, snap.with_handles(q), gmd)
+    tab = g.oracle_table(q, gmd)
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+    assert 0.05 < gpu.mean() < 0.95
+
+
+def test_drive_owner_relation_decides(drive):
+    """Requests for a file's own owner (reached only through files:d#view@(files:d#owner), the
+    intra-object edge) are allowed at every depth >= 2 and denied at depth 1."""
+    g, snap = drive
+    rng = np.random.default_rng(1)
+    files = rng.integers(0, g.params["n_docs"], size=5000)
+    owner_rows = (2 * files).astype(np.int64)
+    first_owner = g.edges[g.row_ptr[owner_rows].astype(np.int64)]
+    q = np.zeros(len(files), dtype=[("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
+    q["row"] = 2 * files + 1
+    q["target"] = first_owner
+    for d, want in ((1, 0), (2, 1), (5, 1)):
+        q["max_depth"] = d
+        gpu = _gpu_check(snap, snap.with_handles(q), 5)
+        assert (gpu == want).all(), (d, int((gpu != want).sum()))
+
+
+def test_drive_expand_matches_oracle(drive):
+    _expand_matches_oracle(*drive)
+
+
+def test_drive_full_scale_matches_oracle():
+    """Config #2 at its full size (exactly 10,000,000 tuples, seed 2): 1,000,000 checks on the GPU,
+    the first 100,000 compared with the oracle."""
+    from tools import synth
+    g = synth.SynthGraph(dict(synth.DRIVE_10M), threads=16, kind="drive")
+    try:
+        assert g.n_edges == 10_000_000
+        snap = g.snapshot(device=0)
+        q = g.queries(1_000_000, seed=2, depth=5)
+        gpu = _gpu_check(snap, snap.with_handles(q), 5)
+        k = 100_000
+        tab = g.oracle_table(q[:k], 5)
+        ref = tab.check_batch_reqs(g.oracle_requests(tab, q[:k]), 5, threads=16)
+        assert (gpu[:k] == ref).all(), f"{int((gpu[:k] != ref).sum())} mismatches of {k}"
+        snap.close()
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("lanes,n", [(2048, 2 * 2048 - 3), (2048, 2 * 2048 + 1), (2048, 3 * 2048 - 1),
+                                     (2048, 4 * 2048 + 5), (256, 1001)])
+def test_static_runs_short_match_oracle(powerlaw, monkeypatch, lanes, n):
+    """Static tier-0 runs (KETO_T0_DYN=0) on a pinned lane count (KETO_SLOTS): batches of 2 and 3
+    requests per lane (runs of 1-3 requests, decisions stored byte by byte), a short final run, and
+    runs rounded up to whole groups of 4; every decision equals the oracle's."""
+    g, snap = powerlaw
+    monkeypatch.setenv("KETO_T0_DYN", "0")
+    monkeypatch.setenv("KETO_SLOTS", str(lanes))
+    q = g.queries(n, seed=n, depth=5)
+    gpu = _gpu_check(snap, snap.with_handles(q), 5)
+    tab = g.oracle_table(q, 5)
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), 5, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"

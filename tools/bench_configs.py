@@ -7,8 +7,9 @@ restatement timed on the same sample and host cores.
   #1 cat-videos: the reference's contrib/cat-videos-example tuples (7), 10,000 seeded checks;
      CPU: the SQL-level restatement of the reference engine over in-memory SQLite (ref-sql) and
      the C restatement; GPU: the same 10,000 checks.
-  #2 Drive-like: the power-law docs/folders/groups generator at 10,000,000 tuples, 1,000,000
-     checks, max-depth 5.
+  #2 Drive-like: SURVEY.md 8(d)'s files / folder-forest (fan-out 8, depth <= 6) / Zipf(1.1) groups
+     generator at exactly 10,000,000 tuples (seed 2), 1,000,000 files:d#view@u checks (half along
+     real paths), max-depth 5.
   #3 nested groups: chains of up to 32 nested groups with back-edges (cycles), 100M tuples,
      1,000,000 checks with request depths {5, 16, 32}, global max-depth 32.
   #5 expand: 100,000 roots sampled from #3's rows, global max-depth 5; trees/s for count + fill
@@ -104,7 +105,25 @@ def work_counters(snap, qd, n, gmd):
     return {k: round(v / n, 3) for k, v in zip(WORK_KEYS, w)}
 
 
-def checks_config(a, name, g, q, gmd, sample, reps=3):
+HBM_PEAK_GBS = 8000.0
+
+
+def roofline(tab, reqs, gmd, n_price, n, kernel_ms, threads):
+    """SURVEY.md 8(d) roofline of the tier-0 kernel: B_check(q) = 14 + sum over the BFS rows
+    (8 + 4 deg) from the oracle's BFS-count mode on the first n_price requests, scaled to the n of
+    the launch, over the kernel's HIP-event time."""
+    from oracle.oracle_c import OracleTable
+    t0 = time.perf_counter()
+    bq = tab.bfs_bytes_reqs(OracleTable.prefix(reqs, n_price), gmd, threads=threads)
+    per = float(bq.mean())
+    ach = per * n / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kernel_ms, 4),
+            "alg_bytes_per_check": round(per, 1),
+            "alg_bytes_sample": f"B_check over the first {n_price} requests ({time.perf_counter() - t0:.1f} s)"}
+
+
+def checks_config(a, name, g, q, gmd, sample, reps=3, price=20000):
     log(f"{name}: {g.n_edges} tuples; snapshot")
     snap = g.snapshot(device=0)
     qd = snap.with_handles(q)
@@ -123,7 +142,9 @@ def checks_config(a, name, g, q, gmd, sample, reps=3):
     t0 = time.perf_counter()
     ref = tab.check_batch_reqs(reqs, gmd, threads=a.threads)
     t_cpu = time.perf_counter() - t0
-    return {"config": name, "tuples": int(g.n_edges), "rows": int(g.n_rows), "checks": n, "global_max_depth": gmd,
+    roof = roofline(tab, reqs, gmd, min(price, sample), n, ms[0], a.threads)
+    roof["kernel"] = snap.check_kernel_name(gmd)
+    return {"config": name, "roofline": roof, "tuples": int(g.n_edges), "rows": int(g.n_rows), "checks": n, "global_max_depth": gmd,
             "gpu": {"checks_per_s": round(n / dt, 1), "wall_ms": round(dt * 1e3, 3),
                     "tier_ms": [round(x, 3) for x in ms], "tier_requests": [int(x) for x in cnt],
                     "kernel": snap.check_kernel_name(gmd)},
@@ -136,16 +157,17 @@ def checks_config(a, name, g, q, gmd, sample, reps=3):
 
 def config2(a):
     from tools import synth
-    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 0.01), threads=a.threads)
+    g = synth.SynthGraph(dict(synth.DRIVE_10M), threads=a.threads, kind="drive")
     q = g.queries(1_000_000, seed=2, depth=5, threads=a.threads)
-    return checks_config(a, "#2 Drive-like (power-law docs/folders/groups, 10M tuples)", g, q, 5, 200_000)
+    return checks_config(a, "#2 Drive-like (files / 8-ary folder forest depth <= 6 / Zipf(1.1) groups, 10M tuples)",
+                         g, q, 5, 200_000)
 
 
 def config3(a):
     from tools import synth
     g = synth.SynthGraph(dict(synth.NESTED_100M), threads=a.threads, kind="nested", chain=32)
     q = g.queries_nested(1_000_000, seed=3, depths=(5, 16, 32), threads=a.threads)
-    return checks_config(a, "#3 nested groups (chains <= 32, cycles)", g, q, 32, 20_000, reps=1), g
+    return checks_config(a, "#3 nested groups (chains <= 32, cycles)", g, q, 32, 20_000, reps=1, price=2000), g
 
 
 def config5(a, g=None):

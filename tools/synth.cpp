@@ -277,6 +277,143 @@ int synth_queries_nested(const synth_graph* g, const synth_params* p, uint64_t n
     return 0;
 }
 
+// "Drive-like" graph (BASELINE config #2, SURVEY.md 8(d) exactly): namespaces files(1) /
+// folders(2) / groups(3); relations member(0) < owner(1) < view(2) (byte order).
+//   rows (in (namespace, object, relation) order): files:d#owner = 2d, files:d#view = 2d + 1,
+//        folders:f#view = 2 n_files + f, groups:g#member = 2 n_files + n_folders + g
+//   files:d#view    -> (files:d#owner)  [same object, another relation; ns 1 sorts first]
+//                      (folders:p#view) [the file's folder, uniform over folders]
+//   files:d#owner   -> 1 + Pareto(2.0) users (<= 16)
+//   folders:f#view  -> (folders:parent#view) unless f is a tree root; 0/1/2 x (groups:g#member)
+//                      (p = .6/.3/.1, popular groups preferred); Pareto(1.5) users (<= 1000)
+//   groups:g#member -> users; group sizes Zipf(1.1) (size of the k-th group ~ C / k^1.1),
+//                      scaled so the graph has exactly `target_edges` tuples
+// The folders form a forest of complete 8-ary trees in heap order (folder j of a tree has parent
+// (j - 1) / 8), at most 37,449 folders per tree, i.e. depth <= 6 (levels 0..5).
+constexpr uint64_t DRIVE_TREE = 1 + 8 + 64 + 512 + 4096 + 32768;
+
+static void drive_degrees(const synth_params* p, uint64_t r, uint32_t& ns, uint32_t& ni) {
+    const uint64_t NF = p->n_docs, NO = p->n_folders;
+    Rng g(p->seed * 0x9FB21C651E98DF25ull ^ (r * 0x9E3779B97F4A7C15ull));
+    if (r < 2 * NF) {
+        if (r & 1) { ns = 2; ni = 0; }                                   // files:d#view
+        else { ns = 0; ni = 1 + (uint32_t)pareto(g, 1.0, 2.0, 15); }      // files:d#owner
+    } else if (r < 2 * NF + NO) {
+        const uint64_t f = r - 2 * NF;
+        const uint64_t u = g.next() % 10;
+        ns = (f % DRIVE_TREE == 0 ? 0u : 1u) + (u < 6 ? 0u : u < 9 ? 1u : 2u);
+        ni = (uint32_t)pareto(g, 1.0, 1.5, 1000);
+    } else {
+        ns = 0;
+        ni = 0;                                                           // groups: sized below
+    }
+}
+
+int synth_generate_drive(const synth_params* p, int threads, synth_graph* out) {
+    const uint64_t NF = p->n_docs, NO = p->n_folders, NG = p->n_groups;
+    const uint64_t R = 2 * NF + NO + NG;
+    if (R >= 0x7FFFFFFFull || p->n_users >= 0x7FFFFFFFull || !NF || !NO || !NG || !p->n_users) return -1;
+    std::vector<uint32_t> nset(R), nid(R);
+    parallel_for(R, threads, [&](uint64_t r) { drive_degrees(p, r, nset[r], nid[r]); });
+    uint64_t fixed = 0;
+    for (uint64_t r = 0; r < 2 * NF + NO; ++r) fixed += nset[r] + nid[r];
+    const uint64_t target = p->target_edges ? p->target_edges : fixed + 16 * NG;
+    if (target < fixed + NG) return -4;                                   // every group gets >= 1 member
+    // Zipf(1.1) sizes for the remaining tuples, then +/-1 from the largest groups down to hit it exactly
+    const uint64_t rem = target - fixed;
+    double H = 0;
+    for (uint64_t k = 1; k <= NG; ++k) H += std::pow((double)k, -1.1);
+    uint64_t got = 0;
+    for (uint64_t k = 0; k < NG; ++k) {
+        uint64_t s = (uint64_t)((double)rem / H * std::pow((double)(k + 1), -1.1));
+        if (s < 1) s = 1;
+        if (s > 0xFFFFFFF0ull) s = 0xFFFFFFF0ull;
+        nid[2 * NF + NO + k] = (uint32_t)s;
+        got += s;
+    }
+    for (uint64_t k = 0; got != rem; k = (k + 1) % NG) {
+        uint32_t& s = nid[2 * NF + NO + k];
+        if (got < rem) { ++s; ++got; }
+        else if (s > 1) { --s; --got; }
+    }
+    out->n_rows = (uint32_t)R;
+    out->row_ns = (int32_t*)malloc(R * sizeof(int32_t));
+    out->row_obj = (uint32_t*)malloc(R * sizeof(uint32_t));
+    out->row_rel = (uint32_t*)malloc(R * sizeof(uint32_t));
+    out->row_ptr = (uint64_t*)malloc((R + 1) * sizeof(uint64_t));
+    uint64_t acc = 0, sets = 0;
+    for (uint64_t r = 0; r < R; ++r) {
+        out->row_ptr[r] = acc;
+        acc += nset[r] + nid[r];
+        sets += nset[r];
+    }
+    out->row_ptr[R] = acc;
+    out->n_edges = acc;
+    out->n_set_edges = sets;
+    out->edges = (uint32_t*)malloc(std::max<uint64_t>(acc, 1) * sizeof(uint32_t));
+    if (!out->row_ns || !out->row_obj || !out->row_rel || !out->row_ptr || !out->edges) return -2;
+    enum { D_MEMBER = 0, D_OWNER = 1, D_VIEW = 2 };
+    const uint32_t FO = (uint32_t)(2 * NF), GR = (uint32_t)(2 * NF + NO);
+    parallel_for(R, threads, [&](uint64_t r) {
+        Rng g(p->seed * 0xC2B2AE3D27D4EB4Full ^ (r * 0xD6E8FEB86659FD93ull) ^ 0xD21Eull);
+        uint32_t* e = out->edges + out->row_ptr[r];
+        uint32_t k = 0;
+        const uint32_t ns = nset[r], ni = nid[r];
+        if (r < 2 * NF) {
+            out->row_ns[r] = 1;
+            out->row_obj[r] = (uint32_t)(r >> 1);
+            out->row_rel[r] = (r & 1) ? D_VIEW : D_OWNER;
+            if (r & 1) {
+                e[k++] = 0x80000000u | (uint32_t)(r - 1);                        // (files:d#owner)
+                e[k++] = 0x80000000u | (FO + (uint32_t)(g.next() % NO));         // (folders:p#view)
+            }
+        } else if (r < GR) {
+            const uint64_t f = r - FO;
+            out->row_ns[r] = 2;
+            out->row_obj[r] = (uint32_t)f;
+            out->row_rel[r] = D_VIEW;
+            const uint64_t j = f % DRIVE_TREE;
+            if (j) e[k++] = 0x80000000u | (FO + (uint32_t)(f - j + (j - 1) / 8));   // parent folder
+            while (k < ns) e[k++] = 0x80000000u | (GR + (uint32_t)skewed(g, NG, 2.0));
+        } else {
+            out->row_ns[r] = 3;
+            out->row_obj[r] = (uint32_t)(r - GR);
+            out->row_rel[r] = D_MEMBER;
+        }
+        std::sort(e, e + ns);                     // subject sets by (namespace id, object, relation)
+        for (uint32_t j = 0; j < ni; ++j) e[ns + j] = (uint32_t)skewed(g, p->n_users, 1.5);
+        std::sort(e + ns, e + ns + ni);           // subject ids by bytes
+    });
+    return 0;
+}
+
+// Requests files:d#view@u for the Drive-like graph: d uniform; half a user of a row reached by a
+// random walk of 1..depth-1 subject-set hops from files:d#view (real paths), half random users.
+int synth_queries_drive(const synth_graph* g, const synth_params* p, uint64_t n, uint64_t seed, int32_t depth,
+                        keto_check_ids* out, int threads) {
+    parallel_for(n, threads, [&](uint64_t i) {
+        Rng r(seed * 0xA24BAED4963EE407ull ^ (i * 0x9FB21C651E98DF25ull) ^ 0xD21Eull);
+        const uint32_t row = (uint32_t)(2 * (r.next() % p->n_docs) + 1);
+        keto_check_ids q{row, 0, 0, depth};
+        q.target = (uint32_t)(r.next() % p->n_users);
+        if (r.next() & 1) {
+            uint32_t cur = row;
+            const int hops = 1 + (int)(r.next() % (uint64_t)std::max(1, depth - 1));
+            for (int h = 0; h < hops; ++h) {
+                uint64_t b = g->row_ptr[cur], e = g->row_ptr[cur + 1], ns = 0;
+                while (b + ns < e && (g->edges[b + ns] & 0x80000000u)) ++ns;
+                if (!ns) break;
+                cur = g->edges[b + r.next() % ns] & 0x7FFFFFFFu;
+            }
+            uint64_t b = g->row_ptr[cur], e = g->row_ptr[cur + 1], ns = 0;
+            while (b + ns < e && (g->edges[b + ns] & 0x80000000u)) ++ns;
+            if (e - b > ns) q.target = g->edges[b + ns + r.next() % (e - b - ns)];
+        }
+        out[i] = q;
+    });
+    return 0;
+}
+
 void synth_free(synth_graph* g) {
     free(g->row_ns);
     free(g->row_obj);

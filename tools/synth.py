@@ -12,6 +12,7 @@ SRC = os.path.join(HERE, "synth.cpp")
 LIB = os.path.join(HERE, "libketo_synth.so")
 
 NAMESPACES = [(1, "docs"), (2, "folders"), (3, "groups")]
+DRIVE_NAMESPACES = [(1, "files"), (2, "folders"), (3, "groups")]
 
 
 def build(force=False):
@@ -64,6 +65,11 @@ def lib():
 # BASELINE.json config #3: nested group membership, chains up to 32, cycles (seed 3)
 NESTED_100M = dict(n_docs=0, n_folders=0, n_groups=1 << 24, n_users=1 << 24, target_edges=100_000_000, seed=3)
 
+# BASELINE.json config #2 / SURVEY.md 8(d): Drive-like files / folder forest (fan-out 8, depth <= 6) /
+# Zipf(1.1) groups, exactly 10,000,000 tuples (seed 2); n_docs = files, folders = 8 full trees
+DRIVE_10M = dict(n_docs=2_000_000, n_folders=8 * 37449, n_groups=50_000, n_users=1 << 20,
+                 target_edges=10_000_000, seed=2)
+
 
 class SynthGraph:
     def __init__(self, params: dict, threads: int = 16, kind: str = "powerlaw", chain: int = 32):
@@ -71,8 +77,11 @@ class SynthGraph:
         self.kind = kind
         self.p = Params(**{k: params[k] for k, _ in Params._fields_})
         self.g = Graph()
+        self.namespaces = DRIVE_NAMESPACES if kind == "drive" else NAMESPACES
         if kind == "nested":
             rc = lib().synth_generate_nested(C.byref(self.p), C.c_uint32(chain), C.c_int(threads), C.byref(self.g))
+        elif kind == "drive":
+            rc = lib().synth_generate_drive(C.byref(self.p), C.c_int(threads), C.byref(self.g))
         else:
             rc = lib().synth_generate(C.byref(self.p), C.c_int(threads), C.byref(self.g))
         if rc != 0:
@@ -103,7 +112,8 @@ class SynthGraph:
     def queries(self, n: int, seed: int, depth: int = 5, threads: int = 16) -> np.ndarray:
         from keto_amd.capi import CHECK_IDS_DTYPE
         out = np.zeros(n, dtype=CHECK_IDS_DTYPE)
-        lib().synth_queries(C.byref(self.g), C.byref(self.p), C.c_uint64(n), C.c_uint64(seed), C.c_int32(depth),
+        fn = lib().synth_queries_drive if self.kind == "drive" else lib().synth_queries
+        fn(C.byref(self.g), C.byref(self.p), C.c_uint64(n), C.c_uint64(seed), C.c_int32(depth),
                             out.ctypes.data_as(C.c_void_p), C.c_int(threads))
         return out
 
@@ -118,20 +128,20 @@ class SynthGraph:
 
     def snapshot(self, device=0):
         from keto_amd.capi import Snapshot
-        return Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
+        return Snapshot.from_csr(self.namespaces, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                                  device=device)
 
     def snapshot_part(self, part: int, n_parts: int, device=0):
         """This part's share of the edge-partitioned snapshot (keto_snapshot_upload_part)."""
         from keto_amd.capi import Snapshot
-        s = Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
+        s = Snapshot.from_csr(self.namespaces, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                               device=-1)
         return s.upload_part(part, n_parts, device)
 
     def host_snapshot(self):
         """Host-only snapshot (no device): resolution, row owners."""
         from keto_amd.capi import Snapshot
-        return Snapshot.from_csr(NAMESPACES, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
+        return Snapshot.from_csr(self.namespaces, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                                  device=-1)
 
     def oracle_table(self, q: np.ndarray, depth: int):
@@ -151,14 +161,14 @@ class SynthGraph:
                       sobj=arr(t.sobj, np.uint32), srel=arr(t.srel, np.uint32), key=arr(t.key, np.uint32))
         lib().synth_table_free(C.byref(t))
         # string space: objects / relations are per-row ids; namespace names and "" get ids above them
-        strings = {"": 0xFFFFFFF0, "docs": 0xFFFF0001, "folders": 0xFFFF0002, "groups": 0xFFFF0003}
-        return OracleTable(NAMESPACES, arrays, strings, {}, page_size=100)
+        strings = {"": 0xFFFFFFF0, **{n: 0xFFFF0000 + i for i, n in self.namespaces}}
+        return OracleTable(self.namespaces, arrays, strings, {}, page_size=100)
 
     def sql_store(self, tab):
         """The oracle table's tuples in an in-memory SQLite store with the reference schema
         (oracle/oracle_sql.py's SQLStore; strings are the ids as 8-digit hex, so byte order = id order)."""
         from oracle.oracle_sql import SQLStore, _NID
-        st = SQLStore(NAMESPACES)
+        st = SQLStore(self.namespaces)
         n = tab.t.n
         a = tab.arr
         hx = lambda v: f"{int(v):08x}"
@@ -176,7 +186,7 @@ class SynthGraph:
     def sql_requests(self, q: np.ndarray):
         """keto_check_ids -> (RelationTuple, request max-depth) for oracle_sql.CheckEngine."""
         from oracle.oracle_sql import RelationTuple, SubjectID
-        names = dict(NAMESPACES)
+        names = dict(self.namespaces)
         return [(RelationTuple(names[int(self.row_ns[r["row"]])], f"{int(self.row_obj[r['row']]):08x}",
                                f"{int(self.row_rel[r['row']]):08x}", SubjectID(f"{int(r['target']):08x}")),
                  int(r["max_depth"])) for r in q]
