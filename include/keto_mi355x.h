@@ -300,6 +300,17 @@ const keto_tree_node* keto_tree_nodes(const keto_tree_arena* a, uint32_t i, uint
  * Writes at most cap bytes (NUL-terminated) and returns the full length, or a negative code. */
 int64_t keto_tree_json(const keto_snapshot* s, const keto_tree_arena* a, uint32_t i, char* buf, uint64_t cap);
 
+/* Tree i as acl.SubjectTree protobuf bytes, exactly as proto.Marshal(Tree.ToProto())
+ * (internal/expand/tree.go:165-188; proto/ory/keto/acl/v1alpha1/expand_service.proto): the
+ * gRPC Expand response's `tree`.  Writes min(cap, size) bytes, returns the size (0 for a nil tree,
+ * which the reference sends as an unset field), or a negative code. */
+int64_t keto_tree_proto(const keto_snapshot* s, const keto_tree_arena* a, uint32_t i, uint8_t* buf, uint64_t cap);
+/* Every tree of the arena encoded on host threads: offsets[n+1] (tree i = buf[offsets[i],
+ * offsets[i+1]), empty for nil / error trees); buf is written only if cap >= the total, which is
+ * returned (call with buf = NULL to size it). */
+int64_t keto_tree_proto_all(const keto_snapshot* s, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
+                            uint64_t* offsets);
+
 /* String of a subject reference used in keto_tree_node.subject (Subject.String(), definitions.go:163-169). */
 int64_t keto_subject_string(const keto_snapshot* s, uint32_t subject, char* buf, uint64_t cap);
 

@@ -1,0 +1,291 @@
+//go:build keto_gpu
+// +build keto_gpu
+
+// Package gpu binds Keto's read engines to the MI355X engine (libketo_mi355x.so, C-ABI
+// include/keto_mi355x.h).  Drop this directory into the Keto tree as internal/gpu and build with
+// `-tags sqlite,keto_gpu`.  Written for the reference's toolchain, Go 1.17 (go.mod:221): no generics,
+// no runtime.Pinner, no unsafe.StringData.
+//
+// cgo pointer rules: the C side keeps no pointer after a call returns (keto_mi355x.h), and every
+// array handed to it lives in C memory (one C.malloc'd block of structs plus one of string bytes
+// per call), so no Go pointer is ever passed inside a struct.
+package gpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/include
+#cgo LDFLAGS: -lketo_mi355x
+#include <stdlib.h>
+#include "keto_mi355x.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"unsafe"
+
+	"github.com/ory/keto/internal/expand"
+	"github.com/ory/keto/internal/namespace"
+	"github.com/ory/keto/internal/relationtuple"
+)
+
+// Decision statuses of CheckBatch (KETO_CHECK_*).
+const (
+	StatusOK               = uint8(C.KETO_CHECK_OK)
+	StatusUnknownNamespace = uint8(C.KETO_CHECK_UNKNOWN_NAMESPACE)
+	StatusUndecided        = uint8(C.KETO_CHECK_UNDECIDED) // ask the SQL engine for this one request
+)
+
+var (
+	// ErrNotFound mirrors herodot.ErrNotFound for expand roots in unknown namespaces
+	// (internal/expand/handler_test.go:48-59); the caller maps it to its herodot error.
+	ErrNotFound = errors.New("gpu: unknown namespace")
+	// ErrUndecided: the tree exceeds the engine's limits; fall back to the SQL engine.
+	ErrUndecided = errors.New("gpu: tree exceeds the engine's limits")
+)
+
+// Error is a negative KETO_E_* code with the library's thread-local message.
+type Error struct {
+	Code int
+	Msg  string
+}
+
+func (e *Error) Error() string { return fmt.Sprintf("keto_mi355x error %d: %s", e.Code, e.Msg) }
+
+func lastErr(rc C.int) error {
+	if rc == C.KETO_OK {
+		return nil
+	}
+	return &Error{Code: int(rc), Msg: C.GoString(C.keto_last_error())}
+}
+
+// cmem is one call's C memory: an arena of string bytes and the struct arrays, freed together.
+type cmem struct {
+	blocks []unsafe.Pointer
+	str    unsafe.Pointer
+	used   int
+}
+
+func (m *cmem) alloc(n int) unsafe.Pointer {
+	if n < 1 {
+		n = 1
+	}
+	p := C.malloc(C.size_t(n))
+	if p == nil {
+		panic("gpu: C.malloc failed")
+	}
+	m.blocks = append(m.blocks, p)
+	return p
+}
+
+// strings reserves the byte arena for every string the call will pass.
+func (m *cmem) strings(total int) { m.str = m.alloc(total) }
+
+func (m *cmem) s(v string) C.keto_str {
+	if len(v) == 0 {
+		return C.keto_str{}
+	}
+	dst := unsafe.Add(m.str, m.used)
+	copy(unsafe.Slice((*byte)(dst), len(v)), v)
+	m.used += len(v)
+	return C.keto_str{p: (*C.char)(dst), n: C.uint32_t(len(v))}
+}
+
+func (m *cmem) free() {
+	for _, p := range m.blocks {
+		C.free(p)
+	}
+	m.blocks = nil
+}
+
+// Row is one row of keto_relation_tuples (internal/persistence/sql/relationtuples.go:19-31).
+// Rows are passed in commit order: ties of the reference ORDER BY keep that order.
+type Row struct {
+	NamespaceID    int32
+	Object         string
+	Relation       string
+	SubjectID      *string // nil -> subject set
+	SetNamespaceID int32
+	SetObject      string
+	SetRelation    string
+}
+
+// Snapshot is an immutable, device-resident CSR snapshot of the tuple table.
+type Snapshot struct {
+	h       *C.keto_snapshot
+	Version uint64 // bumped by every Apply (snapshot lifecycle, see apply.go)
+}
+
+// Build sorts the rows with the reference ORDER BY (relationtuples.go:250) and uploads the
+// snapshot to HIP device `device` (-1: host only).
+func Build(nss []*namespace.Namespace, rows []Row, device int) (*Snapshot, error) {
+	var m cmem
+	defer m.free()
+	total := 0
+	for _, n := range nss {
+		total += len(n.Name)
+	}
+	for i := range rows {
+		r := &rows[i]
+		total += len(r.Object) + len(r.Relation) + len(r.SetObject) + len(r.SetRelation)
+		if r.SubjectID != nil {
+			total += len(*r.SubjectID)
+		}
+	}
+	m.strings(total)
+	var cns *C.keto_namespace
+	if len(nss) > 0 {
+		cns = (*C.keto_namespace)(m.alloc(len(nss) * int(C.sizeof_keto_namespace)))
+		s := unsafe.Slice(cns, len(nss))
+		for i, n := range nss {
+			s[i] = C.keto_namespace{id: C.int32_t(n.ID), name: m.s(n.Name)}
+		}
+	}
+	var ct *C.keto_tuple
+	if len(rows) > 0 {
+		ct = (*C.keto_tuple)(m.alloc(len(rows) * int(C.sizeof_keto_tuple)))
+		s := unsafe.Slice(ct, len(rows))
+		for i := range rows {
+			r := &rows[i]
+			t := C.keto_tuple{namespace_id: C.int32_t(r.NamespaceID), object: m.s(r.Object), relation: m.s(r.Relation)}
+			if r.SubjectID != nil {
+				t.subject_kind = 0
+				t.subject_id = m.s(*r.SubjectID)
+			} else {
+				t.subject_kind = 1
+				t.set_namespace_id = C.int32_t(r.SetNamespaceID)
+				t.set_object = m.s(r.SetObject)
+				t.set_relation = m.s(r.SetRelation)
+			}
+			s[i] = t
+		}
+	}
+	opts := C.keto_snapshot_opts{page_size: 100, device: C.int32_t(device)}
+	var h *C.keto_snapshot
+	if rc := C.keto_snapshot_build(cns, C.uint32_t(len(nss)), ct, C.uint64_t(len(rows)), &opts, &h); rc != C.KETO_OK {
+		return nil, lastErr(rc)
+	}
+	return &Snapshot{h: h}, nil
+}
+
+// Close releases the host tables and the device arena.
+func (s *Snapshot) Close() {
+	if s.h != nil {
+		C.keto_snapshot_release(s.h)
+		s.h = nil
+	}
+}
+
+func subjectLen(sub relationtuple.Subject) int {
+	switch v := sub.(type) {
+	case *relationtuple.SubjectID:
+		return len(v.ID)
+	case *relationtuple.SubjectSet:
+		return len(v.Namespace) + len(v.Object) + len(v.Relation)
+	}
+	return 0
+}
+
+func (m *cmem) subject(sub relationtuple.Subject) C.keto_subject {
+	switch v := sub.(type) {
+	case *relationtuple.SubjectID:
+		return C.keto_subject{kind: 0, id: m.s(v.ID)}
+	case *relationtuple.SubjectSet:
+		return C.keto_subject{kind: 1, set_namespace: m.s(v.Namespace), set_object: m.s(v.Object),
+			set_relation: m.s(v.Relation)}
+	}
+	return C.keto_subject{kind: 0} // nil subject: matches nothing
+}
+
+// CheckBatch = check.(*Engine).SubjectIsAllowed (internal/check/engine.go:116-123) for many
+// requests: allowed[i] and status[i] (StatusUndecided: ask the SQL engine for request i).
+func (s *Snapshot) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	n := len(reqs)
+	if n == 0 {
+		return nil, nil, nil
+	}
+	if len(depths) != n {
+		return nil, nil, fmt.Errorf("gpu: %d requests, %d depths", n, len(depths))
+	}
+	var m cmem
+	defer m.free()
+	total := 0
+	for _, r := range reqs {
+		total += len(r.Namespace) + len(r.Object) + len(r.Relation) + subjectLen(r.Subject)
+	}
+	m.strings(total)
+	cr := (*C.keto_check_req)(m.alloc(n * int(C.sizeof_keto_check_req)))
+	cs := unsafe.Slice(cr, n)
+	for i, r := range reqs {
+		cs[i] = C.keto_check_req{namespace_: m.s(r.Namespace), object: m.s(r.Object), relation: m.s(r.Relation),
+			subject: m.subject(r.Subject), max_depth: C.int32_t(depths[i])}
+	}
+	allowed := (*C.uint8_t)(m.alloc(n))
+	status := (*C.uint8_t)(m.alloc(n))
+	if rc := C.keto_check_batch(s.h, cr, C.uint32_t(n), C.int32_t(globalMax), allowed, status); rc != C.KETO_OK {
+		return nil, nil, lastErr(rc)
+	}
+	out := make([]bool, n)
+	st := make([]uint8, n)
+	as, ss := unsafe.Slice(allowed, n), unsafe.Slice(status, n)
+	for i := range out {
+		out[i] = as[i] == 1
+		st[i] = uint8(ss[i])
+	}
+	return out, st, nil
+}
+
+// ExpandBatch = expand.(*Engine).BuildTree (internal/expand/engine.go:33-102) for many roots.
+// trees[i] is nil for a nil tree (JSON null); errs[i] is ErrNotFound / ErrUndecided per root.
+func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([]*expand.Tree, []error, error) {
+	n := len(subs)
+	if n == 0 {
+		return nil, nil, nil
+	}
+	if len(depths) != n {
+		return nil, nil, fmt.Errorf("gpu: %d roots, %d depths", n, len(depths))
+	}
+	var m cmem
+	defer m.free()
+	total := 0
+	for _, sub := range subs {
+		total += subjectLen(sub)
+	}
+	m.strings(total)
+	cr := (*C.keto_expand_req)(m.alloc(n * int(C.sizeof_keto_expand_req)))
+	cs := unsafe.Slice(cr, n)
+	for i, sub := range subs {
+		cs[i] = C.keto_expand_req{subject: m.subject(sub), max_depth: C.int32_t(depths[i])}
+	}
+	var a *C.keto_tree_arena
+	if rc := C.keto_expand_batch(s.h, cr, C.uint32_t(n), C.int32_t(globalMax), &a); rc != C.KETO_OK {
+		return nil, nil, lastErr(rc)
+	}
+	defer C.keto_tree_arena_free(a)
+	trees := make([]*expand.Tree, n)
+	errs := make([]error, n)
+	for i := 0; i < n; i++ {
+		switch C.keto_tree_status(a, C.uint32_t(i)) {
+		case C.KETO_EXPAND_NIL:
+			continue
+		case C.KETO_EXPAND_NOT_FOUND:
+			errs[i] = ErrNotFound
+			continue
+		case C.KETO_EXPAND_UNDECIDED:
+			errs[i] = ErrUndecided
+			continue
+		}
+		ln := C.keto_tree_json(s.h, a, C.uint32_t(i), nil, 0)
+		if ln < 0 {
+			return nil, nil, lastErr(C.int(ln))
+		}
+		buf := (*C.char)(m.alloc(int(ln) + 1))
+		C.keto_tree_json(s.h, a, C.uint32_t(i), buf, C.uint64_t(ln+1))
+		t := &expand.Tree{}
+		if err := t.UnmarshalJSON(C.GoBytes(unsafe.Pointer(buf), C.int(ln))); err != nil {
+			return nil, nil, err
+		}
+		trees[i] = t
+	}
+	return trees, errs, nil
+}

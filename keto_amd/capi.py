@@ -31,7 +31,7 @@ EXPORTS = [
     "keto_last_batch_timing", "keto_check_work_device", "keto_expand_batch_ids", "keto_row_handles",
     "keto_check_kernel_name", "keto_snapshot_upload_part", "keto_row_owner", "keto_check_batch_rows_device",
     "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device", "keto_check_batch_rows",
-    "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs",
+    "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs", "keto_tree_proto", "keto_tree_proto_all",
 ]
 
 
@@ -133,6 +133,8 @@ def load():
     lib.keto_tree_count.restype = C.c_uint32
     lib.keto_tree_nodes.restype = C.POINTER(KTreeNode)
     lib.keto_tree_json.restype = C.c_int64
+    lib.keto_tree_proto.restype = C.c_int64
+    lib.keto_tree_proto_all.restype = C.c_int64
     lib.keto_subject_string.restype = C.c_int64
     lib.keto_route_work_bytes.restype = C.c_uint64
     lib.keto_route_work_bytes.argtypes = [C.c_uint32, C.c_uint32]
@@ -432,8 +434,8 @@ class Snapshot:
             self.lib.keto_tree_arena_free(a)
         return status, offs, nodes
 
-    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False):
-        """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes])."""
+    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False):
+        """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes][, proto])."""
         keep = _Keep()
         n = len(reqs)
         arr = (KExpandReq * max(1, n))()
@@ -457,7 +459,15 @@ class Snapshot:
                     nn = C.c_uint64()
                     ptr = self.lib.keto_tree_nodes(a, C.c_uint32(i), C.byref(nn))
                     nodes = [(ptr[j].subject, ptr[j].info) for j in range(nn.value)] if nn.value else []
-                    item = (st, js, nodes)
+                    item = item + (nodes,)
+                if want_proto:
+                    pn = self.lib.keto_tree_proto(self.h, a, C.c_uint32(i), None, C.c_uint64(0))
+                    pb = None
+                    if pn >= 0:
+                        buf = C.create_string_buffer(max(1, pn))
+                        self.lib.keto_tree_proto(self.h, a, C.c_uint32(i), buf, C.c_uint64(pn))
+                        pb = buf.raw[:pn]
+                    item = item + (pb,)
                 out.append(item)
         finally:
             self.lib.keto_tree_arena_free(a)

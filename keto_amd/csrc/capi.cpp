@@ -1,9 +1,12 @@
 // C-ABI of the engine (include/keto_mi355x.h): request resolution (names -> snapshot ids, the
 // role of whereQuery in internal/persistence/sql/relationtuples.go:178-198), batch dispatch to the
 // device engine, and the expand tree arena with its JSON codec (internal/expand/tree.go:85-163).
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 
 #include "snapshot.hpp"
 
@@ -158,6 +161,75 @@ void tree_json(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node
         o.push_back('}');
     }
     o.push_back('}');
+}
+
+// ---- acl.SubjectTree protobuf (proto/ory/keto/acl/v1alpha1/expand_service.proto, acl.proto), the
+// bytes proto.Marshal gives for Tree.ToProto() (internal/expand/tree.go:165-188): node_type = 1
+// (varint; UNION 1, LEAF 4), subject = 2 (Subject: oneof id = 1 | set = 2 {namespace 1, object 2,
+// relation 3; empty strings omitted}, emitted even when empty), children = 3 (repeated, in order).
+void put_varint(std::string& o, uint64_t v) {
+    while (v >= 0x80) {
+        o.push_back((char)(v | 0x80));
+        v >>= 7;
+    }
+    o.push_back((char)v);
+}
+uint64_t varint_len(uint64_t v) {
+    uint64_t k = 1;
+    while (v >= 0x80) {
+        v >>= 7;
+        ++k;
+    }
+    return k;
+}
+void put_field(std::string& o, uint32_t tag, std::string_view b) {
+    o.push_back((char)tag);
+    put_varint(o, b.size());
+    o.append(b);
+}
+std::string subject_proto(const SubjectFields& f) {
+    std::string o;
+    if (!f.set) {
+        put_field(o, 0x0A, f.id);                         // oneof: present even when ""
+        return o;
+    }
+    std::string set;
+    if (!f.ns.empty()) put_field(set, 0x0A, f.ns);
+    if (!f.obj.empty()) put_field(set, 0x12, f.obj);
+    if (!f.rel.empty()) put_field(set, 0x1A, f.rel);
+    put_field(o, 0x12, set);
+    return o;
+}
+// one tree (pre-order nodes) -> SubjectTree bytes: subtree sizes bottom-up (reverse pre-order
+// with a stack of finished children), then one forward pass writes every node behind its
+// children-field tag and length
+void tree_proto(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node* nd, uint64_t n, std::string& o) {
+    std::vector<std::string> subj(n);
+    std::vector<uint64_t> size(n);
+    std::vector<uint64_t> st;
+    for (uint64_t k = n; k-- > 0;) {
+        subj[k] = subject_proto(fields_of(S, a, nd[k].subject));
+        const bool leaf = (nd[k].info & 0x80000000u) != 0;
+        const uint32_t nc = leaf ? 0 : nd[k].info & 0x7FFFFFFFu;
+        uint64_t z = 2 + 1 + varint_len(subj[k].size()) + subj[k].size();
+        for (uint32_t c = 0; c < nc && !st.empty(); ++c) {
+            const uint64_t cz = st.back();
+            st.pop_back();
+            z += 1 + varint_len(cz) + cz;
+        }
+        size[k] = z;
+        st.push_back(z);
+    }
+    o.reserve(o.size() + (n ? size[0] : 0));
+    for (uint64_t k = 0; k < n; ++k) {
+        if (k) {
+            o.push_back((char)0x1A);
+            put_varint(o, size[k]);
+        }
+        o.push_back((char)0x08);
+        o.push_back((nd[k].info & 0x80000000u) ? (char)4 : (char)1);
+        put_field(o, 0x12, subj[k]);
+    }
 }
 
 int64_t copy_out(const std::string& s, char* buf, uint64_t cap) {
@@ -554,6 +626,49 @@ int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_
         tree_json(*h->s, a, a->r.nodes.data() + b, e - b, pos, o);
     }
     return copy_out(o, buf, cap);
+}
+
+int64_t keto_tree_proto(const keto_snapshot* h, const keto_tree_arena* a, uint32_t i, uint8_t* buf, uint64_t cap) {
+    if (!h || !a || i >= a->r.status.size()) return KETO_E_INVALID;
+    const int st = a->r.status[i];
+    if (st == KETO_EXPAND_NOT_FOUND || st == KETO_EXPAND_UNDECIDED) {
+        g_err = st == KETO_EXPAND_NOT_FOUND ? "Unknown namespace" : "the tree exceeds the engine's limits";
+        return st == KETO_EXPAND_NOT_FOUND ? KETO_E_INVALID : KETO_E_RANGE;
+    }
+    if (st != KETO_EXPAND_TREE) return 0;                         // nil tree: no message
+    std::string o;
+    const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+    tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
+    if (buf && cap) std::memcpy(buf, o.data(), std::min<uint64_t>(cap, o.size()));
+    return (int64_t)o.size();
+}
+
+int64_t keto_tree_proto_all(const keto_snapshot* h, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
+                            uint64_t* offsets) {
+    if (!h || !a || !offsets) return KETO_E_INVALID;
+    const uint32_t n = (uint32_t)a->r.status.size();
+    std::vector<std::string> enc(n);
+    const unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> ts;
+    std::atomic<uint32_t> next{0};
+    for (unsigned t = 0; t < th; ++t)
+        ts.emplace_back([&] {
+            for (;;) {
+                const uint32_t k = next.fetch_add(64);
+                if (k >= n) break;
+                for (uint32_t i = k; i < std::min(n, k + 64); ++i)
+                    if (a->r.status[i] == KETO_EXPAND_TREE) {
+                        const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+                        tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, enc[i]);
+                    }
+            }
+        });
+    for (auto& x : ts) x.join();
+    offsets[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + enc[i].size();
+    if (buf && cap >= offsets[n])
+        for (uint32_t i = 0; i < n; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
+    return (int64_t)offsets[n];
 }
 
 int64_t keto_subject_string(const keto_snapshot* h, uint32_t subject, char* buf, uint64_t cap) {

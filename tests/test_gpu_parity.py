@@ -67,3 +67,27 @@ def test_random_graphs_match_oracle(seed, wide):
                 want = ("error", None)
             have = {EXPAND_TREE: "tree", EXPAND_NIL: "nil", EXPAND_NOT_FOUND: "error"}[st]
             assert (have, js) == want, (seed, s, d, g)
+
+
+@pytest.mark.parametrize("seed", range(2000, 2060))
+def test_random_expand_proto_matches_oracle(seed):
+    """keto_tree_proto = proto.Marshal(Tree.ToProto()) of the oracle's tree (internal/expand/tree.go:165-188),
+    byte for byte, on quirk-heavy random graphs (empty fields, collisions, duplicates, cycles)."""
+    from keto_amd.capi import EXPAND_TREE
+    from tests.proto_util import tree_json_to_proto
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=seed % 3 == 0)
+    snap = _snapshot(ns, rows_from_tuples(ns, tuples, raw), ps)
+    exps = random_expands(seed, alph, k=16)
+    for g in sorted({e[2] for e in exps}):
+        grp = [e for e in exps if e[2] == g]
+        got = snap.expand_batch([(subj(s), d) for s, d, _ in grp], g, want_proto=True)
+        for (s, d, _), (st, js, pb) in zip(grp, got):
+            if st == EXPAND_TREE:
+                assert pb == tree_json_to_proto(js), (seed, s, d, g)
+                try:
+                    t = ExpandEngine(store, g).build_tree(s, d)
+                except NotFoundError:
+                    t = None
+                assert t is not None and pb == tree_json_to_proto(t.to_json())
+            else:
+                assert pb in (None, b""), (seed, st, pb)
