@@ -17,7 +17,7 @@
  *   C <ns> <object> <relation> S <set ns> <set object> <set relation> <max depth> <global max depth>
  *   E I <subject id> <max depth> <global max depth>
  *   E S <ns> <object> <relation> <max depth> <global max depth>
- * Output: "check <i> <allowed> <status>", "expand <i> <status> <json|null|error> <proto bytes>",
+ * Output (tab-separated): "check <i> <allowed> <status>", "expand <i> <status> <json|null|error> <proto hex>",
  * "stats ...", "nodevice <rc>".
  */
 #include <stdint.h>
@@ -182,7 +182,7 @@ int main(int argc, char** argv) {
                 break;
             }
             if (rc != KETO_OK) fail("keto_check_batch", rc);
-            printf("check %d %u %u\n", checks++, allowed, status);
+            printf("check\t%d\t%u\t%u\n", checks++, allowed, status);
         } else if (!strcmp(l->f[0], "E") && device >= 0) {
             keto_expand_req r;
             memset(&r, 0, sizeof r);
@@ -210,7 +210,7 @@ int main(int argc, char** argv) {
                 if (keto_tree_json(snap, ar, 0, js, (uint64_t)jn + 1) != jn) return 6;
             }
             const int64_t pn = keto_tree_proto(snap, ar, 0, NULL, 0);
-            printf("expand %d %d %s ", expands++, s, js ? js : "error");
+            printf("expand\t%d\t%d\t%s\t", expands++, s, js ? js : "error");
             if (pn > 0) {
                 uint8_t* pb = (uint8_t*)malloc((size_t)pn);
                 if (keto_tree_proto(snap, ar, 0, pb, (uint64_t)pn) != pn) return 7;

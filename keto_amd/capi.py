@@ -311,6 +311,14 @@ class Snapshot:
             arr[k].max_depth = depth
         return arr
 
+    def check_batch_reqs(self, arr, n: int, global_max_depth=5):
+        """keto_check_batch on a prepared KCheckReq array (string requests: in-library resolution)."""
+        allowed = np.zeros(max(1, n), dtype=np.uint8)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth),
+                                         allowed.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
+        return allowed[:n], status[:n]
+
     def check_batch(self, reqs, global_max_depth=5):
         """reqs: list of (namespace, object, relation, subject, max_depth). Returns (allowed, status)."""
         keep = _Keep()

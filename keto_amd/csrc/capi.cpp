@@ -4,10 +4,12 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
 
+#include "parallel.hpp"
 #include "snapshot.hpp"
 
 using namespace keto;
@@ -353,13 +355,29 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
         std::vector<keto_check_ids> ids(n);
         Overlay ov;
         ov.base = S.n_rows();
+        // resolution (whereQuery on the snapshot) on host threads; wildcard requests that need a
+        // batch-local overlay row are materialized afterwards, in request order
+        std::vector<uint8_t> st(n), wild(n);
+        std::vector<RowKey> wkey(n);
+        std::atomic<bool> failed{false};
+        Error first{KETO_OK, ""};
+        std::mutex emu;
+        par_chunks(n, n >= 65536 ? build_threads() : 1u, 4096, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e && !failed; ++i) {
+                try {
+                    bool w;
+                    ids[i] = resolve_one(S, reqs[i], st[i], w, wkey[i]);
+                    wild[i] = w;
+                } catch (const Error& x) {
+                    std::lock_guard<std::mutex> lk(emu);
+                    if (!failed.exchange(true)) first = x;
+                }
+            }
+        });
+        if (failed) throw first;
         for (uint32_t i = 0; i < n; ++i) {
-            uint8_t st;
-            bool wild;
-            RowKey k;
-            ids[i] = resolve_one(S, reqs[i], st, wild, k);
-            if (wild) ids[i].row = handle_of(S, &ov, overlay_row(S, ov, k));
-            if (status_out) status_out[i] = st;
+            if (wild[i]) ids[i].row = handle_of(S, &ov, overlay_row(S, ov, wkey[i]));
+            if (status_out) status_out[i] = st[i];
         }
         device_check_host(S, ids.data(), n, global_max_depth, allowed_out, FORM_HANDLES, 0, &ov);
         if (status_out)

@@ -17,16 +17,31 @@
 //     internal/relationtuple/definitions.go:163-169): keys shared by two different subjects get
 //     a shared visit id ("collision class") and their rows take the ordered ROW_SEQ path.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <unordered_set>
 
+#include "parallel.hpp"
 #include "snapshot.hpp"
 
 namespace keto {
 
 namespace {
+
+// KETO_BUILD_TRACE=1: builder phase times on stderr (tooling)
+struct PhaseClock {
+    bool on = getenv("KETO_BUILD_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto build] %-28s %8.3f s\n", what, std::chrono::duration<double>(n - t).count());
+        t = n;
+    }
+};
 
 inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
 
@@ -43,29 +58,130 @@ void load_namespaces(Snapshot& S, const keto_namespace* ns, uint32_t n_ns) {
     }
 }
 
-struct Interner {
-    std::unordered_map<std::string_view, uint32_t> tmp;
-    std::vector<std::string_view> views;
-    uint32_t add(std::string_view s) {
-        auto it = tmp.find(s);
-        if (it != tmp.end()) return it->second;
-        uint32_t id = (uint32_t)views.size();
-        tmp.emplace(s, id);
-        views.push_back(s);
-        return id;
-    }
-    // sorts byte-wise; fills S.strs and returns remap old id -> rank
-    std::vector<uint32_t> finish(Snapshot& S) {
-        std::vector<uint32_t> order(views.size());
-        std::iota(order.begin(), order.end(), 0u);
-        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return views[a] < views[b]; });
-        std::vector<uint32_t> rank(views.size());
-        S.strs.resize(views.size());
-        for (uint32_t r = 0; r < order.size(); ++r) {
-            rank[order[r]] = r;
-            S.strs[r] = std::string(views[order[r]]);
+// Sharded parallel interning of the tuple table's strings (objects, relations, subject ids, subject-set
+// objects and relations) plus extra strings: every occurrence is hashed in parallel, thread t owns
+// the shards h % S == t (mod threads) and dedups its occurrences with an open-addressing table, the
+// unique strings are sorted byte-wise with the parallel sample sort, and each occurrence gets its
+// string's rank (= its id: numeric id order is byte order).
+struct ParInterner {
+    static constexpr int FIELDS = 4;    // per tuple: object, relation, subject id | set object, set relation
+    std::vector<uint32_t> occ;          // per occurrence: global unique id, then rank
+    std::vector<std::string_view> uniq; // unique strings by global id
+    std::vector<uint32_t> rank;         // global id -> rank
+
+    static std::string_view field(const keto_tuple& t, int f) {
+        switch (f) {
+            case 0: return std::string_view(t.object.p ? t.object.p : "", t.object.n);
+            case 1: return std::string_view(t.relation.p ? t.relation.p : "", t.relation.n);
+            case 2:
+                return t.subject_kind ? std::string_view(t.set_object.p ? t.set_object.p : "", t.set_object.n)
+                                      : std::string_view(t.subject_id.p ? t.subject_id.p : "", t.subject_id.n);
+            default:
+                return t.subject_kind ? std::string_view(t.set_relation.p ? t.set_relation.p : "", t.set_relation.n)
+                                      : std::string_view();
         }
-        return rank;
+    }
+
+    // occurrences: FIELDS per tuple, then the extras; slot 3 of a subject-id tuple is unused
+    void run(const keto_tuple* tup, uint64_t n, const std::vector<std::string_view>& extra, unsigned threads) {
+        const uint64_t m = n * FIELDS + extra.size();
+        auto view = [&](uint64_t i) -> std::string_view {
+            return i < n * FIELDS ? field(tup[i / FIELDS], (int)(i % FIELDS)) : extra[i - n * FIELDS];
+        };
+        auto used = [&](uint64_t i) { return i >= n * FIELDS || i % FIELDS != 3 || tup[i / FIELDS].subject_kind; };
+        PhaseClock clk;
+        std::vector<uint64_t> hv(m);                // hash | 1; 0 = unused slot
+        // hash pass over static slices; each slice bins its occurrences by owner thread, so an owner
+        // reads only its own occurrences
+        std::vector<std::vector<std::vector<uint64_t>>> bins(threads, std::vector<std::vector<uint64_t>>(threads));
+        par_threads(threads, [&](unsigned t) {
+            const uint64_t lo = (uint64_t)((unsigned __int128)t * m / threads);
+            const uint64_t hi = (uint64_t)((unsigned __int128)(t + 1) * m / threads);
+            for (auto& b : bins[t]) b.reserve((hi - lo) / threads + 16);
+            for (uint64_t i = lo; i < hi; ++i) {
+                if (!used(i)) {
+                    hv[i] = 0;
+                    continue;
+                }
+                const uint64_t h = hash_bytes(view(i)) | 1;
+                hv[i] = h;
+                bins[t][(h >> 40) % threads].push_back(i);
+            }
+        });
+        clk.lap("  intern: hash");
+        occ.assign(m, 0xFFFFFFFFu);
+        // thread t: occurrences whose hash picks it; local ids, then global = base[t] + local
+        std::vector<std::vector<std::string_view>> loc(threads);
+        std::vector<std::vector<uint32_t>> local_id(threads);
+        par_threads(threads, [&](unsigned t) {
+            std::vector<std::string_view>& L = loc[t];
+            uint64_t cap = 1024;
+            std::vector<uint64_t> th(cap, 0);          // hash | 1 (0 = empty)
+            std::vector<uint32_t> tid(cap, 0);
+            uint64_t cnt = 0;
+            auto grow = [&]() {
+                std::vector<uint64_t> nh(cap * 2, 0);
+                std::vector<uint32_t> ni(cap * 2, 0);
+                for (uint64_t i = 0; i < cap; ++i)
+                    if (th[i]) {
+                        uint64_t j = (th[i] >> 1) & (cap * 2 - 1);
+                        while (nh[j]) j = (j + 1) & (cap * 2 - 1);
+                        nh[j] = th[i];
+                        ni[j] = tid[i];
+                    }
+                th.swap(nh);
+                tid.swap(ni);
+                cap *= 2;
+            };
+            for (unsigned src = 0; src < threads; ++src)
+              for (const uint64_t i : bins[src][t]) {
+                const uint64_t h = hv[i];
+                const std::string_view v = view(i);
+                const uint64_t key = h;
+                uint64_t j = (h >> 1) & (cap - 1);
+                for (;;) {
+                    if (!th[j]) {
+                        th[j] = key;
+                        tid[j] = (uint32_t)L.size();
+                        L.push_back(v);
+                        occ[i] = tid[j];
+                        if (++cnt * 2 > cap) grow();
+                        break;
+                    }
+                    if (th[j] == key && L[tid[j]] == v) {
+                        occ[i] = tid[j];
+                        break;
+                    }
+                    j = (j + 1) & (cap - 1);
+                }
+            }
+        });
+        clk.lap("  intern: shard tables");
+        bins.clear();
+        std::vector<uint32_t> base(threads + 1, 0);
+        for (unsigned t = 0; t < threads; ++t) base[t + 1] = base[t] + (uint32_t)loc[t].size();
+        uniq.resize(base[threads]);
+        for (unsigned t = 0; t < threads; ++t) std::copy(loc[t].begin(), loc[t].end(), uniq.begin() + base[t]);
+        par_chunks(m, threads, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i)
+                if (hv[i]) occ[i] += base[(hv[i] >> 40) % threads];
+        });
+        std::vector<uint64_t>().swap(hv);
+        clk.lap("  intern: global ids");
+        std::vector<uint32_t> order(uniq.size());
+        std::iota(order.begin(), order.end(), 0u);
+        parallel_sort(order, [&](uint32_t a, uint32_t b) { return uniq[a] < uniq[b]; }, threads);
+        clk.lap("  intern: sort uniques");
+        rank.assign(uniq.size(), 0);
+        for (uint32_t r = 0; r < order.size(); ++r) rank[order[r]] = r;
+        par_chunks(m, threads, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i)
+                if (occ[i] != 0xFFFFFFFFu) occ[i] = rank[occ[i]];
+        });
+        std::vector<std::string_view> sorted(uniq.size());
+        for (uint32_t r = 0; r < order.size(); ++r) sorted[r] = uniq[order[r]];
+        uniq.swap(sorted);                      // now by rank
+        clk.lap("  intern: ranks");
     }
 };
 
@@ -378,42 +494,42 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
     load_namespaces(S, ns, n_ns);
     if (n && !tup) throw Error{KETO_E_INVALID, "tuples == NULL"};
 
-    // ---- intern strings
-    Interner in;
-    uint32_t e_id = in.add("");
-    for (const auto& nm : S.ns_names) in.add(nm);
+    // ---- intern strings (ids = ranks in byte order), in parallel
+    PhaseClock clk;
+    const unsigned threads = n >= par_min() ? build_threads() : 1u;
     std::vector<T> ts(n);
-    for (uint64_t i = 0; i < n; ++i) {
-        const keto_tuple& t = tup[i];
-        T& x = ts[i];
-        x.ns = t.namespace_id;
-        x.obj = in.add(sv(t.object));
-        x.rel = in.add(sv(t.relation));
-        x.kind = t.subject_kind ? 1 : 0;
-        x.seq = i;
-        if (x.kind == 0) {
-            x.a = in.add(sv(t.subject_id));
-            x.sns = 0;
-            x.srel = 0;
-        } else {
-            x.a = in.add(sv(t.set_object));
-            x.sns = t.set_namespace_id;
-            x.srel = in.add(sv(t.set_relation));
-        }
+    {
+        std::vector<std::string_view> extra{std::string_view("")};
+        for (const auto& nm : S.ns_names) extra.push_back(nm);
+        ParInterner in;
+        in.run(tup, n, extra, threads);
+        S.strs.resize(in.uniq.size());
+        par_chunks(in.uniq.size(), threads, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i) S.strs[i] = std::string(in.uniq[i]);
+        });
+        S.empty_str = in.occ[n * ParInterner::FIELDS];
+        const uint32_t* o = in.occ.data();
+        par_chunks(n, threads, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i) {
+                const keto_tuple& t = tup[i];
+                T& x = ts[i];
+                const uint32_t* q = o + i * ParInterner::FIELDS;
+                x.ns = t.namespace_id;
+                x.obj = q[0];
+                x.rel = q[1];
+                x.kind = t.subject_kind ? 1 : 0;
+                x.seq = i;
+                x.a = q[2];
+                x.sns = x.kind ? t.set_namespace_id : 0;
+                x.srel = x.kind ? q[3] : 0;
+            }
+        });
     }
-    std::vector<uint32_t> rank = in.finish(S);
-    S.empty_str = rank[e_id];
-    for (auto& x : ts) {
-        x.obj = rank[x.obj];
-        x.rel = rank[x.rel];
-        x.a = rank[x.a];
-        if (x.kind == 1) x.srel = rank[x.srel];
-    }
-    in.tmp.clear();
-    in.views.clear();
 
-    // ---- reference ORDER BY
-    std::sort(ts.begin(), ts.end(), tuple_less);
+    clk.lap("intern");
+    // ---- reference ORDER BY (parallel sample sort; tuple_less is a total order: commit seq last)
+    parallel_sort(ts, tuple_less, threads);
+    clk.lap("order by");
 
     // ---- real rows
     std::vector<uint64_t> real_ptr;   // per real row begin (in tuple index space)
@@ -458,21 +574,46 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
         return id;
     };
 
-    // ---- real-row edges
+    // ---- real-row edges: subject sets whose target is a real row are resolved in parallel (binary
+    // search over the sorted real rows); the rest (unknown namespaces, empty and wildcard targets)
+    // go through target_row in tuple order, which creates their rows in the sequential order
     std::vector<uint32_t> real_edges(n);
     std::vector<uint8_t> poison(n, 0);
-    for (uint64_t i = 0; i < n; ++i) {
-        const T& x = ts[i];
-        bool own_unknown = !S.ns_by_id.count(x.ns);
-        if (x.kind == 0) {
+    constexpr uint32_t LATER = 0xFFFFFFFEu;
+    par_chunks(n, threads, 1 << 15, [&](uint64_t b, uint64_t e, unsigned) {
+        for (uint64_t i = b; i < e; ++i) {
+            const T& x = ts[i];
+            const bool own_unknown = !S.ns_by_id.count(x.ns);
             real_edges[i] = x.a;
             poison[i] = own_unknown;
-        } else {
-            bool p;
-            uint32_t r = target_row(x.sns, x.a, x.srel, p);
-            real_edges[i] = p ? EDGE_POISON : (EDGE_SET | r);
-            poison[i] = p || own_unknown;
+            if (x.kind == 1) {
+                real_edges[i] = LATER;
+                auto it = S.ns_by_id.find(x.sns);
+                if (it == S.ns_by_id.end() || S.ns_names[it->second].empty() || x.a == S.empty_str ||
+                    x.srel == S.empty_str)
+                    continue;
+                const RowKey k{(int64_t)x.sns, x.a, x.srel};
+                uint32_t lo = 0, hi = S.n_real_rows;
+                while (lo < hi) {
+                    const uint32_t m = lo + (hi - lo) / 2;
+                    const int64_t c = key_cmp(S.row_key[m], k);
+                    if (c == 0) {
+                        real_edges[i] = EDGE_SET | m;
+                        break;
+                    }
+                    if (c < 0) lo = m + 1; else hi = m;
+                }
+            }
+            if (poison[i] && real_edges[i] != LATER) real_edges[i] = EDGE_POISON;
         }
+    });
+    for (uint64_t i = 0; i < n; ++i) {
+        if (real_edges[i] != LATER) continue;
+        const T& x = ts[i];
+        bool p;
+        const uint32_t r = target_row(x.sns, x.a, x.srel, p);
+        real_edges[i] = p ? EDGE_POISON : (EDGE_SET | r);
+        poison[i] = p || poison[i];
         if (poison[i]) real_edges[i] = EDGE_POISON;
     }
     uint32_t R = (uint32_t)S.row_key.size();
@@ -509,41 +650,66 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
     }
     row_ptr[R] = S.edges.size();
 
-    // ---- visit-key collision classes over every typed subject: rows (sets) and subject ids
+    clk.lap("rows + edges");
+    // ---- visit-key collision classes over every typed subject: rows (sets) and subject ids.  A
+    // 64-bit hash of every key (rows' String() and used ids, in parallel) is sorted; only keys whose
+    // hash occurs twice are materialized and grouped exactly.
     {
-        std::unordered_map<std::string, uint32_t> owners;   // key -> number of distinct typed subjects
-        std::vector<std::string> row_keys(R);
-        for (uint32_t r = 0; r < R; ++r) {
-            const RowKey& k = S.row_key[r];
-            if (k.ns != ANY_NS && !S.ns_by_id.count((int32_t)k.ns)) continue;   // unknown-ns rows are never subjects
-            row_keys[r] = S.subject_string(EDGE_SET | r);
-            owners[row_keys[r]]++;
-        }
         std::vector<uint8_t> id_used(S.strs.size(), 0);
         for (uint32_t e : S.edges)
             if (!(e & EDGE_SET) && e != EDGE_POISON) id_used[e] = 1;
-        for (uint32_t s = 0; s < S.strs.size(); ++s)
-            if (id_used[s]) owners[S.strs[s]]++;
-        std::unordered_map<std::string, uint32_t> cls;
-        for (auto& kv : owners)
-            if (kv.second >= 2) cls.emplace(kv.first, (uint32_t)cls.size());
-        S.n_coll_keys = (uint32_t)cls.size();
-        if (!cls.empty()) {
-            for (uint32_t r = 0; r < R; ++r) {
-                if (row_keys[r].empty() && S.row_key[r].ns != ANY_NS) continue;
-                auto it = cls.find(row_keys[r]);
-                if (it != cls.end()) S.coll[EDGE_SET | r] = VID_CLASS | it->second;
+        auto row_subject = [&](uint32_t r) {          // unknown-ns rows are never subjects
+            const RowKey& k = S.row_key[r];
+            return k.ns == ANY_NS || S.ns_by_id.count((int32_t)k.ns) != 0;
+        };
+        constexpr uint32_t ROW_TAG = 0x80000000u;
+        std::vector<std::pair<uint64_t, uint32_t>> hk(R + S.strs.size());
+        std::vector<uint8_t> keep(R + S.strs.size(), 0);
+        par_chunks(R + S.strs.size(), threads, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i) {
+                if (i < R) {
+                    if (!row_subject((uint32_t)i)) continue;
+                    hk[i] = {hash_bytes(S.subject_string(EDGE_SET | (uint32_t)i)), ROW_TAG | (uint32_t)i};
+                } else {
+                    const uint32_t sid = (uint32_t)(i - R);
+                    if (!id_used[sid]) continue;
+                    hk[i] = {hash_bytes(S.strs[sid]), sid};
+                }
+                keep[i] = 1;
             }
-            for (uint32_t s = 0; s < S.strs.size(); ++s) {
-                if (!id_used[s]) continue;
-                auto it = cls.find(S.strs[s]);
-                if (it != cls.end()) S.coll[s] = VID_CLASS | it->second;
-            }
+        });
+        {
+            uint64_t w = 0;
+            for (uint64_t i = 0; i < hk.size(); ++i)
+                if (keep[i]) hk[w++] = hk[i];
+            hk.resize(w);
+        }
+        parallel_sort(hk, [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) {
+            return x.first != y.first ? x.first < y.first : x.second < y.second;
+        }, threads);
+        std::unordered_map<std::string, std::vector<uint32_t>> owners;   // candidate key -> typed subjects
+        for (uint64_t i = 0; i < hk.size();) {
+            uint64_t j = i + 1;
+            while (j < hk.size() && hk[j].first == hk[i].first) ++j;
+            if (j - i >= 2)
+                for (uint64_t k = i; k < j; ++k) {
+                    const uint32_t tag = hk[k].second;
+                    owners[(tag & ROW_TAG) ? S.subject_string(EDGE_SET | (tag & ~ROW_TAG)) : S.strs[tag]].push_back(tag);
+                }
+            i = j;
+        }
+        S.n_coll_keys = 0;
+        for (auto& kv : owners) {
+            if (kv.second.size() < 2) continue;             // a hash collision, not a key collision
+            const uint32_t c = VID_CLASS | S.n_coll_keys++;
+            for (uint32_t tag : kv.second) S.coll[(tag & ROW_TAG) ? (EDGE_SET | (tag & ~ROW_TAG)) : tag] = c;
         }
     }
 
+    clk.lap("collision classes");
     finalize_rows(S, row_ptr, is_wild);
     compute_layout(S);
+    clk.lap("rows + layout");
     return Sp;
 }
 

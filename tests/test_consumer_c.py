@@ -73,11 +73,11 @@ def test_consumer_host_only(consumer, tmp_path, case):
 def test_consumer_golden_on_gpu(consumer, tmp_path, case):
     from tests.proto_util import tree_json_to_proto
     out = _run(consumer, tmp_path, case, 0)
-    checks = [ln.split(" ") for ln in out if ln.startswith("check ")]
+    checks = [ln.split("\t") for ln in out if ln.startswith("check\t")]
     assert len(checks) == len(case.get("checks", []))
     for c, (_, _, allowed, status) in zip(case.get("checks", []), checks):
         assert bool(int(allowed)) == c["expected"], c
-    exps = [ln.split(" ", 4) for ln in out if ln.startswith("expand ")]
+    exps = [ln.split("\t") for ln in out if ln.startswith("expand\t")]
     assert len(exps) == len(case.get("expands", []))
     for e, (_, _, status, js, pb) in zip(case.get("expands", []), exps):
         if e.get("expected_error"):

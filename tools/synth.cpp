@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <numeric>
 #include <thread>
 #include <vector>
 
@@ -522,6 +523,111 @@ int synth_extract(const synth_graph* g, const synth_params* p, const keto_check_
         }
     }
     return 0;
+}
+
+// ---- the same graph as keto_relation_tuples rows (strings, commit order) for keto_snapshot_build:
+// objects are "%08x" of their per-namespace id, relations rel_names[id] (byte order = id order),
+// users "u%08x"; tuples come in a seeded pseudo-random commit order (i -> (a i + b) mod E).  Strings
+// are shared: every keto_str points into one name table.
+typedef struct {
+    uint64_t n;
+    keto_tuple* tuples;
+    char* names;
+    uint64_t obj_base, user_base, rel_base;   // offsets of the three tables in `names`
+    uint32_t rel_off[8], rel_len[8];
+} synth_strings;
+
+static inline keto_str kstr(const char* p, uint32_t n) {
+    keto_str s;
+    s.p = p;
+    s.n = n;
+    return s;
+}
+
+int synth_emit_strings(const synth_graph* g, const synth_params* p, const char* const* rel_names, uint32_t n_rel,
+                       uint64_t seed, int threads, synth_strings* out) {
+    if (n_rel > 8) return -1;
+    uint32_t max_obj = 0;
+    for (uint32_t r = 0; r < g->n_rows; ++r) max_obj = std::max(max_obj, g->row_obj[r]);
+    const uint64_t objs = (uint64_t)max_obj + 1, users = p->n_users;
+    uint64_t rel_bytes = 0;
+    for (uint32_t i = 0; i < n_rel; ++i) rel_bytes += strlen(rel_names[i]);
+    out->obj_base = 0;
+    out->user_base = objs * 8;
+    out->rel_base = out->user_base + users * 9;
+    out->names = (char*)malloc(out->rel_base + rel_bytes + 1);
+    out->n = g->n_edges;
+    out->tuples = (keto_tuple*)calloc(std::max<uint64_t>(1, g->n_edges), sizeof(keto_tuple));
+    if (!out->names || !out->tuples) return -2;
+    static const char* hex = "0123456789abcdef";
+    parallel_for(objs, threads, [&](uint64_t i) {
+        char* d = out->names + out->obj_base + i * 8;
+        for (int k = 7; k >= 0; --k) d[7 - k] = hex[(i >> (4 * k)) & 15];
+    });
+    parallel_for(users, threads, [&](uint64_t i) {
+        char* d = out->names + out->user_base + i * 9;
+        d[0] = 'u';
+        for (int k = 7; k >= 0; --k) d[8 - k] = hex[(i >> (4 * k)) & 15];
+    });
+    uint64_t at = out->rel_base;
+    for (uint32_t i = 0; i < n_rel; ++i) {
+        out->rel_off[i] = (uint32_t)(at - out->rel_base);
+        out->rel_len[i] = (uint32_t)strlen(rel_names[i]);
+        memcpy(out->names + at, rel_names[i], out->rel_len[i]);
+        at += out->rel_len[i];
+    }
+    const uint64_t E = g->n_edges;
+    uint64_t a = (splitmix(seed) | 1) % std::max<uint64_t>(E, 1);
+    while (E > 1 && std::gcd(a, E) != 1) a = (a + 2) % E;
+    const uint64_t b = splitmix(seed + 1) % std::max<uint64_t>(E, 1);
+    auto obj = [&](uint32_t o) { return kstr(out->names + out->obj_base + (uint64_t)o * 8, 8); };
+    auto rel = [&](uint32_t r) { return kstr(out->names + out->rel_base + out->rel_off[r], out->rel_len[r]); };
+    parallel_for(g->n_rows, threads, [&](uint64_t r) {
+        for (uint64_t i = g->row_ptr[r]; i < g->row_ptr[r + 1]; ++i) {
+            const uint64_t pos = E > 1 ? (uint64_t)(((unsigned __int128)i * a + b) % E) : i;
+            keto_tuple& t = out->tuples[pos];
+            t.namespace_id = g->row_ns[r];
+            t.object = obj(g->row_obj[r]);
+            t.relation = rel(g->row_rel[r]);
+            const uint32_t e = g->edges[i];
+            if (e & 0x80000000u) {
+                const uint32_t x = e & 0x7FFFFFFFu;
+                t.subject_kind = 1;
+                t.set_namespace_id = g->row_ns[x];
+                t.set_object = obj(g->row_obj[x]);
+                t.set_relation = rel(g->row_rel[x]);
+            } else {
+                t.subject_kind = 0;
+                t.subject_id = kstr(out->names + out->user_base + (uint64_t)e * 9, 9);
+            }
+        }
+    });
+    return 0;
+}
+
+// keto_check_ids with CSR row ids and user targets -> keto_check_req by name (namespace names
+// ns_names[namespace id])
+int synth_check_reqs(const synth_graph* g, const synth_strings* st, const keto_check_ids* q, uint64_t n,
+                     const char* const* ns_names, keto_check_req* out, int threads) {
+    parallel_for(n, threads, [&](uint64_t i) {
+        keto_check_req& r = out[i];
+        memset(&r, 0, sizeof r);
+        const uint32_t row = q[i].row;
+        const char* nm = ns_names[g->row_ns[row]];
+        r.namespace_ = kstr(nm, (uint32_t)strlen(nm));
+        r.object = kstr(st->names + st->obj_base + (uint64_t)g->row_obj[row] * 8, 8);
+        r.relation = kstr(st->names + st->rel_base + st->rel_off[g->row_rel[row]], st->rel_len[g->row_rel[row]]);
+        r.subject.kind = 0;
+        r.subject.id = kstr(st->names + st->user_base + (uint64_t)q[i].target * 9, 9);
+        r.max_depth = q[i].max_depth;
+    });
+    return 0;
+}
+
+void synth_strings_free(synth_strings* s) {
+    free(s->tuples);
+    free(s->names);
+    memset(s, 0, sizeof(*s));
 }
 
 void synth_table_free(synth_table* t) {

@@ -32,6 +32,12 @@ class Graph(C.Structure):
                 ("edges", C.POINTER(C.c_uint32)), ("n_edges", C.c_uint64), ("n_set_edges", C.c_uint64)]
 
 
+class Strings(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("tuples", C.c_void_p), ("names", C.c_void_p), ("obj_base", C.c_uint64),
+                ("user_base", C.c_uint64), ("rel_base", C.c_uint64), ("rel_off", C.c_uint32 * 8),
+                ("rel_len", C.c_uint32 * 8)]
+
+
 class Table(C.Structure):
     _fields_ = [("n", C.c_uint64), ("ns", C.c_void_p), ("obj", C.c_void_p), ("rel", C.c_void_p),
                 ("kind", C.c_void_p), ("sid", C.c_void_p), ("sns", C.c_void_p), ("sobj", C.c_void_p),
@@ -137,6 +143,54 @@ class SynthGraph:
         s = Snapshot.from_csr(self.namespaces, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                               device=-1)
         return s.upload_part(part, n_parts, device)
+
+    def relation_names(self):
+        """Relation names by id (byte order = id order): the generators' relation ids."""
+        return ["member", "owner", "view"] if self.kind == "drive" else ["member", "view"]
+
+    def string_tuples(self, seed=7, threads=16):
+        """The graph as keto_relation_tuples rows with strings, in a seeded commit order
+        (synth_emit_strings); kept alive by the returned object."""
+        rel = self.relation_names()
+        arr = (C.c_char_p * len(rel))(*[x.encode() for x in rel])
+        st = Strings()
+        rc = lib().synth_emit_strings(C.byref(self.g), C.byref(self.p), arr, C.c_uint32(len(rel)), C.c_uint64(seed),
+                                      C.c_int(threads), C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"synth_emit_strings failed: {rc}")
+        self._strings = st
+        return st
+
+    def snapshot_from_strings(self, st, device=0):
+        """keto_snapshot_build (the product's builder: interning, ORDER BY, collision classes) over
+        the string rows; returns (Snapshot, build seconds)."""
+        import time
+        from keto_amd.capi import KNamespace, KOpts, Snapshot, _Keep, _check, load
+        keep = _Keep()
+        ns = (KNamespace * len(self.namespaces))(*[KNamespace(i, keep.s(n)) for i, n in self.namespaces])
+        h = C.c_void_p()
+        opts = KOpts(100, device, 0)
+        t0 = time.perf_counter()
+        _check(load().keto_snapshot_build(ns, len(self.namespaces), C.c_void_p(st.tuples), C.c_uint64(st.n),
+                                          C.byref(opts), C.byref(h)))
+        return Snapshot(h, load()), time.perf_counter() - t0
+
+    def string_requests(self, st, q: np.ndarray, threads=16):
+        """keto_check_ids (CSR row ids, user targets) -> keto_check_req by name, for keto_check_batch."""
+        from keto_amd.capi import KCheckReq
+        names = [b""] * 4
+        for i, n in self.namespaces:
+            names[i] = n.encode()
+        na = (C.c_char_p * 4)(*names)
+        out = (KCheckReq * len(q))()
+        qa = np.ascontiguousarray(q)
+        lib().synth_check_reqs(C.byref(self.g), C.byref(st), qa.ctypes.data_as(C.c_void_p), C.c_uint64(len(q)), na,
+                               out, C.c_int(threads))
+        out._keep = (na, names)
+        return out
+
+    def free_strings(self, st):
+        lib().synth_strings_free(C.byref(st))
 
     def host_snapshot(self):
         """Host-only snapshot (no device): resolution, row owners."""
