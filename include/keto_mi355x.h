@@ -284,6 +284,12 @@ const char* keto_check_kernel_name(int32_t global_max_depth);
 int keto_check_work_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]);
 
+/* Per-request loop iterations of the check_kernel tiers (deep batches, global max-depth > 9): the
+ * length of each request's serial chain of dependent steps, for its latency histogram.  d_steps:
+ * n uint32 on the device (instrumented kernels, same decisions). */
+int keto_check_steps_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                            uint8_t* d_allowed_out, uint32_t* d_steps);
+
 /* Batched BuildTree.  The arena owns all trees; free it with keto_tree_arena_free. */
 int keto_expand_batch(keto_snapshot* s, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
                       keto_tree_arena** out);

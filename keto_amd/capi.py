@@ -32,6 +32,7 @@ EXPORTS = [
     "keto_check_kernel_name", "keto_snapshot_upload_part", "keto_row_owner", "keto_check_batch_rows_device",
     "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device", "keto_check_batch_rows",
     "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs", "keto_tree_proto", "keto_tree_proto_all",
+    "keto_check_steps_device",
 ]
 
 
@@ -415,6 +416,11 @@ class Snapshot:
         _check(self.lib.keto_check_work_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
                                                C.c_int32(global_max_depth), C.c_void_p(d_out_ptr), out))
         return list(out)
+
+    def check_steps_device(self, d_ids_ptr: int, n: int, d_out_ptr: int, d_steps_ptr: int, global_max_depth=32):
+        _check(self.lib.keto_check_steps_device(self.h, C.c_void_p(d_ids_ptr), C.c_uint32(n),
+                                                C.c_int32(global_max_depth), C.c_void_p(d_out_ptr),
+                                                C.c_void_p(d_steps_ptr)))
 
     # ------------------------------------------------------------------ expand
     def expand_batch_ids(self, roots: np.ndarray, depths: np.ndarray, global_max_depth=5):

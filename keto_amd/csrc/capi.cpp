@@ -527,6 +527,16 @@ int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint3
     });
 }
 
+int keto_check_steps_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                            uint8_t* d_allowed_out, uint32_t* d_steps) {
+    return guarded([&] {
+        if (!h || (n && (!d_reqs || !d_allowed_out || !d_steps))) throw Error{KETO_E_INVALID, "NULL argument"};
+        uint64_t w[KETO_WORK_SLOTS];
+        device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, nullptr, w, d_steps);
+        return KETO_OK;
+    });
+}
+
 int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
                       keto_tree_arena** out) {
     return guarded([&] {

@@ -510,6 +510,9 @@ struct TierArgs {
     // eighths of the XCD's range) is done; 0 = static runs only
     uint32_t* heads;
     uint32_t dyn;
+    // COUNT kernels: per-request loop iterations (the serial chain length of a request's search),
+    // added over the tiers that ran it; NULL = not recorded
+    uint32_t* steps;
 };
 
 // ------------------------------------------------------------------ check
@@ -614,6 +617,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     bool tset = false;
     uint32_t cwb = 0;            // T's closure-filter word << 5 | bit
     Frame cur{0, 0, 0, 0};
+    uint32_t it = 0;                // iterations of the current request (COUNT: ta.steps)
     const uint32_t* ce = s.arena;   // arena of the current frame
     uint4 blk = make_uint4(0, 0, 0, 0);
     uint64_t blk_at = ~0ull;        // word index of the 16-B edge block held in blk
@@ -625,6 +629,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
         uint32_t cbw = NONE32;       // its closure-filter word of T (subject sets only)
         const uint32_t* ea = s.arena;   // its arena
         int res = -1;                // >= 0: request decided (RES_*)
+        if constexpr (COUNT) ++it;
         if (!busy) {
             if (j >= j_end) break;
             qi = ta.in_list ? ta.in_list[j] : j;
@@ -638,6 +643,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
                 continue;
             }
             busy = true;
+            if constexpr (COUNT) it = 1;
             tset = (qq.flags & 1u) != 0;
             T = qq.target;
             {
@@ -776,6 +782,9 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             }
         }
         if (res >= 0) {
+            if constexpr (COUNT) {
+                if (ta.steps) ta.steps[qi] += it;
+            }
             if (res == RES_OVERFLOW) {
                 uint32_t at = atomicAdd(ta.out_count, 1u);
                 ta.out_list[at] = qi;
@@ -1465,6 +1474,7 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     a.pool = nullptr;
     a.heads = nullptr;
     a.dyn = 0;
+    a.steps = nullptr;
     a.pool_mask = 0;
     a.pool_n = 0;
     a.pool_epoch = nullptr;
@@ -1968,7 +1978,8 @@ namespace {
 // The check of one device-resident batch: the tier plan and the kernel launches.  The caller holds
 // D.mu and has set the device; `dq` / `da` are device buffers.
 void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
-                  hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate) {
+                  hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
+                  uint32_t* d_steps = nullptr) {
     if (n == 0) {
         if (!accumulate) D.last = keto_batch_timing{};
         return;
@@ -2041,11 +2052,13 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
         dwork = dmalloc<unsigned long long>(KETO_WORK_SLOTS, acc);
         tmp.p.push_back(dwork);
         HIP_OK(hipMemsetAsync(dwork, 0, KETO_WORK_SLOTS * sizeof(unsigned long long), st));
+        if (d_steps) HIP_OK(hipMemsetAsync(d_steps, 0, (uint64_t)n * sizeof(uint32_t), st));
     }
     run_tiers(D, D.tiers, n, p, st,
               [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
+                  a.steps = dwork ? d_steps : nullptr;
                   if (level < 2 && p.pool) {
                       const Tier& tn = D.tiers[level + 1];
                       a.pool = tn.vtab;
@@ -2183,13 +2196,13 @@ uint64_t chunk_requests() {
 }  // namespace
 
 void device_check(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
-                  uint64_t* work_out) {
+                  uint64_t* work_out, uint32_t* d_steps) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));
     hipStream_t st = stream ? (hipStream_t)stream : D.stream;
-    check_locked(S, D, d_reqs, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, work_out, false);
+    check_locked(S, D, d_reqs, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, work_out, false, d_steps);
 }
 
 // Host-buffer batches: the requests go to the device in chunks of KETO_CHUNK (default 4M), so the

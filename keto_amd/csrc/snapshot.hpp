@@ -243,7 +243,7 @@ void device_release(Snapshot& s);
 uint64_t device_bytes(const Snapshot& s);
 // device-resident requests and decisions, enqueued on `stream` (NULL: the snapshot's own)
 void device_check(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
-                  uint64_t* work_out = nullptr);
+                  uint64_t* work_out = nullptr, uint32_t* d_steps = nullptr);
 // host buffers: pipelined chunks (H2D / check / D2H overlapped); form FORM_* (keto_check_ids by
 // handle or by row id, 8-B keto_check_pair by row id with one request depth); ov = batch-local
 // wildcard rows

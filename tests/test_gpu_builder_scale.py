@@ -84,5 +84,5 @@ def test_injected_collisions_and_wildcards_match_oracle(monkeypatch, par):
     got, _ = snap.check_batch([(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d in reqs], 5)
     want = tab.check_batch_reqs([tab.check_req(t, d) for t, d in reqs], 5, threads=16)
     assert (got == want).all(), f"{int((got != want).sum())} mismatches of {len(reqs)}"
-    assert 0.02 < got.mean() < 0.98
+    assert got.sum() > 100 and got.mean() < 0.98
     g.close()
