@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16, help="host threads (generator, cpu baseline)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="requests in the cpu_baseline sample")
-    ap.add_argument("--sql-sample", type=int, default=300, help="requests in the ref_sql (SQLite) sample")
+    ap.add_argument("--sql-sample", type=int, default=10_000, help="requests in the ref_sql (SQLite) sample")
     ap.add_argument("--bytes-sample", type=float, default=0.01,
                     help="fraction of the batch priced in the oracle's BFS-count mode (roofline bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -77,6 +77,62 @@ def parse():
                     help="batches timed end to end through the host API (keto_check_batch_rows, pinned buffers); 0 = skip")
     ap.add_argument("--e2e-only", action="store_true", help="time only the end-to-end leg (profiling runs)")
     return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def sql_leg(g, q, a, gpu_out):
+    """ref-sql: oracle/oracle_sql.py (the reference check engine's recursion issuing its SELECT ...
+    ORDER BY ... LIMIT 100 OFFSET and page count per node) over the tuples the sample reaches, in
+    SQLite, with a.threads worker processes (oracle/sql_bench.py, started as a child process)."""
+    import subprocess
+    import tempfile
+    k = min(a.sql_sample, len(q))
+    log(f"ref_sql over {k} requests (SQLite, {a.threads} worker processes)")
+    t0 = time.perf_counter()
+    stab = g.oracle_table(q[:k], a.depth)
+    store = g.sql_store(stab)
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    fd, db = tempfile.mkstemp(prefix="keto_refsql_", suffix=".sqlite", dir=shm)
+    os.close(fd)
+    fd, rq = tempfile.mkstemp(prefix="keto_refsql_", suffix=".json")
+    os.close(fd)
+    try:
+        dst = __import__("sqlite3").connect(db)
+        store.conn.backup(dst)
+        dst.close()
+        store.conn.close()
+        reqs = [(t.namespace, t.object, t.relation, t.subject.id, d) for t, d in g.sql_requests(q[:k])]
+        json.dump({"namespaces": g.namespaces, "requests": reqs}, open(rq, "w"))
+        t_setup = time.perf_counter() - t0
+        r = subprocess.run([sys.executable, "-m", "oracle.sql_bench", "--db", db, "--requests", rq, "--workers",
+                            str(a.threads), "--gmd", str(a.depth)], capture_output=True, text=True, cwd=ROOT,
+                           timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"oracle.sql_bench failed: {r.stderr[-2000:]}")
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        for f in (db, rq):
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+    dec = np.array(res["decisions"], dtype=np.uint8)
+    return {"value": res["checks_per_s"], "unit": "checks/s", "cores": res["workers"],
+            "mismatches_vs_gpu": int((dec != gpu_out[:k]).sum()),
+            "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model(), "workers_used": res["workers"]},
+            "sample": f"first {k} requests; oracle/oracle_sql.py (the reference check engine's recursion issuing "
+                      f"its SELECT ... ORDER BY ... LIMIT 100 OFFSET and page count per node) over the {stab.t.n} "
+                      f"tuples they reach, in-memory SQLite copies of one image in each of {res['workers']} "
+                      f"worker processes (setup {t_setup:.1f} s, slowest worker {res['slowest_worker_s']:.2f} s)"}
 
 
 def end_to_end(snap, q, a, d_out):
@@ -157,7 +213,7 @@ def main():
         d_q = torch.from_numpy(q.view(np.int32).reshape(-1, 4).copy()).to(f"cuda:{dev}")
         owner_dev = torch.from_numpy(snap.row_owner(np.arange(g.n_rows, dtype=np.uint32), world).astype(np.int16)
                                      ).to(f"cuda:{dev}")
-        routed = [0]
+        routed = [0, None]
 
         def step():
             recv, state = route_device(d_q, owner_dev, rank, world)
@@ -165,6 +221,7 @@ def main():
             snap.check_batch_rows_device(recv.data_ptr(), len(recv), dec.data_ptr(), a.depth, sp)
             send_back(dec, state, d_out, world)
             routed[0] = len(recv)
+            routed[1] = recv
     else:
         qd = snap.with_handles(q)        # request resolution (row ids -> row handles), untimed
         d_q = torch.from_numpy(qd.view(np.uint8)).to(f"cuda:{dev}")
@@ -236,12 +293,19 @@ def main():
         # bytes the tier-0 kernel's own traversal requests (instrumented pass, same decisions):
         # 32 B header + window per row visit, 16 B per id-table bucket, 16 B per edge-block reload,
         # 16 B per request in, 1 B per decision out
-        if a.partitioned:                # the instrumented pass takes handle-form requests
-            w = [0] * 16
+        if a.partitioned:
+            # the instrumented pass takes handle-form requests: the batch this rank received, by handle
+            from keto_amd.capi import CHECK_IDS_DTYPE
+            rq = routed[1].cpu().numpy().view(CHECK_IDS_DTYPE).reshape(-1).copy()
+            rq["row"] = snap.row_handles(rq["row"])
+            d_h = torch.from_numpy(rq.view(np.uint8)).to(f"cuda:{dev}")
+            d_w = torch.empty(len(rq), dtype=torch.uint8, device=f"cuda:{dev}")
+            w = snap.check_work_device(d_h.data_ptr(), len(rq), d_w.data_ptr(), a.depth)
         else:
             w = snap.check_work_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth)
         rows, edges, idreads, vprobes, vinserts, items = w[:6]
-        touched = 32 * w[0] + 16 * w[9] + 16 * w[8] + 17 * a.batch
+        nw = routed[0] if a.partitioned else a.batch        # requests the instrumented pass ran
+        touched = (32 * w[0] + 16 * w[9] + 16 * w[8]) * a.batch / max(1, nw) + 17 * a.batch
         kname = snap.check_kernel_name(a.depth)
         traffic, tsrc = pmc_traffic(kname, {"tuples": int(g.n_edges), "checks_per_gpu_per_step": a.batch,
                                             "max_depth": a.depth, "scale": a.scale})
@@ -255,10 +319,11 @@ def main():
                                         f"{a.threads} threads, {t_bfs:.1f} s)",
                     "traversal_bytes_per_launch": int(touched),
                     "traversal_GBps": round(touched / (tier0_ms * 1e-3) / 1e9, 1)}
-        work = {"rows_per_check": rows / a.batch, "set_edges_per_check": edges / a.batch,
-                "id_words_per_check": idreads / a.batch, "visited_hbm_probes_per_check": vprobes / a.batch,
-                "top_level_items_per_check": items / a.batch,
-                "line_touches_per_check": {k: round(v / a.batch, 3) for k, v in zip(
+        nwd = max(1, nw)
+        work = {"rows_per_check": rows / nwd, "set_edges_per_check": edges / nwd,
+                "id_words_per_check": idreads / nwd, "visited_hbm_probes_per_check": vprobes / nwd,
+                "top_level_items_per_check": items / nwd, "instrumented_requests": int(nw),
+                "line_touches_per_check": {k: round(v / nwd, 3) for k, v in zip(
                     ("request", "header", "edge", "id_table", "id_search", "frame_push", "frame_pop"), w[6:13])}}
         # ---- CPU baseline (N = 1): the oracle restatement timed on the sample, decisions compared
         if world == 1 and not a.no_cpu_baseline:
@@ -268,28 +333,14 @@ def main():
             t_cpu = time.perf_counter() - t0
             parity = {"sample": int(ns), "mismatches": int((ref != gpu_out[:ns]).sum())}
             cpu = {"value": round(ns / t_cpu, 1), "unit": "checks/s", "cores": a.threads, "kind": "port",
+                   "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model()},
                    "sample": f"first {ns} requests of the rank-0 batch; oracle/keto_oracle.c over the "
                              f"{tab.t.n} tuples those requests can reach (extracted in {t_tab:.1f} s), "
                              f"{a.threads} host threads, {t_cpu:.2f} s"}
-            # the reference engine's algorithm issuing its own SQL against in-memory SQLite
-            # (oracle/oracle_sql.py), one core, on a small sample
+            # the reference engine's algorithm issuing its own SQL against SQLite, one worker process
+            # per core (oracle/sql_bench.py), on a bounded sample
             if a.sql_sample > 0:
-                from oracle.oracle_sql import CheckEngine
-                k = min(a.sql_sample, ns)
-                log(f"ref_sql over {k} requests (SQLite, 1 core)")
-                stab = g.oracle_table(q[:k], a.depth)
-                store = g.sql_store(stab)
-                eng = CheckEngine(store, a.depth)
-                rq = g.sql_requests(q[:k])
-                t0 = time.perf_counter()
-                sql = np.array([eng.subject_is_allowed(r, d) for r, d in rq], dtype=np.uint8)
-                t_sql = time.perf_counter() - t0
-                ref_sql = {"value": round(k / t_sql, 1), "unit": "checks/s", "cores": 1,
-                           "mismatches_vs_gpu": int((sql != gpu_out[:k]).sum()),
-                           "sample": f"first {k} requests; oracle/oracle_sql.py (the reference check engine's "
-                                     f"recursion issuing its SELECT ... ORDER BY ... LIMIT 100 OFFSET and page "
-                                     f"count per node) over the {stab.t.n} tuples they reach in in-memory "
-                                     f"SQLite, {t_sql:.2f} s"}
+                ref_sql = sql_leg(g, q, a, gpu_out)
 
     if e2e is not None and roofline is not None:
         e2e["frac"] = round(roofline["alg_bytes_per_launch"] / (e2e["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)

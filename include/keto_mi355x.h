@@ -45,6 +45,7 @@ extern "C" {
 #define KETO_E_NOMEM (-3)       /* host or device allocation failed */
 #define KETO_E_CONFIG (-4)      /* namespace config not supported (duplicate ids or names) */
 #define KETO_E_RANGE (-5)       /* a size limit of the snapshot format was exceeded */
+#define KETO_E_REBUILD (-6)     /* keto_snapshot_apply: this write needs a rebuild (snapshot unchanged) */
 
 /* per-query status of keto_check_batch (allowed_out is always valid) */
 #define KETO_CHECK_OK 0                 /* decision equals the reference engine's */
@@ -178,6 +179,24 @@ int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespac
 
 void keto_snapshot_release(keto_snapshot* s);
 
+/* Snapshot lifecycle: apply one write transaction the way TransactRelationTuples does
+ * (internal/persistence/sql/relationtuples.go:289-297): the inserts first (each after every equal
+ * tuple, as commit_time orders them, :128-149), then the deletes (every tuple equal in namespace,
+ * object, relation and subject, :200-223).  The changed rows are rewritten in the device arena in
+ * place (forwards when a row outgrows its place; the tail grows on demand) and closure filters are
+ * re-closed, between batches; later batches see the new version.  An unknown namespace id fails the
+ * whole transaction (KETO_E_INVALID), like GetNamespaceByName.  KETO_E_REBUILD: this write changes
+ * what the build derives globally (a new Subject.String() collision, a stored subject set with an
+ * empty field, a row a stored wildcard set materializes, a poisoned row, a partitioned snapshot); the
+ * snapshot is unchanged and the caller rebuilds it from the table.  Row handles (keto_row_handles,
+ * keto_resolve_checks) are per version: resolve again after a write.  *version_out (may be NULL)
+ * gets the new version: the snaptoken the reference leaves "not yet implemented"
+ * (internal/check/handler.go:182). */
+int keto_snapshot_apply(keto_snapshot* s, const keto_tuple* inserts, uint64_t n_inserts, const keto_tuple* deletes,
+                        uint64_t n_deletes, uint64_t* version_out);
+/* Version of the snapshot: 0 after the build, +1 per keto_snapshot_apply. */
+uint64_t keto_snapshot_version(const keto_snapshot* s);
+
 /* Edge-partitioned upload, for graphs larger than one GPU (one process per GPU, n_parts parts).
  * Takes a host-only snapshot (built with device = -1) and uploads to `device` only
  *   - every row that is the target of some subject set (these are kept on all parts), and
@@ -188,6 +207,16 @@ void keto_snapshot_release(keto_snapshot* s);
  * level only visits rows every part holds, so each part answers exactly.  Calls naming another
  * part's root row fail with KETO_E_INVALID.  Replaces nothing in the reference. */
 int keto_snapshot_upload_part(keto_snapshot* s, uint32_t part, uint32_t n_parts, int32_t device);
+/* Arena a part of an edge-partitioned upload would hold (host-only snapshots; sizing aid):
+ * arena_bytes of the part's device arena, shared_bytes of it in rows every part keeps. */
+typedef struct {
+    uint64_t arena_bytes;
+    uint64_t shared_bytes;
+    uint32_t rows;              /* rows on the part */
+    uint32_t shared_rows;       /* of them: rows some subject set points at (on every part) */
+    uint32_t root_rows;         /* of them: this part's root rows */
+} keto_part_stats;
+int keto_snapshot_part_stats(keto_snapshot* s, uint32_t part, uint32_t n_parts, keto_part_stats* out);
 /* keto_check_batch_device on requests that name rows by row id (row and subject-set target), the
  * form requests travel in between parts: each is translated to this device's handles first.  A
  * request for another part's root row fails the call with KETO_E_INVALID. */

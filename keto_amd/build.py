@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libketo_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["snapshot.cpp", "capi.cpp", "engine.hip", "route.hip"]
+SOURCES = ["snapshot.cpp", "delta.cpp", "capi.cpp", "engine.hip", "route.hip"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 
 
@@ -20,7 +20,7 @@ def _stale(target, deps):
 
 
 def build(verbose=False, force=False):
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "snapshot.hpp"),
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "parallel.hpp"), os.path.join(CSRC, "snapshot.hpp"),
                                                         os.path.join(HERE, "..", "include", "keto_mi355x.h")]
     if not force and not _stale(OUT, deps):
         return OUT
@@ -29,7 +29,7 @@ def build(verbose=False, force=False):
         path = os.path.join(CSRC, src)
         obj = os.path.join(CSRC, src + ".o")
         objs.append(obj)
-        if not force and not _stale(obj, [path, deps[-2], deps[-1]]):
+        if not force and not _stale(obj, [path] + deps[len(SOURCES):]):
             continue
         cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, "-c", path, "-o", obj]
         if src.endswith(".cpp"):

@@ -17,6 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KETO_LIB") or os.path.join(HERE, "libketo_mi355x.so")   # KETO_LIB: tuning builds
 
 KETO_OK = 0
+E_REBUILD = -6
 CHECK_OK, CHECK_UNKNOWN_NAMESPACE, CHECK_UNDECIDED = 0, 1, 2
 UNDECIDED = 2                 # decision byte of the ids / device entry points
 EXPAND_TREE, EXPAND_NIL, EXPAND_NOT_FOUND, EXPAND_UNDECIDED = 0, 1, 2, 3
@@ -32,7 +33,7 @@ EXPORTS = [
     "keto_check_kernel_name", "keto_snapshot_upload_part", "keto_row_owner", "keto_check_batch_rows_device",
     "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device", "keto_check_batch_rows",
     "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs", "keto_tree_proto", "keto_tree_proto_all",
-    "keto_check_steps_device",
+    "keto_check_steps_device", "keto_snapshot_part_stats", "keto_snapshot_apply", "keto_snapshot_version",
 ]
 
 
@@ -98,6 +99,11 @@ class KTiming(C.Structure):
                 ("chunks", C.c_uint32), ("wall_ms", C.c_float)]
 
 
+class KPartStats(C.Structure):
+    _fields_ = [("arena_bytes", C.c_uint64), ("shared_bytes", C.c_uint64), ("rows", C.c_uint32),
+                ("shared_rows", C.c_uint32), ("root_rows", C.c_uint32)]
+
+
 class KStats(C.Structure):
     _fields_ = [("n_tuples", C.c_uint64), ("n_edges", C.c_uint64), ("n_rows", C.c_uint32),
                 ("n_real_rows", C.c_uint32), ("n_wildcard_rows", C.c_uint32), ("n_seq_rows", C.c_uint32),
@@ -138,6 +144,7 @@ def load():
     lib.keto_tree_proto_all.restype = C.c_int64
     lib.keto_subject_string.restype = C.c_int64
     lib.keto_route_work_bytes.restype = C.c_uint64
+    lib.keto_snapshot_version.restype = C.c_uint64
     lib.keto_route_work_bytes.argtypes = [C.c_uint32, C.c_uint32]
     _lib = lib
     return lib
@@ -233,14 +240,8 @@ class Snapshot:
             pass
 
     # ------------------------------------------------------------------ builders
-    @classmethod
-    def build(cls, namespaces: Sequence[Tuple[int, str]], rows: Iterable[tuple], page_size=100, device=0):
-        """rows: (ns_id, obj, rel, sid) for subject ids, (ns_id, obj, rel, None, sns_id, sobj, srel) for sets,
-        in commit order."""
-        lib = load()
-        keep = _Keep()
-        ns = (KNamespace * max(1, len(namespaces)))(*[KNamespace(i, keep.s(n)) for i, n in namespaces])
-        rows = list(rows)
+    @staticmethod
+    def _tuples(keep: "_Keep", rows):
         tt = (KTuple * max(1, len(rows)))()
         for k, r in enumerate(rows):
             t = tt[k]
@@ -255,6 +256,30 @@ class Snapshot:
                 t.set_namespace_id = r[4]
                 t.set_object = keep.s(r[5])
                 t.set_relation = keep.s(r[6])
+        return tt
+
+    def apply(self, inserts=(), deletes=()) -> int:
+        """keto_snapshot_apply: one TransactRelationTuples (inserts, then deletes), rows as in build();
+        returns the new version.  Raises KetoError (code -6 = KETO_E_REBUILD: rebuild instead)."""
+        keep = _Keep()
+        ins, dels = list(inserts), list(deletes)
+        ver = C.c_uint64()
+        _check(self.lib.keto_snapshot_apply(self.h, self._tuples(keep, ins), C.c_uint64(len(ins)),
+                                            self._tuples(keep, dels), C.c_uint64(len(dels)), C.byref(ver)))
+        return ver.value
+
+    def version(self) -> int:
+        return int(self.lib.keto_snapshot_version(self.h))
+
+    @classmethod
+    def build(cls, namespaces: Sequence[Tuple[int, str]], rows: Iterable[tuple], page_size=100, device=0):
+        """rows: (ns_id, obj, rel, sid) for subject ids, (ns_id, obj, rel, None, sns_id, sobj, srel) for sets,
+        in commit order."""
+        lib = load()
+        keep = _Keep()
+        ns = (KNamespace * max(1, len(namespaces)))(*[KNamespace(i, keep.s(n)) for i, n in namespaces])
+        rows = list(rows)
+        tt = cls._tuples(keep, rows)
         h = C.c_void_p()
         opts = KOpts(page_size, device, 0)
         _check(lib.keto_snapshot_build(ns, len(namespaces), tt, C.c_uint64(len(rows)), C.byref(opts), C.byref(h)))
@@ -264,6 +289,12 @@ class Snapshot:
         """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part)."""
         _check(self.lib.keto_snapshot_upload_part(self.h, C.c_uint32(part), C.c_uint32(n_parts), C.c_int32(device)))
         return self
+
+    def part_stats(self, part: int, n_parts: int) -> dict:
+        """keto_snapshot_part_stats: the arena part `part` of n_parts would hold (host-only snapshot)."""
+        st = KPartStats()
+        _check(self.lib.keto_snapshot_part_stats(self.h, C.c_uint32(part), C.c_uint32(n_parts), C.byref(st)))
+        return {f: getattr(st, f) for f, _ in KPartStats._fields_}
 
     def row_owner(self, rows: np.ndarray, n_parts: int) -> np.ndarray:
         """Owner part of each row id (-1: held by every part)."""

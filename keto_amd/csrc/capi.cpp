@@ -314,6 +314,7 @@ void keto_snapshot_release(keto_snapshot* s) { delete s; }
 int keto_snapshot_get_stats(const keto_snapshot* h, keto_snapshot_stats* out) {
     return guarded([&] {
         if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         const Snapshot& S = *h->s;
         out->n_tuples = S.n_tuples;
         out->n_edges = S.edges.size();
@@ -333,6 +334,7 @@ int keto_resolve_checks(const keto_snapshot* h, const keto_check_req* reqs, uint
                         uint8_t* status_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         for (uint32_t i = 0; i < n; ++i) {
             uint8_t st;
             bool wild;
@@ -351,6 +353,7 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
                      uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         Snapshot& S = *h->s;
         std::vector<keto_check_ids> ids(n);
         Overlay ov;
@@ -394,6 +397,7 @@ int keto_check_batch_ids(keto_snapshot* h, const keto_check_ids* reqs, uint32_t 
                          uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_HANDLES, 0, nullptr);
         return KETO_OK;
     });
@@ -403,6 +407,7 @@ int keto_check_batch_rows(keto_snapshot* h, const keto_check_ids* reqs, uint32_t
                           uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_ROWS, 0, nullptr);
         return KETO_OK;
     });
@@ -412,6 +417,7 @@ int keto_check_batch_pairs(keto_snapshot* h, const keto_check_pair* reqs, uint32
                            int32_t global_max_depth, uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_PAIRS, max_depth, nullptr);
         return KETO_OK;
     });
@@ -431,6 +437,7 @@ int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
                             uint8_t* d_allowed_out, void* stream) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream);
         return KETO_OK;
     });
@@ -439,6 +446,7 @@ int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
 int keto_row_handles(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t* out) {
     return guarded([&] {
         if (!h || (n && (!rows || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         const Snapshot& S = *h->s;
         for (uint64_t i = 0; i < n; ++i) {
             if (rows[i] == KETO_NO_ROW) { out[i] = KETO_NO_ROW; continue; }
@@ -464,10 +472,26 @@ int keto_check_batch_rows_device(keto_snapshot* h, const keto_check_ids* d_reqs,
                                  uint8_t* d_allowed_out, void* stream) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         device_check_rows(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream);
         return KETO_OK;
     });
 }
+
+int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_inserts, const keto_tuple* deletes,
+                        uint64_t n_deletes, uint64_t* version_out) {
+    return guarded([&] {
+        if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        Snapshot& S = *h->s;
+        std::unique_lock<std::shared_mutex> lk(S.rw);
+        apply_writes(S, inserts, n_inserts, deletes, n_deletes);
+        device_apply(S);
+        if (version_out) *version_out = S.version;
+        return KETO_OK;
+    });
+}
+
+uint64_t keto_snapshot_version(const keto_snapshot* h) { return h ? h->s->version : 0; }
 
 int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device) {
     return guarded([&] {
@@ -479,6 +503,28 @@ int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts,
         S.n_parts = n_parts;
         compute_layout(S);
         device_upload(S, device);
+        return KETO_OK;
+    });
+}
+
+int keto_snapshot_part_stats(keto_snapshot* h, uint32_t part, uint32_t n_parts, keto_part_stats* out) {
+    return guarded([&] {
+        if (!h || !out || n_parts == 0 || part >= n_parts) throw Error{KETO_E_INVALID, "bad argument"};
+        Snapshot& S = *h->s;
+        if (S.dev) throw Error{KETO_E_INVALID, "part statistics need a host-only snapshot (device = -1)"};
+        const uint32_t p0 = S.part, n0 = S.n_parts;
+        S.part = part;
+        S.n_parts = n_parts;
+        compute_layout(S);
+        out->arena_bytes = S.n_units * HDR_WORDS * 4;
+        out->shared_bytes = S.shared_words * 4;
+        out->rows = (uint32_t)S.rows_by_unit.size();
+        out->shared_rows = 0;
+        for (uint32_t r = 0; r < S.n_rows(); ++r) out->shared_rows += !S.is_root[r];
+        out->root_rows = out->rows - out->shared_rows;
+        S.part = p0;
+        S.n_parts = n0;
+        compute_layout(S);
         return KETO_OK;
     });
 }
@@ -522,6 +568,7 @@ int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint3
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]) {
     return guarded([&] {
         if (!h || !out || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, nullptr, out);
         return KETO_OK;
     });
@@ -531,6 +578,7 @@ int keto_check_steps_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
                             uint8_t* d_allowed_out, uint32_t* d_steps) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out || !d_steps))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         uint64_t w[KETO_WORK_SLOTS];
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, nullptr, w, d_steps);
         return KETO_OK;
@@ -541,6 +589,7 @@ int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n,
                       keto_tree_arena** out) {
     return guarded([&] {
         if (!h || !out || (n && !reqs)) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         *out = nullptr;
         Snapshot& S = *h->s;
         auto a = std::make_unique<keto_tree_arena>();
@@ -596,6 +645,7 @@ int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t
                           int32_t global_max_depth, keto_tree_arena** out) {
     return guarded([&] {
         if (!h || !out || (n && (!roots || !max_depth))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
         *out = nullptr;
         Snapshot& S = *h->s;
         auto a = std::make_unique<keto_tree_arena>();

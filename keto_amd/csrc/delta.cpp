@@ -1,0 +1,302 @@
+// Snapshot lifecycle: writes applied to a live snapshot as a delta, with a version.
+//
+// The reference reads the live table on every check (internal/persistence/sql/relationtuples.go:
+// 238-277), so a snapshot must follow the writes.  keto_snapshot_apply takes one transaction the way
+// TransactRelationTuples runs it (relationtuples.go:289-297): the inserts first (InsertRelationTuple,
+// :128-149: a new row with commit_time = now, i.e. after every equal tuple), then the deletes
+// (DeleteRelationTuples, :200-223: every tuple equal to the given one -- namespace, object,
+// relation and the exact subject).  A namespace name that is not configured fails the whole
+// transaction, as GetNamespaceByName does there.
+//
+// Every row the transaction touches gets its new edge list in ORDER BY order (sets before ids,
+// sets by namespace id then object / relation bytes, ids by bytes, ties in commit order) in
+// Snapshot::row_over; device_apply (engine.hip) rewrites those rows in the device arena.  New strings
+// are appended after the build's byte-ordered ones and compared by bytes wherever order matters.
+//
+// Writes outside this delta path throw KETO_E_REBUILD and leave the snapshot unchanged; the caller
+// rebuilds it (keto_snapshot_build from the table).  They are the ones that would change what the
+// build derived globally: a new Subject.String() collision, a stored subject set with an empty field
+// (a materialized wildcard row), a row that a stored wildcard set materializes, a poisoned row, or a
+// partitioned snapshot.
+#include <algorithm>
+#include <cstring>
+
+#include "snapshot.hpp"
+
+namespace keto {
+
+namespace {
+
+inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
+
+struct Txn {
+    Snapshot& S;
+    std::unordered_map<uint32_t, std::vector<uint32_t>> rows;    // staged edges per touched row
+    std::vector<uint32_t> order;                                  // touched rows, first-touch order
+    std::vector<std::string> new_strs;                            // strings this transaction adds
+    std::unordered_map<std::string, uint32_t> new_str_id;
+    std::vector<RowKey> new_keys;                                 // rows this transaction adds
+    std::unordered_map<RowKey, uint32_t, RowKeyHash> new_row_id;
+    std::vector<uint32_t> new_targets;                            // rows some inserted subject set points at
+
+    explicit Txn(Snapshot& s) : S(s) {}
+
+    int32_t ns_id(std::string_view name) const {
+        auto it = S.ns_by_name.find(std::string(name));
+        if (it == S.ns_by_name.end())
+            throw Error{KETO_E_INVALID, "Unknown namespace with name " + std::string(name) + "."};
+        return S.ns_ids[it->second];
+    }
+    int32_t ns_id_checked(int32_t id) const {
+        if (!S.ns_by_id.count(id)) throw Error{KETO_E_INVALID, "Unknown namespace with id " + std::to_string(id) + "."};
+        return id;
+    }
+    // string id, existing or staged (-1: absent and !add)
+    int64_t str(std::string_view s, bool add) {
+        const int64_t id = S.lookup_str(s);
+        if (id >= 0) return id;
+        auto it = new_str_id.find(std::string(s));
+        if (it != new_str_id.end()) return it->second;
+        if (!add) return -1;
+        const uint32_t nid = (uint32_t)(S.strs.size() + new_strs.size());
+        if (nid >= EDGE_VAL) throw Error{KETO_E_RANGE, "more than 2^31-1 strings"};
+        new_strs.emplace_back(s);
+        new_str_id.emplace(std::string(s), nid);
+        return nid;
+    }
+    const std::string& str_of(uint32_t id) const {
+        return id < S.strs.size() ? S.strs[id] : new_strs[id - S.strs.size()];
+    }
+    int cmp(uint32_t a, uint32_t b) const {
+        if (a == b) return 0;
+        if (a < S.n_sorted_strs && b < S.n_sorted_strs) return a < b ? -1 : 1;
+        const int c = str_of(a).compare(str_of(b));
+        return c < 0 ? -1 : c > 0 ? 1 : 0;
+    }
+    const RowKey& key(uint32_t r) const { return r < S.row_key.size() ? S.row_key[r] : new_keys[r - S.row_key.size()]; }
+    // ORDER BY position of a subject set: (namespace id, object bytes, relation bytes)
+    int set_cmp(uint32_t ra, uint32_t rb) const {
+        const RowKey &a = key(ra), &b = key(rb);
+        if (a.ns != b.ns) return a.ns < b.ns ? -1 : 1;
+        if (a.obj != b.obj) return cmp(a.obj, b.obj);
+        if (a.rel != b.rel) return cmp(a.rel, b.rel);
+        return 0;
+    }
+    // row of a complete key (-1: none yet)
+    int64_t row(const RowKey& k) const {
+        uint32_t lo = 0, hi = S.n_real_rows;
+        while (lo < hi) {
+            const uint32_t m = lo + (hi - lo) / 2;
+            const RowKey& x = S.row_key[m];
+            const int c = x.ns != k.ns ? (x.ns < k.ns ? -1 : 1) : x.obj != k.obj ? (x.obj < k.obj ? -1 : 1)
+                                                                    : x.rel != k.rel ? (x.rel < k.rel ? -1 : 1) : 0;
+            if (c == 0) return m;
+            if (c < 0) lo = m + 1; else hi = m;
+        }
+        auto it = S.row_of.find(k);
+        if (it != S.row_of.end()) return it->second;
+        auto jt = new_row_id.find(k);
+        return jt == new_row_id.end() ? -1 : (int64_t)jt->second;
+    }
+    uint32_t row_or_new(const RowKey& k) {
+        const int64_t r = row(k);
+        if (r >= 0) return (uint32_t)r;
+        const uint32_t id = (uint32_t)(S.row_key.size() + new_keys.size());
+        if (id >= EDGE_VAL) throw Error{KETO_E_RANGE, "more than 2^31-1 rows"};
+        new_keys.push_back(k);
+        new_row_id.emplace(k, id);
+        return id;
+    }
+    std::vector<uint32_t>& edges(uint32_t r) {
+        auto it = rows.find(r);
+        if (it != rows.end()) return it->second;
+        const auto e = r < S.rows.size() ? S.row_edges(r) : std::pair<const uint32_t*, uint64_t>{nullptr, 0};
+        order.push_back(r);
+        return rows.emplace(r, std::vector<uint32_t>(e.first, e.first + e.second)).first->second;
+    }
+    // 0 < position of edge value v among e (sets before ids), after every equal edge
+    uint64_t upper(const std::vector<uint32_t>& e, uint32_t v) const {
+        uint64_t lo = 0, hi = e.size();
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) / 2;
+            if (less(v, e[m])) hi = m; else lo = m + 1;
+        }
+        return lo;
+    }
+    bool less(uint32_t a, uint32_t b) const {           // strict ORDER BY of two edge values
+        const bool sa = a & EDGE_SET, sb = b & EDGE_SET;
+        if (sa != sb) return sa;                        // subject_id NULL (sets) first
+        if (sa) return set_cmp(a & EDGE_VAL, b & EDGE_VAL) < 0;
+        return cmp(a, b) < 0;
+    }
+
+    RowKey tuple_key(const keto_tuple& t, bool add) {
+        RowKey k;
+        k.ns = ns_id_checked(t.namespace_id);
+        const int64_t o = str(sv(t.object), add), r = str(sv(t.relation), add);
+        k.obj = o < 0 ? ANY : (uint32_t)o;                                // ANY: absent (delete only)
+        k.rel = r < 0 ? ANY : (uint32_t)r;
+        return k;
+    }
+    // edge value of the tuple's subject; ~0 when it cannot exist (delete of unknown strings)
+    uint32_t subject_value(const keto_tuple& t, bool add) {
+        if (!t.subject_kind) {
+            const int64_t id = str(sv(t.subject_id), add);
+            return id < 0 ? NONE : (uint32_t)id;
+        }
+        const int32_t sns = ns_id_checked(t.set_namespace_id);
+        const std::string& name = S.ns_names[S.ns_by_id.at(sns)];
+        if (name.empty() || t.set_object.n == 0 || t.set_relation.n == 0)
+            throw Error{KETO_E_REBUILD, "a subject set with an empty field (a wildcard row) needs a rebuild"};
+        const int64_t o = str(sv(t.set_object), add), r = str(sv(t.set_relation), add);
+        if (o < 0 || r < 0) return NONE;
+        const RowKey k{(int64_t)sns, (uint32_t)o, (uint32_t)r};
+        if (!add) {
+            const int64_t x = row(k);
+            return x < 0 ? NONE : (EDGE_SET | (uint32_t)x);
+        }
+        const uint32_t x = row_or_new(k);
+        new_targets.push_back(x);
+        return EDGE_SET | x;
+    }
+    static constexpr uint32_t NONE = 0xFFFFFFFFu;
+};
+
+std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {
+    auto it = S.ns_by_id.find((int32_t)k.ns);
+    const std::string ns = it == S.ns_by_id.end() ? "" : S.ns_names[it->second];
+    return ns + ":" + T.str_of(k.obj) + "#" + T.str_of(k.rel);
+}
+
+}  // namespace
+
+void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del) {
+    if (S.n_parts > 1) throw Error{KETO_E_INVALID, "writes need a replicated snapshot (not an edge-partitioned part)"};
+    if ((n_ins && !ins) || (n_del && !del)) throw Error{KETO_E_INVALID, "NULL tuples"};
+    Txn T(S);
+    // ---- inserts (commit order: after every equal tuple), then deletes (every equal tuple)
+    for (uint64_t i = 0; i < n_ins; ++i) {
+        const keto_tuple& t = ins[i];
+        const RowKey k = T.tuple_key(t, true);
+        const uint32_t v = T.subject_value(t, true);
+        const uint32_t r = T.row_or_new(k);
+        std::vector<uint32_t>& e = T.edges(r);
+        e.insert(e.begin() + T.upper(e, v), v);
+    }
+    for (uint64_t i = 0; i < n_del; ++i) {
+        const keto_tuple& t = del[i];
+        const RowKey k = T.tuple_key(t, false);
+        const uint32_t v = T.subject_value(t, false);
+        if (k.obj == ANY || k.rel == ANY || v == Txn::NONE) continue;     // nothing can match
+        const int64_t r = T.row(k);
+        if (r < 0) continue;
+        std::vector<uint32_t>& e = T.edges((uint32_t)r);
+        e.erase(std::remove(e.begin(), e.end(), v), e.end());
+    }
+    // ---- what the delta path cannot express: the caller rebuilds
+    for (uint32_t r : T.order) {
+        if (r < S.rows.size()) {
+            if (S.row_pp[r] != NO_PAGE) throw Error{KETO_E_REBUILD, "a write touches a poisoned row"};
+            const RowKey& k = S.row_key[r];
+            if (k.ns == ANY_NS || k.obj == ANY || k.rel == ANY) throw Error{KETO_E_REBUILD, "a write touches a wildcard row"};
+        }
+        if (S.n_wild_rows) {
+            const RowKey& k = T.key(r);
+            for (uint32_t w = 0; w < S.n_rows(); ++w) {
+                const RowKey& wk = S.row_key[w];
+                if (!(wk.ns == ANY_NS || wk.obj == ANY || wk.rel == ANY)) continue;
+                if ((wk.ns == ANY_NS || wk.ns == k.ns) && (wk.obj == ANY || wk.obj == k.obj) &&
+                    (wk.rel == ANY || wk.rel == k.rel))
+                    throw Error{KETO_E_REBUILD, "a write touches a row a stored wildcard set materializes"};
+            }
+        }
+    }
+    {
+        // Subject.String() collisions (graph_utils.go:13-35 keys): a new row whose String() is an
+        // existing string (a subject id, or any text: conservative) or another row's, and a new
+        // subject id equal to some row's String()
+        auto row_key_str = [&](uint32_t r) { return key_string(S, T, T.key(r)); };
+        std::unordered_map<std::string, uint32_t> written_keys;
+        for (uint32_t i = 0; i < T.new_keys.size(); ++i) {
+            const uint32_t r = (uint32_t)S.row_key.size() + i;
+            const std::string ks = row_key_str(r);
+            if (S.lookup_str(ks) >= 0 || T.new_str_id.count(ks) || S.vid_of_key(ks) != 0xFFFFFFF0u ||
+                written_keys.count(ks))
+                throw Error{KETO_E_REBUILD, "a new row's key collides with another subject's (Subject.String())"};
+            written_keys.emplace(ks, r);
+        }
+        for (uint64_t i = 0; i < n_ins; ++i) {
+            const keto_tuple& t = ins[i];
+            if (t.subject_kind) continue;
+            const std::string_view sid = sv(t.subject_id);
+            if (sid.find(':') == std::string_view::npos || sid.find('#') == std::string_view::npos) continue;
+            const int64_t id = T.str(sid, false);
+            if (id >= 0 && S.coll.count((uint32_t)id)) continue;           // an existing collision class
+            if (S.vid_of_key(std::string(sid)) != 0xFFFFFFF0u || written_keys.count(std::string(sid)))
+                throw Error{KETO_E_REBUILD, "a subject id collides with a subject set's String()"};
+        }
+    }
+    // ---- commit
+    const uint32_t R0 = S.n_rows();
+    for (auto& x : T.new_strs) {
+        S.added_str.emplace(x, (uint32_t)S.strs.size());
+        S.strs.push_back(std::move(x));
+    }
+    for (auto& k : T.new_keys) {
+        S.row_of.emplace(k, (uint32_t)S.row_key.size());
+        S.row_key.push_back(k);
+        S.rows.push_back(RowRec{0, 0, 0, 0});
+        S.row_pp.push_back(NO_PAGE);
+        S.unit_of_row.push_back(NO_UNIT);
+        S.is_root.push_back(1);
+        S.row_cb.push_back(0);
+    }
+    if (!T.new_keys.empty()) S.key_index.reset();
+    S.dirty.clear();
+    S.needs_cb.clear();
+    for (uint32_t r : T.order) {
+        std::vector<uint32_t>& e = T.rows[r];
+        bool seq = false;
+        for (uint32_t v : e)
+            if (S.coll.count(v)) { seq = true; break; }
+        RowRec rec{0, (uint32_t)((seq ? ROW_SEQ : 0u) << 8), 0, 0};
+        if (seq) {
+            rec.n_sets = (uint32_t)e.size();
+        } else {
+            uint32_t ns = 0;
+            while (ns < e.size() && (e[ns] & EDGE_SET)) ++ns;
+            rec.n_sets = ns;
+            rec.n_ids = (uint32_t)(e.size() - ns);
+        }
+        if (S.row_flags(r) & ROW_SEQ) S.n_seq_rows -= 1;
+        if (seq) S.n_seq_rows += 1;
+        // the place its content had before this write (base rows: their build layout)
+        if (S.dev && !S.row_place.count(r) && r < R0 && S.unit_of_row[r] != NO_UNIT) {
+            const auto old = S.row_edges(r);
+            S.row_place[r] = Snapshot::RowPlace{S.unit_of_row[r], S.row_hlog2(r), (old.second + 3) & ~3ull,
+                                                S.row_cb[r] != 0};
+        }
+        S.rows[r] = rec;
+        S.n_tuples += e.size();
+        S.n_tuples -= r < R0 ? S.row_edges(r).second : 0;
+        S.row_over[r] = std::move(e);
+        S.dirty.push_back(r);
+    }
+    for (uint32_t i = 0; i < T.new_keys.size(); ++i) {            // new rows only subject sets point at
+        const uint32_t r = R0 + i;
+        if (S.row_over.count(r)) continue;
+        S.row_over[r] = {};
+        S.dirty.push_back(r);
+    }
+    for (uint32_t x : T.new_targets)
+        if (S.is_root[x]) {
+            S.is_root[x] = 0;
+            if (!S.row_cb[x]) S.needs_cb.push_back(x);
+        }
+    std::sort(S.needs_cb.begin(), S.needs_cb.end());
+    S.needs_cb.erase(std::unique(S.needs_cb.begin(), S.needs_cb.end()), S.needs_cb.end());
+    S.version += 1;
+    if (!S.dev) compute_layout(S);            // host-only: a later upload lays everything out afresh
+}
+
+}  // namespace keto

@@ -101,7 +101,11 @@ __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint3
         rv.a = s.arena;
         w = (uint64_t)h * HDR_WORDS;
     }
-    const uint4 v = *reinterpret_cast<const uint4*>(rv.a + w);
+    uint4 v = *reinterpret_cast<const uint4*>(rv.a + w);
+    while (v.z & HDR_FWD) {                        // a row a write moved (delta.cpp): its current place
+        w = (uint64_t)v.x * HDR_WORDS;
+        v = *reinterpret_cast<const uint4*>(rv.a + w);
+    }
     rv.beg = w + HDR_WORDS;
     rv.n_sets = v.x;
     rv.n_ids = v.y;
@@ -169,50 +173,6 @@ struct Work<true> {
     }
     __device__ inline void pruned() { ++c[15]; }
 };
-// Can subject id t be reached from the row at all (closure filter; rv.closure only)?
-__device__ inline bool closure_has(const RowView& rv, uint32_t t) {
-    uint32_t wd, bit;
-    closure_bit(t, wd, bit);
-    return (rv.a[rv.beg - HDR_WORDS - CB_WORDS + wd] >> bit) & 1u;
-}
-
-// Is subject id t in the row's (effective) id region?
-template <class W>
-__device__ inline bool row_has_id(const RowView& rv, uint32_t t, W& w) {
-    if (rv.n_ids == 0) return false;
-    const uint32_t* __restrict__ e = rv.a;
-    if (rv.hlog2) {
-        // bucketed table in front of the header (and its closure filter)
-        const uint32_t nb = (1u << rv.hlog2) / BUCKET_WORDS;
-        const uint64_t tb = rv.beg - HDR_WORDS - (rv.closure ? CB_WORDS : 0u) - (1ull << rv.hlog2);
-        for (uint32_t b = mix32(t) & (nb - 1);; b = (b + 1) & (nb - 1)) {
-            const uint4 v = *reinterpret_cast<const uint4*>(e + tb + (uint64_t)b * BUCKET_WORDS);
-            w.idread(BUCKET_WORDS);
-            w.id_at(e + tb + (uint64_t)b * BUCKET_WORDS, true);
-            if (v.x == t || v.y == t || v.z == t || v.w == t) return true;
-            if (v.x == NONE32 || v.y == NONE32 || v.z == NONE32 || v.w == NONE32) return false;
-        }
-    }
-    // lower_bound over the byte-ordered id region; invariant: answer in [lo, hi] (hi included)
-    const uint64_t b = rv.beg + rv.n_sets;
-    const uint32_t n = rv.n_ids;
-    uint32_t lo = 0, hi = n;
-    while (hi - lo > 8) {
-        uint32_t m = (lo + hi) >> 1;
-        w.idread(1);
-        w.id_at(e + b + m, false);
-        if (e[b + m] < t) lo = m + 1; else hi = m;
-    }
-    const uint32_t end = hi < n ? hi + 1 : n;
-    for (uint32_t i = lo; i < end; ++i) {
-        uint32_t v = e[b + i];
-        w.idread(1);
-        w.id_at(e + b + i, false);
-        if (v >= t) return v == t;
-    }
-    return false;
-}
-
 // ------------------------------------------------------------------ visited maps
 struct Visited {
     uint64_t* tab;
@@ -725,11 +685,21 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             }
         }
         if (enter != NONE32) {
+            // a forward at the row's identity (delta.cpp): prune with the identity's filter below, then
+            // read the row where it lives now
+            const bool pruned_cb = (h0.z & HDR_CLOSURE) != 0;
+            uint32_t at = enter;
+            while (h0.z & HDR_FWD) {
+                at = h0.x;
+                h0 = *reinterpret_cast<const uint4*>(ea + (uint64_t)at * HDR_WORDS);
+                h1 = *reinterpret_cast<const uint4*>(ea + (uint64_t)at * HDR_WORDS + HDR_WORDS);
+            }
             const uint32_t n_sets = h0.x, n_ids = h0.y;
             const bool seq = (h0.z & HDR_SEQ) != 0;
             const uint32_t hl = (h0.z >> 8) & 31u;
-            const bool cb = (h0.z & HDR_CLOSURE) != 0;
-            const uint64_t beg = (enter >= ov.base ? (uint64_t)(enter - ov.base) : (uint64_t)enter) * HDR_WORDS + HDR_WORDS;
+            const bool cb = pruned_cb;
+            const bool tcb = (h0.z & HDR_CLOSURE) != 0;       // the id table sits below a filter
+            const uint64_t beg = (at >= ov.base ? (uint64_t)(at - ov.base) : (uint64_t)at) * HDR_WORDS + HDR_WORDS;
             w.row();
             w.header(ea + beg - HDR_WORDS);
             if (cb && !tset && !(enter_fl & FR_TOP) && !((cbw >> (cwb & 31u)) & 1u)) {
@@ -747,7 +717,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
                     bloom_bits(T, b1, b2);
                     if (bloom_has(h0.z, h0.w, b1) && bloom_has(h0.z, h0.w, b2)) {
                         const uint32_t nb = (1u << hl) / BUCKET_WORDS;
-                        const uint64_t tb = beg - HDR_WORDS - (cb ? CB_WORDS : 0u) - (1ull << hl);
+                        const uint64_t tb = beg - HDR_WORDS - (tcb ? CB_WORDS : 0u) - (1ull << hl);
                         for (uint32_t b = mix32(T) & (nb - 1);; b = (b + 1) & (nb - 1)) {
                             const uint4 v = *reinterpret_cast<const uint4*>(ea + tb + (uint64_t)b * BUCKET_WORDS);
                             w.idread(BUCKET_WORDS);
@@ -1057,6 +1027,10 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             w.row();
             w.pruned();
             c = bf_set(c, C_PH, 3, P_WALK);
+        } else if (ph == P_HDR && (v0.z & HDR_FWD)) {
+            // the row's identity header forwards to where a write moved the row (delta.cpp): load
+            // it there next iteration (the prune above used the identity's filter)
+            eh = v0.x;
         } else if (ph == P_HDR) {
             // entering a row (engine.go:82-114): save the parent if it still has edges
             w.row();
@@ -1357,6 +1331,7 @@ struct Tier {
 struct DeviceState {
     int device = 0;
     uint32_t* arena = nullptr;
+    uint64_t arena_words = 0;     // allocated (the tail beyond S.n_units holds rows writes move)
     uint64_t* coll = nullptr;
     uint32_t coll_mask = 0;
     uint64_t bytes = 0;
@@ -1576,11 +1551,16 @@ __global__ void __launch_bounds__(256) closure_pass(uint32_t* __restrict__ arena
     uint4 acc[CB_WORDS / 4];
 #pragma unroll
     for (int k = 0; k < (int)(CB_WORDS / 4); ++k) acc[k] = cf[k];
-    const uint4 v = *reinterpret_cast<const uint4*>(arena + h);
+    uint4 v = *reinterpret_cast<const uint4*>(arena + h);
+    uint64_t hc = h;                                   // where the row's edges are (forwards: delta.cpp)
+    while (v.z & HDR_FWD) {
+        hc = (uint64_t)v.x * HDR_WORDS;
+        v = *reinterpret_cast<const uint4*>(arena + hc);
+    }
     const uint32_t n_sets = v.x;
     uint32_t more = 0;
     for (uint32_t e = 0; e < n_sets; ++e) {
-        const uint32_t x = arena[h + HDR_WORDS + e];
+        const uint32_t x = arena[hc + HDR_WORDS + e];
         if (!(x & EDGE_SET)) continue;
         const uint64_t ch = (uint64_t)(x & EDGE_VAL) * HDR_WORDS;
         const uint32_t cz = arena[ch + 2];
@@ -1626,13 +1606,12 @@ __global__ void __launch_bounds__(256) closure_fill(uint32_t* __restrict__ arena
 // a filter and subject sets, until a round changes nothing.  A graph that has not converged after
 // CLOSURE_MAX_ROUNDS rounds gets full filters (no pruning) instead.
 constexpr int CLOSURE_MAX_ROUNDS = 2048;
-void build_closures(const Snapshot& S, uint32_t* d_arena, const std::vector<uint32_t>& host_arena) {
+void build_closures(const Snapshot& S, uint32_t* d_arena) {
     std::vector<uint32_t> list, all;
     for (uint32_t r = 0; r < S.n_rows(); ++r) {
-        if (S.is_root[r] || !S.present(r)) continue;
+        if (!S.row_cb[r] || !S.present(r)) continue;
         all.push_back(S.unit_of_row[r]);
-        const uint64_t h = (uint64_t)S.unit_of_row[r] * HDR_WORDS;
-        if (host_arena[h] > 0 && !(host_arena[h + 2] & HDR_SEQ)) list.push_back(S.unit_of_row[r]);
+        if (S.rows[r].n_sets > 0 && !(S.row_flags(r) & ROW_SEQ)) list.push_back(S.unit_of_row[r]);
     }
     if (list.empty()) return;
     uint32_t *d_rows = nullptr, *d_changed = nullptr;
@@ -1676,14 +1655,15 @@ void device_upload(Snapshot& S, int device) {
     const uint32_t R = S.n_rows();
     host_parallel_for(R, [&](uint64_t r) {
         if (!S.present((uint32_t)r)) return;                 // another part's root row
-        const uint64_t b = S.row_begin((uint32_t)r);
-        const uint64_t e = r + 1 < R ? S.row_begin((uint32_t)r + 1) : S.edges.size();
-        put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), S.edges.data() + b,
-                e - b, S.unit_of_row, !S.is_root[r]);
+        const auto ed = S.row_edges((uint32_t)r);
+        put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), ed.first, ed.second,
+                S.unit_of_row, S.row_cb[r] != 0);
     });
-    D->arena = dmalloc<uint32_t>(arena.size(), acc);
+    // room at the tail for rows writes move (keto_snapshot_apply; grown on demand)
+    D->arena_words = std::min<uint64_t>(2ull << 32, arena.size() + std::max<uint64_t>(arena.size() / 16, 1ull << 20));
+    D->arena = dmalloc<uint32_t>(D->arena_words, acc);
     HIP_OK(hipMemcpy(D->arena, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    build_closures(S, D->arena, arena);
+    build_closures(S, D->arena);
     if (!S.coll.empty()) {
         uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
         std::vector<uint64_t> tab(cap, ~0ull);
@@ -1714,6 +1694,195 @@ void device_upload(Snapshot& S, int device) {
     for (auto& e : D->pev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     S.device = device;
     S.dev.reset(D.release());
+}
+
+namespace {
+// A tail place for a row (the same line rules as compute_layout): returns its header unit.
+uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint64_t& total_words) {
+    const uint64_t table = hlog2 ? (1ull << hlog2) : 0;
+    const uint64_t c = cb ? CB_WORDS : 0;
+    const uint64_t slot = c + HDR_WORDS + WINDOW_WORDS;
+    const uint64_t total = table + c + HDR_WORDS + ((n_edges + 3) & ~3ull);
+    const uint64_t fit = std::max(total, table + slot);
+    auto align = [&](uint64_t x) {
+        if (fit <= LINE_WORDS) {
+            if (x % LINE_WORDS + fit > LINE_WORDS) x = (x + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
+        } else {
+            const uint64_t o = (x + table) % LINE_WORDS;
+            if (o + slot > LINE_WORDS) x += LINE_WORDS - o;
+        }
+        return x;
+    };
+    uint64_t w = align(S.n_units * HDR_WORDS);
+    if (w < (1ull << 32) && w + fit > (1ull << 32)) w = align(1ull << 32);
+    const uint64_t unit = (w + table + c) / HDR_WORDS;
+    if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
+    S.n_units = (w + total) / HDR_WORDS;
+    total_words = total;
+    return (uint32_t)unit;
+}
+}  // namespace
+
+// Patch the device arena after apply_writes (delta.cpp): every changed row is rewritten where it is
+// if its new content fits there, else placed at the arena's tail with a forward at its identity
+// handle (the handle subject sets hold; its closure filter stays in front of it).  New rows, and
+// root rows that became subject-set targets (a target must have a closure filter in front of its
+// identity header), get a new identity at the tail; an old identity keeps a forward for handles
+// resolved before.  Closure filters are then re-closed on the device from their rows' own ids
+// (filters of other rows only ever lose precision: a deleted id's bit may stay, never a needed one
+// go missing).  Runs under the snapshot's device lock, between batches.
+void device_apply(Snapshot& S) {
+    if (!S.dev) return;
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    struct Write {
+        uint64_t word;                    // first word of the image in the arena
+        std::vector<uint32_t> img;
+    };
+    std::vector<Write> writes;
+    auto image = [&](uint32_t r, uint32_t unit, bool cb) {
+        const auto ed = S.row_edges(r);
+        const uint32_t hl = S.row_hlog2(r);
+        const uint64_t table = hl ? (1ull << hl) : 0, c = cb ? CB_WORDS : 0;
+        Write w;
+        w.word = (uint64_t)unit * HDR_WORDS - table - c;
+        w.img.assign(table + c + HDR_WORDS + ((ed.second + 3) & ~3ull), 0);
+        // put_row writes relative to the header: lay it out in a scratch arena starting at word 0
+        const uint32_t u0 = (uint32_t)((table + c + HDR_WORDS - 1) / HDR_WORDS);
+        std::vector<uint32_t> scratch((uint64_t)u0 * HDR_WORDS + HDR_WORDS + ((ed.second + 3) & ~3ull) + 8, 0);
+        put_row(scratch.data(), u0, S.rows[r], S.row_pp[r], hl, ed.first, ed.second, S.unit_of_row, cb);
+        const uint64_t from = (uint64_t)u0 * HDR_WORDS - table - c;
+        std::copy(scratch.begin() + from, scratch.begin() + from + w.img.size(), w.img.begin());
+        writes.push_back(std::move(w));
+    };
+    auto forward = [&](uint32_t at, uint32_t to, bool cb) {
+        Write w;
+        w.word = (uint64_t)at * HDR_WORDS;
+        w.img = {to, 0u, HDR_FWD | (cb ? HDR_CLOSURE : 0u), 0u};
+        writes.push_back(std::move(w));
+    };
+    // 1. new identities first: edges name targets by identity handle
+    std::vector<std::pair<uint32_t, uint32_t>> moved;        // (row, old identity)
+    std::vector<uint32_t> fresh;
+    for (uint32_t r : S.dirty)
+        if (S.unit_of_row[r] == NO_UNIT) fresh.push_back(r);
+    for (uint32_t r : S.needs_cb)
+        if (S.unit_of_row[r] != NO_UNIT && !S.row_cb[r]) {
+            moved.push_back({r, S.unit_of_row[r]});
+            fresh.push_back(r);
+        }
+    for (uint32_t r : fresh) {
+        uint64_t tw = 0;
+        const uint32_t u = tail_place(S, S.row_hlog2(r), true, S.row_edges(r).second, tw);
+        S.unit_of_row[r] = u;
+        S.row_cb[r] = 1;
+        S.is_root[r] = 0;
+        S.row_place[r] = Snapshot::RowPlace{u, S.row_hlog2(r), (S.row_edges(r).second + 3) & ~3ull, true};
+        S.layout_units.push_back(u);
+        S.rows_by_unit.push_back(r);
+    }
+    // 2. every changed row's content
+    std::vector<uint8_t> is_fresh(S.n_rows(), 0);
+    for (uint32_t r : fresh) is_fresh[r] = 1;
+    std::vector<uint32_t> todo(S.dirty);
+    for (auto& m : moved) todo.push_back(m.first);
+    std::sort(todo.begin(), todo.end());
+    todo.erase(std::unique(todo.begin(), todo.end()), todo.end());
+    for (uint32_t r : todo) {
+        const uint32_t id = S.unit_of_row[r];
+        const uint32_t hl = S.row_hlog2(r);
+        const uint64_t cap = (S.row_edges(r).second + 3) & ~3ull;
+        Snapshot::RowPlace& pl = S.row_place[r];
+        if (is_fresh[r]) {
+            image(r, id, true);
+        } else if (pl.hlog2 == hl && pl.edge_cap >= cap) {
+            image(r, pl.unit, pl.cb);                         // fits where it is
+            if (pl.unit != id && S.row_cb[r]) {               // a forwarded row: re-seed the identity filter
+                Write w;
+                w.word = (uint64_t)id * HDR_WORDS - CB_WORDS;
+                w.img.assign(CB_WORDS, 0);
+                const auto ed = S.row_edges(r);
+                const bool seq = (S.row_flags(r) & ROW_SEQ) != 0;
+                for (auto& x : w.img) x = seq ? NONE32 : 0u;
+                if (!seq)
+                    for (uint64_t i = 0; i < ed.second; ++i)
+                        if (!(ed.first[i] & EDGE_SET)) {
+                            uint32_t wd, bit;
+                            closure_bit(ed.first[i], wd, bit);
+                            w.img[wd] |= 1u << bit;
+                        }
+                writes.push_back(std::move(w));
+            }
+        } else {
+            uint64_t tw = 0;
+            const uint32_t u = tail_place(S, hl, false, S.row_edges(r).second, tw);
+            pl = Snapshot::RowPlace{u, hl, cap, false};
+            image(r, u, false);
+            forward(id, u, S.row_cb[r] != 0);
+            if (S.row_cb[r]) {                                // the identity's filter, re-seeded
+                Write w;
+                w.word = (uint64_t)id * HDR_WORDS - CB_WORDS;
+                w.img.assign(CB_WORDS, 0);
+                const auto ed = S.row_edges(r);
+                const bool seq = (S.row_flags(r) & ROW_SEQ) != 0;
+                for (auto& x : w.img) x = seq ? NONE32 : 0u;
+                if (!seq)
+                    for (uint64_t i = 0; i < ed.second; ++i)
+                        if (!(ed.first[i] & EDGE_SET)) {
+                            uint32_t wd, bit;
+                            closure_bit(ed.first[i], wd, bit);
+                            w.img[wd] |= 1u << bit;
+                        }
+                writes.push_back(std::move(w));
+            }
+        }
+    }
+    for (auto& m : moved) forward(m.second, S.unit_of_row[m.first], false);   // stale top-level handles
+    // 3. room: grow the arena if the tail outgrew it (handles are word offsets: copied as is)
+    const uint64_t need = S.n_units * HDR_WORDS;
+    if (need > (2ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^33 words (32 GiB)"};
+    if (need > D.arena_words) {
+        const uint64_t cap = std::min<uint64_t>(2ull << 32, std::max<uint64_t>(need, D.arena_words + D.arena_words / 4));
+        uint64_t acc = 0;
+        uint32_t* na = dmalloc<uint32_t>(cap, acc);
+        HIP_OK(hipMemcpy(na, D.arena, D.arena_words * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+        (void)hipFree(D.arena);
+        D.bytes += (cap - D.arena_words) * sizeof(uint32_t);
+        D.arena = na;
+        D.arena_words = cap;
+    }
+    for (const Write& w : writes)
+        HIP_OK(hipMemcpyAsync(D.arena + w.word, w.img.data(), w.img.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              D.stream));
+    HIP_OK(hipStreamSynchronize(D.stream));
+    // 4. closure filters of every row with one (from their own ids up)
+    build_closures(S, D.arena);
+    // 5. what the kernels and expand output read next
+    D.n_units = (uint32_t)S.n_units;
+    D.vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
+    if (!moved.empty()) {
+        // old identities are no longer row handles of expand output
+        std::vector<uint32_t> lu, rbu;
+        std::vector<uint8_t> gone(S.n_rows(), 0);
+        std::unordered_map<uint32_t, uint32_t> old_of;
+        for (auto& m : moved) old_of[m.second] = m.first;
+        for (size_t i = 0; i < S.layout_units.size(); ++i) {
+            auto it = old_of.find(S.layout_units[i]);
+            if (it != old_of.end() && S.rows_by_unit[i] == it->second) continue;
+            lu.push_back(S.layout_units[i]);
+            rbu.push_back(S.rows_by_unit[i]);
+        }
+        S.layout_units.swap(lu);
+        S.rows_by_unit.swap(rbu);
+    }
+    for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit})
+        if (*p) {
+            (void)hipFree(*p);
+            *p = nullptr;
+        }
+    S.dirty.clear();
+    S.needs_cb.clear();
 }
 
 void device_release(Snapshot& S) {

@@ -256,10 +256,49 @@ void finalize_rows(Snapshot& S, const std::vector<uint64_t>& row_ptr, const std:
 }  // namespace
 
 int64_t Snapshot::lookup_str(std::string_view s) const {
-    auto it = std::lower_bound(strs.begin(), strs.end(), s,
+    const auto end = strs.begin() + n_sorted_strs;
+    auto it = std::lower_bound(strs.begin(), end, s,
                                [](const std::string& a, std::string_view b) { return std::string_view(a) < b; });
-    if (it == strs.end() || std::string_view(*it) != s) return -1;
-    return it - strs.begin();
+    if (it != end && std::string_view(*it) == s) return it - strs.begin();
+    if (added_str.empty()) return -1;
+    auto f = added_str.find(std::string(s));
+    return f == added_str.end() ? -1 : (int64_t)f->second;
+}
+
+int Snapshot::key_cmp_bytes(const RowKey& a, const RowKey& b) const {
+    if (a.ns != b.ns) return a.ns < b.ns ? -1 : 1;
+    if (a.obj != b.obj) return str_cmp(a.obj, b.obj);
+    if (a.rel != b.rel) return str_cmp(a.rel, b.rel);
+    return 0;
+}
+
+std::vector<uint32_t> Snapshot::rows_in_key_order(const RowKey& k) const {
+    auto match = [&](const RowKey& rk) {
+        return (k.ns == ANY_NS || rk.ns == k.ns) && (k.obj == ANY || rk.obj == k.obj) && (k.rel == ANY || rk.rel == k.rel);
+    };
+    std::vector<uint32_t> out, extra;
+    for (uint32_t q = 0; q < n_real_rows; ++q)
+        if (match(row_key[q])) out.push_back(q);
+    // rows outside the build's sorted range that hold tuples now (written by keto_snapshot_apply)
+    for (uint32_t q = n_real_rows; q < n_rows(); ++q) {
+        const RowKey& rk = row_key[q];
+        if (rk.ns == ANY_NS || rk.obj == ANY || rk.rel == ANY || !row_over.count(q)) continue;
+        if (row_over.at(q).empty() || !match(rk)) continue;
+        extra.push_back(q);
+    }
+    if (extra.empty()) return out;
+    auto less = [&](uint32_t a, uint32_t b) { return key_cmp_bytes(row_key[a], row_key[b]) < 0; };
+    std::sort(extra.begin(), extra.end(), less);
+    std::vector<uint32_t> all(out.size() + extra.size());
+    std::merge(out.begin(), out.end(), extra.begin(), extra.end(), all.begin(), less);
+    return all;
+}
+
+int Snapshot::str_cmp(uint32_t a, uint32_t b) const {
+    if (a == b) return 0;
+    if (a < n_sorted_strs && b < n_sorted_strs) return a < b ? -1 : 1;
+    const int c = strs[a].compare(strs[b]);
+    return c < 0 ? -1 : c > 0 ? 1 : 0;
 }
 
 int64_t Snapshot::resolve_query(std::string_view ns, std::string_view obj, std::string_view rel,
@@ -321,15 +360,11 @@ uint32_t overlay_row(const Snapshot& S, Overlay& ov, const RowKey& k) {
     uint32_t id = ov.base + (uint32_t)ov.rows.size();
     uint64_t b = ov.edges.size(), pos = 0;
     uint32_t pp = NO_PAGE;
-    for (uint32_t q = 0; q < S.n_real_rows; ++q) {          // matching real rows in ORDER BY order
-        const RowKey& rk = S.row_key[q];
-        if ((k.ns != ANY_NS && rk.ns != k.ns) || (k.obj != ANY && rk.obj != k.obj) || (k.rel != ANY && rk.rel != k.rel))
-            continue;
-        uint64_t rb = S.row_begin(q);
-        uint64_t re = q + 1 < S.rows.size() ? S.row_begin(q + 1) : S.edges.size();
-        for (uint64_t i = rb; i < re; ++i, ++pos) {
-            if (S.edges[i] == EDGE_POISON && pp == NO_PAGE) pp = (uint32_t)(pos / S.page_size);
-            ov.edges.push_back(S.edges[i]);
+    for (uint32_t q : S.rows_in_key_order(k)) {              // matching real rows in ORDER BY order
+        const auto e = S.row_edges(q);
+        for (uint64_t i = 0; i < e.second; ++i, ++pos) {
+            if (e.first[i] == EDGE_POISON && pp == NO_PAGE) pp = (uint32_t)(pos / S.page_size);
+            ov.edges.push_back(e.first[i]);
         }
     }
     uint64_t n = ov.edges.size() - b;
@@ -350,9 +385,7 @@ uint32_t overlay_row(const Snapshot& S, Overlay& ov, const RowKey& k) {
 }
 
 namespace {
-uint64_t row_end_of(const Snapshot& S, uint32_t r) {
-    return r + 1 < S.rows.size() ? S.row_begin(r + 1) : S.edges.size();
-}
+uint64_t row_size(const Snapshot& S, uint32_t r) { return S.row_edges(r).second; }
 uint32_t ceil_log2(uint64_t x) {
     uint32_t k = 0;
     while ((1ull << k) < x) ++k;
@@ -376,8 +409,13 @@ void compute_layout(Snapshot& S) {
     std::vector<uint8_t> band(R, 0);
     {
         std::vector<uint32_t> indeg(R, 0);
-        for (uint32_t e : S.edges)
-            if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
+        for (uint32_t r = 0; r < R; ++r) {
+            const auto ed = S.row_edges(r);
+            for (uint64_t i = 0; i < ed.second; ++i) {
+                const uint32_t e = ed.first[i];
+                if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
+            }
+        }
         S.is_root.assign(R, 0);
         for (uint32_t r = 0; r < R; ++r) {
             band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
@@ -402,6 +440,7 @@ void compute_layout(Snapshot& S) {
         if (keep[r]) S.rows_by_unit[start[33 - band[r]]++] = r;
     }
     S.layout_units.assign(kept, 0);
+    S.shared_words = 0;
     // test hook: start the layout this many words into the arena, so a small graph straddles the
     // segment boundary at 2^32 words (tests/test_gpu_synth.py)
     uint64_t w = 0;
@@ -410,7 +449,7 @@ void compute_layout(Snapshot& S) {
         const uint32_t r = S.rows_by_unit[x];
         const uint32_t h = S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
-        const uint64_t n = row_end_of(S, r) - S.row_begin(r);
+        const uint64_t n = row_size(S, r);
         // line placement: a row that fits in a 128-B line never straddles one (closure filter,
         // header, window and id table come in with one miss); a bigger row keeps closure filter +
         // header + window in one line
@@ -433,9 +472,13 @@ void compute_layout(Snapshot& S) {
         if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
         S.unit_of_row[r] = (uint32_t)unit;
         S.layout_units[x] = (uint32_t)unit;
+        if (!S.is_root[r]) S.shared_words += total;
         w += total;
     }
     S.n_units = w / HDR_WORDS;
+    S.row_cb.assign(R, 0);
+    for (uint32_t r = 0; r < R; ++r) S.row_cb[r] = !S.is_root[r];
+    S.row_place.clear();
 }
 
 uint32_t Snapshot::root_owner(uint32_t r, uint32_t parts) const {
@@ -504,6 +547,7 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
         ParInterner in;
         in.run(tup, n, extra, threads);
         S.strs.resize(in.uniq.size());
+        S.n_sorted_strs = (uint32_t)in.uniq.size();
         par_chunks(in.uniq.size(), threads, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
             for (uint64_t i = b; i < e; ++i) S.strs[i] = std::string(in.uniq[i]);
         });
@@ -707,6 +751,7 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
     }
 
     clk.lap("collision classes");
+    S.n_base_rows = R;
     finalize_rows(S, row_ptr, is_wild);
     compute_layout(S);
     clk.lap("rows + layout");
@@ -728,6 +773,7 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
     if (strings) {
         S.strs.resize(n_strings);
         for (uint32_t i = 0; i < n_strings; ++i) S.strs[i] = std::string(sv(strings[i]));
+        S.n_sorted_strs = n_strings;
         int64_t e = S.lookup_str("");
         S.empty_str = e < 0 ? ANY : (uint32_t)e;
     }
@@ -744,6 +790,7 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
     S.row_pp.assign(n_rows, NO_PAGE);
     std::vector<uint64_t> rp(row_ptr, row_ptr + n_rows + 1);
     std::vector<uint8_t> is_wild(n_rows, 0);
+    S.n_base_rows = n_rows;
     finalize_rows(S, rp, is_wild);
     compute_layout(S);
     return Sp;

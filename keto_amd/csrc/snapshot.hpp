@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -67,6 +68,10 @@ constexpr uint32_t HDR_SEQ = 1u;                // walked edge by edge (ROW_SEQ)
 constexpr uint32_t HDR_POISON = 2u;             // some page fails toInternal (expand: error)
 constexpr uint32_t HDR_POISON0 = 4u;            // the first page fails (check: empty row)
 constexpr uint32_t HDR_CLOSURE = 8u;            // a closure filter precedes the header
+// A row rewritten by a write that no longer fits its place (delta.cpp / device_apply) lives at the
+// arena's tail; its identity header (whose handle every subject set holds, and whose closure filter
+// stays in front of it) becomes a forward: word 0 = handle of the row's current header.
+constexpr uint32_t HDR_FWD = 16u;
 // Closure filter of a row some subject set points at: a 768-bit, one-hash bloom filter of every
 // subject id reachable from the row through any number of subject sets (its own ids included).  A
 // check entering such a row for a requested id the filter rules out skips the row: every node the
@@ -168,9 +173,40 @@ struct Snapshot {
     uint32_t root_owner(uint32_t r, uint32_t parts) const;   // part owning root row r
     bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT; }
     uint64_t n_units = 0;
+    uint64_t shared_words = 0;            // arena words of the rows every part keeps (non-root rows)
     uint32_t handle(uint32_t row) const { return unit_of_row[row]; }
     int64_t row_of_handle(uint32_t unit) const;   // -1 if not a row header
     uint32_t row_hlog2(uint32_t r) const;         // 0 = no id table
+
+    // ---- lifecycle (delta.cpp): writes applied since the build
+    std::shared_mutex rw;                      // calls read the host tables shared; keto_snapshot_apply exclusive
+    uint64_t version = 0;                      // bumped by every keto_snapshot_apply
+    uint32_t n_sorted_strs = 0;                // strs[0, n) are in byte order (id = rank); later ones were added
+    std::unordered_map<std::string, uint32_t> added_str;
+    uint32_t n_base_rows = 0;                  // rows of the build; rows >= n_base_rows were added by writes
+    std::unordered_map<uint32_t, std::vector<uint32_t>> row_over;   // current edges of rows changed by writes
+    std::vector<uint8_t> row_cb;               // the row's identity handle has a closure filter in front of it
+    struct RowPlace {                          // where a changed row's content is (device arenas)
+        uint32_t unit;                         // its header (== identity handle unless forwarded)
+        uint32_t hlog2;
+        uint64_t edge_cap;                     // edge words the place holds
+        bool cb;                               // a closure filter precedes that header
+    };
+    std::unordered_map<uint32_t, RowPlace> row_place;
+    std::vector<uint32_t> dirty;               // rows the last apply changed (device_apply's work list)
+    std::vector<uint32_t> needs_cb;            // of them: rows that became subject-set targets without a filter
+    // edges of row r in ORDER BY order (row-id encoded), whether or not a write changed it
+    std::pair<const uint32_t*, uint64_t> row_edges(uint32_t r) const {
+        auto it = row_over.find(r);
+        if (it != row_over.end()) return {it->second.data(), it->second.size()};
+        if (r >= n_base_rows) return {nullptr, 0};
+        const uint64_t b = row_begin(r), e = r + 1 < n_base_rows ? row_begin(r + 1) : edges.size();
+        return {edges.data() + b, e - b};
+    }
+    int str_cmp(uint32_t a, uint32_t b) const;    // byte order of two string ids
+    int key_cmp_bytes(const RowKey& a, const RowKey& b) const;   // (namespace id, object bytes, relation bytes)
+    // rows a (wildcard) RelationQuery k returns, in the reference ORDER BY (relationtuples.go:250)
+    std::vector<uint32_t> rows_in_key_order(const RowKey& k) const;
 
     // ---- device
     int device = -1;
@@ -236,6 +272,11 @@ uint32_t overlay_row(const Snapshot& s, Overlay& ov, const RowKey& k);
 uint32_t handle_of(const Snapshot& s, const Overlay* ov, uint32_t row);
 // arena layout of every row (called by the builders)
 void compute_layout(Snapshot& s);
+// snapshot lifecycle (delta.cpp): apply an insert / delete transaction to the host tables
+// (TransactRelationTuples, internal/persistence/sql/relationtuples.go:289-297); throws KETO_E_REBUILD
+// for writes outside the delta path; device_apply then patches the device arena
+void apply_writes(Snapshot& s, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del);
+void device_apply(Snapshot& s);
 
 // device engine (engine.hip)
 void device_upload(Snapshot& s, int device);

@@ -140,6 +140,8 @@ CREATE TABLE keto_relation_tuples
          (subject_id IS NOT NULL AND
           subject_set_namespace_id IS NULL AND subject_set_object IS NULL AND subject_set_relation IS NULL))
 );
+"""
+_INDEX = """
 CREATE INDEX keto_relation_tuples_full_idx ON keto_relation_tuples
     (nid, namespace_id, object, relation, subject_id, subject_set_namespace_id, subject_set_object,
      subject_set_relation, commit_time);
@@ -178,11 +180,14 @@ class SQLStore:
     """
 
     def __init__(self, namespaces: Sequence[Tuple[int, str]], tuples: Sequence[RelationTuple] = (),
-                 page_size: int = DEFAULT_PAGE_SIZE, raw_rows: Sequence[tuple] = ()):
+                 page_size: int = DEFAULT_PAGE_SIZE, raw_rows: Sequence[tuple] = (), bulk_rows=None):
         self.nm = Namespaces(namespaces)
         self.page_size = page_size
         self.conn = sqlite3.connect(":memory:")
         self.conn.executescript(_SCHEMA)
+        if bulk_rows is not None:       # full keto_relation_tuples rows, indexed after the insert (bench)
+            self.conn.executemany("INSERT INTO keto_relation_tuples VALUES (?,?,?,?,?,?,?,?,?,?)", bulk_rows)
+        self.conn.executescript(_INDEX)
         self._seq = 0
         self.requested_pages: List[int] = []  # ManagerWrapper.RequestedPages analogue
         for t in tuples:
@@ -204,6 +209,36 @@ class SQLStore:
         self.conn.execute(
             "INSERT INTO keto_relation_tuples VALUES (?,?,?,?,?,?,?,?,?,?)",
             (f"shard-{self._seq}", _NID, ns_id, obj, rel, sid, sns, sobj, srel, self._seq))
+
+    def delete(self, t: RelationTuple):
+        """DeleteRelationTuples for one tuple (relationtuples.go:200-223, whereSubject :151-176):
+        every row with its namespace, object, relation and exact subject."""
+        ns_id, _ = self.nm.by_name(t.namespace)
+        if isinstance(t.subject, SubjectID):
+            self.conn.execute("DELETE FROM keto_relation_tuples WHERE nid = ? AND namespace_id = ? AND object = ? AND "
+                              "relation = ? AND subject_id = ? AND subject_set_namespace_id IS NULL AND "
+                              "subject_set_object IS NULL AND subject_set_relation IS NULL",
+                              (_NID, ns_id, t.object, t.relation, t.subject.id))
+        else:
+            sns, _ = self.nm.by_name(t.subject.namespace)
+            self.conn.execute("DELETE FROM keto_relation_tuples WHERE nid = ? AND namespace_id = ? AND object = ? AND "
+                              "relation = ? AND subject_id IS NULL AND subject_set_namespace_id = ? AND "
+                              "subject_set_object = ? AND subject_set_relation = ?",
+                              (_NID, ns_id, t.object, t.relation, sns, t.subject.object, t.subject.relation))
+
+    def tuples(self):
+        """Every row in commit order, as RelationTuples (rows with unknown namespaces skipped)."""
+        out = []
+        for ns_id, obj, rel, sid, sns, sobj, srel in self.conn.execute(
+                "SELECT namespace_id, object, relation, subject_id, subject_set_namespace_id, subject_set_object, "
+                "subject_set_relation FROM keto_relation_tuples ORDER BY commit_time"):
+            _, nm = self.nm.by_id(ns_id)
+            if sid is not None:
+                out.append(RelationTuple(nm, obj, rel, SubjectID(sid)))
+            else:
+                _, snm = self.nm.by_id(sns)
+                out.append(RelationTuple(nm, obj, rel, SubjectSet(snm, sobj, srel)))
+        return out
 
     def _to_internal(self, row) -> RelationTuple:  # relationtuples.go:43-80
         ns_id, obj, rel, sid, sns, sobj, srel = row

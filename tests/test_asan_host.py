@@ -17,7 +17,7 @@ def test_host_library_under_asan(tmp_path):
     csrc = os.path.join(ROOT, "keto_amd", "csrc")
     san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     objs = []
-    for f in ("snapshot.cpp", "capi.cpp"):
+    for f in ("snapshot.cpp", "delta.cpp", "capi.cpp"):
         o = str(tmp_path / (f + ".o"))
         subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *san, "-c", os.path.join(csrc, f), "-o", o])
         objs.append(o)

@@ -1,0 +1,124 @@
+"""Snapshot lifecycle on the GPU (keto_snapshot_apply): write transactions interleaved with check
+and expand batches, every decision and tree compared with the SQL oracle after each write
+(oracle_sql.SQLStore insert / delete = InsertRelationTuple / DeleteRelationTuples,
+internal/persistence/sql/relationtuples.go:128-149,200-223).
+
+The writes exercise the delta path: rows rewritten in place, rows that outgrow their place (a
+forward at the identity handle), rows that get an id table, root rows that become subject-set
+targets (a new identity with a closure filter), new rows, new strings that sort between the build's,
+duplicate inserts and deletes of every equal tuple.  Writes the delta path refuses (KETO_E_REBUILD)
+leave the snapshot unchanged and are followed by a rebuild, as a caller would do."""
+import random
+
+import pytest
+
+from oracle.oracle_sql import (CheckEngine, ExpandEngine, NotFoundError, RelationTuple, SQLStore, SubjectID,
+                               SubjectSet)
+from tests.engine_util import rows_from_tuples, subj
+from tests.randgraph import random_checks, random_expands, random_graph
+
+pytestmark = pytest.mark.gpu
+
+
+def _row(ns_ids, t):
+    return rows_from_tuples(ns_ids, [t])[0]
+
+
+def _random_write(rng, names, objs, rels, users):
+    o = rng.choice(objs + [f"new{rng.randrange(40)}", "a0", "Z", "b#c"])
+    r = rng.choice(rels + ["q"])
+    if rng.random() < 0.55:
+        sub = SubjectID(rng.choice(users + [f"w{rng.randrange(200):03d}", "a", "zz"]))
+    else:
+        sub = SubjectSet(rng.choice(names), rng.choice(objs + [f"new{rng.randrange(40)}"]), rng.choice(rels + ["q"]))
+    return RelationTuple(rng.choice(names), o, r, sub)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_writes_interleaved_with_checks(seed):
+    import keto_amd
+    wide = seed % 4 == 3
+    ns, tuples, raw, ps, alph = random_graph(seed + 500, wide=wide, allow_wildcards=seed % 5 == 0,
+                                             allow_poison=False, allow_collisions=seed % 3 == 0)
+    names, objs, rels, users = alph
+    names = [n for n in names if n]                   # a namespace named "" makes wildcard subject sets
+    if not names:
+        pytest.skip("only a namespace named ''")
+    store = SQLStore(ns, tuples, page_size=ps)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), page_size=ps, device=0)
+    rng = random.Random(seed)
+    applied = rebuilt = 0
+    for step in range(10):
+        cur = store.tuples()
+        ins = [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(1, 30 if wide else 8))]
+        dels = [rng.choice(cur) for _ in range(rng.randint(0, 4))] if cur else []
+        dels += [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(0, 2))]
+        v0 = snap.version()
+        try:
+            v = snap.apply([_row(ns, t) for t in ins], [_row(ns, t) for t in dels])
+            assert v == v0 + 1
+            applied += 1
+        except keto_amd.KetoError as e:
+            assert "-6" in str(e), e                   # KETO_E_REBUILD only
+            assert snap.version() == v0
+            rebuilt += 1
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+        if snap.version() == v0:                       # refused: rebuild from the table
+            snap.close()
+            snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, store.tuples()), page_size=ps, device=0)
+        checks = random_checks(seed * 31 + step, (names, objs + ["new1", "new7", "a0"], rels + ["q"],
+                                                  users + ["w001", "a"]), k=40)
+        for g in sorted({c[2] for c in checks}):
+            grp = [c for c in checks if c[2] == g]
+            allowed, _ = snap.check_batch([(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in grp], g)
+            for (t, d, _), a in zip(grp, allowed):
+                assert bool(a) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, step, t, d, g)
+        exps = random_expands(seed * 17 + step, (names, objs + ["new3"], rels + ["q"], users), k=10)
+        for g in sorted({e[2] for e in exps}):
+            grp = [e for e in exps if e[2] == g]
+            got = snap.expand_batch([(subj(s), d) for s, d, _ in grp], g)
+            for (s, d, _), (st, js) in zip(grp, got):
+                try:
+                    tr = ExpandEngine(store, g).build_tree(s, d)
+                    want = ("tree", tr.to_json()) if tr is not None else ("nil", None)
+                except NotFoundError:
+                    want = ("error", None)
+                have = {0: "tree", 1: "nil", 2: "error"}[st]
+                assert (have, js) == want, (seed, step, s, d, g)
+    assert applied > 0
+    snap.close()
+
+
+def test_large_row_growth_and_new_targets():
+    """One hub row grown from 2 to 3,000 ids over several writes (in place, then relocated with an
+    id table, then relocated again), a root row turned into a subject-set target (identity move), and
+    checks through both after every write."""
+    import keto_amd
+    ns = [(1, "n")]
+    base = [RelationTuple("n", "doc", "view", SubjectSet("n", "hub", "member")),
+            RelationTuple("n", "hub", "member", SubjectID("u0001")),
+            RelationTuple("n", "hub", "member", SubjectID("u0002")),
+            RelationTuple("n", "root", "view", SubjectID("r1"))]
+    store = SQLStore(ns, base)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, base), device=0)
+    rng = random.Random(1)
+    for step, k in enumerate((1, 5, 40, 400, 2600)):
+        ins = [RelationTuple("n", "hub", "member", SubjectID(f"u{rng.randrange(10000):04d}")) for _ in range(k)]
+        if step == 2:
+            ins.append(RelationTuple("n", "hub", "member", SubjectSet("n", "root", "view")))     # root -> target
+        snap.apply([_row(ns, t) for t in ins])
+        for t in ins:
+            store.insert(t)
+        reqs = [("n", "doc", "view", ("id", f"u{i:04d}"), 0) for i in range(0, 10000, 7)]
+        reqs += [("n", "doc", "view", ("id", "r1"), 0), ("n", "doc", "view", ("id", "r1"), 2),
+                 ("n", "root", "view", ("id", "r1"), 0), ("n", "hub", "member", ("id", "r1"), 0)]
+        allowed, _ = snap.check_batch(reqs, 5)
+        eng = CheckEngine(store, 5)
+        for (n_, o, r, u, d), a in zip(reqs, allowed):
+            assert bool(a) == eng.subject_is_allowed(RelationTuple(n_, o, r, SubjectID(u[1])), d), (step, o, u, d)
+        (st, js), = snap.expand_batch([(("set", "n", "doc", "view"), 0)], 5)
+        assert js == ExpandEngine(store, 5).build_tree(SubjectSet("n", "doc", "view"), 0).to_json()
+    assert snap.version() == 5

@@ -222,20 +222,19 @@ class SynthGraph:
         """The oracle table's tuples in an in-memory SQLite store with the reference schema
         (oracle/oracle_sql.py's SQLStore; strings are the ids as 8-digit hex, so byte order = id order)."""
         from oracle.oracle_sql import SQLStore, _NID
-        st = SQLStore(self.namespaces)
         n = tab.t.n
         a = tab.arr
-        hx = lambda v: f"{int(v):08x}"
-        rows = []
-        for i in range(n):
-            if a["kind"][i]:
-                rows.append((f"s{i}", _NID, int(a["ns"][i]), hx(a["obj"][i]), hx(a["rel"][i]), None,
-                             int(a["sns"][i]), hx(a["sobj"][i]), hx(a["srel"][i]), i))
-            else:
-                rows.append((f"s{i}", _NID, int(a["ns"][i]), hx(a["obj"][i]), hx(a["rel"][i]), hx(a["sid"][i]),
-                             None, None, None, i))
-        st.conn.executemany("INSERT INTO keto_relation_tuples VALUES (?,?,?,?,?,?,?,?,?,?)", rows)
-        return st
+        hx = lambda v: f"{v:08x}"
+        ns, obj, rel = a["ns"].tolist(), a["obj"].tolist(), a["rel"].tolist()
+        kind, sid, sns, sobj, srel = (a[k].tolist() for k in ("kind", "sid", "sns", "sobj", "srel"))
+
+        def rows():
+            for i in range(n):
+                if kind[i]:
+                    yield (f"s{i:010d}", _NID, ns[i], hx(obj[i]), hx(rel[i]), None, sns[i], hx(sobj[i]), hx(srel[i]), i)
+                else:
+                    yield (f"s{i:010d}", _NID, ns[i], hx(obj[i]), hx(rel[i]), hx(sid[i]), None, None, None, i)
+        return SQLStore(self.namespaces, bulk_rows=rows())
 
     def sql_requests(self, q: np.ndarray):
         """keto_check_ids -> (RelationTuple, request max-depth) for oracle_sql.CheckEngine."""
