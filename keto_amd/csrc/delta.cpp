@@ -74,12 +74,28 @@ struct Txn {
         return c < 0 ? -1 : c > 0 ? 1 : 0;
     }
     const RowKey& key(uint32_t r) const { return r < S.row_key.size() ? S.row_key[r] : new_keys[r - S.row_key.size()]; }
+    // a key field of a subject set's target row: ANY stands for the empty string the tuple stored
+    int field_cmp(uint32_t a, uint32_t b) const {
+        if (a == b) return 0;
+        static const std::string empty;
+        const std::string& x = a == ANY ? empty : str_of(a);
+        const std::string& y = b == ANY ? empty : str_of(b);
+        if (a != ANY && b != ANY) return cmp(a, b);
+        const int c = x.compare(y);
+        return c < 0 ? -1 : c > 0 ? 1 : 0;
+    }
+    int64_t ns_field(int64_t ns) const {              // ANY_NS: the namespace named "" (its config id)
+        if (ns != ANY_NS) return ns;
+        auto it = S.ns_by_name.find("");
+        return it == S.ns_by_name.end() ? ANY_NS : (int64_t)S.ns_ids[it->second];
+    }
     // ORDER BY position of a subject set: (namespace id, object bytes, relation bytes)
     int set_cmp(uint32_t ra, uint32_t rb) const {
         const RowKey &a = key(ra), &b = key(rb);
-        if (a.ns != b.ns) return a.ns < b.ns ? -1 : 1;
-        if (a.obj != b.obj) return cmp(a.obj, b.obj);
-        if (a.rel != b.rel) return cmp(a.rel, b.rel);
+        const int64_t na = ns_field(a.ns), nb = ns_field(b.ns);
+        if (na != nb) return na < nb ? -1 : 1;
+        if (a.obj != b.obj) return field_cmp(a.obj, b.obj);
+        if (a.rel != b.rel) return field_cmp(a.rel, b.rel);
         return 0;
     }
     // row of a complete key (-1: none yet)
@@ -110,6 +126,8 @@ struct Txn {
     std::vector<uint32_t>& edges(uint32_t r) {
         auto it = rows.find(r);
         if (it != rows.end()) return it->second;
+        if (r < S.rows.size() && S.row_pp[r] != NO_PAGE)           // holds EDGE_POISON entries
+            throw Error{KETO_E_REBUILD, "a write touches a poisoned row"};
         const auto e = r < S.rows.size() ? S.row_edges(r) : std::pair<const uint32_t*, uint64_t>{nullptr, 0};
         order.push_back(r);
         return rows.emplace(r, std::vector<uint32_t>(e.first, e.first + e.second)).first->second;
@@ -259,7 +277,9 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
         bool seq = false;
         for (uint32_t v : e)
             if (S.coll.count(v)) { seq = true; break; }
-        RowRec rec{0, (uint32_t)((seq ? ROW_SEQ : 0u) << 8), 0, 0};
+        // base rows keep their build edge range (row_edges of the row before reads it as its end)
+        RowRec rec{r < R0 ? S.rows[r].edge_lo : 0u,
+                   (r < R0 ? (S.rows[r].hi_flags & 0xFFu) : 0u) | ((seq ? ROW_SEQ : 0u) << 8), 0, 0};
         if (seq) {
             rec.n_sets = (uint32_t)e.size();
         } else {

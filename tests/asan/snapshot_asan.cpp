@@ -100,6 +100,39 @@ int tuple_round(int it) {
         std::fprintf(stderr, "FAIL round %d: compute on a host-only snapshot did not fail with KETO_E_HIP\n", it);
         return 1;
     }
+    // writes (keto_snapshot_apply) on the host-only snapshot: inserts with new strings and new rows,
+    // deletes of existing and absent tuples; refusals (KETO_E_REBUILD) and unknown namespaces
+    // (KETO_E_INVALID) leave it as it was
+    auto random_tuple = [&](keto_tuple& x) {
+        std::memset(&x, 0, sizeof x);
+        x.namespace_id = pick(20) ? ns[pick(n_ns)].id : 99;
+        x.object = pick(3) ? keep(objs[pick(7)]) : keep("new" + std::to_string(pick(30)));
+        x.relation = keep(rels[pick(4)]);
+        if (pick(2)) {
+            x.subject_kind = 0;
+            x.subject_id = pick(4) ? keep("u" + std::to_string(pick(9))) : keep("w" + std::to_string(pick(50)));
+        } else {
+            x.subject_kind = 1;
+            x.set_namespace_id = ns[pick(n_ns)].id;
+            x.set_object = pick(3) ? keep(objs[pick(7)]) : keep("new" + std::to_string(pick(30)));
+            x.set_relation = keep(rels[pick(4)]);
+        }
+    };
+    for (int w = 0; w < 6; ++w) {
+        std::vector<keto_tuple> ins(pick(7)), del(pick(4));
+        for (auto& x : ins) random_tuple(x);
+        for (auto& x : del) {
+            if (n && pick(2)) x = t[pick(n)];
+            else random_tuple(x);
+        }
+        uint64_t ver = 0;
+        rc = keto_snapshot_apply(s, ins.empty() ? nullptr : ins.data(), ins.size(), del.empty() ? nullptr : del.data(),
+                                 del.size(), &ver);
+        if (rc != KETO_OK && rc != KETO_E_REBUILD && rc != KETO_E_INVALID) return fail("apply");
+        if (keto_snapshot_get_stats(s, &st) != KETO_OK) return fail("stats after apply");
+        rc = keto_resolve_checks(s, q.data(), (uint32_t)q.size(), ids.data(), status.data());
+        if (rc != KETO_OK && rc != KETO_E_INVALID) return fail("resolve after apply");
+    }
     keto_snapshot_release(s);
     return 0;
 }
