@@ -1195,6 +1195,391 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     }
 }
 
+// ------------------------------------------------------------------ check, deep requests
+// Tier 0 for global max-depth 10..64 (config #3: nested groups, depth 32, cycles).  The same design
+// as check_wave_kernel -- a per-lane state machine over a persistent grid in which every loop
+// iteration issues at most one global access per lane, from one instruction for the whole wave --
+// extended to the two things deep searches do all the time and the shallow kernel does inline:
+//   * saved frames live in HBM ([frame][lane], 8 B each, coalesced across the wave); a pop is its
+//     own phase (P_POP: the frame load is the iteration's access);
+//   * visited maps outgrow registers + LDS after a few dozen sets, so their HBM hash-table probes are
+//     a phase too (P_VIS: one probe per iteration, test-and-insert).
+// A lane whose map needs another probe, or whose row needs another id-table bucket, takes another
+// iteration while the other lanes of its wave go on: no lane waits for another lane's probe chain,
+// which is what bounded the inline check_kernel (an iteration there waited for the longest chain of
+// 64 lanes: 5-6 us per step for the long searches in a full wave, 1.9 us alone,
+// profiles/r02h_deep_experiments.log).  A map that fills its table moves the request to tier 1
+// (check_kernel with larger / borrowed tables), as does a search deeper than DF saved frames.
+constexpr uint32_t P_POP = 5, P_VIS = 6;
+// control word: phase 0..2 | k 3..9 | fl 10..13 | sp 14..19 | have 20 | nq 21 | tset 22 | hl 23..27 |
+// nq2 28 | cb 29 | seg 30 | match 31 (the pending visited test decides the request when it is new)
+constexpr uint32_t D_K = 3, D_FL = 10, D_SP = 14, D_HL = 23;
+constexpr uint32_t D_HAVE = 1u << 20, D_NQ = 1u << 21, D_TSET = 1u << 22, D_NQ2 = 1u << 28, D_CB = 1u << 29;
+constexpr uint32_t D_SEG = 1u << 30, D_MATCH = 1u << 31;
+// saved frame: x = position (word within its segment) or the saved single edge (FR_WV);
+// y = left 0..19 | k 20..26 | seg 27 | fl 28..31
+constexpr uint32_t DF_LEFT_MAX = (1u << 20) - 1u;
+constexpr int DF = 63;                                     // saved frames: max-depth <= 64
+
+template <int RV, int LV, bool COUNT>
+__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
+    deep_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                     uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t slot = blockIdx.x * blockDim.x + tid;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
+    __shared__ uint4 lds_nq[2 * LDS_STRIDE];                   // the lane's prefetched request pair
+    uint32_t* const vcol = lds_vis + tid;
+    uint2* const frames = reinterpret_cast<uint2*>(ta.gstack) + slot;   // frame f at frames[f * stride]
+    uint64_t* const tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
+    Work<COUNT> w;
+    // visited map: the first RV ids in registers, the next LV in the lane's LDS column, the rest in
+    // the lane's epoch-tagged HBM table (probed by P_VIS); a 64-bit filter of all of them
+    uint32_t vr[RV];
+    uint32_t vf0 = 0, vf1 = 0, vn = 0, vcount = 0;
+    uint32_t epoch = ta.slot_epoch[slot];
+    auto vfresh = [&]() {
+        vn = 0;
+        vf0 = vf1 = 0;
+#pragma unroll
+        for (int i = 0; i < RV; ++i) vr[i] = NONE32;
+        if (epoch >= 0xFFFFFFFEu) {                            // epoch wrap: clear this lane's table once
+            for (uint32_t i = 0; i <= ta.mask; ++i) tab[i] = 0;
+            epoch = 0;
+        }
+        ++epoch;
+        vcount = 0;
+    };
+    vfresh();
+    // runs of requests: as check_wave_kernel (static runs, or per-XCD dynamic runs)
+    const uint32_t R = ta.dyn & 0xFFFFu;
+    uint32_t j, j_end, xe = n, dyn_base = 0;
+    uint32_t* head = nullptr;
+    bool whole_groups = true;
+    if (R == 0) {
+        uint32_t per = (n + stride - 1) / stride;
+        if (per >= 4u) per = (per + 3u) & ~3u;
+        whole_groups = (per & 3u) == 0;
+        j = min(n, slot * per);
+        j_end = min(n, j + per);
+    } else {
+        const uint32_t nx = min(8u, gridDim.x);
+        const uint32_t xcd = blockIdx.x % nx;
+        const uint32_t lanes_x = (gridDim.x - xcd + nx - 1u) / nx * blockDim.x;
+        const uint32_t lx = (blockIdx.x / nx) * blockDim.x + tid;
+        const uint32_t xs = (uint32_t)(((uint64_t)n * xcd / nx) & ~3ull);
+        xe = xcd == nx - 1u ? n : (uint32_t)(((uint64_t)n * (xcd + 1u) / nx) & ~3ull);
+        const uint32_t r0 = (uint32_t)((uint64_t)(xe - xs) * (ta.dyn >> 16) / 8u / lanes_x) & ~3u;
+        j = min(xe, xs + lx * r0);
+        j_end = min(xe, j + r0);
+        dyn_base = xs + lanes_x * r0;
+        head = ta.heads + 32u * xcd;
+    }
+    const bool packed = ((uintptr_t)allowed & 3u) == 0 && whole_groups;
+    uint32_t acc = 0;
+
+    uint32_t c = P_REQ;
+    uint32_t T = 0;
+    uint32_t pos = 0, left = 0;
+    uint4 win = make_uint4(0, 0, 0, 0);
+    uint32_t eh = 0;                                           // row to enter / bucket / pending child
+    uint32_t vv = 0, pi = 0;                                   // pending visited test: id, probe slot
+    uint32_t it = 0;                                           // COUNT: iterations of the request
+    auto decide = [&](uint32_t qi, uint32_t r) {
+        if (!packed || (qi | 3u) >= j_end) {
+            allowed[qi] = (uint8_t)r;
+            return;
+        }
+        acc |= r << ((qi & 3u) * 8u);
+        if ((qi & 3u) == 3u) {
+            *reinterpret_cast<uint32_t*>(allowed + (qi & ~3u)) = acc;
+            acc = 0;
+        }
+    };
+    auto start_next = [&]() {
+        while (c & D_NQ) {
+            const uint4 nq = lds_nq[tid];
+            const uint32_t qi = j++;
+            uint32_t keep = 0;
+            if (c & D_NQ2) {
+                lds_nq[tid] = lds_nq[LDS_STRIDE + tid];
+                keep = D_NQ;
+            }
+            int d = (int)nq.w;
+            if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
+            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
+                decide(qi, 0);
+                c = keep;
+                continue;
+            }
+            T = nq.y;
+            eh = nq.x;
+            if constexpr (COUNT) it = 0;
+            c = P_HDR | ((uint32_t)d << D_K) | ((nq.z & 1u) ? D_TSET : 0u) | keep;
+            return;
+        }
+        c = (c & ~7u) | P_REQ;
+    };
+    // a visited test the registers / LDS decide: 1 visited, 0 new (inserted), -1 the HBM table must
+    // be probed (P_VIS; vv set, the first probe slot in pi)
+    auto vtest = [&](uint32_t vid) -> int {
+        const uint32_t b = (vid * 0x9E3779B1u) >> 26;
+        const uint32_t bit = 1u << (b & 31u);
+        const bool maybe = ((b < 32 ? vf0 : vf1) & bit) != 0;
+        if (maybe) {
+            const uint32_t m = min(vn, (uint32_t)(RV + LV));
+            bool hit = false;
+#pragma unroll
+            for (int i = 0; i < RV; ++i) hit |= vr[i] == vid;
+            for (uint32_t i = RV; i < m && !hit; ++i) hit = vcol[(i - RV) * LDS_STRIDE] == vid;
+            if (hit) return 1;
+        }
+        if (b < 32) vf0 |= bit;
+        else vf1 |= bit;
+        if (vn < (uint32_t)RV) {
+#pragma unroll
+            for (int i = 0; i < RV; ++i)
+                if ((uint32_t)i == vn) vr[i] = vid;
+            ++vn;
+            return 0;
+        }
+        if (vn < (uint32_t)(RV + LV)) {
+            vcol[(vn - RV) * LDS_STRIDE] = vid;
+            ++vn;
+            return 0;
+        }
+        if (!maybe && vn == (uint32_t)(RV + LV)) {
+            // (the filter ruled it out, but the table may be needed for the insert)
+        }
+        vv = vid;
+        pi = mix32(vid) & ta.mask;
+        return -1;
+    };
+    for (;;) {
+        uint32_t ph = bf(c, C_PH, 3);
+        if (ph == P_REQ && j >= j_end) {
+            if (R == 0) break;
+            const uint64_t m = __ballot(1);
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            uint32_t base = 0;
+            if ((tid & 63u) == leader) base = atomicAdd(head, (uint32_t)__popcll(m));
+            base = __shfl(base, (int)leader);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint64_t st = (uint64_t)dyn_base + (uint64_t)(base + below) * R;
+            if (st >= xe) break;
+            j = (uint32_t)st;
+            j_end = (uint32_t)min<uint64_t>(xe, st + R);
+        }
+        if constexpr (COUNT) ++it;
+        // ---- the iteration's global access (one per lane) and the next request pair's prefetch
+        const bool hdr = ph == P_HDR;
+        const bool in_ov = hdr ? eh >= ov.base : (bf(c, D_FL, 4) & FR_OV) != 0;
+        const bool hi = hdr ? ((eh >> SEG_SHIFT) & 1u) != 0 : (c & D_SEG) != 0;
+        const uint32_t* const ar = (in_ov ? ov.arena : s.arena) + ((hi && !in_ov) ? (1ull << 32) : 0ull);
+        const uint32_t hl = bf(c, D_HL, 5);
+        const uint32_t sp = bf(c, D_SP, 6);
+        const uint4* a0 = reinterpret_cast<const uint4*>(
+            ar + (hdr ? (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS
+                      : ph == P_IDQ ? pos - HDR_WORDS - ((c & D_CB) ? CB_WORDS : 0u) - (1u << hl) + eh * BUCKET_WORDS
+                                    : (pos & ~3u)));
+        const bool cbq = hdr && (c & (D_HAVE | D_TSET)) == D_HAVE;
+        uint32_t cwd, cbit;
+        closure_bit(T, cwd, cbit);
+        if (hdr) w.header(a0);
+        else if (ph == P_IDQ) w.id_at(a0, true);
+        else if (ph == P_EDGE) w.edge_at(a0);
+        if (!(c & D_NQ) && j < j_end) {
+            prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
+            c |= D_NQ | (j + 1u < j_end ? D_NQ2 : 0u);
+            w.request();
+        }
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+        uint2 fr = make_uint2(0, 0);
+        uint64_t ve = 0;
+        uint32_t cbw = NONE32;
+        if (ph == P_POP) fr = frames[(uint64_t)(sp - 1u) * stride];
+        else if (ph == P_VIS) ve = tab[pi];
+        else if (ph != P_REQ) v0 = a0[0];
+        if (hdr) v1 = a0[1];
+        if (cbq) cbw = reinterpret_cast<const uint32_t*>(a0)[(int)cwd - (int)CB_WORDS];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ph == P_REQ) {
+            start_next();
+            continue;
+        }
+        int res = -1;
+        const bool tset = (c & D_TSET) != 0;
+        if (ph == P_VIS) {
+            // one probe of the HBM table: empty (another epoch) -> the id is new, insert it here
+            w.vprobe();
+            const uint64_t want = ((uint64_t)epoch << 32) | vv;
+            if ((uint32_t)(ve >> 32) != epoch) {
+                if ((++vcount) * 2u > ta.mask + 1u) {
+                    res = RES_OVERFLOW;                        // the map outgrew the table: next tier
+                } else {
+                    tab[pi] = want;
+                    w.vinsert();
+                    if (c & D_MATCH) res = RES_TRUE;          // engine.go:54-57
+                    else c = bf_set(c, C_PH, 3, eh != NONE32 ? P_HDR : P_WALK);
+                }
+            } else if (ve == want) {
+                c = bf_set(c, C_PH, 3, P_WALK);               // visited: skip it
+            } else {
+                pi = (pi + 1u) & ta.mask;                     // next probe, next iteration
+            }
+            c &= ~(res < 0 && bf(c, C_PH, 3) != P_VIS ? D_MATCH : 0u);
+        } else if (ph == P_POP) {
+            const uint32_t nsp = sp - 1u;
+            if ((fr.y >> 28) & FR_WV) {                        // a saved single edge
+                win = make_uint4(fr.x, fr.x, fr.x, fr.x);
+                pos = 0;
+            } else {
+                pos = fr.x;
+            }
+            left = fr.y & DF_LEFT_MAX;
+            c = bf_set(bf_set(bf_set(c, D_SP, 6, nsp), D_K, 7, (fr.y >> 20) & 127u), D_FL, 4, fr.y >> 28);
+            c = ((fr.y >> 27) & 1u) ? (c | D_SEG) : (c & ~D_SEG);
+            c = bf_set(c, C_PH, 3, P_WALK);
+            w.pop();
+        } else if (ph == P_HDR && cbq && (v0.z & HDR_CLOSURE) && !((cbw >> cbit) & 1u)) {
+            w.row();
+            w.pruned();
+            c = bf_set(c, C_PH, 3, P_WALK);                   // T is not below this set: skip it
+        } else if (ph == P_HDR && (v0.z & HDR_FWD)) {
+            eh = v0.x;                                        // a row a write moved (delta.cpp)
+        } else if (ph == P_HDR) {
+            w.row();
+            const bool have = (c & D_HAVE) != 0;
+            if (have && left > 0) {                           // save the parent (it has edges left)
+                if (sp == (uint32_t)DF || left > DF_LEFT_MAX) {
+                    res = RES_OVERFLOW;
+                } else {
+                    const uint32_t fl0 = bf(c, D_FL, 4);
+                    uint32_t fl = fl0, px = pos;
+                    if (left == 1 && (fl0 & FR_WV)) px = win_at(win, pos & 3u);
+                    else fl = fl0 & ~(uint32_t)FR_WV;
+                    frames[(uint64_t)sp * stride] =
+                        make_uint2(px, left | (bf(c, D_K, 7) << 20) | ((c & D_SEG) ? (1u << 27) : 0u) | (fl << 28));
+                    c = bf_set(c, D_SP, 6, sp + 1u);
+                    w.push();
+                }
+            }
+            if (res < 0) {
+                const bool is_ov = eh >= ov.base;
+                const bool seq = (v0.z & HDR_SEQ) != 0;
+                const uint32_t hln = (v0.z >> 8) & 31u;
+                const uint32_t k = have ? bf(c, D_K, 7) - 1u : bf(c, D_K, 7);
+                const uint32_t fl = (have ? 0u : (uint32_t)FR_TOP) | (seq ? FR_SEQ : 0u) | (is_ov ? FR_OV : 0u) | FR_WV;
+                pos = (is_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS + HDR_WORDS;
+                left = v0.x;
+                win = v1;
+                c = bf_set(bf_set(bf_set(bf_set(c, D_K, 7, k), D_FL, 4, fl), D_HL, 5, hln), C_PH, 3, P_WALK) | D_HAVE;
+                c = (v0.z & HDR_CLOSURE) ? (c | D_CB) : (c & ~D_CB);
+                c = (!is_ov && ((eh >> SEG_SHIFT) & 1u)) ? (c | D_SEG) : (c & ~D_SEG);
+                const uint32_t n_sets = v0.x, n_ids = v0.y;
+                if (!seq && !tset && n_ids > 0) {             // is the requested id in the row?
+                    if (hln == 0) {
+                        bool hit = false;
+#pragma unroll
+                        for (uint32_t i = 0; i < WINDOW_WORDS; ++i)
+                            hit |= (i >= n_sets) & (i < n_sets + n_ids) & (win_at(win, i) == T);
+                        w.idread(n_ids);
+                        if (hit) res = RES_TRUE;
+                    } else {
+                        uint32_t b1, b2;
+                        bloom_bits(T, b1, b2);
+                        if (bloom_has(v0.z, v0.w, b1) && bloom_has(v0.z, v0.w, b2)) {
+                            eh = mix32(T) & ((1u << hln) / BUCKET_WORDS - 1u);
+                            c = bf_set(c, C_PH, 3, P_IDQ);
+                        }
+                    }
+                }
+            }
+        } else if (ph == P_IDQ) {
+            w.idread(BUCKET_WORDS);
+            if (has4(v0, T)) res = RES_TRUE;
+            else if (has4(v0, NONE32)) c = bf_set(c, C_PH, 3, P_WALK);
+            else eh = (eh + 1u) & ((1u << bf(c, D_HL, 5)) / BUCKET_WORDS - 1u);
+        } else if (ph == P_EDGE) {
+            win = v0;
+            c = bf_set(c, C_PH, 3, P_WALK) | ((uint32_t)FR_WV << D_FL);
+        }
+        // ---- walk the window (registers, LDS); HBM probes, pops and reloads are phases
+        while (res < 0 && bf(c, C_PH, 3) == P_WALK) {
+            if (left == 0) {                                  // row exhausted: pop
+                if (bf(c, D_SP, 6) == 0) {
+                    res = RES_FALSE;
+                    break;
+                }
+                c = bf_set(c, C_PH, 3, P_POP);
+                break;
+            }
+            const uint32_t fl = bf(c, D_FL, 4);
+            if (!(fl & FR_WV)) {
+                c = bf_set(c, C_PH, 3, P_EDGE);
+                break;
+            }
+            const uint32_t e = win_at(win, pos & 3u);
+            ++pos;
+            --left;
+            if ((pos & 3u) == 0) c &= ~((uint32_t)FR_WV << D_FL);
+            w.edge();
+            const uint32_t tval = tset ? (EDGE_SET | T) : T;
+            int t = 0;
+            bool match = false;
+            eh = NONE32;
+            if (e & EDGE_SET) {
+                uint32_t vid = e & EDGE_VAL;
+                if (fl & FR_SEQ) {
+                    const uint32_t cv = coll_lookup(s, e);
+                    if (cv != NONE32) vid = cv;
+                }
+                if (fl & FR_TOP) {                            // fresh map per top-level tuple
+                    vfresh();
+                    w.item();
+                }
+                match = tset && e == tval;
+                if (!match && bf(c, D_K, 7) >= 2) eh = e & EDGE_VAL;   // remaining depth after the hop >= 1
+                t = vtest(vid);
+            } else {                                          // subject id in an ordered row
+                match = !tset && e == tval;
+                if (!(fl & FR_TOP)) {
+                    const uint32_t cv = coll_lookup(s, e);
+                    if (cv != NONE32) t = vtest(cv);
+                }
+            }
+            if (t < 0) {                                      // the HBM table decides: P_VIS
+                c = bf_set(c, C_PH, 3, P_VIS) | (match ? D_MATCH : 0u);
+                break;
+            }
+            if (t == 0) {
+                if (match) res = RES_TRUE;                    // engine.go:54-57
+                else if (eh != NONE32) c = bf_set(c, C_PH, 3, P_HDR);
+            }
+        }
+        if (res >= 0) {
+            const uint32_t qi = j - 1;
+            if constexpr (COUNT) {
+                if (ta.steps) ta.steps[qi] += it;
+            }
+            c &= ~D_MATCH;
+            if (res == RES_OVERFLOW) {
+                const uint32_t at = atomicAdd(ta.out_count, 1u);
+                ta.out_list[at] = qi;
+                decide(qi, 0);
+            } else {
+                decide(qi, (uint32_t)res);
+            }
+            start_next();
+        }
+    }
+    ta.slot_epoch[slot] = epoch;
+    if constexpr (COUNT) {
+        for (int i = 0; i < 16; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
+    }
+}
+
 // ------------------------------------------------------------------ expand
 struct ExpandOut {
     keto_tree_node* nodes;   // FILL only
@@ -2136,8 +2521,18 @@ CheckKernelFn t0_kernel(int var, bool count) {
 }
 }  // namespace
 
+// deep batches (global max-depth 10..64) take deep_wave_kernel as tier 0 only with KETO_DEEP_WAVE=1:
+// on config #3 it lost to the inline check_kernel (366 + 231 ms vs 258 ms, the critical path is ~4
+// dependent accesses per DFS step either way, and its 16K-entry maps overflow to tier 1 where the
+// inline kernel borrows in place; profiles/r02j_deep_sweep.log)
+bool deep_wave(int32_t gmd) {
+    const char* e = getenv("KETO_DEEP_WAVE");
+    return gmd - 1 <= DF && e && atoi(e) == 1;
+}
+
 const char* device_check_kernel_name(int32_t gmd) {
     const int fr = std::max(1, std::min<int32_t>(gmd, 65535) - 1);
+    if (fr > 8 && deep_wave(gmd)) return "keto::deep_wave_kernel<8, 8, false>";
     if (fr > 8) return "keto::check_kernel<keto::GlobalStack, false, 0>";
     return t0_kernel_name(fr <= 4 ? t0_variant() : T0_VARIANTS);
 }
@@ -2175,11 +2570,14 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
         while (s2 * 2 <= want) s2 *= 2;
         p.slots[2] = s2;
     }
-    const int var = kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : T0_VARIANTS + 1;
+    const bool dw = kind == 2 && deep_wave(gmd);
+    const int var = kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
-        if (kind == 2)
+        if (dw)
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, deep_wave_kernel<8, 8, false>, 256, 0));
+        else if (kind == 2)
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_kernel<GlobalStack, false, 0>, 256, 0));
         else
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_kernel(var, false), 256, 0));
@@ -2208,7 +2606,9 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
         const char* e0 = getenv("KETO_T0_CAP");
         const char* e1 = getenv("KETO_T1_SLOTS");
         const char* e2 = getenv("KETO_T1_CAP");
-        p.cap[0] = fit(p.slots[0], 256, e0 ? (uint32_t)atoi(e0) : 16384u);
+        // tier-0 tables of up to 32K entries (profiles/r02h_deep_experiments.log: 16K -> 32K took the
+        // inline kernel from 302 to 254 ms on config #3)
+        p.cap[0] = fit(p.slots[0], 256, e0 ? (uint32_t)atoi(e0) : 32768u);
         p.slots[1] = (uint32_t)std::min<uint64_t>(e1 ? (uint32_t)atoi(e1) : 131072u, ((uint64_t)n + 255) / 256 * 256);
         p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, e2 ? (uint32_t)atoi(e2) : 65536u));
         p.pool = getenv("KETO_NO_POOL") == nullptr;
@@ -2253,6 +2653,22 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                           a.heads = D.heads;
                       }
                       go(t0_kernel(var, dwork != nullptr));
+                  }
+                  else if (level == 0 && dw) {
+                      // frames: the tier's GlobalStack area as [frame][lane] 8-B words (DF per lane)
+                      // (a search holds at most gmd - 1 saved frames)
+                      if ((uint64_t)t.gstack_n * 2 < (uint64_t)std::max(1, gmd - 1))
+                          throw Error{KETO_E_RANGE, "deep frame area too small"};
+                      a.dyn = getenv("KETO_T0_DYN_FORCE") ? t0_dyn(n, slots) : 0u;
+                      if (a.dyn) {
+                          if (!D.heads) {
+                              uint64_t acc = 0;
+                              D.heads = dmalloc<uint32_t>(8 * 32, acc);
+                          }
+                          HIP_OK(hipMemsetAsync(D.heads, 0, 8 * 32 * sizeof(uint32_t), st));
+                          a.heads = D.heads;
+                      }
+                      dwork ? go(deep_wave_kernel<8, 8, true>) : go(deep_wave_kernel<8, 8, false>);
                   }
                   else if (level == 0)
                       dwork ? go(check_kernel<GlobalStack, true, 0>) : go(check_kernel<GlobalStack, false, 0>);

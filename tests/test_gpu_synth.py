@@ -29,11 +29,12 @@ def nested():
     g.close()
 
 
-@pytest.mark.parametrize("gmd", [32, 16, 40, 7])
-def test_nested_deep_checks_match_oracle(nested, gmd):
+@pytest.mark.parametrize("gmd,wave", [(32, 0), (16, 0), (40, 0), (7, 0), (32, 1), (12, 1), (40, 1)])
+def test_nested_deep_checks_match_oracle(nested, monkeypatch, gmd, wave):
     """Config #3 shape: chains of 32 nested groups with cycles; global max-depth up to 40 takes the
-    deep (global-stack) kernel tiers."""
+    deep (global-stack) kernel tiers, or deep_wave_kernel as tier 0 (KETO_DEEP_WAVE=1)."""
     g, snap = nested
+    monkeypatch.setenv("KETO_DEEP_WAVE", str(wave))
     q = g.queries_nested(12000, seed=100 + gmd, depths=(5, 16, 32, 0, -1, 40))
     gpu = snap.check_batch_ids(snap.with_handles(q), gmd)
     tab = g.oracle_table(q, max(gmd, 1))
