@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -134,6 +135,7 @@ struct Work {
     __device__ inline void pop() {}
     __device__ inline void leaf(bool, uint32_t) {}
     __device__ inline void pruned() {}
+    __device__ inline void simt(int) {}
 };
 template <>
 struct Work<true> {
@@ -172,6 +174,14 @@ struct Work<true> {
         if (miss) ++c[14];
     }
     __device__ inline void pruned() { ++c[15]; }
+    // SIMT profile (work slots 16..23, KETO_SIMT_PROF): even k = wave-level count of event k/2
+    // (once per wave, by its first active lane), odd k = lane-level count of it
+    uint32_t s[8] = {};
+    __device__ inline void simt(int k) {
+        const uint64_t m = __ballot(1);
+        if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)m) - 1u) ++s[2 * k];
+        ++s[2 * k + 1];
+    }
 };
 // ------------------------------------------------------------------ visited maps
 struct Visited {
@@ -465,11 +475,16 @@ struct TierArgs {
     uint32_t pool_mask, pool_n;
     uint32_t* pool_epoch;
     uint32_t* pool_busy;
-    // tier-0 wave kernel: dyn bits 0..15 > 0 hand out request runs of that many requests from 8
-    // per-XCD heads (heads[32 x]) once a lane's static first run (its share of dyn bits 16..19
-    // eighths of the XCD's range) is done; 0 = static runs only
+    // tier-0 wave kernel: dyn bits 0..15 > 0 hand out request runs of that many requests once a
+    // lane's static first run (its share of dyn bits 16..18 eighths of the XCD's range) is done,
+    // from 2^(dyn bits 20..23) heads per XCD (heads[32 (xcd H + h)], one line each) that deal the
+    // XCD's runs out interleaved (head h: runs h, h + H, ...); 0 = static runs only
     uint32_t* heads;
     uint32_t dyn;
+    // tier-0 wave kernel: walk at most this many window edges / pops per loop iteration (>= 1;
+    // ~0u = until the lane needs a global access); a lane stopped early goes on next iteration
+    // without one
+    uint32_t walk_cap;
     // COUNT kernels: per-request loop iterations (the serial chain length of a request's search),
     // added over the tiers that ran it; NULL = not recorded
     uint32_t* steps;
@@ -785,14 +800,16 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
 // A request needing more than F saved frames, or a row with more than WF_LEFT_MAX edges left when
 // saved, overflows to the next tier (check_kernel).  Lane control state is one packed word.
 constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
-constexpr uint32_t WF_LEFT_MAX = (1u << 23) - 1u;   // saved lkf = left | k << 23 | fl << 28
+constexpr uint32_t WF_LEFT_MAX = (1u << 19) - 1u;   // saved lkf = left | skip << 19 | k << 23 | seg << 27 | fl << 28
 // control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23 | nq2 24
 // | cb 25 (the current row has a closure filter, so its id table starts CB_WORDS further down)
 // | seg 26 (the current row lies in arena segment 1: positions are 32-bit words within a segment)
-constexpr uint32_t C_PH = 0, C_K = 3, C_FL = 8, C_SP = 12, C_HL = 19;
+// | skip 27..30 (window slot i's subject set is ruled out by the row's child signatures; cleared
+//   when the walk leaves the row's first block)
+constexpr uint32_t C_PH = 0, C_K = 3, C_FL = 8, C_SP = 12, C_HL = 19, C_MK = 27;
 constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18, C_NQ2 = 1u << 24, C_CB = 1u << 25;
-constexpr uint32_t C_SEG = 1u << 26;
-// saved frame word: left 0..22 | k 23..26 (tier 0 runs max-depth <= 9) | seg 27 | fl 28..31
+constexpr uint32_t C_SEG = 1u << 26, C_MKS = 15u << C_MK;
+// saved frame word: left 0..18 | skip 19..22 | k 23..26 (tier 0 runs max-depth <= 9) | seg 27 | fl 28..31
 __device__ inline uint32_t bf(uint32_t c, uint32_t off, uint32_t wd) { return (c >> off) & ((1u << wd) - 1u); }
 __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_t v) {
     const uint32_t m = ((1u << wd) - 1u) << off;
@@ -911,11 +928,11 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         const uint32_t lx = (blockIdx.x / nx) * blockDim.x + tid;
         const uint32_t xs = (uint32_t)(((uint64_t)n * xcd / nx) & ~3ull);
         xe = xcd == nx - 1u ? n : (uint32_t)(((uint64_t)n * (xcd + 1u) / nx) & ~3ull);
-        const uint32_t r0 = (uint32_t)((uint64_t)(xe - xs) * (ta.dyn >> 16) / 8u / lanes_x) & ~3u;
+        const uint32_t r0 = (uint32_t)((uint64_t)(xe - xs) * ((ta.dyn >> 16) & 7u) / 8u / lanes_x) & ~3u;
         j = min(xe, xs + lx * r0);
         j_end = min(xe, j + r0);
         dyn_base = xs + lanes_x * r0;
-        head = ta.heads + 32u * xcd;
+        head = ta.heads + 32u * (xcd << ((ta.dyn >> 20) & 15u));
     }
     const bool packed = ((uintptr_t)allowed & 3u) == 0 && whole_groups;
     uint32_t acc = 0;                                          // decisions of the current group of 4
@@ -968,18 +985,29 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         const uint32_t ph = bf(c, C_PH, 3);
         if (ph == P_REQ && j >= j_end) {
             if (R == 0) break;
-            // the lanes that finished their run take the next runs of their XCD's range together
-            const uint64_t m = __ballot(1);
-            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-            uint32_t base = 0;
-            if ((tid & 63u) == leader) base = atomicAdd(head, (uint32_t)__popcll(m));
-            base = __shfl(base, (int)leader);
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint64_t st = (uint64_t)dyn_base + (uint64_t)(base + below) * R;
-            if (st >= xe) break;
-            j = (uint32_t)st;
-            j_end = (uint32_t)min<uint64_t>(xe, st + R);
+            // the lanes that finished their run take the next runs of their XCD's range together:
+            // from the wave's home head first, then (that head dealt out) from the XCD's others
+            const uint32_t hl2 = (ta.dyn >> 20) & 15u, H = 1u << hl2;
+            uint32_t h = ((blockIdx.x / min(8u, gridDim.x)) * (blockDim.x >> 6) + (tid >> 6)) & (H - 1u);
+            bool got = false;
+            for (uint32_t t = 0; t < H; ++t, h = (h + 1u) & (H - 1u)) {
+                const uint64_t m = __ballot(1);
+                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+                uint32_t base = 0;
+                if ((tid & 63u) == leader) base = atomicAdd(head + 32u * h, (uint32_t)__popcll(m));
+                base = __shfl(base, (int)leader);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                const uint64_t st = (uint64_t)dyn_base + (((uint64_t)(base + below) << hl2) + h) * R;
+                if (st < xe) {
+                    j = (uint32_t)st;
+                    j_end = (uint32_t)min<uint64_t>(xe, st + R);
+                    got = true;
+                    break;
+                }
+            }
+            if (!got) break;
         }
+        w.simt(0);
         // ---- the iteration's global accesses: one per lane (selected without branches), plus the
         // next request pair's prefetch
         const bool hdr = ph == P_HDR;
@@ -1010,15 +1038,20 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             w.request();
         }
         uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-        uint32_t cbw = NONE32;
-        if (ph != P_REQ) v0 = a0[0];
+        uint32_t cbw = NONE32, sgw = NONE32;
+        if (ph != P_REQ && ph != P_WALK) v0 = a0[0];
         if (hdr) v1 = a0[1];
-        if (cbq) cbw = reinterpret_cast<const uint32_t*>(a0)[(int)cwd - (int)CB_WORDS];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // also retires the LDS-direct prefetch
+        if (cbq) {
+            // T's closure-filter word and T's child-signature word (both in the header's line)
+            cbw = reinterpret_cast<const uint32_t*>(a0)[(int)cwd - (int)CB_WORDS];
+            sgw = reinterpret_cast<const uint32_t*>(a0)[(int)((cbit & 15u) >> 3) - (int)SIG_WORDS];
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), seen by the compiler's waitcnt pass; also retires the LDS-direct prefetch
         if (ph == P_REQ) {
             start_next();
             continue;
         }
+        w.simt(1);
         int res = -1;
         const bool tset = (c & C_TSET) != 0;
         if (ph == P_HDR && cbq && (v0.z & HDR_CLOSURE) && !((cbw >> cbit) & 1u)) {
@@ -1034,6 +1067,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         } else if (ph == P_HDR) {
             // entering a row (engine.go:82-114): save the parent if it still has edges
             w.row();
+            w.simt(3);
             const bool have = (c & C_HAVE) != 0;
             if (have && left > 0) {
                 const uint32_t sp = bf(c, C_SP, 4);
@@ -1048,8 +1082,11 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                         if (left == 1 && (fl0 & FR_WV)) px = win_at(win, pos & 3u);
                         else fl = fl0 & ~(uint32_t)FR_WV;
                     }
+                    // the window's skip bits go with it (a saved single edge: its own, as slot 0)
+                    const uint32_t mk = !WIN && (fl & FR_WV) && left == 1 ? (c >> (C_MK + (pos & 3u))) & 1u : bf(c, C_MK, 4);
                     sf_pk[sp * LDS_STRIDE + tid] =
-                        make_uint2(px, left | (bf(c, C_K, 5) << 23) | ((c & C_SEG) ? (1u << 27) : 0u) | (fl << 28));
+                        make_uint2(px, left | (mk << 19) | (bf(c, C_K, 5) << 23) | ((c & C_SEG) ? (1u << 27) : 0u) |
+                                           (fl << 28));
                     if constexpr (WIN) sf_win[sp * LDS_STRIDE + tid] = win;
                     c = bf_set(c, C_SP, 4, sp + 1);
                     w.push();
@@ -1067,6 +1104,10 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 c = bf_set(bf_set(bf_set(bf_set(c, C_K, 5, k), C_FL, 4, fl), C_HL, 5, hl), C_PH, 3, P_WALK) | C_HAVE;
                 c = (v0.z & HDR_CLOSURE) ? (c | C_CB) : (c & ~C_CB);
                 c = (!is_ov && ((eh >> SEG_SHIFT) & 1u)) ? (c | C_SEG) : (c & ~C_SEG);
+                // window slots whose subject set cannot reach T (child signatures, read entering a
+                // subject set; never for a subject-set request)
+                const uint32_t skip = (have && !tset && (v0.z & HDR_CLOSURE)) ? ~(sgw >> ((cbit & 7u) * 4u)) & 15u : 0u;
+                c = (c & ~C_MKS) | (skip << C_MK);
                 const uint32_t n_sets = v0.x, n_ids = v0.y;
                 if constexpr (COUNT) {
                     if (!seq && n_sets == 0 && !tset) {
@@ -1113,7 +1154,9 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             c = bf_set(c, C_PH, 3, P_WALK) | ((uint32_t)FR_WV << C_FL);
         }
         // ---- walk the window (registers, LDS; HBM only for visited spills and collisions)
-        while (res < 0 && bf(c, C_PH, 3) == P_WALK) {
+        for (uint32_t trip = 0; res < 0 && bf(c, C_PH, 3) == P_WALK; ++trip) {
+            if (trip == ta.walk_cap) break;                       // go on next iteration
+            w.simt(2);
             if (left == 0) {                                      // row exhausted: pop
                 uint32_t sp = bf(c, C_SP, 4);
                 if (sp == 0) {
@@ -1132,7 +1175,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                     pos = pk.x;
                 }
                 left = pk.y & WF_LEFT_MAX;
-                c = bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 15u), C_FL, 4, pk.y >> 28);
+                c = bf_set(bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 15u), C_FL, 4, pk.y >> 28), C_MK,
+                           4, pk.y >> 19);
                 c = ((pk.y >> 27) & 1u) ? (c | C_SEG) : (c & ~C_SEG);
                 w.pop();
                 continue;
@@ -1143,9 +1187,10 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 break;
             }
             const uint32_t e = win_at(win, pos & 3u);
+            const bool skip = (c >> (C_MK + (pos & 3u))) & 1u;
             ++pos;
             --left;
-            if ((pos & 3u) == 0) c &= ~((uint32_t)FR_WV << C_FL);
+            if ((pos & 3u) == 0) c &= ~(((uint32_t)FR_WV << C_FL) | C_MKS);
             w.edge();
             const uint32_t tval = tset ? (EDGE_SET | T) : T;
             if (e & EDGE_SET) {
@@ -1163,8 +1208,12 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 else if (t == 0) {
                     if (tset && e == tval) res = RES_TRUE;        // engine.go:54-57
                     else if (bf(c, C_K, 5) >= 2) {                // remaining depth after the hop >= 1
-                        eh = e & EDGE_VAL;
-                        c = bf_set(c, C_PH, 3, P_HDR);
+                        if (skip) {
+                            w.pruned();                           // its closure filter rules T out
+                        } else {
+                            eh = e & EDGE_VAL;
+                            c = bf_set(c, C_PH, 3, P_HDR);
+                        }
                     }
                 }
             } else {                                              // subject id in an ordered row
@@ -1192,6 +1241,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     ta.slot_epoch[slot] = V.epoch;
     if constexpr (COUNT) {
         for (int i = 0; i < 16; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
+        for (int i = 0; i < 8; ++i) atomicAdd(work + 16 + i, (unsigned long long)w.s[i]);
     }
 }
 
@@ -1270,7 +1320,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         const uint32_t lx = (blockIdx.x / nx) * blockDim.x + tid;
         const uint32_t xs = (uint32_t)(((uint64_t)n * xcd / nx) & ~3ull);
         xe = xcd == nx - 1u ? n : (uint32_t)(((uint64_t)n * (xcd + 1u) / nx) & ~3ull);
-        const uint32_t r0 = (uint32_t)((uint64_t)(xe - xs) * (ta.dyn >> 16) / 8u / lanes_x) & ~3u;
+        const uint32_t r0 = (uint32_t)((uint64_t)(xe - xs) * ((ta.dyn >> 16) & 7u) / 8u / lanes_x) & ~3u;
         j = min(xe, xs + lx * r0);
         j_end = min(xe, j + r0);
         dyn_base = xs + lanes_x * r0;
@@ -1403,7 +1453,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         else if (ph != P_REQ) v0 = a0[0];
         if (hdr) v1 = a0[1];
         if (cbq) cbw = reinterpret_cast<const uint32_t*>(a0)[(int)cwd - (int)CB_WORDS];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (visible to the compiler's waitcnt pass)
         if (ph == P_REQ) {
             start_next();
             continue;
@@ -1731,7 +1781,7 @@ struct DeviceState {
     uint32_t* pool_busy = nullptr; // borrowed-table bitmaps: tier 2's tables (8 words), tier 1's
     uint64_t pool_words = 0;
     uint32_t* counters = nullptr; // 2 counters
-    uint32_t* heads = nullptr;    // tier-0 per-XCD run heads (8 x 128 B)
+    uint32_t* heads = nullptr;    // tier-0 run heads (8 XCDs x up to 16 heads x 128 B)
     uint64_t list_cap = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
@@ -1834,6 +1884,7 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     a.pool = nullptr;
     a.heads = nullptr;
     a.dyn = 0;
+    a.walk_cap = 0xFFFFFFFFu;
     a.steps = nullptr;
     a.pool_mask = 0;
     a.pool_n = 0;
@@ -1862,7 +1913,7 @@ void host_parallel_for(uint64_t n, F f) {
 
 // Write one row (table, closure filter seed, header, edges) into an arena at its handle.  The
 // closure filter starts as the row's own ids (all bits for a ROW_SEQ row); closure_pass adds the
-// closures of its subject sets on the device.
+// closures of its subject sets on the device, then sig_pass its child signatures.
 void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uint32_t hlog2, const uint32_t* edges,
              uint64_t n_stored, const std::vector<uint32_t>& unit_of_row, bool closure) {
     uint64_t h = (uint64_t)unit * HDR_WORDS;
@@ -1873,7 +1924,8 @@ void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uin
                   (closure ? HDR_CLOSURE : 0u) | (hlog2 << 8);
     if (closure) {
         uint32_t* cf = arena + h - CB_WORDS;
-        for (uint32_t i = 0; i < CB_WORDS; ++i) cf[i] = seq ? NONE32 : 0u;
+        for (uint32_t i = 0; i < CF_WORDS; ++i) cf[i] = seq ? NONE32 : 0u;
+        for (uint32_t i = CF_WORDS; i < CB_WORDS; ++i) cf[i] = NONE32;   // signatures: sig_pass
         if (!seq)
             for (uint64_t i = 0; i < n_stored; ++i) {
                 const uint32_t v = edges[i];
@@ -1932,10 +1984,10 @@ __global__ void __launch_bounds__(256) closure_pass(uint32_t* __restrict__ arena
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = (uint64_t)rows[i] * HDR_WORDS;
-    uint4* const cf = reinterpret_cast<uint4*>(arena + h - CB_WORDS);
-    uint4 acc[CB_WORDS / 4];
+    uint2* const cf = reinterpret_cast<uint2*>(arena + h - CB_WORDS);
+    uint2 acc[CF_WORDS / 2];
 #pragma unroll
-    for (int k = 0; k < (int)(CB_WORDS / 4); ++k) acc[k] = cf[k];
+    for (int k = 0; k < (int)(CF_WORDS / 2); ++k) acc[k] = cf[k];
     uint4 v = *reinterpret_cast<const uint4*>(arena + h);
     uint64_t hc = h;                                   // where the row's edges are (forwards: delta.cpp)
     while (v.z & HDR_FWD) {
@@ -1953,25 +2005,23 @@ __global__ void __launch_bounds__(256) closure_pass(uint32_t* __restrict__ arena
             more = NONE32;
             continue;
         }
-        const uint4* const cc = reinterpret_cast<const uint4*>(arena + ch - CB_WORDS);
+        const uint2* const cc = reinterpret_cast<const uint2*>(arena + ch - CB_WORDS);
 #pragma unroll
-        for (int k = 0; k < (int)(CB_WORDS / 4); ++k) {
-            const uint4 y = cc[k];
+        for (int k = 0; k < (int)(CF_WORDS / 2); ++k) {
+            const uint2 y = cc[k];
             acc[k].x |= y.x;
             acc[k].y |= y.y;
-            acc[k].z |= y.z;
-            acc[k].w |= y.w;
         }
     }
     if (more) {
 #pragma unroll
-        for (int k = 0; k < (int)(CB_WORDS / 4); ++k) acc[k] = make_uint4(NONE32, NONE32, NONE32, NONE32);
+        for (int k = 0; k < (int)(CF_WORDS / 2); ++k) acc[k] = make_uint2(NONE32, NONE32);
     }
     bool diff = false;
 #pragma unroll
-    for (int k = 0; k < (int)(CB_WORDS / 4); ++k) {
-        const uint4 o = cf[k];
-        if (o.x != acc[k].x || o.y != acc[k].y || o.z != acc[k].z || o.w != acc[k].w) {
+    for (int k = 0; k < (int)(CF_WORDS / 2); ++k) {
+        const uint2 o = cf[k];
+        if (o.x != acc[k].x || o.y != acc[k].y) {
             cf[k] = acc[k];
             diff = true;
         }
@@ -1984,7 +2034,36 @@ __global__ void __launch_bounds__(256) closure_fill(uint32_t* __restrict__ arena
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t* const cf = arena + (uint64_t)rows[i] * HDR_WORDS - CB_WORDS;
-    for (uint32_t k = 0; k < CB_WORDS; ++k) cf[k] = NONE32;
+    for (uint32_t k = 0; k < CF_WORDS; ++k) cf[k] = NONE32;
+}
+
+// Child signatures of one closure row (see SIG_WORDS): the 16-bit OR-fold of the closure filter
+// of each subject set in its window, stored transposed.  Runs once the filters are closed.  One
+// lane per row; a forwarded row keeps none (its content is elsewhere, without a filter block).
+__global__ void __launch_bounds__(256) sig_pass(uint32_t* __restrict__ arena, const uint32_t* __restrict__ rows,
+                                               uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = (uint64_t)rows[i] * HDR_WORDS;
+    const uint4 v = *reinterpret_cast<const uint4*>(arena + h);
+    if ((v.z & HDR_FWD) || !(v.z & HDR_CLOSURE)) return;
+    const uint4 win = *reinterpret_cast<const uint4*>(arena + h + HDR_WORDS);
+    const uint32_t n_edges = (v.z & HDR_SEQ) ? v.x : v.x + v.y;
+    uint32_t fold[4];
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t e = k == 0 ? win.x : k == 1 ? win.y : k == 2 ? win.z : win.w;
+        fold[k] = 0xFFFFu;
+        if (k >= n_edges || !(e & EDGE_SET) || e == EDGE_POISON) continue;
+        const uint64_t ch = (uint64_t)(e & EDGE_VAL) * HDR_WORDS;
+        if (!(arena[ch + 2] & HDR_CLOSURE)) continue;           // cannot happen: a set's target has a filter
+        uint32_t f = 0;
+        for (uint32_t w = 0; w < CF_WORDS; ++w) f |= arena[ch - CB_WORDS + w];
+        fold[k] = (f | (f >> 16)) & 0xFFFFu;
+    }
+    uint32_t out[SIG_WORDS] = {0, 0};
+    for (uint32_t b = 0; b < 16; ++b)
+        for (uint32_t k = 0; k < 4; ++k) out[b >> 3] |= ((fold[k] >> b) & 1u) << ((b & 7u) * 4u + k);
+    *reinterpret_cast<uint2*>(arena + h - SIG_WORDS) = make_uint2(out[0], out[1]);
 }
 
 // Close every row's closure filter on the device: rounds of closure_pass over the rows that have
@@ -1998,13 +2077,13 @@ void build_closures(const Snapshot& S, uint32_t* d_arena) {
         all.push_back(S.unit_of_row[r]);
         if (S.rows[r].n_sets > 0 && !(S.row_flags(r) & ROW_SEQ)) list.push_back(S.unit_of_row[r]);
     }
-    if (list.empty()) return;
+    if (all.empty()) return;
     uint32_t *d_rows = nullptr, *d_changed = nullptr;
     HIP_OK(hipMalloc(&d_rows, std::max(list.size(), all.size()) * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_changed, sizeof(uint32_t)));
     HIP_OK(hipMemcpy(d_rows, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     const uint32_t n = (uint32_t)list.size();
-    bool done = false;
+    bool done = list.empty();
     for (int round = 0; round < CLOSURE_MAX_ROUNDS && !done; ++round) {
         HIP_OK(hipMemset(d_changed, 0, sizeof(uint32_t)));
         hipLaunchKernelGGL(closure_pass, dim3((n + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, n, d_changed);
@@ -2019,6 +2098,11 @@ void build_closures(const Snapshot& S, uint32_t* d_arena) {
         hipLaunchKernelGGL(closure_fill, dim3((m + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, m);
         HIP_OK(hipGetLastError());
     }
+    // child signatures of every closure row, from the closed filters
+    HIP_OK(hipMemcpy(d_rows, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const uint32_t m = (uint32_t)all.size();
+    hipLaunchKernelGGL(sig_pass, dim3((m + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, m);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipDeviceSynchronize());
     (void)hipFree(d_rows);
     (void)hipFree(d_changed);
@@ -2186,7 +2270,7 @@ void device_apply(Snapshot& S) {
             if (pl.unit != id && S.row_cb[r]) {               // a forwarded row: re-seed the identity filter
                 Write w;
                 w.word = (uint64_t)id * HDR_WORDS - CB_WORDS;
-                w.img.assign(CB_WORDS, 0);
+                w.img.assign(CF_WORDS, 0);
                 const auto ed = S.row_edges(r);
                 const bool seq = (S.row_flags(r) & ROW_SEQ) != 0;
                 for (auto& x : w.img) x = seq ? NONE32 : 0u;
@@ -2208,7 +2292,7 @@ void device_apply(Snapshot& S) {
             if (S.row_cb[r]) {                                // the identity's filter, re-seeded
                 Write w;
                 w.word = (uint64_t)id * HDR_WORDS - CB_WORDS;
-                w.img.assign(CB_WORDS, 0);
+                w.img.assign(CF_WORDS, 0);
                 const auto ed = S.row_edges(r);
                 const bool seq = (S.row_flags(r) & ROW_SEQ) != 0;
                 for (auto& x : w.img) x = seq ? NONE32 : 0u;
@@ -2480,25 +2564,33 @@ using CheckKernelFn = void (*)(DevSnap, DevOverlay, const keto_check_ids*, uint3
 // tier-0 variants for max-depth <= 5 (4 saved frames): {save windows, LDS visit ids}; then the
 // max-depth <= 9 kernel (8 frames).  KETO_T0 picks a variant (tuning); 0 is the default.
 constexpr int T0_VARIANTS = 4;
+constexpr uint32_t KETO_HEAD_WORDS = 8 * 16 * 32;
 int t0_variant() {
     const char* e = getenv("KETO_T0");
     const int v = e ? atoi(e) : 0;
     return v >= 0 && v < T0_VARIANTS ? v : 0;
 }
 // request runs handed out per grab by the tier-0 wave kernel (TierArgs::dyn) for a batch of n
-// requests over `lanes` lanes: runs of 32 after a static first half (profiles/r01v_dyn_runs_tune.log:
-// 2.73 ms vs 2.90 ms static on the 1B graph), used once every lane has at least 16 requests (with
-// fewer, one static run per lane keeps more lanes busy than runs of 32 would).  KETO_T0_DYN
-// overrides the run size (0 = static runs), KETO_T0_DYN_STATIC the static eighths,
-// KETO_T0_DYN_FORCE=1 drops the batch-size condition (tests).
+// requests over `lanes` lanes: runs of 4 after a static first quarter, dealt by 4 heads per XCD,
+// used once every lane has at least 16 requests (with fewer, one static run per lane keeps more
+// lanes busy).  On the 1B graph a lane holds only ~32 requests of a 16.7M batch, so runs of 32
+// (the round-1 setting: 2.81-3.00 ms) left the launch's tail to a few lanes per wave (37 of 64
+// lanes busy per wave-iteration); runs of 4 keep 56 busy (2.76-2.82 ms, profiles/r02m_dyn_heads.log,
+// r02q_tune_sigs.log).  KETO_T0_DYN overrides the run size (0 = static runs), KETO_T0_DYN_STATIC
+// the static eighths, KETO_T0_HEADS the heads per XCD, KETO_T0_DYN_FORCE=1 drops the batch-size
+// condition (tests).
 uint32_t t0_dyn(uint64_t n, uint64_t lanes) {
     const char* e = getenv("KETO_T0_DYN");
     const char* f = getenv("KETO_T0_DYN_STATIC");       // eighths of a range handed out statically
     const char* force = getenv("KETO_T0_DYN_FORCE");
     if (!(force && atoi(force) == 1) && n < 16 * lanes) return 0u;
-    const int v = e ? atoi(e) : 32;
-    const int st = f ? std::min(7, std::max(0, atoi(f))) : 4;
-    return v > 0 ? (std::min<uint32_t>((uint32_t)v + 3u, 0xFFFCu) & ~3u) | ((uint32_t)st << 16) : 0u;
+    const char* hs = getenv("KETO_T0_HEADS");          // heads per XCD (a power of two, <= 16)
+    const int v = e ? atoi(e) : 4;
+    const int st = f ? std::min(7, std::max(0, atoi(f))) : 2;
+    const int heads = hs ? std::min(16, atoi(hs)) : 4;
+    uint32_t hl2 = 0;
+    while ((1 << (hl2 + 1)) <= heads) ++hl2;
+    return v > 0 ? (std::min<uint32_t>((uint32_t)v + 3u, 0xFFFCu) & ~3u) | ((uint32_t)st << 16) | (hl2 << 20) : 0u;
 }
 const char* t0_kernel_name(int var) {
     switch (var) {
@@ -2618,9 +2710,9 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
     unsigned long long* dwork = nullptr;
     if (work_out) {
         uint64_t acc = 0;
-        dwork = dmalloc<unsigned long long>(KETO_WORK_SLOTS, acc);
+        dwork = dmalloc<unsigned long long>(2 * KETO_WORK_SLOTS, acc);   // + the SIMT profile
         tmp.p.push_back(dwork);
-        HIP_OK(hipMemsetAsync(dwork, 0, KETO_WORK_SLOTS * sizeof(unsigned long long), st));
+        HIP_OK(hipMemsetAsync(dwork, 0, 2 * KETO_WORK_SLOTS * sizeof(unsigned long long), st));
         if (d_steps) HIP_OK(hipMemsetAsync(d_steps, 0, (uint64_t)n * sizeof(uint32_t), st));
     }
     run_tiers(D, D.tiers, n, p, st,
@@ -2644,12 +2736,14 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                   const bool local = p.frames[level] == 0;
                   if (level == 0 && kind < 2) {
                       a.dyn = t0_dyn(n, slots);
+                      if (const char* wc = getenv("KETO_T0_WALK"))
+                          if (atoi(wc) > 0) a.walk_cap = (uint32_t)atoi(wc);
                       if (a.dyn) {
                           if (!D.heads) {
                               uint64_t acc = 0;
-                              D.heads = dmalloc<uint32_t>(8 * 32, acc);
+                              D.heads = dmalloc<uint32_t>(KETO_HEAD_WORDS, acc);
                           }
-                          HIP_OK(hipMemsetAsync(D.heads, 0, 8 * 32 * sizeof(uint32_t), st));
+                          HIP_OK(hipMemsetAsync(D.heads, 0, KETO_HEAD_WORDS * sizeof(uint32_t), st));
                           a.heads = D.heads;
                       }
                       go(t0_kernel(var, dwork != nullptr));
@@ -2663,9 +2757,9 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                       if (a.dyn) {
                           if (!D.heads) {
                               uint64_t acc = 0;
-                              D.heads = dmalloc<uint32_t>(8 * 32, acc);
+                              D.heads = dmalloc<uint32_t>(KETO_HEAD_WORDS, acc);
                           }
-                          HIP_OK(hipMemsetAsync(D.heads, 0, 8 * 32 * sizeof(uint32_t), st));
+                          HIP_OK(hipMemsetAsync(D.heads, 0, KETO_HEAD_WORDS * sizeof(uint32_t), st));
                           a.heads = D.heads;
                       }
                       dwork ? go(deep_wave_kernel<8, 8, true>) : go(deep_wave_kernel<8, 8, false>);
@@ -2682,10 +2776,13 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
               },
               Undecided{da, nullptr, (uint8_t)KETO_UNDECIDED}, accumulate);
     if (work_out) {
-        unsigned long long h[KETO_WORK_SLOTS];
+        unsigned long long h[2 * KETO_WORK_SLOTS];
         HIP_OK(hipMemcpyAsync(h, dwork, sizeof(h), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         for (int i = 0; i < KETO_WORK_SLOTS; ++i) work_out[i] = h[i];
+        if (getenv("KETO_SIMT_PROF"))       // tier-0 SIMT profile (tooling): wave / lane counts
+            fprintf(stderr, "simt: iter %llu/%llu work %llu/%llu walk %llu/%llu enter %llu/%llu\n", h[16], h[17],
+                    h[18], h[19], h[20], h[21], h[22], h[23]);
     }
 }
 

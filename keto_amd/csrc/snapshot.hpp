@@ -45,7 +45,8 @@ constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys l
 // Device arena (one u32 array per device).  Row r occupies
 //   [subject-id table, 2^hlog2 words of 16-B buckets, for rows whose ids do not all fit in the
 //    window (n_ids > 0 and n_sets + n_ids > WINDOW_WORDS)]
-//   [closure filter, CB_WORDS words, only for rows some subject set points at (HDR_CLOSURE)]
+//   [closure filter (CF_WORDS) + child signatures (SIG_WORDS): CB_WORDS words, only for rows
+//    some subject set points at (HDR_CLOSURE)]
 //   [16-B header: n_sets, n_ids, flags | hlog2 << 8 | bloom, bloom]   <- handle = word / 4
 //   [edges in ORDER BY order; subject sets hold the target's handle]  padded to 16 B
 // A row visit reads the header and the window (the first 4 edge words) -- and, entering a subject
@@ -72,19 +73,30 @@ constexpr uint32_t HDR_CLOSURE = 8u;            // a closure filter precedes the
 // arena's tail; its identity header (whose handle every subject set holds, and whose closure filter
 // stays in front of it) becomes a forward: word 0 = handle of the row's current header.
 constexpr uint32_t HDR_FWD = 16u;
-// Closure filter of a row some subject set points at: a 768-bit, one-hash bloom filter of every
+// Closure filter of a row some subject set points at: a 704-bit, one-hash bloom filter of every
 // subject id reachable from the row through any number of subject sets (its own ids included).  A
 // check entering such a row for a requested id the filter rules out skips the row: every node the
 // skipped search would have marked visited lies inside that closure, which never reaches the
 // requested id, so no answer changes (rows whose closure holds a colliding visit key, ROW_SEQ,
 // have all bits set).  Built on the device at upload (closure_pass).
-constexpr uint32_t CB_WORDS = 24;
+//
+// Child signatures (the last SIG_WORDS words in front of a closure row's header): for each of the
+// row's 4 window slots, the 16-bit OR-fold of the closure filter of the subject set in that slot
+// (fold bit b = some filter bit p with p % 16 == b is set; all ones for a slot holding no subject
+// set).  T sits at filter bit p, so fold bit p % 16 clear means the child's own filter rules T out:
+// a walk inside this row skips that child without loading its line, exactly as the child's filter
+// word would have.  Stored transposed so one word serves all 4 slots: word (b >> 3) bit
+// ((b & 7) * 4 + slot) = fold bit b of that slot.  Built on the device after the filters are
+// closed (sig_pass); all ones until then (no skip).
+constexpr uint32_t CF_WORDS = 22;               // closure filter: 704 bits
+constexpr uint32_t SIG_WORDS = 2;
+constexpr uint32_t CB_WORDS = CF_WORDS + SIG_WORDS;   // in front of a closure row's header
 KETO_HD inline void closure_bit(uint32_t id, uint32_t& word, uint32_t& bit) {
     uint32_t h = id * 0x85EBCA77u + 0x165667B1u;
     h ^= h >> 13;
     h *= 0xC2B2AE3Du;
     h ^= h >> 16;
-    const uint32_t p = (uint32_t)(((uint64_t)h * (CB_WORDS * 32u)) >> 32);
+    const uint32_t p = (uint32_t)(((uint64_t)h * (CF_WORDS * 32u)) >> 32);
     word = p >> 5;
     bit = p & 31u;
 }

@@ -213,22 +213,39 @@ def test_segment1_expand_matches_oracle(powerlaw_seg1):
     _expand_matches_oracle(*powerlaw_seg1)
 
 
-@pytest.mark.parametrize("dyn,static8,gmd", [("32", "4", 5), ("4", "0", 5), ("16", "7", 8), ("100", "2", 5),
-                                              ("0", "4", 5)])
-def test_powerlaw_dynamic_runs_match_oracle(powerlaw, monkeypatch, dyn, static8, gmd):
+@pytest.mark.parametrize("dyn,static8,gmd,heads", [("32", "4", 5, "1"), ("4", "0", 5, "4"), ("16", "7", 8, "16"),
+                                                    ("100", "2", 5, "2"), ("0", "4", 5, "4"), ("4", "2", 5, "4"),
+                                                    ("4", "2", 8, "8")])
+def test_powerlaw_dynamic_runs_match_oracle(powerlaw, monkeypatch, dyn, static8, gmd, heads):
     """Tier 0 with dynamic per-XCD request runs (TierArgs::dyn; forced on a batch far below the
     16-requests-per-lane threshold, so most lanes grab runs, several lanes find their XCD's range
     exhausted and a run ends at the batch end; grids of 4 and 20 workgroups split the batch into
-    fewer or uneven XCD ranges): every decision equals the oracle's.  Batch sizes
+    fewer or uneven XCD ranges; 1-16 heads per XCD deal the runs out interleaved, so waves move on
+    to other heads once theirs is dealt out): every decision equals the oracle's.  Batch sizes
     that are not multiples of 4 exercise the byte-wise decision stores of a run's last group."""
     g, snap = powerlaw
     monkeypatch.setenv("KETO_T0_DYN_FORCE", "1")
     monkeypatch.setenv("KETO_T0_DYN", dyn)
     monkeypatch.setenv("KETO_T0_DYN_STATIC", static8)
+    monkeypatch.setenv("KETO_T0_HEADS", heads)
     for n, seed in ((300_001, 70), (1_003, 71), (5_001, 72)):
         q = g.queries(n, seed=seed + gmd, depth=gmd)
         rng = np.random.default_rng(seed)
         q["max_depth"] = rng.integers(-1, gmd + 2, size=len(q))
+        gpu = _gpu_check(snap, snap.with_handles(q), gmd)
+        tab = g.oracle_table(q, gmd)
+        ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
+        assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+
+
+@pytest.mark.parametrize("cap", ["1", "3"])
+def test_powerlaw_walk_cap_matches_oracle(powerlaw, monkeypatch, cap):
+    """Tier 0 walking at most `cap` window edges / pops per loop iteration (KETO_T0_WALK; a lane
+    stopped early goes on next iteration without a global access): decisions equal the oracle's."""
+    g, snap = powerlaw
+    monkeypatch.setenv("KETO_T0_WALK", cap)
+    for gmd in (5, 8):
+        q = g.queries(100_003, seed=80 + gmd, depth=gmd)
         gpu = _gpu_check(snap, snap.with_handles(q), gmd)
         tab = g.oracle_table(q, gmd)
         ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)

@@ -3,7 +3,8 @@ KETO_T0 variant on the same resident batch, checks that all variants agree bit f
 the work / line-touch counters of each.
 
   python tools/tune.py [--scale 1.0] [--batch 16777216] [--depth 5] [--variants 0,1,2,3] [--reps 3]
-  (a variant may carry a dynamic run size: --variants 0:0,0:16 sets KETO_T0_DYN)
+  (a variant may carry a dynamic run size, static share and heads per XCD: --variants 0:0,0:16:4:8
+  sets KETO_T0_DYN, KETO_T0_DYN_STATIC, KETO_T0_HEADS)
 """
 import argparse
 import json
@@ -45,12 +46,16 @@ def main():
     ref = None
     print(f"graph: {g.n_edges} tuples, {g.n_rows} rows", flush=True)
     for tok in a.variants.split(","):
-        # "variant[:run size[:static eighths]]" (KETO_T0_DYN, KETO_T0_DYN_STATIC; run size 0 = static runs)
-        v, dyn, st = (tok.split(":") + ["", ""])[:3]
+        # "variant[:run size[:static eighths[:heads per XCD[:walk cap]]]]" (KETO_T0_DYN,
+        # KETO_T0_DYN_STATIC, KETO_T0_HEADS, KETO_T0_WALK; run size 0 = static runs; empty = default)
+        v, dyn, st, hd, wc = (tok.split(":") + ["", "", "", ""])[:5]
         v = int(v)
         os.environ["KETO_T0"] = str(v)
-        os.environ["KETO_T0_DYN"] = dyn or "0"
-        os.environ["KETO_T0_DYN_STATIC"] = st or "4"
+        for k, x in (("KETO_T0_DYN", dyn), ("KETO_T0_DYN_STATIC", st), ("KETO_T0_HEADS", hd), ("KETO_T0_WALK", wc)):
+            if x:
+                os.environ[k] = x
+            else:
+                os.environ.pop(k, None)            # the engine's default
         snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
         torch.cuda.synchronize()
         ms = []
