@@ -479,6 +479,34 @@ class Snapshot:
             self.lib.keto_tree_arena_free(a)
         return status, offs, nodes
 
+    def expand_batch_ids_proto(self, roots: np.ndarray, depths: np.ndarray, global_max_depth=5):
+        """Pre-resolved roots -> every tree's SubjectTree proto in one buffer (keto_tree_proto_all).
+        Returns (status[n], offsets[n+1] into the blob, blob, expand seconds, encode seconds)."""
+        import time
+        roots = np.ascontiguousarray(roots, dtype=np.uint32)
+        depths = np.ascontiguousarray(depths, dtype=np.int32)
+        n = len(roots)
+        a = C.c_void_p()
+        t0 = time.perf_counter()
+        _check(self.lib.keto_expand_batch_ids(self.h, roots.ctypes.data_as(C.c_void_p),
+                                              depths.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                              C.c_int32(global_max_depth), C.byref(a)))
+        t1 = time.perf_counter()
+        try:
+            offs = np.zeros(n + 1, dtype=np.uint64)
+            total = self.lib.keto_tree_proto_all(self.h, a, None, C.c_uint64(0), offs.ctypes.data_as(C.c_void_p))
+            _check(min(0, total))
+            t2 = time.perf_counter()
+            blob = np.zeros(max(1, total), dtype=np.uint8)
+            got = self.lib.keto_tree_proto_all(self.h, a, blob.ctypes.data_as(C.c_void_p), C.c_uint64(total),
+                                               offs.ctypes.data_as(C.c_void_p))
+            t3 = time.perf_counter()
+            assert got == total
+            status = np.array([self.lib.keto_tree_status(a, C.c_uint32(i)) for i in range(n)], dtype=np.int32)
+        finally:
+            self.lib.keto_tree_arena_free(a)
+        return status, offs, blob[:total].tobytes(), t1 - t0, min(t2 - t1, t3 - t2)
+
     def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False):
         """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes][, proto])."""
         keep = _Keep()

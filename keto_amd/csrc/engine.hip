@@ -3105,6 +3105,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
     ExpandOut o{nullptr, nullptr, dcount, dstatus};
+    // (the batch timing sums both passes' tiers: keto_last_batch_timing after an expand)
     auto launch_pass = [&](bool fill, const ExpandOut& eo) {
         run_tiers(D, D.etiers, n, p, st,
                   [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
@@ -3127,7 +3128,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                                              gmd, eo, a);
                       HIP_OK(hipGetLastError());
                   },
-                  Undecided{dstatus, fill ? nullptr : dcount, (uint8_t)EXP_OVERFLOW});
+                  Undecided{dstatus, fill ? nullptr : dcount, (uint8_t)EXP_OVERFLOW}, fill);
     };
     // count pass, exclusive scan on the host, fill pass (same tier plan: a root overflows on the
     // same tiers both times, and a partial pre-order is a prefix of the full one)

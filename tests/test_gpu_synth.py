@@ -153,6 +153,41 @@ def test_powerlaw_expand_matches_oracle(powerlaw):
     _expand_matches_oracle(*powerlaw)
 
 
+def test_powerlaw_proto_all_equals_per_tree(powerlaw):
+    """keto_tree_proto_all (every tree of an arena encoded on host threads into one buffer) gives
+    byte for byte the per-tree keto_tree_proto encodings, at the offsets it reports; nil trees
+    (rows with no tuples) are empty; the sizing call writes nothing."""
+    g, snap = powerlaw
+    rng = np.random.default_rng(9)
+    n = 2000
+    rows = rng.integers(0, g.n_rows, size=n).astype(np.uint32) | np.uint32(0x80000000)
+    depths = rng.integers(0, 5, size=n).astype(np.int32)
+    lib = snap.lib
+    a = C.c_void_p()
+    assert lib.keto_expand_batch_ids(snap.h, rows.ctypes.data_as(C.c_void_p), depths.ctypes.data_as(C.c_void_p),
+                                     C.c_uint32(n), C.c_int32(5), C.byref(a)) == 0
+    try:
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        total = lib.keto_tree_proto_all(snap.h, a, None, C.c_uint64(0), offs.ctypes.data_as(C.c_void_p))
+        assert total == int(offs[-1]) > 0
+        blob = C.create_string_buffer(total)
+        assert lib.keto_tree_proto_all(snap.h, a, blob, C.c_uint64(total), offs.ctypes.data_as(C.c_void_p)) == total
+        nil = 0
+        for i in range(n):
+            pn = lib.keto_tree_proto(snap.h, a, C.c_uint32(i), None, C.c_uint64(0))
+            one = b""
+            if pn > 0:
+                buf = C.create_string_buffer(pn)
+                lib.keto_tree_proto(snap.h, a, C.c_uint32(i), buf, C.c_uint64(pn))
+                one = buf.raw[:pn]
+            else:
+                nil += 1
+            assert blob.raw[int(offs[i]):int(offs[i + 1])] == one, i
+        assert nil < n
+    finally:
+        lib.keto_tree_arena_free(a)
+
+
 def _expand_matches_oracle(g, snap):
     rng = np.random.default_rng(5)
     rows = rng.integers(0, g.n_rows, size=300).astype(np.uint32)

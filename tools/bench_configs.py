@@ -13,8 +13,9 @@ restatement timed on the same sample and host cores.
   #3 nested groups: chains of up to 32 nested groups with back-edges (cycles), 100M tuples,
      1,000,000 checks with request depths {5, 16, 32}, global max-depth 32.
   #5 expand: 100,000 roots sampled from #3's rows, global max-depth 5; trees/s for count + fill
-     passes; a sample of trees compared node by node (pre-order, child order included) with the
-     oracle.
+     passes, the roofline of both passes' kernels (SURVEY 8(d) B_expand), every tree encoded as an
+     acl.SubjectTree protobuf (keto_tree_proto_all), and 5,000 trees compared node by node
+     (pre-order, child order included) with the oracle.
 
   python tools/bench_configs.py [--configs 1,2,3,5] [--threads 16]
 """
@@ -170,6 +171,23 @@ def config3(a):
     return checks_config(a, "#3 nested groups (chains <= 32, cycles)", g, q, 32, 20_000, reps=1, price=2000), g
 
 
+def expand_bytes(g, tree):
+    """SURVEY.md 8(d) B_expand of one tree: 12 + sum over the rows it expands (8 + 4 deg) + 9 per
+    tree node.  A set node is an expanded row when it has children or is an empty row.  `tree` is
+    the engine's node list of a tree found identical to the oracle's: (subject, info) with set
+    subjects as bit31 | row id."""
+    deg = np.diff(g.row_ptr)
+    b = 12 + 9 * len(tree)
+    for subj, info in tree:
+        if not (int(subj) >> 31):
+            continue
+        r = int(subj) & 0x7FFFFFFF
+        leaf, nc = int(info) >> 31, int(info) & 0x7FFFFFFF
+        if nc > 0 or (leaf and deg[r] == 0):
+            b += 8 + 4 * int(deg[r])
+    return b
+
+
 def config5(a, g=None):
     from tools import synth
     from keto_amd.capi import load
@@ -182,7 +200,7 @@ def config5(a, g=None):
     roots = rows | np.uint32(0x80000000)
     depths = np.zeros(n, dtype=np.int32)          # request depth 0 -> global max-depth 5
     lib = load()
-    best = None
+    best, kern = None, None
     for _ in range(3):
         arena = C.c_void_p()
         t0 = time.perf_counter()
@@ -191,20 +209,26 @@ def config5(a, g=None):
         dt = time.perf_counter() - t0
         assert rc == 0
         lib.keto_tree_arena_free(arena)
-        best = dt if best is None else min(best, dt)
-    # node-by-node comparison of a sample of trees with the oracle
+        ms, _ = snap.last_timing()
+        if best is None or dt < best:
+            best, kern = dt, sum(ms)
+    # every tree as a SubjectTree proto (keto_tree_proto_all, host threads)
+    _st, poffs, blob, _te, t_proto = snap.expand_batch_ids_proto(roots, depths, 5)
+    # node-by-node comparison of a sample of trees with the oracle (pre-order, child order included)
     from tests.test_gpu_synth import _oracle_expand_nodes
-    k = 300
+    k = a.expand_sample
     status, offs, nodes = snap.expand_batch_ids(roots[:k], depths[:k], 5)
     q = np.zeros(k, dtype=[("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
     q["row"] = rows[:k]
     tab = g.oracle_table(q, 5)
     bad = 0
     n_nodes = 0
+    bytes_ = []
     for i in range(k):
         r, want = _oracle_expand_nodes(g, tab, int(rows[i]), 5, 5)
         if r == 0:
             bad += int(status[i] != 1)
+            bytes_.append(12 + 8)
             continue
         have = []
         for subj, info in nodes[offs[i]:offs[i + 1]]:
@@ -216,9 +240,23 @@ def config5(a, g=None):
                 have.append((leaf, 0, int(subj), 0, 0, 0, nc))
         n_nodes += len(have)
         bad += int(have != want or status[i] != 0)
+        if have == want:
+            bytes_.append(expand_bytes(g, nodes[offs[i]:offs[i + 1]]))
+    per = float(np.mean(bytes_))
+    ach = per * n / (kern * 1e-3) / 1e9
     return {"config": "#5 expand (100k roots on the #3 graph, max-depth 5)", "tuples": int(g.n_edges), "roots": n,
             "gpu": {"trees_per_s": round(n / best, 1), "wall_ms": round(best * 1e3, 3),
-                    "what": "keto_expand_batch_ids: H2D roots, count pass, host scan, fill pass, D2H tree arena"},
+                    "kernel_ms": round(kern, 3),
+                    "what": "keto_expand_batch_ids: H2D roots, count pass, host scan, fill pass, D2H tree arena; "
+                            "kernel_ms = both passes' tier kernels (HIP events)"},
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern, 3),
+                         "alg_bytes_per_root": round(per, 1),
+                         "alg_bytes_sample": f"SURVEY 8(d) B_expand over the first {k} roots' trees (those equal "
+                                             "to the oracle's)"},
+            "proto": {"trees_per_s": round(n / t_proto, 1), "bytes": len(blob), "encode_ms": round(t_proto * 1e3, 3),
+                      "MB_per_s": round(len(blob) / t_proto / 1e6, 1),
+                      "what": "keto_tree_proto_all: every tree of the arena as acl.SubjectTree protobuf, 16 host threads"},
             "parity": {"sample_trees": k, "sample_nodes": n_nodes, "mismatched_trees": bad}}
 
 
@@ -228,6 +266,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--work", action="store_true", help="add per-check traversal counters (instrumented run)")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle legs (tuning sweeps)")
+    ap.add_argument("--expand-sample", type=int, default=5000, help="config #5 trees compared with the oracle")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
