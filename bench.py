@@ -4,8 +4,8 @@
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 the driver starts one
 rank per GPU with torch.distributed.run.  A step = one keto_check_batch_device call over a
 resident batch of synthetic docs:d#view@u requests (16M per GPU by default).  The path shards by
-request with no data-path collective: every rank holds the whole snapshot (the 1B-tuple CSR is
-~6.4 GB of a 288 GB HBM3E) and checks its own batch ("weak" scaling).  Rank 0 prints one JSON line.
+request with no data-path collective: every rank holds the whole snapshot (the 1B-tuple arena is
+17.2 GiB of a 288 GB HBM3E) and checks its own batch ("weak" scaling).  Rank 0 prints one JSON line.
 
 Extras on the same line:
   roofline      SURVEY.md 8(d) algorithmic bytes of the dominant kernel (the tier-0 check kernel)
@@ -15,9 +15,14 @@ Extras on the same line:
                 launch stream); peak = 8 TB/s HBM3E.  `traffic` = HBM bytes per launch from the
                 committed rocprofv3 PMC passes of this same engine build (profiles/*_traffic.json);
                 `traversal_bytes_per_launch` = what the kernel's own traversal requests.
+  end_to_end    SURVEY.md 8(d) t_batch: host entry to decisions on the host (pinned 8-B row-id
+                requests -> H2D -> translation -> check -> D2H, chunks pipelined by the library),
+                and its frac; the 16-B row-id form alongside.
   cpu_baseline  the C restatement of the reference engine (oracle/keto_oracle.c) on the box's host
                 cores over a bounded sample of the same requests; its decisions are also compared
                 with the GPU's for that sample ("parity").
+  ref_sql       the reference recursion issuing its own SQL against in-memory SQLite, one worker
+                process per core, over the first 10,000 requests (compared with the GPU too).
 """
 import argparse
 import json

@@ -110,10 +110,47 @@ type Row struct {
 	SetRelation    string
 }
 
-// Snapshot is an immutable, device-resident CSR snapshot of the tuple table.
+// Snapshot is a device-resident snapshot of the tuple table, patched in place by Apply.
 type Snapshot struct {
 	h       *C.keto_snapshot
 	Version uint64 // bumped by every Apply (snapshot lifecycle, see apply.go)
+}
+
+// rowsLen is the string bytes of rows (one arena per call).
+func rowsLen(rows []Row) int {
+	total := 0
+	for i := range rows {
+		r := &rows[i]
+		total += len(r.Object) + len(r.Relation) + len(r.SetObject) + len(r.SetRelation)
+		if r.SubjectID != nil {
+			total += len(*r.SubjectID)
+		}
+	}
+	return total
+}
+
+// tuples copies rows into C memory as keto_tuple structs (nil for none).
+func (m *cmem) tuples(rows []Row) *C.keto_tuple {
+	if len(rows) == 0 {
+		return nil
+	}
+	ct := (*C.keto_tuple)(m.alloc(len(rows) * int(C.sizeof_keto_tuple)))
+	s := unsafe.Slice(ct, len(rows))
+	for i := range rows {
+		r := &rows[i]
+		t := C.keto_tuple{namespace_id: C.int32_t(r.NamespaceID), object: m.s(r.Object), relation: m.s(r.Relation)}
+		if r.SubjectID != nil {
+			t.subject_kind = 0
+			t.subject_id = m.s(*r.SubjectID)
+		} else {
+			t.subject_kind = 1
+			t.set_namespace_id = C.int32_t(r.SetNamespaceID)
+			t.set_object = m.s(r.SetObject)
+			t.set_relation = m.s(r.SetRelation)
+		}
+		s[i] = t
+	}
+	return ct
 }
 
 // Build sorts the rows with the reference ORDER BY (relationtuples.go:250) and uploads the
@@ -121,16 +158,9 @@ type Snapshot struct {
 func Build(nss []*namespace.Namespace, rows []Row, device int) (*Snapshot, error) {
 	var m cmem
 	defer m.free()
-	total := 0
+	total := rowsLen(rows)
 	for _, n := range nss {
 		total += len(n.Name)
-	}
-	for i := range rows {
-		r := &rows[i]
-		total += len(r.Object) + len(r.Relation) + len(r.SetObject) + len(r.SetRelation)
-		if r.SubjectID != nil {
-			total += len(*r.SubjectID)
-		}
 	}
 	m.strings(total)
 	var cns *C.keto_namespace
@@ -141,25 +171,7 @@ func Build(nss []*namespace.Namespace, rows []Row, device int) (*Snapshot, error
 			s[i] = C.keto_namespace{id: C.int32_t(n.ID), name: m.s(n.Name)}
 		}
 	}
-	var ct *C.keto_tuple
-	if len(rows) > 0 {
-		ct = (*C.keto_tuple)(m.alloc(len(rows) * int(C.sizeof_keto_tuple)))
-		s := unsafe.Slice(ct, len(rows))
-		for i := range rows {
-			r := &rows[i]
-			t := C.keto_tuple{namespace_id: C.int32_t(r.NamespaceID), object: m.s(r.Object), relation: m.s(r.Relation)}
-			if r.SubjectID != nil {
-				t.subject_kind = 0
-				t.subject_id = m.s(*r.SubjectID)
-			} else {
-				t.subject_kind = 1
-				t.set_namespace_id = C.int32_t(r.SetNamespaceID)
-				t.set_object = m.s(r.SetObject)
-				t.set_relation = m.s(r.SetRelation)
-			}
-			s[i] = t
-		}
-	}
+	ct := m.tuples(rows)
 	opts := C.keto_snapshot_opts{page_size: 100, device: C.int32_t(device)}
 	var h *C.keto_snapshot
 	if rc := C.keto_snapshot_build(cns, C.uint32_t(len(nss)), ct, C.uint64_t(len(rows)), &opts, &h); rc != C.KETO_OK {
