@@ -1656,8 +1656,11 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     V.fresh();
     Work<false> nw;
     V.test_add(root_vid, nw);                               // :40-43 (root marked too)
+    // the current frame lives in registers; a parent is saved on the stack only while it still
+    // has edges (a child whose parent is exhausted returns straight to the grandparent)
     int sp = 0;
-    // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union pushed
+    Frame cur{0, 0, 0, 0};
+    // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union entered
     auto open = [&](uint32_t h, int k) -> int {
         const RowView rv = load_row(s, ov, h);
         const uint32_t n_all = rv.n_sets + rv.n_ids;
@@ -1668,35 +1671,49 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             return EXP_TREE;
         }
         if (rv.poison) return EXP_ERROR;                    // a later page fails
-        if (sp == st.cap()) return EXP_OVERFLOW;
+        if (cur.left > 0) {
+            if (sp == st.cap()) return EXP_OVERFLOW;
+            st[sp] = cur;
+            ++sp;
+        }
         emit(out, cnt, FILL, EDGE_SET | h, n_all);
-        st[sp] = Frame{rv.beg, n_all, (uint16_t)k,
-                       (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
-        ++sp;
+        cur = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
         return EXP_TREE;
     };
     int r0 = open(root, d);
     if (r0 != EXP_TREE) return r0;
-    while (sp > 0) {
-        Frame& f = st[sp - 1];
-        if (f.left == 0) {
+    for (;;) {
+        if (cur.left == 0) {
+            if (sp == 0) break;
             --sp;
+            cur = st[sp];
             continue;
         }
-        const uint32_t e = (f.fl & FR_OV) ? ov.arena[f.pos] : s.arena[f.pos];
-        f.pos++;
-        f.left--;
+        const uint32_t* const a = (cur.fl & FR_OV) ? ov.arena : s.arena;
+        const uint32_t e = a[cur.pos];
+        if (!(e & EDGE_SET) && !(cur.fl & FR_SEQ)) {
+            // a normal row keeps its subject sets first: every edge left is a subject id, and each
+            // is a leaf (:97-101) -- counted at once, copied in one pass
+            if constexpr (FILL) {
+                for (uint32_t i = 0; i < cur.left; ++i) out[cnt + i] = keto_tree_node{a[cur.pos + i], 0x80000000u};
+            }
+            cnt += cur.left;
+            cur.left = 0;
+            continue;
+        }
+        cur.pos++;
+        cur.left--;
         if (!(e & EDGE_SET)) {
             emit(out, cnt, FILL, e, 0x80000000u);          // subject id child -> Leaf
             continue;
         }
         const uint32_t c = e & EDGE_VAL;
         uint32_t vid = c;
-        if (f.fl & FR_SEQ) {
+        if (cur.fl & FR_SEQ) {
             uint32_t cv = coll_lookup(s, e);
             if (cv != NONE32) vid = cv;
         }
-        const uint16_t k = f.k - 1;
+        const uint16_t k = cur.k - 1;
         int t = V.test_add(vid, nw);
         if (t == 2) return EXP_OVERFLOW;
         if (t == 1) {                                       // visited -> nil -> Leaf(set)
