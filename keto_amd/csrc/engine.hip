@@ -2891,6 +2891,12 @@ uint64_t chunk_requests() {
     const long long v = e ? atoll(e) : (4ll << 20);
     return (uint64_t)std::max<long long>(256, v);
 }
+// the first chunk of a host batch: shorter, so the check starts after a shorter copy
+uint64_t first_chunk_requests(uint64_t C) {
+    const char* e = getenv("KETO_CHUNK_FIRST");         // tuning / tests
+    const long long v = e ? atoll(e) : (long long)C;
+    return (uint64_t)std::min<long long>((long long)C, std::max<long long>(256, v));
+}
 
 }  // namespace
 
@@ -2924,7 +2930,8 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     if (n == 0) return;
     OverlayBuf ov(S, ovh);
     const uint64_t C = std::min<uint64_t>(n, chunk_requests());
-    const uint32_t chunks = (uint32_t)((n + C - 1) / C);
+    const uint64_t C0 = first_chunk_requests(C);        // chunk 0; then chunks of C
+    const uint32_t chunks = 1u + (uint32_t)((n - std::min<uint64_t>(n, C0) + C - 1) / C);
     uint64_t acc = 0;
     if (D.slot_cap < C) {
         for (int i = 0; i < 2; ++i) {
@@ -2963,8 +2970,8 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     hipEvent_t* out_done = D.pev + 4;
     uint32_t* d_bad = D.counters + 4;
     HIP_OK(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), D.stream));
-    auto lo = [&](uint32_t c) { return (uint64_t)c * C; };
-    auto len = [&](uint32_t c) { return (uint32_t)(std::min<uint64_t>(n, lo(c) + C) - lo(c)); };
+    auto lo = [&](uint32_t c) { return c == 0 ? 0 : std::min<uint64_t>(n, C0 + (uint64_t)(c - 1) * C); };
+    auto len = [&](uint32_t c) { return (uint32_t)(std::min<uint64_t>(n, c == 0 ? C0 : lo(c) + C) - lo(c)); };
     // stage chunk c's requests and enqueue its H2D into slot c % 2 (slot reuse waits for chunk
     // c - 2's check, which read it, through kern_done)
     auto put = [&](uint32_t c) {

@@ -32,14 +32,19 @@ def _oracle(g, q, gmd):
     return tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
 
 
-@pytest.mark.parametrize("chunk,pinned", [(1000, False), (1000, True), (4096, True), (1, False), (0, False)])
-def test_rows_pipeline_matches_oracle(graph, monkeypatch, chunk, pinned):
+@pytest.mark.parametrize("chunk,pinned,first", [(1000, False, 0), (1000, True, 0), (4096, True, 0), (1, False, 0),
+                                                (0, False, 0), (1000, True, 300), (4096, False, 5000)])
+def test_rows_pipeline_matches_oracle(graph, monkeypatch, chunk, pinned, first):
+    """The pipelined host path (chunks of KETO_CHUNK after a first chunk of KETO_CHUNK_FIRST)
+    decides like the oracle and reports its chunk count."""
     from keto_amd.capi import CHECK_IDS_DTYPE, HostBuffer
     g, snap = graph
     n = 10_007 if chunk != 1 else 700
     q = g.queries(n, seed=chunk + 3, depth=5)
     if chunk:
         monkeypatch.setenv("KETO_CHUNK", str(chunk))
+    if first:
+        monkeypatch.setenv("KETO_CHUNK_FIRST", str(first))
     if pinned:
         hq, ho = HostBuffer(n, CHECK_IDS_DTYPE), HostBuffer(n, np.uint8)
         hq.array[:] = q
@@ -47,7 +52,9 @@ def test_rows_pipeline_matches_oracle(graph, monkeypatch, chunk, pinned):
     else:
         out = snap.check_batch_rows(q, 5)
     t = snap.last_timing_full()
-    want_chunks = 1 if not chunk else -(-n // max(chunk, 256))
+    c = max(chunk, 256) if chunk else 4 << 20
+    c0 = min(c, max(first, 256)) if first else c
+    want_chunks = 1 + -(-(n - min(n, c0)) // c)
     assert t["chunks"] == want_chunks and t["requests"][0] == n, t
     ref = _oracle(g, q, 5)
     assert (out == ref).all(), f"{int((out != ref).sum())} mismatches of {n}"
