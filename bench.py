@@ -190,9 +190,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL; KETO_BENCH_BACKEND=gloo (rehearsal: several ranks sharing the
+    # GPUs of a smaller box, the rank's device = LOCAL_RANK modulo the devices) -- never the driver's run
+    backend = os.environ.get("KETO_BENCH_BACKEND", "nccl")
     if world > 1:
+        local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -260,7 +267,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total = world * a.batch * a.steps
