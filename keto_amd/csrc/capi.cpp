@@ -169,13 +169,6 @@ void tree_json(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node
 // bytes proto.Marshal gives for Tree.ToProto() (internal/expand/tree.go:165-188): node_type = 1
 // (varint; UNION 1, LEAF 4), subject = 2 (Subject: oneof id = 1 | set = 2 {namespace 1, object 2,
 // relation 3; empty strings omitted}, emitted even when empty), children = 3 (repeated, in order).
-void put_varint(std::string& o, uint64_t v) {
-    while (v >= 0x80) {
-        o.push_back((char)(v | 0x80));
-        v >>= 7;
-    }
-    o.push_back((char)v);
-}
 uint64_t varint_len(uint64_t v) {
     uint64_t k = 1;
     while (v >= 0x80) {
@@ -184,54 +177,102 @@ uint64_t varint_len(uint64_t v) {
     }
     return k;
 }
-void put_field(std::string& o, uint32_t tag, std::string_view b) {
-    o.push_back((char)tag);
-    put_varint(o, b.size());
-    o.append(b);
-}
-std::string subject_proto(const SubjectFields& f) {
-    std::string o;
+// the subject's strings as views into the snapshot / arena (no copies)
+struct SubjectViews {
+    bool set;
+    std::string_view id, ns, obj, rel;
+};
+SubjectViews views_of(const Snapshot& S, const keto_tree_arena* a, uint32_t ref) {
+    SubjectViews f{(ref & EDGE_SET) != 0, {}, {}, {}, {}};
+    const uint32_t v = ref & EDGE_VAL;
+    auto str = [&](uint32_t x) { return x == ANY || x >= S.strs.size() ? std::string_view() : std::string_view(S.strs[x]); };
+    auto nsv = [&](int64_t ns) {
+        if (ns == ANY_NS) return std::string_view();
+        auto it = S.ns_by_id.find((int32_t)ns);
+        return it == S.ns_by_id.end() ? std::string_view() : std::string_view(S.ns_names[it->second]);
+    };
     if (!f.set) {
-        put_field(o, 0x0A, f.id);                         // oneof: present even when ""
-        return o;
+        if (a && v >= a->extra_base && v - a->extra_base < a->extra.size()) f.id = a->extra[v - a->extra_base];
+        else f.id = str(v);
+        return f;
     }
-    std::string set;
-    if (!f.ns.empty()) put_field(set, 0x0A, f.ns);
-    if (!f.obj.empty()) put_field(set, 0x12, f.obj);
-    if (!f.rel.empty()) put_field(set, 0x1A, f.rel);
-    put_field(o, 0x12, set);
-    return o;
+    const RowKey& k = (a && v >= a->ov_base && v - a->ov_base < a->ov_keys.size()) ? a->ov_keys[v - a->ov_base] : S.row_key[v];
+    f.ns = nsv(k.ns);
+    f.obj = str(k.obj);
+    f.rel = str(k.rel);
+    return f;
 }
-// one tree (pre-order nodes) -> SubjectTree bytes: subtree sizes bottom-up (reverse pre-order
-// with a stack of finished children), then one forward pass writes every node behind its
-// children-field tag and length
+inline uint64_t field_len(uint64_t n) { return 1 + varint_len(n) + n; }
+// bytes of the Subject message: oneof id (present even when "") | set {namespace, object,
+// relation; empty strings omitted}
+uint64_t subject_len(const SubjectViews& f) {
+    if (!f.set) return field_len(f.id.size());
+    const uint64_t in = (f.ns.empty() ? 0 : field_len(f.ns.size())) + (f.obj.empty() ? 0 : field_len(f.obj.size())) +
+                        (f.rel.empty() ? 0 : field_len(f.rel.size()));
+    return field_len(in);
+}
+inline char* put_varint(char* p, uint64_t v) {
+    while (v >= 0x80) {
+        *p++ = (char)(v | 0x80);
+        v >>= 7;
+    }
+    *p++ = (char)v;
+    return p;
+}
+inline char* put_field(char* p, uint32_t tag, std::string_view b) {
+    *p++ = (char)tag;
+    p = put_varint(p, b.size());
+    std::memcpy(p, b.data(), b.size());
+    return p + b.size();
+}
+char* put_subject(char* p, const SubjectViews& f) {
+    if (!f.set) return put_field(p, 0x0A, f.id);
+    const uint64_t in = (f.ns.empty() ? 0 : field_len(f.ns.size())) + (f.obj.empty() ? 0 : field_len(f.obj.size())) +
+                        (f.rel.empty() ? 0 : field_len(f.rel.size()));
+    *p++ = (char)0x12;
+    p = put_varint(p, in);
+    if (!f.ns.empty()) p = put_field(p, 0x0A, f.ns);
+    if (!f.obj.empty()) p = put_field(p, 0x12, f.obj);
+    if (!f.rel.empty()) p = put_field(p, 0x1A, f.rel);
+    return p;
+}
+// one tree (pre-order nodes) -> SubjectTree bytes appended to o: subtree sizes bottom-up (reverse
+// pre-order with a stack of finished children), then one forward pass writes every node behind its
+// children-field tag and length, straight into o's buffer
 void tree_proto(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node* nd, uint64_t n, std::string& o) {
-    std::vector<std::string> subj(n);
-    std::vector<uint64_t> size(n);
+    std::vector<uint64_t> size(n), slen(n);
     std::vector<uint64_t> st;
     for (uint64_t k = n; k-- > 0;) {
-        subj[k] = subject_proto(fields_of(S, a, nd[k].subject));
+        slen[k] = subject_len(views_of(S, a, nd[k].subject));
         const bool leaf = (nd[k].info & 0x80000000u) != 0;
         const uint32_t nc = leaf ? 0 : nd[k].info & 0x7FFFFFFFu;
-        uint64_t z = 2 + 1 + varint_len(subj[k].size()) + subj[k].size();
+        uint64_t z = 2 + field_len(slen[k]);
         for (uint32_t c = 0; c < nc && !st.empty(); ++c) {
             const uint64_t cz = st.back();
             st.pop_back();
-            z += 1 + varint_len(cz) + cz;
+            z += field_len(cz);
         }
         size[k] = z;
         st.push_back(z);
     }
-    o.reserve(o.size() + (n ? size[0] : 0));
+    if (!n) return;
+    uint64_t total = size[0];
+    for (uint64_t k = 1; k < n; ++k) total += 1 + varint_len(size[k]);
+    const uint64_t at = o.size();
+    o.resize(at + total);
+    char* p = &o[at];
     for (uint64_t k = 0; k < n; ++k) {
         if (k) {
-            o.push_back((char)0x1A);
-            put_varint(o, size[k]);
+            *p++ = (char)0x1A;
+            p = put_varint(p, size[k]);
         }
-        o.push_back((char)0x08);
-        o.push_back((nd[k].info & 0x80000000u) ? (char)4 : (char)1);
-        put_field(o, 0x12, subj[k]);
+        *p++ = (char)0x08;
+        *p++ = (nd[k].info & 0x80000000u) ? (char)4 : (char)1;
+        *p++ = (char)0x12;
+        p = put_varint(p, slen[k]);
+        p = put_subject(p, views_of(S, a, nd[k].subject));
     }
+    o.resize((uint64_t)(p - o.data()));
 }
 
 int64_t copy_out(const std::string& s, char* buf, uint64_t cap) {
