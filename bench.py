@@ -245,6 +245,7 @@ def main():
     if not a.partitioned and a.e2e_steps > 0:
         e2e = end_to_end(snap, q, a, d_out)
         if a.e2e_only:
+            e2e.pop("_out")
             if rank == 0:
                 print(json.dumps({"end_to_end": e2e}), flush=True)
             return

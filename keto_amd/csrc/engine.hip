@@ -1824,6 +1824,11 @@ struct DeviceState {
     uint8_t* pin_a[2] = {};
     uint64_t pin_cap = 0;
     hipEvent_t pev[8] = {};           // pipeline events: in_done[2], kern_done[2], out_done[2]
+    keto_check_ids* ps_q = nullptr;   // pipeline stash of tier-1 overflows (PipeStash), kept across calls
+    uint32_t* ps_idx = nullptr;
+    uint32_t* ps_count = nullptr;     // [0] stashed, [1] tier-1 requests
+    uint64_t ps_cap = 0;
+    std::vector<hipEvent_t> ps_ev;    // per chunk: 3 timing events
 
     DevSnap view() const { return DevSnap{arena, coll, coll_mask, n_units}; }
 };
@@ -2403,6 +2408,10 @@ void device_release(Snapshot& S) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : D.pev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : D.ps_ev) (void)hipEventDestroy(e);
+    if (D.ps_q) (void)hipFree(D.ps_q);
+    if (D.ps_idx) (void)hipFree(D.ps_idx);
+    if (D.ps_count) (void)hipFree(D.ps_count);
     S.dev.reset();
 }
 
@@ -2470,11 +2479,43 @@ struct Undecided {
     uint8_t value = 0;
 };
 
+// Pipelined host batches (device_check_host) defer everything after tier 1: no host synchronization
+// per chunk, so the next chunk's work is already queued when this one ends.  The chunk's tier-1
+// overflows (requests that need tier 2) are copied to a batch-wide stash instead, and decided by a
+// full check of the stash once every chunk is done.
+struct PipeStash {
+    keto_check_ids* q = nullptr;   // device: stashed requests (handle form)
+    uint32_t* idx = nullptr;       // device: their batch indices
+    uint32_t* count = nullptr;     // device: how many
+    uint64_t cap = 0;
+    uint32_t base = 0;             // batch index of the current chunk's first request
+    const keto_check_ids* dq = nullptr;   // the current chunk's requests
+    std::vector<hipEvent_t> ev;    // per chunk: tier 0 start, tier 0 end, tier 1 end
+    uint32_t chunk = 0;
+};
+
+__global__ void __launch_bounds__(256) stash_overflow(const keto_check_ids* __restrict__ q, const uint32_t* __restrict__ list,
+                                                      const uint32_t* __restrict__ count, keto_check_ids* __restrict__ sq,
+                                                      uint32_t* __restrict__ sidx, uint32_t* __restrict__ scount,
+                                                      uint32_t base, uint64_t cap, const uint32_t* __restrict__ t1_count,
+                                                      uint32_t* __restrict__ t1_total) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(t1_total, *t1_count);   // tier-1 requests (timing)
+    const uint32_t m = *count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint32_t at = atomicAdd(scount, 1u);
+        if (at < cap) {
+            sq[at] = q[list[i]];
+            sidx[at] = base + list[i];
+        }
+    }
+}
+
 // Runs tiers 0..2 over a batch of n; the batch's timing goes to D.last (added to it when
-// `accumulate`, for the chunks of one host-buffer call).
+// `accumulate`, for the chunks of one host-buffer call).  With `stash`: tiers 0 and 1 only, no
+// host synchronization, tier-1 overflows to the stash (the caller finishes the batch).
 template <class Launch>
 void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t st, Launch launch,
-               const Undecided& und, bool accumulate = false) {
+               const Undecided& und, bool accumulate = false, PipeStash* stash = nullptr) {
     ensure_lists(D, n);
     uint32_t* list0 = D.lists;
     uint32_t* list1 = D.lists + D.list_cap;
@@ -2494,6 +2535,19 @@ void run_tiers(DeviceState& D, Tier* set, uint32_t n, const Plan& p, hipStream_t
         HIP_OK(hipMemsetAsync(D.pool_busy, 0, words * sizeof(uint32_t), st));
     }
     HIP_OK(hipMemsetAsync(D.counters, 0, 4 * sizeof(uint32_t), st));
+    if (stash) {
+        // deferred: tiers 0 and 1, then the tier-1 overflows into the stash; no synchronization
+        hipEvent_t* e = stash->ev.data() + 3 * stash->chunk;
+        HIP_OK(hipEventRecord(e[0], st));
+        launch(0, set[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
+        HIP_OK(hipEventRecord(e[1], st));
+        launch(1, set[1], list0, c0, list1, c1, p.slots[1]);
+        HIP_OK(hipEventRecord(e[2], st));
+        hipLaunchKernelGGL(stash_overflow, dim3(16), dim3(256), 0, st, stash->dq, list1, c1, stash->q, stash->idx,
+                           stash->count, stash->base, stash->cap, c0, stash->count + 1);
+        HIP_OK(hipGetLastError());
+        return;
+    }
     // tier 0 over all requests
     HIP_OK(hipEventRecord(D.ev[0], st));
     launch(0, set[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
@@ -2652,7 +2706,7 @@ namespace {
 // D.mu and has set the device; `dq` / `da` are device buffers.
 void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
                   hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
-                  uint32_t* d_steps = nullptr) {
+                  uint32_t* d_steps = nullptr, PipeStash* stash = nullptr) {
     if (n == 0) {
         if (!accumulate) D.last = keto_batch_timing{};
         return;
@@ -2791,7 +2845,7 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                       dwork ? go(check_kernel<GlobalStack, true, 1>) : go(check_kernel<GlobalStack, false, 1>);
                   HIP_OK(hipGetLastError());
               },
-              Undecided{da, nullptr, (uint8_t)KETO_UNDECIDED}, accumulate);
+              Undecided{da, nullptr, (uint8_t)KETO_UNDECIDED}, accumulate, stash);
     if (work_out) {
         unsigned long long h[2 * KETO_WORK_SLOTS];
         HIP_OK(hipMemcpyAsync(h, dwork, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -2969,7 +3023,31 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     hipEvent_t* kern_done = D.pev + 2;
     hipEvent_t* out_done = D.pev + 4;
     uint32_t* d_bad = D.counters + 4;
-    HIP_OK(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), D.stream));
+    HIP_OK(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), D.copy_in));     // the translations run on copy_in
+    // requests that overflow tier 1 are stashed and decided after the last chunk (PipeStash)
+    if (D.ps_cap < n) {
+        if (D.ps_q) (void)hipFree(D.ps_q);
+        if (D.ps_idx) (void)hipFree(D.ps_idx);
+        D.ps_q = nullptr;
+        D.ps_idx = nullptr;
+        D.ps_cap = 0;
+        D.ps_q = dmalloc<keto_check_ids>(n, acc);
+        D.ps_idx = dmalloc<uint32_t>(n, acc);
+        D.ps_cap = n;
+    }
+    if (!D.ps_count) D.ps_count = dmalloc<uint32_t>(2, acc);
+    while (D.ps_ev.size() < 3ull * chunks) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        D.ps_ev.push_back(e);
+    }
+    HIP_OK(hipMemsetAsync(D.ps_count, 0, 2 * sizeof(uint32_t), D.stream));
+    PipeStash ps;
+    ps.q = D.ps_q;
+    ps.idx = D.ps_idx;
+    ps.count = D.ps_count;
+    ps.cap = D.ps_cap;
+    ps.ev = D.ps_ev;
     auto lo = [&](uint32_t c) { return c == 0 ? 0 : std::min<uint64_t>(n, C0 + (uint64_t)(c - 1) * C); };
     auto len = [&](uint32_t c) { return (uint32_t)(std::min<uint64_t>(n, c == 0 ? C0 : lo(c) + C) - lo(c)); };
     // stage chunk c's requests and enqueue its H2D into slot c % 2 (slot reuse waits for chunk
@@ -2988,6 +3066,13 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
             src = dst;
         }
         HIP_OK(hipMemcpyAsync(D.slot_q[k], src, (uint64_t)len(c) * esz, hipMemcpyHostToDevice, D.copy_in));
+        // row ids -> handles right behind the copy, on the copy stream: it runs beside the check of
+        // the chunk before (in its tail) instead of between the two checks
+        if (form == FORM_ROWS)
+            translate_rows_locked(S, D, D.slot_q[k], D.slot_x[k], len(c), D.copy_in, d_bad);
+        else if (form == FORM_PAIRS)
+            translate_pairs_locked(S, D, reinterpret_cast<const keto_check_pair*>(D.slot_q[k]), D.slot_x[k], len(c),
+                                   pair_depth, D.copy_in, d_bad);
         HIP_OK(hipEventRecord(in_done[k], D.copy_in));
     };
     // bring chunk c's decisions home (pageable: via staging, copied out once the D2H is done)
@@ -3004,16 +3089,11 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
         if (c + 1 < chunks) put(c + 1);
         HIP_OK(hipStreamWaitEvent(D.stream, in_done[k], 0));
         if (c >= 2) HIP_OK(hipStreamWaitEvent(D.stream, out_done[k], 0));   // slot_a[k] drained
-        const keto_check_ids* dq = D.slot_q[k];
-        if (form == FORM_ROWS) {
-            translate_rows_locked(S, D, dq, D.slot_x[k], len(c), D.stream, d_bad);
-            dq = D.slot_x[k];
-        } else if (form == FORM_PAIRS) {
-            translate_pairs_locked(S, D, reinterpret_cast<const keto_check_pair*>(dq), D.slot_x[k], len(c), pair_depth,
-                                   D.stream, d_bad);
-            dq = D.slot_x[k];
-        }
-        check_locked(S, D, dq, len(c), gmd, D.slot_a[k], D.stream, ov.v, nullptr, true);
+        const keto_check_ids* dq = form == FORM_HANDLES ? D.slot_q[k] : D.slot_x[k];   // translated on copy_in
+        ps.base = (uint32_t)lo(c);
+        ps.dq = dq;
+        ps.chunk = c;
+        check_locked(S, D, dq, len(c), gmd, D.slot_a[k], D.stream, ov.v, nullptr, true, nullptr, &ps);
         HIP_OK(hipEventRecord(kern_done[k], D.stream));
         HIP_OK(hipStreamWaitEvent(D.copy_out, kern_done[k], 0));
         if (!pinned && c >= 2) drain(c - 2);
@@ -3028,6 +3108,40 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     if (form != FORM_HANDLES) {
         HIP_OK(hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, D.stream));
         HIP_OK(hipStreamSynchronize(D.stream));
+    }
+    // timing of the chunks' tiers 0 and 1, and the stash
+    uint32_t pc[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(pc, D.ps_count, sizeof(pc), hipMemcpyDeviceToHost, D.stream));
+    HIP_OK(hipStreamSynchronize(D.stream));
+    D.last.requests[0] = n;
+    D.last.requests[1] = pc[1];
+    for (uint32_t c = 0; c < chunks; ++c) {
+        float a = 0, b = 0;
+        HIP_OK(hipEventElapsedTime(&a, D.ps_ev[3 * c], D.ps_ev[3 * c + 1]));
+        HIP_OK(hipEventElapsedTime(&b, D.ps_ev[3 * c + 1], D.ps_ev[3 * c + 2]));
+        D.last.tier_ms[0] += a;
+        D.last.tier_ms[1] += b;
+    }
+    if (pc[0] && !bad) {
+        // the stashed tier-1 overflows: one full check of them (tier 2, then per-request UNDECIDED),
+        // and their decisions written over the ones the chunks left
+        const uint32_t m = (uint32_t)std::min<uint64_t>(pc[0], D.ps_cap);
+        const keto_batch_timing before = D.last;
+        uint8_t* d_dec = nullptr;
+        HIP_OK(hipMalloc(&d_dec, m));
+        check_locked(S, D, D.ps_q, m, gmd, d_dec, D.stream, ov.v, nullptr, false);
+        const keto_batch_timing stash_t = D.last;
+        std::vector<uint8_t> dec(m);
+        std::vector<uint32_t> idx(m);
+        HIP_OK(hipMemcpyAsync(dec.data(), d_dec, m, hipMemcpyDeviceToHost, D.stream));
+        HIP_OK(hipMemcpyAsync(idx.data(), D.ps_idx, m * sizeof(uint32_t), hipMemcpyDeviceToHost, D.stream));
+        HIP_OK(hipStreamSynchronize(D.stream));
+        (void)hipFree(d_dec);
+        for (uint32_t i = 0; i < m; ++i) allowed[idx[i]] = dec[i];
+        D.last = before;
+        D.last.requests[2] = stash_t.requests[2];
+        D.last.tier_ms[2] = stash_t.tier_ms[0] + stash_t.tier_ms[1] + stash_t.tier_ms[2];
+        D.last.undecided = stash_t.undecided;
     }
     D.last.chunks = chunks;
     D.last.wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
