@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 2
+#define KETO_ABI_VERSION 3
 
 /* return codes */
 #define KETO_OK 0
@@ -207,22 +207,85 @@ uint64_t keto_snapshot_version(const keto_snapshot* s);
  * level only visits rows every part holds, so each part answers exactly.  Calls naming another
  * part's root row fail with KETO_E_INVALID.  Replaces nothing in the reference. */
 int keto_snapshot_upload_part(keto_snapshot* s, uint32_t part, uint32_t n_parts, int32_t device);
+
+/* Partition modes of keto_snapshot_upload_part_mode. */
+#define KETO_PART_SHARED 0      /* keto_snapshot_upload_part: set targets on every part, root rows by hash */
+#define KETO_PART_MIGRATE 1     /* every row on exactly one part by hash(namespace_id, object) */
+#define KETO_MIG_MAX_PARTS 31
+/* Edge-partitioned upload in either mode.  KETO_PART_MIGRATE is for graphs whose set-target rows
+ * (folders, groups) do not fit on one GPU either: each part holds only its own rows, plus a stub for
+ * every other part's row one of its subject sets points at, and a check's DFS migrates between parts
+ * at those crossings (keto_mig_begin / keto_mig_round).  After the upload the parts exchange closure
+ * filters (keto_part_stubs / keto_part_filters / keto_part_close) until no filter changes anywhere,
+ * then call keto_part_closure_done.  A migrating part answers checks only through keto_mig_*;
+ * expand and the other check entry points fail with KETO_E_INVALID.  n_parts <= 31. */
+int keto_snapshot_upload_part_mode(keto_snapshot* s, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode);
 /* Arena a part of an edge-partitioned upload would hold (host-only snapshots; sizing aid):
  * arena_bytes of the part's device arena, shared_bytes of it in rows every part keeps. */
 typedef struct {
     uint64_t arena_bytes;
     uint64_t shared_bytes;
-    uint32_t rows;              /* rows on the part */
-    uint32_t shared_rows;       /* of them: rows some subject set points at (on every part) */
+    uint32_t rows;              /* rows on the part (stubs not counted) */
+    uint32_t shared_rows;       /* of them: rows some subject set points at (on every part; KETO_PART_SHARED) */
     uint32_t root_rows;         /* of them: this part's root rows */
+    uint64_t stub_rows;         /* KETO_PART_MIGRATE: stubs of other parts' rows */
 } keto_part_stats;
 int keto_snapshot_part_stats(keto_snapshot* s, uint32_t part, uint32_t n_parts, keto_part_stats* out);
+int keto_snapshot_part_stats_mode(keto_snapshot* s, uint32_t part, uint32_t n_parts, uint32_t mode,
+                                  keto_part_stats* out);
+
+/* Closure-filter exchange of a migrating partition.  A closure filter (KETO_FILTER_WORDS words) is
+ * the bloom filter of every subject id reachable from a row; a stub must carry its row's filter from
+ * the owner part.  Round: every part lists its stubs (keto_part_stubs: row ids, ascending; returns
+ * the count, writes at most cap), asks each stub's owner (keto_row_owner) for its current filter
+ * (keto_part_filters on the owner: the filters of rows it holds, stubs included), and ORs the answers into its stubs
+ * (keto_part_close, which then re-closes the part's own filters; *changed_out = filters that
+ * changed).  When a round changes nothing on any part, every filter is exact: keto_part_closure_done
+ * (converged = 1).  converged = 0 gives all-ones filters (no pruning; still exact answers). */
+#define KETO_FILTER_WORDS 22
+int64_t keto_part_stubs(const keto_snapshot* s, uint32_t* rows_out, uint64_t cap);
+int keto_part_filters(keto_snapshot* s, const uint32_t* rows, uint64_t n, uint32_t* filters_out);
+int keto_part_close(keto_snapshot* s, const uint32_t* stub_rows, uint64_t n, const uint32_t* filters,
+                    uint64_t* changed_out);
+int keto_part_closure_done(keto_snapshot* s, int converged);
+
+/* Check batches on a migrating partition (replaces check.(*Engine).SubjectIsAllowed,
+ * internal/check/engine.go:116-123, for graphs spread over several GPUs).  keto_mig_begin takes the
+ * requests routed to this part (row-id form, every top-level row owned here: keto_row_owner /
+ * keto_route_rows_device) and runs their searches until each is decided or crosses to another
+ * part.  The crossings come back as continuation records grouped by destination part (out->units[p]
+ * 16-B units at d_records + the prefix of units before p, out->records[p] records whose unit
+ * offsets inside p's segment are at d_offsets + the prefix of records before p; valid until the next
+ * call on this snapshot).  The caller exchanges them (one all-to-all: each part receives the
+ * segments addressed to it from every source part, concatenated in source order) and passes what it
+ * received to keto_mig_round (in_records[s], in_units[s] per source part s), which continues the
+ * searches and emits the next records.  Decisions land in d_allowed_out (the routed batch's order)
+ * of the part that began the request.  The batch is done when a round emits no record on any part.
+ * Decision bytes as keto_check_batch_device (KETO_UNDECIDED: a search beyond the engine's limits). */
+typedef struct {
+    uint64_t units[KETO_MIG_MAX_PARTS];
+    uint32_t records[KETO_MIG_MAX_PARTS];
+    const void* d_records;
+    const uint32_t* d_offsets;
+    uint32_t decided;           /* decisions written on this part in the call */
+    uint32_t undecided;         /* of the searches ended in the call: KETO_UNDECIDED */
+    uint32_t entered;           /* searches started or continued by an ENTER record */
+    uint32_t resumed;           /* searches continued by a RESUME record */
+} keto_mig_out;
+int keto_mig_begin(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                   uint8_t* d_allowed_out, void* stream, keto_mig_out* out);
+int keto_mig_round(keto_snapshot* s, const void* d_records, const uint32_t* d_offsets, const uint32_t* in_records,
+                   const uint64_t* in_units, void* stream, keto_mig_out* out);
+/* Device-to-device copy on `stream`, returning when it is done: for callers whose exchange layer
+ * needs the records in buffers of its own (e.g. torch.distributed tensors). */
+int keto_device_copy(void* dst, const void* src, uint64_t bytes, void* stream);
 /* keto_check_batch_device on requests that name rows by row id (row and subject-set target), the
  * form requests travel in between parts: each is translated to this device's handles first.  A
  * request for another part's root row fails the call with KETO_E_INVALID. */
 int keto_check_batch_rows_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                                  uint8_t* d_allowed_out, void* stream);
-/* Owner part of each row id for n_parts parts: -1 = a row every part holds (route anywhere). */
+/* Owner part of each row id for n_parts parts: -1 = a row every part holds (route anywhere; a
+ * KETO_PART_SHARED part's set targets).  A KETO_PART_MIGRATE part owns every row it holds. */
 int keto_row_owner(const keto_snapshot* s, const uint32_t* rows, uint64_t n, uint32_t n_parts, int32_t* out);
 /* Device-side routing of a row-id batch over n_parts (<= 64) parts, all buffers on one device:
  * a stable counting sort by destination part = d_owner[row] (keto_row_owner's output as int16,

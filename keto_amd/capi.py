@@ -34,7 +34,12 @@ EXPORTS = [
     "keto_route_work_bytes", "keto_route_rows_device", "keto_unroute_device", "keto_check_batch_rows",
     "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs", "keto_tree_proto", "keto_tree_proto_all",
     "keto_check_steps_device", "keto_snapshot_part_stats", "keto_snapshot_apply", "keto_snapshot_version",
+    "keto_snapshot_upload_part_mode", "keto_snapshot_part_stats_mode", "keto_part_stubs", "keto_part_filters",
+    "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy",
 ]
+PART_SHARED, PART_MIGRATE = 0, 1
+MIG_MAX_PARTS = 31
+FILTER_WORDS = 22
 
 
 class KetoError(RuntimeError):
@@ -101,7 +106,13 @@ class KTiming(C.Structure):
 
 class KPartStats(C.Structure):
     _fields_ = [("arena_bytes", C.c_uint64), ("shared_bytes", C.c_uint64), ("rows", C.c_uint32),
-                ("shared_rows", C.c_uint32), ("root_rows", C.c_uint32)]
+                ("shared_rows", C.c_uint32), ("root_rows", C.c_uint32), ("stub_rows", C.c_uint64)]
+
+
+class KMigOut(C.Structure):
+    _fields_ = [("units", C.c_uint64 * 31), ("records", C.c_uint32 * 31), ("d_records", C.c_void_p),
+                ("d_offsets", C.c_void_p), ("decided", C.c_uint32), ("undecided", C.c_uint32),
+                ("entered", C.c_uint32), ("resumed", C.c_uint32)]
 
 
 class KStats(C.Structure):
@@ -145,6 +156,7 @@ def load():
     lib.keto_subject_string.restype = C.c_int64
     lib.keto_route_work_bytes.restype = C.c_uint64
     lib.keto_snapshot_version.restype = C.c_uint64
+    lib.keto_part_stubs.restype = C.c_int64
     lib.keto_route_work_bytes.argtypes = [C.c_uint32, C.c_uint32]
     _lib = lib
     return lib
@@ -170,6 +182,11 @@ def route_rows_device(d_reqs_ptr: int, n: int, d_owner_ptr: int, n_rows: int, se
                                          C.c_void_p(d_work_ptr), C.c_uint64(work_bytes), C.c_void_p(d_send_ptr),
                                          C.c_void_p(d_order_ptr), counts, C.c_void_p(stream)))
     return list(counts)
+
+
+def device_copy(dst_ptr: int, src_ptr: int, nbytes: int, stream=0) -> None:
+    """keto_device_copy: synchronous device-to-device copy on `stream`."""
+    _check(load().keto_device_copy(C.c_void_p(dst_ptr), C.c_void_p(src_ptr), C.c_uint64(nbytes), C.c_void_p(stream)))
 
 
 def unroute_device(d_back_ptr: int, d_order_ptr: int, n: int, d_out_ptr: int, stream=0) -> None:
@@ -285,16 +302,73 @@ class Snapshot:
         _check(lib.keto_snapshot_build(ns, len(namespaces), tt, C.c_uint64(len(rows)), C.byref(opts), C.byref(h)))
         return cls(h, lib)
 
-    def upload_part(self, part: int, n_parts: int, device: int = 0):
-        """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part)."""
-        _check(self.lib.keto_snapshot_upload_part(self.h, C.c_uint32(part), C.c_uint32(n_parts), C.c_int32(device)))
+    def upload_part(self, part: int, n_parts: int, device: int = 0, mode: int = PART_SHARED):
+        """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part_mode)."""
+        _check(self.lib.keto_snapshot_upload_part_mode(self.h, C.c_uint32(part), C.c_uint32(n_parts),
+                                                       C.c_int32(device), C.c_uint32(mode)))
+        self.part, self.n_parts, self.part_mode = part, n_parts, mode
         return self
 
-    def part_stats(self, part: int, n_parts: int) -> dict:
-        """keto_snapshot_part_stats: the arena part `part` of n_parts would hold (host-only snapshot)."""
+    def part_stats(self, part: int, n_parts: int, mode: int = PART_SHARED) -> dict:
+        """keto_snapshot_part_stats_mode: the arena part `part` of n_parts would hold (host-only snapshot)."""
         st = KPartStats()
-        _check(self.lib.keto_snapshot_part_stats(self.h, C.c_uint32(part), C.c_uint32(n_parts), C.byref(st)))
+        _check(self.lib.keto_snapshot_part_stats_mode(self.h, C.c_uint32(part), C.c_uint32(n_parts), C.c_uint32(mode),
+                                                      C.byref(st)))
         return {f: getattr(st, f) for f, _ in KPartStats._fields_}
+
+    # ---- migrating partition (keto_part_* / keto_mig_*)
+    def part_stubs(self) -> np.ndarray:
+        """Row ids of this migrating part's stubs (other parts' rows its subject sets point at)."""
+        n = int(self.lib.keto_part_stubs(self.h, None, C.c_uint64(0)))
+        _check(0 if n >= 0 else n)
+        out = np.empty(n, dtype=np.uint32)
+        if n:
+            self.lib.keto_part_stubs(self.h, out.ctypes.data_as(C.c_void_p), C.c_uint64(n))
+        return out
+
+    def part_filters(self, rows: np.ndarray) -> np.ndarray:
+        """Current closure filters [n, FILTER_WORDS] of rows this part owns."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        out = np.empty((len(rows), FILTER_WORDS), dtype=np.uint32)
+        _check(self.lib.keto_part_filters(self.h, rows.ctypes.data_as(C.c_void_p), C.c_uint64(len(rows)),
+                                          out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def part_close(self, stub_rows: np.ndarray, filters: np.ndarray) -> int:
+        """OR the owners' filters into these stubs and re-close this part's filters; returns changes."""
+        stub_rows = np.ascontiguousarray(stub_rows, dtype=np.uint32)
+        filters = np.ascontiguousarray(filters, dtype=np.uint32)
+        ch = C.c_uint64(0)
+        _check(self.lib.keto_part_close(self.h, stub_rows.ctypes.data_as(C.c_void_p), C.c_uint64(len(stub_rows)),
+                                        filters.ctypes.data_as(C.c_void_p), C.byref(ch)))
+        return int(ch.value)
+
+    def part_closure_done(self, converged: bool = True):
+        _check(self.lib.keto_part_closure_done(self.h, C.c_int(1 if converged else 0)))
+
+    @staticmethod
+    def _mig_out(o: "KMigOut", n_parts: int) -> dict:
+        return {"units": [int(o.units[p]) for p in range(n_parts)],
+                "records": [int(o.records[p]) for p in range(n_parts)],
+                "d_records": int(o.d_records or 0), "d_offsets": int(o.d_offsets or 0),
+                "decided": int(o.decided), "undecided": int(o.undecided), "entered": int(o.entered),
+                "resumed": int(o.resumed)}
+
+    def mig_begin(self, d_reqs_ptr: int, n: int, d_out_ptr: int, global_max_depth=5, stream=0) -> dict:
+        """keto_mig_begin: start the searches of the row-id requests routed to this part."""
+        o = KMigOut()
+        _check(self.lib.keto_mig_begin(self.h, C.c_void_p(d_reqs_ptr), C.c_uint32(n), C.c_int32(global_max_depth),
+                                       C.c_void_p(d_out_ptr), C.c_void_p(stream), C.byref(o)))
+        return self._mig_out(o, self.n_parts)
+
+    def mig_round(self, d_records_ptr: int, d_offsets_ptr: int, in_records, in_units, stream=0) -> dict:
+        """keto_mig_round: continue the searches of the records received from every source part."""
+        rec = (C.c_uint32 * MIG_MAX_PARTS)(*[int(x) for x in in_records])
+        uni = (C.c_uint64 * MIG_MAX_PARTS)(*[int(x) for x in in_units])
+        o = KMigOut()
+        _check(self.lib.keto_mig_round(self.h, C.c_void_p(d_records_ptr), C.c_void_p(d_offsets_ptr), rec, uni,
+                                       C.c_void_p(stream), C.byref(o)))
+        return self._mig_out(o, self.n_parts)
 
     def row_owner(self, rows: np.ndarray, n_parts: int) -> np.ndarray:
         """Owner part of each row id (-1: held by every part)."""

@@ -33,7 +33,7 @@ thread_local std::string g_err;
 inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
 
 template <class F>
-int guarded(F&& f) {
+auto guarded(F&& f) -> decltype(f()) {
     try {
         g_err.clear();
         return f();
@@ -534,38 +534,150 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
 
 uint64_t keto_snapshot_version(const keto_snapshot* h) { return h ? h->s->version : 0; }
 
-int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device) {
+int keto_snapshot_upload_part_mode(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode) {
     return guarded([&] {
         if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
         Snapshot& S = *h->s;
         if (S.dev) throw Error{KETO_E_INVALID, "snapshot is already on a device (build it with device = -1)"};
         if (n_parts == 0 || part >= n_parts) throw Error{KETO_E_INVALID, "bad part"};
+        if (mode != KETO_PART_SHARED && mode != KETO_PART_MIGRATE) throw Error{KETO_E_INVALID, "bad partition mode"};
+        if (mode == KETO_PART_MIGRATE && n_parts > KETO_MIG_MAX_PARTS)
+            throw Error{KETO_E_INVALID, "a migrating partition has at most 31 parts"};
         S.part = part;
         S.n_parts = n_parts;
+        S.part_mode = (int)mode;
         compute_layout(S);
         device_upload(S, device);
         return KETO_OK;
     });
 }
 
-int keto_snapshot_part_stats(keto_snapshot* h, uint32_t part, uint32_t n_parts, keto_part_stats* out) {
+int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device) {
+    return keto_snapshot_upload_part_mode(h, part, n_parts, device, KETO_PART_SHARED);
+}
+
+int keto_snapshot_part_stats_mode(keto_snapshot* h, uint32_t part, uint32_t n_parts, uint32_t mode,
+                                  keto_part_stats* out) {
     return guarded([&] {
         if (!h || !out || n_parts == 0 || part >= n_parts) throw Error{KETO_E_INVALID, "bad argument"};
+        if (mode != KETO_PART_SHARED && mode != KETO_PART_MIGRATE) throw Error{KETO_E_INVALID, "bad partition mode"};
+        if (mode == KETO_PART_MIGRATE && n_parts > KETO_MIG_MAX_PARTS)
+            throw Error{KETO_E_INVALID, "a migrating partition has at most 31 parts"};
         Snapshot& S = *h->s;
         if (S.dev) throw Error{KETO_E_INVALID, "part statistics need a host-only snapshot (device = -1)"};
         const uint32_t p0 = S.part, n0 = S.n_parts;
+        const int m0 = S.part_mode;
         S.part = part;
         S.n_parts = n_parts;
+        S.part_mode = (int)mode;
         compute_layout(S);
         out->arena_bytes = S.n_units * HDR_WORDS * 4;
-        out->shared_bytes = S.shared_words * 4;
-        out->rows = (uint32_t)S.rows_by_unit.size();
+        out->shared_bytes = mode == KETO_PART_SHARED ? S.shared_words * 4 : 0;
+        out->rows = 0;
         out->shared_rows = 0;
-        for (uint32_t r = 0; r < S.n_rows(); ++r) out->shared_rows += !S.is_root[r];
-        out->root_rows = out->rows - out->shared_rows;
+        out->root_rows = 0;
+        for (uint32_t r = 0; r < S.n_rows(); ++r) {
+            if (!S.present(r)) continue;
+            ++out->rows;
+            if (S.is_root[r]) ++out->root_rows;
+            else if (mode == KETO_PART_SHARED) ++out->shared_rows;
+        }
+        out->stub_rows = S.n_stubs;
         S.part = p0;
         S.n_parts = n0;
+        S.part_mode = m0;
         compute_layout(S);
+        return KETO_OK;
+    });
+}
+
+int keto_snapshot_part_stats(keto_snapshot* h, uint32_t part, uint32_t n_parts, keto_part_stats* out) {
+    return keto_snapshot_part_stats_mode(h, part, n_parts, KETO_PART_SHARED, out);
+}
+
+int64_t keto_part_stubs(const keto_snapshot* h, uint32_t* rows_out, uint64_t cap) {
+    return guarded([&]() -> int64_t {
+        if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        const Snapshot& S = *h->s;
+        if (S.part_mode != PART_MIGRATE || S.stub.empty()) return 0;
+        uint64_t k = 0;
+        for (uint32_t r = 0; r < S.n_rows(); ++r) {
+            if (!S.stub[r]) continue;
+            if (rows_out && k < cap) rows_out[k] = r;
+            ++k;
+        }
+        return (int64_t)k;
+    });
+}
+
+int keto_part_filters(keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t* filters_out) {
+    return guarded([&] {
+        if (!h || (n && (!rows || !filters_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        part_filters(*h->s, rows, n, filters_out);
+        return KETO_OK;
+    });
+}
+
+int keto_part_close(keto_snapshot* h, const uint32_t* stub_rows, uint64_t n, const uint32_t* filters,
+                    uint64_t* changed_out) {
+    return guarded([&] {
+        if (!h || (n && (!stub_rows || !filters))) throw Error{KETO_E_INVALID, "NULL argument"};
+        const uint64_t c = part_close(*h->s, stub_rows, n, filters);
+        if (changed_out) *changed_out = c;
+        return KETO_OK;
+    });
+}
+
+int keto_part_closure_done(keto_snapshot* h, int converged) {
+    return guarded([&] {
+        if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        if (h->s->part_mode != PART_MIGRATE) throw Error{KETO_E_INVALID, "not a migrating part"};
+        part_closure_done(*h->s, converged != 0);
+        return KETO_OK;
+    });
+}
+
+namespace {
+void copy_out(const MigOut& m, keto_mig_out* out) {
+    for (uint32_t p = 0; p < KETO_MIG_MAX_PARTS; ++p) {
+        out->units[p] = m.units[p];
+        out->records[p] = m.records[p];
+    }
+    out->d_records = m.d_buf;
+    out->d_offsets = m.d_off;
+    out->decided = m.decided;
+    out->undecided = m.undecided;
+    out->entered = m.started;
+    out->resumed = m.resumed;
+}
+}  // namespace
+
+int keto_mig_begin(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
+                   uint8_t* d_allowed_out, void* stream, keto_mig_out* out) {
+    return guarded([&] {
+        if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        MigOut m{};
+        mig_begin(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream, m);
+        copy_out(m, out);
+        return KETO_OK;
+    });
+}
+
+int keto_device_copy(void* dst, const void* src, uint64_t bytes, void* stream) {
+    return guarded([&] {
+        if (bytes && (!dst || !src)) throw Error{KETO_E_INVALID, "NULL argument"};
+        device_copy(dst, src, bytes, stream);
+        return KETO_OK;
+    });
+}
+
+int keto_mig_round(keto_snapshot* h, const void* d_records, const uint32_t* d_offsets, const uint32_t* in_records,
+                   const uint64_t* in_units, void* stream, keto_mig_out* out) {
+    return guarded([&] {
+        if (!h || !out || !in_records || !in_units) throw Error{KETO_E_INVALID, "NULL argument"};
+        MigOut m{};
+        mig_round(*h->s, d_records, d_offsets, in_records, in_units, stream, m);
+        copy_out(m, out);
         return KETO_OK;
     });
 }
@@ -599,7 +711,7 @@ int keto_row_owner(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uin
         for (uint64_t i = 0; i < n; ++i) {
             if (rows[i] == KETO_NO_ROW) { out[i] = -1; continue; }
             if (rows[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "row id out of range"};
-            out[i] = S.is_root[rows[i]] ? (int32_t)S.root_owner(rows[i], n_parts) : -1;
+            out[i] = S.row_owner(rows[i], n_parts);
         }
         return KETO_OK;
     });

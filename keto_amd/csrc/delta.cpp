@@ -189,7 +189,7 @@ std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {
 }  // namespace
 
 void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del) {
-    if (S.n_parts > 1) throw Error{KETO_E_INVALID, "writes need a replicated snapshot (not an edge-partitioned part)"};
+    if (S.n_parts > 1 || S.part_mode == PART_MIGRATE) throw Error{KETO_E_INVALID, "writes need a replicated snapshot (not an edge-partitioned part)"};
     if ((n_ins && !ins) || (n_del && !del)) throw Error{KETO_E_INVALID, "NULL tuples"};
     Txn T(S);
     // ---- inserts (commit order: after every equal tuple), then deletes (every equal tuple)

@@ -1845,6 +1845,21 @@ T* dmalloc(uint64_t n, uint64_t& acc) {
     return (T*)p;
 }
 
+// a device buffer freed at scope exit
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    explicit DevBuf(uint64_t n) {
+        uint64_t acc = 0;
+        p = dmalloc<T>(n, acc);
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+};
+
 uint32_t pow2_at_least(uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
@@ -2061,14 +2076,15 @@ __global__ void __launch_bounds__(256) closure_fill(uint32_t* __restrict__ arena
 
 // Child signatures of one closure row (see SIG_WORDS): the 16-bit OR-fold of the closure filter
 // of each subject set in its window, stored transposed.  Runs once the filters are closed.  One
-// lane per row; a forwarded row keeps none (its content is elsewhere, without a filter block).
+// lane per row; a forwarded row keeps none (its content is elsewhere, without a filter block), and a
+// migrating part's stub has no edges (its owner holds the row).
 __global__ void __launch_bounds__(256) sig_pass(uint32_t* __restrict__ arena, const uint32_t* __restrict__ rows,
                                                uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = (uint64_t)rows[i] * HDR_WORDS;
     const uint4 v = *reinterpret_cast<const uint4*>(arena + h);
-    if ((v.z & HDR_FWD) || !(v.z & HDR_CLOSURE)) return;
+    if ((v.z & (HDR_FWD | HDR_REMOTE)) || !(v.z & HDR_CLOSURE)) return;   // stubs: no edges here
     const uint4 win = *reinterpret_cast<const uint4*>(arena + h + HDR_WORDS);
     const uint32_t n_edges = (v.z & HDR_SEQ) ? v.x : v.x + v.y;
     uint32_t fold[4];
@@ -2092,20 +2108,26 @@ __global__ void __launch_bounds__(256) sig_pass(uint32_t* __restrict__ arena, co
 // a filter and subject sets, until a round changes nothing.  A graph that has not converged after
 // CLOSURE_MAX_ROUNDS rounds gets full filters (no pruning) instead.
 constexpr int CLOSURE_MAX_ROUNDS = 2048;
-void build_closures(const Snapshot& S, uint32_t* d_arena) {
-    std::vector<uint32_t> list, all;
+// The rows of a snapshot with a closure block: `all` (stubs included) and `list`, those whose
+// filter closure_pass recomputes (this part's rows with subject sets, not ROW_SEQ).
+void closure_rows(const Snapshot& S, std::vector<uint32_t>& list, std::vector<uint32_t>& all) {
     for (uint32_t r = 0; r < S.n_rows(); ++r) {
-        if (!S.row_cb[r] || !S.present(r)) continue;
+        if (!S.row_cb[r] || !S.mapped(r)) continue;
         all.push_back(S.unit_of_row[r]);
-        if (S.rows[r].n_sets > 0 && !(S.row_flags(r) & ROW_SEQ)) list.push_back(S.unit_of_row[r]);
+        if (S.present(r) && S.rows[r].n_sets > 0 && !(S.row_flags(r) & ROW_SEQ)) list.push_back(S.unit_of_row[r]);
     }
-    if (all.empty()) return;
+}
+
+// Rounds of closure_pass over `list` until one changes nothing (true), or CLOSURE_MAX_ROUNDS
+// (false).  *changed_total (optional) gets the number of filter updates.
+bool close_filters(uint32_t* d_arena, const std::vector<uint32_t>& list, uint64_t* changed_total) {
+    if (list.empty()) return true;
     uint32_t *d_rows = nullptr, *d_changed = nullptr;
-    HIP_OK(hipMalloc(&d_rows, std::max(list.size(), all.size()) * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_rows, list.size() * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_changed, sizeof(uint32_t)));
     HIP_OK(hipMemcpy(d_rows, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     const uint32_t n = (uint32_t)list.size();
-    bool done = list.empty();
+    bool done = false;
     for (int round = 0; round < CLOSURE_MAX_ROUNDS && !done; ++round) {
         HIP_OK(hipMemset(d_changed, 0, sizeof(uint32_t)));
         hipLaunchKernelGGL(closure_pass, dim3((n + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, n, d_changed);
@@ -2113,21 +2135,47 @@ void build_closures(const Snapshot& S, uint32_t* d_arena) {
         uint32_t ch = 0;
         HIP_OK(hipMemcpy(&ch, d_changed, sizeof(uint32_t), hipMemcpyDeviceToHost));
         done = ch == 0;
+        if (changed_total) *changed_total += ch;
     }
-    if (!done) {
-        HIP_OK(hipMemcpy(d_rows, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        const uint32_t m = (uint32_t)all.size();
+    (void)hipFree(d_rows);
+    (void)hipFree(d_changed);
+    return done;
+}
+
+// Full filters (no pruning) for the given closure rows, or child signatures from closed filters.
+void finish_filters(uint32_t* d_arena, const std::vector<uint32_t>& all, bool converged) {
+    if (all.empty()) return;
+    uint32_t* d_rows = nullptr;
+    HIP_OK(hipMalloc(&d_rows, all.size() * sizeof(uint32_t)));
+    HIP_OK(hipMemcpy(d_rows, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const uint32_t m = (uint32_t)all.size();
+    if (!converged) {
         hipLaunchKernelGGL(closure_fill, dim3((m + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, m);
         HIP_OK(hipGetLastError());
     }
     // child signatures of every closure row, from the closed filters
-    HIP_OK(hipMemcpy(d_rows, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    const uint32_t m = (uint32_t)all.size();
     hipLaunchKernelGGL(sig_pass, dim3((m + 255) / 256), dim3(256), 0, 0, d_arena, d_rows, m);
     HIP_OK(hipGetLastError());
     HIP_OK(hipDeviceSynchronize());
     (void)hipFree(d_rows);
-    (void)hipFree(d_changed);
+}
+
+// Close every row's closure filter on the device: rounds of closure_pass over the rows that have
+// a filter and subject sets, until a round changes nothing.  A graph that has not converged after
+// CLOSURE_MAX_ROUNDS rounds gets full filters (no pruning) instead.  A migrating part's stubs start
+// empty and its filters are only partial until the parts' filter exchange has converged
+// (part_close / part_closure_done), so the signatures wait for that.
+void build_closures(const Snapshot& S, uint32_t* d_arena) {
+    std::vector<uint32_t> list, all;
+    closure_rows(S, list, all);
+    if (all.empty()) return;
+    const bool done = close_filters(d_arena, list, nullptr);
+    if (S.part_mode == PART_MIGRATE && S.n_parts > 1) {
+        if (!done) finish_filters(d_arena, all, false);
+        HIP_OK(hipDeviceSynchronize());
+        return;
+    }
+    finish_filters(d_arena, all, done);
 }
 
 }  // namespace
@@ -2145,7 +2193,18 @@ void device_upload(Snapshot& S, int device) {
     std::vector<uint32_t> arena(std::max<uint64_t>(words, 4));
     const uint32_t R = S.n_rows();
     host_parallel_for(R, [&](uint64_t r) {
-        if (!S.present((uint32_t)r)) return;                 // another part's root row
+        if (!S.mapped((uint32_t)r)) return;                  // another part's row
+        if (!S.present((uint32_t)r)) {                       // a stub (PART_MIGRATE): owner + its handle
+            uint32_t* h = arena.data() + (uint64_t)S.unit_of_row[r] * HDR_WORDS;
+            uint32_t* cf = h - CB_WORDS;
+            for (uint32_t i = 0; i < CF_WORDS; ++i) cf[i] = 0u;                 // filled by the exchange
+            for (uint32_t i = CF_WORDS; i < CB_WORDS; ++i) cf[i] = NONE32;
+            h[0] = S.root_owner((uint32_t)r, S.n_parts);
+            h[1] = S.g_handle[r];
+            h[2] = HDR_REMOTE | HDR_CLOSURE;
+            h[3] = 0;
+            return;
+        }
         const auto ed = S.row_edges((uint32_t)r);
         put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), ed.first, ed.second,
                 S.unit_of_row, S.row_cb[r] != 0);
@@ -2155,13 +2214,14 @@ void device_upload(Snapshot& S, int device) {
     D->arena = dmalloc<uint32_t>(D->arena_words, acc);
     HIP_OK(hipMemcpy(D->arena, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     build_closures(S, D->arena);
+    S.mig_ready = !(S.part_mode == PART_MIGRATE && S.n_parts > 1);   // else after the filter exchange
     if (!S.coll.empty()) {
         uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
         std::vector<uint64_t> tab(cap, ~0ull);
         for (auto& kv : S.coll) {
             uint32_t key = kv.first;
             if (key & EDGE_SET) {
-                if (!S.present(key & EDGE_VAL)) continue;    // another part's root row
+                if (!S.mapped(key & EDGE_VAL)) continue;     // another part's row (stubs are mapped)
                 key = EDGE_SET | S.unit_of_row[key & EDGE_VAL];   // row -> handle
             }
             uint32_t vid = kv.second;
@@ -2185,6 +2245,105 @@ void device_upload(Snapshot& S, int device) {
     for (auto& e : D->pev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     S.device = device;
     S.dev.reset(D.release());
+}
+
+DevView device_view(const Snapshot& S) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    const DeviceState& D = *S.dev;
+    return DevView{D.arena, D.coll, D.coll_mask, D.device, (void*)D.stream};
+}
+
+namespace {
+// filters of the listed handles -> out (CF_WORDS words each)
+__global__ void __launch_bounds__(256) filters_get(const uint32_t* __restrict__ arena, const uint32_t* __restrict__ units,
+                                                   uint32_t n, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* cf = arena + (uint64_t)units[i] * HDR_WORDS - CB_WORDS;
+    for (uint32_t k = 0; k < CF_WORDS; ++k) out[(uint64_t)i * CF_WORDS + k] = cf[k];
+}
+// OR the given filters into the listed stubs' filters; counts the stubs that gained bits
+__global__ void __launch_bounds__(256) filters_or(uint32_t* __restrict__ arena, const uint32_t* __restrict__ units,
+                                                  uint32_t n, const uint32_t* __restrict__ in, uint32_t* changed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t* cf = arena + (uint64_t)units[i] * HDR_WORDS - CB_WORDS;
+    bool diff = false;
+    for (uint32_t k = 0; k < CF_WORDS; ++k) {
+        const uint32_t o = cf[k], v = o | in[(uint64_t)i * CF_WORDS + k];
+        if (v != o) {
+            cf[k] = v;
+            diff = true;
+        }
+    }
+    if (diff) atomicAdd(changed, 1u);
+}
+
+std::vector<uint32_t> units_of(const Snapshot& S, const uint32_t* rows, uint64_t n, bool stubs) {
+    std::vector<uint32_t> u(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t r = rows[i];
+        // reads (stubs = false) take this part's set targets and its stubs; writes only stubs
+        if (r >= S.n_rows() || !S.mapped(r) || (stubs && S.present(r)) || !S.row_cb[r])
+            throw Error{KETO_E_INVALID, "row " + std::to_string(r) + (stubs ? " is not a stub of this part"
+                                                                           : " has no closure filter on this part")};
+        u[i] = S.unit_of_row[r];
+    }
+    return u;
+}
+}  // namespace
+
+void part_filters(Snapshot& S, const uint32_t* rows, uint64_t n, uint32_t* out) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    if (n == 0) return;
+    const std::vector<uint32_t> u = units_of(S, rows, n, false);
+    DevBuf<uint32_t> du(n), dout(n * CF_WORDS);
+    HIP_OK(hipMemcpy(du.p, u.data(), n * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(filters_get, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, D.arena, du.p, (uint32_t)n, dout.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpy(out, dout.p, n * CF_WORDS * 4, hipMemcpyDeviceToHost));
+}
+
+uint64_t part_close(Snapshot& S, const uint32_t* rows, uint64_t n, const uint32_t* filters) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    if (S.part_mode != PART_MIGRATE) throw Error{KETO_E_INVALID, "not a migrating part"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    uint64_t changed = 0;
+    if (n) {
+        const std::vector<uint32_t> u = units_of(S, rows, n, true);
+        DevBuf<uint32_t> du(n), din(n * CF_WORDS), dch(1);
+        HIP_OK(hipMemcpy(du.p, u.data(), n * 4, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(din.p, filters, n * CF_WORDS * 4, hipMemcpyHostToDevice));
+        HIP_OK(hipMemset(dch.p, 0, 4));
+        hipLaunchKernelGGL(filters_or, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, D.arena, du.p, (uint32_t)n,
+                           din.p, dch.p);
+        HIP_OK(hipGetLastError());
+        uint32_t c = 0;
+        HIP_OK(hipMemcpy(&c, dch.p, 4, hipMemcpyDeviceToHost));
+        changed += c;
+    }
+    std::vector<uint32_t> list, all;
+    closure_rows(S, list, all);
+    if (!close_filters(D.arena, list, &changed)) {
+        finish_filters(D.arena, all, false);       // all ones from now on: the exchange ends here
+    }
+    return changed;
+}
+
+void part_closure_done(Snapshot& S, bool converged) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    std::vector<uint32_t> list, all;
+    closure_rows(S, list, all);
+    finish_filters(D.arena, all, converged);
+    S.mig_ready = true;
 }
 
 namespace {
@@ -2380,6 +2539,7 @@ void device_release(Snapshot& S) {
     if (!S.dev) return;
     DeviceState& D = *S.dev;
     (void)hipSetDevice(D.device);
+    mig_release(S);
     for (auto& t : D.tiers) free_tier(t);
     for (auto& t : D.etiers) free_tier(t);
     if (D.arena) (void)hipFree(D.arena);
@@ -2707,6 +2867,8 @@ namespace {
 void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
                   hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
                   uint32_t* d_steps = nullptr, PipeStash* stash = nullptr) {
+    if (S.part_mode == PART_MIGRATE)
+        throw Error{KETO_E_INVALID, "a migrating part answers checks through keto_mig_begin / keto_mig_round"};
     if (n == 0) {
         if (!accumulate) D.last = keto_batch_timing{};
         return;
@@ -3209,6 +3371,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                    const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
                    const Overlay* ovh, ExpandResult& out) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    if (S.part_mode == PART_MIGRATE)
+        throw Error{KETO_E_INVALID, "expand needs a replicated snapshot or a shared-rows part (PART_SHARED)"};
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));

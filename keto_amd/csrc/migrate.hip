@@ -1,0 +1,830 @@
+// Migrating partition (PART_MIGRATE): check batches over a graph whose rows are ALL split across
+// parts by hash(namespace id, object), for graphs whose shared rows (folders, groups) no longer fit
+// on one GPU (SURVEY.md 8(e) "partitioned mode"; DESIGN.md "Multi-GPU").
+//
+// The reference answers a check with an ordered DFS whose visited map marks nodes on first
+// encounter (internal/check/engine.go:36-114, internal/x/graph/graph_utils.go:13-35), so the
+// search cannot be cut into level-synchronous frontier exchanges without changing answers.  It is
+// cut at part crossings instead: a lane walks the DFS on its part; when the walk enters a subject
+// set whose row another part owns (a stub: HDR_REMOTE), or pops back to a frame of a row another
+// part owns, it writes the whole DFS state -- request, saved frames, visited map -- as a
+// continuation record, and the owner resumes the DFS there in the next round.  The order of events
+// inside every search stays the reference's, so answers stay exact.  Rounds exchange records with
+// one all-to-all each (keto_amd/multi.py); a decided request sends its decision to the part that
+// started it.
+//
+// Visit ids are global: (owner part, handle on the owner) for rows, (31, class) for colliding
+// Subject.String() keys (collision classes are computed on the host for the whole graph).
+//
+// Record (u32 words, 16-B units):
+//   head 8 words: idx (request index on its origin part) | info (kind 0..1, tset 2, decision 3..4,
+//   enter flags 5..7, origin part 8..15) | T (string id, or the set target's handle) | T's owner part
+//   (set targets) | enter handle | enter remaining depth | saved frames ns | visit ids nv
+//   ns frames of 16 B {pos lo, pos hi | part << 8, edges left, depth | flags << 16}
+//   nv visit ids of 8 B
+// ENTER: enter the row `enter` (a row of the receiving part) at the given depth, as the walk would
+// after the hop; RESUME: pop the top saved frame (a frame of the receiving part); DECISION: the
+// request's decision, for its origin part.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "snapshot.hpp"
+
+namespace keto {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t err__ = (x);                                                                     \
+        if (err__ != hipSuccess)                                                                    \
+            throw Error{KETO_E_HIP, std::string(#x) + ": " + hipGetErrorString(err__)};             \
+    } while (0)
+
+namespace {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t HEAD_WORDS = 8;
+constexpr uint32_t K_ENTER = 0, K_RESUME = 1, K_DECISION = 2;
+constexpr uint32_t F_SEQ = 1, F_TOP = 2;            // frame flags
+constexpr uint32_t MIG_FRAMES = 64;                 // saved frames of one search (max-depth <= 65)
+constexpr uint64_t VID_CLASS_PART = 31;
+constexpr uint32_t EPOCH_MAX = (1u << 28) - 1u;
+constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_UNDECIDED = 2, RES_BIG = 3;
+// two lane tiers: many lanes with small visited tables, and a few with big ones for the searches
+// whose maps outgrow the small ones (re-run from their input record, which is exact: a record's
+// processing is deterministic and an overflowed lane has emitted nothing)
+constexpr uint32_t VCAP_SMALL = 512, VCAP_BIG = 1u << 16;
+constexpr uint32_t LANES_SMALL = 256 * 1024, LANES_BIG = 512;
+
+__host__ __device__ inline uint32_t mixv(uint64_t v) {
+    uint64_t k = v * 0x9E3779B97F4A7C15ull;
+    k ^= k >> 29;
+    k *= 0xBF58476D1CE4E5B9ull;
+    return (uint32_t)(k >> 32);
+}
+__device__ inline uint64_t vid_row(uint32_t part, uint32_t handle) { return ((uint64_t)part << 31) | handle; }
+__device__ inline uint64_t vid_class(uint32_t c) { return (VID_CLASS_PART << 31) | (c & 0x7FFFFFFFu); }
+
+// the hash of engine.hip's id tables and collision table (same layouts)
+__device__ inline uint32_t mix32d(uint32_t k) {
+    k ^= k >> 16;
+    k *= 0x7feb352dU;
+    k ^= k >> 15;
+    k *= 0x846ca68bU;
+    k ^= k >> 16;
+    return k;
+}
+
+__device__ inline uint32_t coll_find(const uint64_t* coll, uint32_t mask, uint32_t key) {
+    if (mask == 0) return NONE;
+    for (uint32_t i = mix32d(key) & mask;; i = (i + 1) & mask) {
+        const uint64_t e = coll[i];
+        if (e == ~0ull) return NONE;
+        if ((uint32_t)(e >> 32) == key) return (uint32_t)e;
+    }
+}
+
+// A visited map in the lane's HBM table (epoch-tagged: entry = epoch << 36 | visit id), with an
+// insertion log so the whole map can travel in a record.
+struct MigVisited {
+    uint64_t* tab;
+    uint64_t* log;
+    uint32_t mask, cap;      // cap = ids a map may hold (half the table)
+    uint32_t epoch, n;
+    __device__ inline void fresh() {
+        if (++epoch > EPOCH_MAX) {
+            for (uint32_t i = 0; i <= mask; ++i) tab[i] = 0;
+            epoch = 1;
+        }
+        n = 0;
+    }
+    // 0 = new, 1 = present, 2 = the map is full
+    __device__ inline int test_add(uint64_t vid) {
+        uint32_t i = mixv(vid) & mask;
+        const uint64_t want = ((uint64_t)epoch << 36) | vid;
+        for (;;) {
+            const uint64_t e = tab[i];
+            if ((uint32_t)(e >> 36) != epoch) {
+                if (n >= cap) return 2;
+                tab[i] = want;
+                log[n++] = vid;
+                return 0;
+            }
+            if (e == want) return 1;
+            i = (i + 1) & mask;
+        }
+    }
+};
+
+struct MigArgs {
+    const uint32_t* arena;
+    const uint64_t* coll;
+    uint32_t coll_mask;
+    uint32_t self;
+    // input records: record j of source s (rec_base[s] <= j < rec_base[s + 1]) starts at unit
+    // unit_base[s] + in_off[j]
+    const uint32_t* in;
+    const uint32_t* in_off;
+    const uint32_t* rec_base;
+    const uint64_t* unit_base;
+    uint32_t n_src;
+    uint32_t n_in;
+    const uint32_t* list;        // NULL: every input record; else list[0 .. *n_list)
+    const uint32_t* n_list;
+    // output records (unordered pool) and their (destination, unit, length)
+    uint32_t* pool;
+    uint64_t pool_cap;
+    unsigned long long* pool_used;
+    uint32_t* out_dest;
+    uint32_t* out_unit;
+    uint32_t* out_len;
+    uint32_t* out_count;
+    uint32_t* spill;             // inputs whose record did not fit the pool
+    uint32_t* n_spill;
+    uint32_t* big;               // inputs whose map outgrew this tier's tables
+    uint32_t* n_big;
+    uint8_t* allowed;            // decisions of this part's own requests
+    uint32_t* stats;             // [0] decided here, [1] undecided, [2] entered, [3] resumed
+    // lane workspaces
+    uint64_t* vtab;
+    uint64_t* vlog;
+    uint4* frames;
+    uint32_t* lane_epoch;
+    uint32_t vcap;
+};
+
+// One search state machine per lane over the round's input records (persistent grid).
+__global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    MigVisited V{a.vtab + (uint64_t)slot * a.vcap, a.vlog + (uint64_t)slot * (a.vcap / 2), a.vcap - 1u, a.vcap / 2,
+                 a.lane_epoch[slot], 0};
+    uint4* const fr = a.frames + (uint64_t)slot * MIG_FRAMES;
+    const uint32_t total = a.list ? *a.n_list : a.n_in;
+    for (uint32_t j = slot; j < total; j += stride) {
+        const uint32_t rj = a.list ? a.list[j] : j;
+        uint32_t s = 0;
+        while (s + 1 < a.n_src && a.rec_base[s + 1] <= rj) ++s;
+        const uint32_t* rec = a.in + (a.unit_base[s] + a.in_off[rj]) * 4ull;
+        const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
+        const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 4);
+        const uint32_t idx = h0.x, info = h0.y;
+        const uint32_t kind = info & 3u, origin = (info >> 8) & 0xFFu;
+        if (kind == K_DECISION) {
+            a.allowed[idx] = (uint8_t)((info >> 3) & 3u);
+            atomicAdd(a.stats + 0, 1u);
+            continue;
+        }
+        const bool tset = (info >> 2) & 1u;
+        const uint32_t T = h0.z;
+        const uint64_t T64 = vid_row(h0.w, h0.z);
+        uint32_t cw = 0, cb = 0;
+        closure_bit(T, cw, cb);
+        int res = -1;
+        // restore the map and the saved frames
+        V.fresh();
+        const uint32_t ns = min(h1.z, MIG_FRAMES), nv = h1.w;     // senders keep ns <= MIG_FRAMES
+        if (nv > V.cap) res = RES_BIG;
+        const uint64_t* rv = reinterpret_cast<const uint64_t*>(rec + HEAD_WORDS + 4ull * ns);
+        for (uint32_t i = 0; i < nv && res < 0; ++i)
+            if (V.test_add(rv[i]) == 2) res = RES_BIG;
+        uint32_t sp = ns;
+        for (uint32_t i = 0; i < ns; ++i) fr[i] = *reinterpret_cast<const uint4*>(rec + HEAD_WORDS + 4ull * i);
+        uint64_t pos = 0;
+        uint32_t left = 0, k = 0, fl = 0;
+        bool have = false;
+        uint32_t enter = NONE, enter_k = 0, enter_fl = 0;
+        if (kind == K_ENTER) {
+            enter = h1.x;
+            enter_k = h1.y;
+            enter_fl = (info >> 5) & 7u;
+            atomicAdd(a.stats + 2, 1u);
+        } else {
+            atomicAdd(a.stats + 3, 1u);
+        }
+        // emitted record: destination part, kind, enter handle / depth
+        uint32_t e_dest = NONE, e_kind = 0, e_enter = 0, e_k = 0;
+        while (res < 0) {
+            if (enter != NONE) {
+                uint64_t hw = (uint64_t)enter * HDR_WORDS;
+                uint4 hd = *reinterpret_cast<const uint4*>(a.arena + hw);
+                while (hd.z & HDR_FWD) {
+                    hw = (uint64_t)hd.x * HDR_WORDS;
+                    hd = *reinterpret_cast<const uint4*>(a.arena + hw);
+                }
+                const uint32_t n_sets = hd.x, n_ids = hd.y;
+                const bool seq = (hd.z & HDR_SEQ) != 0;
+                const uint32_t hl = (hd.z >> 8) & 31u;
+                const uint64_t beg = hw + HDR_WORDS;
+                if (!seq && !tset && n_ids > 0) {                     // is the requested id in the row?
+                    bool hit = false;
+                    if (hl == 0) {
+                        for (uint32_t i = n_sets; i < n_sets + n_ids; ++i) hit |= a.arena[beg + i] == T;
+                    } else {
+                        uint32_t b1, b2;
+                        bloom_bits(T, b1, b2);
+                        if (bloom_has(hd.z, hd.w, b1) && bloom_has(hd.z, hd.w, b2)) {
+                            const uint32_t nb = (1u << hl) / BUCKET_WORDS;
+                            const uint64_t tb = hw - ((hd.z & HDR_CLOSURE) ? CB_WORDS : 0u) - (1ull << hl);
+                            for (uint32_t b = mix32d(T) & (nb - 1);; b = (b + 1) & (nb - 1)) {
+                                const uint4 v = *reinterpret_cast<const uint4*>(a.arena + tb + (uint64_t)b * BUCKET_WORDS);
+                                if (v.x == T || v.y == T || v.z == T || v.w == T) {
+                                    hit = true;
+                                    break;
+                                }
+                                if (v.x == NONE || v.y == NONE || v.z == NONE || v.w == NONE) break;
+                            }
+                        }
+                    }
+                    if (hit) {
+                        res = RES_TRUE;
+                        break;
+                    }
+                }
+                if (have && left > 0) {                               // the parent keeps its place
+                    if (sp >= MIG_FRAMES) {
+                        res = RES_UNDECIDED;
+                        break;
+                    }
+                    fr[sp++] = make_uint4((uint32_t)pos, (uint32_t)(pos >> 32) | (a.self << 8), left, k | (fl << 16));
+                }
+                pos = beg;
+                left = n_sets;
+                k = enter_k;
+                fl = enter_fl | (seq ? F_SEQ : 0u);
+                have = true;
+                enter = NONE;
+                continue;
+            }
+            if (!have || left == 0) {                                 // row done: pop
+                if (sp == 0) {
+                    res = RES_FALSE;
+                    break;
+                }
+                const uint4 f = fr[sp - 1];
+                const uint32_t part = f.y >> 8;
+                if (part != a.self) {                                 // the parent lives elsewhere
+                    e_dest = part;
+                    e_kind = K_RESUME;
+                    break;
+                }
+                --sp;
+                pos = (uint64_t)f.x | ((uint64_t)(f.y & 0xFFu) << 32);
+                left = f.z;
+                k = f.w & 0xFFFFu;
+                fl = f.w >> 16;
+                have = true;
+                continue;
+            }
+            const uint32_t e = a.arena[pos];
+            ++pos;
+            --left;
+            if (e & EDGE_SET) {
+                const uint32_t child = e & EDGE_VAL;
+                const uint64_t cw4 = (uint64_t)child * HDR_WORDS;
+                const uint4 ch = *reinterpret_cast<const uint4*>(a.arena + cw4);
+                const bool remote = (ch.z & HDR_REMOTE) != 0;
+                const uint64_t rvid = remote ? vid_row(ch.x, ch.y) : vid_row(a.self, child);
+                uint64_t vid = rvid;
+                if (fl & F_SEQ) {
+                    const uint32_t c = coll_find(a.coll, a.coll_mask, e);
+                    if (c != NONE) vid = vid_class(c);
+                }
+                if (fl & F_TOP) V.fresh();                            // a fresh map per top-level tuple
+                const int t = V.test_add(vid);
+                if (t == 2) {
+                    res = RES_BIG;
+                    break;
+                }
+                if (t == 1) continue;
+                if (tset && rvid == T64) {                            // engine.go:54-57
+                    res = RES_TRUE;
+                    break;
+                }
+                if (k < 2) continue;                                  // remaining depth after the hop >= 1
+                if (!tset && (ch.z & HDR_CLOSURE) && !((a.arena[cw4 - CB_WORDS + cw] >> cb) & 1u))
+                    continue;                                         // T is not below this set
+                if (remote) {                                         // the walk goes on on the owner
+                    if (left > 0) {
+                        if (sp >= MIG_FRAMES) {
+                            res = RES_UNDECIDED;
+                            break;
+                        }
+                        fr[sp++] = make_uint4((uint32_t)pos, (uint32_t)(pos >> 32) | (a.self << 8), left, k | (fl << 16));
+                    }
+                    e_dest = ch.x;
+                    e_kind = K_ENTER;
+                    e_enter = ch.y;
+                    e_k = k - 1;
+                    break;
+                }
+                enter = child;
+                enter_k = k - 1;
+                enter_fl = 0;
+            } else {                                                  // a subject id of an ordered row
+                int t = 0;
+                if (!(fl & F_TOP)) {
+                    const uint32_t c = coll_find(a.coll, a.coll_mask, e);
+                    if (c != NONE) t = V.test_add(vid_class(c));
+                }
+                if (t == 2) {
+                    res = RES_BIG;
+                    break;
+                }
+                if (t == 0 && !tset && e == T) res = RES_TRUE;
+            }
+        }
+        if (res == RES_BIG) {                                         // re-run on the big tier
+            if (a.big) {
+                a.big[atomicAdd(a.n_big, 1u)] = rj;
+                continue;
+            }
+            res = RES_UNDECIDED;
+        }
+        uint32_t units = 2, nvo = 0, nso = 0;
+        if (res >= 0) {
+            if (origin == a.self) {
+                a.allowed[idx] = (uint8_t)res;
+                atomicAdd(a.stats + 0, 1u);
+                if (res == RES_UNDECIDED) atomicAdd(a.stats + 1, 1u);
+                continue;
+            }
+            if (res == RES_UNDECIDED) atomicAdd(a.stats + 1, 1u);
+            e_dest = origin;
+            e_kind = K_DECISION;
+        } else {
+            nso = sp;
+            nvo = V.n;
+            units = 2 + nso + (nvo + 1) / 2;
+        }
+        const unsigned long long u = atomicAdd(a.pool_used, (unsigned long long)units);
+        if (u + units > a.pool_cap) {
+            a.spill[atomicAdd(a.n_spill, 1u)] = rj;
+            continue;
+        }
+        uint32_t* o = a.pool + u * 4ull;
+        // (an ENTER record's row is never a top-level row: enter flags 0)
+        const uint32_t oinfo = e_kind | (tset ? 4u : 0u) | ((res >= 0 ? (uint32_t)res : 0u) << 3) | (origin << 8);
+        *reinterpret_cast<uint4*>(o) = make_uint4(idx, oinfo, h0.z, h0.w);
+        *reinterpret_cast<uint4*>(o + 4) = make_uint4(e_enter, e_k, nso, nvo);
+        for (uint32_t i = 0; i < nso; ++i) *reinterpret_cast<uint4*>(o + HEAD_WORDS + 4ull * i) = fr[i];
+        uint64_t* ov = reinterpret_cast<uint64_t*>(o + HEAD_WORDS + 4ull * nso);
+        for (uint32_t i = 0; i < nvo; ++i) ov[i] = V.log[i];
+        if (nvo & 1u) ov[nvo] = 0;
+        const uint32_t at = atomicAdd(a.out_count, 1u);
+        a.out_dest[at] = e_dest;
+        a.out_unit[at] = (uint32_t)u;
+        a.out_len[at] = units;
+    }
+    a.lane_epoch[slot] = V.epoch;
+}
+
+// START records of a routed batch (row-id requests of this part): the depth clamp
+// (engine.go:118-120), the row's handle, a set target's global identity.  Trivial requests become
+// DECISION records for this part.
+__global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restrict__ q, uint32_t n, int32_t gmd,
+                                                 const uint32_t* __restrict__ g_handle,
+                                                 const uint8_t* __restrict__ owner, uint32_t n_rows, uint32_t self,
+                                                 uint32_t* __restrict__ out, uint32_t* __restrict__ off,
+                                                 uint32_t* misrouted) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const keto_check_ids r = q[i];
+    int d = r.max_depth;
+    if (d <= 0 || gmd < d) d = gmd;
+    uint32_t info = K_ENTER | (F_TOP << 5) | (self << 8);
+    uint32_t t_lo = r.target, t_hi = 0, enter = NONE;
+    bool trivial = r.row == KETO_NO_ROW || d <= 0 || r.target == KETO_NO_TARGET;
+    if (!trivial) {
+        if (r.row >= n_rows || owner[r.row] != self) {
+            atomicAdd(misrouted, 1u);
+            trivial = true;
+        } else {
+            enter = g_handle[r.row];
+        }
+    }
+    if (!trivial && (r.flags & 1u)) {
+        info |= 4u;
+        if (r.target >= n_rows) {
+            trivial = true;                                      // no such row: no tuple names it
+        } else {
+            t_lo = g_handle[r.target];
+            t_hi = owner[r.target];
+        }
+    }
+    if (trivial) info = K_DECISION | (self << 8);              // denied (decision 0)
+    uint32_t* o = out + (uint64_t)i * 8;
+    *reinterpret_cast<uint4*>(o) = make_uint4(i, info, t_lo, t_hi);
+    *reinterpret_cast<uint4*>(o + 4) = make_uint4(enter, (uint32_t)d, 0u, 0u);
+    off[i] = 2 * i;
+}
+
+// group the round's output records by destination part: counts, then a scatter in which every
+// record takes its place with one 64-bit atomic (records << 36 | units) on its destination cursor
+__global__ void __launch_bounds__(256) mig_count(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ len,
+                                                 const uint32_t* __restrict__ n, unsigned long long* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *n) return;
+    atomicAdd(cnt + dest[i], (1ull << 36) | len[i]);
+}
+__global__ void __launch_bounds__(256) mig_scatter(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ unit,
+                                                   const uint32_t* __restrict__ len, const uint32_t* __restrict__ n,
+                                                   const uint32_t* __restrict__ pool,
+                                                   unsigned long long* __restrict__ cursor,
+                                                   const uint64_t* __restrict__ unit_base,
+                                                   const uint32_t* __restrict__ rec_base, uint32_t* __restrict__ send,
+                                                   uint32_t* __restrict__ send_off) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *n) return;
+    const uint32_t d = dest[i], l = len[i];
+    const unsigned long long c = atomicAdd(cursor + d, (1ull << 36) | l);
+    const uint64_t u_in = c & ((1ull << 36) - 1), r_in = c >> 36;
+    const uint4* src = reinterpret_cast<const uint4*>(pool) + unit[i];
+    uint4* dst = reinterpret_cast<uint4*>(send) + unit_base[d] + u_in;
+    for (uint32_t k = 0; k < l; ++k) dst[k] = src[k];
+    send_off[rec_base[d] + r_in] = (uint32_t)u_in;
+}
+
+template <class T>
+T* dalloc(uint64_t n) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    const hipError_t e = hipMalloc(&p, n * sizeof(T));
+    if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+    return (T*)p;
+}
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+struct Lanes {
+    uint64_t* vtab = nullptr;
+    uint64_t* vlog = nullptr;
+    uint4* frames = nullptr;
+    uint32_t* epoch = nullptr;
+    uint32_t n = 0, vcap = 0;
+    void alloc(uint32_t lanes, uint32_t cap) {
+        n = lanes;
+        vcap = cap;
+        vtab = dalloc<uint64_t>((uint64_t)lanes * cap);
+        HIP_OK(hipMemset(vtab, 0, (uint64_t)lanes * cap * 8));
+        vlog = dalloc<uint64_t>((uint64_t)lanes * (cap / 2));
+        frames = dalloc<uint4>((uint64_t)lanes * MIG_FRAMES);
+        epoch = dalloc<uint32_t>(lanes);
+        HIP_OK(hipMemset(epoch, 0, (uint64_t)lanes * 4));
+        // the memsets run on the null stream, which does not order the caller's non-blocking
+        // streams: finish them before any batch uses the lanes (a late epoch reset would bring
+        // back the epochs of marks still in the tables)
+        HIP_OK(hipDeviceSynchronize());
+    }
+    void release() {
+        dfree(vtab);
+        dfree(vlog);
+        dfree(frames);
+        dfree(epoch);
+    }
+};
+
+}  // namespace
+
+struct MigState {
+    int device = 0;
+    uint32_t n_rows = 0;
+    uint32_t* g_handle = nullptr;
+    uint8_t* owner = nullptr;
+    Lanes small, bigl;
+    // the batch
+    uint8_t* allowed = nullptr;
+    uint32_t n = 0;
+    int32_t gmd = 5;
+    bool active = false;
+    // START records
+    uint32_t* start = nullptr;
+    uint32_t* start_off = nullptr;
+    uint64_t start_cap = 0;
+    // outputs of a round
+    uint32_t* pool = nullptr;
+    uint64_t pool_cap = 0;             // units
+    uint32_t *out_dest = nullptr, *out_unit = nullptr, *out_len = nullptr;
+    uint32_t *spill = nullptr, *spill2 = nullptr, *bigq = nullptr;
+    uint64_t out_cap = 0;
+    uint32_t* ctr = nullptr;           // [0] out_count [1] n_spill [2] n_big [3] scratch [4..7] stats
+    unsigned long long* pool_used = nullptr;
+    unsigned long long* cursor = nullptr;   // [MIG_MAX_PARTS]
+    uint64_t* unit_base = nullptr;          // [MIG_MAX_PARTS] source / destination unit bases
+    uint32_t* rec_base = nullptr;           // [MIG_MAX_PARTS + 1]
+    uint64_t* dunit_base = nullptr;
+    uint32_t* drec_base = nullptr;
+    uint32_t* send = nullptr;
+    uint64_t send_cap = 0;
+    uint32_t* send_off = nullptr;
+    uint64_t send_off_cap = 0;
+
+    ~MigState() {
+        (void)hipSetDevice(device);
+        dfree(g_handle);
+        dfree(owner);
+        small.release();
+        bigl.release();
+        dfree(start);
+        dfree(start_off);
+        dfree(pool);
+        dfree(out_dest);
+        dfree(out_unit);
+        dfree(out_len);
+        dfree(spill);
+        dfree(spill2);
+        dfree(bigq);
+        dfree(ctr);
+        dfree(pool_used);
+        dfree(cursor);
+        dfree(unit_base);
+        dfree(rec_base);
+        dfree(dunit_base);
+        dfree(drec_base);
+        dfree(send);
+        dfree(send_off);
+    }
+};
+
+void MigStateDeleter::operator()(MigState* m) const { delete m; }
+
+void mig_release(Snapshot& S) { S.mig.reset(); }
+
+namespace {
+
+MigState& mig_state(Snapshot& S) {
+    if (S.part_mode != PART_MIGRATE) throw Error{KETO_E_INVALID, "not a migrating part (keto_snapshot_upload_part_mode)"};
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    if (!S.mig_ready) throw Error{KETO_E_INVALID, "closure filter exchange not finished (keto_part_closure_done)"};
+    if (!S.mig) {
+        const DevView dv = device_view(S);
+        HIP_OK(hipSetDevice(dv.device));
+        auto M = std::unique_ptr<MigState, MigStateDeleter>(new MigState);
+        M->device = dv.device;
+        M->n_rows = S.n_rows();
+        M->g_handle = dalloc<uint32_t>(S.n_rows());
+        HIP_OK(hipMemcpy(M->g_handle, S.g_handle.data(), (uint64_t)S.n_rows() * 4, hipMemcpyHostToDevice));
+        std::vector<uint8_t> own(S.n_rows());
+        for (uint32_t r = 0; r < S.n_rows(); ++r) own[r] = (uint8_t)S.root_owner(r, S.n_parts);
+        M->owner = dalloc<uint8_t>(S.n_rows());
+        HIP_OK(hipMemcpy(M->owner, own.data(), own.size(), hipMemcpyHostToDevice));
+        M->ctr = dalloc<uint32_t>(8);
+        M->pool_used = dalloc<unsigned long long>(1);
+        M->cursor = dalloc<unsigned long long>(MIG_MAX_PARTS);
+        M->unit_base = dalloc<uint64_t>(MIG_MAX_PARTS);
+        M->rec_base = dalloc<uint32_t>(MIG_MAX_PARTS + 1);
+        M->dunit_base = dalloc<uint64_t>(MIG_MAX_PARTS);
+        M->drec_base = dalloc<uint32_t>(MIG_MAX_PARTS + 1);
+        S.mig.reset(M.release());
+    }
+    return *S.mig;
+}
+
+void ensure_out(MigState& M, uint64_t n_in) {
+    if (M.out_cap >= n_in && M.out_dest) return;
+    dfree(M.out_dest);
+    dfree(M.out_unit);
+    dfree(M.out_len);
+    dfree(M.spill);
+    dfree(M.spill2);
+    dfree(M.bigq);
+    M.out_cap = std::max<uint64_t>(n_in, 4096);
+    M.out_dest = dalloc<uint32_t>(M.out_cap);
+    M.out_unit = dalloc<uint32_t>(M.out_cap);
+    M.out_len = dalloc<uint32_t>(M.out_cap);
+    M.spill = dalloc<uint32_t>(M.out_cap);
+    M.spill2 = dalloc<uint32_t>(M.out_cap);
+    M.bigq = dalloc<uint32_t>(M.out_cap);
+}
+
+// grow the output pool, keeping the records already written (all below the old capacity)
+void grow_pool(MigState& M, uint64_t want, hipStream_t st) {
+    uint64_t cap = std::max<uint64_t>(want, 1ull << 20);
+    if (cap <= M.pool_cap) return;
+    uint32_t* p = dalloc<uint32_t>(cap * 4);
+    if (M.pool) HIP_OK(hipMemcpyAsync(p, M.pool, M.pool_cap * 16, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    dfree(M.pool);
+    M.pool = p;
+    M.pool_cap = cap;
+}
+
+// Process one round's input (n_in records in n_src source segments) and group the outputs.
+void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d_in_off, uint32_t n_in,
+               const uint32_t* in_records, const uint64_t* in_units, uint32_t n_src, hipStream_t st, MigOut& out) {
+    const DevView dv = device_view(S);
+    const uint32_t P = S.n_parts;
+    ensure_out(M, n_in);
+    if (!M.pool) grow_pool(M, std::max<uint64_t>((uint64_t)n_in * 4, 1ull << 20), st);
+    if (!M.small.vtab) M.small.alloc(LANES_SMALL, VCAP_SMALL);
+    if (!M.bigl.vtab) M.bigl.alloc(LANES_BIG, VCAP_BIG);
+    // source segments
+    uint32_t rb[MIG_MAX_PARTS + 1];
+    uint64_t ub[MIG_MAX_PARTS];
+    rb[0] = 0;
+    uint64_t acc = 0;
+    for (uint32_t s = 0; s < n_src; ++s) {
+        ub[s] = acc;
+        acc += in_units[s];
+        rb[s + 1] = rb[s] + in_records[s];
+    }
+    if (rb[n_src] != n_in) throw Error{KETO_E_INVALID, "record counts do not add up"};
+    HIP_OK(hipMemcpyAsync(M.rec_base, rb, (n_src + 1) * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(M.unit_base, ub, n_src * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(M.ctr, 0, 8 * 4, st));
+    HIP_OK(hipMemsetAsync(M.pool_used, 0, 8, st));
+    MigArgs a{};
+    a.arena = dv.arena;
+    a.coll = dv.coll;
+    a.coll_mask = dv.coll_mask;
+    a.self = S.part;
+    a.in = d_in;
+    a.in_off = d_in_off;
+    a.rec_base = M.rec_base;
+    a.unit_base = M.unit_base;
+    a.n_src = n_src;
+    a.n_in = n_in;
+    a.pool_used = M.pool_used;
+    a.out_dest = M.out_dest;
+    a.out_unit = M.out_unit;
+    a.out_len = M.out_len;
+    a.out_count = M.ctr + 0;
+    a.n_spill = M.ctr + 1;
+    a.n_big = M.ctr + 2;
+    a.allowed = M.allowed;
+    a.stats = M.ctr + 4;
+    auto launch = [&](Lanes& L, const uint32_t* list, const uint32_t* n_list, uint32_t n_max, uint32_t* big,
+                      uint32_t* spill) {
+        a.list = list;
+        a.n_list = n_list;
+        a.big = big;
+        a.spill = spill;
+        a.pool = M.pool;
+        a.pool_cap = M.pool_cap;
+        a.vtab = L.vtab;
+        a.vlog = L.vlog;
+        a.frames = L.frames;
+        a.lane_epoch = L.epoch;
+        a.vcap = L.vcap;
+        const uint32_t lanes = (uint32_t)std::min<uint64_t>(L.n, ((uint64_t)n_max + 255) / 256 * 256);
+        if (lanes == 0) return;
+        hipLaunchKernelGGL(mig_kernel, dim3(lanes / 256), dim3(256), 0, st, a);
+        HIP_OK(hipGetLastError());
+    };
+    // small tier over every input, then the big tier over the inputs whose maps outgrew it, then the
+    // inputs whose output did not fit the pool (with a bigger pool), until none is left
+    uint32_t cnt[8];
+    if (n_in) launch(M.small, nullptr, nullptr, n_in, M.bigq, M.spill);
+    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    uint32_t n_big = cnt[2];
+    for (int pass = 0; pass < 2; ++pass) {       // pass 0: the small tier's spills, pass 1: the big tier
+        uint32_t n_sp = cnt[1];
+        bool small_tier = pass == 0;
+        while (n_sp) {
+            // rerun the spilled inputs with a pool twice the size (list copied: the rerun spills into spill)
+            unsigned long long used = 0;
+            HIP_OK(hipMemcpyAsync(&used, M.pool_used, 8, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            const unsigned long long cap_used = std::min<unsigned long long>(used, M.pool_cap);
+            grow_pool(M, std::max<uint64_t>(M.pool_cap * 2, used * 2), st);
+            HIP_OK(hipMemcpyAsync(M.spill2, M.spill, (uint64_t)n_sp * 4, hipMemcpyDeviceToDevice, st));
+            HIP_OK(hipMemcpyAsync(M.ctr + 3, M.ctr + 1, 4, hipMemcpyDeviceToDevice, st));
+            HIP_OK(hipMemsetAsync(M.ctr + 1, 0, 4, st));
+            HIP_OK(hipMemcpyAsync(M.pool_used, &cap_used, 8, hipMemcpyHostToDevice, st));
+            if (small_tier) launch(M.small, M.spill2, M.ctr + 3, n_sp, M.bigq, M.spill);
+            else launch(M.bigl, M.spill2, M.ctr + 3, n_sp, nullptr, M.spill);
+            HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            n_sp = cnt[1];
+        }
+        if (pass == 0) {
+            n_big = cnt[2];
+            if (n_big == 0) break;
+            HIP_OK(hipMemsetAsync(M.ctr + 1, 0, 4, st));
+            launch(M.bigl, M.bigq, M.ctr + 2, n_big, nullptr, M.spill);
+            HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+        }
+    }
+    const uint32_t n_out = cnt[0];
+    if (getenv("KETO_MIG_DEBUG"))
+        fprintf(stderr, "mig part %u: in %u big %u out %u decided %u undecided %u pool %llu\n", S.part, n_in, n_big, n_out,
+                cnt[4], cnt[5], (unsigned long long)M.pool_cap);
+    // group by destination
+    HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
+    if (n_out) {
+        hipLaunchKernelGGL(mig_count, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_len, M.ctr + 0,
+                           M.cursor);
+        HIP_OK(hipGetLastError());
+    }
+    unsigned long long c[MIG_MAX_PARTS];
+    HIP_OK(hipMemcpyAsync(c, M.cursor, MIG_MAX_PARTS * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    uint64_t dub[MIG_MAX_PARTS], total_units = 0;
+    uint32_t drb[MIG_MAX_PARTS + 1];
+    drb[0] = 0;
+    for (uint32_t p = 0; p < P; ++p) {
+        out.units[p] = c[p] & ((1ull << 36) - 1);
+        out.records[p] = (uint32_t)(c[p] >> 36);
+        dub[p] = total_units;
+        total_units += out.units[p];
+        drb[p + 1] = drb[p] + out.records[p];
+    }
+    for (uint32_t p = P; p < MIG_MAX_PARTS; ++p) {
+        out.units[p] = 0;
+        out.records[p] = 0;
+    }
+    if (M.send_cap < total_units || !M.send) {
+        dfree(M.send);
+        M.send_cap = std::max<uint64_t>(total_units * 2, 1ull << 16);
+        M.send = dalloc<uint32_t>(M.send_cap * 4);
+    }
+    if (M.send_off_cap < n_out || !M.send_off) {
+        dfree(M.send_off);
+        M.send_off_cap = std::max<uint64_t>((uint64_t)n_out * 2, 4096);
+        M.send_off = dalloc<uint32_t>(M.send_off_cap);
+    }
+    if (n_out) {
+        HIP_OK(hipMemcpyAsync(M.dunit_base, dub, P * 8, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(M.drec_base, drb, (P + 1) * 4, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
+        hipLaunchKernelGGL(mig_scatter, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_unit, M.out_len,
+                           M.ctr + 0, M.pool, M.cursor, M.dunit_base, M.drec_base, M.send, M.send_off);
+        HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    out.d_buf = M.send;
+    out.d_off = M.send_off;
+    out.decided = cnt[4];
+    out.undecided = cnt[5];
+    out.started = cnt[6];
+    out.resumed = cnt[7];
+}
+
+}  // namespace
+
+void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
+               MigOut& out) {
+    std::lock_guard<std::mutex> lk(S.mu);
+    MigState& M = mig_state(S);
+    HIP_OK(hipSetDevice(M.device));
+    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)device_view(S).stream;
+    if (gmd > 65535) gmd = 65535;
+    if (n && (!d_reqs || !d_allowed)) throw Error{KETO_E_INVALID, "NULL argument"};
+    M.allowed = d_allowed;
+    M.n = n;
+    M.gmd = gmd;
+    M.active = true;
+    if (M.start_cap < n || !M.start) {
+        dfree(M.start);
+        dfree(M.start_off);
+        M.start_cap = std::max<uint64_t>(n, 4096);
+        M.start = dalloc<uint32_t>(M.start_cap * 8);
+        M.start_off = dalloc<uint32_t>(M.start_cap);
+    }
+    HIP_OK(hipMemsetAsync(M.ctr, 0, 4, st));
+    if (n) {
+        hipLaunchKernelGGL(mig_start, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, n, gmd, M.g_handle, M.owner,
+                           M.n_rows, S.part, M.start, M.start_off, M.ctr);
+        HIP_OK(hipGetLastError());
+    }
+    uint32_t bad = 0;
+    HIP_OK(hipMemcpyAsync(&bad, M.ctr, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name rows another part owns"};
+    const uint32_t recs = n;
+    const uint64_t units = 2ull * n;
+    run_round(S, M, M.start, M.start_off, n, &recs, &units, 1, st, out);
+}
+
+void mig_round(Snapshot& S, const void* d_in, const uint32_t* d_in_off, const uint32_t* in_records,
+               const uint64_t* in_units, void* stream, MigOut& out) {
+    std::lock_guard<std::mutex> lk(S.mu);
+    MigState& M = mig_state(S);
+    HIP_OK(hipSetDevice(M.device));
+    if (!M.active) throw Error{KETO_E_INVALID, "no migrating batch (keto_mig_begin)"};
+    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)device_view(S).stream;
+    uint64_t n_in = 0;
+    for (uint32_t s = 0; s < S.n_parts; ++s) n_in += in_records[s];
+    if (n_in > 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "too many records in one round"};
+    if (n_in && (!d_in || !d_in_off)) throw Error{KETO_E_INVALID, "NULL argument"};
+    run_round(S, M, static_cast<const uint32_t*>(d_in), d_in_off, (uint32_t)n_in, in_records, in_units, S.n_parts, st,
+              out);
+}
+
+void device_copy(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (bytes == 0) return;
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+}
+
+}  // namespace keto

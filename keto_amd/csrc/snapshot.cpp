@@ -400,56 +400,70 @@ uint32_t Snapshot::row_hlog2(uint32_t r) const {
     return std::max<uint32_t>(2, ceil_log2(2ull * x.n_ids));                      // load <= 1/2, >= 1 bucket
 }
 
-void compute_layout(Snapshot& S) {
+namespace {
+// The arena layout of one part: which rows it holds, where, and (PART_MIGRATE) its stubs.
+struct PartLayout {
+    std::vector<uint32_t> unit_of_row, rows_by_unit, layout_units;
+    std::vector<uint8_t> stub;
+    uint64_t n_units = 0, shared_words = 0, n_stubs = 0;
+};
+
+void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t part, uint32_t n_parts, int mode,
+                 PartLayout& L) {
     const uint32_t R = S.n_rows();
-    S.unit_of_row.resize(R);
-    // Hot rows first: rows that many subject sets point at (popular folders, groups) are laid out
-    // densely at the front of the arena, most-referenced first, so the lines most traversals touch
-    // stay in L2 and the Infinity Cache.  A stable counting sort by floor(log2(in-degree)).
-    std::vector<uint8_t> band(R, 0);
-    {
-        std::vector<uint32_t> indeg(R, 0);
-        for (uint32_t r = 0; r < R; ++r) {
-            const auto ed = S.row_edges(r);
-            for (uint64_t i = 0; i < ed.second; ++i) {
-                const uint32_t e = ed.first[i];
-                if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
-            }
-        }
-        S.is_root.assign(R, 0);
-        for (uint32_t r = 0; r < R; ++r) {
-            band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
-            S.is_root[r] = indeg[r] == 0;
-        }
-    }
-    // edge partitioning: root rows of other parts are left out of this device's arena
+    L.unit_of_row.assign(R, NO_UNIT);
+    // edge partitioning: PART_SHARED leaves other parts' root rows out of this device's arena;
+    // PART_MIGRATE keeps only this part's rows, plus a stub for every other part's row that one of
+    // them points at
     std::vector<uint8_t> keep(R, 1);
-    uint32_t kept = R;
-    if (S.n_parts > 1)
-        for (uint32_t r = 0; r < R; ++r)
-            if (S.is_root[r] && S.root_owner(r, S.n_parts) != S.part) {
-                keep[r] = 0;
-                --kept;
+    L.stub.clear();
+    L.n_stubs = 0;
+    if (n_parts > 1) {
+        if (mode == PART_MIGRATE) {
+            L.stub.assign(R, 0);
+            for (uint32_t r = 0; r < R; ++r) keep[r] = S.root_owner(r, n_parts) == part;
+            for (uint32_t r = 0; r < R; ++r) {
+                if (!keep[r]) continue;
+                const auto ed = S.row_edges(r);
+                for (uint64_t i = 0; i < ed.second; ++i) {
+                    const uint32_t e = ed.first[i];
+                    if (!(e & EDGE_SET) || e == EDGE_POISON) continue;
+                    const uint32_t t = e & EDGE_VAL;
+                    if (t < R && !keep[t] && !L.stub[t]) {
+                        L.stub[t] = 1;
+                        ++L.n_stubs;
+                    }
+                }
             }
-    std::vector<uint64_t> start(35, 0);                  // key = 33 - band: hottest first
-    for (uint32_t r = 0; r < R; ++r) start[33 - band[r] + 1] += keep[r];
-    for (int b = 1; b < 35; ++b) start[b] += start[b - 1];
-    S.rows_by_unit.assign(kept, 0);
-    for (uint32_t r = 0; r < R; ++r) {
-        S.unit_of_row[r] = NO_UNIT;
-        if (keep[r]) S.rows_by_unit[start[33 - band[r]]++] = r;
+        } else {
+            for (uint32_t r = 0; r < R; ++r)
+                if (S.is_root[r] && S.root_owner(r, n_parts) != part) keep[r] = 0;
+        }
     }
-    S.layout_units.assign(kept, 0);
-    S.shared_words = 0;
+    auto held = [&](uint32_t r) { return keep[r] || (!L.stub.empty() && L.stub[r]); };
+    uint64_t kept = 0;
+    std::vector<uint64_t> start(35, 0);                  // key = 33 - band: hottest first
+    for (uint32_t r = 0; r < R; ++r)
+        if (held(r)) {
+            ++start[33 - band[r] + 1];
+            ++kept;
+        }
+    for (int b = 1; b < 35; ++b) start[b] += start[b - 1];
+    L.rows_by_unit.assign(kept, 0);
+    for (uint32_t r = 0; r < R; ++r)
+        if (held(r)) L.rows_by_unit[start[33 - band[r]]++] = r;
+    L.layout_units.assign(kept, 0);
+    L.shared_words = 0;
     // test hook: start the layout this many words into the arena, so a small graph straddles the
     // segment boundary at 2^32 words (tests/test_gpu_synth.py)
     uint64_t w = 0;
     if (const char* base = getenv("KETO_TEST_ARENA_BASE")) w = strtoull(base, nullptr, 0) & ~(uint64_t)(LINE_WORDS - 1);
-    for (uint32_t x = 0; x < kept; ++x) {
-        const uint32_t r = S.rows_by_unit[x];
-        const uint32_t h = S.row_hlog2(r);
+    for (uint64_t x = 0; x < kept; ++x) {
+        const uint32_t r = L.rows_by_unit[x];
+        const bool stub = !keep[r];                                  // header + closure block only
+        const uint32_t h = stub ? 0 : S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
-        const uint64_t n = row_size(S, r);
+        const uint64_t n = stub ? 0 : row_size(S, r);
         // line placement: a row that fits in a 128-B line never straddles one (closure filter,
         // header, window and id table come in with one miss); a bigger row keeps closure filter +
         // header + window in one line
@@ -470,12 +484,63 @@ void compute_layout(Snapshot& S) {
         if (w < (1ull << 32) && w + fit > (1ull << 32)) w = align(1ull << 32);   // rows stay in a segment
         const uint64_t unit = (w + table + cb) / HDR_WORDS;
         if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
-        S.unit_of_row[r] = (uint32_t)unit;
-        S.layout_units[x] = (uint32_t)unit;
-        if (!S.is_root[r]) S.shared_words += total;
+        L.unit_of_row[r] = (uint32_t)unit;
+        L.layout_units[x] = (uint32_t)unit;
+        if (!S.is_root[r] && !stub) L.shared_words += total;
         w += total;
     }
-    S.n_units = w / HDR_WORDS;
+    L.n_units = w / HDR_WORDS;
+}
+}  // namespace
+
+void compute_layout(Snapshot& S) {
+    const uint32_t R = S.n_rows();
+    // Hot rows first: rows that many subject sets point at (popular folders, groups) are laid out
+    // densely at the front of the arena, most-referenced first, so the lines most traversals touch
+    // stay in L2 and the Infinity Cache.  A stable counting sort by floor(log2(in-degree)).
+    std::vector<uint8_t> band(R, 0);
+    {
+        std::vector<uint32_t> indeg(R, 0);
+        for (uint32_t r = 0; r < R; ++r) {
+            const auto ed = S.row_edges(r);
+            for (uint64_t i = 0; i < ed.second; ++i) {
+                const uint32_t e = ed.first[i];
+                if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
+            }
+        }
+        S.is_root.assign(R, 0);
+        for (uint32_t r = 0; r < R; ++r) {
+            band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
+            S.is_root[r] = indeg[r] == 0;
+        }
+    }
+    if (S.part_mode == PART_MIGRATE && S.n_parts > MIG_MAX_PARTS)
+        throw Error{KETO_E_INVALID, "a migrating partition has at most 31 parts"};
+    PartLayout L;
+    layout_part(S, band, S.part, S.n_parts, S.part_mode, L);
+    S.unit_of_row = std::move(L.unit_of_row);
+    S.rows_by_unit = std::move(L.rows_by_unit);
+    S.layout_units = std::move(L.layout_units);
+    S.stub = std::move(L.stub);
+    S.n_stubs = L.n_stubs;
+    S.n_units = L.n_units;
+    S.shared_words = L.shared_words;
+    S.g_handle.clear();
+    if (S.part_mode == PART_MIGRATE) {
+        // every row's handle on its owner part: the layouts of the other parts are computed here too
+        // (each is a deterministic function of the snapshot and the part)
+        S.g_handle.assign(R, NO_UNIT);
+        for (uint32_t q = 0; q < S.n_parts; ++q) {
+            const std::vector<uint32_t>* u = &S.unit_of_row;
+            PartLayout Q;
+            if (q != S.part) {
+                layout_part(S, band, q, S.n_parts, S.part_mode, Q);
+                u = &Q.unit_of_row;
+            }
+            for (uint32_t r = 0; r < R; ++r)
+                if (S.root_owner(r, S.n_parts) == q) S.g_handle[r] = (*u)[r];
+        }
+    }
     S.row_cb.assign(R, 0);
     for (uint32_t r = 0; r < R; ++r) S.row_cb[r] = !S.is_root[r];
     S.row_place.clear();

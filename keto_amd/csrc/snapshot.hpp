@@ -73,6 +73,15 @@ constexpr uint32_t HDR_CLOSURE = 8u;            // a closure filter precedes the
 // arena's tail; its identity header (whose handle every subject set holds, and whose closure filter
 // stays in front of it) becomes a forward: word 0 = handle of the row's current header.
 constexpr uint32_t HDR_FWD = 16u;
+// Migrating partition (PART_MIGRATE): a stub stands for a row another part owns that some set edge
+// of this part points at.  It is a closure block (the remote row's closure filter, filled in by
+// the filter exchange) and a header {owner part, handle on the owner, HDR_REMOTE | HDR_CLOSURE, 0}
+// with no edges; a walk that enters it continues on the owner (migrate.hip).
+constexpr uint32_t HDR_REMOTE = 32u;
+// upload modes of an edge-partitioned snapshot (keto_snapshot_upload_part_mode)
+constexpr int PART_SHARED = 0;    // rows some set points at on every part, root rows by hash
+constexpr int PART_MIGRATE = 1;   // every row on one part by hash, stubs for remote set targets
+constexpr uint32_t MIG_MAX_PARTS = 31;
 // Closure filter of a row some subject set points at: a 704-bit, one-hash bloom filter of every
 // subject id reachable from the row through any number of subject sets (its own ids included).  A
 // check entering such a row for a requested id the filter rules out skips the row: every node the
@@ -142,6 +151,10 @@ struct DeviceState;      // engine.hip
 struct DeviceStateDeleter {
     void operator()(DeviceState* d) const;   // engine.hip
 };
+struct MigState;         // migrate.hip
+struct MigStateDeleter {
+    void operator()(MigState* m) const;      // migrate.hip
+};
 
 struct Snapshot {
     // ---- config
@@ -182,8 +195,21 @@ struct Snapshot {
     // kept on every part; root rows (never a subject set) only on part hash(ns, object) % n_parts
     std::vector<uint8_t> is_root;
     uint32_t part = 0, n_parts = 1;
-    uint32_t root_owner(uint32_t r, uint32_t parts) const;   // part owning root row r
-    bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT; }
+    int part_mode = PART_SHARED;
+    uint32_t root_owner(uint32_t r, uint32_t parts) const;   // hash(namespace id, object) % parts
+    // owner of row r under this snapshot's partitioning: -1 = on every part (PART_SHARED non-root rows)
+    int32_t row_owner(uint32_t r, uint32_t parts) const {
+        return (part_mode == PART_MIGRATE || is_root[r]) ? (int32_t)root_owner(r, parts) : -1;
+    }
+    // PART_MIGRATE: stub[r] = r is another part's row with a stub here; g_handle[r] = r's handle on its
+    // owner part (every row), for the request translation of set targets and for the stubs
+    std::vector<uint8_t> stub;
+    std::vector<uint32_t> g_handle;
+    uint64_t n_stubs = 0;
+    bool mig_ready = false;   // PART_MIGRATE: closure filters final (part_closure_done, or one part)
+    // r is held by this device (owned, or on every part); stubs are not rows of this part
+    bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT && (stub.empty() || !stub[r]); }
+    bool mapped(uint32_t r) const { return unit_of_row[r] != NO_UNIT; }   // a row or a stub here
     uint64_t n_units = 0;
     uint64_t shared_words = 0;            // arena words of the rows every part keeps (non-root rows)
     uint32_t handle(uint32_t row) const { return unit_of_row[row]; }
@@ -223,6 +249,7 @@ struct Snapshot {
     // ---- device
     int device = -1;
     std::unique_ptr<DeviceState, DeviceStateDeleter> dev;
+    std::unique_ptr<MigState, MigStateDeleter> mig;      // migrating-partition batches (migrate.hip)
     std::mutex mu;
 
     ~Snapshot();
@@ -316,6 +343,36 @@ void route_rows(const keto_check_ids* d_reqs, uint32_t n, const int16_t* d_owner
                 uint32_t n_parts, void* d_work, uint64_t work_len, keto_check_ids* d_send, uint32_t* d_order,
                 uint32_t* counts_out, void* stream);
 void unroute_rows(const uint8_t* d_back, const uint32_t* d_order, uint32_t n, uint8_t* d_out, void* stream);
+// migrating partition (engine.hip): closure-filter exchange between parts.  part_filters copies the
+// closure filters (CF_WORDS words each) of this part's rows; part_close ORs the owners' filters into
+// the stubs of `rows`, re-closes this part's filters and returns how many filters changed;
+// part_closure_done finishes the filters (signatures) or, when the exchange did not converge, sets
+// every filter to all ones (no pruning, still exact)
+void part_filters(Snapshot& s, const uint32_t* rows, uint64_t n, uint32_t* out);
+uint64_t part_close(Snapshot& s, const uint32_t* rows, uint64_t n, const uint32_t* filters);
+void part_closure_done(Snapshot& s, bool converged);
+struct DevView {             // what migrate.hip needs of a device snapshot
+    const uint32_t* arena;
+    const uint64_t* coll;
+    uint32_t coll_mask;
+    int device;
+    void* stream;
+};
+DevView device_view(const Snapshot& s);
+// migrating-partition check batches (migrate.hip); see keto_mig_begin / keto_mig_round
+struct MigOut {
+    uint64_t units[MIG_MAX_PARTS];
+    uint32_t records[MIG_MAX_PARTS];
+    const void* d_buf;
+    const uint32_t* d_off;
+    uint32_t decided, undecided, started, resumed;
+};
+void mig_begin(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
+               MigOut& out);
+void mig_round(Snapshot& s, const void* d_in, const uint32_t* d_in_off, const uint32_t* in_records,
+               const uint64_t* in_units, void* stream, MigOut& out);
+void mig_release(Snapshot& s);
+void device_copy(void* dst, const void* src, uint64_t bytes, void* stream);   // D2D, synchronous
 struct ExpandResult {
     std::vector<uint8_t> status;
     std::vector<uint64_t> offset;          // n+1

@@ -165,3 +165,178 @@ def send_back(decisions, state, out, world: int, group=None):
         dist.all_to_all_single(back, decisions.contiguous(), output_split_sizes=cs, input_split_sizes=ics, group=group)
     capi.unroute_device(back.data_ptr(), order.data_ptr(), sum(cs), out.data_ptr(),
                         torch.cuda.current_stream(out.device).cuda_stream)
+
+
+# ---------------------------------------------------------------------------------------------
+# Migrating partition (KETO_PART_MIGRATE): every row on one part, searches migrate between parts.
+#
+# The reference's DFS (internal/check/engine.go:36-114) marks nodes on first encounter in SQL
+# order, so it cannot be split into level-synchronous frontier exchanges without changing answers
+# (SURVEY.md H1).  Each search runs on the part that owns the row it is in and moves, as one
+# continuation record (its frames and visited map), when it crosses to a row another part owns
+# (repo:keto_amd/csrc/migrate.hip).  A round = every part continues the searches it received, then
+# one all-to-all delivers the records they emitted.  Closure filters (the exact pruning of
+# DESIGN.md) are closed across parts the same way before the first batch.
+
+def _prefix(xs):
+    out = [0]
+    for x in xs:
+        out.append(out[-1] + int(x))
+    return out
+
+
+class SnapshotMigEngine:
+    """The mig_* calls of one migrating part (keto_amd.capi.Snapshot) on its GPU, with the library's
+    output copied into torch tensors for the exchange layer."""
+
+    def __init__(self, snap, device="cuda:0"):
+        self.snap = snap
+        self.device = device
+
+    def _stream(self):
+        import torch
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def begin(self, routed, decisions, global_max_depth):
+        return self.snap.mig_begin(routed.data_ptr(), len(routed), decisions.data_ptr(), global_max_depth,
+                                   self._stream())
+
+    def round(self, buf, off, in_records, in_units):
+        return self.snap.mig_round(buf.data_ptr(), off.data_ptr(), in_records, in_units, self._stream())
+
+    def fetch(self, out):
+        """(records as uint8 [16 * units], unit offsets as int32 [records]) of a begin/round output."""
+        import torch
+        from . import capi
+        units, recs = sum(out["units"]), sum(out["records"])
+        buf = torch.empty(units * 16, dtype=torch.uint8, device=self.device)
+        off = torch.empty(recs, dtype=torch.int32, device=self.device)
+        st = self._stream()
+        if units:
+            capi.device_copy(buf.data_ptr(), out["d_records"], units * 16, st)
+        if recs:
+            capi.device_copy(off.data_ptr(), out["d_offsets"], recs * 4, st)
+        return buf, off
+
+
+def mig_check(engine, routed, global_max_depth=5, group=None, device="cuda:0", max_rounds=1 << 20):
+    """Decisions (uint8 [len(routed)] on `device`) of the row-id requests routed to this rank, all
+    owned by its part, on a migrating partition with one rank per part.  Every rank calls this
+    collectively.  engine: SnapshotMigEngine (or an object with the same begin/round/fetch).
+    Returns (decisions, rounds)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dec = torch.full((len(routed),), 255, dtype=torch.uint8, device=device)
+    out = engine.begin(routed, dec, global_max_depth)
+    rounds = 0
+    while True:
+        mine = sum(out["records"])
+        tot = torch.tensor([mine], dtype=torch.int64, device=device)
+        dist.all_reduce(tot, group=group)
+        if int(tot.item()) == 0:
+            return dec, rounds
+        if rounds >= max_rounds:
+            raise RuntimeError(f"migrating check did not finish in {max_rounds} rounds")
+        buf, off = engine.fetch(out)
+        units, recs = out["units"][:world], out["records"][:world]
+        cnt = torch.tensor([[u, r] for u, r in zip(units, recs)], dtype=torch.int64, device=device).reshape(-1)
+        in_cnt = torch.empty_like(cnt)
+        dist.all_to_all_single(in_cnt, cnt, group=group)
+        ic = in_cnt.reshape(world, 2).cpu().tolist()
+        in_units, in_recs = [c[0] for c in ic], [c[1] for c in ic]
+        rbuf = torch.empty(sum(in_units) * 16, dtype=torch.uint8, device=device)
+        dist.all_to_all_single(rbuf, buf, output_split_sizes=[u * 16 for u in in_units],
+                               input_split_sizes=[u * 16 for u in units], group=group)
+        roff = torch.empty(sum(in_recs), dtype=torch.int32, device=device)
+        dist.all_to_all_single(roff, off, output_split_sizes=in_recs, input_split_sizes=recs, group=group)
+        out = engine.round(rbuf, roff, in_recs, in_units)
+        rounds += 1
+
+
+def mig_check_loopback(engines, routed, global_max_depth=5, device="cuda:0", max_rounds=1 << 20):
+    """mig_check for every part in one process (all parts on one GPU, the exchange by copies):
+    SURVEY.md section 4's "test partitioning on one device before RCCL".  routed[p]: the requests
+    owned by part p.  Returns (decisions per part, rounds)."""
+    import torch
+    P = len(engines)
+    dec = [torch.full((len(r),), 255, dtype=torch.uint8, device=device) for r in routed]
+    outs = [engines[p].begin(routed[p], dec[p], global_max_depth) for p in range(P)]
+    rounds = 0
+    while sum(sum(o["records"]) for o in outs):
+        if rounds >= max_rounds:
+            raise RuntimeError(f"migrating check did not finish in {max_rounds} rounds")
+        inbox = [[None] * P for _ in range(P)]
+        for s in range(P):
+            buf, off = engines[s].fetch(outs[s])
+            ub, rb = _prefix(outs[s]["units"][:P]), _prefix(outs[s]["records"][:P])
+            for q in range(P):
+                inbox[q][s] = (buf[ub[q] * 16: ub[q + 1] * 16], off[rb[q]: rb[q + 1]])
+        for q in range(P):
+            rbuf = torch.cat([inbox[q][s][0] for s in range(P)])
+            roff = torch.cat([inbox[q][s][1] for s in range(P)])
+            in_units = [len(inbox[q][s][0]) // 16 for s in range(P)]
+            in_recs = [len(inbox[q][s][1]) for s in range(P)]
+            outs[q] = engines[q].round(rbuf, roff, in_recs, in_units)
+        rounds += 1
+    return dec, rounds
+
+
+def close_filters_loopback(parts, max_rounds=256):
+    """Closure-filter exchange of a migrating partition whose parts all live in this process:
+    rounds of (every part asks each stub's owner for its filter, then ORs the answers in and
+    re-closes) until a round changes nothing anywhere.  Returns the number of rounds."""
+    from .capi import FILTER_WORDS
+    P = len(parts)
+    stubs = [p.part_stubs() for p in parts]
+    owners = [parts[0].row_owner(s, P) for s in stubs]
+    changed, rounds = 1, 0
+    while changed and rounds < max_rounds:
+        answers = []
+        for i in range(P):
+            f = np.zeros((len(stubs[i]), FILTER_WORDS), dtype=np.uint32)
+            for q in range(P):
+                sel = owners[i] == q
+                if sel.any():
+                    f[sel] = parts[q].part_filters(stubs[i][sel])
+            answers.append(f)
+        changed = sum(parts[i].part_close(stubs[i], answers[i]) for i in range(P))
+        rounds += 1
+    for p in parts:
+        p.part_closure_done(changed == 0)
+    return rounds
+
+
+def close_filters_dist(snap, group=None, device="cpu", max_rounds=256):
+    """close_filters_loopback with one rank per part: the stub lists go to their owners once (one
+    all-to-all), then every round returns the owners' filters with one all-to-all and ends with an
+    all-reduce of the changes.  Every rank calls this collectively.  Returns the number of rounds."""
+    import torch
+    import torch.distributed as dist
+    from .capi import FILTER_WORDS
+    world = dist.get_world_size(group)
+    stubs = snap.part_stubs()
+    own = np.asarray(snap.row_owner(stubs, world), dtype=np.int64)
+    order = np.argsort(own, kind="stable")
+    stubs = np.ascontiguousarray(stubs[order])
+    counts = np.bincount(own, minlength=world).astype(np.int64)
+    c_in = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_to_all_single(c_in, torch.from_numpy(counts).to(device), group=group)
+    in_counts = c_in.cpu().numpy()
+    asked_t = torch.empty(int(in_counts.sum()), dtype=torch.int32, device=device)
+    dist.all_to_all_single(asked_t, torch.from_numpy(stubs.view(np.int32)).to(device),
+                           output_split_sizes=in_counts.tolist(), input_split_sizes=counts.tolist(), group=group)
+    asked = asked_t.cpu().numpy().view(np.uint32)
+    changed, rounds = 1, 0
+    while changed and rounds < max_rounds:
+        ans = snap.part_filters(asked)
+        got = torch.empty((len(stubs), FILTER_WORDS), dtype=torch.int32, device=device)
+        dist.all_to_all_single(got, torch.from_numpy(ans.view(np.int32)).to(device),
+                               output_split_sizes=counts.tolist(), input_split_sizes=in_counts.tolist(), group=group)
+        ch = snap.part_close(stubs, got.cpu().numpy().view(np.uint32))
+        tot = torch.tensor([ch], dtype=torch.int64, device=device)
+        dist.all_reduce(tot, group=group)
+        changed = int(tot.item())
+        rounds += 1
+    snap.part_closure_done(changed == 0)
+    return rounds

@@ -95,6 +95,21 @@ int tuple_round(int it) {
     for (uint32_t i = 0; i < st.n_rows; ++i) rows[i] = i;
     rows[st.n_rows] = KETO_NO_ROW;
     if (keto_row_handles(s, rows.data(), rows.size(), hs.data()) != KETO_OK) return fail("row_handles");
+    // partition layouts (host side of keto_snapshot_upload_part_mode): both modes, 1..4 parts; a
+    // migrating part's stubs are other parts' rows
+    for (uint32_t mode = KETO_PART_SHARED; mode <= KETO_PART_MIGRATE; ++mode) {
+        const uint32_t P = 1 + pick(4);
+        uint64_t rows_total = 0;
+        for (uint32_t p = 0; p < P; ++p) {
+            keto_part_stats ps;
+            if (keto_snapshot_part_stats_mode(s, p, P, mode, &ps) != KETO_OK) return fail("part_stats_mode");
+            rows_total += ps.rows;
+            if (mode == KETO_PART_SHARED && ps.stub_rows) return fail("stubs in a shared-rows part");
+            if (mode == KETO_PART_MIGRATE && P == 1 && ps.stub_rows) return fail("stubs with one part");
+        }
+        if (mode == KETO_PART_MIGRATE && rows_total != st.n_rows) return fail("migrating parts do not split the rows");
+    }
+    if (keto_snapshot_part_stats_mode(s, 0, 32, KETO_PART_MIGRATE, nullptr) == KETO_OK) return fail("NULL stats");
     std::vector<uint8_t> allowed(q.size());
     if (keto_check_batch(s, q.data(), (uint32_t)q.size(), 5, allowed.data(), nullptr) != KETO_E_HIP) {
         std::fprintf(stderr, "FAIL round %d: compute on a host-only snapshot did not fail with KETO_E_HIP\n", it);

@@ -120,3 +120,185 @@ def test_partitioned_routing_gloo_world2(tmp_path):
     assert (got == want).all()
     routed = int(np.load(out + ".0.seen.npy").sum() + np.load(out + ".1.seen.npy").sum())
     assert routed == int((own >= 0).sum())
+
+
+# ---- migrating partition: the exchange loop of keto_amd.multi.mig_check over gloo, driving a
+# Python restatement of the migrating DFS (the GPU engine's protocol, repo:keto_amd/csrc/migrate.hip)
+# over the synthetic CSR graph, checked against the C oracle.  Every row has an owner part; a search
+# that enters a row or pops to a frame another part owns travels as a record (head, frames, visited
+# map) in 16-B units.
+
+class _PyMigEngine:
+    """begin / round / fetch of SnapshotMigEngine, on the CPU, for the synthetic graphs (no
+    visit-key collisions, subject-id requests): the ordered DFS of internal/check/engine.go:36-123
+    with a visited map per top-level tuple, cut at part crossings."""
+    ENTER, RESUME, DECISION = 0, 1, 2
+
+    def __init__(self, g, rank, world):
+        self.ptr, self.edges, self.rank, self.world = g.row_ptr, g.edges, rank, world
+        self.n_sets = None
+
+    def owner(self, r):
+        return int((r * 2654435761) >> 7) % self.world
+
+    def _sets(self, r):
+        lo, hi = int(self.ptr[r]), int(self.ptr[r + 1])
+        e = self.edges[lo:hi]
+        k = int(np.searchsorted(~(e >> 31).astype(bool), True)) if len(e) else 0   # sets come first
+        return lo, k, e[k:]
+
+    def _run(self, st, out):
+        idx, origin, T = st["idx"], st["origin"], st["T"]
+        frames, vis = st["frames"], st["vis"]
+        cur, enter = None, st.get("enter")
+        if st["kind"] == self.RESUME:
+            cur = frames.pop()
+        while True:
+            if enter is not None:
+                r, k, fl = enter
+                enter = None
+                lo, n_sets, ids = self._sets(r)
+                if T in set(ids.tolist()):
+                    return self._decide(idx, origin, 1, out)
+                if cur is not None and cur[2] > 0:
+                    frames.append(cur)
+                cur = [r, lo, n_sets, k, fl]
+                continue
+            if cur is None or cur[2] == 0:
+                if not frames:
+                    return self._decide(idx, origin, 0, out)
+                if self.owner(frames[-1][0]) != self.rank:
+                    return out.append((self.owner(frames[-1][0]), dict(st, kind=self.RESUME, frames=frames, vis=vis)))
+                cur = frames.pop()
+                continue
+            e = int(self.edges[cur[1]])
+            cur[1] += 1
+            cur[2] -= 1
+            c = e & 0x7FFFFFFF
+            if cur[4]:                                   # top-level tuple: a fresh map
+                vis = []
+            if c in vis:
+                continue
+            vis.append(c)
+            if cur[3] < 2:
+                continue
+            if self.owner(c) != self.rank:
+                if cur[2] > 0:
+                    frames.append(cur)
+                return out.append((self.owner(c), dict(st, kind=self.ENTER, enter=(c, cur[3] - 1, 0), frames=frames,
+                                                       vis=vis)))
+            enter = (c, cur[3] - 1, 0)
+
+    def _decide(self, idx, origin, v, out):
+        if origin == self.rank:
+            self.dec[idx] = v
+        else:
+            out.append((origin, dict(kind=self.DECISION, idx=idx, origin=origin, v=v)))
+
+    @staticmethod
+    def _pack(st):
+        """A state as int32 16-B units: head, frames (5 words padded to 8), visited ids."""
+        fr = st.get("frames", [])
+        vis = st.get("vis", [])
+        en = st.get("enter") or (0, 0, 0)
+        head = [st["kind"], st["idx"], st["origin"], st.get("T", 0), st.get("v", 0), en[0], en[1], en[2],
+                len(fr), len(vis), 0, 0]
+        words = head + [w for f in fr for w in (list(f) + [0, 0, 0])] + list(vis)
+        words += [0] * (-len(words) % 4)
+        return np.array(words, dtype=np.int32)
+
+    @staticmethod
+    def _unpack(w):
+        kind, idx, origin, T, v, e0, e1, e2, nf, nv = (int(x) for x in w[:10])
+        fr = [list(int(y) for y in w[12 + 8 * i: 12 + 8 * i + 5]) for i in range(nf)]
+        vis = [int(x) for x in w[12 + 8 * nf: 12 + 8 * nf + nv]]
+        return dict(kind=kind, idx=idx, origin=origin, T=T, v=v, enter=(e0, e1, e2), frames=fr, vis=vis)
+
+    def _emit(self, out):
+        import torch
+        by = [[] for _ in range(self.world)]
+        for dest, st in out:
+            by[dest].append(self._pack(st))
+        units, recs, chunks, offs = [], [], [], []
+        for d in range(self.world):
+            u = 0
+            for a in by[d]:
+                offs.append(u)
+                chunks.append(a)
+                u += len(a) // 4
+            units.append(u)
+            recs.append(len(by[d]))
+        self._buf = torch.from_numpy(np.concatenate(chunks).view(np.uint8).copy() if chunks else np.zeros(0, np.uint8))
+        self._off = torch.tensor(offs, dtype=torch.int32)
+        return {"units": units, "records": recs}
+
+    def begin(self, routed, decisions, global_max_depth):
+        self.dec = decisions
+        out = []
+        for i, (row, target, flags, d) in enumerate(routed.tolist()):
+            d = global_max_depth if d <= 0 or d > global_max_depth else d
+            assert self.owner(row) == self.rank
+            self._run(dict(kind=self.ENTER, idx=i, origin=self.rank, T=target, enter=(row, d, 1), frames=[],
+                           vis=[]), out)
+        return self._emit(out)
+
+    def round(self, buf, off, in_records, in_units):
+        w = buf.numpy().view(np.int32)
+        offs = off.numpy()
+        out, j, base = [], 0, 0
+        for s in range(self.world):
+            for _ in range(in_records[s]):
+                st = self._unpack(w[(base + int(offs[j])) * 4:])
+                j += 1
+                if st["kind"] == self.DECISION:
+                    self.dec[st["idx"]] = st["v"]
+                else:
+                    self._run(st, out)
+            base += in_units[s]
+        return self._emit(out)
+
+    def fetch(self, out):
+        return self._buf, self._off
+
+
+def _mig_worker(rank, world, port, q_bytes, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from keto_amd.multi import mig_check
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    q = np.frombuffer(q_bytes, dtype=g.queries(1, seed=0).dtype)
+    eng = _PyMigEngine(g, rank, world)
+    own = np.array([eng.owner(int(r)) for r in q["row"]])
+    mine = q[own == rank]
+    routed = torch.from_numpy(np.ascontiguousarray(mine).view(np.int32).reshape(-1, 4).copy())
+    dec, rounds = mig_check(eng, routed, 5, device="cpu")
+    np.save(out_path + f".{rank}.npy", dec.numpy())
+    np.save(out_path + f".{rank}.rounds.npy", np.array([rounds]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_migrating_dfs_gloo(tmp_path, world):
+    """keto_amd.multi.mig_check over gloo: searches cross parts as records and every decision
+    equals the C oracle's on the whole graph."""
+    import torch.multiprocessing as mp
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    q = g.queries(300, seed=41 + world, depth=5)
+    tab = g.oracle_table(q, 5)
+    want = tab.check_batch_reqs(g.oracle_requests(tab, q), 5, threads=2)
+    out = str(tmp_path / "mig")
+    mp.start_processes(_mig_worker, args=(world, _free_port(), q.tobytes(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    eng = _PyMigEngine(g, 0, world)
+    own = np.array([eng.owner(int(r)) for r in q["row"]])
+    got = np.full(len(q), 255, dtype=np.uint8)
+    for r in range(world):
+        got[own == r] = np.load(out + f".{r}.npy")
+    assert (got == want).all(), f"{int((got != want).sum())} mismatches"
+    assert int(np.load(out + ".0.rounds.npy")[0]) >= 2          # searches crossed parts
+    assert 0.05 < want.mean() < 0.95
