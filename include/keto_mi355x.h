@@ -269,8 +269,8 @@ typedef struct {
     const uint32_t* d_offsets;
     uint32_t decided;           /* decisions written on this part in the call */
     uint32_t undecided;         /* of the searches ended in the call: KETO_UNDECIDED */
-    uint32_t entered;           /* searches started or continued by an ENTER record */
-    uint32_t resumed;           /* searches continued by a RESUME record */
+    uint32_t processed;         /* records (requests, continuations, decisions) handled in the call */
+    uint32_t reruns;            /* of them: re-run with bigger visited tables or a bigger record pool */
 } keto_mig_out;
 int keto_mig_begin(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                    uint8_t* d_allowed_out, void* stream, keto_mig_out* out);

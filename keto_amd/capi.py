@@ -112,7 +112,7 @@ class KPartStats(C.Structure):
 class KMigOut(C.Structure):
     _fields_ = [("units", C.c_uint64 * 31), ("records", C.c_uint32 * 31), ("d_records", C.c_void_p),
                 ("d_offsets", C.c_void_p), ("decided", C.c_uint32), ("undecided", C.c_uint32),
-                ("entered", C.c_uint32), ("resumed", C.c_uint32)]
+                ("processed", C.c_uint32), ("reruns", C.c_uint32)]
 
 
 class KStats(C.Structure):
@@ -351,8 +351,8 @@ class Snapshot:
         return {"units": [int(o.units[p]) for p in range(n_parts)],
                 "records": [int(o.records[p]) for p in range(n_parts)],
                 "d_records": int(o.d_records or 0), "d_offsets": int(o.d_offsets or 0),
-                "decided": int(o.decided), "undecided": int(o.undecided), "entered": int(o.entered),
-                "resumed": int(o.resumed)}
+                "decided": int(o.decided), "undecided": int(o.undecided), "processed": int(o.processed),
+                "reruns": int(o.reruns)}
 
     def mig_begin(self, d_reqs_ptr: int, n: int, d_out_ptr: int, global_max_depth=5, stream=0) -> dict:
         """keto_mig_begin: start the searches of the row-id requests routed to this part."""

@@ -647,8 +647,8 @@ void copy_out(const MigOut& m, keto_mig_out* out) {
     out->d_offsets = m.d_off;
     out->decided = m.decided;
     out->undecided = m.undecided;
-    out->entered = m.started;
-    out->resumed = m.resumed;
+    out->processed = m.processed;
+    out->reruns = m.reruns;
 }
 }  // namespace
 

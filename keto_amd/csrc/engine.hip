@@ -2250,7 +2250,7 @@ void device_upload(Snapshot& S, int device) {
 DevView device_view(const Snapshot& S) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     const DeviceState& D = *S.dev;
-    return DevView{D.arena, D.coll, D.coll_mask, D.device, (void*)D.stream};
+    return DevView{D.arena, D.arena_words, D.coll, D.coll_mask, D.device, (void*)D.stream};
 }
 
 namespace {
@@ -3122,7 +3122,9 @@ void device_check(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));
-    hipStream_t st = stream ? (hipStream_t)stream : D.stream;
+    // NULL = the default stream, as the header says: ordered after the caller's default-stream work
+    // that produced the inputs (the snapshot's own stream is non-blocking and would not be)
+    hipStream_t st = (hipStream_t)stream;
     check_locked(S, D, d_reqs, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, work_out, false, d_steps);
 }
 
@@ -3325,7 +3327,9 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
                        void* stream) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     DeviceState& D = *S.dev;
-    hipStream_t st = stream ? (hipStream_t)stream : D.stream;
+    // NULL = the default stream, as the header says: ordered after the caller's default-stream work
+    // that produced the inputs (the snapshot's own stream is non-blocking and would not be)
+    hipStream_t st = (hipStream_t)stream;
     // the lock is held from the translation through the check: D.xlate is shared by all callers
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));

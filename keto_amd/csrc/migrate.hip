@@ -148,239 +148,371 @@ struct MigArgs {
     uint32_t* big;               // inputs whose map outgrew this tier's tables
     uint32_t* n_big;
     uint8_t* allowed;            // decisions of this part's own requests
-    uint32_t* stats;             // [0] decided here, [1] undecided, [2] entered, [3] resumed
+    uint32_t* stats;             // [0] decided here, [1] undecided, [2] records handled
     // lane workspaces
     uint64_t* vtab;
     uint64_t* vlog;
     uint4* frames;
     uint32_t* lane_epoch;
     uint32_t vcap;
+    // bounds of every index the kernel follows: a record or handle out of range is reported
+    // (err: [0] count, [1] first code, [2] its input record, [3] its value) and the search is
+    // dropped as KETO_UNDECIDED instead of reading out of bounds
+    uint64_t arena_words;
+    uint64_t in_units;
+    uint32_t n_allowed;
+    uint32_t n_parts;
+    uint32_t* err;
 };
 
-// One search state machine per lane over the round's input records (persistent grid).
-__global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    MigVisited V{a.vtab + (uint64_t)slot * a.vcap, a.vlog + (uint64_t)slot * (a.vcap / 2), a.vcap - 1u, a.vcap / 2,
-                 a.lane_epoch[slot], 0};
-    uint4* const fr = a.frames + (uint64_t)slot * MIG_FRAMES;
-    const uint32_t total = a.list ? *a.n_list : a.n_in;
-    for (uint32_t j = slot; j < total; j += stride) {
-        const uint32_t rj = a.list ? a.list[j] : j;
-        uint32_t s = 0;
-        while (s + 1 < a.n_src && a.rec_base[s + 1] <= rj) ++s;
-        const uint32_t* rec = a.in + (a.unit_base[s] + a.in_off[rj]) * 4ull;
-        const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
-        const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 4);
-        const uint32_t idx = h0.x, info = h0.y;
-        const uint32_t kind = info & 3u, origin = (info >> 8) & 0xFFu;
-        if (kind == K_DECISION) {
-            a.allowed[idx] = (uint8_t)((info >> 3) & 3u);
-            atomicAdd(a.stats + 0, 1u);
-            continue;
+constexpr uint32_t E_RECORD = 1, E_HANDLE = 2, E_POS = 3, E_IDX = 4, E_DEST = 5, E_TABLE = 6;
+__device__ inline void report(const MigArgs& a, uint32_t code, uint32_t rj, uint64_t v) {
+    if (atomicAdd(a.err, 1u) == 0) {
+        a.err[1] = code;
+        a.err[2] = rj;
+        a.err[3] = (uint32_t)v;
+    }
+}
+
+// What one input record turned into.
+struct Outcome {
+    int res;                     // RES_* decision, or -1: a continuation record (dest, kind, enter, k)
+    uint32_t dest, kind, enter, k;
+    uint32_t idx, origin;
+    uint32_t t_lo, t_hi;
+    bool tset;
+    bool skip;                   // nothing to emit (a decision written here, a bad record, a re-run)
+};
+
+// The search of one input record on this part, until it is decided or crosses to another part.
+// Uses the lane's visited table (V) and frame stack (fr); sp = saved frames on return.
+__device__ inline Outcome run_record(const MigArgs& a, uint32_t rj, MigVisited& V, uint4* fr, uint32_t& sp) {
+    Outcome o{-1, NONE, 0, 0, 0, 0, 0, 0, 0, false, true};
+    sp = 0;
+    uint32_t s = 0;
+    while (s + 1 < a.n_src && a.rec_base[s + 1] <= rj) ++s;
+    const uint64_t at_unit = a.unit_base[s] + a.in_off[rj];
+    if (at_unit + 2 > a.in_units) {
+        report(a, E_RECORD, rj, at_unit);
+        return o;
+    }
+    const uint32_t* rec = a.in + at_unit * 4ull;
+    const uint4 h0 = *reinterpret_cast<const uint4*>(rec);
+    const uint4 h1 = *reinterpret_cast<const uint4*>(rec + 4);
+    const uint32_t idx = h0.x, info = h0.y;
+    const uint32_t kind = info & 3u, origin = (info >> 8) & 0xFFu;
+    if (origin >= a.n_parts || kind > K_DECISION) {
+        report(a, E_RECORD, rj, info);
+        return o;
+    }
+    if (kind == K_DECISION) {
+        if (origin != a.self || idx >= a.n_allowed) {
+            report(a, E_IDX, rj, idx);
+            return o;
         }
-        const bool tset = (info >> 2) & 1u;
-        const uint32_t T = h0.z;
-        const uint64_t T64 = vid_row(h0.w, h0.z);
-        uint32_t cw = 0, cb = 0;
-        closure_bit(T, cw, cb);
-        int res = -1;
-        // restore the map and the saved frames
-        V.fresh();
-        const uint32_t ns = min(h1.z, MIG_FRAMES), nv = h1.w;     // senders keep ns <= MIG_FRAMES
-        if (nv > V.cap) res = RES_BIG;
-        const uint64_t* rv = reinterpret_cast<const uint64_t*>(rec + HEAD_WORDS + 4ull * ns);
-        for (uint32_t i = 0; i < nv && res < 0; ++i)
-            if (V.test_add(rv[i]) == 2) res = RES_BIG;
-        uint32_t sp = ns;
-        for (uint32_t i = 0; i < ns; ++i) fr[i] = *reinterpret_cast<const uint4*>(rec + HEAD_WORDS + 4ull * i);
-        uint64_t pos = 0;
-        uint32_t left = 0, k = 0, fl = 0;
-        bool have = false;
-        uint32_t enter = NONE, enter_k = 0, enter_fl = 0;
-        if (kind == K_ENTER) {
-            enter = h1.x;
-            enter_k = h1.y;
-            enter_fl = (info >> 5) & 7u;
-            atomicAdd(a.stats + 2, 1u);
-        } else {
-            atomicAdd(a.stats + 3, 1u);
-        }
-        // emitted record: destination part, kind, enter handle / depth
-        uint32_t e_dest = NONE, e_kind = 0, e_enter = 0, e_k = 0;
-        while (res < 0) {
-            if (enter != NONE) {
-                uint64_t hw = (uint64_t)enter * HDR_WORDS;
-                uint4 hd = *reinterpret_cast<const uint4*>(a.arena + hw);
-                while (hd.z & HDR_FWD) {
-                    hw = (uint64_t)hd.x * HDR_WORDS;
-                    hd = *reinterpret_cast<const uint4*>(a.arena + hw);
-                }
-                const uint32_t n_sets = hd.x, n_ids = hd.y;
-                const bool seq = (hd.z & HDR_SEQ) != 0;
-                const uint32_t hl = (hd.z >> 8) & 31u;
-                const uint64_t beg = hw + HDR_WORDS;
-                if (!seq && !tset && n_ids > 0) {                     // is the requested id in the row?
-                    bool hit = false;
-                    if (hl == 0) {
-                        for (uint32_t i = n_sets; i < n_sets + n_ids; ++i) hit |= a.arena[beg + i] == T;
-                    } else {
-                        uint32_t b1, b2;
-                        bloom_bits(T, b1, b2);
-                        if (bloom_has(hd.z, hd.w, b1) && bloom_has(hd.z, hd.w, b2)) {
-                            const uint32_t nb = (1u << hl) / BUCKET_WORDS;
-                            const uint64_t tb = hw - ((hd.z & HDR_CLOSURE) ? CB_WORDS : 0u) - (1ull << hl);
-                            for (uint32_t b = mix32d(T) & (nb - 1);; b = (b + 1) & (nb - 1)) {
-                                const uint4 v = *reinterpret_cast<const uint4*>(a.arena + tb + (uint64_t)b * BUCKET_WORDS);
-                                if (v.x == T || v.y == T || v.z == T || v.w == T) {
-                                    hit = true;
-                                    break;
-                                }
-                                if (v.x == NONE || v.y == NONE || v.z == NONE || v.w == NONE) break;
+        a.allowed[idx] = (uint8_t)((info >> 3) & 3u);
+        o.res = RES_FALSE;                                            // counted as decided here
+        o.dest = NONE;
+        o.skip = false;
+        return o;
+    }
+    if (h1.z > MIG_FRAMES || at_unit + 2 + h1.z + (h1.w + 1ull) / 2 > a.in_units) {
+        report(a, E_RECORD, rj, h1.z);
+        return o;
+    }
+    o.idx = idx;
+    o.origin = origin;
+    o.t_lo = h0.z;
+    o.t_hi = h0.w;
+    const bool tset = (info >> 2) & 1u;
+    o.tset = tset;
+    const uint32_t T = h0.z;
+    const uint64_t T64 = vid_row(h0.w, h0.z);
+    uint32_t cw = 0, cb = 0;
+    closure_bit(T, cw, cb);
+    int res = -1;
+    // restore the map and the saved frames
+    V.fresh();
+    const uint32_t ns = h1.z, nv = h1.w;
+    if (nv > V.cap) res = RES_BIG;
+    const uint64_t* rv = reinterpret_cast<const uint64_t*>(rec + HEAD_WORDS + 4ull * ns);
+    for (uint32_t i = 0; i < nv && res < 0; ++i)
+        if (V.test_add(rv[i]) == 2) res = RES_BIG;
+    sp = ns;
+    for (uint32_t i = 0; i < ns; ++i) fr[i] = *reinterpret_cast<const uint4*>(rec + HEAD_WORDS + 4ull * i);
+    uint64_t pos = 0;
+    uint32_t left = 0, k = 0, fl = 0;
+    bool have = false;
+    uint32_t enter = NONE, enter_k = 0, enter_fl = 0;
+    if (kind == K_ENTER) {
+        enter = h1.x;
+        enter_k = h1.y;
+        enter_fl = (info >> 5) & 7u;
+    }
+    while (res < 0) {
+        if (enter != NONE) {
+            uint64_t hw = (uint64_t)enter * HDR_WORDS;
+            if (hw + 2 * HDR_WORDS > a.arena_words) {
+                report(a, E_HANDLE, rj, enter);
+                res = RES_UNDECIDED;
+                break;
+            }
+            uint4 hd = *reinterpret_cast<const uint4*>(a.arena + hw);
+            while ((hd.z & HDR_FWD) && (uint64_t)hd.x * HDR_WORDS + 2 * HDR_WORDS <= a.arena_words) {
+                hw = (uint64_t)hd.x * HDR_WORDS;
+                hd = *reinterpret_cast<const uint4*>(a.arena + hw);
+            }
+            const uint32_t n_sets = hd.x, n_ids = hd.y;
+            const bool seq = (hd.z & HDR_SEQ) != 0;
+            const uint32_t hl = (hd.z >> 8) & 31u;
+            const uint64_t beg = hw + HDR_WORDS;
+            const uint64_t tbl = (hl ? (1ull << hl) : 0ull) + ((hd.z & HDR_CLOSURE) ? CB_WORDS : 0u);
+            if ((hd.z & (HDR_REMOTE | HDR_FWD)) || hl == 1 || beg + (uint64_t)n_sets + n_ids > a.arena_words ||
+                hw < tbl) {
+                report(a, E_POS, rj, enter);
+                res = RES_UNDECIDED;
+                break;
+            }
+            if (!seq && !tset && n_ids > 0) {                         // is the requested id in the row?
+                bool hit = false;
+                if (hl == 0) {
+                    const uint4 w = *reinterpret_cast<const uint4*>(a.arena + beg);   // the window
+                    for (uint32_t i = n_sets; i < n_sets + n_ids && i < WINDOW_WORDS; ++i)
+                        hit |= (i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w) == T;
+                } else {
+                    uint32_t b1, b2;
+                    bloom_bits(T, b1, b2);
+                    if (bloom_has(hd.z, hd.w, b1) && bloom_has(hd.z, hd.w, b2)) {
+                        const uint32_t nb = (1u << hl) / BUCKET_WORDS;
+                        const uint64_t tb = hw - tbl;
+                        uint32_t b = mix32d(T) & (nb - 1);
+                        for (uint32_t probe = 0; probe < nb; ++probe, b = (b + 1) & (nb - 1)) {   // load <= 1/2
+                            const uint4 v = *reinterpret_cast<const uint4*>(a.arena + tb + (uint64_t)b * BUCKET_WORDS);
+                            if (v.x == T || v.y == T || v.z == T || v.w == T) {
+                                hit = true;
+                                break;
                             }
+                            if (v.x == NONE || v.y == NONE || v.z == NONE || v.w == NONE) break;
                         }
                     }
-                    if (hit) {
-                        res = RES_TRUE;
-                        break;
-                    }
                 }
-                if (have && left > 0) {                               // the parent keeps its place
+                if (hit) {
+                    res = RES_TRUE;
+                    break;
+                }
+            }
+            if (have && left > 0) {                                   // the parent keeps its place
+                if (sp >= MIG_FRAMES) {
+                    res = RES_UNDECIDED;
+                    break;
+                }
+                fr[sp++] = make_uint4((uint32_t)pos, (uint32_t)(pos >> 32) | (a.self << 8), left, k | (fl << 16));
+            }
+            pos = beg;
+            left = n_sets;
+            k = enter_k;
+            fl = enter_fl | (seq ? F_SEQ : 0u);
+            have = true;
+            enter = NONE;
+            continue;
+        }
+        if (!have || left == 0) {                                     // row done: pop
+            if (sp == 0) {
+                res = RES_FALSE;
+                break;
+            }
+            const uint4 f = fr[sp - 1];
+            const uint32_t part = f.y >> 8;
+            if (part >= a.n_parts ||
+                (part == a.self && ((uint64_t)f.x | ((uint64_t)(f.y & 0xFFu) << 32)) + f.z > a.arena_words)) {
+                report(a, E_POS, rj, f.x);
+                res = RES_UNDECIDED;
+                break;
+            }
+            if (part != a.self) {                                     // the parent lives elsewhere
+                o.dest = part;
+                o.kind = K_RESUME;
+                break;
+            }
+            --sp;
+            pos = (uint64_t)f.x | ((uint64_t)(f.y & 0xFFu) << 32);
+            left = f.z;
+            k = f.w & 0xFFFFu;
+            fl = f.w >> 16;
+            have = true;
+            continue;
+        }
+        const uint32_t e = a.arena[pos];
+        ++pos;
+        --left;
+        if (e & EDGE_SET) {
+            const uint32_t child = e & EDGE_VAL;
+            const uint64_t cw4 = (uint64_t)child * HDR_WORDS;
+            if (cw4 < CB_WORDS || cw4 + 2 * HDR_WORDS > a.arena_words) {
+                report(a, E_HANDLE, rj, child);
+                res = RES_UNDECIDED;
+                break;
+            }
+            const uint4 ch = *reinterpret_cast<const uint4*>(a.arena + cw4);
+            const bool remote = (ch.z & HDR_REMOTE) != 0;
+            if (remote && ch.x >= a.n_parts) {
+                report(a, E_DEST, rj, ch.x);
+                res = RES_UNDECIDED;
+                break;
+            }
+            const uint64_t rvid = remote ? vid_row(ch.x, ch.y) : vid_row(a.self, child);
+            uint64_t vid = rvid;
+            if (fl & F_SEQ) {
+                const uint32_t c = coll_find(a.coll, a.coll_mask, e);
+                if (c != NONE) vid = vid_class(c);
+            }
+            if (fl & F_TOP) V.fresh();                                // a fresh map per top-level tuple
+            const int t = V.test_add(vid);
+            if (t == 2) {
+                res = RES_BIG;
+                break;
+            }
+            if (t == 1) continue;
+            if (tset && rvid == T64) {                                // engine.go:54-57
+                res = RES_TRUE;
+                break;
+            }
+            if (k < 2) continue;                                      // remaining depth after the hop >= 1
+            if (!tset && (ch.z & HDR_CLOSURE) && !((a.arena[cw4 - CB_WORDS + cw] >> cb) & 1u))
+                continue;                                             // T is not below this set
+            if (remote) {                                             // the walk goes on on the owner
+                if (left > 0) {
                     if (sp >= MIG_FRAMES) {
                         res = RES_UNDECIDED;
                         break;
                     }
                     fr[sp++] = make_uint4((uint32_t)pos, (uint32_t)(pos >> 32) | (a.self << 8), left, k | (fl << 16));
                 }
-                pos = beg;
-                left = n_sets;
-                k = enter_k;
-                fl = enter_fl | (seq ? F_SEQ : 0u);
-                have = true;
-                enter = NONE;
-                continue;
+                o.dest = ch.x;
+                o.kind = K_ENTER;
+                o.enter = ch.y;
+                o.k = k - 1;
+                break;
             }
-            if (!have || left == 0) {                                 // row done: pop
-                if (sp == 0) {
-                    res = RES_FALSE;
-                    break;
-                }
-                const uint4 f = fr[sp - 1];
-                const uint32_t part = f.y >> 8;
-                if (part != a.self) {                                 // the parent lives elsewhere
-                    e_dest = part;
-                    e_kind = K_RESUME;
-                    break;
-                }
-                --sp;
-                pos = (uint64_t)f.x | ((uint64_t)(f.y & 0xFFu) << 32);
-                left = f.z;
-                k = f.w & 0xFFFFu;
-                fl = f.w >> 16;
-                have = true;
-                continue;
+            enter = child;
+            enter_k = k - 1;
+            enter_fl = 0;
+        } else {                                                      // a subject id of an ordered row
+            int t = 0;
+            if (!(fl & F_TOP)) {
+                const uint32_t c = coll_find(a.coll, a.coll_mask, e);
+                if (c != NONE) t = V.test_add(vid_class(c));
             }
-            const uint32_t e = a.arena[pos];
-            ++pos;
-            --left;
-            if (e & EDGE_SET) {
-                const uint32_t child = e & EDGE_VAL;
-                const uint64_t cw4 = (uint64_t)child * HDR_WORDS;
-                const uint4 ch = *reinterpret_cast<const uint4*>(a.arena + cw4);
-                const bool remote = (ch.z & HDR_REMOTE) != 0;
-                const uint64_t rvid = remote ? vid_row(ch.x, ch.y) : vid_row(a.self, child);
-                uint64_t vid = rvid;
-                if (fl & F_SEQ) {
-                    const uint32_t c = coll_find(a.coll, a.coll_mask, e);
-                    if (c != NONE) vid = vid_class(c);
-                }
-                if (fl & F_TOP) V.fresh();                            // a fresh map per top-level tuple
-                const int t = V.test_add(vid);
-                if (t == 2) {
-                    res = RES_BIG;
-                    break;
-                }
-                if (t == 1) continue;
-                if (tset && rvid == T64) {                            // engine.go:54-57
-                    res = RES_TRUE;
-                    break;
-                }
-                if (k < 2) continue;                                  // remaining depth after the hop >= 1
-                if (!tset && (ch.z & HDR_CLOSURE) && !((a.arena[cw4 - CB_WORDS + cw] >> cb) & 1u))
-                    continue;                                         // T is not below this set
-                if (remote) {                                         // the walk goes on on the owner
-                    if (left > 0) {
-                        if (sp >= MIG_FRAMES) {
-                            res = RES_UNDECIDED;
-                            break;
-                        }
-                        fr[sp++] = make_uint4((uint32_t)pos, (uint32_t)(pos >> 32) | (a.self << 8), left, k | (fl << 16));
-                    }
-                    e_dest = ch.x;
-                    e_kind = K_ENTER;
-                    e_enter = ch.y;
-                    e_k = k - 1;
-                    break;
-                }
-                enter = child;
-                enter_k = k - 1;
-                enter_fl = 0;
-            } else {                                                  // a subject id of an ordered row
-                int t = 0;
-                if (!(fl & F_TOP)) {
-                    const uint32_t c = coll_find(a.coll, a.coll_mask, e);
-                    if (c != NONE) t = V.test_add(vid_class(c));
-                }
-                if (t == 2) {
-                    res = RES_BIG;
-                    break;
-                }
-                if (t == 0 && !tset && e == T) res = RES_TRUE;
+            if (t == 2) {
+                res = RES_BIG;
+                break;
             }
+            if (t == 0 && !tset && e == T) res = RES_TRUE;
         }
-        if (res == RES_BIG) {                                         // re-run on the big tier
-            if (a.big) {
-                a.big[atomicAdd(a.n_big, 1u)] = rj;
-                continue;
-            }
-            res = RES_UNDECIDED;
+    }
+    if (res == RES_BIG) {                                             // re-run on the big tier
+        if (a.big) {
+            a.big[atomicAdd(a.n_big, 1u)] = rj;
+            return o;                                                 // skip
         }
-        uint32_t units = 2, nvo = 0, nso = 0;
-        if (res >= 0) {
-            if (origin == a.self) {
-                a.allowed[idx] = (uint8_t)res;
-                atomicAdd(a.stats + 0, 1u);
-                if (res == RES_UNDECIDED) atomicAdd(a.stats + 1, 1u);
-                continue;
+        res = RES_UNDECIDED;
+    }
+    o.res = res;
+    if (res >= 0) {
+        if (origin == a.self) {
+            if (idx >= a.n_allowed) {
+                report(a, E_IDX, rj, idx);
+                return o;
             }
-            if (res == RES_UNDECIDED) atomicAdd(a.stats + 1, 1u);
-            e_dest = origin;
-            e_kind = K_DECISION;
+            a.allowed[idx] = (uint8_t)res;
+            o.dest = NONE;                                            // decided here: nothing to send
         } else {
-            nso = sp;
-            nvo = V.n;
-            units = 2 + nso + (nvo + 1) / 2;
+            o.dest = origin;
+            o.kind = K_DECISION;
         }
-        const unsigned long long u = atomicAdd(a.pool_used, (unsigned long long)units);
-        if (u + units > a.pool_cap) {
-            a.spill[atomicAdd(a.n_spill, 1u)] = rj;
-            continue;
+    }
+    o.skip = false;
+    return o;
+}
+
+__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// inclusive prefix sum over the 64 lanes of a wave (every lane active)
+__device__ inline uint32_t wave_scan(uint32_t v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(v, (unsigned)d);
+        if (lane >= (uint32_t)d) v += x;
+    }
+    return v;
+}
+
+// One search state machine per lane over the round's input records (persistent grid).  The loop
+// runs the same number of times on every lane of a wave, so a record's output is placed with
+// wave-wide prefix sums and one atomic per wave instead of one per record.
+__global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t stride = gridDim.x * blockDim.x;
+    MigVisited V{a.vtab + (uint64_t)slot * a.vcap, a.vlog + (uint64_t)slot * (a.vcap / 2), a.vcap - 1u, a.vcap / 2,
+                 a.lane_epoch[slot], 0};
+    uint4* const fr = a.frames + (uint64_t)slot * MIG_FRAMES;
+    const uint32_t total = a.list ? *a.n_list : a.n_in;
+    uint32_t n_dec = 0, n_und = 0, n_in = 0;
+    for (uint32_t base = slot - lane; base < total; base += stride) {
+        const uint32_t j = base + lane;
+        uint32_t sp = 0;
+        Outcome o{-1, NONE, 0, 0, 0, 0, 0, 0, 0, false, true};
+        if (j < total) {
+            ++n_in;
+            o = run_record(a, a.list ? a.list[j] : j, V, fr, sp);
         }
-        uint32_t* o = a.pool + u * 4ull;
+        const bool out = !o.skip && o.dest != NONE;
+        if (!o.skip && o.res >= 0 && o.dest == NONE) {
+            ++n_dec;
+            if (o.res == RES_UNDECIDED) ++n_und;
+        }
+        if (!o.skip && o.res == RES_UNDECIDED && o.dest != NONE) ++n_und;
+        // place the record: units and record slots by wave prefix sums, one atomic each per wave
+        const uint32_t units = out ? (o.res >= 0 ? 2u : 2u + sp + (V.n + 1) / 2) : 0u;
+        const uint32_t incl = wave_scan(units);
+        const uint32_t wave_units = __shfl(incl, 63);
+        if (wave_units == 0) continue;
+        unsigned long long ub = 0;
+        if (lane == 0) ub = atomicAdd(a.pool_used, (unsigned long long)wave_units);
+        ub = __shfl(ub, 0);
+        const unsigned long long u = ub + incl - units;
+        const bool fits = out && u + units <= a.pool_cap;
+        const uint64_t m = __ballot(fits);
+        uint32_t rb = 0;
+        if (lane == 0 && m) rb = atomicAdd(a.out_count, (uint32_t)__popcll(m));
+        rb = __shfl(rb, 0);
+        if (out && !fits) a.spill[atomicAdd(a.n_spill, 1u)] = a.list ? a.list[j] : j;   // re-run once the pool has grown
+        if (!fits) continue;
+        const uint32_t at = rb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint32_t nso = o.res >= 0 ? 0u : sp, nvo = o.res >= 0 ? 0u : V.n;
+        uint32_t* ow = a.pool + u * 4ull;
         // (an ENTER record's row is never a top-level row: enter flags 0)
-        const uint32_t oinfo = e_kind | (tset ? 4u : 0u) | ((res >= 0 ? (uint32_t)res : 0u) << 3) | (origin << 8);
-        *reinterpret_cast<uint4*>(o) = make_uint4(idx, oinfo, h0.z, h0.w);
-        *reinterpret_cast<uint4*>(o + 4) = make_uint4(e_enter, e_k, nso, nvo);
-        for (uint32_t i = 0; i < nso; ++i) *reinterpret_cast<uint4*>(o + HEAD_WORDS + 4ull * i) = fr[i];
-        uint64_t* ov = reinterpret_cast<uint64_t*>(o + HEAD_WORDS + 4ull * nso);
+        const uint32_t oinfo = o.kind | (o.tset ? 4u : 0u) | ((o.res >= 0 ? (uint32_t)o.res : 0u) << 3) | (o.origin << 8);
+        *reinterpret_cast<uint4*>(ow) = make_uint4(o.idx, oinfo, o.t_lo, o.t_hi);
+        *reinterpret_cast<uint4*>(ow + 4) = make_uint4(o.enter, o.k, nso, nvo);
+        for (uint32_t i = 0; i < nso; ++i) *reinterpret_cast<uint4*>(ow + HEAD_WORDS + 4ull * i) = fr[i];
+        uint64_t* ov = reinterpret_cast<uint64_t*>(ow + HEAD_WORDS + 4ull * nso);
         for (uint32_t i = 0; i < nvo; ++i) ov[i] = V.log[i];
         if (nvo & 1u) ov[nvo] = 0;
-        const uint32_t at = atomicAdd(a.out_count, 1u);
-        a.out_dest[at] = e_dest;
+        a.out_dest[at] = o.dest;
         a.out_unit[at] = (uint32_t)u;
         a.out_len[at] = units;
     }
     a.lane_epoch[slot] = V.epoch;
+    // statistics: one atomic per wave
+    const uint32_t d = wave_scan(n_dec), un = wave_scan(n_und), ni = wave_scan(n_in);
+    if (lane == 63) {
+        if (d) atomicAdd(a.stats + 0, d);
+        if (un) atomicAdd(a.stats + 1, un);
+        if (ni) atomicAdd(a.stats + 2, ni);
+    }
 }
 
 // START records of a routed batch (row-id requests of this part): the depth clamp
@@ -428,7 +560,7 @@ __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restric
 __global__ void __launch_bounds__(256) mig_count(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ len,
                                                  const uint32_t* __restrict__ n, unsigned long long* __restrict__ cnt) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *n) return;
+    if (i >= *n || dest[i] >= MIG_MAX_PARTS) return;            // (the kernel only emits parts < n_parts)
     atomicAdd(cnt + dest[i], (1ull << 36) | len[i]);
 }
 __global__ void __launch_bounds__(256) mig_scatter(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ unit,
@@ -439,7 +571,7 @@ __global__ void __launch_bounds__(256) mig_scatter(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ rec_base, uint32_t* __restrict__ send,
                                                    uint32_t* __restrict__ send_off) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *n) return;
+    if (i >= *n || dest[i] >= MIG_MAX_PARTS) return;
     const uint32_t d = dest[i], l = len[i];
     const unsigned long long c = atomicAdd(cursor + d, (1ull << 36) | l);
     const uint64_t u_in = c & ((1ull << 36) - 1), r_in = c >> 36;
@@ -514,7 +646,7 @@ struct MigState {
     uint32_t *out_dest = nullptr, *out_unit = nullptr, *out_len = nullptr;
     uint32_t *spill = nullptr, *spill2 = nullptr, *bigq = nullptr;
     uint64_t out_cap = 0;
-    uint32_t* ctr = nullptr;           // [0] out_count [1] n_spill [2] n_big [3] scratch [4..7] stats
+    uint32_t* ctr = nullptr;           // [0] out_count [1] n_spill [2] n_big [3] scratch [4..7] stats [8..11] err
     unsigned long long* pool_used = nullptr;
     unsigned long long* cursor = nullptr;   // [MIG_MAX_PARTS]
     uint64_t* unit_base = nullptr;          // [MIG_MAX_PARTS] source / destination unit bases
@@ -575,7 +707,7 @@ MigState& mig_state(Snapshot& S) {
         for (uint32_t r = 0; r < S.n_rows(); ++r) own[r] = (uint8_t)S.root_owner(r, S.n_parts);
         M->owner = dalloc<uint8_t>(S.n_rows());
         HIP_OK(hipMemcpy(M->owner, own.data(), own.size(), hipMemcpyHostToDevice));
-        M->ctr = dalloc<uint32_t>(8);
+        M->ctr = dalloc<uint32_t>(16);
         M->pool_used = dalloc<unsigned long long>(1);
         M->cursor = dalloc<unsigned long long>(MIG_MAX_PARTS);
         M->unit_base = dalloc<uint64_t>(MIG_MAX_PARTS);
@@ -606,7 +738,7 @@ void ensure_out(MigState& M, uint64_t n_in) {
 
 // grow the output pool, keeping the records already written (all below the old capacity)
 void grow_pool(MigState& M, uint64_t want, hipStream_t st) {
-    uint64_t cap = std::max<uint64_t>(want, 1ull << 20);
+    uint64_t cap = want;
     if (cap <= M.pool_cap) return;
     uint32_t* p = dalloc<uint32_t>(cap * 4);
     if (M.pool) HIP_OK(hipMemcpyAsync(p, M.pool, M.pool_cap * 16, hipMemcpyDeviceToDevice, st));
@@ -622,7 +754,12 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     const DevView dv = device_view(S);
     const uint32_t P = S.n_parts;
     ensure_out(M, n_in);
-    if (!M.pool) grow_pool(M, std::max<uint64_t>((uint64_t)n_in * 4, 1ull << 20), st);
+    if (!M.pool) {
+        // records are ~10 units at max-depth 5; a short pool only costs reruns (tests force them)
+        uint64_t want = std::max<uint64_t>((uint64_t)n_in * 16, 1ull << 20);
+        if (const char* e = getenv("KETO_MIG_POOL_UNITS")) want = std::max<uint64_t>(64, strtoull(e, nullptr, 0));
+        grow_pool(M, want, st);
+    }
     if (!M.small.vtab) M.small.alloc(LANES_SMALL, VCAP_SMALL);
     if (!M.bigl.vtab) M.bigl.alloc(LANES_BIG, VCAP_BIG);
     // source segments
@@ -638,7 +775,7 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     if (rb[n_src] != n_in) throw Error{KETO_E_INVALID, "record counts do not add up"};
     HIP_OK(hipMemcpyAsync(M.rec_base, rb, (n_src + 1) * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(M.unit_base, ub, n_src * 8, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(M.ctr, 0, 8 * 4, st));
+    HIP_OK(hipMemsetAsync(M.ctr, 0, 16 * 4, st));
     HIP_OK(hipMemsetAsync(M.pool_used, 0, 8, st));
     MigArgs a{};
     a.arena = dv.arena;
@@ -660,6 +797,11 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     a.n_big = M.ctr + 2;
     a.allowed = M.allowed;
     a.stats = M.ctr + 4;
+    a.err = M.ctr + 8;
+    a.arena_words = dv.arena_words;
+    a.in_units = acc;
+    a.n_allowed = M.n;
+    a.n_parts = P;
     auto launch = [&](Lanes& L, const uint32_t* list, const uint32_t* n_list, uint32_t n_max, uint32_t* big,
                       uint32_t* spill) {
         a.list = list;
@@ -680,15 +822,17 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     };
     // small tier over every input, then the big tier over the inputs whose maps outgrew it, then the
     // inputs whose output did not fit the pool (with a bigger pool), until none is left
-    uint32_t cnt[8];
+    uint32_t cnt[16];
     if (n_in) launch(M.small, nullptr, nullptr, n_in, M.bigq, M.spill);
-    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 16 * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     uint32_t n_big = cnt[2];
+    uint32_t spilled = 0;
     for (int pass = 0; pass < 2; ++pass) {       // pass 0: the small tier's spills, pass 1: the big tier
         uint32_t n_sp = cnt[1];
         bool small_tier = pass == 0;
         while (n_sp) {
+            spilled += n_sp;
             // rerun the spilled inputs with a pool twice the size (list copied: the rerun spills into spill)
             unsigned long long used = 0;
             HIP_OK(hipMemcpyAsync(&used, M.pool_used, 8, hipMemcpyDeviceToHost, st));
@@ -701,7 +845,7 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
             HIP_OK(hipMemcpyAsync(M.pool_used, &cap_used, 8, hipMemcpyHostToDevice, st));
             if (small_tier) launch(M.small, M.spill2, M.ctr + 3, n_sp, M.bigq, M.spill);
             else launch(M.bigl, M.spill2, M.ctr + 3, n_sp, nullptr, M.spill);
-            HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipMemcpyAsync(cnt, M.ctr, 16 * 4, hipMemcpyDeviceToHost, st));
             HIP_OK(hipStreamSynchronize(st));
             n_sp = cnt[1];
         }
@@ -710,14 +854,14 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
             if (n_big == 0) break;
             HIP_OK(hipMemsetAsync(M.ctr + 1, 0, 4, st));
             launch(M.bigl, M.bigq, M.ctr + 2, n_big, nullptr, M.spill);
-            HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipMemcpyAsync(cnt, M.ctr, 16 * 4, hipMemcpyDeviceToHost, st));
             HIP_OK(hipStreamSynchronize(st));
         }
     }
     const uint32_t n_out = cnt[0];
     if (getenv("KETO_MIG_DEBUG"))
-        fprintf(stderr, "mig part %u: in %u big %u out %u decided %u undecided %u pool %llu\n", S.part, n_in, n_big, n_out,
-                cnt[4], cnt[5], (unsigned long long)M.pool_cap);
+        fprintf(stderr, "mig part %u: in %u big %u out %u decided %u undecided %u pool %llu spilled %u\n", S.part, n_in,
+                n_big, n_out, cnt[4], cnt[5], (unsigned long long)M.pool_cap, spilled);
     // group by destination
     HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
     if (n_out) {
@@ -760,14 +904,18 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
                            M.ctr + 0, M.pool, M.cursor, M.dunit_base, M.drec_base, M.send, M.send_off);
         HIP_OK(hipGetLastError());
     }
-    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 8 * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 16 * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    if (cnt[8])
+        throw Error{KETO_E_INVALID, std::to_string(cnt[8]) + " malformed continuation records or handles (first: code " +
+                                        std::to_string(cnt[9]) + ", input record " + std::to_string(cnt[10]) +
+                                        ", value " + std::to_string(cnt[11]) + ")"};
     out.d_buf = M.send;
     out.d_off = M.send_off;
     out.decided = cnt[4];
     out.undecided = cnt[5];
-    out.started = cnt[6];
-    out.resumed = cnt[7];
+    out.processed = cnt[6];
+    out.reruns = spilled + n_big;
 }
 
 }  // namespace
@@ -777,7 +925,9 @@ void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gm
     std::lock_guard<std::mutex> lk(S.mu);
     MigState& M = mig_state(S);
     HIP_OK(hipSetDevice(M.device));
-    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)device_view(S).stream;
+    // NULL = the default stream, as the header says: ordered after the caller's default-stream work
+    // that produced the inputs (the snapshot's own stream is non-blocking and would not be)
+    hipStream_t st = (hipStream_t)stream;
     if (gmd > 65535) gmd = 65535;
     if (n && (!d_reqs || !d_allowed)) throw Error{KETO_E_INVALID, "NULL argument"};
     M.allowed = d_allowed;
@@ -812,7 +962,9 @@ void mig_round(Snapshot& S, const void* d_in, const uint32_t* d_in_off, const ui
     MigState& M = mig_state(S);
     HIP_OK(hipSetDevice(M.device));
     if (!M.active) throw Error{KETO_E_INVALID, "no migrating batch (keto_mig_begin)"};
-    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)device_view(S).stream;
+    // NULL = the default stream, as the header says: ordered after the caller's default-stream work
+    // that produced the inputs (the snapshot's own stream is non-blocking and would not be)
+    hipStream_t st = (hipStream_t)stream;
     uint64_t n_in = 0;
     for (uint32_t s = 0; s < S.n_parts; ++s) n_in += in_records[s];
     if (n_in > 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "too many records in one round"};

@@ -353,6 +353,7 @@ uint64_t part_close(Snapshot& s, const uint32_t* rows, uint64_t n, const uint32_
 void part_closure_done(Snapshot& s, bool converged);
 struct DevView {             // what migrate.hip needs of a device snapshot
     const uint32_t* arena;
+    uint64_t arena_words;
     const uint64_t* coll;
     uint32_t coll_mask;
     int device;
@@ -365,7 +366,7 @@ struct MigOut {
     uint32_t records[MIG_MAX_PARTS];
     const void* d_buf;
     const uint32_t* d_off;
-    uint32_t decided, undecided, started, resumed;
+    uint32_t decided, undecided, processed, reruns;
 };
 void mig_begin(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
                MigOut& out);
