@@ -211,22 +211,29 @@ int keto_snapshot_upload_part(keto_snapshot* s, uint32_t part, uint32_t n_parts,
 /* Partition modes of keto_snapshot_upload_part_mode. */
 #define KETO_PART_SHARED 0      /* keto_snapshot_upload_part: set targets on every part, root rows by hash */
 #define KETO_PART_MIGRATE 1     /* every row on exactly one part by hash(namespace_id, object) */
-#define KETO_MIG_MAX_PARTS 31
+#define KETO_MIG_MAX_PARTS 30
 /* Edge-partitioned upload in either mode.  KETO_PART_MIGRATE is for graphs whose set-target rows
  * (folders, groups) do not fit on one GPU either: each part holds only its own rows, plus a stub for
  * every other part's row one of its subject sets points at, and a check's DFS migrates between parts
  * at those crossings (keto_mig_begin / keto_mig_round).  After the upload the parts exchange closure
  * filters (keto_part_stubs / keto_part_filters / keto_part_close) until no filter changes anywhere,
  * then call keto_part_closure_done.  A migrating part answers checks only through keto_mig_*;
- * expand and the other check entry points fail with KETO_E_INVALID.  n_parts <= 31. */
+ * expand and the other check entry points fail with KETO_E_INVALID.  n_parts <= 30. */
 int keto_snapshot_upload_part_mode(keto_snapshot* s, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode);
+/* KETO_PART_MIGRATE with the rows most subject sets point at (the hottest in-degree bands whose rows
+ * fit hot_bytes of arena) replicated on every part, at the same place: searches cross parts only on
+ * the colder rows.  hot_bytes = 0 is keto_snapshot_upload_part_mode(..., KETO_PART_MIGRATE); every
+ * part of one partition must be uploaded with the same hot_bytes. */
+int keto_snapshot_upload_part_migrate(keto_snapshot* s, uint32_t part, uint32_t n_parts, int32_t device,
+                                      uint64_t hot_bytes);
 /* Arena a part of an edge-partitioned upload would hold (host-only snapshots; sizing aid):
  * arena_bytes of the part's device arena, shared_bytes of it in rows every part keeps. */
 typedef struct {
     uint64_t arena_bytes;
     uint64_t shared_bytes;
     uint32_t rows;              /* rows on the part (stubs not counted) */
-    uint32_t shared_rows;       /* of them: rows some subject set points at (on every part; KETO_PART_SHARED) */
+    uint32_t shared_rows;       /* of them: rows on every part (KETO_PART_SHARED: set targets; KETO_PART_MIGRATE:
+                                   the replicated hot rows, shared_bytes their arena) */
     uint32_t root_rows;         /* of them: this part's root rows */
     uint64_t stub_rows;         /* KETO_PART_MIGRATE: stubs of other parts' rows */
 } keto_part_stats;

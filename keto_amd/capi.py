@@ -35,10 +35,10 @@ EXPORTS = [
     "keto_host_alloc", "keto_host_free", "keto_check_batch_pairs", "keto_tree_proto", "keto_tree_proto_all",
     "keto_check_steps_device", "keto_snapshot_part_stats", "keto_snapshot_apply", "keto_snapshot_version",
     "keto_snapshot_upload_part_mode", "keto_snapshot_part_stats_mode", "keto_part_stubs", "keto_part_filters",
-    "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy",
+    "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
-MIG_MAX_PARTS = 31
+MIG_MAX_PARTS = 30
 FILTER_WORDS = 22
 
 
@@ -110,7 +110,7 @@ class KPartStats(C.Structure):
 
 
 class KMigOut(C.Structure):
-    _fields_ = [("units", C.c_uint64 * 31), ("records", C.c_uint32 * 31), ("d_records", C.c_void_p),
+    _fields_ = [("units", C.c_uint64 * 30), ("records", C.c_uint32 * 30), ("d_records", C.c_void_p),
                 ("d_offsets", C.c_void_p), ("decided", C.c_uint32), ("undecided", C.c_uint32),
                 ("processed", C.c_uint32), ("reruns", C.c_uint32)]
 
@@ -302,10 +302,15 @@ class Snapshot:
         _check(lib.keto_snapshot_build(ns, len(namespaces), tt, C.c_uint64(len(rows)), C.byref(opts), C.byref(h)))
         return cls(h, lib)
 
-    def upload_part(self, part: int, n_parts: int, device: int = 0, mode: int = PART_SHARED):
-        """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part_mode)."""
-        _check(self.lib.keto_snapshot_upload_part_mode(self.h, C.c_uint32(part), C.c_uint32(n_parts),
-                                                       C.c_int32(device), C.c_uint32(mode)))
+    def upload_part(self, part: int, n_parts: int, device: int = 0, mode: int = PART_SHARED, hot_bytes: int = 0):
+        """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part_mode; a migrating
+        partition with hot_bytes > 0 replicates its hottest rows: keto_snapshot_upload_part_migrate)."""
+        if mode == PART_MIGRATE and hot_bytes:
+            _check(self.lib.keto_snapshot_upload_part_migrate(self.h, C.c_uint32(part), C.c_uint32(n_parts),
+                                                              C.c_int32(device), C.c_uint64(hot_bytes)))
+        else:
+            _check(self.lib.keto_snapshot_upload_part_mode(self.h, C.c_uint32(part), C.c_uint32(n_parts),
+                                                           C.c_int32(device), C.c_uint32(mode)))
         self.part, self.n_parts, self.part_mode = part, n_parts, mode
         return self
 

@@ -534,7 +534,8 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
 
 uint64_t keto_snapshot_version(const keto_snapshot* h) { return h ? h->s->version : 0; }
 
-int keto_snapshot_upload_part_mode(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode) {
+namespace {
+int upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode, uint64_t hot_bytes) {
     return guarded([&] {
         if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
         Snapshot& S = *h->s;
@@ -542,14 +543,25 @@ int keto_snapshot_upload_part_mode(keto_snapshot* h, uint32_t part, uint32_t n_p
         if (n_parts == 0 || part >= n_parts) throw Error{KETO_E_INVALID, "bad part"};
         if (mode != KETO_PART_SHARED && mode != KETO_PART_MIGRATE) throw Error{KETO_E_INVALID, "bad partition mode"};
         if (mode == KETO_PART_MIGRATE && n_parts > KETO_MIG_MAX_PARTS)
-            throw Error{KETO_E_INVALID, "a migrating partition has at most 31 parts"};
+            throw Error{KETO_E_INVALID, "a migrating partition has at most 30 parts"};
         S.part = part;
         S.n_parts = n_parts;
         S.part_mode = (int)mode;
+        S.hot_bytes = mode == KETO_PART_MIGRATE ? hot_bytes : 0;
         compute_layout(S);
         device_upload(S, device);
         return KETO_OK;
     });
+}
+}  // namespace
+
+int keto_snapshot_upload_part_mode(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode) {
+    return upload_part(h, part, n_parts, device, mode, 0);
+}
+
+int keto_snapshot_upload_part_migrate(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device,
+                                      uint64_t hot_bytes) {
+    return upload_part(h, part, n_parts, device, KETO_PART_MIGRATE, hot_bytes);
 }
 
 int keto_snapshot_upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device) {
@@ -562,7 +574,7 @@ int keto_snapshot_part_stats_mode(keto_snapshot* h, uint32_t part, uint32_t n_pa
         if (!h || !out || n_parts == 0 || part >= n_parts) throw Error{KETO_E_INVALID, "bad argument"};
         if (mode != KETO_PART_SHARED && mode != KETO_PART_MIGRATE) throw Error{KETO_E_INVALID, "bad partition mode"};
         if (mode == KETO_PART_MIGRATE && n_parts > KETO_MIG_MAX_PARTS)
-            throw Error{KETO_E_INVALID, "a migrating partition has at most 31 parts"};
+            throw Error{KETO_E_INVALID, "a migrating partition has at most 30 parts"};
         Snapshot& S = *h->s;
         if (S.dev) throw Error{KETO_E_INVALID, "part statistics need a host-only snapshot (device = -1)"};
         const uint32_t p0 = S.part, n0 = S.n_parts;
@@ -583,6 +595,10 @@ int keto_snapshot_part_stats_mode(keto_snapshot* h, uint32_t part, uint32_t n_pa
             else if (mode == KETO_PART_SHARED) ++out->shared_rows;
         }
         out->stub_rows = S.n_stubs;
+        if (mode == KETO_PART_MIGRATE) {                 // the replicated hot prefix
+            out->shared_rows = (uint32_t)S.hot_rows;
+            out->shared_bytes = (uint64_t)S.hot_units * HDR_WORDS * 4;
+        }
         S.part = p0;
         S.n_parts = n0;
         S.part_mode = m0;

@@ -13,8 +13,10 @@
 // one all-to-all each (keto_amd/multi.py); a decided request sends its decision to the part that
 // started it.
 //
-// Visit ids are global: (owner part, handle on the owner) for rows, (31, class) for colliding
-// Subject.String() keys (collision classes are computed on the host for the whole graph).
+// Visit ids are global: (owner part, handle on the owner) for rows, (30, handle) for the hot rows
+// every part holds at the same handle (the prefix [0, hot_units) of every part's arena), (31, class)
+// for colliding Subject.String() keys (collision classes are computed on the host for the whole
+// graph).
 //
 // Record (u32 words, 16-B units):
 //   head 8 words: idx (request index on its origin part) | info (kind 0..1, tset 2, decision 3..4,
@@ -52,6 +54,7 @@ constexpr uint32_t K_ENTER = 0, K_RESUME = 1, K_DECISION = 2;
 constexpr uint32_t F_SEQ = 1, F_TOP = 2;            // frame flags
 constexpr uint32_t MIG_FRAMES = 64;                 // saved frames of one search (max-depth <= 65)
 constexpr uint64_t VID_CLASS_PART = 31;
+constexpr uint32_t VID_HOT_PART = 30;                // rows every part holds (hot_units prefix)
 constexpr uint32_t EPOCH_MAX = (1u << 28) - 1u;
 constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_UNDECIDED = 2, RES_BIG = 3;
 // two lane tiers: many lanes with small visited tables, and a few with big ones for the searches
@@ -163,6 +166,7 @@ struct MigArgs {
     uint32_t n_allowed;
     uint32_t n_parts;
     uint32_t* err;
+    uint32_t hot_units;          // handles below it are rows every part holds at the same handle
 };
 
 constexpr uint32_t E_RECORD = 1, E_HANDLE = 2, E_POS = 3, E_IDX = 4, E_DEST = 5, E_TABLE = 6;
@@ -360,7 +364,7 @@ __device__ inline Outcome run_record(const MigArgs& a, uint32_t rj, MigVisited& 
                 res = RES_UNDECIDED;
                 break;
             }
-            const uint64_t rvid = remote ? vid_row(ch.x, ch.y) : vid_row(a.self, child);
+            const uint64_t rvid = remote ? vid_row(ch.x, ch.y) : vid_row(child < a.hot_units ? VID_HOT_PART : a.self, child);
             uint64_t vid = rvid;
             if (fl & F_SEQ) {
                 const uint32_t c = coll_find(a.coll, a.coll_mask, e);
@@ -521,6 +525,7 @@ __global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
 __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restrict__ q, uint32_t n, int32_t gmd,
                                                  const uint32_t* __restrict__ g_handle,
                                                  const uint8_t* __restrict__ owner, uint32_t n_rows, uint32_t self,
+                                                 uint32_t hot_units,
                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ off,
                                                  uint32_t* misrouted) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -545,7 +550,7 @@ __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restric
             trivial = true;                                      // no such row: no tuple names it
         } else {
             t_lo = g_handle[r.target];
-            t_hi = owner[r.target];
+            t_hi = t_lo < hot_units ? VID_HOT_PART : owner[r.target];
         }
     }
     if (trivial) info = K_DECISION | (self << 8);              // denied (decision 0)
@@ -556,29 +561,54 @@ __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restric
 }
 
 // group the round's output records by destination part: counts, then a scatter in which every
-// record takes its place with one 64-bit atomic (records << 36 | units) on its destination cursor
+// record takes its place; per wave and destination one 64-bit atomic (records << 36 | units) on the
+// destination's cursor, the wave's records placed by prefix sums (a same-address atomic per record
+// would serialize the whole round on one or two addresses)
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
 __global__ void __launch_bounds__(256) mig_count(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ len,
-                                                 const uint32_t* __restrict__ n, unsigned long long* __restrict__ cnt) {
+                                                 const uint32_t* __restrict__ n, uint32_t n_parts,
+                                                 unsigned long long* __restrict__ cnt) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *n || dest[i] >= MIG_MAX_PARTS) return;            // (the kernel only emits parts < n_parts)
-    atomicAdd(cnt + dest[i], (1ull << 36) | len[i]);
+    const bool valid = i < *n;
+    const uint32_t d = valid ? dest[i] : NONE, l = valid ? len[i] : 0u;
+    for (uint32_t p = 0; p < n_parts; ++p) {
+        const uint64_t m = __ballot(d == p);
+        if (!m) continue;
+        const uint32_t units = wave_sum(d == p ? l : 0u);
+        if (lane_id() == 0) atomicAdd(cnt + p, ((unsigned long long)__popcll(m) << 36) | units);
+    }
 }
 __global__ void __launch_bounds__(256) mig_scatter(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ unit,
                                                    const uint32_t* __restrict__ len, const uint32_t* __restrict__ n,
-                                                   const uint32_t* __restrict__ pool,
+                                                   uint32_t n_parts, const uint32_t* __restrict__ pool,
                                                    unsigned long long* __restrict__ cursor,
                                                    const uint64_t* __restrict__ unit_base,
                                                    const uint32_t* __restrict__ rec_base, uint32_t* __restrict__ send,
                                                    uint32_t* __restrict__ send_off) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *n || dest[i] >= MIG_MAX_PARTS) return;
-    const uint32_t d = dest[i], l = len[i];
-    const unsigned long long c = atomicAdd(cursor + d, (1ull << 36) | l);
-    const uint64_t u_in = c & ((1ull << 36) - 1), r_in = c >> 36;
-    const uint4* src = reinterpret_cast<const uint4*>(pool) + unit[i];
-    uint4* dst = reinterpret_cast<uint4*>(send) + unit_base[d] + u_in;
-    for (uint32_t k = 0; k < l; ++k) dst[k] = src[k];
-    send_off[rec_base[d] + r_in] = (uint32_t)u_in;
+    const uint32_t lane = lane_id();
+    const bool valid = i < *n;
+    const uint32_t d = valid ? dest[i] : NONE, l = valid ? len[i] : 0u;
+    for (uint32_t p = 0; p < n_parts; ++p) {
+        const uint64_t m = __ballot(d == p);
+        if (!m) continue;
+        const uint32_t incl = wave_scan(d == p ? l : 0u);
+        const uint32_t tot = __shfl(incl, 63);
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(cursor + p, ((unsigned long long)__popcll(m) << 36) | tot);
+        base = __shfl(base, 0);
+        if (d != p) continue;
+        const uint64_t u_in = (base & ((1ull << 36) - 1)) + incl - l;
+        const uint64_t r_in = (base >> 36) + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint4* src = reinterpret_cast<const uint4*>(pool) + unit[i];
+        uint4* dst = reinterpret_cast<uint4*>(send) + unit_base[p] + u_in;
+        for (uint32_t k = 0; k < l; ++k) dst[k] = src[k];
+        send_off[rec_base[p] + r_in] = (uint32_t)u_in;
+    }
 }
 
 template <class T>
@@ -802,6 +832,7 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     a.in_units = acc;
     a.n_allowed = M.n;
     a.n_parts = P;
+    a.hot_units = S.hot_units;
     auto launch = [&](Lanes& L, const uint32_t* list, const uint32_t* n_list, uint32_t n_max, uint32_t* big,
                       uint32_t* spill) {
         a.list = list;
@@ -865,7 +896,7 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     // group by destination
     HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
     if (n_out) {
-        hipLaunchKernelGGL(mig_count, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_len, M.ctr + 0,
+        hipLaunchKernelGGL(mig_count, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_len, M.ctr + 0, P,
                            M.cursor);
         HIP_OK(hipGetLastError());
     }
@@ -901,7 +932,7 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
         HIP_OK(hipMemcpyAsync(M.drec_base, drb, (P + 1) * 4, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
         hipLaunchKernelGGL(mig_scatter, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_unit, M.out_len,
-                           M.ctr + 0, M.pool, M.cursor, M.dunit_base, M.drec_base, M.send, M.send_off);
+                           M.ctr + 0, P, M.pool, M.cursor, M.dunit_base, M.drec_base, M.send, M.send_off);
         HIP_OK(hipGetLastError());
     }
     HIP_OK(hipMemcpyAsync(cnt, M.ctr, 16 * 4, hipMemcpyDeviceToHost, st));
@@ -944,7 +975,7 @@ void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gm
     HIP_OK(hipMemsetAsync(M.ctr, 0, 4, st));
     if (n) {
         hipLaunchKernelGGL(mig_start, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, n, gmd, M.g_handle, M.owner,
-                           M.n_rows, S.part, M.start, M.start_off, M.ctr);
+                           M.n_rows, S.part, S.hot_units, M.start, M.start_off, M.ctr);
         HIP_OK(hipGetLastError());
     }
     uint32_t bad = 0;

@@ -405,11 +405,13 @@ namespace {
 struct PartLayout {
     std::vector<uint32_t> unit_of_row, rows_by_unit, layout_units;
     std::vector<uint8_t> stub;
-    uint64_t n_units = 0, shared_words = 0, n_stubs = 0;
+    uint64_t n_units = 0, shared_words = 0, n_stubs = 0, hot_words = 0, hot_rows = 0;
 };
 
+// hot_band (PART_MIGRATE): rows of in-degree band >= hot_band are kept on every part; sorted
+// hottest first, they come first in every part's layout, identically
 void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t part, uint32_t n_parts, int mode,
-                 PartLayout& L) {
+                 uint32_t hot_band, PartLayout& L) {
     const uint32_t R = S.n_rows();
     L.unit_of_row.assign(R, NO_UNIT);
     // edge partitioning: PART_SHARED leaves other parts' root rows out of this device's arena;
@@ -421,7 +423,7 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
     if (n_parts > 1) {
         if (mode == PART_MIGRATE) {
             L.stub.assign(R, 0);
-            for (uint32_t r = 0; r < R; ++r) keep[r] = S.root_owner(r, n_parts) == part;
+            for (uint32_t r = 0; r < R; ++r) keep[r] = S.root_owner(r, n_parts) == part || band[r] >= hot_band;
             for (uint32_t r = 0; r < R; ++r) {
                 if (!keep[r]) continue;
                 const auto ed = S.row_edges(r);
@@ -454,6 +456,8 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
         if (held(r)) L.rows_by_unit[start[33 - band[r]]++] = r;
     L.layout_units.assign(kept, 0);
     L.shared_words = 0;
+    L.hot_words = 0;
+    L.hot_rows = 0;
     // test hook: start the layout this many words into the arena, so a small graph straddles the
     // segment boundary at 2^32 words (tests/test_gpu_synth.py)
     uint64_t w = 0;
@@ -488,6 +492,10 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
         L.layout_units[x] = (uint32_t)unit;
         if (!S.is_root[r] && !stub) L.shared_words += total;
         w += total;
+        if (mode == PART_MIGRATE && band[r] >= hot_band) {          // the replicated prefix so far
+            L.hot_words = w;
+            ++L.hot_rows;
+        }
     }
     L.n_units = w / HDR_WORDS;
 }
@@ -515,9 +523,25 @@ void compute_layout(Snapshot& S) {
         }
     }
     if (S.part_mode == PART_MIGRATE && S.n_parts > MIG_MAX_PARTS)
-        throw Error{KETO_E_INVALID, "a migrating partition has at most 31 parts"};
+        throw Error{KETO_E_INVALID, "a migrating partition has at most 30 parts"};
+    // PART_MIGRATE: the hottest in-degree bands whose rows fit S.hot_bytes are replicated
+    uint32_t hot_band = 64;                              // none
+    if (S.part_mode == PART_MIGRATE && S.hot_bytes > 0 && S.n_parts > 1) {
+        std::vector<uint64_t> bw(34, 0);
+        for (uint32_t r = 0; r < R; ++r) {
+            if (!band[r]) continue;
+            const uint32_t h = S.row_hlog2(r);
+            bw[band[r]] += (h ? (1ull << h) : 0) + CB_WORDS + HDR_WORDS + ((row_size(S, r) + 3) & ~3ull);
+        }
+        uint64_t acc = 0;
+        for (uint32_t b = 33; b >= 1; --b) {
+            if ((acc + bw[b]) * 4 > S.hot_bytes) break;
+            acc += bw[b];
+            hot_band = b;
+        }
+    }
     PartLayout L;
-    layout_part(S, band, S.part, S.n_parts, S.part_mode, L);
+    layout_part(S, band, S.part, S.n_parts, S.part_mode, hot_band, L);
     S.unit_of_row = std::move(L.unit_of_row);
     S.rows_by_unit = std::move(L.rows_by_unit);
     S.layout_units = std::move(L.layout_units);
@@ -525,6 +549,8 @@ void compute_layout(Snapshot& S) {
     S.n_stubs = L.n_stubs;
     S.n_units = L.n_units;
     S.shared_words = L.shared_words;
+    S.hot_units = (uint32_t)(L.hot_words / HDR_WORDS);
+    S.hot_rows = L.hot_rows;
     S.g_handle.clear();
     if (S.part_mode == PART_MIGRATE) {
         // every row's handle on its owner part: the layouts of the other parts are computed here too
@@ -534,7 +560,7 @@ void compute_layout(Snapshot& S) {
             const std::vector<uint32_t>* u = &S.unit_of_row;
             PartLayout Q;
             if (q != S.part) {
-                layout_part(S, band, q, S.n_parts, S.part_mode, Q);
+                layout_part(S, band, q, S.n_parts, S.part_mode, hot_band, Q);
                 u = &Q.unit_of_row;
             }
             for (uint32_t r = 0; r < R; ++r)

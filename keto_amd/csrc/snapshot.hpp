@@ -81,7 +81,7 @@ constexpr uint32_t HDR_REMOTE = 32u;
 // upload modes of an edge-partitioned snapshot (keto_snapshot_upload_part_mode)
 constexpr int PART_SHARED = 0;    // rows some set points at on every part, root rows by hash
 constexpr int PART_MIGRATE = 1;   // every row on one part by hash, stubs for remote set targets
-constexpr uint32_t MIG_MAX_PARTS = 31;
+constexpr uint32_t MIG_MAX_PARTS = 30;   // visit-id part field: 0..29 parts, 30 replicated rows, 31 classes
 // Closure filter of a row some subject set points at: a 704-bit, one-hash bloom filter of every
 // subject id reachable from the row through any number of subject sets (its own ids included).  A
 // check entering such a row for a requested id the filter rules out skips the row: every node the
@@ -206,6 +206,11 @@ struct Snapshot {
     std::vector<uint8_t> stub;
     std::vector<uint32_t> g_handle;
     uint64_t n_stubs = 0;
+    // PART_MIGRATE: the rows most subject sets point at are replicated on every part, hottest first, up
+    // to hot_bytes of arena; they form the identical prefix [0, hot_units) of every part's arena
+    uint64_t hot_bytes = 0;
+    uint32_t hot_units = 0;
+    uint64_t hot_rows = 0;
     bool mig_ready = false;   // PART_MIGRATE: closure filters final (part_closure_done, or one part)
     // r is held by this device (owned, or on every part); stubs are not rows of this part
     bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT && (stub.empty() || !stub[r]); }

@@ -16,12 +16,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _parts_from_csr(g, n_parts):
+def _parts_from_csr(g, n_parts, hot_bytes=0):
     from keto_amd.capi import Snapshot
     parts = []
     for p in range(n_parts):
         s = Snapshot.from_csr(g.namespaces, g.row_ns, g.row_obj, g.row_rel, g.row_ptr, g.edges, device=-1)
-        parts.append(s.upload_part(p, n_parts, 0, mode=PART_MIGRATE))
+        parts.append(s.upload_part(p, n_parts, 0, mode=PART_MIGRATE, hot_bytes=hot_bytes))
     return parts
 
 
@@ -53,12 +53,13 @@ def _mig_decide(parts, q, gmd):
     return out, rounds
 
 
-@pytest.mark.parametrize("n_parts", [1, 2, 3, 5])
-def test_powerlaw_parts_match_replicated(n_parts):
+@pytest.mark.parametrize("n_parts,hot_bytes", [(1, 0), (2, 0), (3, 0), (5, 0), (2, 1 << 20), (3, 4 << 20), (4, 1 << 30)])
+def test_powerlaw_parts_match_replicated(n_parts, hot_bytes):
+    """hot_bytes > 0: the hottest rows replicated on every part (1 GiB: every set target, no stubs)."""
     from tools import synth
     g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 512), threads=16)
     full = g.snapshot(device=0)
-    parts = _parts_from_csr(g, n_parts)
+    parts = _parts_from_csr(g, n_parts, hot_bytes)
     q = g.queries(60000, seed=140 + n_parts, depth=5)
     rng = np.random.default_rng(n_parts)
     q["max_depth"] = rng.integers(-1, 7, size=len(q))
@@ -66,8 +67,10 @@ def test_powerlaw_parts_match_replicated(n_parts):
         want = full.check_batch_ids(full.with_handles(q), gmd)
         got, rounds = _mig_decide(parts, q, gmd)
         assert (got == want).all(), f"gmd {gmd}: {int((got != want).sum())} mismatches"
-        if n_parts > 1:
+        if n_parts > 1 and hot_bytes < (1 << 30):
             assert rounds >= 2                                    # searches did cross parts
+        if hot_bytes >= (1 << 30):
+            assert rounds == 0 and all(len(p.part_stubs()) == 0 for p in parts)
     if n_parts > 1:
         st = [p.stats()["device_bytes"] for p in parts]
         assert max(st) < full.stats()["device_bytes"]
@@ -80,7 +83,7 @@ def test_nested_groups_deep_parts_match_replicated():
     g = synth.SynthGraph(dict(n_docs=0, n_folders=0, n_groups=1 << 14, n_users=1 << 14, target_edges=0, seed=3),
                          threads=16, kind="nested", chain=32)
     full = g.snapshot(device=0)
-    parts = _parts_from_csr(g, 3)
+    parts = _parts_from_csr(g, 3, hot_bytes=64 << 10)
     q = g.queries_nested(6000, seed=5, depths=(5, 16, 32, 0, 40))
     for gmd in (32, 40):
         want = full.check_batch_ids(full.with_handles(q), gmd)
@@ -185,7 +188,9 @@ def test_random_graphs_match_oracle(seed):
     rows = rows_from_tuples(ns, tuples, raw)
     full = keto_amd.Snapshot.build(ns, rows, page_size=ps, device=0)
     n_parts = 2 + seed % 3
-    parts = [keto_amd.Snapshot.build(ns, rows, page_size=ps, device=-1).upload_part(p, n_parts, 0, mode=PART_MIGRATE)
+    hot = [0, 256, 4096][seed % 3 if seed % 2 else 0]
+    parts = [keto_amd.Snapshot.build(ns, rows, page_size=ps, device=-1).upload_part(p, n_parts, 0, mode=PART_MIGRATE,
+                                                                                    hot_bytes=hot)
              for p in range(n_parts)]
     checks = random_checks(seed, alph, k=40)
     for gmd in sorted({c[2] for c in checks}):

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--hot-mb", type=float, nargs="+", default=[0.0],
+                    help="replicated hot rows per part (MB of arena; keto_snapshot_upload_part_migrate)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -59,13 +61,13 @@ def main():
     want = d_out.cpu().numpy()
     full_bytes = full.stats()["device_bytes"]
     del full, qd
-    for P in a.parts:
-        log(f"P = {P}: building and uploading {P} parts")
+    for P, hot_mb in [(P, h) for P in a.parts for h in (a.hot_mb if P > 1 else [0.0])]:
+        log(f"P = {P}, hot {hot_mb} MB: building and uploading {P} parts")
         t0 = time.perf_counter()
         parts = []
         for p in range(P):
             s = Snapshot.from_csr(g.namespaces, g.row_ns, g.row_obj, g.row_rel, g.row_ptr, g.edges, device=-1)
-            parts.append(s.upload_part(p, P, 0, mode=PART_MIGRATE))
+            parts.append(s.upload_part(p, P, 0, mode=PART_MIGRATE, hot_bytes=int(hot_mb * 1e6)))
         t_up = time.perf_counter() - t0
         t0 = time.perf_counter()
         crounds = close_filters_loopback(parts)
@@ -108,7 +110,8 @@ def main():
         got = np.full(a.batch, 255, dtype=np.uint8)
         for p in range(P):
             got[where[p]] = dec[p].cpu().numpy()
-        line = {"what": "migrating partition, loopback on one MI355X", "parts": P, "tuples": int(g.n_edges),
+        line = {"what": "migrating partition, loopback on one MI355X", "parts": P, "hot_mb": hot_mb,
+                "tuples": int(g.n_edges),
                 "rows": int(g.n_rows), "batch": a.batch, "max_depth": a.depth,
                 "ms_per_batch": round(ms, 2), "checks_per_s": round(a.batch / (ms * 1e-3), 1),
                 "replicated_ms_per_batch": round(rep_ms, 3),
