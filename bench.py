@@ -77,6 +77,13 @@ def parse():
     ap.add_argument("--partitioned", action="store_true",
                     help="edge-partitioned snapshot (root rows split by hash(ns, object)); each step routes the "
                          "batch to the owners with RCCL all-to-all, checks, and returns the decisions")
+    ap.add_argument("--part-mode", choices=["shared", "migrate"], default="shared",
+                    help="--partitioned layout: shared = set targets on every part; migrate = every row on one part, "
+                         "searches move between parts as records (keto_mig_*), one all-to-all per round")
+    ap.add_argument("--hot-mb", type=float, default=0.0, help="--part-mode migrate: replicated hot rows per part (MB)")
+    ap.add_argument("--check-parity", action="store_true",
+                    help="partitioned runs: every rank also checks its batch on a replicated snapshot and the "
+                         "mismatches are summed over ranks (small scales: needs the whole graph on each GPU)")
     ap.add_argument("--no-work", action="store_true", help="skip the roofline / cpu_baseline legs (profiling runs)")
     ap.add_argument("--e2e-steps", type=int, default=5,
                     help="batches timed end to end through the host API (keto_check_batch_rows, pinned buffers); 0 = skip")
@@ -213,7 +220,20 @@ def main():
     t_gen = time.time() - t0
     log(f"rank {rank}: {g.n_edges} tuples, {g.n_rows} rows; building + uploading the snapshot")
     t0 = time.time()
-    snap = g.snapshot_part(rank, world, dev) if a.partitioned else g.snapshot(device=dev)
+    migrate = a.partitioned and a.part_mode == "migrate"
+    # collectives of the partitioned modes: on the GPU with RCCL, staged through the host with gloo
+    comm = f"cuda:{dev}" if backend == "nccl" else "cpu"
+    if migrate:
+        from keto_amd.capi import PART_MIGRATE
+        from keto_amd.multi import close_filters_dist
+        snap = g.snapshot_part(rank, world, dev, mode=PART_MIGRATE, hot_bytes=int(a.hot_mb * 1e6))
+        if world > 1:
+            rounds = close_filters_dist(snap, device=comm)
+            log(f"rank {rank}: closure filters exchanged in {rounds} rounds")
+        else:
+            snap.part_closure_done(True)
+    else:
+        snap = g.snapshot_part(rank, world, dev) if a.partitioned else g.snapshot(device=dev)
     t_snap = time.time() - t0
     q = g.queries(a.batch, seed=1000 + rank, depth=a.depth, threads=a.threads)
     d_out = torch.empty(a.batch, dtype=torch.uint8, device=f"cuda:{dev}")
@@ -225,13 +245,19 @@ def main():
         d_q = torch.from_numpy(q.view(np.int32).reshape(-1, 4).copy()).to(f"cuda:{dev}")
         owner_dev = torch.from_numpy(snap.row_owner(np.arange(g.n_rows, dtype=np.uint32), world).astype(np.int16)
                                      ).to(f"cuda:{dev}")
-        routed = [0, None]
+        routed = [0, None, 0]
+        if migrate:
+            from keto_amd.multi import SnapshotMigEngine, mig_check
+            engine = SnapshotMigEngine(snap, f"cuda:{dev}")
 
         def step():
-            recv, state = route_device(d_q, owner_dev, rank, world)
-            dec = torch.empty(len(recv), dtype=torch.uint8, device=d_q.device)
-            snap.check_batch_rows_device(recv.data_ptr(), len(recv), dec.data_ptr(), a.depth, sp)
-            send_back(dec, state, d_out, world)
+            recv, state = route_device(d_q, owner_dev, rank, world, comm_device=comm)
+            if migrate:
+                dec, routed[2] = mig_check(engine, recv, a.depth, device=f"cuda:{dev}", comm_device=comm)
+            else:
+                dec = torch.empty(len(recv), dtype=torch.uint8, device=d_q.device)
+                snap.check_batch_rows_device(recv.data_ptr(), len(recv), dec.data_ptr(), a.depth, sp)
+            send_back(dec, state, d_out, world, comm_device=comm)
             routed[0] = len(recv)
             routed[1] = recv
     else:
@@ -285,7 +311,7 @@ def main():
     cpu = None
     parity = None
     ref_sql = None
-    if rank == 0 and not a.no_work:
+    if rank == 0 and not a.no_work and not migrate:
         # oracle table over a bounded sample of the batch: every tuple those requests can reach
         ns = min(a.cpu_sample, a.batch)
         sample = q[:ns]
@@ -355,6 +381,15 @@ def main():
             if a.sql_sample > 0:
                 ref_sql = sql_leg(g, q, a, gpu_out)
 
+    part_parity = None
+    if a.partitioned and a.check_parity:
+        full = g.snapshot(device=dev)
+        want = full.check_batch_ids(full.with_handles(q), a.depth)
+        bad = torch.tensor([int((want != gpu_out).sum())], dtype=torch.int64, device=comm if world > 1 else "cpu")
+        if world > 1:
+            dist.all_reduce(bad)
+        part_parity = {"requests": world * a.batch, "mismatches_vs_replicated": int(bad.item())}
+        del full
     if e2e is not None and roofline is not None:
         e2e["frac"] = round(roofline["alg_bytes_per_launch"] / (e2e["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if e2e is not None:
@@ -366,20 +401,25 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "powerlaw-acl-1B (BASELINE config #4) on one GPU per rank, " +
-                                   ("edge-partitioned snapshot, requests routed by all-to-all" if a.partitioned
+                                   ("migrating partition (every row on one part, searches move between parts as "
+                                    f"records, {a.hot_mb} MB of replicated hot rows per part)" if migrate else
+                                    "edge-partitioned snapshot, requests routed by all-to-all" if a.partitioned
                                     else "replicated snapshot"),
                        "tuples": int(g.n_edges), "set_edge_fraction": round(g.n_set_edges / max(1, g.n_edges), 4),
                        "rows": int(g.n_rows), "checks_per_gpu_per_step": a.batch, "max_depth": a.depth,
-                       "global_batch": a.batch * world, "parallelism": f"partitioned-{world}" if a.partitioned else f"replicated-dp{world}",
+                       "global_batch": a.batch * world,
+                       "parallelism": (f"migrating-{world}" if migrate else f"partitioned-{world}" if a.partitioned
+                                       else f"replicated-dp{world}"),
                        "scale": a.scale},
             "roofline": roofline,
             "end_to_end": e2e,
             "cpu_baseline": cpu,
             "ref_sql": ref_sql,
-            "parity": parity,
+            "parity": parity if part_parity is None else part_parity,
             "detail": {"tier0_ms": round(tier0_ms, 3), "tier1_ms": round(tier1_ms, 3),
                        "tier0_overflow_requests": overflow, "allowed_fraction": round(allowed_rate, 4),
-                       "gen_s": round(t_gen, 1), "snapshot_upload_s": round(t_snap, 1), "work": work},
+                       "gen_s": round(t_gen, 1), "snapshot_upload_s": round(t_snap, 1), "work": work,
+                       "migrate_rounds_last_step": routed[2] if migrate else None},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -118,7 +118,20 @@ class PartitionedChecker:
         return res
 
 
-def route_device(d_reqs, owner_dev, rank: int, world: int, group=None):
+def _a2a(out, inp, out_splits=None, in_splits=None, group=None, comm_device=None):
+    """all_to_all_single, staged through comm_device when the backend cannot use the tensors' own
+    device (gloo with GPU tensors: the rehearsal of a multi-rank run on a smaller box)."""
+    import torch.distributed as dist
+    if comm_device is None or str(comm_device) == str(inp.device):
+        dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+        return
+    o = out.new_empty(out.shape, device=comm_device)
+    dist.all_to_all_single(o, inp.to(comm_device), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                           group=group)
+    out.copy_(o)
+
+
+def route_device(d_reqs, owner_dev, rank: int, world: int, group=None, comm_device=None):
     """Device-side routing of a partitioned check batch (all tensors on this rank's GPU).
 
     d_reqs: int32 [n, 4] keto_check_ids naming rows by row id; owner_dev: int16 [n_rows] owner part
@@ -144,14 +157,14 @@ def route_device(d_reqs, owner_dev, rank: int, world: int, group=None):
         return send, (order, cs, cs)
     counts = torch.tensor(cs, dtype=torch.int64, device=d_reqs.device)
     in_counts = torch.empty_like(counts)
-    dist.all_to_all_single(in_counts, counts, group=group)
+    _a2a(in_counts, counts, group=group, comm_device=comm_device)
     ics = in_counts.cpu().tolist()
     recv = torch.empty((sum(ics), 4), dtype=d_reqs.dtype, device=d_reqs.device)
-    dist.all_to_all_single(recv, send, output_split_sizes=ics, input_split_sizes=cs, group=group)
+    _a2a(recv, send, ics, cs, group, comm_device)
     return recv, (order, cs, ics)
 
 
-def send_back(decisions, state, out, world: int, group=None):
+def send_back(decisions, state, out, world: int, group=None, comm_device=None):
     """Return the decisions of route_device()'s received requests to their origins, in the
     origin's order, into `out` (uint8 [n] on the device; keto_unroute_device)."""
     import torch
@@ -162,7 +175,7 @@ def send_back(decisions, state, out, world: int, group=None):
         back = decisions
     else:
         back = torch.empty(sum(cs), dtype=torch.uint8, device=decisions.device)
-        dist.all_to_all_single(back, decisions.contiguous(), output_split_sizes=cs, input_split_sizes=ics, group=group)
+        _a2a(back, decisions.contiguous(), cs, ics, group, comm_device)
     capi.unroute_device(back.data_ptr(), order.data_ptr(), sum(cs), out.data_ptr(),
                         torch.cuda.current_stream(out.device).cuda_stream)
 
@@ -219,10 +232,12 @@ class SnapshotMigEngine:
         return buf, off
 
 
-def mig_check(engine, routed, global_max_depth=5, group=None, device="cuda:0", max_rounds=1 << 20):
+def mig_check(engine, routed, global_max_depth=5, group=None, device="cuda:0", max_rounds=1 << 20,
+              comm_device=None):
     """Decisions (uint8 [len(routed)] on `device`) of the row-id requests routed to this rank, all
     owned by its part, on a migrating partition with one rank per part.  Every rank calls this
-    collectively.  engine: SnapshotMigEngine (or an object with the same begin/round/fetch).
+    collectively.  engine: SnapshotMigEngine (or an object with the same begin/round/fetch);
+    comm_device: where the collectives run when the backend cannot use `device` (gloo).
     Returns (decisions, rounds)."""
     import torch
     import torch.distributed as dist
@@ -232,7 +247,7 @@ def mig_check(engine, routed, global_max_depth=5, group=None, device="cuda:0", m
     rounds = 0
     while True:
         mine = sum(out["records"])
-        tot = torch.tensor([mine], dtype=torch.int64, device=device)
+        tot = torch.tensor([mine], dtype=torch.int64, device=comm_device or device)
         dist.all_reduce(tot, group=group)
         if int(tot.item()) == 0:
             return dec, rounds
@@ -242,14 +257,13 @@ def mig_check(engine, routed, global_max_depth=5, group=None, device="cuda:0", m
         units, recs = out["units"][:world], out["records"][:world]
         cnt = torch.tensor([[u, r] for u, r in zip(units, recs)], dtype=torch.int64, device=device).reshape(-1)
         in_cnt = torch.empty_like(cnt)
-        dist.all_to_all_single(in_cnt, cnt, group=group)
+        _a2a(in_cnt, cnt, group=group, comm_device=comm_device)
         ic = in_cnt.reshape(world, 2).cpu().tolist()
         in_units, in_recs = [c[0] for c in ic], [c[1] for c in ic]
         rbuf = torch.empty(sum(in_units) * 16, dtype=torch.uint8, device=device)
-        dist.all_to_all_single(rbuf, buf, output_split_sizes=[u * 16 for u in in_units],
-                               input_split_sizes=[u * 16 for u in units], group=group)
+        _a2a(rbuf, buf, [u * 16 for u in in_units], [u * 16 for u in units], group, comm_device)
         roff = torch.empty(sum(in_recs), dtype=torch.int32, device=device)
-        dist.all_to_all_single(roff, off, output_split_sizes=in_recs, input_split_sizes=recs, group=group)
+        _a2a(roff, off, in_recs, recs, group, comm_device)
         out = engine.round(rbuf, roff, in_recs, in_units)
         rounds += 1
 

@@ -137,12 +137,13 @@ class SynthGraph:
         return Snapshot.from_csr(self.namespaces, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                                  device=device)
 
-    def snapshot_part(self, part: int, n_parts: int, device=0):
-        """This part's share of the edge-partitioned snapshot (keto_snapshot_upload_part)."""
+    def snapshot_part(self, part: int, n_parts: int, device=0, mode=0, hot_bytes=0):
+        """This part's share of the edge-partitioned snapshot (keto_snapshot_upload_part_mode; mode 1 =
+        the migrating partition, with hot_bytes of replicated hot rows)."""
         from keto_amd.capi import Snapshot
         s = Snapshot.from_csr(self.namespaces, self.row_ns, self.row_obj, self.row_rel, self.row_ptr, self.edges,
                               device=-1)
-        return s.upload_part(part, n_parts, device)
+        return s.upload_part(part, n_parts, device, mode=mode, hot_bytes=hot_bytes)
 
     def relation_names(self):
         """Relation names by id (byte order = id order): the generators' relation ids."""
