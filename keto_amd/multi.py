@@ -241,8 +241,12 @@ def mig_check(engine, routed, global_max_depth=5, group=None, device="cuda:0", m
     Returns (decisions, rounds)."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
     dec = torch.full((len(routed),), 255, dtype=torch.uint8, device=device)
+    if not dist.is_initialized():                      # one part, no process group: a local loop
+        dl, rounds = mig_check_loopback([engine], [routed], global_max_depth, device, max_rounds)
+        dec.copy_(dl[0])
+        return dec, rounds
+    world = dist.get_world_size(group)
     out = engine.begin(routed, dec, global_max_depth)
     rounds = 0
     while True:
