@@ -415,6 +415,11 @@ int64_t keto_tree_proto(const keto_snapshot* s, const keto_tree_arena* a, uint32
  * returned (call with buf = NULL to size it). */
 int64_t keto_tree_proto_all(const keto_snapshot* s, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
                             uint64_t* offsets);
+/* keto_tree_proto_all encoded on the GPU from the arena's nodes and the snapshot's strings (uploaded
+ * to the snapshot's device on first use): the same bytes and offsets.  offsets
+ * is always written; buf only when cap >= the returned total (call with buf = NULL to size it). */
+int64_t keto_tree_proto_all_device(keto_snapshot* s, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
+                                   uint64_t* offsets);
 
 /* String of a subject reference used in keto_tree_node.subject (Subject.String(), definitions.go:163-169). */
 int64_t keto_subject_string(const keto_snapshot* s, uint32_t subject, char* buf, uint64_t cap);

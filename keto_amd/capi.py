@@ -36,6 +36,7 @@ EXPORTS = [
     "keto_check_steps_device", "keto_snapshot_part_stats", "keto_snapshot_apply", "keto_snapshot_version",
     "keto_snapshot_upload_part_mode", "keto_snapshot_part_stats_mode", "keto_part_stubs", "keto_part_filters",
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
+    "keto_tree_proto_all_device",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -153,6 +154,7 @@ def load():
     lib.keto_tree_json.restype = C.c_int64
     lib.keto_tree_proto.restype = C.c_int64
     lib.keto_tree_proto_all.restype = C.c_int64
+    lib.keto_tree_proto_all_device.restype = C.c_int64
     lib.keto_subject_string.restype = C.c_int64
     lib.keto_route_work_bytes.restype = C.c_uint64
     lib.keto_snapshot_version.restype = C.c_uint64
@@ -558,9 +560,10 @@ class Snapshot:
             self.lib.keto_tree_arena_free(a)
         return status, offs, nodes
 
-    def expand_batch_ids_proto(self, roots: np.ndarray, depths: np.ndarray, global_max_depth=5):
-        """Pre-resolved roots -> every tree's SubjectTree proto in one buffer (keto_tree_proto_all).
-        Returns (status[n], offsets[n+1] into the blob, blob, expand seconds, encode seconds)."""
+    def expand_batch_ids_proto(self, roots: np.ndarray, depths: np.ndarray, global_max_depth=5, device=False):
+        """Pre-resolved roots -> every tree's SubjectTree proto in one buffer (keto_tree_proto_all, or
+        keto_tree_proto_all_device).  Returns (status[n], offsets[n+1] into the blob, blob, expand seconds,
+        encode seconds)."""
         import time
         roots = np.ascontiguousarray(roots, dtype=np.uint32)
         depths = np.ascontiguousarray(depths, dtype=np.int32)
@@ -572,22 +575,31 @@ class Snapshot:
                                               C.c_int32(global_max_depth), C.byref(a)))
         t1 = time.perf_counter()
         try:
-            offs = np.zeros(n + 1, dtype=np.uint64)
-            total = self.lib.keto_tree_proto_all(self.h, a, None, C.c_uint64(0), offs.ctypes.data_as(C.c_void_p))
-            _check(min(0, total))
-            t2 = time.perf_counter()
-            blob = np.zeros(max(1, total), dtype=np.uint8)
-            got = self.lib.keto_tree_proto_all(self.h, a, blob.ctypes.data_as(C.c_void_p), C.c_uint64(total),
-                                               offs.ctypes.data_as(C.c_void_p))
-            t3 = time.perf_counter()
-            assert got == total
+            offs, blob, t_enc = self._proto_all(a, n, device=device)
             status = np.array([self.lib.keto_tree_status(a, C.c_uint32(i)) for i in range(n)], dtype=np.int32)
         finally:
             self.lib.keto_tree_arena_free(a)
-        return status, offs, blob[:total].tobytes(), t1 - t0, min(t2 - t1, t3 - t2)
+        return status, offs, blob, t1 - t0, t_enc
 
-    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False):
-        """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes][, proto])."""
+    def _proto_all(self, a, n, device=False):
+        """(offsets[n+1], blob, seconds of the filling call) of keto_tree_proto_all[_device]."""
+        import time
+        fn = self.lib.keto_tree_proto_all_device if device else self.lib.keto_tree_proto_all
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        total = fn(self.h, a, None, C.c_uint64(0), offs.ctypes.data_as(C.c_void_p))
+        _check(min(0, total))
+        blob = np.zeros(max(1, total), dtype=np.uint8)
+        t0 = time.perf_counter()
+        got = fn(self.h, a, blob.ctypes.data_as(C.c_void_p), C.c_uint64(total), offs.ctypes.data_as(C.c_void_p))
+        dt = time.perf_counter() - t0
+        _check(min(0, got))
+        assert got == total
+        return offs, blob[:total].tobytes(), dt
+
+    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False, proto_all=None):
+        """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes][, proto]);
+        proto_all = "host" / "device": also every tree's bytes from keto_tree_proto_all[_device]
+        (returned as (list, per-tree bytes list))."""
         keep = _Keep()
         n = len(reqs)
         arr = (KExpandReq * max(1, n))()
@@ -621,6 +633,9 @@ class Snapshot:
                         pb = buf.raw[:pn]
                     item = item + (pb,)
                 out.append(item)
+            if proto_all:
+                offs, blob, _ = self._proto_all(a, n, device=proto_all == "device")
+                return out, [blob[int(offs[i]):int(offs[i + 1])] for i in range(n)]
         finally:
             self.lib.keto_tree_arena_free(a)
         return out

@@ -918,6 +918,38 @@ int64_t keto_tree_proto_all(const keto_snapshot* h, const keto_tree_arena* a, ui
     return (int64_t)offsets[n];
 }
 
+int64_t keto_tree_proto_all_device(keto_snapshot* h, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
+                                   uint64_t* offsets) {
+    return guarded([&]() -> int64_t {
+        if (!h || !a || !offsets) throw Error{KETO_E_INVALID, "NULL argument"};
+        const uint32_t n = (uint32_t)a->r.status.size();
+        // the nodes of the trees (other statuses have none), tree t = [toff[t], toff[t + 1])
+        std::vector<uint64_t> toff(n + 1, 0);
+        bool all = true;
+        for (uint32_t i = 0; i < n; ++i) {
+            const bool tree = a->r.status[i] == KETO_EXPAND_TREE;
+            all &= tree || a->r.offset[i] == a->r.offset[i + 1];
+        }
+        std::vector<keto_tree_node> sel;
+        const keto_tree_node* nodes = a->r.nodes.data();
+        uint64_t n_nodes = a->r.nodes.size();
+        if (all) {
+            for (uint32_t i = 0; i <= n; ++i) toff[i] = a->r.offset[i];
+        } else {
+            for (uint32_t i = 0; i < n; ++i) {
+                toff[i] = sel.size();
+                if (a->r.status[i] == KETO_EXPAND_TREE)
+                    sel.insert(sel.end(), a->r.nodes.begin() + a->r.offset[i], a->r.nodes.begin() + a->r.offset[i + 1]);
+            }
+            toff[n] = sel.size();
+            nodes = sel.data();
+            n_nodes = sel.size();
+        }
+        return (int64_t)device_tree_proto(*h->s, nodes, n_nodes, toff.data(), n, a->ov_base, a->ov_keys, a->extra_base,
+                                          a->extra, buf, cap, offsets);
+    });
+}
+
 int64_t keto_subject_string(const keto_snapshot* h, uint32_t subject, char* buf, uint64_t cap) {
     if (!h) return KETO_E_INVALID;
     SubjectFields f = fields_of(*h->s, nullptr, subject);

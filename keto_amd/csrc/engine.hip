@@ -2549,6 +2549,7 @@ void device_release(Snapshot& S) {
     DeviceState& D = *S.dev;
     (void)hipSetDevice(D.device);
     mig_release(S);
+    S.proto.reset();
     for (auto& W : D.ws) {
         for (auto& t : W.tiers) free_tier(t);
         if (W.lists) (void)hipFree(W.lists);

@@ -169,7 +169,7 @@ struct MigArgs {
     uint32_t hot_units;          // handles below it are rows every part holds at the same handle
 };
 
-constexpr uint32_t E_RECORD = 1, E_HANDLE = 2, E_POS = 3, E_IDX = 4, E_DEST = 5, E_TABLE = 6;
+constexpr uint32_t E_RECORD = 1, E_HANDLE = 2, E_POS = 3, E_IDX = 4, E_DEST = 5;
 __device__ inline void report(const MigArgs& a, uint32_t code, uint32_t rj, uint64_t v) {
     if (atomicAdd(a.err, 1u) == 0) {
         a.err[1] = code;

@@ -155,6 +155,10 @@ struct MigState;         // migrate.hip
 struct MigStateDeleter {
     void operator()(MigState* m) const;      // migrate.hip
 };
+struct ProtoState;       // proto.hip
+struct ProtoStateDeleter {
+    void operator()(ProtoState* p) const;    // proto.hip
+};
 
 struct Snapshot {
     // ---- config
@@ -255,6 +259,7 @@ struct Snapshot {
     int device = -1;
     std::unique_ptr<DeviceState, DeviceStateDeleter> dev;
     std::unique_ptr<MigState, MigStateDeleter> mig;      // migrating-partition batches (migrate.hip)
+    std::unique_ptr<ProtoState, ProtoStateDeleter> proto; // strings on the device for tree encoding (proto.hip)
     std::mutex mu;
 
     ~Snapshot();
@@ -378,6 +383,11 @@ void mig_begin(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gm
 void mig_round(Snapshot& s, const void* d_in, const uint32_t* d_in_off, const uint32_t* in_records,
                const uint64_t* in_units, void* stream, MigOut& out);
 void mig_release(Snapshot& s);
+// acl.SubjectTree bytes of trees (pre-order nodes, tree t = nodes[tree_off[t], tree_off[t+1])) encoded
+// on the device (proto.hip): offsets[n_trees + 1] always; buf written when cap >= the total returned
+uint64_t device_tree_proto(Snapshot& s, const keto_tree_node* nodes, uint64_t n_nodes, const uint64_t* tree_off,
+                           uint32_t n_trees, uint32_t ov_base, const std::vector<RowKey>& ov_keys, uint32_t extra_base,
+                           const std::vector<std::string>& extra, uint8_t* buf, uint64_t cap, uint64_t* offsets);
 void device_copy(void* dst, const void* src, uint64_t bytes, void* stream);   // D2D, synchronous
 struct ExpandResult {
     std::vector<uint8_t> status;

@@ -21,7 +21,7 @@ def test_host_library_under_asan(tmp_path):
         o = str(tmp_path / (f + ".o"))
         subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *san, "-c", os.path.join(csrc, f), "-o", o])
         objs.append(o)
-    for f in ("engine.hip", "route.hip", "migrate.hip"):
+    for f in ("engine.hip", "route.hip", "migrate.hip", "proto.hip"):
         o = str(tmp_path / (f + ".o"))
         subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-Xarch_host",
                                "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-fno-omit-frame-pointer",

@@ -69,6 +69,21 @@ def test_random_graphs_match_oracle(seed, wide):
             assert (have, js) == want, (seed, s, d, g)
 
 
+@pytest.mark.parametrize("seed", range(2100, 2160))
+def test_random_expand_proto_device_equals_host(seed):
+    """keto_tree_proto_all_device on quirk-heavy random graphs (wildcard roots answered by batch-local
+    rows, subject ids the snapshot does not know, empty fields, unknown namespaces, collisions): the
+    host encoder's bytes, tree by tree."""
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=seed % 3 == 0)
+    snap = _snapshot(ns, rows_from_tuples(ns, tuples, raw), ps)
+    exps = random_expands(seed, alph, k=24)
+    for g in sorted({e[2] for e in exps}):
+        grp = [(subj(s), d) for s, d, gg in exps if gg == g]
+        _, host = snap.expand_batch(grp, g, proto_all="host")
+        _, dev = snap.expand_batch(grp, g, proto_all="device")
+        assert host == dev, (seed, g)
+
+
 @pytest.mark.parametrize("seed", range(2000, 2060))
 def test_random_expand_proto_matches_oracle(seed):
     """keto_tree_proto = proto.Marshal(Tree.ToProto()) of the oracle's tree (internal/expand/tree.go:165-188),

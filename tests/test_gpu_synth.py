@@ -153,6 +153,20 @@ def test_powerlaw_expand_matches_oracle(powerlaw):
     _expand_matches_oracle(*powerlaw)
 
 
+def test_powerlaw_proto_all_device_equals_host(powerlaw):
+    """keto_tree_proto_all_device (encoded on the GPU) gives the host encoder's bytes and offsets."""
+    g, snap = powerlaw
+    rng = np.random.default_rng(19)
+    n = 5000
+    rows = rng.integers(0, g.n_rows, size=n).astype(np.uint32) | np.uint32(0x80000000)
+    depths = rng.integers(-1, 7, size=n).astype(np.int32)
+    for gmd in (5, 2):
+        st_h, offs_h, blob_h, _, _ = snap.expand_batch_ids_proto(rows, depths, gmd)
+        st_d, offs_d, blob_d, _, _ = snap.expand_batch_ids_proto(rows, depths, gmd, device=True)
+        assert (st_h == st_d).all() and (offs_h == offs_d).all()
+        assert len(blob_h) > 0 and blob_h == blob_d
+
+
 def test_powerlaw_proto_all_equals_per_tree(powerlaw):
     """keto_tree_proto_all (every tree of an arena encoded on host threads into one buffer) gives
     byte for byte the per-tree keto_tree_proto encodings, at the offsets it reports; nil trees

@@ -214,6 +214,13 @@ def config5(a, g=None):
             best, kern = dt, sum(ms)
     # every tree as a SubjectTree proto (keto_tree_proto_all, host threads)
     _st, poffs, blob, _te, t_proto = snap.expand_batch_ids_proto(roots, depths, 5)
+    # the same on the GPU (keto_tree_proto_all_device: strings resident on the device), best of 3,
+    # byte-compared with the host encoder's buffer
+    t_dev, dev_equal = None, None
+    for _ in range(3):
+        _sd, doffs, dblob, _td, t = snap.expand_batch_ids_proto(roots, depths, 5, device=True)
+        dev_equal = dblob == blob and bool((doffs == poffs).all())
+        t_dev = t if t_dev is None else min(t_dev, t)
     # node-by-node comparison of a sample of trees with the oracle (pre-order, child order included)
     from tests.test_gpu_synth import _oracle_expand_nodes
     k = a.expand_sample
@@ -257,6 +264,10 @@ def config5(a, g=None):
             "proto": {"trees_per_s": round(n / t_proto, 1), "bytes": len(blob), "encode_ms": round(t_proto * 1e3, 3),
                       "MB_per_s": round(len(blob) / t_proto / 1e6, 1),
                       "what": "keto_tree_proto_all: every tree of the arena as acl.SubjectTree protobuf, 16 host threads"},
+            "proto_device": {"trees_per_s": round(n / t_dev, 1), "encode_ms": round(t_dev * 1e3, 3),
+                             "MB_per_s": round(len(blob) / t_dev / 1e6, 1), "bytes_equal_host": dev_equal,
+                             "what": "keto_tree_proto_all_device: the same bytes encoded on the GPU (node upload, "
+                                     "sizes, scan, write, D2H into pageable numpy memory), one call with the buffer"},
             "parity": {"sample_trees": k, "sample_nodes": n_nodes, "mismatched_trees": bad}}
 
 
