@@ -9,7 +9,10 @@
 // 4 leaf] [subject tag 0x12 + varint(subject size)] [subject] -- so
 //   1. per node (parallel): the subject's encoded size;
 //   2. per tree (one lane, reverse pre-order with a stack kept in the tree's own slice of a
-//      scratch array): every subtree's size;
+//      scratch array): every union node's subtree size.  Leaves (most nodes: a group's members)
+//      are sized in parallel; a run of consecutive leaves is one step and one stack entry of the
+//      serial pass, its children-field bytes a difference of prefix sums -- so a hub tree costs
+//      its union nodes and leaf runs, not its leaves;
 //   3. per node: its header length; one exclusive scan over all nodes gives every node's byte
 //      offset, the trees' offsets included;
 //   4. per node (parallel): write the header and the subject's strings.
@@ -143,31 +146,69 @@ __device__ inline uint64_t subject_len(const Sub& s) {
     return flen(in);
 }
 
+// per node: the subject's size; a leaf's subtree size and its children-field bytes (leafw); the
+// node's own position if it is a union node, else -1 (max-scanned into "last union at or before")
 __global__ void __launch_bounds__(256) proto_slen(const keto_tree_node* __restrict__ nd, uint64_t n, Tables T,
-                                                  uint64_t* __restrict__ slen) {
+                                                  uint64_t* __restrict__ slen, uint64_t* __restrict__ size,
+                                                  uint64_t* __restrict__ leafw, int64_t* __restrict__ uni) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
-    slen[k] = subject_len(subject_of(T, nd[k].subject));
+    const uint64_t l = subject_len(subject_of(T, nd[k].subject));
+    slen[k] = l;
+    const bool leaf = (nd[k].info & 0x80000000u) != 0;
+    const uint64_t z = 2 + flen(l);
+    size[k] = z;                                          // final for leaves; unions: proto_sizes
+    leafw[k] = leaf ? flen(z) : 0;
+    uni[k] = leaf ? -1 : (int64_t)k;
 }
 
-// one lane per tree: subtree sizes in reverse pre-order; the stack of finished children's sizes
-// lives in the tree's own slice of `st`
+// one lane per tree: union nodes' subtree sizes in reverse pre-order.  Stack entries (2 words in
+// the tree's slice of `st`): a finished union child {UNION, size}, or a run of leaf children
+// {first, end} whose children-field bytes are lp[end] - lp[first] (lp = exclusive prefix of leafw);
+// last_union[j] = the last union node at or before j (runs end there)
+constexpr uint64_t ST_UNION = ~0ull;
 __global__ void __launch_bounds__(256) proto_sizes(const keto_tree_node* __restrict__ nd,
                                                    const uint64_t* __restrict__ toff, uint32_t n_trees,
-                                                   const uint64_t* __restrict__ slen, uint64_t* __restrict__ size,
-                                                   uint64_t* __restrict__ st) {
+                                                   const uint64_t* __restrict__ lp,
+                                                   const int64_t* __restrict__ last_union,
+                                                   uint64_t* __restrict__ size, uint64_t* __restrict__ st) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_trees) return;
     const uint64_t b = toff[t], e = toff[t + 1];
-    uint64_t* const stack = st + b;
+    uint64_t* const stack = st + 2 * b;
     uint64_t sp = 0;
-    for (uint64_t k = e; k-- > b;) {
-        const bool leaf = (nd[k].info & 0x80000000u) != 0;
-        const uint32_t nc = leaf ? 0u : nd[k].info & 0x7FFFFFFFu;
-        uint64_t z = 2 + flen(slen[k]);
-        for (uint32_t c = 0; c < nc && sp > 0; ++c) z += flen(stack[--sp]);
+    uint64_t k = e;
+    while (k > b) {
+        --k;
+        if (nd[k].info & 0x80000000u) {                   // the run of leaves ending at k
+            const int64_t u = last_union[k];
+            const uint64_t first = (u < 0 || (uint64_t)u < b) ? b : (uint64_t)u + 1;
+            stack[2 * sp] = first;
+            stack[2 * sp + 1] = k + 1;
+            ++sp;
+            k = first;
+            continue;
+        }
+        uint32_t need = nd[k].info & 0x7FFFFFFFu;
+        uint64_t z = size[k];                             // 2 + the subject field
+        while (need > 0 && sp > 0) {
+            uint64_t* top = stack + 2 * (sp - 1);
+            if (top[0] == ST_UNION) {
+                z += flen(top[1]);
+                --need;
+                --sp;
+                continue;
+            }
+            const uint64_t m = top[1] - top[0], take = m < need ? m : need;   // the first `take` leaves
+            z += lp[top[0] + take] - lp[top[0]];
+            need -= (uint32_t)take;
+            top[0] += take;
+            if (top[0] == top[1]) --sp;
+        }
         size[k] = z;
-        stack[sp++] = z;
+        stack[2 * sp] = ST_UNION;
+        stack[2 * sp + 1] = z;
+        ++sp;
     }
 }
 
@@ -393,7 +434,12 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     lap("upload");
     uint64_t* d_slen = b_slen.get<uint64_t>(n_nodes);
     uint64_t* d_size = b_size.get<uint64_t>(n_nodes);
-    uint64_t* d_st = b_st.get<uint64_t>(n_nodes);
+    uint64_t* d_st = b_st.get<uint64_t>(2 * n_nodes);
+    PBuf b_lw, b_lp, b_uni, b_lu;
+    uint64_t* d_lw = b_lw.get<uint64_t>(n_nodes + 1);
+    uint64_t* d_lp = b_lp.get<uint64_t>(n_nodes + 1);
+    int64_t* d_uni = b_uni.get<int64_t>(n_nodes);
+    int64_t* d_lu = b_lu.get<int64_t>(n_nodes);
     uint8_t* d_root = b_root.get<uint8_t>(n_nodes);
     uint64_t* d_hdr = b_hdr.get<uint64_t>(n_nodes + 1);
     uint64_t* d_pos = b_pos.get<uint64_t>(n_nodes + 1);
@@ -402,10 +448,18 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     lap("alloc");
     HIP_OK(hipMemsetAsync(d_root, 0, std::max<uint64_t>(1, n_nodes), st));
     HIP_OK(hipMemsetAsync(d_hdr + n_nodes, 0, 8, st));
+    HIP_OK(hipMemsetAsync(d_lw + n_nodes, 0, 8, st));
+    size_t tmp_bytes = 0, tb2 = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_lw, d_lp, n_nodes + 1, st));
+    HIP_OK(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, d_uni, d_lu, hipcub::Max(), std::max<uint64_t>(1, n_nodes), st));
+    tmp_bytes = std::max(tmp_bytes, tb2);
     if (n_nodes) {
-        hipLaunchKernelGGL(proto_slen, g(n_nodes), dim3(256), 0, st, d_nodes, n_nodes, T, d_slen);
+        hipLaunchKernelGGL(proto_slen, g(n_nodes), dim3(256), 0, st, d_nodes, n_nodes, T, d_slen, d_size, d_lw, d_uni);
         lap("slen");
-        hipLaunchKernelGGL(proto_sizes, g(n_trees), dim3(256), 0, st, d_nodes, d_toff, n_trees, d_slen, d_size, d_st);
+        void* d_t0 = b_tmp.get<uint8_t>(tmp_bytes);
+        HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_t0, tmp_bytes, d_lw, d_lp, n_nodes + 1, st));
+        HIP_OK(hipcub::DeviceScan::InclusiveScan(d_t0, tb2, d_uni, d_lu, hipcub::Max(), n_nodes, st));
+        hipLaunchKernelGGL(proto_sizes, g(n_trees), dim3(256), 0, st, d_nodes, d_toff, n_trees, d_lp, d_lu, d_size, d_st);
         lap("sizes");
         hipLaunchKernelGGL(proto_roots, g(n_trees), dim3(256), 0, st, d_toff, n_trees, d_root);
         hipLaunchKernelGGL(proto_hdr, g(n_nodes), dim3(256), 0, st, d_slen, d_size, d_root, n_nodes, d_hdr);
@@ -413,10 +467,11 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     }
     lap("hdr");
     // exclusive scan over n_nodes + 1 entries (the last is 0): pos[n_nodes] = total
-    size_t tmp_bytes = 0;
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_hdr, d_pos, n_nodes + 1, st));
-    void* d_tmp = b_tmp.get<uint8_t>(tmp_bytes);
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_hdr, d_pos, n_nodes + 1, st));
+    size_t tb3 = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, d_hdr, d_pos, n_nodes + 1, st));
+    PBuf b_tmp3;
+    void* d_tmp = b_tmp3.get<uint8_t>(tb3);
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb3, d_hdr, d_pos, n_nodes + 1, st));
     uint64_t total = 0;
     HIP_OK(hipMemcpyAsync(&total, d_pos + n_nodes, 8, hipMemcpyDeviceToHost, st));
     hipLaunchKernelGGL(proto_tree_offsets, g(n_trees + 1ull), dim3(256), 0, st, d_toff, n_trees, d_pos, total, n_nodes,
