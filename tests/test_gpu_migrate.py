@@ -215,3 +215,18 @@ def test_random_graphs_match_oracle(seed):
         for k, i in enumerate(sel):
             t, d, _ = grp[i]
             assert bool(got[k]) == CheckEngine(store, gmd).subject_is_allowed(t, d), (seed, t, d, gmd)
+
+
+def test_tiny_record_pool_reruns_exact(monkeypatch):
+    """A record pool far too small for a round (KETO_MIG_POOL_UNITS): the records that do not fit
+    are re-run from their input records once the pool has grown, and every decision stays exact."""
+    from tools import synth
+    monkeypatch.setenv("KETO_MIG_POOL_UNITS", "64")
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 1024), threads=16)
+    full = g.snapshot(device=0)
+    parts = _parts_from_csr(g, 3)
+    q = g.queries(30000, seed=12, depth=5)
+    want = full.check_batch_ids(full.with_handles(q), 5)
+    got, rounds = _mig_decide(parts, q, 5)
+    assert rounds >= 2
+    assert (got == want).all(), f"{int((got != want).sum())} mismatches"
