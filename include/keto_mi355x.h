@@ -417,7 +417,9 @@ int64_t keto_tree_proto_all(const keto_snapshot* s, const keto_tree_arena* a, ui
                             uint64_t* offsets);
 /* keto_tree_proto_all encoded on the GPU from the arena's nodes and the snapshot's strings (uploaded
  * to the snapshot's device on first use): the same bytes and offsets.  offsets
- * is always written; buf only when cap >= the returned total (call with buf = NULL to size it). */
+ * is always written; buf only when cap >= the returned total (call with buf = NULL to size it).
+ * The call's device buffers stay with the snapshot for the next call (freed with its device
+ * state); a pinned (hipHostMalloc'd) buf takes one DMA, a pageable one two pinned bounce chunks. */
 int64_t keto_tree_proto_all_device(keto_snapshot* s, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
                                    uint64_t* offsets);
 

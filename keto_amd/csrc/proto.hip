@@ -26,6 +26,7 @@
 #include <cstring>
 #include <vector>
 
+#include "parallel.hpp"
 #include "snapshot.hpp"
 
 namespace keto {
@@ -49,16 +50,29 @@ T* palloc(uint64_t n) {
     if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
     return (T*)p;
 }
-struct PBuf {                     // a device buffer freed at scope exit
+struct PBuf {                     // a grow-only device buffer, freed with its owner
     void* p = nullptr;
+    uint64_t cap = 0;
+    PBuf() = default;
+    PBuf(const PBuf&) = delete;
+    PBuf& operator=(const PBuf&) = delete;
     template <class T>
     T* get(uint64_t n) {
-        p = palloc<uint8_t>(n * sizeof(T));
+        const uint64_t want = std::max<uint64_t>(1, n * sizeof(T));
+        if (want > cap) {
+            release();
+            const uint64_t c = std::max<uint64_t>(want, cap + cap / 4);   // some headroom for the next call
+            p = palloc<uint8_t>(c);
+            cap = c;
+        }
         return (T*)p;
     }
-    ~PBuf() {
+    void release() {
         if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
     }
+    ~PBuf() { release(); }
 };
 
 // the strings a subject can name: snapshot strings, namespace names, the arena's extra strings
@@ -286,14 +300,14 @@ __global__ void __launch_bounds__(256) proto_tree_offsets(const uint64_t* __rest
     out[t] = toff[t] < n_nodes ? pos[toff[t]] : total;
 }
 
-// a string table on the device from host strings
+// a string table on the device from host strings (its buffers are reused by the next upload)
 struct DevStrs {
+    PBuf b_bytes, b_off;
     uint8_t* bytes = nullptr;
     uint64_t* off = nullptr;
     uint32_t n = 0;
     template <class Get>
     void upload(uint32_t count, Get get) {
-        release();
         std::vector<uint64_t> o(count + 1, 0);
         for (uint32_t i = 0; i < count; ++i) o[i + 1] = o[i] + get(i).size();
         std::vector<uint8_t> b(std::max<uint64_t>(1, o[count]));
@@ -301,20 +315,26 @@ struct DevStrs {
             const std::string_view s = get(i);
             if (!s.empty()) std::memcpy(b.data() + o[i], s.data(), s.size());
         }
-        bytes = palloc<uint8_t>(b.size());
-        off = palloc<uint64_t>(o.size());
+        bytes = b_bytes.get<uint8_t>(b.size());
+        off = b_off.get<uint64_t>(o.size());
         HIP_OK(hipMemcpy(bytes, b.data(), b.size(), hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(off, o.data(), o.size() * 8, hipMemcpyHostToDevice));
         n = count;
     }
     void release() {
-        if (bytes) (void)hipFree(bytes);
-        if (off) (void)hipFree(off);
+        b_bytes.release();
+        b_off.release();
         bytes = nullptr;
         off = nullptr;
         n = 0;
     }
     StrTab view() const { return StrTab{bytes, off, n}; }
+};
+
+// device_tree_proto's per-call buffers, kept across calls (one call at a time: the snapshot lock)
+struct ProtoWork {
+    DevStrs ex;
+    PBuf ons, oobj, orel, nodes, toff, slen, size, st, root, hdr, pos, out, to, tmp, tmp3, lw, lp, uni, lu;
 };
 
 }  // namespace
@@ -328,6 +348,11 @@ struct ProtoState {
     uint32_t* row_obj = nullptr;
     uint32_t* row_rel = nullptr;
     uint32_t n_rows = 0;
+    // two pinned bounce chunks for the output's D2H (d2h_staged)
+    uint8_t* pin[2] = {nullptr, nullptr};
+    uint64_t pin_bytes = 0;
+    ProtoWork work;
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
     void release_rows() {
         if (row_ns) (void)hipFree(row_ns);
         if (row_obj) (void)hipFree(row_obj);
@@ -340,6 +365,10 @@ struct ProtoState {
         strs.release();
         ns.release();
         release_rows();
+        for (int i = 0; i < 2; ++i) {
+            if (pin[i]) (void)hipHostFree(pin[i]);
+            if (pin_ev[i]) (void)hipEventDestroy(pin_ev[i]);
+        }
     }
 };
 
@@ -382,6 +411,52 @@ ProtoState& proto_state(Snapshot& S, int device) {
 }
 }  // namespace
 
+// D2H of the encoded bytes into the caller's buffer.  A pinned buffer takes one DMA.  A pageable
+// one (the usual case: a fresh numpy / std::vector buffer) goes through two pinned bounce chunks:
+// the DMA of chunk i + 1 overlaps the host threads' copy of chunk i out of its bounce buffer, which
+// also takes the first-touch page faults of the caller's buffer in parallel (a plain pageable
+// hipMemcpy ran at 16.8 GB/s on config #5's 36 MB).
+// KETO_PROTO_PIN_CHUNK (bytes, tests): a smaller chunk, so small outputs take the staged path.
+static void d2h_staged(ProtoState& P, uint8_t* buf, const uint8_t* d_src, uint64_t total, hipStream_t st) {
+    uint64_t PIN_CHUNK = 8ull << 20;
+    if (const char* e = getenv("KETO_PROTO_PIN_CHUNK")) PIN_CHUNK = std::max(1ll, atoll(e));
+    hipPointerAttribute_t at{};
+    const bool pinned = hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError();                       // pageable pointers report an error here
+    if (pinned || total <= std::min<uint64_t>(1ull << 20, PIN_CHUNK)) {
+        HIP_OK(hipMemcpyAsync(buf, d_src, total, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        return;
+    }
+    if (P.pin_bytes != PIN_CHUNK) {
+        for (int i = 0; i < 2; ++i) {
+            if (P.pin[i]) HIP_OK(hipHostFree(P.pin[i]));
+            P.pin[i] = nullptr;
+        }
+        P.pin_bytes = PIN_CHUNK;
+    }
+    for (int i = 0; i < 2; ++i) {
+        if (!P.pin[i]) HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&P.pin[i]), PIN_CHUNK, hipHostMallocDefault));
+        if (!P.pin_ev[i]) HIP_OK(hipEventCreateWithFlags(&P.pin_ev[i], hipEventDisableTiming));
+    }
+    const uint64_t n_ch = (total + PIN_CHUNK - 1) / PIN_CHUNK;
+    auto issue = [&](uint64_t c) {
+        const uint64_t off = c * PIN_CHUNK, len = std::min(PIN_CHUNK, total - off);
+        HIP_OK(hipMemcpyAsync(P.pin[c & 1], d_src + off, len, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipEventRecord(P.pin_ev[c & 1], st));
+    };
+    issue(0);
+    if (n_ch > 1) issue(1);
+    const unsigned th = std::min(8u, build_threads());
+    for (uint64_t c = 0; c < n_ch; ++c) {
+        HIP_OK(hipEventSynchronize(P.pin_ev[c & 1]));
+        const uint64_t off = c * PIN_CHUNK, len = std::min(PIN_CHUNK, total - off);
+        const uint8_t* src = P.pin[c & 1];
+        par_chunks(len, th, 1ull << 20, [&](uint64_t b, uint64_t e, unsigned) { memcpy(buf + off + b, src + b, e - b); });
+        if (c + 2 < n_ch) issue(c + 2);
+    }
+}
+
 uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_nodes, const uint64_t* tree_off,
                            uint32_t n_trees, uint32_t ov_base, const std::vector<RowKey>& ov_keys, uint32_t extra_base,
                            const std::vector<std::string>& extra, uint8_t* buf, uint64_t cap, uint64_t* offsets) {
@@ -401,7 +476,8 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     ProtoState& P = proto_state(S, dv.device);
     const hipStream_t st = 0;
     // the arena's overlay rows and extra strings
-    DevStrs ex;
+    ProtoWork& W = P.work;
+    DevStrs& ex = W.ex;
     ex.upload((uint32_t)extra.size(), [&](uint32_t i) { return std::string_view(extra[i]); });
     const uint32_t n_ov = (uint32_t)ov_keys.size();
     std::vector<int32_t> ons(n_ov);
@@ -416,10 +492,9 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
         oobj[i] = ov_keys[i].obj;
         orel[i] = ov_keys[i].rel;
     }
-    PBuf b_ons, b_oobj, b_orel, b_nodes, b_toff, b_slen, b_size, b_st, b_root, b_hdr, b_pos, b_out, b_to, b_tmp;
-    int32_t* d_ons = b_ons.get<int32_t>(n_ov);
-    uint32_t* d_oobj = b_oobj.get<uint32_t>(n_ov);
-    uint32_t* d_orel = b_orel.get<uint32_t>(n_ov);
+    int32_t* d_ons = W.ons.get<int32_t>(n_ov);
+    uint32_t* d_oobj = W.oobj.get<uint32_t>(n_ov);
+    uint32_t* d_orel = W.orel.get<uint32_t>(n_ov);
     if (n_ov) {
         HIP_OK(hipMemcpy(d_ons, ons.data(), n_ov * 4, hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(d_oobj, oobj.data(), n_ov * 4, hipMemcpyHostToDevice));
@@ -427,23 +502,22 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     }
     Tables T{P.strs.view(), P.ns.view(), ex.view(), P.row_ns, P.row_obj, P.row_rel, P.n_rows, d_ons, d_oobj, d_orel,
              ov_base, n_ov, extra_base};
-    keto_tree_node* d_nodes = b_nodes.get<keto_tree_node>(n_nodes);
-    uint64_t* d_toff = b_toff.get<uint64_t>(n_trees + 1ull);
+    keto_tree_node* d_nodes = W.nodes.get<keto_tree_node>(n_nodes);
+    uint64_t* d_toff = W.toff.get<uint64_t>(n_trees + 1ull);
     HIP_OK(hipMemcpy(d_nodes, nodes, n_nodes * sizeof(keto_tree_node), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_toff, tree_off, (n_trees + 1ull) * 8, hipMemcpyHostToDevice));
     lap("upload");
-    uint64_t* d_slen = b_slen.get<uint64_t>(n_nodes);
-    uint64_t* d_size = b_size.get<uint64_t>(n_nodes);
-    uint64_t* d_st = b_st.get<uint64_t>(2 * n_nodes);
-    PBuf b_lw, b_lp, b_uni, b_lu;
-    uint64_t* d_lw = b_lw.get<uint64_t>(n_nodes + 1);
-    uint64_t* d_lp = b_lp.get<uint64_t>(n_nodes + 1);
-    int64_t* d_uni = b_uni.get<int64_t>(n_nodes);
-    int64_t* d_lu = b_lu.get<int64_t>(n_nodes);
-    uint8_t* d_root = b_root.get<uint8_t>(n_nodes);
-    uint64_t* d_hdr = b_hdr.get<uint64_t>(n_nodes + 1);
-    uint64_t* d_pos = b_pos.get<uint64_t>(n_nodes + 1);
-    uint64_t* d_to = b_to.get<uint64_t>(n_trees + 1ull);
+    uint64_t* d_slen = W.slen.get<uint64_t>(n_nodes);
+    uint64_t* d_size = W.size.get<uint64_t>(n_nodes);
+    uint64_t* d_st = W.st.get<uint64_t>(2 * n_nodes);
+    uint64_t* d_lw = W.lw.get<uint64_t>(n_nodes + 1);
+    uint64_t* d_lp = W.lp.get<uint64_t>(n_nodes + 1);
+    int64_t* d_uni = W.uni.get<int64_t>(n_nodes);
+    int64_t* d_lu = W.lu.get<int64_t>(n_nodes);
+    uint8_t* d_root = W.root.get<uint8_t>(n_nodes);
+    uint64_t* d_hdr = W.hdr.get<uint64_t>(n_nodes + 1);
+    uint64_t* d_pos = W.pos.get<uint64_t>(n_nodes + 1);
+    uint64_t* d_to = W.to.get<uint64_t>(n_trees + 1ull);
     const auto g = [](uint64_t n) { return dim3((unsigned)std::max<uint64_t>(1, (n + 255) / 256)); };
     lap("alloc");
     HIP_OK(hipMemsetAsync(d_root, 0, std::max<uint64_t>(1, n_nodes), st));
@@ -456,7 +530,7 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     if (n_nodes) {
         hipLaunchKernelGGL(proto_slen, g(n_nodes), dim3(256), 0, st, d_nodes, n_nodes, T, d_slen, d_size, d_lw, d_uni);
         lap("slen");
-        void* d_t0 = b_tmp.get<uint8_t>(tmp_bytes);
+        void* d_t0 = W.tmp.get<uint8_t>(tmp_bytes);
         HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_t0, tmp_bytes, d_lw, d_lp, n_nodes + 1, st));
         HIP_OK(hipcub::DeviceScan::InclusiveScan(d_t0, tb2, d_uni, d_lu, hipcub::Max(), n_nodes, st));
         hipLaunchKernelGGL(proto_sizes, g(n_trees), dim3(256), 0, st, d_nodes, d_toff, n_trees, d_lp, d_lu, d_size, d_st);
@@ -469,8 +543,7 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
     // exclusive scan over n_nodes + 1 entries (the last is 0): pos[n_nodes] = total
     size_t tb3 = 0;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, d_hdr, d_pos, n_nodes + 1, st));
-    PBuf b_tmp3;
-    void* d_tmp = b_tmp3.get<uint8_t>(tb3);
+    void* d_tmp = W.tmp3.get<uint8_t>(tb3);
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb3, d_hdr, d_pos, n_nodes + 1, st));
     uint64_t total = 0;
     HIP_OK(hipMemcpyAsync(&total, d_pos + n_nodes, 8, hipMemcpyDeviceToHost, st));
@@ -484,13 +557,12 @@ uint64_t device_tree_proto(Snapshot& S, const keto_tree_node* nodes, uint64_t n_
         if (tree_off[t] >= n_nodes) offsets[t] = total;
     lap("scan");
     if (!buf || cap < total || total == 0) return total;
-    uint8_t* d_out = b_out.get<uint8_t>(total);
+    uint8_t* d_out = W.out.get<uint8_t>(total);
     hipLaunchKernelGGL(proto_write, g(n_nodes), dim3(256), 0, st, d_nodes, n_nodes, T, d_slen, d_size, d_root, d_pos,
                        d_out);
     HIP_OK(hipGetLastError());
     lap("write");
-    HIP_OK(hipMemcpyAsync(buf, d_out, total, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    d2h_staged(P, buf, d_out, total, st);
     lap("d2h");
     return total;
 }

@@ -153,8 +153,12 @@ def test_powerlaw_expand_matches_oracle(powerlaw):
     _expand_matches_oracle(*powerlaw)
 
 
-def test_powerlaw_proto_all_device_equals_host(powerlaw):
-    """keto_tree_proto_all_device (encoded on the GPU) gives the host encoder's bytes and offsets."""
+@pytest.mark.parametrize("pin_chunk", [None, 4096, 1 << 16])
+def test_powerlaw_proto_all_device_equals_host(powerlaw, monkeypatch, pin_chunk):
+    """keto_tree_proto_all_device (encoded on the GPU) gives the host encoder's bytes and offsets;
+    pin_chunk: the D2H through many small pinned bounce chunks (KETO_PROTO_PIN_CHUNK)."""
+    if pin_chunk:
+        monkeypatch.setenv("KETO_PROTO_PIN_CHUNK", str(pin_chunk))
     g, snap = powerlaw
     rng = np.random.default_rng(19)
     n = 5000

@@ -267,7 +267,8 @@ def config5(a, g=None):
             "proto_device": {"trees_per_s": round(n / t_dev, 1), "encode_ms": round(t_dev * 1e3, 3),
                              "MB_per_s": round(len(blob) / t_dev / 1e6, 1), "bytes_equal_host": dev_equal,
                              "what": "keto_tree_proto_all_device: the same bytes encoded on the GPU (node upload, "
-                                     "sizes, scan, write, D2H into pageable numpy memory), one call with the buffer"},
+                                     "sizes, scan, write, D2H into pageable numpy memory via pinned bounce chunks; device "
+                                     "buffers kept across calls), one call with the buffer"},
             "parity": {"sample_trees": k, "sample_nodes": n_nodes, "mismatched_trees": bad}}
 
 
