@@ -404,6 +404,14 @@ const keto_tree_node* keto_tree_nodes(const keto_tree_arena* a, uint32_t i, uint
 /* JSON of tree i exactly as Tree.MarshalJSON (internal/expand/tree.go:156-163); "null" for nil.
  * Writes at most cap bytes (NUL-terminated) and returns the full length, or a negative code. */
 int64_t keto_tree_json(const keto_snapshot* s, const keto_tree_arena* a, uint32_t i, char* buf, uint64_t cap);
+/* Every tree of the arena as JSON on host threads (the REST Expand response body of each root,
+ * internal/expand/handler.go:77-91, h.d.Writer().Write of the
+ * BuildTree result, via Tree.MarshalJSON): offsets[n+1], tree i = buf[offsets[i],
+ * offsets[i+1]) -- keto_tree_json's text for a tree, "null" for a nil tree, empty for the roots
+ * keto_tree_json reports as errors (KETO_EXPAND_NOT_FOUND / KETO_EXPAND_UNDECIDED).  buf is written
+ * only if cap >= the total, which is returned (call with buf = NULL to size it). */
+int64_t keto_tree_json_all(const keto_snapshot* s, const keto_tree_arena* a, char* buf, uint64_t cap,
+                           uint64_t* offsets);
 
 /* Tree i as acl.SubjectTree protobuf bytes, exactly as proto.Marshal(Tree.ToProto())
  * (internal/expand/tree.go:165-188; proto/ory/keto/acl/v1alpha1/expand_service.proto): the

@@ -36,7 +36,7 @@ EXPORTS = [
     "keto_check_steps_device", "keto_snapshot_part_stats", "keto_snapshot_apply", "keto_snapshot_version",
     "keto_snapshot_upload_part_mode", "keto_snapshot_part_stats_mode", "keto_part_stubs", "keto_part_filters",
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
-    "keto_tree_proto_all_device",
+    "keto_tree_proto_all_device", "keto_tree_json_all",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -155,6 +155,7 @@ def load():
     lib.keto_tree_proto.restype = C.c_int64
     lib.keto_tree_proto_all.restype = C.c_int64
     lib.keto_tree_proto_all_device.restype = C.c_int64
+    lib.keto_tree_json_all.restype = C.c_int64
     lib.keto_subject_string.restype = C.c_int64
     lib.keto_route_work_bytes.restype = C.c_uint64
     lib.keto_snapshot_version.restype = C.c_uint64
@@ -596,10 +597,23 @@ class Snapshot:
         assert got == total
         return offs, blob[:total].tobytes(), dt
 
-    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False, proto_all=None):
+    def _json_all(self, a, n):
+        """Every tree's JSON text from keto_tree_json_all ("null" for nil trees, "" for errors)."""
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        total = self.lib.keto_tree_json_all(self.h, a, None, C.c_uint64(0), offs.ctypes.data_as(C.c_void_p))
+        _check(min(0, total))
+        blob = C.create_string_buffer(max(1, total))
+        got = self.lib.keto_tree_json_all(self.h, a, blob, C.c_uint64(total), offs.ctypes.data_as(C.c_void_p))
+        _check(min(0, got))
+        raw = blob.raw[:total]
+        return [raw[int(offs[i]):int(offs[i + 1])].decode() for i in range(n)]
+
+    def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False, proto_all=None,
+                     json_all=False):
         """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes][, proto]);
         proto_all = "host" / "device": also every tree's bytes from keto_tree_proto_all[_device]
-        (returned as (list, per-tree bytes list))."""
+        (returned as (list, per-tree bytes list)); json_all: also every tree's JSON text from
+        keto_tree_json_all (returned as (list, per-tree text list))."""
         keep = _Keep()
         n = len(reqs)
         arr = (KExpandReq * max(1, n))()
@@ -636,6 +650,8 @@ class Snapshot:
             if proto_all:
                 offs, blob, _ = self._proto_all(a, n, device=proto_all == "device")
                 return out, [blob[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+            if json_all:
+                return out, self._json_all(a, n)
         finally:
             self.lib.keto_tree_arena_free(a)
         return out

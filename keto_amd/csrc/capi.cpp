@@ -135,36 +135,6 @@ SubjectFields fields_of(const Snapshot& S, const keto_tree_arena* a, uint32_t re
     return f;
 }
 
-void tree_json(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node* nd, uint64_t n, uint64_t& pos,
-               std::string& o) {
-    const keto_tree_node x = nd[pos++];
-    const bool leaf = (x.info & 0x80000000u) != 0;
-    const uint32_t nc = x.info & 0x7FFFFFFFu;
-    o += leaf ? "{\"type\":\"leaf\"" : "{\"type\":\"union\"";
-    if (!leaf && nc) {
-        o += ",\"children\":[";
-        for (uint32_t c = 0; c < nc && pos < n; ++c) {
-            if (c) o.push_back(',');
-            tree_json(S, a, nd, n, pos, o);
-        }
-        o.push_back(']');
-    }
-    SubjectFields f = fields_of(S, a, x.subject);
-    if (!f.set) {
-        o += ",\"subject_id\":";
-        json_escape(o, f.id);
-    } else {
-        o += ",\"subject_set\":{\"namespace\":";
-        json_escape(o, f.ns);
-        o += ",\"object\":";
-        json_escape(o, f.obj);
-        o += ",\"relation\":";
-        json_escape(o, f.rel);
-        o.push_back('}');
-    }
-    o.push_back('}');
-}
-
 // ---- acl.SubjectTree protobuf (proto/ory/keto/acl/v1alpha1/expand_service.proto, acl.proto), the
 // bytes proto.Marshal gives for Tree.ToProto() (internal/expand/tree.go:165-188): node_type = 1
 // (varint; UNION 1, LEAF 4), subject = 2 (Subject: oneof id = 1 | set = 2 {namespace 1, object 2,
@@ -202,6 +172,63 @@ SubjectViews views_of(const Snapshot& S, const keto_tree_arena* a, uint32_t ref)
     f.rel = str(k.rel);
     return f;
 }
+void subject_json(const Snapshot& S, const keto_tree_arena* a, uint32_t ref, std::string& o) {
+    const SubjectViews f = views_of(S, a, ref);
+    if (!f.set) {
+        o += ",\"subject_id\":";
+        json_escape(o, f.id);
+    } else {
+        o += ",\"subject_set\":{\"namespace\":";
+        json_escape(o, f.ns);
+        o += ",\"object\":";
+        json_escape(o, f.obj);
+        o += ",\"relation\":";
+        json_escape(o, f.rel);
+        o.push_back('}');
+    }
+    o.push_back('}');
+}
+
+// One tree's JSON (Tree.MarshalJSON, internal/expand/tree.go:85-163: type, children, then the
+// subject) from its pre-order nodes, without recursion: a tree is as deep as its max-depth (up to
+// 65535 levels).  `left` holds the children still to write of every open union; a union's subject
+// and closing brace follow its last child.  A truncated node list closes what is open.
+void tree_json(const Snapshot& S, const keto_tree_arena* a, const keto_tree_node* nd, uint64_t n, std::string& o) {
+    if (n == 0) return;
+    std::vector<uint32_t> left, subj;
+    uint64_t pos = 0;
+    for (;;) {
+        const keto_tree_node x = nd[pos++];
+        const bool leaf = (x.info & 0x80000000u) != 0;
+        const uint32_t nc = x.info & 0x7FFFFFFFu;
+        o += leaf ? "{\"type\":\"leaf\"" : "{\"type\":\"union\"";
+        if (!leaf && nc) {
+            o += ",\"children\":[";
+            if (pos < n) {                       // its first child is the next node
+                left.push_back(nc);
+                subj.push_back(x.subject);
+                continue;
+            }
+            o.push_back(']');
+        }
+        subject_json(S, a, x.subject, o);
+        // a node is complete: go on with its parent's next child, or close the parent
+        bool more = false;
+        while (!left.empty()) {
+            if (--left.back() > 0 && pos < n) {
+                o.push_back(',');
+                more = true;
+                break;
+            }
+            o.push_back(']');
+            subject_json(S, a, subj.back(), o);
+            left.pop_back();
+            subj.pop_back();
+        }
+        if (!more) return;
+    }
+}
+
 inline uint64_t field_len(uint64_t n) { return 1 + varint_len(n) + n; }
 // bytes of the Subject message: oneof id (present even when "") | set {namespace, object,
 // relation; empty strings omitted}
@@ -869,10 +896,42 @@ int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_
     if (a->r.status[i] != KETO_EXPAND_TREE) {
         o = "null";
     } else {
-        uint64_t b = a->r.offset[i], e = a->r.offset[i + 1], pos = 0;
-        tree_json(*h->s, a, a->r.nodes.data() + b, e - b, pos, o);
+        const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+        tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
     }
     return copy_out(o, buf, cap);
+}
+
+int64_t keto_tree_json_all(const keto_snapshot* h, const keto_tree_arena* a, char* buf, uint64_t cap,
+                           uint64_t* offsets) {
+    if (!h || !a || !offsets) return KETO_E_INVALID;
+    const uint32_t n = (uint32_t)a->r.status.size();
+    std::vector<std::string> enc(n);
+    const unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> ts;
+    std::atomic<uint32_t> next{0};
+    for (unsigned t = 0; t < th; ++t)
+        ts.emplace_back([&] {
+            for (;;) {
+                const uint32_t k = next.fetch_add(64);
+                if (k >= n) break;
+                for (uint32_t i = k; i < std::min(n, k + 64); ++i) {
+                    const int st = a->r.status[i];
+                    if (st == KETO_EXPAND_TREE) {
+                        const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+                        tree_json(*h->s, a, a->r.nodes.data() + b, e - b, enc[i]);
+                    } else if (st != KETO_EXPAND_NOT_FOUND && st != KETO_EXPAND_UNDECIDED) {
+                        enc[i] = "null";
+                    }
+                }
+            }
+        });
+    for (auto& x : ts) x.join();
+    offsets[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + enc[i].size();
+    if (buf && cap >= offsets[n])
+        for (uint32_t i = 0; i < n; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
+    return (int64_t)offsets[n];
 }
 
 int64_t keto_tree_proto(const keto_snapshot* h, const keto_tree_arena* a, uint32_t i, uint8_t* buf, uint64_t cap) {

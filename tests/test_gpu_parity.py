@@ -84,6 +84,53 @@ def test_random_expand_proto_device_equals_host(seed):
         assert host == dev, (seed, g)
 
 
+@pytest.mark.parametrize("seed", range(2200, 2240))
+def test_random_expand_json_all_equals_per_tree(seed):
+    """keto_tree_json_all (every tree's JSON on host threads) gives keto_tree_json's text for each
+    tree, "null" for nil trees and "" for error roots, on quirk-heavy random graphs."""
+    import json
+    from keto_amd.capi import EXPAND_NIL, EXPAND_TREE
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=seed % 3 == 0)
+    snap = _snapshot(ns, rows_from_tuples(ns, tuples, raw), ps)
+    exps = random_expands(seed, alph, k=24)
+    for g in sorted({e[2] for e in exps}):
+        grp = [(subj(s), d) for s, d, gg in exps if gg == g]
+        got, texts = snap.expand_batch(grp, g, json_all=True)
+        for (st, js), txt in zip(got, texts):
+            if st == EXPAND_TREE:
+                assert json.loads(txt) == js, (seed, g)
+            elif st == EXPAND_NIL:
+                assert txt == "null"
+            else:
+                assert txt == ""
+
+
+def test_deep_chain_tree_json():
+    """A 2,500-level tree (a chain of nested groups expanded with max-depth 3000): the JSON encoders
+    are iterative, so a tree as deep as the max-depth allows encodes without exhausting the host
+    stack; the text equals the chain's expected JSON."""
+    import sys
+    from keto_amd.capi import EXPAND_TREE
+    from oracle.oracle_sql import RelationTuple, SubjectID, SubjectSet
+    k = 2500
+    ns = [(1, "n")]
+    tuples = [RelationTuple("n", f"g{i}", "m", SubjectSet("n", f"g{i + 1}", "m")) for i in range(k - 1)]
+    tuples.append(RelationTuple("n", f"g{k - 1}", "m", SubjectID("user")))
+    snap = _snapshot(ns, rows_from_tuples(ns, tuples), 100)
+    want = '{"type":"leaf","subject_id":"user"}'
+    for i in reversed(range(k)):
+        want = ('{"type":"union","children":[' + want +
+                '],"subject_set":{"namespace":"n","object":"g%d","relation":"m"}}' % i)
+    old = sys.getrecursionlimit()
+    sys.setrecursionlimit(max(old, 4 * k + 1000))   # expand_batch parses the per-tree text
+    try:
+        got, texts = snap.expand_batch([(("set", "n", "g0", "m"), 3000)], 3000, json_all=True)
+    finally:
+        sys.setrecursionlimit(old)
+    assert got[0][0] == EXPAND_TREE
+    assert texts[0] == want
+
+
 @pytest.mark.parametrize("seed", range(2000, 2060))
 def test_random_expand_proto_matches_oracle(seed):
     """keto_tree_proto = proto.Marshal(Tree.ToProto()) of the oracle's tree (internal/expand/tree.go:165-188),

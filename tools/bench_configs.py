@@ -221,6 +221,25 @@ def config5(a, g=None):
         _sd, doffs, dblob, _td, t = snap.expand_batch_ids_proto(roots, depths, 5, device=True)
         dev_equal = dblob == blob and bool((doffs == poffs).all())
         t_dev = t if t_dev is None else min(t_dev, t)
+    # every tree as JSON (keto_tree_json_all, host threads: the REST Expand bodies), best of 3
+    t_json, json_bytes = None, 0
+    arena = C.c_void_p()
+    assert lib.keto_expand_batch_ids(snap.h, roots.ctypes.data_as(C.c_void_p), depths.ctypes.data_as(C.c_void_p),
+                                     C.c_uint32(n), C.c_int32(5), C.byref(arena)) == 0
+    try:
+        joffs = np.zeros(n + 1, dtype=np.uint64)
+        json_bytes = lib.keto_tree_json_all(snap.h, arena, None, C.c_uint64(0), joffs.ctypes.data_as(C.c_void_p))
+        assert json_bytes >= 0
+        for _ in range(3):
+            jbuf = np.zeros(max(1, json_bytes), dtype=np.uint8)
+            t0 = time.perf_counter()
+            got = lib.keto_tree_json_all(snap.h, arena, jbuf.ctypes.data_as(C.c_void_p), C.c_uint64(json_bytes),
+                                         joffs.ctypes.data_as(C.c_void_p))
+            t = time.perf_counter() - t0
+            assert got == json_bytes
+            t_json = t if t_json is None else min(t_json, t)
+    finally:
+        lib.keto_tree_arena_free(arena)
     # node-by-node comparison of a sample of trees with the oracle (pre-order, child order included)
     from tests.test_gpu_synth import _oracle_expand_nodes
     k = a.expand_sample
@@ -269,6 +288,9 @@ def config5(a, g=None):
                              "what": "keto_tree_proto_all_device: the same bytes encoded on the GPU (node upload, "
                                      "sizes, scan, write, D2H into pageable numpy memory via pinned bounce chunks; device "
                                      "buffers kept across calls), one call with the buffer"},
+            "json": {"trees_per_s": round(n / t_json, 1), "bytes": int(json_bytes), "encode_ms": round(t_json * 1e3, 3),
+                     "MB_per_s": round(json_bytes / t_json / 1e6, 1),
+                     "what": "keto_tree_json_all: every tree as Tree.MarshalJSON text, 16 host threads"},
             "parity": {"sample_trees": k, "sample_nodes": n_nodes, "mismatched_trees": bad}}
 
 
