@@ -209,6 +209,16 @@ int main(int argc, char** argv) {
                 js = (char*)malloc((size_t)jn + 1);
                 if (keto_tree_json(snap, ar, 0, js, (uint64_t)jn + 1) != jn) return 6;
             }
+            {   /* the batch form (what the Go shim calls): the same text, "" for an error root */
+                uint64_t offs[2];
+                const int64_t an = keto_tree_json_all(snap, ar, NULL, 0, offs);
+                if (an < 0) fail("keto_tree_json_all", (int)an);
+                char* all = (char*)malloc((size_t)an + 1);
+                if (keto_tree_json_all(snap, ar, all, (uint64_t)an, offs) != an) return 6;
+                if (offs[0] != 0 || offs[1] != (uint64_t)an) return 6;
+                if (js ? (an != jn || memcmp(all, js, (size_t)an) != 0) : an != 0) return 6;
+                free(all);
+            }
             const int64_t pn = keto_tree_proto(snap, ar, 0, NULL, 0);
             printf("expand\t%d\t%d\t%s\t", expands++, s, js ? js : "error");
             if (pn > 0) {

@@ -274,6 +274,18 @@ func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globa
 		return nil, nil, lastErr(rc)
 	}
 	defer C.keto_tree_arena_free(a)
+	// every tree's JSON in one buffer (keto_tree_json_all, host threads): size, then fill
+	offs := (*C.uint64_t)(m.alloc((n + 1) * 8))
+	jsonLen := C.keto_tree_json_all(s.h, a, nil, 0, offs)
+	if jsonLen < 0 {
+		return nil, nil, lastErr(C.int(jsonLen))
+	}
+	buf := (*C.char)(m.alloc(int(jsonLen) + 1))
+	if rc := C.keto_tree_json_all(s.h, a, buf, C.uint64_t(jsonLen), offs); rc != jsonLen {
+		return nil, nil, lastErr(C.int(rc))
+	}
+	text := C.GoBytes(unsafe.Pointer(buf), C.int(jsonLen))
+	off := unsafe.Slice(offs, n+1)
 	trees := make([]*expand.Tree, n)
 	errs := make([]error, n)
 	for i := 0; i < n; i++ {
@@ -287,14 +299,8 @@ func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globa
 			errs[i] = ErrUndecided
 			continue
 		}
-		ln := C.keto_tree_json(s.h, a, C.uint32_t(i), nil, 0)
-		if ln < 0 {
-			return nil, nil, lastErr(C.int(ln))
-		}
-		buf := (*C.char)(m.alloc(int(ln) + 1))
-		C.keto_tree_json(s.h, a, C.uint32_t(i), buf, C.uint64_t(ln+1))
 		t := &expand.Tree{}
-		if err := t.UnmarshalJSON(C.GoBytes(unsafe.Pointer(buf), C.int(ln))); err != nil {
+		if err := t.UnmarshalJSON(text[off[i]:off[i+1]]); err != nil {
 			return nil, nil, err
 		}
 		trees[i] = t
