@@ -1631,11 +1631,23 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
 }
 
 // ------------------------------------------------------------------ expand
+// A long run of a row's subject ids (all leaves) is not copied by the fill pass's lane, one node
+// per iteration while its wave waits, but queued and copied afterwards by copy_runs, a block per run
+// (coalesced).  Runs of at most RUN_INLINE ids are copied in place.
+constexpr uint32_t RUN_INLINE = 32;
+struct CopyRun {
+    const uint32_t* src;     // the ids
+    keto_tree_node* dst;     // their leaf nodes
+    uint64_t len;
+};
 struct ExpandOut {
     keto_tree_node* nodes;   // FILL only
     const uint64_t* offset;  // FILL only
     uint64_t* count;         // count pass: nodes per root
     uint8_t* status;
+    CopyRun* runs;           // FILL only: queued id runs (NULL = copy every run in place)
+    uint32_t* n_runs;
+    uint32_t runs_cap;
 };
 
 __device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint32_t subject, uint32_t info) {
@@ -1647,7 +1659,8 @@ __device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint3
 // a string id.  Set nodes are emitted with their row handle (the host maps handles to row ids).
 template <bool FILL, class Stack>
 __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
-                          uint32_t root_vid, int d, Visited& V, keto_tree_node* out, uint64_t& cnt, Stack& st) {
+                          uint32_t root_vid, int d, Visited& V, keto_tree_node* out, uint64_t& cnt, Stack& st,
+                          const ExpandOut& o) {
     if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
         emit(out, cnt, FILL, root, 0x80000000u);
         return EXP_TREE;
@@ -1695,7 +1708,14 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             // a normal row keeps its subject sets first: every edge left is a subject id, and each
             // is a leaf (:97-101) -- counted at once, copied in one pass
             if constexpr (FILL) {
-                for (uint32_t i = 0; i < cur.left; ++i) out[cnt + i] = keto_tree_node{a[cur.pos + i], 0x80000000u};
+                uint32_t at = NONE32;
+                if (cur.left > RUN_INLINE && o.runs) {
+                    at = atomicAdd(o.n_runs, 1u);
+                    if (at < o.runs_cap) o.runs[at] = CopyRun{a + cur.pos, out + cnt, cur.left};
+                    else at = NONE32;                       // queue full: copy it here
+                }
+                if (at == NONE32)
+                    for (uint32_t i = 0; i < cur.left; ++i) out[cnt + i] = keto_tree_node{a[cur.pos + i], 0x80000000u};
             }
             cnt += cur.left;
             cur.left = 0;
@@ -1758,7 +1778,7 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         if (d <= 0 || gmd < d) d = gmd;
         uint64_t cnt = 0;
         keto_tree_node* out = FILL ? o.nodes + o.offset[i] : nullptr;
-        int r = expand_one<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, st);
+        int r = expand_one<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, st, o);
         if (r == EXP_OVERFLOW) {
             uint32_t at = atomicAdd(ta.out_count, 1u);
             ta.out_list[at] = i;
@@ -1768,6 +1788,17 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         }
     }
     ta.slot_epoch[slot] = V.epoch;
+}
+
+// The queued id runs of a fill pass, a block per run (grid-stride over runs).  A run queued twice (a
+// root that overflowed a tier and was filled again on the next) is copied twice, to the same bytes.
+__global__ void __launch_bounds__(256) copy_runs(const CopyRun* __restrict__ runs, const uint32_t* __restrict__ n_runs,
+                                                 uint32_t cap) {
+    const uint32_t n = min(*n_runs, cap);
+    for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const CopyRun c = runs[r];
+        for (uint64_t i = threadIdx.x; i < c.len; i += blockDim.x) c.dst[i] = keto_tree_node{c.src[i], 0x80000000u};
+    }
 }
 
 // ------------------------------------------------------------------ host side
@@ -1818,6 +1849,9 @@ struct DeviceState {
     uint64_t ex_cap = 0;
     keto_tree_node* ex_nodes = nullptr;
     uint64_t ex_nodes_cap = 0;
+    CopyRun* ex_runs = nullptr;       // the fill pass's queued id runs | their count (last 8 B)
+    uint32_t ex_runs_cap = 0;
+    hipEvent_t ex_ev[2] = {};         // copy_runs timing (added to tier 0 of the batch timing)
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
     // host-buffer calls (device_check_host): a pipeline of chunks over two device slots, H2D on
@@ -2569,6 +2603,9 @@ void device_release(Snapshot& S) {
     if (D.rows_by_unit) (void)hipFree(D.rows_by_unit);
     if (D.ex_buf) (void)hipFree(D.ex_buf);
     if (D.ex_nodes) (void)hipFree(D.ex_nodes);
+    if (D.ex_runs) (void)hipFree(D.ex_runs);
+    for (hipEvent_t e : D.ex_ev)
+        if (e) (void)hipEventDestroy(e);
     if (D.xlate) (void)hipFree(D.xlate);
     for (int i = 0; i < 2; ++i) {
         if (D.slot_q[i]) (void)hipFree(D.slot_q[i]);
@@ -3418,6 +3455,16 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (n == 0) return;
     if (gmd > 65535) gmd = 65535;
     hipStream_t st = D.stream;
+    // KETO_EXPAND_TRACE=1: phase times on stderr (tooling)
+    const bool trace = getenv("KETO_EXPAND_TRACE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        (void)hipStreamSynchronize(st);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[expand] %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     OverlayBuf ov(S, ovh);
     uint64_t acc = 0;
     // workspace, reused across calls: requests | counts (n + 1) | offsets (n + 1) | statuses
@@ -3438,10 +3485,11 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         HIP_OK(hipMemcpyAsync(dq, hq.data(), n * sizeof(ExpandReq), hipMemcpyHostToDevice, st));
         HIP_OK(hipStreamSynchronize(st));
     }
+    lap("h2d");
     Plan p = make_plan(D, n, gmd);            // expand holds at most gmd frames
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
-    ExpandOut o{nullptr, nullptr, dcount, dstatus};
+    ExpandOut o{nullptr, nullptr, dcount, dstatus, nullptr, nullptr, 0};
     // (the batch timing sums both passes' tiers: keto_last_batch_timing after an expand)
     auto launch_pass = [&](bool fill, const ExpandOut& eo) {
         run_tiers(D, D.ews, n, p, st,
@@ -3470,6 +3518,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     // count pass, exclusive scan on the host, fill pass (same tier plan: a root overflows on the
     // same tiers both times, and a partial pre-order is a prefix of the full one)
     launch_pass(false, o);
+    lap("count");
     std::vector<uint64_t> cnt(n);
     HIP_OK(hipMemcpyAsync(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(out.status.data(), dstatus, n, hipMemcpyDeviceToHost, st));
@@ -3477,6 +3526,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     for (uint32_t i = 0; i < n; ++i) out.offset[i + 1] = out.offset[i] + cnt[i];
     const uint64_t total = out.offset[n];
     out.nodes.resize(total);
+    lap("scan");
     if (total == 0) return;
     if (D.ex_nodes_cap < total) {
         if (D.ex_nodes) (void)hipFree(D.ex_nodes);
@@ -3493,12 +3543,38 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                          hipMemcpyHostToDevice));
     }
     HIP_OK(hipMemcpyAsync(doff, out.offset.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus});
+    // id runs longer than RUN_INLINE hold more than RUN_INLINE nodes each: total / (RUN_INLINE + 1)
+    // bounds them (slack for roots filled again on a later tier; a full queue copies in place)
+    const uint32_t runs_cap = (uint32_t)std::min<uint64_t>(total / (RUN_INLINE + 1) + 4096, 1u << 30);
+    if (D.ex_runs_cap < runs_cap) {
+        if (D.ex_runs) (void)hipFree(D.ex_runs);
+        D.ex_runs = nullptr;
+        D.ex_runs_cap = 0;
+        D.ex_runs = reinterpret_cast<CopyRun*>(dmalloc<uint8_t>((uint64_t)runs_cap * sizeof(CopyRun) + 8, acc));
+        D.ex_runs_cap = runs_cap;
+    }
+    uint32_t* d_nruns = reinterpret_cast<uint32_t*>(D.ex_runs + D.ex_runs_cap);
+    HIP_OK(hipMemsetAsync(d_nruns, 0, sizeof(uint32_t), st));
+    launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_nruns, D.ex_runs_cap});
+    for (int e = 0; e < 2; ++e)
+        if (!D.ex_ev[e]) HIP_OK(hipEventCreate(&D.ex_ev[e]));
+    HIP_OK(hipEventRecord(D.ex_ev[0], st));
+    hipLaunchKernelGGL(copy_runs, dim3(std::min<uint32_t>(D.ex_runs_cap, 8192)), dim3(256), 0, st, D.ex_runs, d_nruns,
+                       D.ex_runs_cap);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(D.ex_ev[1], st));
+    lap("fill");
     hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
                        D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
     HIP_OK(hipGetLastError());
+    lap("h2rows");
     HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    lap("d2h");
+    {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, D.ex_ev[0], D.ex_ev[1]) == hipSuccess) D.last.tier_ms[0] += ms;
+    }
     // overlay handles -> ovh->base + overlay index (batch-local wildcard roots only)
     if (ovh && !ovh->empty())
         host_parallel_for(total, [&](uint64_t i) {

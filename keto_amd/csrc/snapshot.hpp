@@ -19,6 +19,8 @@
 #include <shared_mutex>
 #include <string>
 #include <string_view>
+#include <type_traits>
+#include <utility>
 #include <unordered_map>
 #include <vector>
 
@@ -389,10 +391,31 @@ uint64_t device_tree_proto(Snapshot& s, const keto_tree_node* nodes, uint64_t n_
                            uint32_t n_trees, uint32_t ov_base, const std::vector<RowKey>& ov_keys, uint32_t extra_base,
                            const std::vector<std::string>& extra, uint8_t* buf, uint64_t cap, uint64_t* offsets);
 void device_copy(void* dst, const void* src, uint64_t bytes, void* stream);   // D2D, synchronous
+// An allocator whose resize() leaves new elements default-initialized (no zero fill): the expand
+// node arena is sized, then overwritten by one D2H copy.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new ((void*)p) U;
+    }
+};
+
 struct ExpandResult {
     std::vector<uint8_t> status;
     std::vector<uint64_t> offset;          // n+1
-    std::vector<keto_tree_node> nodes;
+    std::vector<keto_tree_node, NoInitAlloc<keto_tree_node>> nodes;
 };
 // roots: row handles (root_flags bit0 = subject set) or string ids; out.nodes carry row ids
 void device_expand(Snapshot& s, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,

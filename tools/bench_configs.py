@@ -274,7 +274,7 @@ def config5(a, g=None):
             "gpu": {"trees_per_s": round(n / best, 1), "wall_ms": round(best * 1e3, 3),
                     "kernel_ms": round(kern, 3),
                     "what": "keto_expand_batch_ids: H2D roots, count pass, host scan, fill pass, D2H tree arena; "
-                            "kernel_ms = both passes' tier kernels (HIP events)"},
+                            "kernel_ms = both passes' tier kernels and the fill pass's id-run copies (HIP events)"},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern, 3),
                          "alg_bytes_per_root": round(per, 1),
