@@ -27,7 +27,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <new>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -3437,6 +3440,69 @@ __global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restric
         else hi = m;
     }
     nodes[i].subject = EDGE_SET | rows[lo];
+}
+
+// ---- the pinned block pool behind PinnedAlloc (snapshot.hpp); never destroyed, so an arena freed
+// late in process exit still finds it
+namespace {
+struct PinPool {
+    std::mutex mu;
+    std::multimap<size_t, void*> idle;                              // idle blocks by size
+    std::unordered_map<void*, std::pair<size_t, bool>> live;        // block -> (size, page-locked)
+    size_t idle_bytes = 0;
+};
+PinPool& pin_pool() {
+    static PinPool* p = new PinPool;
+    return *p;
+}
+constexpr size_t PIN_IDLE_MAX = 1ull << 30;                         // idle pinned bytes kept for reuse
+}  // namespace
+
+void* pinned_take(size_t bytes) {
+    PinPool& P = pin_pool();
+    if (bytes == 0) bytes = 1;
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        auto it = P.idle.lower_bound(bytes);
+        if (it != P.idle.end() && it->first <= 2 * bytes + (1u << 20)) {   // not much bigger than asked
+            void* p = it->second;
+            P.idle_bytes -= it->first;
+            P.idle.erase(it);
+            return p;
+        }
+    }
+    const size_t sz = (bytes + 4095) & ~(size_t)4095;
+    void* p = nullptr;
+    const bool pinned = hipHostMalloc(&p, sz, hipHostMallocDefault) == hipSuccess && p;
+    if (!pinned) {
+        (void)hipGetLastError();
+        p = malloc(sz);
+        if (!p) throw std::bad_alloc();
+    }
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.live[p] = {sz, pinned};
+    return p;
+}
+
+void pinned_give(void* p) noexcept {
+    if (!p) return;
+    PinPool& P = pin_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.live.find(p);
+    if (it == P.live.end()) return;
+    const size_t sz = it->second.first;
+    if (!it->second.second) {
+        P.live.erase(it);
+        free(p);
+        return;
+    }
+    if (P.idle_bytes + sz <= PIN_IDLE_MAX) {      // keep it (still in `live`) for the next arena
+        P.idle.emplace(sz, p);
+        P.idle_bytes += sz;
+        return;
+    }
+    P.live.erase(it);
+    (void)hipHostFree(p);
 }
 
 void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,

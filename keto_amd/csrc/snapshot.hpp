@@ -412,10 +412,33 @@ struct NoInitAlloc : std::allocator<T> {
     }
 };
 
+// Page-locked host memory for expand node arenas (engine.hip): blocks are recycled across arenas,
+// so the arena's D2H is one DMA at the link's rate without a hipHostMalloc per call.  Falls back to
+// malloc when no pinned memory can be had.
+void* pinned_take(size_t bytes);
+void pinned_give(void* p) noexcept;
+template <class T>
+struct PinnedAlloc : NoInitAlloc<T> {
+    using value_type = T;
+    template <class U>
+    struct rebind {
+        using other = PinnedAlloc<U>;
+    };
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U>&) noexcept {}
+    T* allocate(size_t n) { return static_cast<T*>(pinned_take(n * sizeof(T))); }
+    void deallocate(T* p, size_t) noexcept { pinned_give(p); }
+};
+template <class T, class U>
+bool operator==(const PinnedAlloc<T>&, const PinnedAlloc<U>&) noexcept { return true; }
+template <class T, class U>
+bool operator!=(const PinnedAlloc<T>&, const PinnedAlloc<U>&) noexcept { return false; }
+
 struct ExpandResult {
     std::vector<uint8_t> status;
     std::vector<uint64_t> offset;          // n+1
-    std::vector<keto_tree_node, NoInitAlloc<keto_tree_node>> nodes;
+    std::vector<keto_tree_node, PinnedAlloc<keto_tree_node>> nodes;
 };
 // roots: row handles (root_flags bit0 = subject set) or string ids; out.nodes carry row ids
 void device_expand(Snapshot& s, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
