@@ -129,6 +129,16 @@ def test_deep_chain_tree_json():
         sys.setrecursionlimit(old)
     assert got[0][0] == EXPAND_TREE
     assert texts[0] == want
+    # the protobuf encoders on the same tree: per tree, all trees on host threads, and on the GPU
+    sys.setrecursionlimit(max(old, 4 * k + 1000))
+    try:
+        (st, _, pb), = snap.expand_batch([(("set", "n", "g0", "m"), 3000)], 3000, want_proto=True)
+        _, host = snap.expand_batch([(("set", "n", "g0", "m"), 3000)], 3000, proto_all="host")
+        _, dev = snap.expand_batch([(("set", "n", "g0", "m"), 3000)], 3000, proto_all="device")
+    finally:
+        sys.setrecursionlimit(old)
+    assert st == EXPAND_TREE and len(pb) > 0
+    assert host[0] == pb and dev[0] == pb
 
 
 @pytest.mark.parametrize("seed", range(2000, 2060))
