@@ -389,7 +389,9 @@ int keto_check_work_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint3
 int keto_check_steps_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                             uint8_t* d_allowed_out, uint32_t* d_steps);
 
-/* Batched BuildTree.  The arena owns all trees; free it with keto_tree_arena_free. */
+/* Batched BuildTree.  The arena owns all trees; free it with keto_tree_arena_free.  Its node array
+ * lives in page-locked host memory from a process-wide pool (blocks are recycled by later arenas;
+ * up to 1 GiB of idle blocks is kept), so keto_tree_proto_all_device uploads it in one DMA. */
 int keto_expand_batch(keto_snapshot* s, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
                       keto_tree_arena** out);
 /* Same with pre-resolved roots: roots[i] bit31 set -> subject set (bits 0..30 = row id), else a
