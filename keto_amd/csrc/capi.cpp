@@ -930,7 +930,9 @@ int64_t keto_tree_json_all(const keto_snapshot* h, const keto_tree_arena* a, cha
     offsets[0] = 0;
     for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + enc[i].size();
     if (buf && cap >= offsets[n])
-        for (uint32_t i = 0; i < n; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
+        par_chunks(n, offsets[n] >= (8u << 20) ? th : 1u, 256, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
+        });
     return (int64_t)offsets[n];
 }
 
@@ -973,7 +975,9 @@ int64_t keto_tree_proto_all(const keto_snapshot* h, const keto_tree_arena* a, ui
     offsets[0] = 0;
     for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + enc[i].size();
     if (buf && cap >= offsets[n])
-        for (uint32_t i = 0; i < n; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
+        par_chunks(n, offsets[n] >= (8u << 20) ? th : 1u, 256, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
+        });
     return (int64_t)offsets[n];
 }
 
