@@ -583,14 +583,15 @@ class Snapshot:
         return status, offs, blob, t1 - t0, t_enc
 
     def _proto_all(self, a, n, device=False):
-        """(offsets[n+1], blob, seconds of the filling call) of keto_tree_proto_all[_device]."""
+        """(offsets[n+1], blob, seconds of the sizing + filling calls, as a caller pays them) of
+        keto_tree_proto_all[_device] (the host encoder keeps a sizing call's encodings for the fill)."""
         import time
         fn = self.lib.keto_tree_proto_all_device if device else self.lib.keto_tree_proto_all
         offs = np.zeros(n + 1, dtype=np.uint64)
+        t0 = time.perf_counter()
         total = fn(self.h, a, None, C.c_uint64(0), offs.ctypes.data_as(C.c_void_p))
         _check(min(0, total))
-        blob = np.zeros(max(1, total), dtype=np.uint8)
-        t0 = time.perf_counter()
+        blob = np.empty(max(1, total), dtype=np.uint8)
         got = fn(self.h, a, blob.ctypes.data_as(C.c_void_p), C.c_uint64(total), offs.ctypes.data_as(C.c_void_p))
         dt = time.perf_counter() - t0
         _check(min(0, got))

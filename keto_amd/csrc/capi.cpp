@@ -24,6 +24,13 @@ struct keto_tree_arena {
     std::vector<RowKey> ov_keys;           // overlay roots (wildcard queries)
     uint32_t extra_base = 0;               // subject-id strings not in the snapshot
     std::vector<std::string> extra;
+    // keto_tree_json_all / keto_tree_proto_all: the encodings of a sizing call (buf too small), kept
+    // for the filling call that follows it, so a size-then-fill pair encodes once
+    mutable std::mutex enc_mu;
+    mutable int enc_kind = 0;              // 0 none, 1 JSON, 2 protobuf
+    mutable const void* enc_snap = nullptr;
+    mutable uint64_t enc_version = 0;
+    mutable std::vector<std::string> enc;
 };
 
 namespace {
@@ -902,38 +909,61 @@ int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_
     return copy_out(o, buf, cap);
 }
 
-int64_t keto_tree_json_all(const keto_snapshot* h, const keto_tree_arena* a, char* buf, uint64_t cap,
-                           uint64_t* offsets) {
-    if (!h || !a || !offsets) return KETO_E_INVALID;
+extern "C++" {
+// Every tree of the arena encoded on host threads by `one(i, out)`, into buf at offsets (see
+// keto_tree_json_all / keto_tree_proto_all).  A call whose buf cannot take the total keeps the
+// encodings in the arena for the next call of the same kind on the same snapshot version.
+template <class One>
+int64_t encode_all(const keto_snapshot* h, const keto_tree_arena* a, int kind, char* buf, uint64_t cap,
+                   uint64_t* offsets, One one) {
     const uint32_t n = (uint32_t)a->r.status.size();
-    std::vector<std::string> enc(n);
     const unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::thread> ts;
-    std::atomic<uint32_t> next{0};
-    for (unsigned t = 0; t < th; ++t)
-        ts.emplace_back([&] {
-            for (;;) {
-                const uint32_t k = next.fetch_add(64);
-                if (k >= n) break;
-                for (uint32_t i = k; i < std::min(n, k + 64); ++i) {
-                    const int st = a->r.status[i];
-                    if (st == KETO_EXPAND_TREE) {
-                        const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
-                        tree_json(*h->s, a, a->r.nodes.data() + b, e - b, enc[i]);
-                    } else if (st != KETO_EXPAND_NOT_FOUND && st != KETO_EXPAND_UNDECIDED) {
-                        enc[i] = "null";
-                    }
+    std::lock_guard<std::mutex> lk(a->enc_mu);
+    std::vector<std::string>& enc = a->enc;
+    if (!(a->enc_kind == kind && a->enc_snap == h && a->enc_version == h->s->version && enc.size() == n)) {
+        enc.assign(n, std::string());
+        std::vector<std::thread> ts;
+        std::atomic<uint32_t> next{0};
+        for (unsigned t = 0; t < th; ++t)
+            ts.emplace_back([&] {
+                for (;;) {
+                    const uint32_t k = next.fetch_add(64);
+                    if (k >= n) break;
+                    for (uint32_t i = k; i < std::min(n, k + 64); ++i) one(i, enc[i]);
                 }
-            }
-        });
-    for (auto& x : ts) x.join();
+            });
+        for (auto& x : ts) x.join();
+    }
     offsets[0] = 0;
     for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + enc[i].size();
-    if (buf && cap >= offsets[n])
+    const int64_t total = (int64_t)offsets[n];
+    if (buf && cap >= offsets[n]) {
         par_chunks(n, offsets[n] >= (8u << 20) ? th : 1u, 256, [&](uint64_t b, uint64_t e, unsigned) {
             for (uint64_t i = b; i < e; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
         });
-    return (int64_t)offsets[n];
+        std::vector<std::string>().swap(enc);          // written: drop the cache
+        a->enc_kind = 0;
+    } else {
+        a->enc_kind = kind;
+        a->enc_snap = h;
+        a->enc_version = h->s->version;
+    }
+    return total;
+}
+}  // extern "C++"
+
+int64_t keto_tree_json_all(const keto_snapshot* h, const keto_tree_arena* a, char* buf, uint64_t cap,
+                           uint64_t* offsets) {
+    if (!h || !a || !offsets) return KETO_E_INVALID;
+    return encode_all(h, a, 1, buf, cap, offsets, [&](uint32_t i, std::string& o) {
+        const int st = a->r.status[i];
+        if (st == KETO_EXPAND_TREE) {
+            const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+            tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
+        } else if (st != KETO_EXPAND_NOT_FOUND && st != KETO_EXPAND_UNDECIDED) {
+            o = "null";
+        }
+    });
 }
 
 int64_t keto_tree_proto(const keto_snapshot* h, const keto_tree_arena* a, uint32_t i, uint8_t* buf, uint64_t cap) {
@@ -954,31 +984,12 @@ int64_t keto_tree_proto(const keto_snapshot* h, const keto_tree_arena* a, uint32
 int64_t keto_tree_proto_all(const keto_snapshot* h, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
                             uint64_t* offsets) {
     if (!h || !a || !offsets) return KETO_E_INVALID;
-    const uint32_t n = (uint32_t)a->r.status.size();
-    std::vector<std::string> enc(n);
-    const unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::thread> ts;
-    std::atomic<uint32_t> next{0};
-    for (unsigned t = 0; t < th; ++t)
-        ts.emplace_back([&] {
-            for (;;) {
-                const uint32_t k = next.fetch_add(64);
-                if (k >= n) break;
-                for (uint32_t i = k; i < std::min(n, k + 64); ++i)
-                    if (a->r.status[i] == KETO_EXPAND_TREE) {
-                        const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
-                        tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, enc[i]);
-                    }
-            }
-        });
-    for (auto& x : ts) x.join();
-    offsets[0] = 0;
-    for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + enc[i].size();
-    if (buf && cap >= offsets[n])
-        par_chunks(n, offsets[n] >= (8u << 20) ? th : 1u, 256, [&](uint64_t b, uint64_t e, unsigned) {
-            for (uint64_t i = b; i < e; ++i) std::memcpy(buf + offsets[i], enc[i].data(), enc[i].size());
-        });
-    return (int64_t)offsets[n];
+    return encode_all(h, a, 2, reinterpret_cast<char*>(buf), cap, offsets, [&](uint32_t i, std::string& o) {
+        if (a->r.status[i] == KETO_EXPAND_TREE) {
+            const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+            tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
+        }
+    });
 }
 
 int64_t keto_tree_proto_all_device(keto_snapshot* h, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
