@@ -411,7 +411,9 @@ int64_t keto_tree_json(const keto_snapshot* s, const keto_tree_arena* a, uint32_
  * BuildTree result, via Tree.MarshalJSON): offsets[n+1], tree i = buf[offsets[i],
  * offsets[i+1]) -- keto_tree_json's text for a tree, "null" for a nil tree, empty for the roots
  * keto_tree_json reports as errors (KETO_EXPAND_NOT_FOUND / KETO_EXPAND_UNDECIDED).  buf is written
- * only if cap >= the total, which is returned (call with buf = NULL to size it). */
+ * only if cap >= the total, which is returned (call with buf = NULL to size it).  A sizing call
+ * keeps its encodings in the arena until the filling call (or keto_tree_arena_free), so the pair
+ * encodes once; keto_tree_proto_all does the same. */
 int64_t keto_tree_json_all(const keto_snapshot* s, const keto_tree_arena* a, char* buf, uint64_t cap,
                            uint64_t* offsets);
 
