@@ -23,6 +23,12 @@ Extras on the same line:
                 with the GPU's for that sample ("parity").
   ref_sql       the reference recursion issuing its own SQL against in-memory SQLite, one worker
                 process per core, over the first 10,000 requests (compared with the GPU too).
+  string_form   (N = 1) the same batch as named requests (keto_check_req: namespace, object, relation,
+                subject id strings in C memory) through keto_check_batch, the entry point the Go
+                shim calls: name resolution on host threads, then the pipelined device part.  The
+                snapshot then carries the graph's string table (tools/synth.py unified()).
+Host cores: --threads defaults to the CPUs this job may use (tools/hostcpu.py: affinity mask,
+cgroup quota, the harness's OMP_NUM_THREADS share), recorded with every CPU leg.
 """
 import argparse
 import json
@@ -68,7 +74,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=16 * 1024 * 1024, help="checks per GPU per step")
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale (1.0 = 1B tuples)")
     ap.add_argument("--depth", type=int, default=5)
-    ap.add_argument("--threads", type=int, default=16, help="host threads (generator, cpu baseline)")
+    ap.add_argument("--threads", type=int, default=None,
+                    help="host threads (generator, resolution, cpu baseline); default: the usable host CPUs")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="requests in the cpu_baseline sample")
     ap.add_argument("--sql-sample", type=int, default=10_000, help="requests in the ref_sql (SQLite) sample")
     ap.add_argument("--bytes-sample", type=float, default=0.01,
@@ -88,17 +95,15 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=5,
                     help="batches timed end to end through the host API (keto_check_batch_rows, pinned buffers); 0 = skip")
     ap.add_argument("--e2e-only", action="store_true", help="time only the end-to-end leg (profiling runs)")
-    return ap.parse_args()
-
-
-def cpu_model():
-    try:
-        for ln in open("/proc/cpuinfo"):
-            if ln.startswith("model name"):
-                return ln.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return None
+    ap.add_argument("--string-steps", type=int, default=3,
+                    help="N = 1: batches timed through keto_check_batch with named requests (0 = skip)")
+    a = ap.parse_args()
+    from tools.hostcpu import host_cores
+    a.host = host_cores()
+    if a.threads is None:
+        a.threads = a.host["usable"]
+    os.environ.setdefault("KETO_BUILD_THREADS", str(a.threads))     # the library's host thread pools
+    return a
 
 
 def sql_leg(g, q, a, gpu_out):
@@ -140,7 +145,7 @@ def sql_leg(g, q, a, gpu_out):
     dec = np.array(res["decisions"], dtype=np.uint8)
     return {"value": res["checks_per_s"], "unit": "checks/s", "cores": res["workers"],
             "mismatches_vs_gpu": int((dec != gpu_out[:k]).sum()),
-            "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model(), "workers_used": res["workers"]},
+            "host": {**a.host, "workers_used": res["workers"]},
             "sample": f"first {k} requests; oracle/oracle_sql.py (the reference check engine's recursion issuing "
                       f"its SELECT ... ORDER BY ... LIMIT 100 OFFSET and page count per node) over the {stab.t.n} "
                       f"tuples they reach, in-memory SQLite copies of one image in each of {res['workers']} "
@@ -189,6 +194,42 @@ def end_to_end(snap, q, a, d_out):
                     "streams; median of the timed batches", "_out": outs}
 
 
+def string_form(g, u, snap, q, a):
+    """keto_check_batch on the batch as named requests (strings in C memory, built by the
+    generator from the same request ids): resolution on host threads, then the device pipeline."""
+    n = len(q)
+    log(f"string-form leg: {a.string_steps} batches of {n} named requests through keto_check_batch")
+    t0 = time.perf_counter()
+    reqs = g.string_requests(u.names, q, threads=a.threads)
+    t_make = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    out, st = snap.check_batch_reqs(reqs, n, a.depth)               # warm-up: builds the string / row indexes
+    t_first = time.perf_counter() - t0
+    ts, res, walls = [], [], []
+    for _ in range(a.string_steps):
+        t0 = time.perf_counter()
+        out, st = snap.check_batch_reqs(reqs, n, a.depth)
+        ts.append(time.perf_counter() - t0)
+        t = snap.last_timing_full()
+        res.append(t["resolve_ms"])
+        walls.append(t["wall_ms"])
+    ms = float(np.median(ts)) * 1e3
+    return {"value": round(n / (ms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(ms, 3),
+            "resolve_ms": round(float(np.median(res)), 3), "device_wall_ms": round(float(np.median(walls)), 3),
+            "threads": a.threads, "first_call_ms": round(t_first * 1e3, 1), "request_build_s": round(t_make, 2),
+            "strings_in_snapshot": int(u.n_strings), "statuses_not_ok": int((st != 0).sum()),
+            "what": "keto_check_batch (the Go shim's entry point): 128-B keto_check_req with namespace / object / "
+                    "relation / subject-id strings in C memory -> name resolution on host threads (hashed string "
+                    "and row indexes) -> pipelined H2D / check / D2H; median of the timed batches; first_call_ms "
+                    "includes building the indexes", "_out": out.copy()}
+
+
+def rusage():
+    import resource
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_maxrss / 1e6, r.ru_utime + r.ru_stime          # GB (ru_maxrss is in KB), CPU seconds
+
+
 def main():
     a = parse()
     import torch
@@ -221,6 +262,7 @@ def main():
     log(f"rank {rank}: {g.n_edges} tuples, {g.n_rows} rows; building + uploading the snapshot")
     t0 = time.time()
     migrate = a.partitioned and a.part_mode == "migrate"
+    unified = None
     # collectives of the partitioned modes: on the GPU with RCCL, staged through the host with gloo
     comm = f"cuda:{dev}" if backend == "nccl" else "cpu"
     if migrate:
@@ -233,9 +275,19 @@ def main():
         else:
             snap.part_closure_done(True)
     else:
-        snap = g.snapshot_part(rank, world, dev) if a.partitioned else g.snapshot(device=dev)
+        if a.partitioned:
+            snap = g.snapshot_part(rank, world, dev)
+        elif world == 1 and a.string_steps > 0:
+            # one string id space and the string table in the snapshot, for the string-form leg
+            unified = g.unified(threads=a.threads)
+            snap = g.snapshot_unified(unified, device=dev)
+        else:
+            snap = g.snapshot(device=dev)
     t_snap = time.time() - t0
     q = g.queries(a.batch, seed=1000 + rank, depth=a.depth, threads=a.threads)
+    q_gen = q                                           # generator ids: the oracle legs' requests
+    if not migrate and not a.partitioned and unified is not None:
+        q = unified.to_device_targets(q)                # the snapshot's subject-id space
     d_out = torch.empty(a.batch, dtype=torch.uint8, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
@@ -267,6 +319,9 @@ def main():
         def step():
             snap.check_batch_device(d_q.data_ptr(), a.batch, d_out.data_ptr(), a.depth, sp)
 
+    strf = None
+    if not migrate and not a.partitioned and unified is not None:
+        strf = string_form(g, unified, snap, q_gen, a)
     e2e = None
     if not a.partitioned and a.e2e_steps > 0:
         e2e = end_to_end(snap, q, a, d_out)
@@ -314,7 +369,7 @@ def main():
     if rank == 0 and not a.no_work and not migrate:
         # oracle table over a bounded sample of the batch: every tuple those requests can reach
         ns = min(a.cpu_sample, a.batch)
-        sample = q[:ns]
+        sample = q_gen[:ns]
         log(f"oracle table over the first {ns} requests")
         t0 = time.perf_counter()
         tab = g.oracle_table(sample, a.depth)
@@ -372,14 +427,14 @@ def main():
             t_cpu = time.perf_counter() - t0
             parity = {"sample": int(ns), "mismatches": int((ref != gpu_out[:ns]).sum())}
             cpu = {"value": round(ns / t_cpu, 1), "unit": "checks/s", "cores": a.threads, "kind": "port",
-                   "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model()},
+                   "host": {**a.host, "threads_used": a.threads},
                    "sample": f"first {ns} requests of the rank-0 batch; oracle/keto_oracle.c over the "
                              f"{tab.t.n} tuples those requests can reach (extracted in {t_tab:.1f} s), "
                              f"{a.threads} host threads, {t_cpu:.2f} s"}
             # the reference engine's algorithm issuing its own SQL against SQLite, one worker process
             # per core (oracle/sql_bench.py), on a bounded sample
             if a.sql_sample > 0:
-                ref_sql = sql_leg(g, q, a, gpu_out)
+                ref_sql = sql_leg(g, q_gen, a, gpu_out)
 
     part_parity = None
     if a.partitioned and a.check_parity:
@@ -394,6 +449,20 @@ def main():
         e2e["frac"] = round(roofline["alg_bytes_per_launch"] / (e2e["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if e2e is not None:
         e2e["decisions_equal_device_resident"] = all(bool((o == gpu_out).all()) for o in e2e.pop("_out"))
+    if strf is not None:
+        strf["decisions_equal_device_resident"] = bool((strf.pop("_out") == gpu_out).all())
+        if roofline is not None:
+            strf["frac"] = round(roofline["alg_bytes_per_launch"] / (strf["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if e2e is not None:
+            e2e["string_form"] = strf
+    # host resources per rank (the 8-rank run: every rank holds the graph and the snapshot's host tables)
+    rss, cpu_s = rusage()
+    host_ranks = [[rss, cpu_s]]
+    if world > 1:
+        t = torch.tensor([rss, cpu_s], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
+        allr = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        host_ranks = [x.tolist() for x in allr]
     if rank == 0:
         line = {
             "metric": "checks/sec (whole node) on 1B-tuple graph, max-depth 5; % of HBM roofline",
@@ -419,6 +488,9 @@ def main():
             "detail": {"tier0_ms": round(tier0_ms, 3), "tier1_ms": round(tier1_ms, 3),
                        "tier0_overflow_requests": overflow, "allowed_fraction": round(allowed_rate, 4),
                        "gen_s": round(t_gen, 1), "snapshot_upload_s": round(t_snap, 1), "work": work,
+                       "host_per_rank": [{"peak_rss_gb": round(r_, 2), "cpu_s": round(c_, 1)} for r_, c_ in host_ranks],
+                       "host": a.host, "threads": a.threads,
+                       "string_table": unified is not None if not migrate else False,
                        "migrate_rounds_last_step": routed[2] if migrate else None},
         }
         print(json.dumps(line), flush=True)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 3
+#define KETO_ABI_VERSION 4
 
 /* return codes */
 #define KETO_OK 0
@@ -367,6 +367,7 @@ typedef struct {
     uint32_t undecided;         /* requests left KETO_UNDECIDED */
     uint32_t chunks;            /* host-buffer calls: pipeline chunks (0 for device calls) */
     float wall_ms;              /* host-buffer calls: entry to return, H2D + checks + D2H */
+    float resolve_ms;           /* keto_check_batch: name resolution on host threads before the device part */
 } keto_batch_timing;
 int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
 
@@ -434,6 +435,18 @@ int64_t keto_tree_proto_all(const keto_snapshot* s, const keto_tree_arena* a, ui
  * state); a pinned (hipHostMalloc'd) buf takes one DMA, a pageable one two pinned bounce chunks. */
 int64_t keto_tree_proto_all_device(keto_snapshot* s, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
                                    uint64_t* offsets);
+
+/* The fields of subject references as keto_tree_node.subject holds them, for building expand.Tree
+ * values (internal/expand/tree.go:26-30: relationtuple.SubjectID / SubjectSet,
+ * internal/relationtuple/definitions.go:40-42,102-117) straight from the node arena without a text
+ * codec.  a: the arena the references come from (its batch-local wildcard roots and subject ids the
+ * snapshot does not know), or NULL.  Reference i: lens_out[3i..3i+2] = (id length, 0, 0) for a subject
+ * id, (namespace, object, relation lengths) for a subject set; the strings follow one another in buf
+ * in that order.  buf is written only if cap >= the total byte count, which is returned (call with
+ * buf = NULL to size it; the count of a reference never changes, so a size-then-fill pair agrees
+ * even across keto_snapshot_apply). */
+int64_t keto_subject_fields(const keto_snapshot* s, const keto_tree_arena* a, const uint32_t* subjects, uint64_t n,
+                            char* buf, uint64_t cap, uint32_t* lens_out);
 
 /* String of a subject reference used in keto_tree_node.subject (Subject.String(), definitions.go:163-169). */
 int64_t keto_subject_string(const keto_snapshot* s, uint32_t subject, char* buf, uint64_t cap);

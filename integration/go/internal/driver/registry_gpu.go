@@ -1,0 +1,302 @@
+//go:build keto_gpu
+// +build keto_gpu
+
+package driver
+
+import (
+	"context"
+	"errors"
+	"os"
+	"strconv"
+	"sync"
+
+	"github.com/ory/keto/internal/gpu"
+	"github.com/ory/keto/internal/persistence"
+	"github.com/ory/keto/internal/relationtuple"
+)
+
+// The registry side of the GPU path.  After Init (internal/driver/registry_default.go:241-262) the
+// server calls EnableGPU once, the one change to cmd/server/serve.go:45-55:
+//
+//	reg, err := driver.NewDefaultRegistry(cmd.Context(), cmd.Flags(), false)
+//	...
+//	if err := driver.EnableGPU(cmd.Context(), reg, driver.GPUDeviceFromEnv()); err != nil {
+//		return err
+//	}
+//	return reg.ServeAllSQA(cmd)
+//
+// EnableGPU builds the snapshot from one full scan of the table, starts the check and expand
+// batchers over it, and wraps the persister so that every committed write transaction is applied to
+// the snapshot before the write returns.  The engines find the batchers through GPUCheckBatcher /
+// GPUExpandBatcher (internal/check/engine_gpu.go, internal/expand/engine_gpu.go) and answer on SQL
+// whenever those return nil: no GPU, or a snapshot that is behind the table while it is rebuilt.
+
+// GPUDeviceFromEnv is the HIP device of the GPU path: KETO_GPU_DEVICE (unset or negative: off).
+func GPUDeviceFromEnv() int {
+	v, err := strconv.Atoi(os.Getenv("KETO_GPU_DEVICE"))
+	if err != nil {
+		return -1
+	}
+	return v
+}
+
+// gpuRowSource is the persister's full scan (internal/persistence/sql/snapshot_gpu.go).
+type gpuRowSource interface {
+	SnapshotRows(ctx context.Context) ([]gpu.Row, error)
+}
+
+type gpuState struct {
+	r      *RegistryDefault
+	device int
+	check  *gpu.Batcher
+	expand *gpu.ExpandBatcher
+
+	mu    sync.RWMutex
+	snap  *gpu.Snapshot
+	stale bool // the snapshot is behind the table: the engines answer on SQL until the rebuild lands
+
+	wmu        sync.Mutex // one write transaction (SQL commit + Apply) at a time; the rebuild's scan holds it too
+	rebuilding bool
+	pending    [][2][]gpu.Row // writes committed after the rebuild's scan, applied to the new snapshot
+	rescan     bool           // a write during the rebuild cannot be replayed: scan the table again
+}
+
+// one state per registry (RegistryDefault's fields are in registry_default.go)
+var gpuStates sync.Map // *RegistryDefault -> *gpuState
+
+func gpuOf(r *RegistryDefault) *gpuState {
+	if v, ok := gpuStates.Load(r); ok {
+		return v.(*gpuState)
+	}
+	return nil
+}
+
+// EnableGPU loads the GPU snapshot for HIP device `device` (< 0: leave the registry on SQL).
+func EnableGPU(ctx context.Context, reg Registry, device int) error {
+	r, ok := reg.(*RegistryDefault)
+	if !ok || device < 0 {
+		return nil
+	}
+	if err := r.Init(ctx); err != nil {
+		return err
+	}
+	st := &gpuState{r: r, device: device}
+	snap, err := st.build(ctx)
+	if err != nil {
+		return err
+	}
+	st.snap = snap
+	globalMax := func() int { return r.Config().ReadAPIMaxDepth() }
+	st.check = gpu.NewBatcher(snap, globalMax, r.PermissionEngine().Fallback())
+	st.expand = gpu.NewExpandBatcher(snap, globalMax)
+	r.p = &gpuPersister{Persister: r.p, g: st}
+	gpuStates.Store(r, st)
+	return nil
+}
+
+// GPUCheckBatcher implements check.GPUProvider (nil: answer on SQL).
+func (r *RegistryDefault) GPUCheckBatcher() *gpu.Batcher {
+	st := gpuOf(r)
+	if st == nil {
+		return nil
+	}
+	st.mu.RLock()
+	defer st.mu.RUnlock()
+	if st.stale {
+		return nil
+	}
+	return st.check
+}
+
+// GPUExpandBatcher implements expand.GPUProvider (nil: answer on SQL).
+func (r *RegistryDefault) GPUExpandBatcher() *gpu.ExpandBatcher {
+	st := gpuOf(r)
+	if st == nil {
+		return nil
+	}
+	st.mu.RLock()
+	defer st.mu.RUnlock()
+	if st.stale {
+		return nil
+	}
+	return st.expand
+}
+
+// build scans the table (caller holds wmu when it must be consistent with writes) and uploads.
+func (g *gpuState) build(ctx context.Context) (*gpu.Snapshot, error) {
+	src, ok := g.r.p.(gpuRowSource) // EnableGPU builds before it wraps the persister
+	if !ok {
+		return nil, errors.New("gpu: the persister has no full-scan source")
+	}
+	rows, err := src.SnapshotRows(ctx)
+	if err != nil {
+		return nil, err
+	}
+	return g.buildFrom(ctx, rows)
+}
+
+func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) (*gpu.Snapshot, error) {
+	nm, err := g.r.Config().NamespaceManager()
+	if err != nil {
+		return nil, err
+	}
+	nss, err := nm.Namespaces(ctx) // config order: the builder maps names to ids with it
+	if err != nil {
+		return nil, err
+	}
+	return gpu.Build(nss, rows, g.device)
+}
+
+// applyLocked runs after a write committed, with wmu held: the snapshot follows the table one
+// transaction at a time, or goes stale and is rebuilt.
+func (g *gpuState) applyLocked(ctx context.Context, ins, del []*relationtuple.InternalRelationTuple) {
+	nm, err := g.r.Config().NamespaceManager()
+	var iRows, dRows []gpu.Row
+	if err == nil {
+		iRows, err = gpu.RowsOf(ctx, nm, ins)
+	}
+	if err == nil {
+		dRows, err = gpu.RowsOf(ctx, nm, del)
+	}
+	if g.rebuilding {
+		if err != nil { // cannot replay this write: the rebuild scans the table again
+			g.rescan = true
+			return
+		}
+		g.pending = append(g.pending, [2][]gpu.Row{iRows, dRows})
+		return
+	}
+	g.mu.RLock()
+	snap, stale := g.snap, g.stale
+	g.mu.RUnlock()
+	if stale { // an earlier rebuild failed: the snapshot is behind, try again
+		g.startRebuildLocked()
+		return
+	}
+	if err == nil {
+		err = snap.Apply(iRows, dRows)
+	}
+	if err != nil { // gpu.ErrRebuild (or a failed write to the device): serve SQL until rebuilt
+		g.startRebuildLocked()
+	}
+}
+
+// startRebuildLocked (wmu held): mark the snapshot stale and rebuild it in the background.
+func (g *gpuState) startRebuildLocked() {
+	g.mu.Lock()
+	g.stale = true
+	g.mu.Unlock()
+	if g.rebuilding {
+		return
+	}
+	g.rebuilding = true
+	go g.rebuild()
+}
+
+// rebuild: scan the table under wmu (so the scan sees every committed write and none is half
+// applied), build without it, replay the writes that committed meanwhile, swap the new snapshot into
+// the batchers and serve from the GPU again.
+func (g *gpuState) rebuild() {
+	ctx := context.Background()
+	for {
+		g.wmu.Lock()
+		g.pending = nil
+		g.rescan = false
+		var src gpuRowSource
+		if w, ok := g.r.p.(*gpuPersister); ok {
+			src, _ = w.Persister.(gpuRowSource)
+		}
+		var rows []gpu.Row
+		var err error
+		if src == nil {
+			err = errors.New("gpu: the persister has no full-scan source")
+		} else {
+			rows, err = src.SnapshotRows(ctx)
+		}
+		g.wmu.Unlock()
+		var snap *gpu.Snapshot
+		if err == nil {
+			snap, err = g.buildFrom(ctx, rows)
+		}
+		rows = nil
+		g.wmu.Lock()
+		if err != nil || g.rescan {
+			g.wmu.Unlock()
+			if snap != nil {
+				snap.Close()
+			}
+			if err != nil { // stay stale (SQL answers); a later write retries the rebuild
+				g.wmu.Lock()
+				g.rebuilding = false
+				g.wmu.Unlock()
+				return
+			}
+			continue
+		}
+		replayed := true
+		for _, w := range g.pending {
+			if snap.Apply(w[0], w[1]) != nil {
+				replayed = false
+				break
+			}
+		}
+		if !replayed { // a replayed write needs a rebuild itself: scan again
+			g.wmu.Unlock()
+			snap.Close()
+			continue
+		}
+		old := g.check.Swap(snap) // waits for batches running on the old version
+		g.expand.Swap(snap)
+		g.mu.Lock()
+		g.snap = snap
+		g.stale = false
+		g.mu.Unlock()
+		g.pending = nil
+		g.rebuilding = false
+		g.wmu.Unlock()
+		old.Close()
+		return
+	}
+}
+
+// gpuPersister wraps the SQL persister: every committed write reaches the snapshot before the call
+// returns, in commit order (relationtuple.Manager, internal/relationtuple/definitions.go:28-34;
+// TransactRelationTuples = inserts, then deletes, internal/persistence/sql/relationtuples.go:290-297).
+type gpuPersister struct {
+	persistence.Persister
+	g *gpuState
+}
+
+func (p *gpuPersister) WriteRelationTuples(ctx context.Context, rs ...*relationtuple.InternalRelationTuple) error {
+	return p.TransactRelationTuples(ctx, rs, nil)
+}
+
+func (p *gpuPersister) DeleteRelationTuples(ctx context.Context, rs ...*relationtuple.InternalRelationTuple) error {
+	return p.TransactRelationTuples(ctx, nil, rs)
+}
+
+func (p *gpuPersister) TransactRelationTuples(ctx context.Context, ins, del []*relationtuple.InternalRelationTuple) error {
+	p.g.wmu.Lock()
+	defer p.g.wmu.Unlock()
+	if err := p.Persister.TransactRelationTuples(ctx, ins, del); err != nil {
+		return err // rolled back: the snapshot stays as it is
+	}
+	p.g.applyLocked(ctx, ins, del)
+	return nil
+}
+
+// DeleteAllRelationTuples deletes by query (whereQuery, relationtuples.go:178-198): the rows are not
+// named, so the snapshot is rebuilt from the table.
+func (p *gpuPersister) DeleteAllRelationTuples(ctx context.Context, q *relationtuple.RelationQuery) error {
+	p.g.wmu.Lock()
+	defer p.g.wmu.Unlock()
+	if err := p.Persister.DeleteAllRelationTuples(ctx, q); err != nil {
+		return err
+	}
+	if p.g.rebuilding {
+		p.g.rescan = true
+		return nil
+	}
+	p.g.startRebuildLocked()
+	return nil
+}

@@ -5,52 +5,159 @@ package gpu
 
 import (
 	"context"
+	"errors"
+	"fmt"
 	"sync"
 	"time"
 
 	"github.com/ory/keto/internal/relationtuple"
 )
 
+var (
+	// ErrClosed: the batcher was closed; the caller answers on the SQL engine.
+	ErrClosed = errors.New("gpu: batcher closed")
+	// ErrBatchFailed wraps the error of a whole batch (no device, snapshot gone): every request of
+	// the batch goes to the SQL engine.
+	ErrBatchFailed = errors.New("gpu: batch failed")
+)
+
+// coalescer gathers concurrent requests (one goroutine per gRPC / REST request,
+// internal/check/handler.go:108,154,174, internal/expand/handler.go:84,98) into batches: a batch is
+// flushed when maxBatch requests are queued or maxWait after its first request.  Close answers every
+// request still queued through drain, and later calls get ErrClosed without queueing.
+type coalescer struct {
+	maxBatch int
+	maxWait  time.Duration
+	queue    chan *pending
+	stop     chan struct{}
+	done     chan struct{}
+	closeMu  sync.RWMutex // held shared while enqueueing, exclusively by Close
+	closed   bool
+	flush    func([]*pending) // answers every request of a batch
+	drain    func([]*pending) // answers the requests left at Close
+}
+
+type pending struct {
+	ctx  context.Context
+	req  interface{}
+	done chan result
+}
+
+type result struct {
+	val interface{}
+	err error
+}
+
+func newCoalescer(maxBatch int, maxWait time.Duration, flush, drain func([]*pending)) *coalescer {
+	c := &coalescer{maxBatch: maxBatch, maxWait: maxWait, queue: make(chan *pending, maxBatch),
+		stop: make(chan struct{}), done: make(chan struct{}), flush: flush, drain: drain}
+	go c.loop()
+	return c
+}
+
+// submit queues one request and waits for its answer (or ctx).  After Close it returns ErrClosed.
+func (c *coalescer) submit(ctx context.Context, req interface{}) (interface{}, error) {
+	p := &pending{ctx: ctx, req: req, done: make(chan result, 1)}
+	c.closeMu.RLock()
+	if c.closed {
+		c.closeMu.RUnlock()
+		return nil, ErrClosed
+	}
+	select {
+	case c.queue <- p: // the loop runs until Close, which waits for this lock: it will be read
+	case <-ctx.Done():
+		c.closeMu.RUnlock()
+		return nil, ctx.Err()
+	}
+	c.closeMu.RUnlock()
+	select {
+	case res := <-p.done:
+		return res.val, res.err
+	case <-ctx.Done():
+		return nil, ctx.Err()
+	}
+}
+
+// close stops the loop after it has answered (drain) every queued request.
+func (c *coalescer) close() {
+	c.closeMu.Lock()
+	if c.closed {
+		c.closeMu.Unlock()
+		<-c.done
+		return
+	}
+	c.closed = true
+	close(c.stop)
+	c.closeMu.Unlock()
+	<-c.done
+}
+
+func (c *coalescer) loop() {
+	defer close(c.done)
+	for {
+		var first *pending
+		select {
+		case first = <-c.queue:
+		case <-c.stop:
+			// closed: nothing can be enqueued any more (Close held the lock); answer what is left
+			var left []*pending
+			for {
+				select {
+				case p := <-c.queue:
+					left = append(left, p)
+				default:
+					if len(left) > 0 {
+						c.drain(left)
+					}
+					return
+				}
+			}
+		}
+		batch := []*pending{first}
+		timer := time.NewTimer(c.maxWait)
+	fill:
+		for len(batch) < c.maxBatch {
+			select {
+			case p := <-c.queue:
+				batch = append(batch, p)
+			case <-timer.C:
+				break fill
+			}
+		}
+		timer.Stop()
+		c.flush(batch)
+	}
+}
+
 // Fallback answers one check on the reference engine (the SQL path of
 // check.(*Engine).SubjectIsAllowed, internal/check/engine.go:116-123): used for requests the GPU
-// leaves KETO_CHECK_UNDECIDED and when a batch fails as a whole (no device, snapshot gone).
+// leaves KETO_CHECK_UNDECIDED, when a batch fails as a whole (no device, snapshot gone) and for the
+// requests still queued when the batcher closes.
 type Fallback func(ctx context.Context, r *relationtuple.InternalRelationTuple, restDepth int) (bool, error)
 
-// Batcher coalesces concurrent SubjectIsAllowed calls (one goroutine per gRPC / REST request,
-// internal/check/handler.go:108,154,174) into keto_check_batch calls: a batch is flushed when
-// MaxBatch requests are queued or MaxWait after its first request, whichever comes first.
+// Batcher coalesces concurrent SubjectIsAllowed calls into keto_check_batch calls (defaults: 65,536
+// requests or 200 µs per batch).
 type Batcher struct {
 	mu        sync.RWMutex
 	snap      *Snapshot
 	GlobalMax func() int // config.ReadAPIMaxDepth (internal/driver/config/provider.go:143-145)
 	Fallback  Fallback
-	MaxBatch  int
-	MaxWait   time.Duration
-	queue     chan *pending
-	stop      chan struct{}
+	c         *coalescer
 }
 
-type pending struct {
-	ctx   context.Context
+type checkReq struct {
 	r     *relationtuple.InternalRelationTuple
 	depth int
-	done  chan result
 }
 
-type result struct {
-	allowed bool
-	err     error
-}
-
-// NewBatcher starts the flush loop.  Defaults: 65,536 requests or 200 µs per batch.
+// NewBatcher starts the flush loop.
 func NewBatcher(s *Snapshot, globalMax func() int, fb Fallback) *Batcher {
-	b := &Batcher{snap: s, GlobalMax: globalMax, Fallback: fb, MaxBatch: 1 << 16, MaxWait: 200 * time.Microsecond,
-		queue: make(chan *pending, 1<<16), stop: make(chan struct{})}
-	go b.loop()
+	b := &Batcher{snap: s, GlobalMax: globalMax, Fallback: fb}
+	b.c = newCoalescer(1<<16, 200*time.Microsecond, b.flush, b.fallbackAll)
 	return b
 }
 
-// Swap installs a new snapshot version (Apply / rebuild); batches already running keep theirs.
+// Swap installs a new snapshot version (a rebuild); it returns once no batch uses the old one.
 func (b *Batcher) Swap(s *Snapshot) *Snapshot {
 	b.mu.Lock()
 	defer b.mu.Unlock()
@@ -59,48 +166,28 @@ func (b *Batcher) Swap(s *Snapshot) *Snapshot {
 	return old
 }
 
-// Close stops the loop; queued requests are answered by the fallback.
-func (b *Batcher) Close() { close(b.stop) }
+// Close stops the loop; queued requests are answered by the fallback, later ones too.
+func (b *Batcher) Close() { b.c.close() }
 
 // Check = SubjectIsAllowed through the GPU batch path.
 func (b *Batcher) Check(ctx context.Context, r *relationtuple.InternalRelationTuple, restDepth int) (bool, error) {
-	p := &pending{ctx: ctx, r: r, depth: restDepth, done: make(chan result, 1)}
-	select {
-	case b.queue <- p:
-	case <-ctx.Done():
-		return false, ctx.Err()
-	case <-b.stop:
+	v, err := b.c.submit(ctx, checkReq{r, restDepth})
+	if errors.Is(err, ErrClosed) {
 		return b.Fallback(ctx, r, restDepth)
 	}
-	select {
-	case res := <-p.done:
-		return res.allowed, res.err
-	case <-ctx.Done():
-		return false, ctx.Err()
+	if err != nil {
+		return false, err
 	}
+	return v.(bool), nil
 }
 
-func (b *Batcher) loop() {
-	for {
-		var first *pending
-		select {
-		case first = <-b.queue:
-		case <-b.stop:
-			return
-		}
-		batch := []*pending{first}
-		timer := time.NewTimer(b.MaxWait)
-	fill:
-		for len(batch) < b.MaxBatch {
-			select {
-			case p := <-b.queue:
-				batch = append(batch, p)
-			case <-timer.C:
-				break fill
-			}
-		}
-		timer.Stop()
-		b.flush(batch)
+func (b *Batcher) fallbackAll(ps []*pending) {
+	for _, p := range ps {
+		go func(p *pending) {
+			q := p.req.(checkReq)
+			a, e := b.Fallback(p.ctx, q.r, q.depth)
+			p.done <- result{a, e}
+		}(p)
 	}
 }
 
@@ -108,21 +195,94 @@ func (b *Batcher) flush(batch []*pending) {
 	reqs := make([]*relationtuple.InternalRelationTuple, len(batch))
 	depths := make([]int, len(batch))
 	for i, p := range batch {
-		reqs[i], depths[i] = p.r, p.depth
+		q := p.req.(checkReq)
+		reqs[i], depths[i] = q.r, q.depth
 	}
 	b.mu.RLock()
 	allowed, status, err := b.snap.CheckBatch(reqs, depths, b.GlobalMax())
 	b.mu.RUnlock()
+	if err != nil {
+		b.fallbackAll(batch)
+		return
+	}
+	var undecided []*pending
 	for i, p := range batch {
-		if err != nil || status[i] == StatusUndecided {
-			// one request (or, on a batch error, each) goes to the reference engine on its own goroutine
-			go func(p *pending) {
-				a, e := b.Fallback(p.ctx, p.r, p.depth)
-				p.done <- result{a, e}
-			}(p)
+		if status[i] == StatusUndecided {
+			undecided = append(undecided, p) // this one request goes to the reference engine
 			continue
 		}
 		// StatusUnknownNamespace is allowed = false, nil like the reference (engine.go:98-100)
 		p.done <- result{allowed[i], nil}
+	}
+	b.fallbackAll(undecided)
+}
+
+// ExpandBatcher coalesces concurrent BuildTree calls into keto_expand_batch calls (defaults: 4,096
+// roots or 200 µs per batch).  Trees come back as pre-order Nodes; errors per root are ErrNotFound,
+// ErrUndecided, a wrapped ErrBatchFailed or ErrClosed (the last three: answer on the SQL engine).
+type ExpandBatcher struct {
+	mu        sync.RWMutex
+	snap      *Snapshot
+	GlobalMax func() int
+	c         *coalescer
+}
+
+type expandReq struct {
+	sub   relationtuple.Subject
+	depth int
+}
+
+// NewExpandBatcher starts the flush loop.
+func NewExpandBatcher(s *Snapshot, globalMax func() int) *ExpandBatcher {
+	b := &ExpandBatcher{snap: s, GlobalMax: globalMax}
+	b.c = newCoalescer(1<<12, 200*time.Microsecond, b.flush, func(ps []*pending) {
+		for _, p := range ps {
+			p.done <- result{nil, ErrClosed}
+		}
+	})
+	return b
+}
+
+// Swap installs a new snapshot version; it returns once no batch uses the old one.
+func (b *ExpandBatcher) Swap(s *Snapshot) *Snapshot {
+	b.mu.Lock()
+	defer b.mu.Unlock()
+	old := b.snap
+	b.snap = s
+	return old
+}
+
+// Close stops the loop; queued and later requests get ErrClosed.
+func (b *ExpandBatcher) Close() { b.c.close() }
+
+// Expand = BuildTree through the GPU batch path: root's nodes in pre-order (nil: a nil tree).
+func (b *ExpandBatcher) Expand(ctx context.Context, sub relationtuple.Subject, restDepth int) ([]Node, error) {
+	v, err := b.c.submit(ctx, expandReq{sub, restDepth})
+	if err != nil {
+		return nil, err
+	}
+	nodes, _ := v.([]Node)
+	return nodes, nil
+}
+
+func (b *ExpandBatcher) flush(batch []*pending) {
+	subs := make([]relationtuple.Subject, len(batch))
+	depths := make([]int, len(batch))
+	for i, p := range batch {
+		q := p.req.(expandReq)
+		subs[i], depths[i] = q.sub, q.depth
+	}
+	b.mu.RLock()
+	trees, errs, err := b.snap.ExpandBatch(subs, depths, b.GlobalMax())
+	b.mu.RUnlock()
+	for i, p := range batch {
+		switch {
+		case err != nil:
+			p.done <- result{nil, fmt.Errorf("%w: %v", ErrBatchFailed, err)}
+		case errs[i] != nil:
+			p.done <- result{nil, errs[i]}
+		default:
+			p.done <- result{trees[i], nil}
+		}
 	}
 }

@@ -24,10 +24,13 @@ import (
 	"fmt"
 	"unsafe"
 
-	"github.com/ory/keto/internal/expand"
 	"github.com/ory/keto/internal/namespace"
 	"github.com/ory/keto/internal/relationtuple"
 )
+
+// This package must not import internal/expand, internal/check or internal/driver: those import it
+// (engine_gpu.go, registry_gpu.go).  Trees therefore come back as pre-order Nodes, and
+// internal/expand builds its *Tree values from them.
 
 // Decision statuses of CheckBatch (KETO_CHECK_*).
 const (
@@ -247,9 +250,19 @@ func (s *Snapshot) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depth
 	return out, st, nil
 }
 
+// Node is one node of an expand tree in pre-order (keto_tree_node): a leaf, or a union whose next
+// Children subtrees follow it (internal/expand/tree.go:26-30; only union and leaf are produced).
+type Node struct {
+	Leaf     bool
+	Children int
+	Subject  relationtuple.Subject
+}
+
 // ExpandBatch = expand.(*Engine).BuildTree (internal/expand/engine.go:33-102) for many roots.
-// trees[i] is nil for a nil tree (JSON null); errs[i] is ErrNotFound / ErrUndecided per root.
-func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([]*expand.Tree, []error, error) {
+// trees[i] holds root i's nodes in pre-order (nil for a nil tree, JSON null); errs[i] is ErrNotFound /
+// ErrUndecided per root.  Subjects are built from the node arena and keto_subject_fields: no text
+// codec on the way.
+func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([][]Node, []error, error) {
 	n := len(subs)
 	if n == 0 {
 		return nil, nil, nil
@@ -274,20 +287,13 @@ func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globa
 		return nil, nil, lastErr(rc)
 	}
 	defer C.keto_tree_arena_free(a)
-	// every tree's JSON in one buffer (keto_tree_json_all, host threads): size, then fill
-	offs := (*C.uint64_t)(m.alloc((n + 1) * 8))
-	jsonLen := C.keto_tree_json_all(s.h, a, nil, 0, offs)
-	if jsonLen < 0 {
-		return nil, nil, lastErr(C.int(jsonLen))
-	}
-	buf := (*C.char)(m.alloc(int(jsonLen) + 1))
-	if rc := C.keto_tree_json_all(s.h, a, buf, C.uint64_t(jsonLen), offs); rc != jsonLen {
-		return nil, nil, lastErr(C.int(rc))
-	}
-	text := C.GoBytes(unsafe.Pointer(buf), C.int(jsonLen))
-	off := unsafe.Slice(offs, n+1)
-	trees := make([]*expand.Tree, n)
+
+	// the arena's nodes, tree by tree, and every distinct subject reference they hold
+	type span struct{ nodes []C.keto_tree_node }
+	spans := make([]span, n)
 	errs := make([]error, n)
+	refIdx := make(map[uint32]int)
+	var refs []uint32
 	for i := 0; i < n; i++ {
 		switch C.keto_tree_status(a, C.uint32_t(i)) {
 		case C.KETO_EXPAND_NIL:
@@ -299,11 +305,84 @@ func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globa
 			errs[i] = ErrUndecided
 			continue
 		}
-		t := &expand.Tree{}
-		if err := t.UnmarshalJSON(text[off[i]:off[i+1]]); err != nil {
-			return nil, nil, err
+		var nn C.uint64_t
+		p := C.keto_tree_nodes(a, C.uint32_t(i), &nn)
+		if p == nil || nn == 0 {
+			continue
 		}
-		trees[i] = t
+		nodes := unsafe.Slice(p, int(nn)) // arena memory: read before keto_tree_arena_free
+		spans[i].nodes = nodes
+		for _, x := range nodes {
+			ref := uint32(x.subject)
+			if _, ok := refIdx[ref]; !ok {
+				refIdx[ref] = len(refs)
+				refs = append(refs, ref)
+			}
+		}
+	}
+	subjects, err := s.subjects(a, refs, &m)
+	if err != nil {
+		return nil, nil, err
+	}
+	trees := make([][]Node, n)
+	for i := range spans {
+		if spans[i].nodes == nil {
+			continue
+		}
+		out := make([]Node, len(spans[i].nodes))
+		for k, x := range spans[i].nodes {
+			info := uint32(x.info)
+			out[k] = Node{Leaf: info&0x80000000 != 0, Children: int(info & 0x7FFFFFFF),
+				Subject: subjects[refIdx[uint32(x.subject)]]}
+		}
+		trees[i] = out
 	}
 	return trees, errs, nil
+}
+
+// subjects resolves subject references of arena a (keto_tree_node.subject) to Subjects with one
+// keto_subject_fields sizing call and one filling call; a reference's strings never change, so the
+// pair agrees even if a write lands in between (the fill is retried on a larger total regardless).
+func (s *Snapshot) subjects(a *C.keto_tree_arena, refs []uint32, m *cmem) ([]relationtuple.Subject, error) {
+	k := len(refs)
+	if k == 0 {
+		return nil, nil
+	}
+	cref := (*C.uint32_t)(m.alloc(k * 4))
+	copy(unsafe.Slice((*uint32)(unsafe.Pointer(cref)), k), refs)
+	lens := (*C.uint32_t)(m.alloc(3 * k * 4))
+	total := C.keto_subject_fields(s.h, a, cref, C.uint64_t(k), nil, 0, lens)
+	for {
+		if total < 0 {
+			return nil, lastErr(C.int(total))
+		}
+		buf := (*C.char)(m.alloc(int(total) + 1))
+		got := C.keto_subject_fields(s.h, a, cref, C.uint64_t(k), buf, C.uint64_t(total), lens)
+		if got < 0 {
+			return nil, lastErr(C.int(got))
+		}
+		if got > total { // cannot happen (see above); size again rather than misread
+			total = got
+			continue
+		}
+		text := C.GoStringN(buf, C.int(got)) // one Go string; the fields are substrings of it
+		ls := unsafe.Slice((*uint32)(unsafe.Pointer(lens)), 3*k)
+		out := make([]relationtuple.Subject, k)
+		at := 0
+		take := func(n uint32) string {
+			v := text[at : at+int(n)]
+			at += int(n)
+			return v
+		}
+		for i, ref := range refs {
+			if ref&0x80000000 == 0 {
+				out[i] = &relationtuple.SubjectID{ID: take(ls[3*i])}
+				continue
+			}
+			ns := take(ls[3*i])
+			obj := take(ls[3*i+1])
+			out[i] = &relationtuple.SubjectSet{Namespace: ns, Object: obj, Relation: take(ls[3*i+2])}
+		}
+		return out, nil
+	}
 }

@@ -36,7 +36,7 @@ EXPORTS = [
     "keto_check_steps_device", "keto_snapshot_part_stats", "keto_snapshot_apply", "keto_snapshot_version",
     "keto_snapshot_upload_part_mode", "keto_snapshot_part_stats_mode", "keto_part_stubs", "keto_part_filters",
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
-    "keto_tree_proto_all_device", "keto_tree_json_all",
+    "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -102,7 +102,7 @@ class KOpts(C.Structure):
 
 class KTiming(C.Structure):
     _fields_ = [("tier_ms", C.c_float * 3), ("requests", C.c_uint32 * 3), ("undecided", C.c_uint32),
-                ("chunks", C.c_uint32), ("wall_ms", C.c_float)]
+                ("chunks", C.c_uint32), ("wall_ms", C.c_float), ("resolve_ms", C.c_float)]
 
 
 class KPartStats(C.Structure):
@@ -157,6 +157,7 @@ def load():
     lib.keto_tree_proto_all_device.restype = C.c_int64
     lib.keto_tree_json_all.restype = C.c_int64
     lib.keto_subject_string.restype = C.c_int64
+    lib.keto_subject_fields.restype = C.c_int64
     lib.keto_route_work_bytes.restype = C.c_uint64
     lib.keto_snapshot_version.restype = C.c_uint64
     lib.keto_part_stubs.restype = C.c_int64
@@ -387,7 +388,9 @@ class Snapshot:
         return out
 
     @classmethod
-    def from_csr(cls, namespaces, row_ns, row_obj, row_rel, row_ptr, edges, strings=None, page_size=100, device=0):
+    def from_csr(cls, namespaces, row_ns, row_obj, row_rel, row_ptr, edges, strings=None, page_size=100, device=0,
+                 kstrs=None):
+        """kstrs: (KStr array, n) string table already in C memory (large graphs), instead of strings."""
         lib = load()
         keep = _Keep()
         ns = (KNamespace * max(1, len(namespaces)))(*[KNamespace(i, keep.s(n)) for i, n in namespaces])
@@ -401,6 +404,8 @@ class Snapshot:
         if strings is not None:
             strs = (KStr * max(1, len(strings)))(*[keep.s(x) for x in strings])
             n_str = len(strings)
+        elif kstrs is not None:
+            strs, n_str = kstrs
         h = C.c_void_p()
         opts = KOpts(page_size, device, 0)
         p = lambda a: a.ctypes.data_as(C.c_void_p)
@@ -443,6 +448,14 @@ class Snapshot:
         _check(self.lib.keto_check_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth),
                                          allowed.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
         return allowed[:n], status[:n]
+
+    def resolve_checks_reqs(self, arr, n: int):
+        """keto_resolve_checks on a prepared KCheckReq array: (device-form requests, statuses)."""
+        out = np.zeros(max(1, n), dtype=CHECK_IDS_DTYPE)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_resolve_checks(self.h, arr, C.c_uint32(n), out.ctypes.data_as(C.c_void_p),
+                                            status.ctypes.data_as(C.c_void_p)))
+        return out[:n], status[:n]
 
     def resolve_checks(self, reqs):
         keep = _Keep()
@@ -517,7 +530,7 @@ class Snapshot:
         t = KTiming()
         _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
         return {"tier_ms": list(t.tier_ms), "requests": list(t.requests), "undecided": t.undecided,
-                "chunks": t.chunks, "wall_ms": t.wall_ms}
+                "chunks": t.chunks, "wall_ms": t.wall_ms, "resolve_ms": t.resolve_ms}
 
     @staticmethod
     def check_kernel_name(global_max_depth=5) -> str:
@@ -609,12 +622,62 @@ class Snapshot:
         raw = blob.raw[:total]
         return [raw[int(offs[i]):int(offs[i + 1])].decode() for i in range(n)]
 
+    def subject_fields(self, refs, arena=None):
+        """keto_subject_fields: per subject reference ("id", id) or ("set", namespace, object, relation)."""
+        refs = np.ascontiguousarray(refs, dtype=np.uint32)
+        n = len(refs)
+        lens = np.zeros(max(1, 3 * n), dtype=np.uint32)
+        a = arena if arena is not None else None
+        total = self.lib.keto_subject_fields(self.h, a, refs.ctypes.data_as(C.c_void_p), C.c_uint64(n), None,
+                                             C.c_uint64(0), lens.ctypes.data_as(C.c_void_p))
+        _check(min(0, total))
+        buf = C.create_string_buffer(max(1, total))
+        got = self.lib.keto_subject_fields(self.h, a, refs.ctypes.data_as(C.c_void_p), C.c_uint64(n), buf,
+                                           C.c_uint64(total), lens.ctypes.data_as(C.c_void_p))
+        _check(min(0, got))
+        raw, at, out = buf.raw[:total], 0, []
+        for i in range(n):
+            parts = []
+            for k in range(3 if refs[i] & 0x80000000 else 1):
+                ln = int(lens[3 * i + k])
+                parts.append(raw[at:at + ln].decode())
+                at += ln
+            out.append(("set", *parts) if refs[i] & 0x80000000 else ("id", parts[0]))
+        return out
+
+    def _tree_via_fields(self, a, i):
+        """Tree i as the Go shim builds expand.Tree: pre-order nodes (keto_tree_nodes) + their subjects'
+        fields (keto_subject_fields), as Tree.MarshalJSON's structure (a dict)."""
+        nn = C.c_uint64()
+        ptr = self.lib.keto_tree_nodes(a, C.c_uint32(i), C.byref(nn))
+        nodes = [(ptr[j].subject, ptr[j].info) for j in range(nn.value)]
+        fields = self.subject_fields([x for x, _ in nodes], arena=a) if nodes else []
+        root, stack = None, []
+        for (subj_ref, info), f in zip(nodes, fields):
+            leaf = bool(info & 0x80000000)
+            t = {"type": "leaf" if leaf else "union"}
+            if f[0] == "id":
+                t["subject_id"] = f[1]
+            else:
+                t["subject_set"] = {"namespace": f[1], "object": f[2], "relation": f[3]}
+            if stack:
+                stack[-1][0].setdefault("children", []).append(t)
+                stack[-1][1] -= 1
+            else:
+                root = t
+            if not leaf and info & 0x7FFFFFFF:
+                stack.append([t, info & 0x7FFFFFFF])
+            while stack and stack[-1][1] == 0:
+                stack.pop()
+        return root
+
     def expand_batch(self, reqs, global_max_depth=5, want_nodes=False, want_proto=False, proto_all=None,
-                     json_all=False):
+                     json_all=False, via_fields=False):
         """reqs: list of (subject, max_depth). Returns list of (status, json_or_None[, nodes][, proto]);
         proto_all = "host" / "device": also every tree's bytes from keto_tree_proto_all[_device]
         (returned as (list, per-tree bytes list)); json_all: also every tree's JSON text from
-        keto_tree_json_all (returned as (list, per-tree text list))."""
+        keto_tree_json_all (returned as (list, per-tree text list)); via_fields: also each tree rebuilt
+        from its nodes and keto_subject_fields (the Go shim's path), as a dict."""
         keep = _Keep()
         n = len(reqs)
         arr = (KExpandReq * max(1, n))()
@@ -634,6 +697,8 @@ class Snapshot:
                     self.lib.keto_tree_json(self.h, a, C.c_uint32(i), buf, C.c_uint64(ln + 1))
                     js = json.loads(buf.raw[:ln].decode())
                 item = (st, js)
+                if via_fields:
+                    item = item + (self._tree_via_fields(a, i) if st == EXPAND_TREE else None,)
                 if want_nodes:
                     nn = C.c_uint64()
                     ptr = self.lib.keto_tree_nodes(a, C.c_uint32(i), C.byref(nn))

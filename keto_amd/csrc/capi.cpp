@@ -3,6 +3,7 @@
 // device engine, and the expand tree arena with its JSON codec (internal/expand/tree.go:85-163).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -318,31 +319,22 @@ int64_t copy_out(const std::string& s, char* buf, uint64_t cap) {
     return (int64_t)s.size();
 }
 
-// RelationQuery of a check request / of a subject set; see Snapshot::resolve_query
-keto_check_ids resolve_one(const Snapshot& S, const keto_check_req& q, uint8_t& status, bool& wild, RowKey& wkey) {
-    keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0, q.max_depth};
-    status = KETO_CHECK_OK;
-    wild = false;
-    int64_t row = S.resolve_query(sv(q.namespace_), sv(q.object), sv(q.relation), &wkey);
-    if (row == -2) status = KETO_CHECK_UNKNOWN_NAMESPACE;
-    else if (row == -3) wild = true;
-    else if (row >= 0) {
-        if (!S.present((uint32_t)row))
-            throw Error{KETO_E_INVALID, "the request's row is a root row owned by part " +
-                                            std::to_string(S.root_owner((uint32_t)row, S.n_parts)) + " (keto_row_owner)"};
-        r.row = S.handle((uint32_t)row);
-    }
-    if (q.subject.kind == 0) {
-        int64_t sid = S.lookup_str(sv(q.subject.id));
-        if (sid >= 0) r.target = (uint32_t)sid;
-    } else {
-        int64_t t = S.resolve_query(sv(q.subject.set_namespace), sv(q.subject.set_object), sv(q.subject.set_relation));
-        if (t >= 0) {
-            r.target = S.handle((uint32_t)t);
-            r.flags = 1;
+// resolve_checks over a whole batch on host threads (the first error wins)
+void resolve_all(const Snapshot& S, const keto_check_req* reqs, uint32_t n, keto_check_ids* ids, uint8_t* st,
+                 uint8_t* wild, RowKey* wkey) {
+    std::atomic<bool> failed{false};
+    Error first{KETO_OK, ""};
+    std::mutex emu;
+    par_chunks(n, n >= 65536 ? build_threads() : 1u, 4096, [&](uint64_t b, uint64_t e, unsigned) {
+        if (failed) return;
+        try {
+            resolve_checks(S, reqs, b, e, ids, st, wild, wkey);
+        } catch (const Error& x) {
+            std::lock_guard<std::mutex> lk(emu);
+            if (!failed.exchange(true)) first = x;
         }
-    }
-    return r;
+    });
+    if (failed) throw first;
 }
 
 }  // namespace
@@ -410,15 +402,14 @@ int keto_resolve_checks(const keto_snapshot* h, const keto_check_req* reqs, uint
     return guarded([&] {
         if (!h || (n && (!reqs || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
         std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::vector<uint8_t> st(n), wild(n);
+        std::vector<RowKey> wkey(n);
+        resolve_all(*h->s, reqs, n, out, st.data(), wild.data(), wkey.data());
         for (uint32_t i = 0; i < n; ++i) {
-            uint8_t st;
-            bool wild;
-            RowKey k;
-            out[i] = resolve_one(*h->s, reqs[i], st, wild, k);
-            if (wild) throw Error{KETO_E_INVALID, "request " + std::to_string(i) +
-                                                      " is a wildcard query that no stored subject set uses; "
-                                                      "pass it to keto_check_batch"};
-            if (status_out) status_out[i] = st;
+            if (wild[i]) throw Error{KETO_E_INVALID, "request " + std::to_string(i) +
+                                                         " is a wildcard query that no stored subject set uses; "
+                                                         "pass it to keto_check_batch"};
+            if (status_out) status_out[i] = st[i];
         }
         return KETO_OK;
     });
@@ -430,6 +421,7 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
         std::shared_lock<std::shared_mutex> lk(h->s->rw);
         Snapshot& S = *h->s;
+        const auto t0 = std::chrono::steady_clock::now();
         std::vector<keto_check_ids> ids(n);
         Overlay ov;
         ov.base = S.n_rows();
@@ -437,26 +429,12 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
         // batch-local overlay row are materialized afterwards, in request order
         std::vector<uint8_t> st(n), wild(n);
         std::vector<RowKey> wkey(n);
-        std::atomic<bool> failed{false};
-        Error first{KETO_OK, ""};
-        std::mutex emu;
-        par_chunks(n, n >= 65536 ? build_threads() : 1u, 4096, [&](uint64_t b, uint64_t e, unsigned) {
-            for (uint64_t i = b; i < e && !failed; ++i) {
-                try {
-                    bool w;
-                    ids[i] = resolve_one(S, reqs[i], st[i], w, wkey[i]);
-                    wild[i] = w;
-                } catch (const Error& x) {
-                    std::lock_guard<std::mutex> lk(emu);
-                    if (!failed.exchange(true)) first = x;
-                }
-            }
-        });
-        if (failed) throw first;
+        resolve_all(S, reqs, n, ids.data(), st.data(), wild.data(), wkey.data());
         for (uint32_t i = 0; i < n; ++i) {
             if (wild[i]) ids[i].row = handle_of(S, &ov, overlay_row(S, ov, wkey[i]));
             if (status_out) status_out[i] = st[i];
         }
+        S.last_resolve_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
         device_check_host(S, ids.data(), n, global_max_depth, allowed_out, FORM_HANDLES, 0, &ov);
         if (status_out)
             for (uint32_t i = 0; i < n; ++i)
@@ -537,6 +515,7 @@ int keto_last_batch_timing(const keto_snapshot* h, keto_batch_timing* out) {
     return guarded([&] {
         if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
         *out = device_last_timing(*h->s);
+        out->resolve_ms = h->s->last_resolve_ms;
         return KETO_OK;
     });
 }
@@ -889,24 +868,24 @@ const keto_tree_node* keto_tree_nodes(const keto_tree_arena* a, uint32_t i, uint
     return a->r.nodes.data() + b;
 }
 
+// The tree encoders read the snapshot's strings and row keys, which keto_snapshot_apply extends
+// (push_back may reallocate): they hold the snapshot's lock shared, like the batch calls.
 int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_t i, char* buf, uint64_t cap) {
-    if (!h || !a || i >= a->r.status.size()) return KETO_E_INVALID;
-    std::string o;
-    if (a->r.status[i] == KETO_EXPAND_NOT_FOUND) {
-        g_err = "Unknown namespace";
-        return KETO_E_INVALID;
-    }
-    if (a->r.status[i] == KETO_EXPAND_UNDECIDED) {
-        g_err = "the tree exceeds the engine's limits (KETO_EXPAND_UNDECIDED)";
-        return KETO_E_RANGE;
-    }
-    if (a->r.status[i] != KETO_EXPAND_TREE) {
-        o = "null";
-    } else {
-        const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
-        tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
-    }
-    return copy_out(o, buf, cap);
+    return guarded([&]() -> int64_t {
+        if (!h || !a || i >= a->r.status.size()) throw Error{KETO_E_INVALID, "bad argument"};
+        if (a->r.status[i] == KETO_EXPAND_NOT_FOUND) throw Error{KETO_E_INVALID, "Unknown namespace"};
+        if (a->r.status[i] == KETO_EXPAND_UNDECIDED)
+            throw Error{KETO_E_RANGE, "the tree exceeds the engine's limits (KETO_EXPAND_UNDECIDED)"};
+        std::string o;
+        if (a->r.status[i] != KETO_EXPAND_TREE) {
+            o = "null";
+        } else {
+            std::shared_lock<std::shared_mutex> lk(h->s->rw);
+            const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+            tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
+        }
+        return copy_out(o, buf, cap);
+    });
 }
 
 extern "C++" {
@@ -918,6 +897,7 @@ int64_t encode_all(const keto_snapshot* h, const keto_tree_arena* a, int kind, c
                    uint64_t* offsets, One one) {
     const uint32_t n = (uint32_t)a->r.status.size();
     const unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::shared_lock<std::shared_mutex> rlk(h->s->rw);      // before enc_mu: apply takes rw alone
     std::lock_guard<std::mutex> lk(a->enc_mu);
     std::vector<std::string>& enc = a->enc;
     if (!(a->enc_kind == kind && a->enc_snap == h && a->enc_version == h->s->version && enc.size() == n)) {
@@ -954,41 +934,48 @@ int64_t encode_all(const keto_snapshot* h, const keto_tree_arena* a, int kind, c
 
 int64_t keto_tree_json_all(const keto_snapshot* h, const keto_tree_arena* a, char* buf, uint64_t cap,
                            uint64_t* offsets) {
-    if (!h || !a || !offsets) return KETO_E_INVALID;
-    return encode_all(h, a, 1, buf, cap, offsets, [&](uint32_t i, std::string& o) {
-        const int st = a->r.status[i];
-        if (st == KETO_EXPAND_TREE) {
-            const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
-            tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
-        } else if (st != KETO_EXPAND_NOT_FOUND && st != KETO_EXPAND_UNDECIDED) {
-            o = "null";
-        }
+    return guarded([&]() -> int64_t {
+        if (!h || !a || !offsets) throw Error{KETO_E_INVALID, "NULL argument"};
+        return encode_all(h, a, 1, buf, cap, offsets, [&](uint32_t i, std::string& o) {
+            const int st = a->r.status[i];
+            if (st == KETO_EXPAND_TREE) {
+                const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+                tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
+            } else if (st != KETO_EXPAND_NOT_FOUND && st != KETO_EXPAND_UNDECIDED) {
+                o = "null";
+            }
+        });
     });
 }
 
 int64_t keto_tree_proto(const keto_snapshot* h, const keto_tree_arena* a, uint32_t i, uint8_t* buf, uint64_t cap) {
-    if (!h || !a || i >= a->r.status.size()) return KETO_E_INVALID;
-    const int st = a->r.status[i];
-    if (st == KETO_EXPAND_NOT_FOUND || st == KETO_EXPAND_UNDECIDED) {
-        g_err = st == KETO_EXPAND_NOT_FOUND ? "Unknown namespace" : "the tree exceeds the engine's limits";
-        return st == KETO_EXPAND_NOT_FOUND ? KETO_E_INVALID : KETO_E_RANGE;
-    }
-    if (st != KETO_EXPAND_TREE) return 0;                         // nil tree: no message
-    std::string o;
-    const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
-    tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
-    if (buf && cap) std::memcpy(buf, o.data(), std::min<uint64_t>(cap, o.size()));
-    return (int64_t)o.size();
+    return guarded([&]() -> int64_t {
+        if (!h || !a || i >= a->r.status.size()) throw Error{KETO_E_INVALID, "bad argument"};
+        const int st = a->r.status[i];
+        if (st == KETO_EXPAND_NOT_FOUND) throw Error{KETO_E_INVALID, "Unknown namespace"};
+        if (st == KETO_EXPAND_UNDECIDED) throw Error{KETO_E_RANGE, "the tree exceeds the engine's limits"};
+        if (st != KETO_EXPAND_TREE) return 0;                     // nil tree: no message
+        std::string o;
+        {
+            std::shared_lock<std::shared_mutex> lk(h->s->rw);
+            const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+            tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
+        }
+        if (buf && cap) std::memcpy(buf, o.data(), std::min<uint64_t>(cap, o.size()));
+        return (int64_t)o.size();
+    });
 }
 
 int64_t keto_tree_proto_all(const keto_snapshot* h, const keto_tree_arena* a, uint8_t* buf, uint64_t cap,
                             uint64_t* offsets) {
-    if (!h || !a || !offsets) return KETO_E_INVALID;
-    return encode_all(h, a, 2, reinterpret_cast<char*>(buf), cap, offsets, [&](uint32_t i, std::string& o) {
-        if (a->r.status[i] == KETO_EXPAND_TREE) {
-            const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
-            tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
-        }
+    return guarded([&]() -> int64_t {
+        if (!h || !a || !offsets) throw Error{KETO_E_INVALID, "NULL argument"};
+        return encode_all(h, a, 2, reinterpret_cast<char*>(buf), cap, offsets, [&](uint32_t i, std::string& o) {
+            if (a->r.status[i] == KETO_EXPAND_TREE) {
+                const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
+                tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
+            }
+        });
     });
 }
 
@@ -996,6 +983,7 @@ int64_t keto_tree_proto_all_device(keto_snapshot* h, const keto_tree_arena* a, u
                                    uint64_t* offsets) {
     return guarded([&]() -> int64_t {
         if (!h || !a || !offsets) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> rlk(h->s->rw);    // strings / row keys (before S.mu)
         const uint32_t n = (uint32_t)a->r.status.size();
         // the nodes of the trees (other statuses have none), tree t = [toff[t], toff[t + 1])
         std::vector<uint64_t> toff(n + 1, 0);
@@ -1024,10 +1012,58 @@ int64_t keto_tree_proto_all_device(keto_snapshot* h, const keto_tree_arena* a, u
     });
 }
 
+int64_t keto_subject_fields(const keto_snapshot* h, const keto_tree_arena* a, const uint32_t* subjects, uint64_t n,
+                            char* buf, uint64_t cap, uint32_t* lens_out) {
+    return guarded([&]() -> int64_t {
+        if (!h || (n && (!subjects || !lens_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        const Snapshot& S = *h->s;
+        uint64_t total = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t ref = subjects[i];
+            if ((ref & EDGE_SET) && (ref & EDGE_VAL) >= S.n_rows() &&
+                !(a && (ref & EDGE_VAL) >= a->ov_base && (ref & EDGE_VAL) - a->ov_base < a->ov_keys.size()))
+                throw Error{KETO_E_INVALID, "subject reference " + std::to_string(i) + " names no row"};
+            const SubjectViews f = views_of(S, a, ref);
+            if (!f.set) {
+                lens_out[3 * i] = (uint32_t)f.id.size();
+                lens_out[3 * i + 1] = lens_out[3 * i + 2] = 0;
+                total += f.id.size();
+            } else {
+                lens_out[3 * i] = (uint32_t)f.ns.size();
+                lens_out[3 * i + 1] = (uint32_t)f.obj.size();
+                lens_out[3 * i + 2] = (uint32_t)f.rel.size();
+                total += f.ns.size() + f.obj.size() + f.rel.size();
+            }
+        }
+        if (buf && cap >= total) {
+            char* p = buf;
+            auto put = [&](std::string_view v) {
+                std::memcpy(p, v.data(), v.size());
+                p += v.size();
+            };
+            for (uint64_t i = 0; i < n; ++i) {
+                const SubjectViews f = views_of(S, a, subjects[i]);
+                if (!f.set) {
+                    put(f.id);
+                } else {
+                    put(f.ns);
+                    put(f.obj);
+                    put(f.rel);
+                }
+            }
+        }
+        return (int64_t)total;
+    });
+}
+
 int64_t keto_subject_string(const keto_snapshot* h, uint32_t subject, char* buf, uint64_t cap) {
-    if (!h) return KETO_E_INVALID;
-    SubjectFields f = fields_of(*h->s, nullptr, subject);
-    return copy_out(f.set ? f.ns + ":" + f.obj + "#" + f.rel : f.id, buf, cap);
+    return guarded([&]() -> int64_t {
+        if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        SubjectFields f = fields_of(*h->s, nullptr, subject);
+        return copy_out(f.set ? f.ns + ":" + f.obj + "#" + f.rel : f.id, buf, cap);
+    });
 }
 
 }  // extern "C"

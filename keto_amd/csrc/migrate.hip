@@ -49,6 +49,7 @@ namespace keto {
 namespace {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint64_t MAX_ROUND_RECORDS = 1ull << 28;   // record counts are 28-bit fields of the grouping cursors
 constexpr uint32_t HEAD_WORDS = 8;
 constexpr uint32_t K_ENTER = 0, K_RESUME = 1, K_DECISION = 2;
 constexpr uint32_t F_SEQ = 1, F_TOP = 2;            // frame flags
@@ -961,6 +962,9 @@ void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gm
     hipStream_t st = (hipStream_t)stream;
     if (gmd > 65535) gmd = 65535;
     if (n && (!d_reqs || !d_allowed)) throw Error{KETO_E_INVALID, "NULL argument"};
+    // the grouping packs a destination's record count into 28 bits (records << 36 | units); a round
+    // emits at most one record per input, so capping the inputs caps every count
+    if (n >= MAX_ROUND_RECORDS) throw Error{KETO_E_RANGE, "a migrating batch holds fewer than 2^28 requests"};
     M.allowed = d_allowed;
     M.n = n;
     M.gmd = gmd;
@@ -998,7 +1002,7 @@ void mig_round(Snapshot& S, const void* d_in, const uint32_t* d_in_off, const ui
     hipStream_t st = (hipStream_t)stream;
     uint64_t n_in = 0;
     for (uint32_t s = 0; s < S.n_parts; ++s) n_in += in_records[s];
-    if (n_in > 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "too many records in one round"};
+    if (n_in >= MAX_ROUND_RECORDS) throw Error{KETO_E_RANGE, "a round takes fewer than 2^28 records"};
     if (n_in && (!d_in || !d_in_off)) throw Error{KETO_E_INVALID, "NULL argument"};
     run_round(S, M, static_cast<const uint32_t*>(d_in), d_in_off, (uint32_t)n_in, in_records, in_units, S.n_parts, st,
               out);

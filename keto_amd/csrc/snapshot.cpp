@@ -56,6 +56,7 @@ void load_namespaces(Snapshot& S, const keto_namespace* ns, uint32_t n_ns) {
         S.ns_ids.push_back(ns[i].id);
         S.ns_names.push_back(std::move(name));
     }
+    for (uint32_t i = 0; i < (uint32_t)S.ns_names.size(); ++i) S.ns_view.emplace(S.ns_names[i], (int)i);
 }
 
 // Sharded parallel interning of the tuple table's strings (objects, relations, subject ids, subject-set
@@ -255,16 +256,6 @@ void finalize_rows(Snapshot& S, const std::vector<uint64_t>& row_ptr, const std:
 
 }  // namespace
 
-int64_t Snapshot::lookup_str(std::string_view s) const {
-    const auto end = strs.begin() + n_sorted_strs;
-    auto it = std::lower_bound(strs.begin(), end, s,
-                               [](const std::string& a, std::string_view b) { return std::string_view(a) < b; });
-    if (it != end && std::string_view(*it) == s) return it - strs.begin();
-    if (added_str.empty()) return -1;
-    auto f = added_str.find(std::string(s));
-    return f == added_str.end() ? -1 : (int64_t)f->second;
-}
-
 int Snapshot::key_cmp_bytes(const RowKey& a, const RowKey& b) const {
     if (a.ns != b.ns) return a.ns < b.ns ? -1 : 1;
     if (a.obj != b.obj) return str_cmp(a.obj, b.obj);
@@ -299,45 +290,6 @@ int Snapshot::str_cmp(uint32_t a, uint32_t b) const {
     if (a < n_sorted_strs && b < n_sorted_strs) return a < b ? -1 : 1;
     const int c = strs[a].compare(strs[b]);
     return c < 0 ? -1 : c > 0 ? 1 : 0;
-}
-
-int64_t Snapshot::resolve_query(std::string_view ns, std::string_view obj, std::string_view rel,
-                                RowKey* key_out) const {
-    RowKey k;
-    if (ns.empty()) {
-        k.ns = ANY_NS;
-    } else {
-        auto it = ns_by_name.find(std::string(ns));
-        if (it == ns_by_name.end()) return -2;                                   // ErrNotFound
-        k.ns = ns_ids[it->second];
-    }
-    if (obj.empty()) k.obj = ANY;
-    else {
-        int64_t o = lookup_str(obj);
-        if (o < 0) return -1;          // no row can match an unknown string
-        k.obj = (uint32_t)o;
-    }
-    if (rel.empty()) k.rel = ANY;
-    else {
-        int64_t r = lookup_str(rel);
-        if (r < 0) return -1;
-        k.rel = (uint32_t)r;
-    }
-    if (key_out) *key_out = k;
-    if (k.ns != ANY_NS && k.obj != ANY && k.rel != ANY) {
-        // real rows are sorted: binary search
-        uint32_t lo = 0, hi = n_real_rows;
-        while (lo < hi) {
-            uint32_t m = lo + (hi - lo) / 2;
-            int64_t c = key_cmp(row_key[m], k);
-            if (c == 0) return m;
-            if (c < 0) lo = m + 1; else hi = m;
-        }
-    }
-    auto it = row_of.find(k);
-    if (it != row_of.end()) return it->second;
-    if (k.ns == ANY_NS || k.obj == ANY || k.rel == ANY) return -3;
-    return -1;
 }
 
 uint32_t Snapshot::vid_of_key(const std::string& key) const {
@@ -863,10 +815,12 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
     if (n_rows >= EDGE_VAL) throw Error{KETO_E_RANGE, "more than 2^31-1 rows"};
     if (strings) {
         S.strs.resize(n_strings);
-        for (uint32_t i = 0; i < n_strings; ++i) S.strs[i] = std::string(sv(strings[i]));
+        par_chunks(n_strings, n_strings >= par_min() ? build_threads() : 1u, 1 << 14,
+                   [&](uint64_t b, uint64_t e, unsigned) {
+                       for (uint64_t i = b; i < e; ++i) S.strs[i] = std::string(sv(strings[i]));
+                   });
         S.n_sorted_strs = n_strings;
-        int64_t e = S.lookup_str("");
-        S.empty_str = e < 0 ? ANY : (uint32_t)e;
+        S.empty_str = n_strings && S.strs[0].empty() ? 0u : ANY;      // "" sorts first
     }
     S.row_key.resize(n_rows);
     for (uint32_t r = 0; r < n_rows; ++r) {

@@ -13,6 +13,7 @@
 // walked edge by edge with full visited semantics.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -257,6 +258,8 @@ struct Snapshot {
     // rows a (wildcard) RelationQuery k returns, in the reference ORDER BY (relationtuples.go:250)
     std::vector<uint32_t> rows_in_key_order(const RowKey& k) const;
 
+    std::atomic<float> last_resolve_ms{0};     // keto_check_batch: name resolution of the last batch (diagnostic)
+
     // ---- device
     int device = -1;
     std::unique_ptr<DeviceState, DeviceStateDeleter> dev;
@@ -272,6 +275,37 @@ struct Snapshot {
     uint32_t row_flags(uint32_t r) const { return (rows[r].hi_flags >> 8) & 0xFFu; }
     uint32_t n_rows() const { return (uint32_t)rows.size(); }
 
+    // ---- request resolution (resolve.cpp): flat open-addressing indexes over the build's strings
+    // (byte-order ids, strs[0, n_sorted_strs)) and its real rows (row_key[0, n_real_rows)), both fixed
+    // after the build, so they are built once, on the first lookup; writes add strings and rows to
+    // added_str / row_of, which the lookups consult after the index.  16-B slots carry what verifies a
+    // hit (a string's length and first 11 bytes, a row's whole key), so a short string or a row is
+    // matched without reading strs / row_key; tables are huge-page mappings (one TLB entry per 2 MB).
+    struct HugeBuf {                                // anonymous zero-filled mapping, THP requested
+        void* p = nullptr;
+        uint64_t bytes = 0;
+        HugeBuf() = default;
+        HugeBuf(const HugeBuf&) = delete;
+        HugeBuf& operator=(const HugeBuf&) = delete;
+        ~HugeBuf();
+        void alloc(uint64_t bytes);
+    };
+    struct StrSlot {                                // id + 1 (0 = empty), length (255: >= 255), leading bytes
+        uint32_t id1;
+        uint8_t n;
+        char b[11];
+    };
+    struct RowSlot {                                // the row's key and row + 1 (0 = empty)
+        int32_t ns;
+        uint32_t obj, rel, row1;
+    };
+    mutable HugeBuf str_idx, row_idx;
+    mutable uint64_t str_mask = 0, row_mask = 0;
+    mutable std::once_flag idx_once;
+    void ensure_index() const;
+    std::unordered_map<std::string_view, int> ns_view;   // name -> config index (views into ns_names)
+    int ns_index(std::string_view name) const;           // config index, -1 if unknown
+    int64_t real_row(const RowKey& k) const;             // real row of a complete key, -1 if none
     // lookups used by request resolution
     int64_t lookup_str(std::string_view s) const;                      // -1 if absent
     // RelationQuery (namespace name, object, relation) -> row, per whereQuery; returns
@@ -295,6 +329,13 @@ struct Error {
     int code;
     std::string msg;
 };
+
+// named check requests [b, e) -> device form (resolve.cpp; the role of whereQuery,
+// internal/persistence/sql/relationtuples.go:178-198): out[i], status[i] (KETO_CHECK_*), and for a
+// wildcard query that no stored subject set materialized wild[i] = 1 with its key in wkey[i].  Throws
+// KETO_E_INVALID for a top-level row another part owns.
+void resolve_checks(const Snapshot& S, const keto_check_req* q, uint64_t b, uint64_t e, keto_check_ids* out,
+                    uint8_t* status, uint8_t* wild, RowKey* wkey);
 
 std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns, const keto_tuple* t, uint64_t n,
                                          uint32_t page_size);

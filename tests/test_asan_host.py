@@ -17,11 +17,12 @@ def test_host_library_under_asan(tmp_path):
     csrc = os.path.join(ROOT, "keto_amd", "csrc")
     san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     objs = []
-    for f in ("snapshot.cpp", "delta.cpp", "capi.cpp"):
+    from keto_amd.build import SOURCES
+    for f in [s for s in SOURCES if s.endswith(".cpp")]:
         o = str(tmp_path / (f + ".o"))
         subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *san, "-c", os.path.join(csrc, f), "-o", o])
         objs.append(o)
-    for f in ("engine.hip", "route.hip", "migrate.hip", "proto.hip"):
+    for f in [s for s in SOURCES if s.endswith(".hip")]:
         o = str(tmp_path / (f + ".o"))
         subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-Xarch_host",
                                "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-fno-omit-frame-pointer",

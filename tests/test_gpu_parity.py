@@ -163,3 +163,19 @@ def test_random_expand_proto_matches_oracle(seed):
                 assert t is not None and pb == tree_json_to_proto(t.to_json())
             else:
                 assert pb in (None, b""), (seed, st, pb)
+
+
+@pytest.mark.parametrize("seed", range(2300, 2340))
+def test_random_expand_via_fields_matches_json(seed):
+    """Trees rebuilt from keto_tree_nodes + keto_subject_fields (how the Go shim builds expand.Tree
+    values, integration/go/internal/gpu/gpu.go) equal keto_tree_json's trees, on quirk-heavy random
+    graphs (batch-local wildcard roots, unknown subject ids, empty fields, collisions)."""
+    from keto_amd.capi import EXPAND_TREE
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=seed % 3 == 0)
+    snap = _snapshot(ns, rows_from_tuples(ns, tuples, raw), ps)
+    exps = random_expands(seed, alph, k=16)
+    for g in sorted({e[2] for e in exps}):
+        grp = [(subj(s), d) for s, d, gg in exps if gg == g]
+        for st, js, tf in snap.expand_batch(grp, g, via_fields=True):
+            assert (st == EXPAND_TREE) == (tf is not None)
+            assert tf == js, (seed, g)

@@ -21,9 +21,9 @@ timeout -k 10 400 python -u bench.py "$@" > $out/bench.log 2>&1 || { tail -30 $o
 tail -1 $out/bench.log
 fi
 step kernel-trace
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- python -u bench.py --no-work --e2e-steps 0 "$@" > $out/kt.log 2>&1 || { tail -30 $out/kt.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- python -u bench.py --no-work --e2e-steps 0 --string-steps 0 "$@" > $out/kt.log 2>&1 || { tail -30 $out/kt.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
   step "pmc $c"
-  timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $out/pmc_$c -o pmc -- python -u bench.py --no-work --e2e-steps 0 "$@" > $out/pmc_$c.log 2>&1 || { tail -30 $out/pmc_$c.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $out/pmc_$c -o pmc -- python -u bench.py --no-work --e2e-steps 0 --string-steps 0 "$@" > $out/pmc_$c.log 2>&1 || { tail -30 $out/pmc_$c.log; exit 1; }
 done
 step done

@@ -544,8 +544,46 @@ static inline keto_str kstr(const char* p, uint32_t n) {
     return s;
 }
 
+static int emit_strings(const synth_graph* g, const synth_params* p, const char* const* rel_names, uint32_t n_rel,
+                        uint64_t seed, int threads, bool with_tuples, synth_strings* out);
+
 int synth_emit_strings(const synth_graph* g, const synth_params* p, const char* const* rel_names, uint32_t n_rel,
                        uint64_t seed, int threads, synth_strings* out) {
+    return emit_strings(g, p, rel_names, n_rel, seed, threads, true, out);
+}
+
+// the name table alone (no tuple rows): objects "%08x", users "u%08x", relation names
+int synth_emit_names(const synth_graph* g, const synth_params* p, const char* const* rel_names, uint32_t n_rel,
+                     int threads, synth_strings* out) {
+    return emit_strings(g, p, rel_names, n_rel, 0, threads, false, out);
+}
+
+// The graph in one string id space for keto_snapshot_from_csr (ids = byte-order ranks): object o ->
+// obj_base + o, user u -> user_base + u, relation r -> rel_id[r] (the caller orders the three blocks).
+// Writes the string table (keto_str into st->names), the rows' object / relation ids and the edges
+// (subject ids moved into the user block; subject sets unchanged).
+int synth_unify(const synth_graph* g, const synth_strings* st, uint64_t n_objs, uint64_t n_users, uint32_t obj_base,
+                uint32_t user_base, const uint32_t* rel_id, uint32_t n_rel, keto_str* strs, uint32_t* row_obj,
+                uint32_t* row_rel, uint32_t* edges, int threads) {
+    parallel_for(n_objs, threads, [&](uint64_t i) { strs[obj_base + i] = kstr(st->names + st->obj_base + i * 8, 8); });
+    parallel_for(n_users, threads, [&](uint64_t i) { strs[user_base + i] = kstr(st->names + st->user_base + i * 9, 9); });
+    for (uint32_t r = 0; r < n_rel; ++r) strs[rel_id[r]] = kstr(st->names + st->rel_base + st->rel_off[r], st->rel_len[r]);
+    parallel_for(g->n_rows, threads, [&](uint64_t r) {
+        row_obj[r] = obj_base + g->row_obj[r];
+        row_rel[r] = rel_id[g->row_rel[r]];
+    });
+    parallel_for((g->n_edges + 65535) / 65536, threads, [&](uint64_t c) {
+        const uint64_t b = c * 65536, e = std::min<uint64_t>(g->n_edges, b + 65536);
+        for (uint64_t i = b; i < e; ++i) {
+            const uint32_t x = g->edges[i];
+            edges[i] = (x & 0x80000000u) ? x : user_base + x;
+        }
+    });
+    return 0;
+}
+
+static int emit_strings(const synth_graph* g, const synth_params* p, const char* const* rel_names, uint32_t n_rel,
+                        uint64_t seed, int threads, bool with_tuples, synth_strings* out) {
     if (n_rel > 8) return -1;
     uint32_t max_obj = 0;
     for (uint32_t r = 0; r < g->n_rows; ++r) max_obj = std::max(max_obj, g->row_obj[r]);
@@ -556,9 +594,9 @@ int synth_emit_strings(const synth_graph* g, const synth_params* p, const char* 
     out->user_base = objs * 8;
     out->rel_base = out->user_base + users * 9;
     out->names = (char*)malloc(out->rel_base + rel_bytes + 1);
-    out->n = g->n_edges;
-    out->tuples = (keto_tuple*)calloc(std::max<uint64_t>(1, g->n_edges), sizeof(keto_tuple));
-    if (!out->names || !out->tuples) return -2;
+    out->n = with_tuples ? g->n_edges : 0;
+    out->tuples = with_tuples ? (keto_tuple*)calloc(std::max<uint64_t>(1, g->n_edges), sizeof(keto_tuple)) : nullptr;
+    if (!out->names || (with_tuples && !out->tuples)) return -2;
     static const char* hex = "0123456789abcdef";
     parallel_for(objs, threads, [&](uint64_t i) {
         char* d = out->names + out->obj_base + i * 8;
@@ -576,6 +614,7 @@ int synth_emit_strings(const synth_graph* g, const synth_params* p, const char* 
         memcpy(out->names + at, rel_names[i], out->rel_len[i]);
         at += out->rel_len[i];
     }
+    if (!with_tuples) return 0;
     const uint64_t E = g->n_edges;
     uint64_t a = (splitmix(seed) | 1) % std::max<uint64_t>(E, 1);
     while (E > 1 && std::gcd(a, E) != 1) a = (a + 2) % E;

@@ -77,6 +77,21 @@ DRIVE_10M = dict(n_docs=2_000_000, n_folders=8 * 37449, n_groups=50_000, n_users
                  target_edges=10_000_000, seed=2)
 
 
+class Unified:
+    """SynthGraph.unified(): from_csr arrays in one string id space plus the string table."""
+
+    def to_device_targets(self, q: np.ndarray) -> np.ndarray:
+        """Requests of SynthGraph.queries (user targets) in the unified id space."""
+        out = q.copy()
+        out["target"] = q["target"] + np.uint32(self.user_base)
+        return out
+
+    def free(self):
+        if getattr(self, "names", None) is not None and self.names.names:
+            lib().synth_strings_free(C.byref(self.names))
+            self.names = None
+
+
 class SynthGraph:
     def __init__(self, params: dict, threads: int = 16, kind: str = "powerlaw", chain: int = 32):
         self.params = params
@@ -175,6 +190,53 @@ class SynthGraph:
         _check(load().keto_snapshot_build(ns, len(self.namespaces), C.c_void_p(st.tuples), C.c_uint64(st.n),
                                           C.byref(opts), C.byref(h)))
         return Snapshot(h, load()), time.perf_counter() - t0
+
+    def unified(self, threads=16):
+        """The graph in one byte-ordered string id space, for a snapshot that holds its strings
+        (keto_snapshot_from_csr with a string table): objects, relation names and users each keep
+        their order; returns a Unified (arrays for from_csr, the string table, the user id offset)."""
+        rel = self.relation_names()
+        st = Strings()
+        arr = (C.c_char_p * len(rel))(*[x.encode() for x in rel])
+        if lib().synth_emit_names(C.byref(self.g), C.byref(self.p), arr, C.c_uint32(len(rel)), C.c_int(threads),
+                                  C.byref(st)) != 0:
+            raise RuntimeError("synth_emit_names failed")
+        n_objs = int(self.row_obj.max()) + 1 if self.n_rows else 0
+        n_users = int(self.params["n_users"])
+        blocks = [("obj", f"{0:08x}", f"{max(n_objs - 1, 0):08x}", n_objs),
+                  ("user", f"u{0:08x}", f"u{max(n_users - 1, 0):08x}", n_users)]
+        for i, r in enumerate(rel):
+            for _, lo, hi, _n in blocks[:2]:
+                if lo < r < hi:
+                    raise ValueError(f"relation name {r!r} sorts inside a generated string block")
+            blocks.append((f"rel{i}", r, r, 1))
+        at, base = 0, {}
+        for name, lo, _hi, cnt in sorted(blocks, key=lambda b: b[1]):
+            base[name] = at
+            at += cnt
+        from keto_amd.capi import KStr
+        u = Unified()
+        u.n_strings = at
+        u.strs = (KStr * max(1, at))()
+        u.row_obj = np.empty(self.n_rows, dtype=np.uint32)
+        u.row_rel = np.empty(self.n_rows, dtype=np.uint32)
+        u.edges = np.empty(max(1, self.n_edges), dtype=np.uint32)[: self.n_edges]
+        u.user_base = base["user"]
+        rel_id = np.array([base[f"rel{i}"] for i in range(len(rel))], dtype=np.uint32)
+        lib().synth_unify(C.byref(self.g), C.byref(st), C.c_uint64(n_objs), C.c_uint64(n_users),
+                          C.c_uint32(base["obj"]), C.c_uint32(base["user"]), rel_id.ctypes.data_as(C.c_void_p),
+                          C.c_uint32(len(rel)), u.strs, u.row_obj.ctypes.data_as(C.c_void_p),
+                          u.row_rel.ctypes.data_as(C.c_void_p), u.edges.ctypes.data_as(C.c_void_p), C.c_int(threads))
+        u.names = st                       # the string bytes the table points into
+        u.graph = self
+        return u
+
+    def snapshot_unified(self, u, device=0):
+        """The graph's snapshot with its string table (string-form requests resolve against it);
+        the device arena equals snapshot()'s up to the subject-id values."""
+        from keto_amd.capi import Snapshot
+        return Snapshot.from_csr(self.namespaces, self.row_ns, u.row_obj, u.row_rel, self.row_ptr, u.edges,
+                                 kstrs=(u.strs, u.n_strings), device=device)
 
     def string_requests(self, st, q: np.ndarray, threads=16):
         """keto_check_ids (CSR row ids, user targets) -> keto_check_req by name, for keto_check_batch."""
