@@ -1,24 +1,31 @@
 /*
  * keto_consumer.c -- a plain C consumer of include/keto_mi355x.h, written against the header only.
  *
- * It makes the calls, in the order, the Go shim (integration/go/internal/gpu/gpu.go) makes: build a
- * snapshot from the keto_relation_tuples rows (strings, commit order), check and expand batches,
- * read the per-request statuses, the expand trees as JSON (size query, then fill) and as protobuf,
- * the last error, and free everything.  tests/test_consumer_c.py compiles it with gcc against the
- * header and runs it: host-only (device -1: compute must fail with KETO_E_HIP) on the CPU, and the
- * reference's golden cases (tests/golden/reference_cases.json) on the GPU.
+ * It makes the calls, in the order, the Go integration makes (integration/go/internal/gpu/gpu.go,
+ * batcher.go; internal/driver/registry_gpu.go): build a snapshot from the keto_relation_tuples rows
+ * (strings, commit order), check batches and expand batches as the micro-batchers flush them, trees
+ * rebuilt from the node arena and keto_subject_fields (what gpu.ExpandBatch hands internal/expand),
+ * write transactions applied after they commit (keto_snapshot_apply) and, when the library answers
+ * KETO_E_REBUILD, a rebuild from the table the consumer keeps, as the registry's persister wrapper
+ * does.  tests/test_consumer_c.py compiles it with gcc against the header and runs it: host-only
+ * (device -1: compute must fail with KETO_E_HIP) on the CPU, and on the GPU the reference's golden
+ * cases (tests/golden/reference_cases.json) and seeded write / check / expand sequences compared with
+ * the SQL oracle.
  *
- * Input (tab-separated lines; empty fields allowed):
+ * Input (tab-separated lines; empty fields allowed), executed in order:
  *   P <page_size>        V <device>
  *   N <ns id> <name>
- *   T <ns id> <object> <relation> I <subject id>
+ *   T <ns id> <object> <relation> I <subject id>                          (a row of the initial table)
  *   T <ns id> <object> <relation> S <set ns id> <set object> <set relation>
  *   C <ns> <object> <relation> I <subject id> <max depth> <global max depth>
  *   C <ns> <object> <relation> S <set ns> <set object> <set relation> <max depth> <global max depth>
  *   E I <subject id> <max depth> <global max depth>
  *   E S <ns> <object> <relation> <max depth> <global max depth>
- * Output (tab-separated): "check <i> <allowed> <status>", "expand <i> <status> <json|null|error> <proto hex>",
- * "stats ...", "nodevice <rc>".
+ *   A+ <tuple as after T>   A- <tuple as after T>   A!   (one write transaction: inserts, deletes, commit)
+ * Consecutive C lines with one global max depth form one keto_check_batch; consecutive E lines one
+ * keto_expand_batch.  Output (tab-separated): "check <i> <allowed> <status>",
+ * "expand <i> <status> <json|null|error> <proto hex|->", "apply <rc> <version> <rebuilt>", "stats ...",
+ * "nodevice <rc>", "done".
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -64,23 +71,194 @@ static keto_str ks(const char* s) {
     return r;
 }
 
-typedef struct {
-    void** v;
-    size_t n, cap;
-} vec;
-
-static void push(vec* v, void* x) {
-    if (v->n == v->cap) {
-        v->cap = v->cap ? 2 * v->cap : 16;
-        v->v = (void**)realloc(v->v, v->cap * sizeof(void*));
-        if (!v->v) exit(3);
-    }
-    v->v[v->n++] = x;
-}
-
 static void fail(const char* what, int rc) {
     fprintf(stderr, "%s failed: %d (%s)\n", what, rc, keto_last_error());
     exit(2);
+}
+
+static void* xrealloc(void* p, size_t n) {
+    p = realloc(p, n ? n : 1);
+    if (!p) exit(3);
+    return p;
+}
+
+/* ---- the table the consumer keeps (the SQL table of the Go server): tuples in commit order */
+typedef struct {
+    keto_tuple* t;
+    size_t n, cap;
+} table_t;
+
+static keto_tuple tuple_of(line_t* l, int k) { /* fields k..: <ns id> <obj> <rel> I <sid> | S <sns> <sobj> <srel> */
+    keto_tuple t;
+    memset(&t, 0, sizeof t);
+    t.namespace_id = atoi(l->f[k]);
+    t.object = ks(l->f[k + 1]);
+    t.relation = ks(l->f[k + 2]);
+    if (!strcmp(l->f[k + 3], "I")) {
+        t.subject_kind = 0;
+        t.subject_id = ks(l->f[k + 4]);
+    } else {
+        t.subject_kind = 1;
+        t.set_namespace_id = atoi(l->f[k + 4]);
+        t.set_object = ks(l->f[k + 5]);
+        t.set_relation = ks(l->f[k + 6]);
+    }
+    return t;
+}
+
+static int str_eq(keto_str a, keto_str b) { return a.n == b.n && (a.n == 0 || memcmp(a.p, b.p, a.n) == 0); }
+
+/* DeleteRelationTuples' WHERE: namespace, object, relation and subject all equal (relationtuples.go:200-223) */
+static int tuple_eq(const keto_tuple* a, const keto_tuple* b) {
+    if (a->namespace_id != b->namespace_id || !str_eq(a->object, b->object) || !str_eq(a->relation, b->relation) ||
+        a->subject_kind != b->subject_kind)
+        return 0;
+    if (a->subject_kind == 0) return str_eq(a->subject_id, b->subject_id);
+    return a->set_namespace_id == b->set_namespace_id && str_eq(a->set_object, b->set_object) &&
+           str_eq(a->set_relation, b->set_relation);
+}
+
+static void table_insert(table_t* tb, keto_tuple t) {
+    if (tb->n == tb->cap) {
+        tb->cap = tb->cap ? 2 * tb->cap : 64;
+        tb->t = (keto_tuple*)xrealloc(tb->t, tb->cap * sizeof(keto_tuple));
+    }
+    tb->t[tb->n++] = t;
+}
+
+static void table_delete(table_t* tb, const keto_tuple* d) {
+    size_t w = 0;
+    for (size_t i = 0; i < tb->n; ++i)
+        if (!tuple_eq(&tb->t[i], d)) tb->t[w++] = tb->t[i];
+    tb->n = w;
+}
+
+/* ---- protobuf of a tree rebuilt from its nodes and subject fields (Tree.ToProto + proto.Marshal,
+ * internal/expand/tree.go:165-188): node_type = 1 (UNION 1, LEAF 4), subject = 2 (Subject: id = 1 |
+ * set = 2 {namespace 1, object 2, relation 3, empty strings omitted}), children = 3 */
+typedef struct {
+    uint8_t* p;
+    size_t n, cap;
+} buf_t;
+
+static void put(buf_t* b, const void* s, size_t n) {
+    if (b->n + n > b->cap) {
+        b->cap = (b->n + n) * 2 + 64;
+        b->p = (uint8_t*)xrealloc(b->p, b->cap);
+    }
+    if (n) memcpy(b->p + b->n, s, n);
+    b->n += n;
+}
+static void put_varint(buf_t* b, uint64_t v) {
+    uint8_t x[10];
+    int k = 0;
+    while (v >= 0x80) {
+        x[k++] = (uint8_t)(v | 0x80);
+        v >>= 7;
+    }
+    x[k++] = (uint8_t)v;
+    put(b, x, (size_t)k);
+}
+static void put_field(buf_t* b, uint8_t tag, const char* s, size_t n) {
+    put(b, &tag, 1);
+    put_varint(b, n);
+    put(b, s, n);
+}
+
+typedef struct {
+    int set;
+    const char *a, *b, *c; /* id | namespace, object, relation */
+    uint32_t na, nb, nc;
+} fields_t;
+
+/* encodes the subtree at nodes[*at] into out; returns 0, or -1 on a malformed arena */
+static int encode(const keto_tree_node* nodes, uint64_t n, uint64_t* at, const fields_t* f, buf_t* out, int depth) {
+    if (*at >= n || depth > 4096) return -1;
+    const uint64_t me = (*at)++;
+    const int leaf = (nodes[me].info & 0x80000000u) != 0;
+    const uint32_t nc = leaf ? 0 : nodes[me].info & 0x7FFFFFFFu;
+    uint8_t tt[2] = {0x08, (uint8_t)(leaf ? 4 : 1)};
+    put(out, tt, 2);
+    buf_t sub = {0, 0, 0};
+    const fields_t* s = &f[me];
+    if (!s->set) {
+        put_field(&sub, 0x0A, s->a, s->na);
+    } else {
+        buf_t in = {0, 0, 0};
+        if (s->na) put_field(&in, 0x0A, s->a, s->na);
+        if (s->nb) put_field(&in, 0x12, s->b, s->nb);
+        if (s->nc) put_field(&in, 0x1A, s->c, s->nc);
+        put_field(&sub, 0x12, (const char*)in.p, in.n);
+        free(in.p);
+    }
+    put_field(out, 0x12, (const char*)sub.p, sub.n);
+    free(sub.p);
+    for (uint32_t c = 0; c < nc; ++c) {
+        buf_t child = {0, 0, 0};
+        if (encode(nodes, n, at, f, &child, depth + 1)) return -1;
+        put_field(out, 0x1A, (const char*)child.p, child.n);
+        free(child.p);
+    }
+    return 0;
+}
+
+/* tree i of arena ar through keto_tree_nodes + keto_subject_fields (size, then fill), as protobuf */
+static int tree_via_fields(keto_snapshot* snap, keto_tree_arena* ar, uint32_t i, buf_t* out) {
+    uint64_t n = 0;
+    const keto_tree_node* nodes = keto_tree_nodes(ar, i, &n);
+    if (!nodes || !n) return 0;
+    uint32_t* refs = (uint32_t*)xrealloc(NULL, n * sizeof(uint32_t));
+    uint32_t* lens = (uint32_t*)xrealloc(NULL, 3 * n * sizeof(uint32_t));
+    for (uint64_t k = 0; k < n; ++k) refs[k] = nodes[k].subject;
+    const int64_t total = keto_subject_fields(snap, ar, refs, n, NULL, 0, lens);
+    if (total < 0) fail("keto_subject_fields", (int)total);
+    char* text = (char*)xrealloc(NULL, (size_t)total + 1);
+    if (keto_subject_fields(snap, ar, refs, n, text, (uint64_t)total, lens) != total) return -1;
+    fields_t* f = (fields_t*)xrealloc(NULL, n * sizeof(fields_t));
+    size_t at = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+        f[k].set = (refs[k] & 0x80000000u) != 0;
+        f[k].na = lens[3 * k];
+        f[k].nb = lens[3 * k + 1];
+        f[k].nc = lens[3 * k + 2];
+        f[k].a = text + at;
+        at += f[k].na;
+        f[k].b = text + at;
+        at += f[k].nb;
+        f[k].c = text + at;
+        at += f[k].nc;
+    }
+    uint64_t pos = 0;
+    const int rc = encode(nodes, n, &pos, f, out, 0) || pos != n ? -1 : 0;
+    free(refs);
+    free(lens);
+    free(text);
+    free(f);
+    return rc;
+}
+
+static keto_snapshot* build(const keto_namespace* ns, size_t n_ns, const table_t* tb, uint32_t page_size, int device) {
+    keto_snapshot_opts opts;
+    opts.page_size = page_size;
+    opts.device = device;
+    opts.flags = 0;
+    keto_snapshot* snap = NULL;
+    const int rc = keto_snapshot_build(ns, (uint32_t)n_ns, tb->t, tb->n, &opts, &snap);
+    if (rc != KETO_OK) fail("keto_snapshot_build", rc);
+    return snap;
+}
+
+static void subject_of(line_t* l, int* k, keto_subject* s) {
+    memset(s, 0, sizeof *s);
+    if (!strcmp(l->f[(*k)++], "I")) {
+        s->kind = 0;
+        s->id = ks(l->f[(*k)++]);
+    } else {
+        s->kind = 1;
+        s->set_namespace = ks(l->f[(*k)++]);
+        s->set_object = ks(l->f[(*k)++]);
+        s->set_relation = ks(l->f[(*k)++]);
+    }
 }
 
 int main(int argc, char** argv) {
@@ -94,7 +272,8 @@ int main(int argc, char** argv) {
         fprintf(stderr, "ABI %d != header %d\n", keto_abi_version(), KETO_ABI_VERSION);
         return 2;
     }
-    vec lines = {0, 0, 0};
+    line_t** lines = NULL;
+    size_t n_lines = 0;
     char buf[1 << 16];
     uint32_t page_size = 100;
     int device = -1;
@@ -103,149 +282,175 @@ int main(int argc, char** argv) {
         if (!l || split(buf, l) < 1) return 1;
         if (!strcmp(l->f[0], "P")) page_size = (uint32_t)atoi(l->f[1]);
         else if (!strcmp(l->f[0], "V")) device = atoi(l->f[1]);
-        else push(&lines, l);
+        lines = (line_t**)xrealloc(lines, (n_lines + 1) * sizeof(line_t*));
+        lines[n_lines++] = l;
     }
     fclose(in);
 
-    /* namespaces and tuples (commit order) */
-    size_t n_ns = 0, n_t = 0;
-    for (size_t i = 0; i < lines.n; ++i) {
-        line_t* l = (line_t*)lines.v[i];
-        n_ns += !strcmp(l->f[0], "N");
-        n_t += !strcmp(l->f[0], "T");
-    }
-    keto_namespace* ns = (keto_namespace*)calloc(n_ns ? n_ns : 1, sizeof(keto_namespace));
-    keto_tuple* tu = (keto_tuple*)calloc(n_t ? n_t : 1, sizeof(keto_tuple));
-    size_t a = 0, b = 0;
-    for (size_t i = 0; i < lines.n; ++i) {
-        line_t* l = (line_t*)lines.v[i];
+    /* namespaces (config order) and the initial table (commit order) */
+    size_t n_ns = 0;
+    keto_namespace* ns = NULL;
+    table_t table = {0, 0, 0};
+    for (size_t i = 0; i < n_lines; ++i) {
+        line_t* l = lines[i];
         if (!strcmp(l->f[0], "N")) {
-            ns[a].id = atoi(l->f[1]);
-            ns[a++].name = ks(l->f[2]);
+            ns = (keto_namespace*)xrealloc(ns, (n_ns + 1) * sizeof(keto_namespace));
+            ns[n_ns].id = atoi(l->f[1]);
+            ns[n_ns++].name = ks(l->f[2]);
         } else if (!strcmp(l->f[0], "T")) {
-            keto_tuple* t = &tu[b++];
-            t->namespace_id = atoi(l->f[1]);
-            t->object = ks(l->f[2]);
-            t->relation = ks(l->f[3]);
-            if (!strcmp(l->f[4], "I")) {
-                t->subject_kind = 0;
-                t->subject_id = ks(l->f[5]);
-            } else {
-                t->subject_kind = 1;
-                t->set_namespace_id = atoi(l->f[5]);
-                t->set_object = ks(l->f[6]);
-                t->set_relation = ks(l->f[7]);
-            }
+            table_insert(&table, tuple_of(l, 1));
         }
     }
-    keto_snapshot_opts opts;
-    opts.page_size = page_size;
-    opts.device = device;
-    opts.flags = 0;
-    keto_snapshot* snap = NULL;
-    int rc = keto_snapshot_build(ns, (uint32_t)n_ns, tu, n_t, &opts, &snap);
-    if (rc != KETO_OK) fail("keto_snapshot_build", rc);
+    keto_snapshot* snap = build(ns, n_ns, &table, page_size, device);
     keto_snapshot_stats st;
-    rc = keto_snapshot_get_stats(snap, &st);
+    int rc = keto_snapshot_get_stats(snap, &st);
     if (rc != KETO_OK) fail("keto_snapshot_get_stats", rc);
     printf("stats tuples=%llu rows=%u real=%u wildcard=%u seq=%u poisoned=%u strings=%u collisions=%u\n",
            (unsigned long long)st.n_tuples, st.n_rows, st.n_real_rows, st.n_wildcard_rows, st.n_seq_rows,
            st.n_poisoned_rows, st.n_strings, st.n_collision_keys);
 
-    /* checks: one batch per request, as the micro-batcher's smallest flush */
     int checks = 0, expands = 0;
-    for (size_t i = 0; i < lines.n; ++i) {
-        line_t* l = (line_t*)lines.v[i];
+    keto_tuple* ins = NULL;
+    keto_tuple* del = NULL;
+    size_t n_ins = 0, n_del = 0;
+    for (size_t i = 0; i < n_lines;) {
+        line_t* l = lines[i];
         if (!strcmp(l->f[0], "C")) {
-            keto_check_req q;
-            memset(&q, 0, sizeof q);
-            q.namespace_ = ks(l->f[1]);
-            q.object = ks(l->f[2]);
-            q.relation = ks(l->f[3]);
-            int k = 5;
-            if (!strcmp(l->f[4], "I")) {
-                q.subject.kind = 0;
-                q.subject.id = ks(l->f[k++]);
-            } else {
-                q.subject.kind = 1;
-                q.subject.set_namespace = ks(l->f[k++]);
-                q.subject.set_object = ks(l->f[k++]);
-                q.subject.set_relation = ks(l->f[k++]);
+            /* one micro-batch: the consecutive checks with this global max depth */
+            const int32_t gmd = atoi(l->f[l->n - 1]);
+            size_t j = i;
+            while (j < n_lines && !strcmp(lines[j]->f[0], "C") && atoi(lines[j]->f[lines[j]->n - 1]) == gmd) ++j;
+            const size_t m = j - i;
+            keto_check_req* q = (keto_check_req*)calloc(m, sizeof(keto_check_req));
+            uint8_t* allowed = (uint8_t*)malloc(m);
+            uint8_t* status = (uint8_t*)malloc(m);
+            if (!q || !allowed || !status) return 3;
+            for (size_t k = 0; k < m; ++k) {
+                line_t* c = lines[i + k];
+                q[k].namespace_ = ks(c->f[1]);
+                q[k].object = ks(c->f[2]);
+                q[k].relation = ks(c->f[3]);
+                int f = 4;
+                subject_of(c, &f, &q[k].subject);
+                q[k].max_depth = atoi(c->f[f]);
             }
-            q.max_depth = atoi(l->f[k++]);
-            const int32_t gmd = atoi(l->f[k]);
-            uint8_t allowed = 9, status = 9;
-            rc = keto_check_batch(snap, &q, 1, gmd, &allowed, &status);
+            rc = keto_check_batch(snap, q, (uint32_t)m, gmd, allowed, status);
             if (device < 0) {
                 printf("nodevice %d\n", rc);
                 if (rc != KETO_E_HIP || !keto_last_error()[0]) return 4;
                 break;
             }
             if (rc != KETO_OK) fail("keto_check_batch", rc);
-            printf("check\t%d\t%u\t%u\n", checks++, allowed, status);
-        } else if (!strcmp(l->f[0], "E") && device >= 0) {
-            keto_expand_req r;
-            memset(&r, 0, sizeof r);
-            int k = 2;
-            if (!strcmp(l->f[1], "I")) {
-                r.subject.kind = 0;
-                r.subject.id = ks(l->f[k++]);
-            } else {
-                r.subject.kind = 1;
-                r.subject.set_namespace = ks(l->f[k++]);
-                r.subject.set_object = ks(l->f[k++]);
-                r.subject.set_relation = ks(l->f[k++]);
-            }
-            r.max_depth = atoi(l->f[k++]);
-            const int32_t gmd = atoi(l->f[k]);
-            keto_tree_arena* ar = NULL;
-            rc = keto_expand_batch(snap, &r, 1, gmd, &ar);
-            if (rc != KETO_OK) fail("keto_expand_batch", rc);
-            if (keto_tree_count(ar) != 1) return 5;
-            const int s = keto_tree_status(ar, 0);
-            const int64_t jn = keto_tree_json(snap, ar, 0, NULL, 0);
-            char* js = NULL;
-            if (jn >= 0) {
-                js = (char*)malloc((size_t)jn + 1);
-                if (keto_tree_json(snap, ar, 0, js, (uint64_t)jn + 1) != jn) return 6;
-            }
-            {   /* the batch form (what the Go shim calls): the same text, "" for an error root */
-                uint64_t offs[2];
-                const int64_t an = keto_tree_json_all(snap, ar, NULL, 0, offs);
-                if (an < 0) fail("keto_tree_json_all", (int)an);
-                char* all = (char*)malloc((size_t)an + 1);
-                if (keto_tree_json_all(snap, ar, all, (uint64_t)an, offs) != an) return 6;
-                if (offs[0] != 0 || offs[1] != (uint64_t)an) return 6;
-                if (js ? (an != jn || memcmp(all, js, (size_t)an) != 0) : an != 0) return 6;
-                free(all);
-            }
-            const int64_t pn = keto_tree_proto(snap, ar, 0, NULL, 0);
-            printf("expand\t%d\t%d\t%s\t", expands++, s, js ? js : "error");
-            if (pn > 0) {
-                uint8_t* pb = (uint8_t*)malloc((size_t)pn);
-                if (keto_tree_proto(snap, ar, 0, pb, (uint64_t)pn) != pn) return 7;
-                for (int64_t x = 0; x < pn; ++x) printf("%02x", pb[x]);
-                free(pb);
-            } else {
-                printf("-");
-            }
-            printf("\n");
-            free(js);
-            keto_tree_arena_free(ar);
+            for (size_t k = 0; k < m; ++k) printf("check\t%d\t%u\t%u\n", checks++, allowed[k], status[k]);
+            free(q);
+            free(allowed);
+            free(status);
+            i = j;
+            continue;
         }
+        if (!strcmp(l->f[0], "E") && device >= 0) {
+            const int32_t gmd = atoi(l->f[l->n - 1]);
+            size_t j = i;
+            while (j < n_lines && !strcmp(lines[j]->f[0], "E") && atoi(lines[j]->f[lines[j]->n - 1]) == gmd) ++j;
+            const size_t m = j - i;
+            keto_expand_req* r = (keto_expand_req*)calloc(m, sizeof(keto_expand_req));
+            if (!r) return 3;
+            for (size_t k = 0; k < m; ++k) {
+                int f = 1;
+                subject_of(lines[i + k], &f, &r[k].subject);
+                r[k].max_depth = atoi(lines[i + k]->f[f]);
+            }
+            keto_tree_arena* ar = NULL;
+            rc = keto_expand_batch(snap, r, (uint32_t)m, gmd, &ar);
+            if (rc != KETO_OK) fail("keto_expand_batch", rc);
+            if (keto_tree_count(ar) != m) return 5;
+            /* the batch JSON (size query, then fill) */
+            uint64_t* offs = (uint64_t*)xrealloc(NULL, (m + 1) * sizeof(uint64_t));
+            const int64_t an = keto_tree_json_all(snap, ar, NULL, 0, offs);
+            if (an < 0) fail("keto_tree_json_all", (int)an);
+            char* all = (char*)xrealloc(NULL, (size_t)an + 1);
+            if (keto_tree_json_all(snap, ar, all, (uint64_t)an, offs) != an) return 6;
+            for (uint32_t k = 0; k < m; ++k) {
+                const int s = keto_tree_status(ar, k);
+                const int64_t jn = keto_tree_json(snap, ar, k, NULL, 0);
+                char* js = NULL;
+                if (jn >= 0) {
+                    js = (char*)malloc((size_t)jn + 1);
+                    if (!js || keto_tree_json(snap, ar, k, js, (uint64_t)jn + 1) != jn) return 6;
+                }
+                const uint64_t tl = offs[k + 1] - offs[k];
+                if (js ? (tl != (uint64_t)jn || memcmp(all + offs[k], js, tl) != 0) : tl != 0) return 6;
+                const int64_t pn = keto_tree_proto(snap, ar, k, NULL, 0);
+                printf("expand\t%d\t%d\t%s\t", expands++, s, js ? js : "error");
+                buf_t via = {0, 0, 0};
+                if (tree_via_fields(snap, ar, k, &via)) return 9;
+                if (pn > 0) {
+                    uint8_t* pb = (uint8_t*)malloc((size_t)pn);
+                    if (!pb || keto_tree_proto(snap, ar, k, pb, (uint64_t)pn) != pn) return 7;
+                    /* the tree the Go shim builds from nodes + fields encodes to the same bytes */
+                    if (via.n != (size_t)pn || memcmp(via.p, pb, (size_t)pn) != 0) return 10;
+                    for (int64_t x = 0; x < pn; ++x) printf("%02x", pb[x]);
+                    free(pb);
+                } else {
+                    if (via.n != 0) return 10;
+                    printf("-");
+                }
+                free(via.p);
+                printf("\n");
+                free(js);
+            }
+            free(all);
+            free(offs);
+            keto_tree_arena_free(ar);
+            free(r);
+            i = j;
+            continue;
+        }
+        if (!strcmp(l->f[0], "A+") || !strcmp(l->f[0], "A-")) {
+            const keto_tuple t = tuple_of(l, 1);
+            if (l->f[0][1] == '+') {
+                ins = (keto_tuple*)xrealloc(ins, (n_ins + 1) * sizeof(keto_tuple));
+                ins[n_ins++] = t;
+            } else {
+                del = (keto_tuple*)xrealloc(del, (n_del + 1) * sizeof(keto_tuple));
+                del[n_del++] = t;
+            }
+        } else if (!strcmp(l->f[0], "A!")) {
+            /* the transaction committed in SQL: the table changes, then the snapshot follows */
+            for (size_t k = 0; k < n_ins; ++k) table_insert(&table, ins[k]);
+            for (size_t k = 0; k < n_del; ++k) table_delete(&table, &del[k]);
+            uint64_t v0 = keto_snapshot_version(snap), v = 0;
+            rc = keto_snapshot_apply(snap, ins, n_ins, del, n_del, &v);
+            int rebuilt = 0;
+            if (rc == KETO_E_REBUILD) {
+                if (keto_snapshot_version(snap) != v0) return 11; /* a refused write leaves it unchanged */
+                keto_snapshot_release(snap);
+                snap = build(ns, n_ns, &table, page_size, device);
+                rebuilt = 1;
+                v = keto_snapshot_version(snap);
+            } else if (rc != KETO_OK) {
+                fail("keto_snapshot_apply", rc);
+            } else if (v != v0 + 1 || keto_snapshot_version(snap) != v) {
+                return 12;
+            }
+            printf("apply\t%d\t%llu\t%d\n", rc, (unsigned long long)v, rebuilt);
+            n_ins = n_del = 0;
+        }
+        ++i;
     }
     /* an error path: a NULL argument must fail with a message, not crash */
     rc = keto_check_batch(snap, NULL, 1, 5, NULL, NULL);
     if (rc != KETO_E_INVALID || !keto_last_error()[0]) return 8;
     keto_snapshot_release(snap);
-    for (size_t i = 0; i < lines.n; ++i) {
-        line_t* l = (line_t*)lines.v[i];
-        for (int k = 0; k < l->n; ++k) free(l->f[k]);
-        free(l);
+    for (size_t i = 0; i < n_lines; ++i) {
+        for (int k = 0; k < lines[i]->n; ++k) free(lines[i]->f[k]);
+        free(lines[i]);
     }
-    free(lines.v);
+    free(lines);
     free(ns);
-    free(tu);
+    free(table.t);
+    free(ins);
+    free(del);
     printf("done\n");
     return 0;
 }

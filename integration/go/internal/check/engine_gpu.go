@@ -11,8 +11,9 @@ import (
 )
 
 // GPUProvider is implemented by the registry once a GPU snapshot is loaded
-// (internal/driver/registry_default.go:159-164 constructs the engine; the registry builds the
-// snapshot after Init, :241-262).  A nil batcher means "no snapshot": the SQL path runs.
+// (internal/driver/registry_default.go:159-164 constructs the engine; registry_gpu.go's EnableGPU
+// builds the snapshot after Init, :241-262).  A nil batcher means "no current snapshot" (none loaded,
+// or one behind the table while it is rebuilt): the SQL path runs.
 type GPUProvider interface {
 	GPUCheckBatcher() *gpu.Batcher
 }

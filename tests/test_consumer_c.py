@@ -88,3 +88,88 @@ def test_consumer_golden_on_gpu(consumer, tmp_path, case):
             assert int(status) == 0 and json.loads(js) == e["expected"]
             assert bytes.fromhex(pb) == tree_json_to_proto(e["expected"])
     assert out[-1] == "done"
+
+
+def _tuple_fields(ids, t):
+    if isinstance(t.subject, SubjectID):
+        return f"{ids[t.namespace]}\t{t.object}\t{t.relation}\tI\t{t.subject.id}"
+    s = t.subject
+    return f"{ids[t.namespace]}\t{t.object}\t{t.relation}\tS\t{ids[s.namespace]}\t{s.object}\t{s.relation}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(24))
+def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed):
+    """The whole Go call sequence from C: build -> check / expand micro-batches -> write transactions
+    applied after they commit (KETO_E_REBUILD -> rebuild from the consumer's table, as the registry's
+    persister wrapper does) -> checks and expands again; trees also rebuilt from keto_tree_nodes +
+    keto_subject_fields (the Go shim's path) and re-encoded byte-equal.  Every decision and tree is
+    compared with the SQL oracle replaying the same transactions."""
+    import random
+    from oracle.oracle_sql import CheckEngine, ExpandEngine, NotFoundError, SQLStore
+    from tests.proto_util import tree_json_to_proto
+    from tests.randgraph import random_checks, random_expands, random_graph
+    from tests.test_gpu_lifecycle import _random_write
+    ns, tuples, _raw, ps, alph = random_graph(seed + 900, wide=seed % 4 == 3, allow_wildcards=seed % 5 == 0,
+                                              allow_poison=False, allow_collisions=seed % 3 == 0)
+    names, objs, rels, users = alph
+    names = [n for n in names if n]
+    if not names:
+        pytest.skip("only a namespace named ''")
+    ids = {n: i for i, n in reversed(ns)}
+    store = SQLStore(ns, tuples, page_size=ps)
+    lines = [f"P\t{ps}", "V\t0"] + [f"N\t{i}\t{n}" for i, n in ns] + [f"T\t{_tuple_fields(ids, t)}" for t in tuples]
+    want = []                                  # expected output lines, in order
+    rng = random.Random(seed)
+    for step in range(6):
+        checks = random_checks(seed * 13 + step, (names, objs + ["new1", "a0"], rels + ["q"], users + ["w001"]), k=16)
+        for g in sorted({c[2] for c in checks}):
+            for t, d, _ in (c for c in checks if c[2] == g):
+                sub = (f"I\t{t.subject.id}" if isinstance(t.subject, SubjectID)
+                       else f"S\t{t.subject.namespace}\t{t.subject.object}\t{t.subject.relation}")
+                lines.append(f"C\t{t.namespace}\t{t.object}\t{t.relation}\t{sub}\t{d}\t{g}")
+                want.append(("check", CheckEngine(store, g).subject_is_allowed(t, d)))
+        exps = random_expands(seed * 7 + step, (names, objs + ["new3"], rels + ["q"], users), k=6)
+        for g in sorted({e[2] for e in exps}):
+            for s, d, _ in (e for e in exps if e[2] == g):
+                sub = f"I\t{s.id}" if isinstance(s, SubjectID) else f"S\t{s.namespace}\t{s.object}\t{s.relation}"
+                lines.append(f"E\t{sub}\t{d}\t{g}")
+                try:
+                    tr = ExpandEngine(store, g).build_tree(s, d)
+                    want.append(("expand", tr.to_json() if tr is not None else None))
+                except NotFoundError:
+                    want.append(("expand", "error"))
+        cur = store.tuples()
+        ins = [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(1, 8))]
+        dels = [rng.choice(cur) for _ in range(rng.randint(0, 3))] if cur else []
+        lines += [f"A+\t{_tuple_fields(ids, t)}" for t in ins] + [f"A-\t{_tuple_fields(ids, t)}" for t in dels]
+        lines.append("A!")
+        want.append(("apply", None))
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+    p = tmp_path / "in.tsv"
+    p.write_text("\n".join(lines) + "\n")
+    r = subprocess.run([consumer, str(p)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = [ln.split("\t") for ln in r.stdout.splitlines() if ln.split("\t")[0] in ("check", "expand", "apply")]
+    # the consumer runs a batch of checks before the expands of a step: same order as `want`
+    assert [g[0] for g in got] == [w[0] for w in want]
+    versions = 0
+    for g, (kind, exp) in zip(got, want):
+        if kind == "check":
+            assert bool(int(g[2])) == exp, (seed, g)
+        elif kind == "expand":
+            _, _, status, js, pb = g
+            if exp == "error":
+                assert int(status) == 2 and js == "error"
+            elif exp is None:
+                assert int(status) == 1 and js == "null" and pb == "-"
+            else:
+                assert int(status) == 0 and json.loads(js) == exp, (seed, js, exp)
+                assert bytes.fromhex(pb) == tree_json_to_proto(exp)
+        else:
+            assert int(g[1]) in (0, -6)                  # applied, or KETO_E_REBUILD -> rebuilt
+            versions += int(g[3]) == 0
+    assert r.stdout.splitlines()[-1] == "done"

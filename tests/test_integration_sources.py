@@ -1,22 +1,37 @@
 """Consistency of the Go integration sources (integration/go, not compiled here: no Go toolchain)
-with the C-ABI they bind: every C.keto_* / C.KETO_* name they use is declared in
-include/keto_mi355x.h, and they stay within Go 1.17 (the reference's go.mod:221)."""
+with the C-ABI they bind and with each other: every C.keto_* / C.KETO_* name they use is declared in
+include/keto_mi355x.h, every exported gpu.X another package uses is declared in package gpu, the
+package graph has no cycle (gpu imports none of the packages that import it), and the sources stay
+within Go 1.17 (the reference's go.mod:221)."""
 import glob
 import os
 import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GO = os.path.join(ROOT, "integration", "go")
+MODULE = "github.com/ory/keto/"
 
 
 def _go_files():
-    return sorted(glob.glob(os.path.join(ROOT, "integration", "go", "**", "*.go"), recursive=True))
+    return sorted(glob.glob(os.path.join(GO, "**", "*.go"), recursive=True))
+
+
+def _code(src):
+    return "\n".join(ln.split("//")[0] for ln in src.splitlines())     # comments may name anything
+
+
+def _imports(src):
+    m = re.search(r"^import \((.*?)^\)", src, re.S | re.M)
+    block = m.group(1) if m else ""
+    single = re.findall(r'^import\s+"([^"]+)"', src, re.M)
+    return set(re.findall(r'"([^"]+)"', block)) | set(single)
 
 
 def test_go_sources_use_declared_c_names():
     hdr = open(os.path.join(ROOT, "include", "keto_mi355x.h")).read()
     declared = set(re.findall(r"\b((?:keto|KETO)_[A-Za-z0-9_]+)\b", hdr))
     files = _go_files()
-    assert len(files) >= 5
+    assert len(files) >= 8
     for f in files:
         src = open(f).read()
         for name in set(re.findall(r"\bC\.(?:sizeof_)?((?:keto|KETO)_[A-Za-z0-9_]+)", src)):
@@ -26,10 +41,58 @@ def test_go_sources_use_declared_c_names():
 def test_go_sources_stay_on_go_1_17():
     for f in _go_files():
         src = open(f).read()
-        code = "\n".join(ln.split("//")[0] for ln in src.splitlines())     # comments may name them
+        code = _code(src)
         for banned in ("runtime.Pinner", "unsafe.StringData", "unsafe.SliceData", "unsafe.String(", "[T any]",
-                       "min(", "max(", "clear("):
+                       "min(", "max(", "clear(", "atomic.Pointer", "atomic.Int64", "errors.Join", "slices.",
+                       "maps."):
             assert banned not in code, (os.path.relpath(f, ROOT), banned)
-        # cgo files carry both build-constraint forms (the // +build line is what Go 1.17 reads)
-        if 'import "C"' in src:
+        # cgo files and their importers are behind the keto_gpu tag, in both build-constraint forms
+        # (Go 1.17 reads // +build); cmd/check's batch mode is a plain gRPC client and builds always
+        if 'import "C"' in src or MODULE + "internal/gpu" in src:
             assert "//go:build keto_gpu" in src and "// +build keto_gpu" in src, f
+
+
+def test_go_package_graph():
+    pkgs = {}
+    for f in _go_files():
+        src = open(f).read()
+        rel = os.path.relpath(os.path.dirname(f), GO).replace(os.sep, "/")
+        pkg = re.search(r"^package (\w+)", src, re.M).group(1)
+        assert pkg == rel.split("/")[-1], (f, pkg)             # the package of its drop-in directory
+        pkgs.setdefault(rel, set()).update(i[len(MODULE):] for i in _imports(src) if i.startswith(MODULE))
+    # internal/gpu is imported by check, expand, driver and persistence/sql: it must import none of them
+    assert not (pkgs["internal/gpu"] & {"internal/check", "internal/expand", "internal/driver",
+                                        "internal/persistence/sql"}), pkgs["internal/gpu"]
+    for p, deps in pkgs.items():
+        for d in deps:
+            assert p not in pkgs.get(d, set()), (p, d)          # no two-package cycle among our files
+    assert "internal/gpu" in pkgs["internal/expand"] and "internal/gpu" in pkgs["internal/check"]
+    assert "internal/gpu" in pkgs["internal/driver"] and "internal/gpu" in pkgs["internal/persistence/sql"]
+
+
+def test_exported_gpu_names_exist():
+    decl = set()
+    for f in glob.glob(os.path.join(GO, "internal", "gpu", "*.go")):
+        code = _code(open(f).read())
+        decl |= set(re.findall(r"^func (?:\([^)]*\) )?([A-Z]\w*)", code, re.M))
+        decl |= set(re.findall(r"^type ([A-Z]\w*)", code, re.M))
+        decl |= set(re.findall(r"^\s*([A-Z]\w*)\s*=", code, re.M))          # var / const blocks
+        decl |= set(re.findall(r"^(?:var|const) ([A-Z]\w*)", code, re.M))
+    for f in _go_files():
+        if os.sep + os.path.join("internal", "gpu") + os.sep in f:
+            continue
+        for name in set(re.findall(r"\bgpu\.([A-Z]\w*)", _code(open(f).read()))):
+            assert name in decl, (os.path.relpath(f, ROOT), name)
+
+
+def test_engine_dispatch_hooks_match_the_registry():
+    """The providers the engines look for are the methods registry_gpu.go adds to RegistryDefault."""
+    reg = _code(open(os.path.join(GO, "internal", "driver", "registry_gpu.go")).read())
+    for eng, method in (("check", "GPUCheckBatcher"), ("expand", "GPUExpandBatcher")):
+        src = _code(open(os.path.join(GO, "internal", eng, "engine_gpu.go")).read())
+        assert f"{method}() *gpu." in src
+        assert re.search(r"func \(r \*RegistryDefault\) " + method + r"\(\) \*gpu\.", reg), method
+    # the persister wrapper overrides every write method of relationtuple.Manager
+    # (internal/relationtuple/definitions.go:28-34)
+    for m in ("WriteRelationTuples", "DeleteRelationTuples", "DeleteAllRelationTuples", "TransactRelationTuples"):
+        assert re.search(r"func \(p \*gpuPersister\) " + m + r"\(", reg), m
