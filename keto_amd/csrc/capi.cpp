@@ -319,22 +319,29 @@ int64_t copy_out(const std::string& s, char* buf, uint64_t cap) {
     return (int64_t)s.size();
 }
 
-// resolve_checks over a whole batch on host threads (the first error wins)
-void resolve_all(const Snapshot& S, const keto_check_req* reqs, uint32_t n, keto_check_ids* ids, uint8_t* st,
-                 uint8_t* wild, RowKey* wkey) {
+// resolve_checks over a whole batch on host threads (the first error wins); the wildcard requests
+// come back in request order
+std::vector<WildReq> resolve_all(const Snapshot& S, const keto_check_req* reqs, uint32_t n, keto_check_ids* ids,
+                                 uint8_t* st) {
     std::atomic<bool> failed{false};
     Error first{KETO_OK, ""};
     std::mutex emu;
-    par_chunks(n, n >= 65536 ? build_threads() : 1u, 4096, [&](uint64_t b, uint64_t e, unsigned) {
+    const unsigned th = n >= 65536 ? build_threads() : 1u;
+    std::vector<std::vector<WildReq>> wild(th);
+    par_chunks(n, th, 4096, [&](uint64_t b, uint64_t e, unsigned t) {
         if (failed) return;
         try {
-            resolve_checks(S, reqs, b, e, ids, st, wild, wkey);
+            resolve_checks(S, reqs, b, e, ids, st, wild[t]);
         } catch (const Error& x) {
             std::lock_guard<std::mutex> lk(emu);
             if (!failed.exchange(true)) first = x;
         }
     });
     if (failed) throw first;
+    std::vector<WildReq> all;
+    for (auto& w : wild) all.insert(all.end(), w.begin(), w.end());
+    std::sort(all.begin(), all.end(), [](const WildReq& a, const WildReq& b) { return a.i < b.i; });
+    return all;
 }
 
 }  // namespace
@@ -402,15 +409,12 @@ int keto_resolve_checks(const keto_snapshot* h, const keto_check_req* reqs, uint
     return guarded([&] {
         if (!h || (n && (!reqs || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
         std::shared_lock<std::shared_mutex> lk(h->s->rw);
-        std::vector<uint8_t> st(n), wild(n);
-        std::vector<RowKey> wkey(n);
-        resolve_all(*h->s, reqs, n, out, st.data(), wild.data(), wkey.data());
-        for (uint32_t i = 0; i < n; ++i) {
-            if (wild[i]) throw Error{KETO_E_INVALID, "request " + std::to_string(i) +
-                                                         " is a wildcard query that no stored subject set uses; "
-                                                         "pass it to keto_check_batch"};
-            if (status_out) status_out[i] = st[i];
-        }
+        std::vector<uint8_t, NoInitAlloc<uint8_t>> st(status_out ? 0 : n);
+        const auto wild = resolve_all(*h->s, reqs, n, out, status_out ? status_out : st.data());
+        if (!wild.empty())
+            throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
+                                            " is a wildcard query that no stored subject set uses; "
+                                            "pass it to keto_check_batch"};
         return KETO_OK;
     });
 }
@@ -422,18 +426,16 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
         std::shared_lock<std::shared_mutex> lk(h->s->rw);
         Snapshot& S = *h->s;
         const auto t0 = std::chrono::steady_clock::now();
-        std::vector<keto_check_ids> ids(n);
+        // resolution (whereQuery on the snapshot) on host threads into uninitialized buffers (every
+        // entry is written); wildcard requests that need a batch-local overlay row are materialized
+        // afterwards, in request order
+        std::vector<keto_check_ids, NoInitAlloc<keto_check_ids>> ids(n);
+        std::vector<uint8_t, NoInitAlloc<uint8_t>> st(status_out ? 0 : n);
+        uint8_t* status = status_out ? status_out : st.data();
         Overlay ov;
         ov.base = S.n_rows();
-        // resolution (whereQuery on the snapshot) on host threads; wildcard requests that need a
-        // batch-local overlay row are materialized afterwards, in request order
-        std::vector<uint8_t> st(n), wild(n);
-        std::vector<RowKey> wkey(n);
-        resolve_all(S, reqs, n, ids.data(), st.data(), wild.data(), wkey.data());
-        for (uint32_t i = 0; i < n; ++i) {
-            if (wild[i]) ids[i].row = handle_of(S, &ov, overlay_row(S, ov, wkey[i]));
-            if (status_out) status_out[i] = st[i];
-        }
+        for (const WildReq& w : resolve_all(S, reqs, n, ids.data(), status))
+            ids[w.i].row = handle_of(S, &ov, overlay_row(S, ov, w.key));
         S.last_resolve_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
         device_check_host(S, ids.data(), n, global_max_depth, allowed_out, FORM_HANDLES, 0, &ov);
         if (status_out)

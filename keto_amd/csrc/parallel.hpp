@@ -123,17 +123,44 @@ inline uint64_t mix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
+inline uint64_t load64(const char* p) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    return w;
+}
+inline uint32_t load32(const char* p) {
+    uint32_t w;
+    std::memcpy(&w, p, 4);
+    return w;
+}
+
+// 64-bit hash of a byte string.  Short strings (the usual identifiers) take no loop and no
+// variable-length copy: 1..3 bytes are read as first / middle / last byte, 4..8 as two overlapping
+// 32-bit words, 9..16 as two overlapping 64-bit words -- together they cover every byte, so two
+// strings of one length that differ anywhere differ in the mixed words.
 inline uint64_t hash_bytes(std::string_view s, uint64_t seed = 0x9E3779B97F4A7C15ull) {
-    uint64_t h = seed ^ (s.size() * 0xC2B2AE3D27D4EB4Full);
-    size_t i = 0;
-    for (; i + 8 <= s.size(); i += 8) {
-        uint64_t w;
-        std::memcpy(&w, s.data() + i, 8);
-        h = mix64(h ^ w) * 0x9E3779B97F4A7C15ull;
+    const char* p = s.data();
+    const size_t n = s.size();
+    uint64_t h = seed ^ (n * 0xC2B2AE3D27D4EB4Full);
+    uint64_t a, b;
+    if (n <= 16) {
+        if (n >= 8) {
+            a = load64(p);
+            b = load64(p + n - 8);
+        } else if (n >= 4) {
+            a = load32(p);
+            b = load32(p + n - 4);
+        } else if (n > 0) {
+            a = (uint64_t)(uint8_t)p[0] | (uint64_t)(uint8_t)p[n / 2] << 8 | (uint64_t)(uint8_t)p[n - 1] << 16;
+            b = 0;
+        } else {
+            a = b = 0;
+        }
+        return mix64(mix64(h ^ a) * 0x9E3779B97F4A7C15ull ^ b);
     }
-    uint64_t w = 0;
-    std::memcpy(&w, s.data() + i, s.size() - i);
-    return mix64(h ^ w ^ ((uint64_t)(s.size() - i) << 56));
+    size_t i = 0;
+    for (; i + 8 < n; i += 8) h = mix64(h ^ load64(p + i)) * 0x9E3779B97F4A7C15ull;
+    return mix64(h ^ load64(p + n - 8));
 }
 
 }  // namespace keto

@@ -332,10 +332,15 @@ struct Error {
 
 // named check requests [b, e) -> device form (resolve.cpp; the role of whereQuery,
 // internal/persistence/sql/relationtuples.go:178-198): out[i], status[i] (KETO_CHECK_*), and for a
-// wildcard query that no stored subject set materialized wild[i] = 1 with its key in wkey[i].  Throws
+// wildcard query that no stored subject set materialized an entry {i, its key} appended to `wild`
+// (out[i].row is then KETO_NO_ROW until the caller gives it a batch-local row).  Throws
 // KETO_E_INVALID for a top-level row another part owns.
+struct WildReq {
+    uint32_t i;
+    RowKey key;
+};
 void resolve_checks(const Snapshot& S, const keto_check_req* q, uint64_t b, uint64_t e, keto_check_ids* out,
-                    uint8_t* status, uint8_t* wild, RowKey* wkey);
+                    uint8_t* status, std::vector<WildReq>& wild);
 
 std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns, const keto_tuple* t, uint64_t n,
                                          uint32_t page_size);

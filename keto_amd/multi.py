@@ -1,4 +1,5 @@
-"""Multi-GPU check batches: one process per GPU, every rank holding the whole (replicated) snapshot.
+"""Multi-GPU check and expand batches: one process per GPU, every rank holding the whole (replicated)
+snapshot, or a part of an edge-partitioned one.
 
 The check path shards by request: requests are independent, so a batch is split into contiguous
 per-rank shards, each rank runs its shard through its own GPU's engine, and the decisions are
@@ -116,6 +117,151 @@ class PartitionedChecker:
         res = np.empty(n, dtype=np.uint8)
         res[order] = back.cpu().numpy()
         return res
+
+
+# ---------------------------------------------------------------------------------------------
+# Expand across GPUs ("roots split across GPUs").  A batch of BuildTree roots
+# (internal/expand/engine.go:33-102) is as independent as a batch of checks: every tree is built by
+# one DFS with its own visited map.  Trees travel as the engine's arena: per root a status and a
+# pre-order node list (keto_tree_node: subject = bit31 | row id, or a string id; info = leaf bit |
+# child count).  Row and string ids are the host snapshot's, the same on every rank (every part is
+# uploaded from the same build), so a tree expanded on one GPU reads the same on any other.
+
+_TREE_NODE = np.dtype([("subject", "<u4"), ("info", "<u4")])
+
+
+def _pack_trees(status, offsets, nodes):
+    """(status int32 [n], offsets int64 [n+1], nodes uint32 [m, 2]) -> one int64 header per root
+    (status << 40 | node count) and the uint32 node words."""
+    status = np.asarray(status, dtype=np.int64)
+    counts = np.diff(np.asarray(offsets, dtype=np.int64))
+    return status << 40 | counts, np.ascontiguousarray(nodes, dtype=np.uint32).reshape(-1)
+
+
+def _unpack_trees(head, words):
+    status = (head >> 40).astype(np.int32)
+    counts = head & ((1 << 40) - 1)
+    offsets = np.zeros(len(head) + 1, dtype=np.int64)
+    np.cumsum(counts, out=offsets[1:])
+    return status, offsets, words.reshape(-1, 2)
+
+
+class ShardedExpander:
+    """Replicated snapshot: each rank expands its contiguous shard of the roots on its own GPU
+    (local_expand(roots, depths) -> (status, offsets, nodes), e.g. Snapshot.expand_batch_ids), and
+    the trees are all-gathered so every rank returns the whole batch's trees, in root order."""
+
+    def __init__(self, local_expand, group=None, device: str = "cpu"):
+        import torch.distributed as dist
+        self.local_expand = local_expand
+        self.group = group
+        self.device = device
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def _gather(self, arr: np.ndarray, width: int):
+        import torch
+        import torch.distributed as dist
+        buf = torch.zeros(width, dtype=torch.int64 if arr.dtype == np.int64 else torch.int32, device=self.device)
+        if len(arr):
+            buf[: len(arr)] = torch.from_numpy(arr.view(np.int32) if arr.dtype == np.uint32 else arr).to(self.device)
+        out = torch.empty(width * self.world, dtype=buf.dtype, device=self.device)
+        dist.all_gather_into_tensor(out, buf, group=self.group)
+        return out.cpu().numpy()
+
+    def __call__(self, roots: np.ndarray, depths: np.ndarray):
+        import torch
+        import torch.distributed as dist
+        n = len(roots)
+        lo, hi = shard_bounds(n, self.rank, self.world)
+        st, off, nd = self.local_expand(roots[lo:hi], depths[lo:hi])
+        if len(st) != hi - lo:
+            raise RuntimeError(f"local engine returned {len(st)} trees for {hi - lo} roots")
+        head, words = _pack_trees(st, off, nd)
+        sizes = torch.tensor([len(words)], dtype=torch.int64, device=self.device)
+        all_sizes = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(all_sizes, sizes, group=self.group)
+        all_sizes = all_sizes.cpu().tolist()
+        hw = shard_bounds(n, 0, self.world)[1]
+        heads = self._gather(head, hw)
+        ww = max(1, max(all_sizes))
+        wordss = self._gather(words, ww).view(np.uint32)
+        h_all, w_all = [], []
+        for r in range(self.world):
+            a, b = shard_bounds(n, r, self.world)
+            h_all.append(heads[r * hw: r * hw + (b - a)])
+            w_all.append(wordss[r * ww: r * ww + all_sizes[r]])
+        return _unpack_trees(np.concatenate(h_all) if h_all else np.zeros(0, np.int64),
+                             np.concatenate(w_all) if w_all else np.zeros(0, np.uint32))
+
+
+class PartitionedExpander:
+    """Edge-partitioned snapshot (KETO_PART_SHARED): a tree below its root only visits subject-set
+    targets, which every part holds, so each root is expanded on the part that owns its row (root rows
+    by hash(namespace_id, object); other rows and subject-id roots where they are) and the trees come
+    back with one all-to-all.  roots: keto_expand_batch_ids form (bit31 | row id for subject sets).
+    owner(rows) -> int32 part per row id (-1 = every part), e.g. Snapshot.row_owner."""
+
+    def __init__(self, owner, local_expand, group=None, device: str = "cpu"):
+        import torch.distributed as dist
+        self.owner = owner
+        self.local_expand = local_expand
+        self.group = group
+        self.device = device
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.last_routed = 0
+
+    def _a2a(self, send: np.ndarray, sc, rc, dtype):
+        import torch
+        import torch.distributed as dist
+        t = torch.from_numpy(np.ascontiguousarray(send).view(dtype)).to(self.device)
+        out = torch.empty(int(sum(rc)), dtype=t.dtype, device=self.device)
+        dist.all_to_all_single(out, t, output_split_sizes=[int(x) for x in rc],
+                               input_split_sizes=[int(x) for x in sc], group=self.group)
+        return out.cpu().numpy()
+
+    def __call__(self, roots: np.ndarray, depths: np.ndarray):
+        import torch
+        import torch.distributed as dist
+        roots = np.ascontiguousarray(roots, dtype=np.uint32)
+        depths = np.ascontiguousarray(depths, dtype=np.int32)
+        n = len(roots)
+        is_set = (roots >> 31).astype(bool)
+        dest = np.full(n, self.rank, dtype=np.int64)
+        if is_set.any():
+            own = np.asarray(self.owner(roots[is_set] & np.uint32(0x7FFFFFFF)), dtype=np.int64)
+            dest[is_set] = np.where(own < 0, self.rank, own)
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=self.world).astype(np.int64)
+        c_in = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(c_in, torch.from_numpy(counts).to(self.device), group=self.group)
+        in_counts = c_in.cpu().numpy()
+        req = np.empty(n, dtype=[("root", "<u4"), ("depth", "<i4")])
+        req["root"], req["depth"] = roots, depths
+        mine = self._a2a(req[order].view(np.int64), counts, in_counts, np.int64).view(req.dtype)
+        self.last_routed = len(mine)
+        st, off, nd = self.local_expand(mine["root"].copy(), mine["depth"].copy())
+        head, words = _pack_trees(st, off, nd)
+        # per source rank: its roots' headers, then their node words
+        src_bounds = _prefix(in_counts)
+        w_counts = [int(off[src_bounds[r + 1]] - off[src_bounds[r]]) * 2 for r in range(self.world)]
+        w_in = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(w_in, torch.tensor(w_counts, dtype=torch.int64, device=self.device), group=self.group)
+        back_heads = self._a2a(head, in_counts, counts, np.int64)
+        back_words = self._a2a(words.view(np.int32), w_counts, w_in.cpu().tolist(), np.int32).view(np.uint32)
+        st_b, off_b, nd_b = _unpack_trees(back_heads, back_words)
+        # back in the caller's root order
+        res_counts = np.empty(n, dtype=np.int64)
+        res_status = np.empty(n, dtype=np.int32)
+        res_counts[order] = np.diff(off_b)
+        res_status[order] = st_b
+        offsets = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(res_counts, out=offsets[1:])
+        nodes = np.empty((int(offsets[-1]), 2), dtype=np.uint32)
+        for j, i in enumerate(order):
+            nodes[offsets[i]:offsets[i + 1]] = nd_b[off_b[j]:off_b[j + 1]]
+        return res_status, offsets, nodes
 
 
 def _a2a(out, inp, out_splits=None, in_splits=None, group=None, comm_device=None):

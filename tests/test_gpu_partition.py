@@ -189,3 +189,34 @@ def test_device_routing_loopback_matches_replicated(n_parts):
         capi.unroute_device(dec.data_ptr(), order.data_ptr(), n, out.data_ptr())
         torch.cuda.synchronize()
         assert (out.cpu().numpy() == want).all()
+
+
+@pytest.mark.parametrize("n_parts", [2, 3])
+def test_expand_on_parts_matches_replicated(n_parts):
+    """Expand on a shared-rows partition (the PartitionedExpander's local step, loopback on one GPU):
+    every root expanded on the part that owns its row gives the replicated snapshot's tree, node for
+    node; a part refuses another part's root row."""
+    from keto_amd.capi import KetoError
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 512), threads=16)
+    full = g.snapshot(device=0)
+    rng = np.random.default_rng(50 + n_parts)
+    n = 6000
+    rows = rng.integers(0, g.n_rows, size=n).astype(np.uint32)
+    roots = rows | np.uint32(0x80000000)
+    depths = rng.integers(-1, 7, size=n).astype(np.int32)
+    st_w, off_w, nd_w = full.expand_batch_ids(roots, depths, 5)
+    own = full.row_owner(rows, n_parts)
+    assert (own >= 0).any() and (own < 0).any()
+    for p in range(n_parts):
+        part = g.snapshot_part(p, n_parts, device=0)
+        sel = np.flatnonzero((own == p) | ((own < 0) & (np.arange(n) % n_parts == p)))
+        st, off, nd = part.expand_batch_ids(roots[sel], depths[sel], 5)
+        assert (st == st_w[sel]).all()
+        for j, i in enumerate(sel):
+            assert (nd[off[j]:off[j + 1]] == nd_w[off_w[i]:off_w[i + 1]]).all(), (p, int(rows[i]))
+        other = roots[own == (p + 1) % n_parts][:4]
+        if len(other):
+            with pytest.raises(KetoError):
+                part.expand_batch_ids(other, np.zeros(len(other), dtype=np.int32), 5)
+        del part

@@ -302,3 +302,101 @@ def test_migrating_dfs_gloo(tmp_path, world):
     assert (got == want).all(), f"{int((got != want).sum())} mismatches"
     assert int(np.load(out + ".0.rounds.npy")[0]) >= 2          # searches crossed parts
     assert 0.05 < want.mean() < 0.95
+
+
+# ---- expand across ranks: ShardedExpander (replicated) and PartitionedExpander (shared-rows
+# partition), with the C oracle's BuildTree as each rank's local engine, against a single-process run
+
+def _oracle_arena(g, roots, depths, gmd=5):
+    """keto_expand_batch_ids' (status, offsets, nodes) from the C oracle (oracle/keto_oracle.c
+    ora_expand): set subjects as bit31 | row id, ids as string ids."""
+    from tests.test_gpu_synth import _oracle_expand_nodes
+    rows = (roots & np.uint32(0x7FFFFFFF)).astype(np.uint32)
+    q = np.zeros(len(rows), dtype=[("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
+    q["row"] = rows
+    status = np.zeros(len(roots), dtype=np.int32)
+    offsets = np.zeros(len(roots) + 1, dtype=np.int64)
+    nodes = []
+    if len(roots):
+        tab = g.oracle_table(q, gmd)
+        key = {(int(a), int(b), int(c)): r for r, (a, b, c) in enumerate(zip(g.row_ns, g.row_obj, g.row_rel))}
+        for i, (row, d) in enumerate(zip(rows, depths)):
+            if not roots[i] >> 31:                      # a SubjectID root is a leaf (engine.go:97-101)
+                nodes.append((int(roots[i]), 0x80000000))
+                offsets[i + 1] = len(nodes)
+                continue
+            r, tree = _oracle_expand_nodes(g, tab, int(row), int(d), gmd)
+            status[i] = 0 if r == 1 else 1
+            for leaf, is_set, sid, name, obj, rel, nc in tree:
+                subj = (0x80000000 | key[(name - 0xFFFF0000, obj, rel)]) if is_set else sid
+                nodes.append((subj, (0x80000000 if leaf else 0) | nc))
+            offsets[i + 1] = len(nodes)
+    return status, offsets, np.array(nodes, dtype=np.uint32).reshape(-1, 2)
+
+
+def _expand_worker(rank, world, port, roots_b, depths_b, mode, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from keto_amd.multi import PartitionedExpander, ShardedExpander
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    roots = np.frombuffer(roots_b, dtype=np.uint32)
+    depths = np.frombuffer(depths_b, dtype=np.int32)
+    if mode == "sharded":
+        st, off, nd = ShardedExpander(lambda r, d: _oracle_arena(g, r, d))(roots, depths)
+    else:
+        host = g.host_snapshot()
+        seen = []
+
+        def local(r, d):
+            sets = (r >> 31).astype(bool)
+            own = host.row_owner(r[sets] & np.uint32(0x7FFFFFFF), world)
+            assert ((own == rank) | (own < 0)).all(), "a root reached a part that does not own its row"
+            seen.append(int((own == rank).sum()))
+            return _oracle_arena(g, r, d)
+
+        half = len(roots) // 2
+        lo, hi = (0, half) if rank == 0 else (half, len(roots))
+        ex = PartitionedExpander(lambda rows: host.row_owner(rows, world), local)
+        st, off, nd = ex(roots[lo:hi], depths[lo:hi])
+        np.save(out_path + f".{rank}.seen.npy", np.array(seen))
+    np.save(out_path + f".{rank}.st.npy", st)
+    np.save(out_path + f".{rank}.off.npy", off)
+    np.save(out_path + f".{rank}.nd.npy", nd)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["sharded", "partitioned"])
+def test_expanders_gloo_world2(tmp_path, mode):
+    """Trees of roots split across two ranks (replicated) or routed to the part owning their row
+    (shared-rows partition) come back in root order, equal to one process expanding them all."""
+    import torch.multiprocessing as mp
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 8192), threads=2)
+    rng = np.random.default_rng(3)
+    n = 301
+    roots = rng.integers(0, g.n_rows, size=n).astype(np.uint32) | np.uint32(0x80000000)
+    roots[::17] = rng.integers(0, 1000, size=len(roots[::17])).astype(np.uint32)     # subject-id roots
+    depths = rng.integers(0, 6, size=n).astype(np.int32)
+    want = _oracle_arena(g, roots, depths)
+    out = str(tmp_path / "res")
+    mp.start_processes(_expand_worker, args=(2, _free_port(), roots.tobytes(), depths.tobytes(), mode, out),
+                       nprocs=2, join=True, start_method="spawn")
+    if mode == "sharded":
+        for r in range(2):              # every rank holds the whole batch
+            st, off, nd = (np.load(out + f".{r}.{k}.npy") for k in ("st", "off", "nd"))
+            assert (st == want[0]).all() and (off == want[1]).all() and (nd == want[2]).all()
+    else:
+        parts = [tuple(np.load(out + f".{r}.{k}.npy") for k in ("st", "off", "nd")) for r in range(2)]
+        st = np.concatenate([p[0] for p in parts])
+        assert (st == want[0]).all()
+        for i in range(n):
+            p, j = (0, i) if i < n // 2 else (1, i - n // 2)
+            off, nd = parts[p][1], parts[p][2]
+            assert (nd[off[j]:off[j + 1]] == want[2][want[1][i]:want[1][i + 1]]).all(), i
+        host = g.host_snapshot()
+        own = host.row_owner(roots[roots >> 31 == 1] & np.uint32(0x7FFFFFFF), 2)
+        routed = int(np.load(out + ".0.seen.npy").sum() + np.load(out + ".1.seen.npy").sum())
+        assert routed == int((own >= 0).sum()) and routed > 0

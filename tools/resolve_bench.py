@@ -21,7 +21,9 @@ def main():
     ap.add_argument("--n", type=int, default=4_000_000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--groups", default="16", help="KETO_RESOLVE_GROUP values to time (comma-separated)")
     a = ap.parse_args()
+    os.environ["KETO_BUILD_THREADS"] = str(a.threads)
     from tools import synth
     t0 = time.perf_counter()
     g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, a.scale), threads=a.threads)
@@ -34,17 +36,21 @@ def main():
     t0 = time.perf_counter()
     snap.resolve_checks_reqs(reqs, 1)                       # builds the indexes
     t_index = time.perf_counter() - t0
-    ts = []
-    for _ in range(a.reps):
-        t0 = time.perf_counter()
-        got, st = snap.resolve_checks_reqs(reqs, len(q))
-        ts.append(time.perf_counter() - t0)
-    bad = int((got != want).sum()) + int((st != 0).sum())
-    best = min(ts)
+    per_group = {}
+    bad = 0
+    for grp in a.groups.split(","):
+        os.environ["KETO_RESOLVE_GROUP"] = grp
+        ts = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            got, st = snap.resolve_checks_reqs(reqs, len(q))
+            ts.append(time.perf_counter() - t0)
+        bad += int((got != want).sum()) + int((st != 0).sum())
+        best = min(ts)
+        per_group[grp] = {"resolve_ms": round(best * 1e3, 2), "requests_per_s": round(a.n / best, 1)}
     print(json.dumps({"tuples": int(g.n_edges), "rows": int(g.n_rows), "strings": int(u.n_strings), "requests": a.n,
                       "threads": a.threads, "build_s": round(t_build, 2), "index_s": round(t_index, 2),
-                      "resolve_ms": round(best * 1e3, 2), "requests_per_s": round(a.n / best, 1),
-                      "mismatches_vs_id_path": bad}))
+                      "by_group": per_group, "mismatches_vs_id_path": bad}))
 
 
 if __name__ == "__main__":
