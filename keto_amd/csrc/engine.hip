@@ -3332,6 +3332,9 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
         HIP_OK(hipEventRecord(kern_done[k], cs));
         HIP_OK(hipStreamWaitEvent(D.copy_out, kern_done[k], 0));
         if (!pinned && c >= 2) drain(c - 2);
+        // decisions come home by a copy: the checks storing them straight into a pinned caller buffer
+        // (scattered 4-B writes over PCIe) took 10-11 ms per batch instead of 3.5
+        // (profiles/r03f_e2e_zerocopy_rejected.log)
         HIP_OK(hipMemcpyAsync(pinned ? allowed + lo(c) : D.pin_a[k], D.slot_a[k], len(c), hipMemcpyDeviceToHost,
                               D.copy_out));
         HIP_OK(hipEventRecord(out_done[k], D.copy_out));
