@@ -13,14 +13,15 @@
 // Snapshot::row_over; device_apply (engine.hip) rewrites those rows in the device arena.  New strings
 // are appended after the build's byte-ordered ones and compared by bytes wherever order matters.
 //
-// Writes outside this delta path throw KETO_E_REBUILD and leave the snapshot unchanged; the caller
-// rebuilds it (keto_snapshot_build from the table).  They are the ones that would change what the
-// build derived globally: a new Subject.String() collision, a stored subject set with an empty field
-// (a materialized wildcard row), a row that a stored wildcard set materializes, a poisoned row, or a
-// partitioned snapshot.
+// A write that creates a Subject.String() collision gives the colliding subjects a collision class and
+// re-flags the rows that hold them ROW_SEQ, as the build would have.  Writes outside this delta path
+// throw KETO_E_REBUILD and leave the snapshot unchanged; the caller rebuilds it (keto_snapshot_build
+// from the table): a stored subject set with an empty field (a materialized wildcard row), a row that
+// a stored wildcard set materializes, a poisoned row.  A partitioned snapshot takes no writes.
 #include <algorithm>
 #include <cstring>
 
+#include "parallel.hpp"
 #include "snapshot.hpp"
 
 namespace keto {
@@ -211,6 +212,74 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
         std::vector<uint32_t>& e = T.edges((uint32_t)r);
         e.erase(std::remove(e.begin(), e.end(), v), e.end());
     }
+    // ---- Subject.String() collisions (graph_utils.go:13-35 keys) this transaction creates: a new row
+    // whose String() is another subject's (a subject id -- conservatively, any existing string -- or
+    // another row's), or a new subject id equal to some row's String().  The typed subjects sharing
+    // a key get one collision class as their visit id (an existing class is joined), and every row
+    // holding one of them as an edge is walked edge by edge from now on (ROW_SEQ), as the build does
+    // (snapshot.cpp, collision classes); its closure filter becomes all ones, and the re-closing in
+    // device_apply carries that up to every row above it, so pruning stays exact.
+    std::unordered_map<uint32_t, uint32_t> new_coll;     // edge value -> class (values not classed before)
+    uint32_t classes = 0;
+    {
+        std::unordered_map<std::string, std::vector<uint32_t>> groups;
+        auto group_of = [&](const std::string& ks) -> std::vector<uint32_t>& {
+            auto it = groups.find(ks);
+            if (it != groups.end()) return it->second;
+            std::vector<uint32_t>& g = groups[ks];
+            for (uint32_t r : S.rows_of_string(ks)) g.push_back(EDGE_SET | r);
+            const int64_t sid = T.str(ks, false);       // existing or staged string
+            if (sid >= 0) g.push_back((uint32_t)sid);
+            return g;
+        };
+        for (uint32_t i = 0; i < T.new_keys.size(); ++i) {
+            const uint32_t r = (uint32_t)S.row_key.size() + i;
+            group_of(key_string(S, T, T.key(r))).push_back(EDGE_SET | r);
+        }
+        for (uint64_t i = 0; i < n_ins; ++i) {
+            const keto_tuple& t = ins[i];
+            if (t.subject_kind) continue;
+            const std::string_view sid = sv(t.subject_id);
+            if (sid.find(':') == std::string_view::npos || sid.find('#') == std::string_view::npos) continue;
+            group_of(std::string(sid));                  // holds the id itself (staged string)
+        }
+        for (auto& kv : groups) {
+            std::vector<uint32_t>& g = kv.second;
+            std::sort(g.begin(), g.end());
+            g.erase(std::unique(g.begin(), g.end()), g.end());
+            if (g.size() < 2) continue;
+            uint32_t c = NO_UNIT;
+            for (uint32_t v : g) {
+                auto it = S.coll.find(v);
+                if (it != S.coll.end()) c = it->second;
+            }
+            if (c == NO_UNIT) c = VID_CLASS | (S.n_coll_keys + classes++);
+            for (uint32_t v : g)
+                if (!S.coll.count(v)) new_coll[v] = c;
+        }
+    }
+    if (!new_coll.empty()) {
+        // the rows holding a newly classed subject as an edge (rows already ROW_SEQ look classes up as
+        // they walk): a parallel scan of every row's current edges
+        const uint32_t R = S.n_rows();
+        std::vector<uint8_t> hit(R, 0);
+        auto holds = [&](const uint32_t* e, uint64_t n) {
+            for (uint64_t i = 0; i < n; ++i)
+                if (new_coll.count(e[i])) return true;
+            return false;
+        };
+        par_chunks(R, R >= par_min() ? build_threads() : 1u, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t r = b; r < e; ++r) {
+                if (S.row_flags((uint32_t)r) & ROW_SEQ) continue;
+                auto st = T.rows.find((uint32_t)r);
+                if (st != T.rows.end()) continue;        // staged rows: checked below
+                const auto ed = S.row_edges((uint32_t)r);
+                if (holds(ed.first, ed.second)) hit[r] = 1;
+            }
+        });
+        for (uint32_t r = 0; r < R; ++r)
+            if (hit[r]) T.edges(r);                      // re-imaged with the new flag (poisoned: rebuild)
+    }
     // ---- what the delta path cannot express: the caller rebuilds
     for (uint32_t r : T.order) {
         if (r < S.rows.size()) {
@@ -229,33 +298,13 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
             }
         }
     }
-    {
-        // Subject.String() collisions (graph_utils.go:13-35 keys): a new row whose String() is an
-        // existing string (a subject id, or any text: conservative) or another row's, and a new
-        // subject id equal to some row's String()
-        auto row_key_str = [&](uint32_t r) { return key_string(S, T, T.key(r)); };
-        std::unordered_map<std::string, uint32_t> written_keys;
-        for (uint32_t i = 0; i < T.new_keys.size(); ++i) {
-            const uint32_t r = (uint32_t)S.row_key.size() + i;
-            const std::string ks = row_key_str(r);
-            if (S.lookup_str(ks) >= 0 || T.new_str_id.count(ks) || S.vid_of_key(ks) != 0xFFFFFFF0u ||
-                written_keys.count(ks))
-                throw Error{KETO_E_REBUILD, "a new row's key collides with another subject's (Subject.String())"};
-            written_keys.emplace(ks, r);
-        }
-        for (uint64_t i = 0; i < n_ins; ++i) {
-            const keto_tuple& t = ins[i];
-            if (t.subject_kind) continue;
-            const std::string_view sid = sv(t.subject_id);
-            if (sid.find(':') == std::string_view::npos || sid.find('#') == std::string_view::npos) continue;
-            const int64_t id = T.str(sid, false);
-            if (id >= 0 && S.coll.count((uint32_t)id)) continue;           // an existing collision class
-            if (S.vid_of_key(std::string(sid)) != 0xFFFFFFF0u || written_keys.count(std::string(sid)))
-                throw Error{KETO_E_REBUILD, "a subject id collides with a subject set's String()"};
-        }
-    }
     // ---- commit
     const uint32_t R0 = S.n_rows();
+    if (!new_coll.empty()) {
+        for (auto& kv : new_coll) S.coll[kv.first] = kv.second;
+        S.n_coll_keys += classes;
+        S.coll_dirty = true;
+    }
     for (auto& x : T.new_strs) {
         S.added_str.emplace(x, (uint32_t)S.strs.size());
         S.strs.push_back(std::move(x));
@@ -269,7 +318,6 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
         S.is_root.push_back(1);
         S.row_cb.push_back(0);
     }
-    if (!T.new_keys.empty()) S.key_index.reset();
     S.dirty.clear();
     S.needs_cb.clear();
     for (uint32_t r : T.order) {

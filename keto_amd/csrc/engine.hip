@@ -2225,6 +2225,31 @@ void build_closures(const Snapshot& S, uint32_t* d_arena) {
 
 }  // namespace
 
+// The device's collision table: edge value (subject sets by handle) -> visit id of its class.
+void upload_coll(Snapshot& S, DeviceState& D, uint64_t& acc) {
+    if (D.coll) (void)hipFree(D.coll);
+    D.coll = nullptr;
+    D.coll_mask = 0;
+    S.coll_dirty = false;
+    if (S.coll.empty()) return;
+    uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
+    std::vector<uint64_t> tab(cap, ~0ull);
+    for (auto& kv : S.coll) {
+        uint32_t key = kv.first;
+        if (key & EDGE_SET) {
+            if (!S.mapped(key & EDGE_VAL)) continue;     // another part's row (stubs are mapped)
+            key = EDGE_SET | S.unit_of_row[key & EDGE_VAL];   // row -> handle
+        }
+        uint32_t vid = kv.second;
+        uint32_t i = mix32(key) & (cap - 1);
+        while (tab[i] != ~0ull) i = (i + 1) & (cap - 1);
+        tab[i] = ((uint64_t)key << 32) | vid;
+    }
+    D.coll = dmalloc<uint64_t>(cap, acc);
+    HIP_OK(hipMemcpy(D.coll, tab.data(), cap * sizeof(uint64_t), hipMemcpyHostToDevice));
+    D.coll_mask = cap - 1;
+}
+
 void device_upload(Snapshot& S, int device) {
     int n_dev = 0;
     if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev <= 0) throw Error{KETO_E_HIP, "no HIP device"};
@@ -2260,24 +2285,7 @@ void device_upload(Snapshot& S, int device) {
     HIP_OK(hipMemcpy(D->arena, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     build_closures(S, D->arena);
     S.mig_ready = !(S.part_mode == PART_MIGRATE && S.n_parts > 1);   // else after the filter exchange
-    if (!S.coll.empty()) {
-        uint32_t cap = pow2_at_least(S.coll.size() * 2 + 2);
-        std::vector<uint64_t> tab(cap, ~0ull);
-        for (auto& kv : S.coll) {
-            uint32_t key = kv.first;
-            if (key & EDGE_SET) {
-                if (!S.mapped(key & EDGE_VAL)) continue;     // another part's row (stubs are mapped)
-                key = EDGE_SET | S.unit_of_row[key & EDGE_VAL];   // row -> handle
-            }
-            uint32_t vid = kv.second;
-            uint32_t i = mix32(key) & (cap - 1);
-            while (tab[i] != ~0ull) i = (i + 1) & (cap - 1);
-            tab[i] = ((uint64_t)key << 32) | vid;
-        }
-        D->coll = dmalloc<uint64_t>(cap, acc);
-        HIP_OK(hipMemcpy(D->coll, tab.data(), cap * sizeof(uint64_t), hipMemcpyHostToDevice));
-        D->coll_mask = cap - 1;
-    }
+    upload_coll(S, *D, acc);
     D->bytes = acc;
     // a map holds at most one id per row / collision class (+ an expand root outside the rows)
     D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
@@ -2554,7 +2562,15 @@ void device_apply(Snapshot& S) {
     HIP_OK(hipStreamSynchronize(D.stream));
     // 4. closure filters of every row with one (from their own ids up)
     build_closures(S, D.arena);
-    // 5. what the kernels and expand output read next
+    // 5. what the kernels and expand output read next: the collision table when a write added
+    // classes or gave a classed row a new identity handle
+    if (!moved.empty() && !S.coll.empty()) S.coll_dirty = true;
+    if (S.coll_dirty) {
+        uint64_t acc = 0;
+        upload_coll(S, D, acc);
+        D.bytes += acc;
+    }
+    D.n_coll = S.n_coll_keys;
     D.n_units = (uint32_t)S.n_units;
     D.vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
     if (!moved.empty()) {

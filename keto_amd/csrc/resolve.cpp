@@ -198,6 +198,50 @@ int64_t Snapshot::resolve_query(std::string_view ns, std::string_view obj, std::
     return -1;
 }
 
+std::vector<uint32_t> Snapshot::rows_of_string(std::string_view key) const {
+    std::vector<uint32_t> out;
+    // the snapshot's subject sets: rows of configured namespaces, and wildcard rows (namespace ANY
+    // prints as ""); a field that is "" is the empty string's id or, in a wildcard row, ANY
+    auto field_ids = [&](std::string_view f, std::vector<uint32_t>& ids) {
+        ids.clear();
+        if (f.empty()) ids.push_back(ANY);
+        const int64_t x = lookup_str(f);
+        if (x >= 0) ids.push_back((uint32_t)x);
+    };
+    std::vector<uint32_t> objs, rels;
+    for (size_t p = key.find(':'); p != std::string_view::npos; p = key.find(':', p + 1)) {
+        const std::string_view ns = key.substr(0, p), rest = key.substr(p + 1);
+        std::vector<int64_t> nss;
+        const int c = ns_index(ns);
+        if (c >= 0) nss.push_back(ns_ids[c]);
+        if (ns.empty()) nss.push_back(ANY_NS);
+        if (nss.empty()) continue;
+        for (size_t q = rest.find('#'); q != std::string_view::npos; q = rest.find('#', q + 1)) {
+            field_ids(rest.substr(0, q), objs);
+            field_ids(rest.substr(q + 1), rels);
+            for (int64_t n : nss)
+                for (uint32_t o : objs)
+                    for (uint32_t r : rels) {
+                        const RowKey k{n, o, r};
+                        int64_t row = n != ANY_NS && o != ANY && r != ANY ? real_row(k) : -1;
+                        if (row < 0) {
+                            auto it = row_of.find(k);
+                            if (it != row_of.end()) row = it->second;
+                        }
+                        if (row >= 0) out.push_back((uint32_t)row);
+                    }
+        }
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
+uint32_t Snapshot::vid_of_key(std::string_view key) const {
+    const std::vector<uint32_t> rows = rows_of_string(key);
+    return rows.empty() ? 0xFFFFFFF0u : vid_of_row(rows[0]);   // 0xFFFFFFF0: no snapshot subject
+}
+
 namespace {
 
 [[noreturn]] void foreign_row(const Snapshot& S, uint32_t row) {

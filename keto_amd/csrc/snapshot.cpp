@@ -292,20 +292,6 @@ int Snapshot::str_cmp(uint32_t a, uint32_t b) const {
     return c < 0 ? -1 : c > 0 ? 1 : 0;
 }
 
-uint32_t Snapshot::vid_of_key(const std::string& key) const {
-    std::lock_guard<std::mutex> lk(key_mu);
-    if (!key_index) {
-        key_index = std::make_unique<std::unordered_map<std::string, uint32_t>>();
-        for (uint32_t r = 0; r < rows.size(); ++r) {
-            const RowKey& k = row_key[r];
-            if (k.ns != ANY_NS && !ns_by_id.count((int32_t)k.ns)) continue;
-            key_index->emplace(subject_string(EDGE_SET | r), vid_of_row(r));
-        }
-    }
-    auto it = key_index->find(key);
-    return it == key_index->end() ? 0xFFFFFFF0u : it->second;   // 0xFFFFFFF0: no snapshot subject
-}
-
 uint32_t overlay_row(const Snapshot& S, Overlay& ov, const RowKey& k) {
     auto f = ov.map.find(k);
     if (f != ov.map.end()) return f->second;

@@ -189,6 +189,7 @@ struct Snapshot {
     // ---- visit-key collisions
     std::unordered_map<uint32_t, uint32_t> coll;             // edge value -> visit id
     uint32_t n_coll_keys = 0;
+    bool coll_dirty = false;                                 // a write added classes: the device table follows
 
     uint64_t n_tuples = 0;
     uint32_t n_poisoned_rows = 0;
@@ -314,10 +315,11 @@ struct Snapshot {
     int64_t resolve_query(std::string_view ns, std::string_view obj, std::string_view rel,
                           RowKey* key_out = nullptr) const;
     // visit id of a Subject.String() key that names no snapshot row: the row sharing the key
-    // (if any), else a fresh id (lazy key index, built on first use)
-    uint32_t vid_of_key(const std::string& key) const;
-    mutable std::unique_ptr<std::unordered_map<std::string, uint32_t>> key_index;
-    mutable std::mutex key_mu;
+    // (if any), else 0xFFFFFFF0 (no snapshot subject has it)
+    uint32_t vid_of_key(std::string_view key) const;
+    // the rows (subject sets) whose Subject.String() is `key` ("ns:obj#rel"; fields may contain ':'
+    // and '#', so every split is tried against the namespaces, strings and row indexes)
+    std::vector<uint32_t> rows_of_string(std::string_view key) const;
     uint32_t vid_of_row(uint32_t row) const;
     std::string subject_string(uint32_t subject_ref) const;
     std::string row_field_ns(uint32_t row) const;

@@ -122,3 +122,63 @@ def test_large_row_growth_and_new_targets():
         (st, js), = snap.expand_batch([(("set", "n", "doc", "view"), 0)], 5)
         assert js == ExpandEngine(store, 5).build_tree(SubjectSet("n", "doc", "view"), 0).to_json()
     assert snap.version() == 5
+
+
+def test_collisions_applied_without_rebuild():
+    """Writes that create Subject.String() collisions (graph_utils.go:13-35 keys) go through the delta
+    path: a subject id equal to an existing set's String() (the DF3 shape), a new row whose String()
+    equals an existing subject id, and two rows with one String() ("a#b"#"c" vs "a"#"b#c").  Each is
+    applied (version + 1, no KETO_E_REBUILD), and every check and expand then equals the SQL oracle."""
+    import keto_amd
+    ns = [(1, "n")]
+    base = [RelationTuple("n", "root", "r", SubjectSet("n", "p", "r")),
+            RelationTuple("n", "p", "r", SubjectSet("n", "q", "r")),
+            RelationTuple("n", "q", "r", SubjectSet("n", "g", "m")),
+            RelationTuple("n", "g", "m", SubjectID("u")),
+            RelationTuple("n", "h", "m", SubjectID("n:x#y")),          # an id that looks like a set
+            RelationTuple("n", "doc", "v", SubjectSet("n", "h", "m")),
+            RelationTuple("n", "a#b", "c", SubjectID("w")),
+            RelationTuple("n", "top", "v", SubjectSet("n", "a#b", "c"))]
+    store = SQLStore(ns, base)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, base), device=0)
+    writes = [
+        # DF3: n:a#r holds the id "n:g#m", checked before the set n:g#m under n:p#r
+        [RelationTuple("n", "a", "r", SubjectID("n:g#m")), RelationTuple("n", "p", "r", SubjectSet("n", "a", "r"))],
+        # a new row n:x#y collides with the subject id "n:x#y"
+        [RelationTuple("n", "x", "y", SubjectID("u2")), RelationTuple("n", "doc", "v", SubjectSet("n", "x", "y"))],
+        # a new row n:a#b#c (object "a", relation "b#c") collides with the row n:a#b#c (object "a#b")
+        [RelationTuple("n", "a", "b#c", SubjectID("w2")), RelationTuple("n", "top", "v", SubjectSet("n", "a", "b#c"))],
+        # more edges to classed subjects, and a delete
+        [RelationTuple("n", "root", "r", SubjectID("n:x#y")), RelationTuple("n", "q", "r", SubjectSet("n", "x", "y"))],
+    ]
+    objs = ["root", "p", "q", "g", "h", "doc", "a#b", "top", "a", "x"]
+    rels = ["r", "m", "v", "c", "y", "b#c"]
+    users = ["u", "u2", "w", "w2", "n:g#m", "n:x#y", "nobody"]
+    for step, ins in enumerate(writes):
+        dels = [base[3]] if step == 3 else []
+        v0 = snap.version()
+        v = snap.apply([_row(ns, t) for t in ins], [_row(ns, t) for t in dels])
+        assert v == v0 + 1, step
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+        assert snap.stats()["n_collision_keys"] >= min(step + 1, 3)
+        reqs = [("n", o, r, ("id", u), d) for o in objs for r in rels for u in users for d in (0, 2, 3)]
+        reqs += [("n", o, r, ("set", "n", so, sr), 0) for o in objs for r in rels for so, sr in
+                 (("g", "m"), ("x", "y"), ("a#b", "c"), ("a", "b#c"))]
+        for g in (3, 5):
+            allowed, _ = snap.check_batch(reqs, g)
+            for (n_, o, r, u, d), a in zip(reqs, allowed):
+                sub = SubjectID(u[1]) if u[0] == "id" else SubjectSet(*u[1:])
+                assert bool(a) == CheckEngine(store, g).subject_is_allowed(RelationTuple(n_, o, r, sub), d), \
+                    (step, g, o, r, u, d)
+            exps = [(("set", "n", o, r), d) for o in objs for r in rels for d in (0, 3)]
+            for ((s_, d), (st, js)) in zip(exps, snap.expand_batch(exps, g)):
+                try:
+                    tr = ExpandEngine(store, g).build_tree(SubjectSet(*s_[1:]), d)
+                    want = ("tree", tr.to_json()) if tr is not None else ("nil", None)
+                except NotFoundError:
+                    want = ("error", None)
+                assert ({0: "tree", 1: "nil", 2: "error"}[st], js) == want, (step, g, s_, d)
+    snap.close()

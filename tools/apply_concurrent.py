@@ -1,0 +1,88 @@
+"""Writes concurrent with reads (tooling): one thread runs keto_check_batch on 1,000,000 string
+requests back to back while another applies TransactRelationTuples of K tuples (keto_snapshot_apply)
+every `--gap-ms`, on config #2's snapshot built from its 10M string tuples.  Reports the check
+batches' latency with and without the writer, the writes' latency under read load, and that the
+untouched requests keep their decisions throughout.  keto_snapshot_apply holds the snapshot's lock
+exclusively, so a write waits for the running batch and the next batch waits for the write.
+
+  python tools/apply_concurrent.py [--k 100] [--gap-ms 20] [--seconds 5]
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pct(xs, p):
+    return round(float(np.percentile(np.asarray(xs) * 1e3, p)), 2) if xs else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--gap-ms", type=float, default=20.0)
+    ap.add_argument("--seconds", type=float, default=5.0)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    from tools import synth
+    g = synth.SynthGraph(dict(synth.DRIVE_10M), threads=a.threads, kind="drive")
+    st = g.string_tuples(seed=11, threads=a.threads)
+    snap, t_build = g.snapshot_from_strings(st, device=0)
+    q = g.queries(1_000_000, seed=2, depth=5, threads=a.threads)
+    reqs = g.string_requests(st, q, threads=a.threads)
+    before, _ = snap.check_batch_reqs(reqs, len(q), 5)
+    hx = lambda v: f"{int(v):08x}"
+    files_view = np.flatnonzero((g.row_ns == 1) & (g.row_rel == 2))
+    rng = np.random.default_rng(7)
+
+    def reads(seconds, lat, bad):
+        t_end = time.perf_counter() + seconds
+        while time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            out, _ = snap.check_batch_reqs(reqs, len(q), 5)
+            lat.append(time.perf_counter() - t0)
+            bad.append(int((out != before).sum()))
+
+    quiet, quiet_bad = [], []
+    reads(a.seconds / 2, quiet, quiet_bad)
+    stop = threading.Event()
+    wlat, serial = [], [0]
+
+    def writer():
+        while not stop.is_set():
+            rows = rng.choice(files_view, size=a.k, replace=False)
+            ins = [(1, hx(g.row_obj[r]), "view", f"uw{serial[0] + i:08x}") for i, r in enumerate(rows)]
+            serial[0] += a.k
+            t0 = time.perf_counter()
+            snap.apply(inserts=ins)
+            snap.apply(deletes=ins)                      # back to the same table: reads stay comparable
+            wlat.append((time.perf_counter() - t0) / 2)
+            time.sleep(a.gap_ms / 1e3)
+
+    loaded, loaded_bad = [], []
+    w = threading.Thread(target=writer)
+    w.start()
+    reads(a.seconds, loaded, loaded_bad)
+    stop.set()
+    w.join()
+    out = {"graph": "drive10m (config #2, built from string tuples)", "tuples": int(g.n_edges),
+           "requests_per_batch": len(q), "write_tuples": a.k, "write_gap_ms": a.gap_ms,
+           "batch_ms_quiet": {"p50": pct(quiet, 50), "p99": pct(quiet, 99), "n": len(quiet)},
+           "batch_ms_with_writes": {"p50": pct(loaded, 50), "p99": pct(loaded, 99), "n": len(loaded)},
+           "write_ms_under_reads": {"p50": pct(wlat, 50), "p99": pct(wlat, 99), "n": len(wlat)},
+           "writes_per_s": round(2 * len(wlat) / a.seconds, 1),
+           "untouched_decisions_changed": int(sum(quiet_bad) + sum(loaded_bad)), "version": int(snap.version())}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
