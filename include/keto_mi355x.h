@@ -368,6 +368,9 @@ typedef struct {
     uint32_t chunks;            /* host-buffer calls: pipeline chunks (0 for device calls) */
     float wall_ms;              /* host-buffer calls: entry to return, H2D + checks + D2H */
     float resolve_ms;           /* keto_check_batch: name resolution on host threads before the device part */
+    float items_ms;             /* deep batches (max-depth > 9): top-level items split and pretested */
+    uint32_t items;             /* deep batches: work requests (items + requests checked whole) */
+    uint32_t items_kept;        /* deep batches: of them, checked after the reachability pretest */
 } keto_batch_timing;
 int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
 

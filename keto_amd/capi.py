@@ -102,7 +102,8 @@ class KOpts(C.Structure):
 
 class KTiming(C.Structure):
     _fields_ = [("tier_ms", C.c_float * 3), ("requests", C.c_uint32 * 3), ("undecided", C.c_uint32),
-                ("chunks", C.c_uint32), ("wall_ms", C.c_float), ("resolve_ms", C.c_float)]
+                ("chunks", C.c_uint32), ("wall_ms", C.c_float), ("resolve_ms", C.c_float),
+                ("items_ms", C.c_float), ("items", C.c_uint32), ("items_kept", C.c_uint32)]
 
 
 class KPartStats(C.Structure):
@@ -530,7 +531,8 @@ class Snapshot:
         t = KTiming()
         _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
         return {"tier_ms": list(t.tier_ms), "requests": list(t.requests), "undecided": t.undecided,
-                "chunks": t.chunks, "wall_ms": t.wall_ms, "resolve_ms": t.resolve_ms}
+                "chunks": t.chunks, "wall_ms": t.wall_ms, "resolve_ms": t.resolve_ms,
+                "items_ms": t.items_ms, "items": t.items, "items_kept": t.items_kept}
 
     @staticmethod
     def check_kernel_name(global_max_depth=5) -> str:

@@ -491,6 +491,15 @@ struct TierArgs {
     // COUNT kernels: per-request loop iterations (the serial chain length of a request's search),
     // added over the tiers that ran it; NULL = not recorded
     uint32_t* steps;
+    // check_kernel: requests with flags bit KETO_ITEM_FLAG are top-level items (reach.hip) when set;
+    // item_owner[w] = the request of work request w, item_acc[request] bit 0 = some item of it is
+    // allowed (set by the lane that finds it; the request's other items stop when they see it)
+    uint32_t items;
+    const uint32_t* item_owner;
+    uint32_t* item_acc;
+    // check_kernel: non-NULL = requests handed out one at a time from this counter after each lane's
+    // first (a lane never holds a run of long searches back to back); NULL = contiguous runs
+    uint32_t* next;
 };
 
 // ------------------------------------------------------------------ check
@@ -586,16 +595,19 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     CheckStack<Stack> st(ta, slot);
     Work<COUNT> w;
     const uint32_t total = ta.in_list ? *ta.in_count : n;
-    // each lane owns a contiguous run of requests, so consecutive fetches share request lines
-    const uint32_t per = (total + stride - 1) / stride;
+    // each lane owns a contiguous run of requests, so consecutive fetches share request lines; with
+    // ta.next, its first request and then one request per grab
+    const uint32_t per = ta.next ? 1u : (total + stride - 1) / stride;
     uint32_t j = slot * per;
-    const uint32_t j_end = min(total, j + per);
+    uint32_t j_end = min(total, j + per);
     bool busy = false;           // a request is in flight on this lane
     uint32_t qi = 0, T = 0;
     bool tset = false;
     uint32_t cwb = 0;            // T's closure-filter word << 5 | bit
     Frame cur{0, 0, 0, 0};
     uint32_t it = 0;                // iterations of the current request (COUNT: ta.steps)
+    uint32_t own = NONE32;          // items: the request the current work request belongs to
+    uint32_t poll = 0;              // items: iterations since the request's decision was last looked at
     const uint32_t* ce = s.arena;   // arena of the current frame
     uint4 blk = make_uint4(0, 0, 0, 0);
     uint64_t blk_at = ~0ull;        // word index of the 16-B edge block held in blk
@@ -609,7 +621,12 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
         int res = -1;                // >= 0: request decided (RES_*)
         if constexpr (COUNT) ++it;
         if (!busy) {
-            if (j >= j_end) break;
+            if (j >= j_end) {
+                if (!ta.next) break;
+                j = stride + atomicAdd(ta.next, 1u);
+                if (j >= total) break;
+                j_end = j + 1;
+            }
             qi = ta.in_list ? ta.in_list[j] : j;
             ++j;
             const keto_check_ids qq = q[qi];
@@ -633,6 +650,18 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             enter = qq.row;
             enter_k = (uint16_t)d;
             enter_fl = FR_TOP;
+            own = ta.item_owner ? ta.item_owner[qi] : NONE32;
+            poll = 0;
+            if (ta.items && (qq.flags & KETO_ITEM_FLAG)) {
+                // a top-level item (reach.hip): the request row's subject set `row`, entered at the
+                // item's depth with the fresh map of its top-level tuple, which holds the set itself
+                // (engine.go:47-48 with the shadowed ctx; the item's root is not ROW_SEQ, so its visit
+                // id is its handle)
+                enter_fl = 0;
+                V.fresh();
+                w.item();
+                (void)V.test_add(qq.row, w);
+            }
             uint64_t hw;
             if (enter >= ov.base) {
                 ea = ov.arena;
@@ -642,6 +671,11 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             }
             h0 = *reinterpret_cast<const uint4*>(ea + hw);
             h1 = *reinterpret_cast<const uint4*>(ea + hw + HDR_WORDS);
+        } else if (own != NONE32 && ++poll >= 256u) {
+            // another item of this request allowed it (engine.go:73-75 returns there): this item's
+            // decision no longer matters, stop its search
+            poll = 0;
+            if (__hip_atomic_load(ta.item_acc + own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u) res = RES_FALSE;
         } else if (cur.left == 0) {                               // row exhausted: pop
             if (--sp == 0) {
                 res = RES_FALSE;
@@ -778,6 +812,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
                 ta.out_list[at] = qi;
             } else {
                 allowed[qi] = (uint8_t)res;
+                if (res == RES_TRUE && own != NONE32) atomicOr(ta.item_acc + own, 1u);
             }
             V.V.release();                                        // a borrowed tier-2 table (tier 1)
             busy = false;
@@ -1968,6 +2003,10 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     a.dyn = 0;
     a.walk_cap = 0xFFFFFFFFu;
     a.steps = nullptr;
+    a.items = 0;
+    a.item_owner = nullptr;
+    a.item_acc = nullptr;
+    a.next = nullptr;
     a.pool_mask = 0;
     a.pool_n = 0;
     a.pool_epoch = nullptr;
@@ -2603,6 +2642,7 @@ void device_release(Snapshot& S) {
     (void)hipSetDevice(D.device);
     mig_release(S);
     S.proto.reset();
+    S.reach.reset();
     for (auto& W : D.ws) {
         for (auto& t : W.tiers) free_tier(t);
         if (W.lists) (void)hipFree(W.lists);
@@ -2938,9 +2978,9 @@ namespace {
 
 // The check of one device-resident batch: the tier plan and the kernel launches.  The caller holds
 // D.mu and has set the device; `dq` / `da` are device buffers.
-void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
-                  hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
-                  uint32_t* d_steps = nullptr, PipeStash* stash = nullptr, int wsi = 0) {
+void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
+                hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate, uint32_t* d_steps,
+                PipeStash* stash, int wsi, const ItemWork* items) {
     WorkSet& W = D.ws[wsi];
     if (S.part_mode == PART_MIGRATE)
         throw Error{KETO_E_INVALID, "a migrating part answers checks through keto_mig_begin / keto_mig_round"};
@@ -3028,6 +3068,23 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                   uint32_t slots) {
                   TierArgs a = tier_args(t, il, ic, ol, oc);
                   a.steps = dwork ? d_steps : nullptr;
+                  if (items) {
+                      a.items = 1u;
+                      a.item_owner = items->owner;
+                      a.item_acc = items->acc;
+                  }
+                  if (level == 0 && kind == 2 && !dw) {
+                      // deep tier 0: one request per grab after each lane's first (KETO_T0_NEXT=0: runs)
+                      const char* en = getenv("KETO_T0_NEXT");
+                      if (!(en && atoi(en) == 0)) {
+                          if (!W.heads) {
+                              uint64_t acc = 0;
+                              W.heads = dmalloc<uint32_t>(KETO_HEAD_WORDS, acc);
+                          }
+                          HIP_OK(hipMemsetAsync(W.heads, 0, sizeof(uint32_t), st));
+                          a.next = W.heads;
+                      }
+                  }
                   if (level < 2 && p.pool) {
                       const Tier& tn = W.tiers[level + 1];
                       a.pool = tn.vtab;
@@ -3091,6 +3148,55 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
         if (getenv("KETO_SIMT_PROF"))       // tier-0 SIMT profile (tooling): wave / lane counts
             fprintf(stderr, "simt: iter %llu/%llu work %llu/%llu walk %llu/%llu enter %llu/%llu\n", h[16], h[17],
                     h[18], h[19], h[20], h[21], h[22], h[23]);
+    }
+}
+
+// The check of one device-resident batch.  Deep batches (max-depth > 9, the check_kernel tiers)
+// first go through reach.hip: requests split into top-level items, items a hop-bounded reachability
+// pretest proves false dropped, the rest checked as work requests and folded back per request.  A
+// pipeline chunk (stash) of a deep batch is decided whole here, without the deferred stash.
+void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
+                  hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
+                  uint32_t* d_steps = nullptr, PipeStash* stash = nullptr, int wsi = 0) {
+    const int32_t g = std::min<int32_t>(gmd, 65535);
+    const bool deep = n > 0 && g - 1 > 8 && !deep_wave(g) && S.part_mode != PART_MIGRATE;
+    ItemWork iw;
+    if (!deep || !reach_split(S, dq, n, gmd, da, dov.base, st, d_steps != nullptr, iw)) {
+        check_core(S, D, dq, n, gmd, da, st, dov, work_out, accumulate, d_steps, stash, wsi, nullptr);
+        return;
+    }
+    if (stash) {
+        // the chunk's tier timing events still bracket it (the caller reads them)
+        hipEvent_t* e = stash->ev.data() + 3 * stash->chunk;
+        HIP_OK(hipEventRecord(e[0], st));
+        HIP_OK(hipEventRecord(e[1], st));
+    }
+    const keto_batch_timing before = D.last;
+    check_core(S, D, iw.work, iw.n_work, gmd, iw.dec, st, dov, work_out, false, iw.wsteps, nullptr, wsi, &iw);
+    keto_batch_timing T = D.last;
+    uint32_t und = 0;
+    if (d_steps) HIP_OK(hipMemsetAsync(d_steps, 0, (uint64_t)n * sizeof(uint32_t), st));
+    reach_merge(S, iw, n, da, d_steps, st, &und);
+    if (stash) HIP_OK(hipEventRecord(stash->ev[3 * stash->chunk + 2], st));
+    T.undecided = und;
+    T.items_ms = iw.split_ms;
+    T.items = iw.n_entries;
+    T.items_kept = iw.n_work;
+    if (accumulate) {
+        // a pipeline chunk: the caller times the chunk's tiers from the stash events
+        keto_batch_timing& L = D.last;
+        L = before;
+        if (!stash)
+            for (int i = 0; i < 3; ++i) {
+                L.tier_ms[i] += T.tier_ms[i];
+                L.requests[i] += T.requests[i];
+            }
+        L.undecided += T.undecided;
+        L.items_ms += T.items_ms;
+        L.items += T.items;
+        L.items_kept += T.items_kept;
+    } else {
+        D.last = T;
     }
 }
 

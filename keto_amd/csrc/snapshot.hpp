@@ -44,6 +44,9 @@ constexpr uint32_t ANY = 0xFFFFFFFFu;           // wildcard field of a row key
 constexpr int64_t ANY_NS = INT64_MIN;
 constexpr uint32_t ROW_SEQ = 1u;                // flag bit (in RowRec.y bits 8..15)
 constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys live above all row ids
+// keto_check_ids.flags bit of the engine's own top-level items (reach.hip; not part of the C-ABI,
+// honoured only for the work arrays reach.hip builds)
+constexpr uint32_t KETO_ITEM_FLAG = 2u;
 
 // Device arena (one u32 array per device).  Row r occupies
 //   [subject-id table, 2^hlog2 words of 16-B buckets, for rows whose ids do not all fit in the
@@ -162,6 +165,10 @@ struct ProtoState;       // proto.hip
 struct ProtoStateDeleter {
     void operator()(ProtoState* p) const;    // proto.hip
 };
+struct ReachState;       // reach.hip
+struct ReachStateDeleter {
+    void operator()(ReachState* r) const;    // reach.hip
+};
 
 struct Snapshot {
     // ---- config
@@ -266,6 +273,7 @@ struct Snapshot {
     std::unique_ptr<DeviceState, DeviceStateDeleter> dev;
     std::unique_ptr<MigState, MigStateDeleter> mig;      // migrating-partition batches (migrate.hip)
     std::unique_ptr<ProtoState, ProtoStateDeleter> proto; // strings on the device for tree encoding (proto.hip)
+    std::unique_ptr<ReachState, ReachStateDeleter> reach; // reverse / postings index of deep batches (reach.hip)
     std::mutex mu;
 
     ~Snapshot();
@@ -395,6 +403,26 @@ keto_batch_timing device_last_timing(const Snapshot& s);
 void device_check_rows(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
                        void* stream);
 const char* device_check_kernel_name(int32_t gmd);
+// deep batches (reach.hip): requests split into top-level items, items pretested by hop-bounded
+// reachability; engine.hip checks the kept work requests, then reach_merge folds their decisions
+// into the requests' (allowed if an item is, else undecided if one is, else denied)
+struct ItemWork {
+    keto_check_ids* work = nullptr;   // device: kept work requests (items, and requests checked whole)
+    uint32_t* owner = nullptr;        // device: the request each belongs to
+    uint32_t n_work = 0;              // kept work requests
+    uint32_t n_entries = 0;           // work requests before the pretest
+    uint32_t* acc = nullptr;          // device: per request, what its items decided
+    uint8_t* dec = nullptr;           // device: decisions of the work requests
+    uint32_t* wsteps = nullptr;       // device: loop iterations per work request (instrumented), or NULL
+    uint32_t* undecided = nullptr;    // device: requests left undecided
+    float split_ms = 0;               // split + pretest + compaction
+};
+bool reach_enabled(const Snapshot& s);
+bool reach_split(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
+                 uint32_t ov_base, void* stream, bool steps, ItemWork& out);
+void reach_merge(Snapshot& s, const ItemWork& w, uint32_t n, uint8_t* d_allowed, uint32_t* d_steps, void* stream,
+                 uint32_t* undecided);
+float reach_build_ms(const Snapshot& s);
 void* host_alloc(uint64_t bytes);    // pinned host memory (hipHostMalloc)
 void host_free(void* p);
 // partitioned-batch routing (route.hip): stable counting sort of row-id requests by owner part

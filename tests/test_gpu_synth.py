@@ -47,10 +47,12 @@ def test_nested_tier1_borrowed_tables_match_oracle(nested, pool):
     """Tiny tier-0/1 visited tables (KETO_T0_CAP / KETO_T1_CAP) make thousands of deep requests
     outgrow tier 1: with the pool, a tier-1 lane borrows one of tier 2's direct tables and finishes
     the request itself (PromoVisited); requests that find every table borrowed, or all of them
-    without the pool, restart on tier 2.  Every decision must equal the oracle's either way."""
+    without the pool, restart on tier 2.  Every decision must equal the oracle's either way.  Whole
+    requests (KETO_ITEMS=0): split into items and pretested, too few searches outgrow the tables
+    (tests/test_gpu_items.py runs the items with these tables)."""
     g, snap = nested
     q = g.queries_nested(12000, seed=77, depths=(16, 32, 0, 40))
-    env = {"KETO_T0_CAP": "256", "KETO_T1_CAP": "1024"}
+    env = {"KETO_T0_CAP": "256", "KETO_T1_CAP": "1024", "KETO_ITEMS": "0"}
     if not pool:
         env["KETO_NO_POOL"] = "1"
     old = {k: os.environ.get(k) for k in env}

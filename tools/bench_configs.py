@@ -52,9 +52,15 @@ def timed_checks(snap, qd, n, gmd, reps=3):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         ms, cnt = snap.last_timing()
+        full = snap.last_timing_full()
         if best is None or dt < best:
             best, tiers = dt, (ms, cnt)
+            timed_checks.items = {"items_ms": round(full["items_ms"], 3), "work_requests": full["items"],
+                                  "kept": full["items_kept"]}
     return best, tiers, d_out.cpu().numpy()
+
+
+timed_checks.items = None
 
 
 def config1(a):
@@ -143,12 +149,16 @@ def checks_config(a, name, g, q, gmd, sample, reps=3, price=20000):
     t0 = time.perf_counter()
     ref = tab.check_batch_reqs(reqs, gmd, threads=a.threads)
     t_cpu = time.perf_counter() - t0
-    roof = roofline(tab, reqs, gmd, min(price, sample), n, ms[0], a.threads)
+    items = timed_checks.items if timed_checks.items and timed_checks.items["work_requests"] else None
+    # deep batches: the batch's device time (items split + pretest, then the work requests' tiers)
+    roof = roofline(tab, reqs, gmd, min(price, sample), n, sum(ms) + items["items_ms"] if items else ms[0], a.threads)
     roof["kernel"] = snap.check_kernel_name(gmd)
+    if items:
+        roof["kernel"] = "reach split + pretest, then " + roof["kernel"] + " tiers over the kept work requests"
     return {"config": name, "roofline": roof, "tuples": int(g.n_edges), "rows": int(g.n_rows), "checks": n, "global_max_depth": gmd,
             "gpu": {"checks_per_s": round(n / dt, 1), "wall_ms": round(dt * 1e3, 3),
                     "tier_ms": [round(x, 3) for x in ms], "tier_requests": [int(x) for x in cnt],
-                    "kernel": snap.check_kernel_name(gmd)},
+                    "kernel": snap.check_kernel_name(gmd), "items": items},
             "work": work,
             "allowed_fraction": round(float(out.mean()), 4),
             "parity": {"sample": sample, "mismatches": int((ref != out[:sample]).sum())},

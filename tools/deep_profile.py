@@ -53,6 +53,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ms, cnt = snap.last_timing()
+    full = snap.last_timing_full()
     out = d_out.cpu().numpy()
     log("instrumented pass (per-request steps)")
     snap.check_steps_device(d_q.data_ptr(), len(q), d_out.data_ptr(), d_steps.data_ptr(), 32)
@@ -64,6 +65,8 @@ def main():
     line = {"config": "#3 nested groups (chains <= 32, cycles), global max-depth 32", "tuples": int(g.n_edges),
             "requests": len(q), "wall_ms": round(wall * 1e3, 3), "tier_ms": [round(x, 3) for x in ms],
             "tier_requests": [int(x) for x in cnt], "kernel": snap.check_kernel_name(32),
+            "items": {"ms": round(full["items_ms"], 3), "work_requests": full["items"], "kept": full["items_kept"],
+                      "env": {k: v for k, v in os.environ.items() if k.startswith("KETO_")}},
             "steps": {"total": tot, "mean": round(float(steps.mean()), 2), "p50": int(np.percentile(steps, 50)),
                       "p99": int(np.percentile(steps, 99)), "p999": int(np.percentile(steps, 99.9)),
                       "max": int(order[0]), "top10": [int(x) for x in order[:10]],
