@@ -371,6 +371,8 @@ typedef struct {
     float items_ms;             /* deep batches (max-depth > 9): top-level items split and pretested */
     uint32_t items;             /* deep batches: work requests (items + requests checked whole) */
     uint32_t items_kept;        /* deep batches: of them, checked after the reachability pretest */
+    float index_ms;             /* deep batches: reverse / postings index (re)built for this snapshot version
+                                   before the batch (host threads + upload; 0 when it was current) */
 } keto_batch_timing;
 int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
 

@@ -46,7 +46,11 @@ namespace keto {
     } while (0)
 
 #ifndef KETO_CHECK_WAVES
-#define KETO_CHECK_WAVES 7      // check_kernel: ask for 7 waves per SIMD (register budget 72 VGPRs, no spills)
+// check_kernel: 5 waves per SIMD (84 VGPRs).  At 7 (72 VGPRs) the kernel spilled 28-40 B per lane to
+// scratch inside the walk loop, and config #3's tier 0 took 158 ms against 124 ms at 5
+// (profiles/r03m_config3_waves.log); it is the deep tier and the overflow tiers, where lanes wait on
+// one long chain, so fewer resident lanes cost nothing.
+#define KETO_CHECK_WAVES 5
 #endif
 
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
@@ -3182,6 +3186,7 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
     T.items_ms = iw.split_ms;
     T.items = iw.n_entries;
     T.items_kept = iw.n_work;
+    T.index_ms = iw.index_ms;
     if (accumulate) {
         // a pipeline chunk: the caller times the chunk's tiers from the stash events
         keto_batch_timing& L = D.last;
@@ -3195,6 +3200,7 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
         L.items_ms += T.items_ms;
         L.items += T.items;
         L.items_kept += T.items_kept;
+        L.index_ms += T.index_ms;
     } else {
         D.last = T;
     }

@@ -56,7 +56,6 @@ namespace keto {
 namespace {
 
 constexpr uint32_t RNONE = 0xFFFFFFFFu;
-constexpr uint64_t TAB_EMPTY = ~0ull;
 
 template <class T>
 T* ralloc(uint64_t n, uint64_t& acc) {
@@ -102,23 +101,31 @@ __host__ __device__ inline uint32_t rmix(uint32_t k) {
     return k;
 }
 
-// open addressing: entry = offset << 32 | key, empty = ~0 (keys < 2^31)
-__device__ inline uint32_t tab_find(const uint64_t* __restrict__ tab, uint32_t mask, uint32_t key) {
-    for (uint32_t i = rmix(key) & mask;; i = (i + 1) & mask) {
-        const uint64_t e = tab[i];
-        if (e == TAB_EMPTY) return RNONE;
-        if ((uint32_t)e == key) return (uint32_t)(e >> 32);
-    }
+// direct-indexed: dir[key] = the offset of the key's list [count, entries...], INLINE | the one
+// entry of a single-entry list (one access fewer), or RNONE
+constexpr uint32_t INLINE = 0x80000000u;
+__device__ inline uint32_t dir_at(const uint32_t* __restrict__ dir, uint32_t n, uint32_t key) {
+    return key < n ? dir[key] : RNONE;
+}
+// the list behind a table value: n entries, entry k = single (n == 1, inlined) or lists[off + k]
+struct IdxList {
+    uint32_t n, off, single;
+    __device__ inline uint32_t at(const uint32_t* lists, uint32_t k) const { return off == RNONE ? single : lists[off + k]; }
+};
+__device__ inline IdxList list_of(uint32_t v, const uint32_t* lists) {
+    if (v == RNONE) return IdxList{0, RNONE, 0};
+    if (v & INLINE) return IdxList{1, RNONE, v & ~INLINE};
+    return IdxList{lists[v], v + 1, 0};
 }
 
 struct ReachDev {
     const uint32_t* arena;
-    const uint64_t* rtab;     // set-target handle -> offset in rev: [count, handles of the rows pointing at it]
+    const uint32_t* rdir;     // set-target handle -> list value (list_of) over rev: the rows pointing at it
     const uint32_t* rev;
-    uint32_t rmask;
-    const uint64_t* ptab;     // subject id -> offset in post: [count, handles of the rows holding it]
+    uint32_t rn;              // rdir entries
+    const uint32_t* pdir;     // subject id -> list value over post: the rows holding it
     const uint32_t* post;
-    uint32_t pmask;
+    uint32_t pn;              // pdir entries
     uint32_t ov_base;         // handles >= ov_base are batch-local overlay rows (never items)
 };
 
@@ -259,14 +266,14 @@ __device__ bool within(const ReachDev& r, const Pretest& P, uint64_t* M, uint32_
                        uint32_t c, uint32_t T, int L) {
     const uint32_t mmask = 2 * P.cap - 1;
     uint32_t nm = 0, nf = 0, nb = 0;
-    const uint32_t po = tab_find(r.ptab, r.pmask, T);
-    if (po == RNONE) return false;                       // no row holds T
-    const uint32_t pn = r.post[po];
+    const IdxList pl = list_of(dir_at(r.pdir, r.pn, T), r.post);
+    if (pl.n == 0) return false;                         // no row holds T
+    const uint32_t pn = pl.n;
     if (pn >= P.cap) return true;                        // too many rows to start from: keep
     (void)mark(M, mmask, ep, nm, P.cap, c, 0);
     F[nf++] = c;
     for (uint32_t k = 0; k < pn; ++k) {
-        const uint32_t h = r.post[po + 1 + k];
+        const uint32_t h = pl.at(r.post, k);
         const int t = mark(M, mmask, ep, nm, P.cap, h, 1);
         if (t == 2 || t == 3) return true;               // c itself holds T, or full
         if (t == 0) B[nb++] = h;
@@ -299,13 +306,12 @@ __device__ bool within(const ReachDev& r, const Pretest& P, uint64_t* M, uint32_
             ++da;
         } else {
             for (uint32_t x = b0; x < b1; ++x) {
-                const uint32_t ro = tab_find(r.rtab, r.rmask, B[x]);
-                if (ro == RNONE) continue;               // a root row: nothing points at it
-                const uint32_t rn = r.rev[ro];
+                const IdxList rl = list_of(dir_at(r.rdir, r.rn, B[x]), r.rev);
+                const uint32_t rn = rl.n;                // 0: a root row, nothing points at it
                 work += rn;
                 if (work > P.work_cap) return true;
                 for (uint32_t k = 0; k < rn; ++k) {
-                    const uint32_t u = r.rev[ro + 1 + k];
+                    const uint32_t u = rl.at(r.rev, k);
                     const int t = mark(M, mmask, ep, nm, P.cap, u, 1);
                     if (t == 2 || t == 3) return true;
                     if (t == 0) {
@@ -352,9 +358,11 @@ __global__ void __launch_bounds__(256) pretest_kernel(ReachDev r, Pretest P, con
 // the marks live in LDS, claimed by compare-and-swap.  An item costs about two memory round trips per
 // level instead of one per edge.  WP_CAP marks (4096 LDS slots) and WP_CAP handles per side bound a
 // search; past them, or past work_cap edges, the item is kept.
-constexpr uint32_t WP_SLOTS = 4096, WP_CAP = 2048, LEMPTY = 0xFFFFFFFFu;
+constexpr uint32_t LEMPTY = 0xFFFFFFFFu;
 
+template <uint32_t WP_SLOTS>
 __device__ inline int lmark(uint32_t* tab, uint32_t* nm, uint32_t h, uint32_t side) {
+    constexpr uint32_t WP_CAP = WP_SLOTS / 2;
     // 0 new (marked), 1 marked by this side, 2 marked by the other side (the frontiers meet), 3 full
     const uint32_t key = (side << 31) | h;
     for (uint32_t i = rmix(h) & (WP_SLOTS - 1);; i = (i + 1) & (WP_SLOTS - 1)) {
@@ -369,11 +377,17 @@ __device__ inline int lmark(uint32_t* tab, uint32_t* nm, uint32_t h, uint32_t si
     }
 }
 
+template <uint32_t WP_SLOTS>
 __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto_check_ids* __restrict__ work, uint32_t n,
                                                          uint8_t* __restrict__ keep, uint32_t* __restrict__ next,
                                                          uint32_t work_cap, int min_depth) {
+    constexpr uint32_t WP_CAP = WP_SLOTS / 2;
     __shared__ uint32_t tab[WP_SLOTS];
-    __shared__ uint32_t F[WP_CAP], B[WP_CAP];
+    // discovered handles: forward from the front, backward from the back (each is a distinct mark,
+    // so together they never exceed WP_CAP)
+    __shared__ uint32_t FB[WP_CAP];
+    uint32_t* const F = FB;
+    auto Bat = [&](uint32_t i) -> uint32_t& { return FB[WP_CAP - 1 - i]; };
     __shared__ uint32_t s_nf, s_nb, s_nm, s_hit, s_work, s_item;
     const uint32_t t = threadIdx.x;
     for (;;) {
@@ -387,41 +401,45 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
             __syncthreads();
             continue;
         }
-        for (uint32_t i = t; i < WP_SLOTS; i += 64) tab[i] = LEMPTY;
+        for (uint32_t i = t; i < WP_SLOTS / 4; i += 64) reinterpret_cast<uint4*>(tab)[i] = make_uint4(LEMPTY, LEMPTY, LEMPTY, LEMPTY);
         if (t == 0) {
             s_nf = s_nb = s_nm = s_hit = s_work = 0;
         }
         __syncthreads();
         const int L = it.max_depth - 1;                    // hops from the item's set to a row it enters
-        const uint32_t po = tab_find(r.ptab, r.pmask, it.target);
-        const uint32_t pn = po == RNONE ? 0u : r.post[po];
+        const IdxList pl = list_of(dir_at(r.pdir, r.pn, it.target), r.post);
         bool kept;
-        if (po == RNONE) {
+        if (pl.n == 0) {
             kept = false;                                  // no row holds T
-        } else if (pn >= WP_CAP) {
+        } else if (pl.n >= WP_CAP) {
             kept = true;
         } else {
             if (t == 0) {
-                (void)lmark(tab, &s_nm, it.row, 0);
+                (void)lmark<WP_SLOTS>(tab, &s_nm, it.row, 0);
                 F[0] = it.row;
                 s_nf = 1;
             }
             __syncthreads();
-            for (uint32_t k = t; k < pn; k += 64) {
-                const uint32_t h = r.post[po + 1 + k];
-                const int m = lmark(tab, &s_nm, h, 1);
+            for (uint32_t k = t; k < pl.n; k += 64) {
+                const uint32_t h = pl.at(r.post, k);
+                const int m = lmark<WP_SLOTS>(tab, &s_nm, h, 1);
                 if (m >= 2) s_hit = 1;                     // the item's set holds T, or full
-                else if (m == 0) B[atomicAdd(&s_nb, 1u)] = h;
+                else if (m == 0) Bat(atomicAdd(&s_nb, 1u)) = h;
             }
             __syncthreads();
             uint32_t f0 = 0, f1 = 1, b0 = 0, b1 = s_nb;
             int da = 0, db = 0;
             while (!s_hit && da + db < L && f1 > f0 && b1 > b0) {
-                if (f1 - f0 <= b1 - b0) {
-                    for (uint32_t x = f0 + t; x < f1 && !s_hit; x += 64) {
+                // expand the smaller frontier; both in one round while they are of similar size and
+                // the hop budget allows two more hops (a meet is then a path of <= da + db + 2 hops)
+                const uint32_t fs = f1 - f0, bs = b1 - b0;
+                const bool both = da + db + 2 <= L && max(fs, bs) <= 4 * min(fs, bs);
+                const uint32_t nfw = (both || fs <= bs) ? fs : 0u, nbw = (both || fs > bs) ? bs : 0u;
+                for (uint32_t x = t; x < nfw + nbw && !s_hit; x += 64) {
+                    if (x < nfw) {
                         uint4 h0, h1;
                         uint64_t beg;
-                        row_at(r.arena, F[x], h0, h1, beg);
+                        row_at(r.arena, F[f0 + x], h0, h1, beg);
                         const uint32_t ns = h0.x;          // ROW_SEQ: every edge, sets and ids mixed
                         if (atomicAdd(&s_work, ns) + ns > work_cap) {
                             s_hit = 1;
@@ -431,7 +449,7 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                             const uint32_t e = j < WINDOW_WORDS ? win(h1, j) : r.arena[beg + j];
                             if (!(e & EDGE_SET)) continue;
                             const uint32_t ch = e & EDGE_VAL;
-                            const int m = lmark(tab, &s_nm, ch, 0);
+                            const int m = lmark<WP_SLOTS>(tab, &s_nm, ch, 0);
                             if (m >= 2) {
                                 s_hit = 1;
                                 break;
@@ -445,23 +463,15 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                                 F[at] = ch;
                             }
                         }
-                    }
-                    __syncthreads();
-                    f0 = f1;
-                    f1 = min(s_nf, WP_CAP);
-                    ++da;
-                } else {
-                    for (uint32_t x = b0 + t; x < b1 && !s_hit; x += 64) {
-                        const uint32_t ro = tab_find(r.rtab, r.rmask, B[x]);
-                        if (ro == RNONE) continue;         // a root row: nothing points at it
-                        const uint32_t rn = r.rev[ro];
-                        if (atomicAdd(&s_work, rn) + rn > work_cap) {
+                    } else {
+                        const IdxList rl = list_of(dir_at(r.rdir, r.rn, Bat(b0 + x - nfw)), r.rev);
+                        if (atomicAdd(&s_work, rl.n) + rl.n > work_cap) {
                             s_hit = 1;
                             break;
                         }
-                        for (uint32_t k = 0; k < rn; ++k) {
-                            const uint32_t u = r.rev[ro + 1 + k];
-                            const int m = lmark(tab, &s_nm, u, 1);
+                        for (uint32_t k = 0; k < rl.n; ++k) {   // 0: a root row, nothing points at it
+                            const uint32_t u = rl.at(r.rev, k);
+                            const int m = lmark<WP_SLOTS>(tab, &s_nm, u, 1);
                             if (m >= 2) {
                                 s_hit = 1;
                                 break;
@@ -472,11 +482,18 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                                     s_hit = 1;
                                     break;
                                 }
-                                B[at] = u;
+                                Bat(at) = u;
                             }
                         }
                     }
-                    __syncthreads();
+                }
+                __syncthreads();
+                if (nfw) {
+                    f0 = f1;
+                    f1 = min(s_nf, WP_CAP);
+                    ++da;
+                }
+                if (nbw) {
                     b0 = b1;
                     b1 = min(s_nb, WP_CAP);
                     ++db;
@@ -522,12 +539,12 @@ struct ReachState {
     int device = 0;
     uint64_t version = ~0ull;
     bool built = false;
-    uint64_t* rtab = nullptr;
+    uint32_t* rdir = nullptr;
     uint32_t* rev = nullptr;
-    uint32_t rmask = 0;
-    uint64_t* ptab = nullptr;
+    uint32_t rn = 0;
+    uint32_t* pdir = nullptr;
     uint32_t* post = nullptr;
-    uint32_t pmask = 0;
+    uint32_t pn = 0;
     uint64_t bytes = 0;
     float build_ms = 0;
     // pretest lanes
@@ -535,15 +552,15 @@ struct ReachState {
     uint32_t* lists = nullptr;
     uint32_t* epochs = nullptr;
     uint32_t lanes = 0, cap = 0;
-    uint32_t wave_blocks = 0;     // resident blocks of pretest_wave_kernel
+    uint32_t wave_blocks[2] = {0, 0};   // resident blocks of pretest_wave_kernel<4096>, <2048>
     // per batch (grow-only)
     RBuf acc, cnt, off, work, owner, keep, work2, owner2, dec, wsteps, nsel, tmp, ctr;
     void free_index() {
-        for (void* p : {(void*)rtab, (void*)rev, (void*)ptab, (void*)post})
+        for (void* p : {(void*)rdir, (void*)rev, (void*)pdir, (void*)post})
             if (p) (void)hipFree(p);
-        rtab = nullptr;
+        rdir = nullptr;
         rev = nullptr;
-        ptab = nullptr;
+        pdir = nullptr;
         post = nullptr;
         bytes = 0;
         built = false;
@@ -567,20 +584,15 @@ uint32_t pow2_ge(uint64_t x) {
     return (uint32_t)p;
 }
 
-// keys -> offsets, open addressing (parallel inserts by compare-and-swap)
-std::vector<uint64_t> make_table(const std::vector<uint32_t>& keys, const std::vector<uint32_t>& offs, unsigned th) {
-    const uint32_t cap = pow2_ge(std::max<uint64_t>(16, 2ull * keys.size()));
-    std::vector<uint64_t> tab(cap, TAB_EMPTY);
+// keys -> list values, direct-indexed (RNONE where no list)
+std::vector<uint32_t> make_dir(const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals, unsigned th) {
+    uint32_t n = 0;
+    for (uint32_t k : keys) n = std::max(n, k + 1);
+    std::vector<uint32_t> dir(std::max<uint32_t>(n, 1), RNONE);
     par_chunks(keys.size(), th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
-        for (uint64_t k = b; k < e; ++k) {
-            const uint64_t v = ((uint64_t)offs[k] << 32) | keys[k];
-            for (uint32_t i = rmix(keys[k]) & (cap - 1);; i = (i + 1) & (cap - 1)) {
-                uint64_t cur = TAB_EMPTY;
-                if (__atomic_compare_exchange_n(&tab[i], &cur, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) break;
-            }
-        }
+        for (uint64_t k = b; k < e; ++k) dir[keys[k]] = vals[k];
     });
-    return tab;
+    return dir;
 }
 
 // The reverse and postings index of the snapshot's current version (host threads, then one upload).
@@ -634,7 +646,7 @@ void build_index(const Snapshot& S, ReachState& R) {
             roffs.push_back((uint32_t)rw);
             rcur[r] = rw + 1;
             rw += 1ull + indeg[r];
-            if (rw >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "reach index exceeds 2^32 words"};
+            if (rw >= INLINE) throw Error{KETO_E_RANGE, "reach index exceeds 2^31 words"};
         }
     for (uint64_t v = 0; v < idc.size(); ++v)
         if (idc[v]) {
@@ -642,7 +654,7 @@ void build_index(const Snapshot& S, ReachState& R) {
             poffs.push_back((uint32_t)pw);
             pcur[v] = pw + 1;
             pw += 1ull + idc[v];
-            if (pw >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "reach index exceeds 2^32 words"};
+            if (pw >= INLINE) throw Error{KETO_E_RANGE, "reach index exceeds 2^31 words"};
         }
     std::vector<uint32_t> rev(std::max<uint64_t>(rw, 1)), post(std::max<uint64_t>(pw, 1));
     par_chunks(NR, th, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
@@ -672,18 +684,27 @@ void build_index(const Snapshot& S, ReachState& R) {
         for (uint64_t v = b; v < e; ++v)
             if (idc[v]) post[pcur[v] - idc[v] - 1] = idc[v];
     });
-    const std::vector<uint64_t> rt = make_table(rkeys, roffs, th), pt = make_table(pkeys, poffs, th);
+    // single-entry lists go into the table value itself (INLINE | entry)
+    par_chunks(rkeys.size(), th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+        for (uint64_t k = b; k < e; ++k)
+            if (rev[roffs[k]] == 1) roffs[k] = INLINE | rev[roffs[k] + 1];
+    });
+    par_chunks(pkeys.size(), th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+        for (uint64_t k = b; k < e; ++k)
+            if (post[poffs[k]] == 1) poffs[k] = INLINE | post[poffs[k] + 1];
+    });
+    const std::vector<uint32_t> rd = make_dir(rkeys, roffs, th), pd = make_dir(pkeys, poffs, th);
     uint64_t acc = 0;
-    R.rtab = ralloc<uint64_t>(rt.size(), acc);
+    R.rdir = ralloc<uint32_t>(rd.size(), acc);
     R.rev = ralloc<uint32_t>(rev.size(), acc);
-    R.ptab = ralloc<uint64_t>(pt.size(), acc);
+    R.pdir = ralloc<uint32_t>(pd.size(), acc);
     R.post = ralloc<uint32_t>(post.size(), acc);
-    HIP_OK(hipMemcpy(R.rtab, rt.data(), rt.size() * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(R.rdir, rd.data(), rd.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(R.rev, rev.data(), rev.size() * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(R.ptab, pt.data(), pt.size() * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(R.pdir, pd.data(), pd.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(R.post, post.data(), post.size() * 4, hipMemcpyHostToDevice));
-    R.rmask = (uint32_t)rt.size() - 1;
-    R.pmask = (uint32_t)pt.size() - 1;
+    R.rn = (uint32_t)rd.size();
+    R.pn = (uint32_t)pd.size();
     R.bytes = acc;
     R.version = S.version;
     R.built = true;
@@ -715,12 +736,16 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
     }
     ReachState& R = *S.reach;
     hipStream_t st = (hipStream_t)stream;
-    if (!R.built || R.version != S.version) build_index(S, R);
+    out.index_ms = 0;
+    if (!R.built || R.version != S.version) {
+        build_index(S, R);
+        out.index_ms = R.build_ms;
+    }
     hipEvent_t e0, e1;
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipEventRecord(e0, st));
-    const ReachDev rd{V.arena, R.rtab, R.rev, R.rmask, R.ptab, R.post, R.pmask, ov_base};
+    const ReachDev rd{V.arena, R.rdir, R.rev, R.rn, R.pdir, R.post, R.pn, ov_base};
     uint32_t* acc = R.acc.get<uint32_t>(n);
     uint32_t* cnt = R.cnt.get<uint32_t>((uint64_t)n + 1);
     uint32_t* off = R.off.get<uint32_t>((uint64_t)n + 1);
@@ -772,15 +797,19 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
     if (m) {
         const uint32_t mode = env_u32("KETO_REACH_PRETEST", 2);   // 2 = wave per item, 1 = lane per item
         if (mode == 2) {
-            if (!R.wave_blocks) {
+            // LDS per wave: 4096 mark slots + 2048 handles (24 KB, 6 waves per CU), or half that
+            const bool small = env_u32("KETO_REACH_WAVE_SLOTS", 4096) <= 2048;
+            auto kern = small ? pretest_wave_kernel<2048> : pretest_wave_kernel<4096>;
+            uint32_t& wb = R.wave_blocks[small ? 1 : 0];
+            if (!wb) {
                 int per_cu = 0, cus = 0;
-                HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pretest_wave_kernel, 64, 0));
+                HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
                 HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, V.device));
-                R.wave_blocks = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus);
+                wb = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus);
             }
-            const uint32_t blocks = std::min<uint32_t>(R.wave_blocks, std::max<uint32_t>(1, m));
-            hipLaunchKernelGGL(pretest_wave_kernel, dim3(blocks), dim3(64), 0, st, rd, work, m, keep, ctr + 2, P.work_cap,
-                               (int)env_u32("KETO_REACH_MIN_DEPTH", 2));
+            const uint32_t blocks = std::min<uint32_t>(wb, std::max<uint32_t>(1, m));
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, st, rd, work, m, keep, ctr + 2, P.work_cap,
+                               (int)env_u32("KETO_REACH_MIN_DEPTH", 16));
         } else if (mode == 1) {
             hipLaunchKernelGGL(pretest_kernel, dim3(lanes / 256), dim3(256), 0, st, rd, P, work, m, keep);
         } else {

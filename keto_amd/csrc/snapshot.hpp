@@ -416,6 +416,7 @@ struct ItemWork {
     uint32_t* wsteps = nullptr;       // device: loop iterations per work request (instrumented), or NULL
     uint32_t* undecided = nullptr;    // device: requests left undecided
     float split_ms = 0;               // split + pretest + compaction
+    float index_ms = 0;               // index rebuilt first (host + upload), 0 if it was current
 };
 bool reach_enabled(const Snapshot& s);
 bool reach_split(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,

@@ -29,11 +29,14 @@ def nested():
 
 ENVS = {
     "default": {},
+    "pretest_all": {"KETO_REACH_MIN_DEPTH": "2"},
     "no_items": {"KETO_ITEMS": "0"},
     "no_pretest": {"KETO_REACH_PRETEST": "0"},
-    "tiny_bounds": {"KETO_REACH_CAP": "64", "KETO_REACH_WORK": "40"},
-    "few_lanes": {"KETO_REACH_LANES": "256"},
-    "runs": {"KETO_T0_NEXT": "0"},
+    "tiny_bounds": {"KETO_REACH_WORK": "40", "KETO_REACH_MIN_DEPTH": "2"},
+    "lane_pretest": {"KETO_REACH_PRETEST": "1", "KETO_REACH_CAP": "64", "KETO_REACH_WORK": "200"},
+    "lane_pretest_few_lanes": {"KETO_REACH_PRETEST": "1", "KETO_REACH_LANES": "256"},
+    "small_wave_tables": {"KETO_REACH_WAVE_SLOTS": "2048", "KETO_REACH_MIN_DEPTH": "2"},
+    "runs": {"KETO_T0_NEXT": "0", "KETO_REACH_MIN_DEPTH": "2"},
     "tiny_tables": {"KETO_T0_CAP": "256", "KETO_T1_CAP": "1024"},
 }
 
@@ -54,7 +57,7 @@ def test_nested_items_match_oracle(nested, monkeypatch, env, gmd):
         assert t["items"] == 0
     else:
         assert t["items"] > 0, t
-        if env in ("default", "few_lanes", "runs"):
+        if env in ("pretest_all", "runs", "lane_pretest_few_lanes", "small_wave_tables") or (env == "default" and gmd > 12):
             assert t["items_kept"] < t["items"], t       # the pretest dropped items it proved false
 
 
@@ -93,10 +96,12 @@ def test_nested_items_steps(nested):
 
 
 @pytest.mark.parametrize("seed,wide", [(s, False) for s in range(3000, 3080)] + [(s, True) for s in range(3500, 3520)])
-def test_random_graphs_deep_match_oracle(seed, wide):
+def test_random_graphs_deep_match_oracle(seed, wide, monkeypatch):
     """Quirk-heavy random graphs (cycles, duplicates, wildcard sets, poisoned pages, visit-key
-    collisions, overlay rows of wildcard requests) at global max-depths 10 and 13."""
+    collisions, overlay rows of wildcard requests) at global max-depths 10 and 13, every item
+    pretested."""
     import keto_amd
+    monkeypatch.setenv("KETO_REACH_MIN_DEPTH", "2")
     store, ns, tuples, raw, ps, alph = random_store(seed, wide=wide)
     snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples, raw), page_size=ps, device=0)
     rng = random.Random(seed)
@@ -120,10 +125,11 @@ def _write(rng, names, objs, rels, users):
 
 
 @pytest.mark.parametrize("seed", range(16))
-def test_writes_then_deep_checks(seed):
+def test_writes_then_deep_checks(seed, monkeypatch):
     """Writes bump the snapshot version; the next deep batch rebuilds the reverse / postings index,
     so new subject-set edges and ids are seen by the pretest (a stale index would drop items)."""
     import keto_amd
+    monkeypatch.setenv("KETO_REACH_MIN_DEPTH", "2")
     ns, tuples, raw, ps, alph = random_graph(seed + 700, allow_wildcards=False, allow_poison=False,
                                              allow_collisions=seed % 3 == 0)
     names, objs, rels, users = alph
