@@ -3031,9 +3031,13 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     const uint32_t lanes = getenv("KETO_SLOTS") ? (uint32_t)hw_slots() : D.v1_lanes[var];
     p.slots[0] = (uint32_t)std::min<uint64_t>(lanes, ((uint64_t)n + 255) / 256 * 256);
     if (kind == 2) {
-        // deep requests (nested groups) visit thousands of sets: give every tier-0 lane a table
-        // of up to 16K entries and tier 1 128K lanes of up to 64K entries, within half of device
-        // memory (tables are reused across batches; ~137 GB on a 288 GB MI355X)
+        // deep requests (nested groups) visit thousands of sets.  Tier 0 gets tables of 64K entries
+        // (32K visit ids before a lane borrows a tier-1 table, after which every test probes two
+        // tables) and as many lanes as three quarters of the budget hold; tier 1 16K lanes with
+        // tables of up to 128K entries in the rest (the borrow pool and the overflow tier).  The
+        // budget is half of device memory (tables are reused across batches).  On config #3 the
+        // items' tier 0 took 113 ms with 229K lanes of 64K entries against 132 ms with 327K lanes of
+        // 32K (profiles/r03s_config3_tables.log, r03r_config3_tables.log).
         size_t free_b = 0, total_b = 0;
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
         uint64_t held = 0;
@@ -3041,20 +3045,24 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
         uint64_t budget = std::min<uint64_t>(total_b / 2, (free_b + held) * 6 / 10);
         if (const char* eb = getenv("KETO_DEEP_BUDGET_GB"))
             budget = std::min<uint64_t>((uint64_t)atoi(eb) << 30, (free_b + held) * 3 / 4);
+        const uint64_t b0 = budget / 4 * 3, b1 = budget - b0;
         const uint32_t full = pow2_at_least(2ull * D.vid_bound + 2);
-        auto fit = [&](uint32_t slots, uint32_t lo, uint32_t hi) {
+        auto fit = [&](uint32_t slots, uint32_t lo, uint32_t hi, uint64_t b) {
             uint32_t c = lo;
-            while (c < hi && (uint64_t)slots * (2ull * c) * sizeof(uint64_t) <= budget) c *= 2;
+            while (c < hi && (uint64_t)slots * (2ull * c) * sizeof(uint64_t) <= b) c *= 2;
             return std::min(c, full);
         };
         const char* e0 = getenv("KETO_T0_CAP");
         const char* e1 = getenv("KETO_T1_SLOTS");
         const char* e2 = getenv("KETO_T1_CAP");
-        // tier-0 tables of up to 32K entries (profiles/r02h_deep_experiments.log: 16K -> 32K took the
-        // inline kernel from 302 to 254 ms on config #3)
-        p.cap[0] = fit(p.slots[0], 256, e0 ? (uint32_t)atoi(e0) : 32768u);
-        p.slots[1] = (uint32_t)std::min<uint64_t>(e1 ? (uint32_t)atoi(e1) : 131072u, ((uint64_t)n + 255) / 256 * 256);
-        p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, e2 ? (uint32_t)atoi(e2) : 65536u));
+        const uint32_t want0 = std::min(full, pow2_at_least(e0 ? (uint32_t)std::max(256, atoi(e0)) : 65536u));
+        if (!getenv("KETO_SLOTS")) {
+            const uint64_t fit_lanes = std::max<uint64_t>(256, b0 / ((uint64_t)want0 * sizeof(uint64_t)) / 256 * 256);
+            p.slots[0] = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(lanes, fit_lanes), ((uint64_t)n + 255) / 256 * 256);
+        }
+        p.cap[0] = fit(p.slots[0], 256, want0, b0);
+        p.slots[1] = (uint32_t)std::min<uint64_t>(e1 ? (uint32_t)atoi(e1) : 16384u, ((uint64_t)n + 255) / 256 * 256);
+        p.cap[1] = std::max(p.cap[0], fit(p.slots[1], 1024, e2 ? (uint32_t)atoi(e2) : 131072u, b1));
         p.pool = getenv("KETO_NO_POOL") == nullptr;
     }
     if (const char* e = getenv("KETO_TEST_T2_FRAMES")) p.frames[2] = 2 * std::max(1, atoi(e));   // test hook

@@ -435,57 +435,87 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                 const uint32_t fs = f1 - f0, bs = b1 - b0;
                 const bool both = da + db + 2 <= L && max(fs, bs) <= 4 * min(fs, bs);
                 const uint32_t nfw = (both || fs <= bs) ? fs : 0u, nbw = (both || fs > bs) ? bs : 0u;
-                for (uint32_t x = t; x < nfw + nbw && !s_hit; x += 64) {
+                // each lane takes up to 4 nodes of the round at once: their header / reverse-list
+                // loads are all issued before any is used, so a round costs ~one memory latency
+                struct Pf {
+                    uint4 h0, h1;
+                    uint64_t beg;
+                    uint32_t val, cnt;
+                };
+                auto gather = [&](Pf& p, uint32_t x) {
+                    p.val = RNONE;
+                    p.cnt = 0;
+                    if (x < nfw) row_at(r.arena, F[f0 + x], p.h0, p.h1, p.beg);
+                    else if (x < nfw + nbw) p.val = dir_at(r.rdir, r.rn, Bat(b0 + x - nfw));
+                };
+                auto count = [&](Pf& p) {               // counts of multi-entry reverse lists
+                    if (p.val != RNONE && !(p.val & INLINE)) p.cnt = r.rev[p.val];
+                };
+                auto process = [&](const Pf& p, uint32_t x) {
+                    if (x >= nfw + nbw || s_hit) return;
                     if (x < nfw) {
-                        uint4 h0, h1;
-                        uint64_t beg;
-                        row_at(r.arena, F[f0 + x], h0, h1, beg);
-                        const uint32_t ns = h0.x;          // ROW_SEQ: every edge, sets and ids mixed
+                        const uint32_t ns = p.h0.x;     // ROW_SEQ: every edge, sets and ids mixed
                         if (atomicAdd(&s_work, ns) + ns > work_cap) {
                             s_hit = 1;
-                            break;
+                            return;
                         }
                         for (uint32_t j = 0; j < ns; ++j) {
-                            const uint32_t e = j < WINDOW_WORDS ? win(h1, j) : r.arena[beg + j];
+                            const uint32_t e = j < WINDOW_WORDS ? win(p.h1, j) : r.arena[p.beg + j];
                             if (!(e & EDGE_SET)) continue;
                             const uint32_t ch = e & EDGE_VAL;
                             const int m = lmark<WP_SLOTS>(tab, &s_nm, ch, 0);
                             if (m >= 2) {
                                 s_hit = 1;
-                                break;
+                                return;
                             }
                             if (m == 0) {
                                 const uint32_t at = atomicAdd(&s_nf, 1u);
                                 if (at >= WP_CAP) {
                                     s_hit = 1;
-                                    break;
+                                    return;
                                 }
                                 F[at] = ch;
                             }
                         }
                     } else {
-                        const IdxList rl = list_of(dir_at(r.rdir, r.rn, Bat(b0 + x - nfw)), r.rev);
-                        if (atomicAdd(&s_work, rl.n) + rl.n > work_cap) {
+                        const uint32_t v = p.val;
+                        const uint32_t n_par = v == RNONE ? 0u : (v & INLINE) ? 1u : p.cnt;
+                        if (atomicAdd(&s_work, n_par) + n_par > work_cap) {
                             s_hit = 1;
-                            break;
+                            return;
                         }
-                        for (uint32_t k = 0; k < rl.n; ++k) {   // 0: a root row, nothing points at it
-                            const uint32_t u = rl.at(r.rev, k);
+                        for (uint32_t q = 0; q < n_par; ++q) {   // 0: a root row, nothing points at it
+                            const uint32_t u = (v & INLINE) ? (v & ~INLINE) : r.rev[v + 1 + q];
                             const int m = lmark<WP_SLOTS>(tab, &s_nm, u, 1);
                             if (m >= 2) {
                                 s_hit = 1;
-                                break;
+                                return;
                             }
                             if (m == 0) {
                                 const uint32_t at = atomicAdd(&s_nb, 1u);
                                 if (at >= WP_CAP) {
                                     s_hit = 1;
-                                    break;
+                                    return;
                                 }
                                 Bat(at) = u;
                             }
                         }
                     }
+                };
+                for (uint32_t base = 0; base < nfw + nbw && !s_hit; base += 256) {
+                    Pf p0, p1, p2, p3;
+                    gather(p0, base + t);
+                    gather(p1, base + t + 64);
+                    gather(p2, base + t + 128);
+                    gather(p3, base + t + 192);
+                    count(p0);
+                    count(p1);
+                    count(p2);
+                    count(p3);
+                    process(p0, base + t);
+                    process(p1, base + t + 64);
+                    process(p2, base + t + 128);
+                    process(p3, base + t + 192);
                 }
                 __syncthreads();
                 if (nfw) {
@@ -741,9 +771,11 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
         build_index(S, R);
         out.index_ms = R.build_ms;
     }
-    hipEvent_t e0, e1;
+    hipEvent_t e0, e1, ea, eb;
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventCreate(&ea));
+    HIP_OK(hipEventCreate(&eb));
     HIP_OK(hipEventRecord(e0, st));
     const ReachDev rd{V.arena, R.rdir, R.rev, R.rn, R.pdir, R.post, R.pn, ov_base};
     uint32_t* acc = R.acc.get<uint32_t>(n);
@@ -769,6 +801,7 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
     uint32_t* owner = R.owner.get<uint32_t>(m);
     hipLaunchKernelGGL(split_fill, g, b, 0, st, rd, dq, n, gmd, cnt, off, work, owner);
     HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ea, st));
     // pretest lanes: marks / lists kept across batches
     const uint32_t cap = pow2_ge(std::max<uint32_t>(64, env_u32("KETO_REACH_CAP", 2048)));
     const uint32_t want_lanes = std::min<uint32_t>(std::max<uint32_t>(256, env_u32("KETO_REACH_LANES", 65536)) / 256 * 256,
@@ -817,6 +850,7 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
         }
         HIP_OK(hipGetLastError());
     }
+    HIP_OK(hipEventRecord(eb, st));
     // the kept entries, in order
     keto_check_ids* work2 = R.work2.get<keto_check_ids>(m);
     uint32_t* owner2 = R.owner2.get<uint32_t>(m);
@@ -835,6 +869,16 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
     HIP_OK(hipStreamSynchronize(st));
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    if (getenv("KETO_REACH_TRACE")) {          // phase timing (tooling)
+        float a = 0, b2 = 0, c = 0;
+        HIP_OK(hipEventElapsedTime(&a, e0, ea));
+        HIP_OK(hipEventElapsedTime(&b2, ea, eb));
+        HIP_OK(hipEventElapsedTime(&c, eb, e1));
+        fprintf(stderr, "reach: split %.3f ms, pretest %.3f ms, select %.3f ms; %u requests, %u work, %u kept\n", a, b2, c, n,
+                m, kept[0]);
+    }
+    (void)hipEventDestroy(ea);
+    (void)hipEventDestroy(eb);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     out.work = work2;
