@@ -627,7 +627,14 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
         if (!busy) {
             if (j >= j_end) {
                 if (!ta.next) break;
-                j = stride + atomicAdd(ta.next, 1u);
+                // the wave's lanes that need a request now take consecutive ones with one atomic
+                const uint64_t want = __ballot(1);
+                const uint32_t lane = threadIdx.x & 63u;
+                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)want) - 1u;
+                uint32_t got = 0;
+                if (lane == leader) got = atomicAdd(ta.next, (uint32_t)__popcll(want));
+                got = __shfl(got, (int)leader);
+                j = stride + got + (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
                 if (j >= total) break;
                 j_end = j + 1;
             }

@@ -118,9 +118,26 @@ __device__ inline IdxList list_of(uint32_t v, const uint32_t* lists) {
     return IdxList{lists[v], v + 1, 0};
 }
 
+// reverse lists: rdir[handle] = RD_NONE (nothing points at the row), tag << 62 | parents for one or
+// two parents inlined (31 bits each), or 3 << 62 | offset of [count, parents...] in rev
+constexpr uint64_t RD_NONE = ~0ull;
+struct RevList {
+    uint64_t e;
+    uint32_t cnt;                                  // tag 3: the list's count (loaded separately)
+    __device__ inline uint32_t tag() const { return e == RD_NONE ? 0u : (uint32_t)(e >> 62); }
+    __device__ inline uint32_t n() const { const uint32_t t = tag(); return t == 3u ? cnt : t; }
+    __device__ inline uint32_t at(const uint32_t* rev, uint32_t q) const {
+        if (tag() == 3u) return rev[(uint32_t)e + 1 + q];
+        return q == 0 ? (uint32_t)(e & EDGE_VAL) : (uint32_t)((e >> 31) & EDGE_VAL);
+    }
+};
+__device__ inline uint64_t rdir_at(const uint64_t* __restrict__ d, uint32_t n, uint32_t key) {
+    return key < n ? d[key] : RD_NONE;
+}
+
 struct ReachDev {
     const uint32_t* arena;
-    const uint32_t* rdir;     // set-target handle -> list value (list_of) over rev: the rows pointing at it
+    const uint64_t* rdir;     // set-target handle -> the rows pointing at it (RevList)
     const uint32_t* rev;
     uint32_t rn;              // rdir entries
     const uint32_t* pdir;     // subject id -> list value over post: the rows holding it
@@ -306,8 +323,9 @@ __device__ bool within(const ReachDev& r, const Pretest& P, uint64_t* M, uint32_
             ++da;
         } else {
             for (uint32_t x = b0; x < b1; ++x) {
-                const IdxList rl = list_of(dir_at(r.rdir, r.rn, B[x]), r.rev);
-                const uint32_t rn = rl.n;                // 0: a root row, nothing points at it
+                RevList rl{rdir_at(r.rdir, r.rn, B[x]), 0};
+                if (rl.tag() == 3u) rl.cnt = r.rev[(uint32_t)rl.e];
+                const uint32_t rn = rl.n();              // 0: a root row, nothing points at it
                 work += rn;
                 if (work > P.work_cap) return true;
                 for (uint32_t k = 0; k < rn; ++k) {
@@ -390,17 +408,23 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
     auto Bat = [&](uint32_t i) -> uint32_t& { return FB[WP_CAP - 1 - i]; };
     __shared__ uint32_t s_nf, s_nb, s_nm, s_hit, s_work, s_item;
     const uint32_t t = threadIdx.x;
+    // work requests are taken 64 at a time (one atomic per chunk: one per request serialized the
+    // grid on the counter, 13.8 ms for 1.2M requests); the chunk's requests that need a pretest are
+    // found by a ballot and searched one after the other (keep[] starts all ones)
     for (;;) {
-        if (t == 0) s_item = atomicAdd(next, 1u);
+        if (t == 0) s_item = atomicAdd(next, 64u);
         __syncthreads();
-        const uint32_t w = s_item;
-        if (w >= n) break;
-        const keto_check_ids it = work[w];
-        if (!(it.flags & KETO_ITEM_FLAG) || it.max_depth < min_depth) {
-            if (t == 0) keep[w] = 1;
-            __syncthreads();
-            continue;
+        const uint32_t base = s_item;
+        __syncthreads();
+        if (base >= n) break;
+        bool need = false;
+        if (base + t < n) {
+            const keto_check_ids c = work[base + t];
+            need = (c.flags & KETO_ITEM_FLAG) && c.max_depth >= min_depth;
         }
+        for (uint64_t mask = __ballot(need); mask; mask &= mask - 1) {
+        const uint32_t w = base + (uint32_t)(__ffsll((unsigned long long)mask) - 1);
+        const keto_check_ids it = work[w];
         for (uint32_t i = t; i < WP_SLOTS / 4; i += 64) reinterpret_cast<uint4*>(tab)[i] = make_uint4(LEMPTY, LEMPTY, LEMPTY, LEMPTY);
         if (t == 0) {
             s_nf = s_nb = s_nm = s_hit = s_work = 0;
@@ -440,16 +464,15 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                 struct Pf {
                     uint4 h0, h1;
                     uint64_t beg;
-                    uint32_t val, cnt;
+                    RevList rl;
                 };
                 auto gather = [&](Pf& p, uint32_t x) {
-                    p.val = RNONE;
-                    p.cnt = 0;
+                    p.rl = RevList{RD_NONE, 0};
                     if (x < nfw) row_at(r.arena, F[f0 + x], p.h0, p.h1, p.beg);
-                    else if (x < nfw + nbw) p.val = dir_at(r.rdir, r.rn, Bat(b0 + x - nfw));
+                    else if (x < nfw + nbw) p.rl.e = rdir_at(r.rdir, r.rn, Bat(b0 + x - nfw));
                 };
-                auto count = [&](Pf& p) {               // counts of multi-entry reverse lists
-                    if (p.val != RNONE && !(p.val & INLINE)) p.cnt = r.rev[p.val];
+                auto count = [&](Pf& p) {               // counts of reverse lists of 3+ parents
+                    if (p.rl.tag() == 3u) p.rl.cnt = r.rev[(uint32_t)p.rl.e];
                 };
                 auto process = [&](const Pf& p, uint32_t x) {
                     if (x >= nfw + nbw || s_hit) return;
@@ -478,14 +501,13 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                             }
                         }
                     } else {
-                        const uint32_t v = p.val;
-                        const uint32_t n_par = v == RNONE ? 0u : (v & INLINE) ? 1u : p.cnt;
+                        const uint32_t n_par = p.rl.n();
                         if (atomicAdd(&s_work, n_par) + n_par > work_cap) {
                             s_hit = 1;
                             return;
                         }
                         for (uint32_t q = 0; q < n_par; ++q) {   // 0: a root row, nothing points at it
-                            const uint32_t u = (v & INLINE) ? (v & ~INLINE) : r.rev[v + 1 + q];
+                            const uint32_t u = p.rl.at(r.rev, q);
                             const int m = lmark<WP_SLOTS>(tab, &s_nm, u, 1);
                             if (m >= 2) {
                                 s_hit = 1;
@@ -533,6 +555,7 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
         }
         if (t == 0) keep[w] = kept ? 1 : 0;
         __syncthreads();                                   // s_* and tab reused by the next item
+        }
     }
 }
 
@@ -569,7 +592,7 @@ struct ReachState {
     int device = 0;
     uint64_t version = ~0ull;
     bool built = false;
-    uint32_t* rdir = nullptr;
+    uint64_t* rdir = nullptr;
     uint32_t* rev = nullptr;
     uint32_t rn = 0;
     uint32_t* pdir = nullptr;
@@ -714,22 +737,31 @@ void build_index(const Snapshot& S, ReachState& R) {
         for (uint64_t v = b; v < e; ++v)
             if (idc[v]) post[pcur[v] - idc[v] - 1] = idc[v];
     });
-    // single-entry lists go into the table value itself (INLINE | entry)
+    // reverse lists of one or two parents go into the index word itself
+    uint32_t rmax = 0;
+    for (uint32_t k : rkeys) rmax = std::max(rmax, k + 1);
+    std::vector<uint64_t> rd(std::max<uint32_t>(rmax, 1), ~0ull);
     par_chunks(rkeys.size(), th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
-        for (uint64_t k = b; k < e; ++k)
-            if (rev[roffs[k]] == 1) roffs[k] = INLINE | rev[roffs[k] + 1];
+        for (uint64_t k = b; k < e; ++k) {
+            const uint32_t o = roffs[k], c = rev[o];
+            uint64_t v;
+            if (c == 1) v = (1ull << 62) | rev[o + 1];
+            else if (c == 2) v = (2ull << 62) | ((uint64_t)rev[o + 2] << 31) | rev[o + 1];
+            else v = (3ull << 62) | o;
+            rd[rkeys[k]] = v;
+        }
     });
     par_chunks(pkeys.size(), th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
         for (uint64_t k = b; k < e; ++k)
             if (post[poffs[k]] == 1) poffs[k] = INLINE | post[poffs[k] + 1];
     });
-    const std::vector<uint32_t> rd = make_dir(rkeys, roffs, th), pd = make_dir(pkeys, poffs, th);
+    const std::vector<uint32_t> pd = make_dir(pkeys, poffs, th);
     uint64_t acc = 0;
-    R.rdir = ralloc<uint32_t>(rd.size(), acc);
+    R.rdir = ralloc<uint64_t>(rd.size(), acc);
     R.rev = ralloc<uint32_t>(rev.size(), acc);
     R.pdir = ralloc<uint32_t>(pd.size(), acc);
     R.post = ralloc<uint32_t>(post.size(), acc);
-    HIP_OK(hipMemcpy(R.rdir, rd.data(), rd.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(R.rdir, rd.data(), rd.size() * 8, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(R.rev, rev.data(), rev.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(R.pdir, pd.data(), pd.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(R.post, post.data(), post.size() * 4, hipMemcpyHostToDevice));
@@ -840,7 +872,8 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
                 HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, V.device));
                 wb = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus);
             }
-            const uint32_t blocks = std::min<uint32_t>(wb, std::max<uint32_t>(1, m));
+            HIP_OK(hipMemsetAsync(keep, 1, m, st));
+            const uint32_t blocks = std::min<uint32_t>(wb, std::max<uint32_t>(1, (m + 63) / 64));
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, st, rd, work, m, keep, ctr + 2, P.work_cap,
                                (int)env_u32("KETO_REACH_MIN_DEPTH", 16));
         } else if (mode == 1) {
