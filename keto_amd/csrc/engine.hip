@@ -1706,9 +1706,9 @@ __device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint3
 
 // BuildTree for one root (engine.go:33-102).  root: row handle (root_flags bit0 = subject set) or
 // a string id.  Set nodes are emitted with their row handle (the host maps handles to row ids).
-template <bool FILL, class Stack>
+template <bool FILL, class Stack, class VT>
 __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
-                          uint32_t root_vid, int d, Visited& V, keto_tree_node* out, uint64_t& cnt, Stack& st,
+                          uint32_t root_vid, int d, VT& V, keto_tree_node* out, uint64_t& cnt, Stack& st,
                           const ExpandOut& o) {
     if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
         emit(out, cnt, FILL, root, 0x80000000u);
@@ -1808,11 +1808,16 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
                                                      uint32_t n, int gmd, ExpandOut o, TierArgs ta) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
-    Visited V;
-    V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
-    V.mask = ta.mask;
-    V.epoch = ta.slot_epoch[slot];
-    V.count = 0;
+    // a tree's map: its first REG_VIDS + LDS_VIDS sets in registers and the lane's LDS column (one
+    // tree at max-depth 5 marks a handful of sets), the rest in the lane's HBM table
+    __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
+    VisitedRS<LDS_VIDS, Visited> V;
+    V.n = 0;
+    V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
+    V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
+    V.V.mask = ta.mask;
+    V.V.epoch = ta.slot_epoch[slot];
+    V.V.count = 0;
     Stack st;
     if constexpr (std::is_same<Stack, GlobalStack>::value) {
         st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
@@ -1827,7 +1832,7 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         if (d <= 0 || gmd < d) d = gmd;
         uint64_t cnt = 0;
         keto_tree_node* out = FILL ? o.nodes + o.offset[i] : nullptr;
-        int r = expand_one<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, st, o);
+        int r = expand_one<FILL, Stack>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, st, o);
         if (r == EXP_OVERFLOW) {
             uint32_t at = atomicAdd(ta.out_count, 1u);
             ta.out_list[at] = i;
@@ -1836,7 +1841,7 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
             o.status[i] = (uint8_t)r;
         }
     }
-    ta.slot_epoch[slot] = V.epoch;
+    ta.slot_epoch[slot] = V.V.epoch;
 }
 
 // The queued id runs of a fill pass, a block per run (grid-stride over runs).  A run queued twice (a
@@ -2341,8 +2346,11 @@ void device_upload(Snapshot& S, int device) {
     D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
     D->n_units = (uint32_t)S.n_units;
     D->n_coll = S.n_coll_keys;
+    // the compute stream and the two copy streams; the pipeline's optional second compute stream is
+    // created on first use (KETO_PIPE_STREAMS=2): a process gets few hardware queues
+    // (GPU_MAX_HW_QUEUES, 4 by default) and streams beyond them share one, so an idle extra stream
+    // could put a copy stream and the compute stream on one queue
     HIP_OK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&D->stream2, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&D->copy_in, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&D->copy_out, hipStreamNonBlocking));
     for (auto& e : D->ev) HIP_OK(hipEventCreate(&e));
@@ -3415,6 +3423,7 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     // one stream stays the default
     const char* eps = getenv("KETO_PIPE_STREAMS");
     const bool two = eps && atoi(eps) == 2;
+    if (two && !D.stream2) HIP_OK(hipStreamCreateWithFlags(&D.stream2, hipStreamNonBlocking));
     hipEvent_t setup_done = D.pev[6];
     HIP_OK(hipEventRecord(setup_done, D.stream));
     if (two) HIP_OK(hipStreamWaitEvent(D.stream2, setup_done, 0));
