@@ -358,6 +358,34 @@ void keto_host_free(void* p);
 int keto_check_batch_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                             uint8_t* d_allowed_out, void* stream);
 
+/* ---- Multi-GPU over RCCL (xGMI), one process per GPU (repo:keto_amd/csrc/comm.cpp) ----
+ * The exchanges of SURVEY.md 8(e) inside the library, for callers without Python (the Go server
+ * process, internal/driver/daemon.go:62-69, calling check.(*Engine).SubjectIsAllowed per request,
+ * internal/check/engine.go:116-123).  keto_comm_id makes a communicator id on one rank; the caller
+ * hands its KETO_COMM_ID_BYTES to every rank (its own channel), and every rank calls
+ * keto_comm_init with it.  Every call below is collective: all ranks of the communicator call it. */
+#define KETO_COMM_ID_BYTES 128
+typedef struct keto_comm keto_comm;
+int keto_comm_id(uint8_t* id_out);
+int keto_comm_init(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, keto_comm** out);
+void keto_comm_free(keto_comm* c);
+/* Replicated snapshot (every rank uploaded the whole graph): every rank passes the same n named
+ * requests (keto_check_batch's form); rank r decides the r-th contiguous shard, and one all-gather
+ * returns all n decisions and statuses to every rank. */
+int keto_check_batch_sharded(keto_comm* c, keto_snapshot* s, const keto_check_req* reqs, uint32_t n,
+                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
+/* Edge-partitioned snapshot (this rank's part: keto_snapshot_upload_part_mode with part = rank and
+ * n_parts = ranks): every rank passes its own batch; requests go to the parts owning their rows
+ * (one all-to-all), are decided there -- on a migrating part by continuation-record rounds with an
+ * all-reduce and all-to-alls per round -- and the decisions come back (a second all-to-all).  A
+ * wildcard query that no stored subject set uses has no row to route by: KETO_E_INVALID. */
+int keto_check_batch_routed(keto_comm* c, keto_snapshot* s, const keto_check_req* reqs, uint32_t n,
+                            int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
+/* A migrating partition's closure-filter exchange, once after every rank uploaded its part (before
+ * the first keto_check_batch_routed; replaces the keto_part_filters / keto_part_close /
+ * keto_part_closure_done loop a caller would otherwise run). */
+int keto_comm_close_filters(keto_comm* c, keto_snapshot* s, uint32_t* rounds_out);
+
 /* Device time of the last keto_check_* call on this snapshot, per tier (tier 0 = every request,
  * tiers 1/2 = requests whose visited map outgrew the previous tier's table), from HIP events on
  * the call's stream; summed over the chunks of a host-buffer call. */

@@ -8,8 +8,9 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libketo_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["snapshot.cpp", "resolve.cpp", "delta.cpp", "capi.cpp", "engine.hip", "route.hip", "migrate.hip", "proto.hip", "reach.hip"]
+SOURCES = ["snapshot.cpp", "resolve.cpp", "delta.cpp", "capi.cpp", "engine.hip", "route.hip", "migrate.hip", "proto.hip", "reach.hip", "comm.cpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+HOST_HIP = ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]   # host-only sources using the HIP / RCCL APIs
 
 
 def _stale(target, deps):
@@ -20,7 +21,7 @@ def _stale(target, deps):
 
 
 def build(verbose=False, force=False):
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "parallel.hpp"), os.path.join(CSRC, "snapshot.hpp"),
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "parallel.hpp"), os.path.join(CSRC, "snapshot.hpp"), os.path.join(CSRC, "capi_internal.hpp"),
                                                         os.path.join(HERE, "..", "include", "keto_mi355x.h")]
     if not force and not _stale(OUT, deps):
         return OUT
@@ -33,11 +34,11 @@ def build(verbose=False, force=False):
             continue
         cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, "-c", path, "-o", obj]
         if src.endswith(".cpp"):
-            cmd = [HIPCC, *CXXFLAGS, "-x", "c++", "-c", path, "-o", obj]
+            cmd = [HIPCC, *CXXFLAGS, *HOST_HIP, "-x", "c++", "-c", path, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs, "-L/opt/rocm/lib", "-lrccl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
@@ -58,11 +59,11 @@ def build_variant(name, defines):
         obj = os.path.join(vdir, f"{name}_{src}.o")
         flags = [f"-D{d}" for d in defines]
         if src.endswith(".cpp"):
-            cmd = [HIPCC, *CXXFLAGS, *flags, "-x", "c++", "-c", path, "-o", obj]
+            cmd = [HIPCC, *CXXFLAGS, *HOST_HIP, *flags, "-x", "c++", "-c", path, "-o", obj]
         else:
             cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, *flags, "-c", path, "-o", obj]
         subprocess.check_call(cmd)
         objs.append(obj)
     out = os.path.join(vdir, f"lib_{name}.so")
-    subprocess.check_call([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs])
+    subprocess.check_call([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs, "-L/opt/rocm/lib", "-lrccl"])
     return out

@@ -37,6 +37,8 @@ EXPORTS = [
     "keto_snapshot_upload_part_mode", "keto_snapshot_part_stats_mode", "keto_part_stubs", "keto_part_filters",
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
     "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
+    "keto_comm_id", "keto_comm_init", "keto_comm_free", "keto_check_batch_sharded", "keto_check_batch_routed",
+    "keto_comm_close_filters",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -724,3 +726,58 @@ class Snapshot:
         finally:
             self.lib.keto_tree_arena_free(a)
         return out
+
+
+class Comm:
+    """A keto_comm: multi-GPU batches over RCCL behind the C-ABI (keto_amd/csrc/comm.cpp), one process
+    per GPU.  Every rank builds it with the id one rank made (Comm.make_id) and distributed."""
+
+    @staticmethod
+    def make_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        _check(load().keto_comm_id(buf))
+        return bytes(buf)
+
+    def __init__(self, comm_id: bytes, n_ranks: int, rank: int, device: int = 0):
+        self.lib = load()
+        self.h = C.c_void_p()
+        idb = (C.c_uint8 * 128).from_buffer_copy(comm_id)
+        _check(self.lib.keto_comm_init(idb, C.c_int32(n_ranks), C.c_int32(rank), C.c_int32(device), C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            self.lib.keto_comm_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _batch(self, fn, snap, reqs, global_max_depth, n=None):
+        """reqs: a list as in Snapshot.check_batch, or a prepared KCheckReq array of n requests."""
+        keep = _Keep()
+        if n is None:
+            arr = snap._check_reqs(keep, reqs)
+            n = len(reqs)
+        else:
+            arr = reqs
+        allowed = np.zeros(max(1, n), dtype=np.uint8)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(fn(self.h, snap.h, arr, C.c_uint32(n), C.c_int32(global_max_depth), allowed.ctypes.data_as(C.c_void_p),
+                  status.ctypes.data_as(C.c_void_p)))
+        return allowed[:n], status[:n]
+
+    def check_batch_sharded(self, snap, reqs, global_max_depth=5, n=None):
+        """keto_check_batch_sharded (replicated snapshot): reqs as in Snapshot.check_batch."""
+        return self._batch(self.lib.keto_check_batch_sharded, snap, reqs, global_max_depth, n)
+
+    def check_batch_routed(self, snap, reqs, global_max_depth=5, n=None):
+        """keto_check_batch_routed (this rank's part of an edge-partitioned snapshot)."""
+        return self._batch(self.lib.keto_check_batch_routed, snap, reqs, global_max_depth, n)
+
+    def close_filters(self, snap) -> int:
+        rounds = C.c_uint32(0)
+        _check(self.lib.keto_comm_close_filters(self.h, snap.h, C.byref(rounds)))
+        return rounds.value

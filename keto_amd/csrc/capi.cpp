@@ -10,14 +10,12 @@
 #include <string>
 #include <thread>
 
+#include "capi_internal.hpp"
 #include "parallel.hpp"
 #include "snapshot.hpp"
 
 using namespace keto;
 
-struct keto_snapshot {
-    std::unique_ptr<Snapshot> s;
-};
 
 struct keto_tree_arena {
     ExpandResult r;
@@ -34,28 +32,11 @@ struct keto_tree_arena {
     mutable std::vector<std::string> enc;
 };
 
+thread_local std::string keto::g_err;
+
 namespace {
 
-thread_local std::string g_err;
-
 inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
-
-template <class F>
-auto guarded(F&& f) -> decltype(f()) {
-    try {
-        g_err.clear();
-        return f();
-    } catch (const Error& e) {
-        g_err = e.msg;
-        return e.code;
-    } catch (const std::bad_alloc&) {
-        g_err = "out of host memory";
-        return KETO_E_NOMEM;
-    } catch (const std::exception& e) {
-        g_err = e.what();
-        return KETO_E_INVALID;
-    }
-}
 
 void json_escape(std::string& o, std::string_view s) {
     // encoding/json's HTMLEscape-compatible string encoding
@@ -319,10 +300,12 @@ int64_t copy_out(const std::string& s, char* buf, uint64_t cap) {
     return (int64_t)s.size();
 }
 
+}  // namespace
+
 // resolve_checks over a whole batch on host threads (the first error wins); the wildcard requests
 // come back in request order
-std::vector<WildReq> resolve_all(const Snapshot& S, const keto_check_req* reqs, uint32_t n, keto_check_ids* ids,
-                                 uint8_t* st) {
+std::vector<WildReq> keto::resolve_all(const Snapshot& S, const keto_check_req* reqs, uint32_t n, keto_check_ids* ids,
+                                       uint8_t* st, bool by_row) {
     std::atomic<bool> failed{false};
     Error first{KETO_OK, ""};
     std::mutex emu;
@@ -331,7 +314,7 @@ std::vector<WildReq> resolve_all(const Snapshot& S, const keto_check_req* reqs, 
     par_chunks(n, th, 4096, [&](uint64_t b, uint64_t e, unsigned t) {
         if (failed) return;
         try {
-            resolve_checks(S, reqs, b, e, ids, st, wild[t]);
+            resolve_checks(S, reqs, b, e, ids, st, wild[t], by_row);
         } catch (const Error& x) {
             std::lock_guard<std::mutex> lk(emu);
             if (!failed.exchange(true)) first = x;
@@ -343,8 +326,6 @@ std::vector<WildReq> resolve_all(const Snapshot& S, const keto_check_req* reqs, 
     std::sort(all.begin(), all.end(), [](const WildReq& a, const WildReq& b) { return a.i < b.i; });
     return all;
 }
-
-}  // namespace
 
 extern "C" {
 

@@ -251,7 +251,7 @@ namespace {
 
 // one request, any form (wildcards, subject sets, unknown namespaces)
 keto_check_ids resolve_general(const Snapshot& S, const keto_check_req& q, uint64_t i, uint8_t& status,
-                               std::vector<WildReq>& wild) {
+                               std::vector<WildReq>& wild, bool by_row) {
     keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0, q.max_depth};
     status = KETO_CHECK_OK;
     RowKey wkey;
@@ -259,8 +259,12 @@ keto_check_ids resolve_general(const Snapshot& S, const keto_check_req& q, uint6
     if (row == -2) status = KETO_CHECK_UNKNOWN_NAMESPACE;
     else if (row == -3) wild.push_back(WildReq{(uint32_t)i, wkey});
     else if (row >= 0) {
-        if (!S.present((uint32_t)row)) foreign_row(S, (uint32_t)row);
-        r.row = S.handle((uint32_t)row);
+        if (by_row) {
+            r.row = (uint32_t)row;
+        } else {
+            if (!S.present((uint32_t)row)) foreign_row(S, (uint32_t)row);
+            r.row = S.handle((uint32_t)row);
+        }
     }
     if (q.subject.kind == 0) {
         const int64_t sid = S.lookup_str(sv(q.subject.id));
@@ -268,7 +272,7 @@ keto_check_ids resolve_general(const Snapshot& S, const keto_check_req& q, uint6
     } else {
         const int64_t t = S.resolve_query(sv(q.subject.set_namespace), sv(q.subject.set_object), sv(q.subject.set_relation));
         if (t >= 0) {
-            r.target = S.handle((uint32_t)t);
+            r.target = by_row ? (uint32_t)t : S.handle((uint32_t)t);
             r.flags = 1;
         }
     }
@@ -296,7 +300,7 @@ struct Group {
 
 template <int G>
 void resolve_group_pipeline(const Snapshot& S, const keto_check_req* q, uint64_t b, uint64_t e, keto_check_ids* out,
-                            uint8_t* status, std::vector<WildReq>& wild) {
+                            uint8_t* status, std::vector<WildReq>& wild, bool by_row) {
     const StrSlot* ST = static_cast<const StrSlot*>(S.str_idx.p);
     const RowSlot* RT = static_cast<const RowSlot*>(S.row_idx.p);
     const uint64_t n_groups = (e - b + G - 1) / G;
@@ -318,7 +322,7 @@ void resolve_group_pipeline(const Snapshot& S, const keto_check_req* q, uint64_t
         for (uint64_t i = g0; i < g1; ++i) {
             const keto_check_req& x = q[i];
             if (!x.namespace_.n || !x.object.n || !x.relation.n || x.subject.kind != 0) {
-                out[i] = resolve_general(S, x, i, status[i], wild);
+                out[i] = resolve_general(S, x, i, status[i], wild, by_row);
                 continue;
             }
             Lane& l = G_.l[G_.n++];
@@ -398,8 +402,12 @@ void resolve_group_pipeline(const Snapshot& S, const keto_check_req* q, uint64_t
             keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0, q[l.i].max_depth};
             status[l.i] = l.ns_ok ? KETO_CHECK_OK : KETO_CHECK_UNKNOWN_NAMESPACE;
             if (l.row >= 0) {
-                if (!S.present((uint32_t)l.row)) foreign_row(S, (uint32_t)l.row);
-                r.row = S.handle((uint32_t)l.row);
+                if (by_row) {
+                    r.row = (uint32_t)l.row;
+                } else {
+                    if (!S.present((uint32_t)l.row)) foreign_row(S, (uint32_t)l.row);
+                    r.row = S.handle((uint32_t)l.row);
+                }
             }
             if (l.id[2] >= 0) r.target = (uint32_t)l.id[2];
             out[l.i] = r;
@@ -419,15 +427,15 @@ void resolve_group_pipeline(const Snapshot& S, const keto_check_req* q, uint64_t
 }  // namespace
 
 void resolve_checks(const Snapshot& S, const keto_check_req* q, uint64_t b, uint64_t e, keto_check_ids* out,
-                    uint8_t* status, std::vector<WildReq>& wild) {
+                    uint8_t* status, std::vector<WildReq>& wild, bool by_row) {
     S.ensure_index();
     // KETO_RESOLVE_GROUP (tuning): requests per pipeline group, 8 / 16 / 32 (8: 96 M requests/s on 16
     // EPYC 9575F threads at 1B tuples, 16: 88 M, 32: 91 M; profiles/r03d_resolve.log)
     const char* v = getenv("KETO_RESOLVE_GROUP");
     const int group = v ? atoi(v) : 8;
-    if (group == 8) resolve_group_pipeline<8>(S, q, b, e, out, status, wild);
-    else if (group == 32) resolve_group_pipeline<32>(S, q, b, e, out, status, wild);
-    else resolve_group_pipeline<16>(S, q, b, e, out, status, wild);
+    if (group == 8) resolve_group_pipeline<8>(S, q, b, e, out, status, wild, by_row);
+    else if (group == 32) resolve_group_pipeline<32>(S, q, b, e, out, status, wild, by_row);
+    else resolve_group_pipeline<16>(S, q, b, e, out, status, wild, by_row);
 }
 
 }  // namespace keto

@@ -344,13 +344,15 @@ struct Error {
 // internal/persistence/sql/relationtuples.go:178-198): out[i], status[i] (KETO_CHECK_*), and for a
 // wildcard query that no stored subject set materialized an entry {i, its key} appended to `wild`
 // (out[i].row is then KETO_NO_ROW until the caller gives it a batch-local row).  Throws
-// KETO_E_INVALID for a top-level row another part owns.
+// KETO_E_INVALID for a top-level row another part owns.  by_row: rows (and subject-set targets)
+// by row id instead of this device's handles, for requests routed to the part owning their row
+// (comm.cpp); no ownership check.
 struct WildReq {
     uint32_t i;
     RowKey key;
 };
 void resolve_checks(const Snapshot& S, const keto_check_req* q, uint64_t b, uint64_t e, keto_check_ids* out,
-                    uint8_t* status, std::vector<WildReq>& wild);
+                    uint8_t* status, std::vector<WildReq>& wild, bool by_row = false);
 
 std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns, const keto_tuple* t, uint64_t n,
                                          uint32_t page_size);
