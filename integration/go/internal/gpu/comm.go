@@ -1,0 +1,84 @@
+//go:build keto_gpu
+// +build keto_gpu
+
+package gpu
+
+/*
+#include <stdlib.h>
+#include "keto_mi355x.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+
+	"github.com/ory/keto/internal/relationtuple"
+)
+
+// Comm is the library's RCCL communicator (keto_comm, include/keto_mi355x.h): one Keto server
+// process per GPU (internal/driver/daemon.go:62-69 serves one process), the processes of a node
+// joined by one communicator.  Every method is collective: all ranks call it.
+type Comm struct {
+	h *C.keto_comm
+}
+
+// NewCommID makes a communicator id on one rank (keto_comm_id); send its bytes to every rank over
+// the deployment's own channel, then every rank calls NewComm with them.
+func NewCommID() ([]byte, error) {
+	buf := (*C.uint8_t)(C.malloc(C.KETO_COMM_ID_BYTES))
+	defer C.free(unsafe.Pointer(buf))
+	if rc := C.keto_comm_id(buf); rc != C.KETO_OK {
+		return nil, lastErr(rc)
+	}
+	return C.GoBytes(unsafe.Pointer(buf), C.KETO_COMM_ID_BYTES), nil
+}
+
+// NewComm joins the communicator as rank of ranks, on GPU device (keto_comm_init).
+func NewComm(id []byte, ranks, rank, device int) (*Comm, error) {
+	if len(id) != C.KETO_COMM_ID_BYTES {
+		return nil, fmt.Errorf("gpu: communicator id of %d bytes, want %d", len(id), C.KETO_COMM_ID_BYTES)
+	}
+	cid := C.CBytes(id)
+	defer C.free(cid)
+	var h *C.keto_comm
+	if rc := C.keto_comm_init((*C.uint8_t)(cid), C.int32_t(ranks), C.int32_t(rank), C.int32_t(device), &h); rc != C.KETO_OK {
+		return nil, lastErr(rc)
+	}
+	return &Comm{h: h}, nil
+}
+
+// Close frees the communicator (keto_comm_free).
+func (c *Comm) Close() {
+	if c.h != nil {
+		C.keto_comm_free(c.h)
+		c.h = nil
+	}
+}
+
+// CheckBatchSharded decides a batch every rank passes identically on a replicated snapshot: each
+// rank checks its contiguous shard, one all-gather returns every decision to every rank
+// (keto_check_batch_sharded).
+func (c *Comm) CheckBatchSharded(s *Snapshot, reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	return checkWith(reqs, depths, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
+		return C.keto_check_batch_sharded(c.h, s.h, cr, n, C.int32_t(globalMax), allowed, status)
+	})
+}
+
+// CheckBatchRouted decides this rank's own batch on an edge-partitioned snapshot: requests travel
+// to the parts owning their rows and their decisions come back (keto_check_batch_routed).
+func (c *Comm) CheckBatchRouted(s *Snapshot, reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	return checkWith(reqs, depths, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
+		return C.keto_check_batch_routed(c.h, s.h, cr, n, C.int32_t(globalMax), allowed, status)
+	})
+}
+
+// CloseFilters runs a migrating partition's closure-filter exchange once after upload
+// (keto_comm_close_filters); it returns the rounds it took.
+func (c *Comm) CloseFilters(s *Snapshot) (int, error) {
+	var rounds C.uint32_t
+	if rc := C.keto_comm_close_filters(c.h, s.h, &rounds); rc != C.KETO_OK {
+		return 0, lastErr(rc)
+	}
+	return int(rounds), nil
+}

@@ -215,6 +215,15 @@ func (m *cmem) subject(sub relationtuple.Subject) C.keto_subject {
 // CheckBatch = check.(*Engine).SubjectIsAllowed (internal/check/engine.go:116-123) for many
 // requests: allowed[i] and status[i] (StatusUndecided: ask the SQL engine for request i).
 func (s *Snapshot) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	return checkWith(reqs, depths, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
+		return C.keto_check_batch(s.h, cr, n, C.int32_t(globalMax), allowed, status)
+	})
+}
+
+// checkWith marshals the requests into C memory, runs call (one of the keto_check_batch* entry
+// points taking keto_check_req) and unpacks its decisions and statuses.
+func checkWith(reqs []*relationtuple.InternalRelationTuple, depths []int,
+	call func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int) ([]bool, []uint8, error) {
 	n := len(reqs)
 	if n == 0 {
 		return nil, nil, nil
@@ -237,7 +246,7 @@ func (s *Snapshot) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depth
 	}
 	allowed := (*C.uint8_t)(m.alloc(n))
 	status := (*C.uint8_t)(m.alloc(n))
-	if rc := C.keto_check_batch(s.h, cr, C.uint32_t(n), C.int32_t(globalMax), allowed, status); rc != C.KETO_OK {
+	if rc := call(cr, C.uint32_t(n), allowed, status); rc != C.KETO_OK {
 		return nil, nil, lastErr(rc)
 	}
 	out := make([]bool, n)
