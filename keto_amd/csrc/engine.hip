@@ -3214,11 +3214,18 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
         // a pipeline chunk: the caller times the chunk's tiers from the stash events
         keto_batch_timing& L = D.last;
         L = before;
-        if (!stash)
+        if (!stash) {
             for (int i = 0; i < 3; ++i) {
                 L.tier_ms[i] += T.tier_ms[i];
                 L.requests[i] += T.requests[i];
             }
+        } else {
+            // the chunk's tiers 0 and 1 are timed by the stash events around this call; its work
+            // requests that went up the tiers are counted here
+            L.requests[1] += T.requests[1];
+            L.requests[2] += T.requests[2];
+            L.tier_ms[2] += T.tier_ms[2];
+        }
         L.undecided += T.undecided;
         L.items_ms += T.items_ms;
         L.items += T.items;
@@ -3504,7 +3511,7 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     HIP_OK(hipMemcpyAsync(pc, D.ps_count, sizeof(pc), hipMemcpyDeviceToHost, D.stream));
     HIP_OK(hipStreamSynchronize(D.stream));
     D.last.requests[0] = n;
-    D.last.requests[1] = pc[1];
+    D.last.requests[1] += pc[1];
     for (uint32_t c = 0; c < chunks; ++c) {
         float a = 0, b = 0;
         HIP_OK(hipEventElapsedTime(&a, D.ps_ev[3 * c], D.ps_ev[3 * c + 1]));
@@ -3529,9 +3536,9 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
         (void)hipFree(d_dec);
         for (uint32_t i = 0; i < m; ++i) allowed[idx[i]] = dec[i];
         D.last = before;
-        D.last.requests[2] = stash_t.requests[2];
-        D.last.tier_ms[2] = stash_t.tier_ms[0] + stash_t.tier_ms[1] + stash_t.tier_ms[2];
-        D.last.undecided = stash_t.undecided;
+        D.last.requests[2] += stash_t.requests[2];
+        D.last.tier_ms[2] += stash_t.tier_ms[0] + stash_t.tier_ms[1] + stash_t.tier_ms[2];
+        D.last.undecided += stash_t.undecided;
     }
     D.last.chunks = chunks;
     D.last.wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
