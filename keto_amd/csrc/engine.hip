@@ -3045,6 +3045,12 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     }
     const uint32_t lanes = getenv("KETO_SLOTS") ? (uint32_t)hw_slots() : D.v1_lanes[var];
     p.slots[0] = (uint32_t)std::min<uint64_t>(lanes, ((uint64_t)n + 255) / 256 * 256);
+    if (stash && kind < 2) {
+        // KETO_CHUNK_LANES (tuning): a pipeline chunk's tier 0 on at most that many lanes, so that the
+        // chunks of two compute streams (KETO_PIPE_STREAMS=2) can run side by side
+        if (const char* e = getenv("KETO_CHUNK_LANES"))
+            p.slots[0] = std::max<uint32_t>(256, std::min<uint32_t>(p.slots[0], (uint32_t)atoi(e) / 256 * 256));
+    }
     if (kind == 2) {
         // deep requests (nested groups) visit thousands of sets.  Tier 0 gets tables of 64K entries
         // (32K visit ids before a lane borrows a tier-1 table, after which every test probes two

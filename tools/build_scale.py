@@ -24,15 +24,22 @@ def log(msg):
     print(f"[build_scale {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def peak_rss_gb():
+    import resource
+    return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 1)   # KiB -> GB
+
+
 def run(name, g, q, gmd, threads):
     log(f"{name}: {g.n_edges} tuples; emitting string rows")
     t0 = time.perf_counter()
     st = g.string_tuples(seed=11, threads=threads)
     t_emit = time.perf_counter() - t0
     log(f"{name}: keto_snapshot_build (host + upload)")
+    rss0 = peak_rss_gb()
     os.environ["KETO_BUILD_TRACE"] = "1"
     snap, t_build = g.snapshot_from_strings(st, device=0)
     del os.environ["KETO_BUILD_TRACE"]
+    rss1 = peak_rss_gb()
     stats = snap.stats()
     log(f"{name}: built in {t_build:.1f} s; from_csr snapshot")
     t0 = time.perf_counter()
@@ -54,7 +61,9 @@ def run(name, g, q, gmd, threads):
             "from_csr_s": round(t_csr, 2), "device_bytes": int(stats["device_bytes"]),
             "string_requests": len(q), "string_batch_s": round(t_str, 3),
             "string_checks_per_s": round(len(q) / t_str, 1), "allowed_fraction": round(float(got.mean()), 4),
-            "mismatches_vs_from_csr": mism, "unknown_namespace_status": int((status == 1).sum())}
+            "mismatches_vs_from_csr": mism, "unknown_namespace_status": int((status == 1).sum()),
+            "peak_rss_gb_before_build": rss0, "peak_rss_gb_after_build": rss1,
+            "what_rss": "process peak RSS (graph CSR + string rows + the builder's working set)"}
 
 
 def main():
@@ -75,8 +84,11 @@ def main():
             g = synth.SynthGraph(dict(synth.NESTED_100M), threads=a.threads, kind="nested", chain=32)
             q = g.queries_nested(a.requests, seed=3, depths=(5, 16, 32), threads=a.threads)
             r = run(name, g, q, 32, a.threads)
-        elif name == "powerlaw100m":
-            g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 0.1), threads=a.threads)
+        elif name.startswith("powerlaw") and name.endswith("m"):
+            # powerlaw100m, powerlaw500m, powerlaw1000m: the bench graph at that many tuples
+            scale = int(name[len("powerlaw"):-1]) / 1000.0
+            g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, scale) if scale != 1.0 else dict(synth.POWERLAW_1B),
+                                 threads=a.threads)
             q = g.queries(a.requests, seed=4, depth=5, threads=a.threads)
             r = run(name, g, q, 5, a.threads)
         else:
