@@ -559,6 +559,18 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
     }
 }
 
+// kept work requests in two classes: deep items (fa) and the rest (fb)
+__global__ void __launch_bounds__(256) classify_kept(const keto_check_ids* __restrict__ work, const uint8_t* __restrict__ keep,
+                                                     uint32_t m, int first_depth, uint8_t* __restrict__ fa,
+                                                     uint8_t* __restrict__ fb) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= m) return;
+    const bool k = keep[w] != 0;
+    const bool deep = (work[w].flags & KETO_ITEM_FLAG) && work[w].max_depth >= first_depth;
+    fa[w] = k && deep;
+    fb[w] = k && !deep;
+}
+
 __global__ void __launch_bounds__(256) merge_kernel(const uint8_t* __restrict__ dec, const uint32_t* __restrict__ owner,
                                                     uint32_t m, uint32_t* __restrict__ acc,
                                                     const uint32_t* __restrict__ wsteps, uint32_t* __restrict__ steps) {
@@ -607,7 +619,7 @@ struct ReachState {
     uint32_t lanes = 0, cap = 0;
     uint32_t wave_blocks[2] = {0, 0};   // resident blocks of pretest_wave_kernel<4096>, <2048>
     // per batch (grow-only)
-    RBuf acc, cnt, off, work, owner, keep, work2, owner2, dec, wsteps, nsel, tmp, ctr;
+    RBuf acc, cnt, off, work, owner, keep, work2, owner2, dec, wsteps, nsel, tmp, ctr, flags;
     void free_index() {
         for (void* p : {(void*)rdir, (void*)rev, (void*)pdir, (void*)post})
             if (p) (void)hipFree(p);
@@ -884,19 +896,34 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
         HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(eb, st));
-    // the kept entries, in order
+    // the kept entries: deep items first (max-depth >= KETO_REACH_FIRST_DEPTH, default 16), so that the
+    // searches that can run long hold lanes from the start of the check instead of waiting for one;
+    // the rest after them, each class in request order
     keto_check_ids* work2 = R.work2.get<keto_check_ids>(m);
     uint32_t* owner2 = R.owner2.get<uint32_t>(m);
-    uint32_t* nsel = R.nsel.get<uint32_t>(2);
-    size_t t1 = 0, t2 = 0;
-    HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, t1, work, keep, work2, nsel, std::max<uint32_t>(m, 1), st));
-    HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, t2, owner, keep, owner2, nsel + 1, std::max<uint32_t>(m, 1), st));
-    tmp = R.tmp.get<uint8_t>(std::max(t1, t2));
+    uint32_t* nsel = R.nsel.get<uint32_t>(4);
+    uint8_t* fl = R.flags.get<uint8_t>(2ull * std::max<uint32_t>(m, 1));
     uint32_t kept[2] = {0, 0};
     if (m) {
-        HIP_OK(hipcub::DeviceSelect::Flagged(tmp, t1, work, keep, work2, nsel, m, st));
-        HIP_OK(hipcub::DeviceSelect::Flagged(tmp, t2, owner, keep, owner2, nsel + 1, m, st));
-        HIP_OK(hipMemcpyAsync(kept, nsel, sizeof(kept), hipMemcpyDeviceToHost, st));
+        hipLaunchKernelGGL(classify_kept, dim3((m + 255) / 256), dim3(256), 0, st, work, keep, m,
+                           (int)env_u32("KETO_REACH_FIRST_DEPTH", 16), fl, fl + m);
+        HIP_OK(hipGetLastError());
+        size_t t1 = 0, t2 = 0;
+        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, t1, work, fl, work2, nsel, m, st));
+        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, t2, owner, fl, owner2, nsel + 1, m, st));
+        tmp = R.tmp.get<uint8_t>(std::max(t1, t2));
+        uint32_t first[2] = {0, 0};
+        HIP_OK(hipcub::DeviceSelect::Flagged(tmp, t1, work, fl, work2, nsel, m, st));
+        HIP_OK(hipcub::DeviceSelect::Flagged(tmp, t2, owner, fl, owner2, nsel + 1, m, st));
+        HIP_OK(hipMemcpyAsync(first, nsel, sizeof(first), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipcub::DeviceSelect::Flagged(tmp, t1, work, fl + m, work2 + first[0], nsel + 2, m, st));
+        HIP_OK(hipcub::DeviceSelect::Flagged(tmp, t2, owner, fl + m, owner2 + first[0], nsel + 3, m, st));
+        uint32_t second[2] = {0, 0};
+        HIP_OK(hipMemcpyAsync(second, nsel + 2, sizeof(second), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        kept[0] = first[0] + second[0];
+        kept[1] = first[1] + second[1];
     }
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipStreamSynchronize(st));
