@@ -17,10 +17,11 @@ def test_host_library_under_asan(tmp_path):
     csrc = os.path.join(ROOT, "keto_amd", "csrc")
     san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     objs = []
-    from keto_amd.build import SOURCES
+    from keto_amd.build import HOST_HIP, SOURCES
     for f in [s for s in SOURCES if s.endswith(".cpp")]:
         o = str(tmp_path / (f + ".o"))
-        subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *san, "-c", os.path.join(csrc, f), "-o", o])
+        subprocess.check_call([HIPCC, "-O1", "-g", "-std=c++17", "-x", "c++", *HOST_HIP, *san, "-c", os.path.join(csrc, f),
+                               "-o", o])
         objs.append(o)
     for f in [s for s in SOURCES if s.endswith(".hip")]:
         o = str(tmp_path / (f + ".o"))
@@ -33,7 +34,7 @@ def test_host_library_under_asan(tmp_path):
                            os.path.join(ROOT, "tests", "asan", "snapshot_asan.cpp"), "-o", d])
     exe = str(tmp_path / "snapshot_asan")
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-fsanitize=address,undefined", "-fno-gpu-sanitize",
-                           d, *objs, "-o", exe])
+                           d, *objs, "-o", exe, "-L/opt/rocm/lib", "-lrccl"])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([exe, "300"], capture_output=True, text=True, timeout=600, env=env)
