@@ -70,6 +70,8 @@ def main():
     r, o = run(qd[rest], "without the 10000 longest")
     r["same_decisions"] = bool((o == out[rest]).all())
     print(json.dumps(r), flush=True)
+    if "--no-knobs" in sys.argv:
+        return
     for env in ({"KETO_T0_CAP": 65536}, {"KETO_T0_CAP": 4096}, {"KETO_NO_POOL": 1},
                 {"KETO_SLOTS": 229376}, {"KETO_SLOTS": 917504}):
         r, o = run(qd, "full batch, knob", **env)
