@@ -14,10 +14,15 @@
 // are appended after the build's byte-ordered ones and compared by bytes wherever order matters.
 //
 // A write that creates a Subject.String() collision gives the colliding subjects a collision class and
-// re-flags the rows that hold them ROW_SEQ, as the build would have.  Writes outside this delta path
-// throw KETO_E_REBUILD and leave the snapshot unchanged; the caller rebuilds it (keto_snapshot_build
-// from the table): a stored subject set with an empty field (a materialized wildcard row), a row that
-// a stored wildcard set materializes, a poisoned row.  A partitioned snapshot takes no writes.
+// re-flags the rows that hold them ROW_SEQ, as the build would have.  A stored subject set with an
+// empty field (a wildcard set: its query leaves that field out, relationtuples.go:178-198) points at
+// a materialized wildcard row, the concatenation of every row its query matches in ORDER BY order
+// (snapshot.cpp); a write that inserts a new wildcard set creates that row, and a write that changes
+// a row some wildcard row matches re-materializes the wildcard row from the staged edges.  Writes
+// outside this delta path throw KETO_E_REBUILD and leave the snapshot unchanged; the caller rebuilds
+// it (keto_snapshot_build from the table): a write that touches a poisoned row (one whose pages hold
+// a tuple of an unknown namespace), or a wildcard row that matches one.  A partitioned snapshot takes
+// no writes.
 #include <algorithm>
 #include <cstring>
 
@@ -29,6 +34,10 @@ namespace keto {
 namespace {
 
 inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
+inline bool wild_key(const RowKey& k) { return k.ns == ANY_NS || k.obj == ANY || k.rel == ANY; }
+inline bool key_matches(const RowKey& w, const RowKey& k) {     // does wildcard query w return row k
+    return (w.ns == ANY_NS || w.ns == k.ns) && (w.obj == ANY || w.obj == k.obj) && (w.rel == ANY || w.rel == k.rel);
+}
 
 struct Txn {
     Snapshot& S;
@@ -164,12 +173,18 @@ struct Txn {
             return id < 0 ? NONE : (uint32_t)id;
         }
         const int32_t sns = ns_id_checked(t.set_namespace_id);
-        const std::string& name = S.ns_names[S.ns_by_id.at(sns)];
-        if (name.empty() || t.set_object.n == 0 || t.set_relation.n == 0)
-            throw Error{KETO_E_REBUILD, "a subject set with an empty field (a wildcard row) needs a rebuild"};
-        const int64_t o = str(sv(t.set_object), add), r = str(sv(t.set_relation), add);
-        if (o < 0 || r < 0) return NONE;
-        const RowKey k{(int64_t)sns, (uint32_t)o, (uint32_t)r};
+        // an empty field is left out of the set's query (the build's target_row): ANY
+        RowKey k{S.ns_names[S.ns_by_id.at(sns)].empty() ? ANY_NS : (int64_t)sns, ANY, ANY};
+        if (t.set_object.n) {
+            const int64_t o = str(sv(t.set_object), add);
+            if (o < 0) return NONE;
+            k.obj = (uint32_t)o;
+        }
+        if (t.set_relation.n) {
+            const int64_t r = str(sv(t.set_relation), add);
+            if (r < 0) return NONE;
+            k.rel = (uint32_t)r;
+        }
         if (!add) {
             const int64_t x = row(k);
             return x < 0 ? NONE : (EDGE_SET | (uint32_t)x);
@@ -179,12 +194,60 @@ struct Txn {
         return EDGE_SET | x;
     }
     static constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+    // ORDER BY position of two complete row keys: (namespace id, object bytes, relation bytes)
+    bool key_less(uint32_t ra, uint32_t rb) const {
+        const RowKey &a = key(ra), &b = key(rb);
+        if (a.ns != b.ns) return a.ns < b.ns;
+        if (a.obj != b.obj) return cmp(a.obj, b.obj) < 0;
+        return cmp(a.rel, b.rel) < 0;
+    }
+    // the edges of wildcard row w as the staged table holds them: the rows its query returns
+    // (relationtuples.go:250 ORDER BY), concatenated -- the build's materialization (snapshot.cpp)
+    std::vector<uint32_t> materialize(const RowKey& w) const {
+        std::vector<uint32_t> sorted, extra;
+        uint32_t lo = 0, hi = S.n_real_rows;           // real rows sort by namespace first
+        if (w.ns != ANY_NS) {
+            lo = (uint32_t)(std::lower_bound(S.row_key.begin(), S.row_key.begin() + hi, w.ns,
+                                             [](const RowKey& x, int64_t n) { return x.ns < n; }) - S.row_key.begin());
+            hi = (uint32_t)(std::upper_bound(S.row_key.begin() + lo, S.row_key.begin() + hi, w.ns,
+                                             [](int64_t n, const RowKey& x) { return n < x.ns; }) - S.row_key.begin());
+        }
+        for (uint32_t q = lo; q < hi; ++q)
+            if (key_matches(w, S.row_key[q])) sorted.push_back(q);
+        // rows outside the build's sorted range that hold tuples: changed by earlier writes or staged now
+        auto extra_row = [&](uint32_t q) {
+            if (q < S.n_real_rows || wild_key(key(q)) || !key_matches(w, key(q))) return;
+            extra.push_back(q);
+        };
+        for (const auto& kv : S.row_over) extra_row(kv.first);
+        for (const auto& kv : rows)
+            if (!S.row_over.count(kv.first)) extra_row(kv.first);
+        std::sort(extra.begin(), extra.end(), [&](uint32_t a, uint32_t b) { return key_less(a, b); });
+        std::vector<uint32_t> order(sorted.size() + extra.size());
+        std::merge(sorted.begin(), sorted.end(), extra.begin(), extra.end(), order.begin(),
+                   [&](uint32_t a, uint32_t b) { return key_less(a, b); });
+        std::vector<uint32_t> out;
+        for (uint32_t q : order) {
+            if (q < S.rows.size() && S.row_pp[q] != NO_PAGE)
+                throw Error{KETO_E_REBUILD, "a wildcard row that changes matches a poisoned row"};
+            auto st = rows.find(q);
+            if (st != rows.end()) {
+                out.insert(out.end(), st->second.begin(), st->second.end());
+            } else {
+                const auto e = S.row_edges(q);
+                out.insert(out.end(), e.first, e.first + e.second);
+            }
+        }
+        return out;
+    }
 };
 
-std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {
-    auto it = S.ns_by_id.find((int32_t)k.ns);
+std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {     // Subject.String()
+    auto it = k.ns == ANY_NS ? S.ns_by_id.end() : S.ns_by_id.find((int32_t)k.ns);
     const std::string ns = it == S.ns_by_id.end() ? "" : S.ns_names[it->second];
-    return ns + ":" + T.str_of(k.obj) + "#" + T.str_of(k.rel);
+    return ns + ":" + (k.obj == ANY ? std::string() : T.str_of(k.obj)) + "#" +
+           (k.rel == ANY ? std::string() : T.str_of(k.rel));
 }
 
 }  // namespace
@@ -280,24 +343,37 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
         for (uint32_t r = 0; r < R; ++r)
             if (hit[r]) T.edges(r);                      // re-imaged with the new flag (poisoned: rebuild)
     }
-    // ---- what the delta path cannot express: the caller rebuilds
-    for (uint32_t r : T.order) {
-        if (r < S.rows.size()) {
-            if (S.row_pp[r] != NO_PAGE) throw Error{KETO_E_REBUILD, "a write touches a poisoned row"};
-            const RowKey& k = S.row_key[r];
-            if (k.ns == ANY_NS || k.obj == ANY || k.rel == ANY) throw Error{KETO_E_REBUILD, "a write touches a wildcard row"};
-        }
-        if (S.n_wild_rows) {
-            const RowKey& k = T.key(r);
-            for (uint32_t w = 0; w < S.n_rows(); ++w) {
-                const RowKey& wk = S.row_key[w];
-                if (!(wk.ns == ANY_NS || wk.obj == ANY || wk.rel == ANY)) continue;
-                if ((wk.ns == ANY_NS || wk.ns == k.ns) && (wk.obj == ANY || wk.obj == k.obj) &&
-                    (wk.rel == ANY || wk.rel == k.rel))
-                    throw Error{KETO_E_REBUILD, "a write touches a row a stored wildcard set materializes"};
+    // ---- wildcard rows: every new one, and every one whose query returns a row this transaction
+    // staged, is materialized again from the staged edges
+    std::vector<uint32_t> new_wild;
+    for (uint32_t i = 0; i < T.new_keys.size(); ++i)
+        if (wild_key(T.new_keys[i])) new_wild.push_back((uint32_t)S.row_key.size() + i);
+    if (!S.wild_rows.empty() || !new_wild.empty()) {
+        std::vector<uint32_t> changed;
+        for (uint32_t r : T.order)
+            if (!wild_key(T.key(r))) changed.push_back(r);
+        auto redo = [&](uint32_t w, bool always) {
+            const RowKey& wk = T.key(w);
+            bool hit = always;
+            for (uint32_t r = 0; !hit && r < changed.size(); ++r) hit = key_matches(wk, T.key(changed[r]));
+            if (!hit) return;
+            if (w < S.rows.size() && S.row_pp[w] != NO_PAGE)
+                throw Error{KETO_E_REBUILD, "a write changes a wildcard row that matches a poisoned row"};
+            std::vector<uint32_t> e = T.materialize(wk);
+            auto it = T.rows.find(w);
+            if (it == T.rows.end()) {
+                T.order.push_back(w);
+                T.rows.emplace(w, std::move(e));
+            } else {
+                it->second = std::move(e);
             }
-        }
+        };
+        for (uint32_t w : S.wild_rows) redo(w, false);
+        for (uint32_t w : new_wild) redo(w, true);
     }
+    // ---- what the delta path cannot express: the caller rebuilds
+    for (uint32_t r : T.order)
+        if (r < S.rows.size() && S.row_pp[r] != NO_PAGE) throw Error{KETO_E_REBUILD, "a write touches a poisoned row"};
     // ---- commit
     const uint32_t R0 = S.n_rows();
     if (!new_coll.empty()) {
@@ -320,11 +396,14 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
     }
     S.dirty.clear();
     S.needs_cb.clear();
+    for (uint32_t w : new_wild) S.wild_rows.push_back(w);
+    S.n_wild_rows += (uint32_t)new_wild.size();
     for (uint32_t r : T.order) {
         std::vector<uint32_t>& e = T.rows[r];
-        bool seq = false;
+        const bool wild = wild_key(S.row_key[r]);          // materialized: walked edge by edge
+        bool seq = wild;
         for (uint32_t v : e)
-            if (S.coll.count(v)) { seq = true; break; }
+            if (!seq && S.coll.count(v)) { seq = true; break; }
         // base rows keep their build edge range (row_edges of the row before reads it as its end)
         RowRec rec{r < R0 ? S.rows[r].edge_lo : 0u,
                    (r < R0 ? (S.rows[r].hi_flags & 0xFFu) : 0u) | ((seq ? ROW_SEQ : 0u) << 8), 0, 0};
@@ -345,8 +424,10 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
                                                 S.row_cb[r] != 0};
         }
         S.rows[r] = rec;
-        S.n_tuples += e.size();
-        S.n_tuples -= r < R0 ? S.row_edges(r).second : 0;
+        if (!wild) {                                        // a wildcard row's edges are other rows' tuples
+            S.n_tuples += e.size();
+            S.n_tuples -= r < R0 ? S.row_edges(r).second : 0;
+        }
         S.row_over[r] = std::move(e);
         S.dirty.push_back(r);
     }

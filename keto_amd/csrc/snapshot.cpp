@@ -708,6 +708,7 @@ std::unique_ptr<Snapshot> build_snapshot(const keto_namespace* ns, uint32_t n_ns
         row_ptr[r] = S.edges.size();
         if (!extra_is_wild[r - S.n_real_rows]) continue;
         is_wild[r] = 1;
+        S.wild_rows.push_back(r);
         const RowKey& k = S.row_key[r];
         uint64_t pos = 0;
         for (uint32_t q = 0; q < S.n_real_rows; ++q) {          // matching real rows in ORDER BY order

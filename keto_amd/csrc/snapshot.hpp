@@ -186,6 +186,7 @@ struct Snapshot {
     // ---- rows
     uint32_t n_real_rows = 0;
     uint32_t n_wild_rows = 0;
+    std::vector<uint32_t> wild_rows;                         // the wildcard rows (keys with an ANY field)
     std::vector<RowKey> row_key;                             // per row
     std::unordered_map<RowKey, uint32_t, RowKeyHash> row_of; // real + empty + wildcard rows
     std::vector<RowRec> rows;

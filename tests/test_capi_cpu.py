@@ -95,3 +95,26 @@ def test_route_argument_checks_need_no_gpu():
                                         C.c_uint32(self_part), C.c_uint32(n_parts), C.c_void_p(8), C.c_uint64(wb),
                                         C.c_void_p(8), C.c_void_p(8), counts, None)
         assert rc == -1, (n_parts, self_part, wb)                 # KETO_E_INVALID
+
+
+def test_host_apply_wildcard_sets():
+    """keto_snapshot_apply on a host-only snapshot: new wildcard subject sets (empty object, empty
+    relation, the namespace named "") become materialized rows and writes to the rows they match take
+    the delta path (version + 1); a write to a row that a poisoned wildcard row matches is refused
+    with KETO_E_REBUILD and leaves the snapshot unchanged."""
+    ns = [(1, "n"), (2, "")]
+    rows = [(1, "a", "r", "u"), (1, "b", "r", None, 1, "", "r"), (1, "c", "s", "v")]
+    s = keto_amd.Snapshot.build(ns, rows, device=-1)
+    assert s.stats()["n_wildcard_rows"] == 1
+    assert s.apply([(1, "a", "r", "w")]) == 1                                   # matched by n:*#r
+    assert s.apply([(1, "d", "r", None, 1, "c", ""), (1, "e", "r", None, 2, "a", "r"),
+                    (1, "f", "r", None, 1, "", "")], [(1, "b", "r", None, 1, "", "r")]) == 2
+    st = s.stats()
+    assert st["n_wildcard_rows"] == 4 and st["n_tuples"] == 6, st
+    assert s.apply([], [(1, "d", "r", None, 1, "c", "")]) == 3
+    p = keto_amd.Snapshot.build(ns, [(1, "a", "r", None, 99, "x", "y"), (1, "b", "r", None, 1, "", "r")],
+                                device=-1)
+    with pytest.raises(keto_amd.KetoError, match="-6"):
+        p.apply([(1, "c", "r", "u")])                                           # n:*#r holds a poisoned page
+    assert p.version() == 0
+    assert p.apply([(1, "c", "s", "u")]) == 1                                   # no wildcard row matches n:c#s
