@@ -1684,10 +1684,18 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
 }
 
 // ------------------------------------------------------------------ expand
-// A long run of a row's subject ids (all leaves) is not copied by the fill pass's lane, one node
-// per iteration while its wave waits, but queued and copied afterwards by copy_runs, a block per run
-// (coalesced).  Runs of at most RUN_INLINE ids are copied in place.
-constexpr uint32_t RUN_INLINE = 32;
+// A row's run of subject ids (all leaves) is not copied by the traversing lane, one node per
+// iteration while its wave waits, but queued and copied afterwards, coalesced (copy_lane_runs,
+// copy_big_runs).  Each tier-0 lane queues into its own RUNS_PER_LANE entries (no atomics: a
+// returning atomic per run, or per few runs, put a round trip on the traversal's critical path:
+// the fill pass took twice the count pass's time, profiles/r03ex_expand_ab.txt); runs of at most
+// ExpandOut::run_inline ids (KETO_EXPAND_RUN_INLINE, default 0), runs past a lane's entries and runs
+// of later tiers are copied in place.
+constexpr uint32_t RUN_INLINE_DEFAULT = 0;
+constexpr uint32_t RUNS_PER_LANE = 32;
+// a run longer than BIG_RUN ids goes to a shared queue instead, cut into BIG_RUN-id pieces that
+// different waves copy (one atomic per big run: rare, and small next to the copy it saves)
+constexpr uint32_t BIG_RUN = 1024;
 struct CopyRun {
     const uint32_t* src;     // the ids
     keto_tree_node* dst;     // their leaf nodes
@@ -1698,13 +1706,28 @@ struct ExpandOut {
     const uint64_t* offset;  // FILL only
     uint64_t* count;         // count pass: nodes per root
     uint8_t* status;
-    CopyRun* runs;           // FILL only: queued id runs (NULL = copy every run in place)
-    uint32_t* n_runs;
-    uint32_t runs_cap;
+    CopyRun* runs;           // FILL, tier 0: the lanes' queued id runs (NULL = copy every run in place)
+    uint32_t* lane_runs;     // runs queued per lane (RUNS_PER_LANE entries per lane at runs + lane * ..)
+    uint32_t run_inline;
+    CopyRun* big;            // pieces of runs longer than BIG_RUN | their count
+    uint32_t* n_big;
+    uint32_t big_cap;
+    // staging (EXP_STAGE, tier 0 of the one-pass expand): each lane writes its roots' trees into its
+    // own region of `stage` (stage_cap nodes, trees back to back) and records where (stage_pos, ~0 =
+    // not staged: the tree did not fit, or a later tier decided it); a fill pass (EXP_FILL) then
+    // skips the staged roots
+    keto_tree_node* stage;
+    uint64_t stage_cap;
+    uint64_t* stage_pos;
 };
+// expand kernel modes: count the trees' nodes; write them at their offsets; write them to staging
+constexpr int EXP_COUNT = 0, EXP_FILL = 1, EXP_STAGE = 2;
+constexpr uint64_t NOT_STAGED = ~0ull;
 
-__device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint32_t subject, uint32_t info) {
-    if (fill) out[cnt] = keto_tree_node{subject, info};
+// cnt < cap: the node is written (cap = ~0 in a fill pass; a staged tree past its region is only
+// counted, and filled again later)
+__device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint64_t cap, uint32_t subject, uint32_t info) {
+    if (fill && cnt < cap) out[cnt] = keto_tree_node{subject, info};
     ++cnt;
 }
 
@@ -1712,10 +1735,10 @@ __device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint3
 // a string id.  Set nodes are emitted with their row handle (the host maps handles to row ids).
 template <bool FILL, class Stack, class VT>
 __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
-                          uint32_t root_vid, int d, VT& V, keto_tree_node* out, uint64_t& cnt, Stack& st,
-                          const ExpandOut& o) {
+                          uint32_t root_vid, int d, VT& V, keto_tree_node* out, uint64_t& cnt, uint64_t cap,
+                          Stack& st, const ExpandOut& o, uint32_t& nr, uint64_t& qend) {
     if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
-        emit(out, cnt, FILL, root, 0x80000000u);
+        emit(out, cnt, FILL, cap, root, 0x80000000u);
         return EXP_TREE;
     }
     if (root == KETO_NO_ROW) return EXP_NIL;                // no tuples at all (:68-70)
@@ -1733,7 +1756,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         if (!rv.poison && n_all == 0) return EXP_NIL;
         if (rv.poison0) return EXP_ERROR;                   // the first page fails toInternal
         if (k <= 1) {                                       // :72-75
-            emit(out, cnt, FILL, EDGE_SET | h, 0x80000000u);
+            emit(out, cnt, FILL, cap, EDGE_SET | h, 0x80000000u);
             return EXP_TREE;
         }
         if (rv.poison) return EXP_ERROR;                    // a later page fails
@@ -1742,7 +1765,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             st[sp] = cur;
             ++sp;
         }
-        emit(out, cnt, FILL, EDGE_SET | h, n_all);
+        emit(out, cnt, FILL, cap, EDGE_SET | h, n_all);
         cur = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
         return EXP_TREE;
     };
@@ -1761,14 +1784,38 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             // a normal row keeps its subject sets first: every edge left is a subject id, and each
             // is a leaf (:97-101) -- counted at once, copied in one pass
             if constexpr (FILL) {
-                uint32_t at = NONE32;
-                if (cur.left > RUN_INLINE && o.runs) {
-                    at = atomicAdd(o.n_runs, 1u);
-                    if (at < o.runs_cap) o.runs[at] = CopyRun{a + cur.pos, out + cnt, cur.left};
-                    else at = NONE32;                       // queue full: copy it here
+                if (cnt + cur.left <= cap) {                // (a staged tree past its region: counted only)
+                    bool queued = false;
+                    if (cur.left > o.run_inline && o.runs) {
+                        if (cur.left <= BIG_RUN && nr < RUNS_PER_LANE) {
+                            o.runs[nr++] = CopyRun{a + cur.pos, out + cnt, cur.left};   // (o.runs: this lane's)
+                            queued = true;
+                        } else if (cur.left > BIG_RUN) {
+                            const uint32_t pieces = (cur.left + BIG_RUN - 1) / BIG_RUN;
+                            const uint32_t at = atomicAdd(o.n_big, pieces);
+                            if ((uint64_t)at + pieces <= o.big_cap) {
+                                for (uint32_t k = 0; k < pieces; ++k)
+                                    o.big[at + k] = CopyRun{a + cur.pos + (uint64_t)k * BIG_RUN, out + cnt + (uint64_t)k * BIG_RUN,
+                                                            min(BIG_RUN, cur.left - k * BIG_RUN)};
+                                queued = true;
+                            }
+                        }
+                        if (queued) qend = max(qend, cnt + cur.left);   // (positions a later copy writes)
+                    }
+                    if (!queued) {
+                        // eight loads in flight per round, then their stores
+                        const uint32_t* src = a + cur.pos;
+                        keto_tree_node* dst = out + cnt;
+                        for (uint32_t i = 0; i < cur.left; i += 8) {
+                            uint32_t v[8];
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) v[j] = i + j < cur.left ? src[i + j] : 0u;
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (i + j < cur.left) dst[i + j] = keto_tree_node{v[j], 0x80000000u};
+                        }
+                    }
                 }
-                if (at == NONE32)
-                    for (uint32_t i = 0; i < cur.left; ++i) out[cnt + i] = keto_tree_node{a[cur.pos + i], 0x80000000u};
             }
             cnt += cur.left;
             cur.left = 0;
@@ -1777,7 +1824,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         cur.pos++;
         cur.left--;
         if (!(e & EDGE_SET)) {
-            emit(out, cnt, FILL, e, 0x80000000u);          // subject id child -> Leaf
+            emit(out, cnt, FILL, cap, e, 0x80000000u);     // subject id child -> Leaf
             continue;
         }
         const uint32_t c = e & EDGE_VAL;
@@ -1790,11 +1837,11 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         int t = V.test_add(vid, nw);
         if (t == 2) return EXP_OVERFLOW;
         if (t == 1) {                                       // visited -> nil -> Leaf(set)
-            emit(out, cnt, FILL, e, 0x80000000u);
+            emit(out, cnt, FILL, cap, e, 0x80000000u);
             continue;
         }
         int r = open(c, k);
-        if (r == EXP_NIL) emit(out, cnt, FILL, e, 0x80000000u);
+        if (r == EXP_NIL) emit(out, cnt, FILL, cap, e, 0x80000000u);
         else if (r != EXP_TREE) return r;
     }
     return EXP_TREE;
@@ -1807,9 +1854,10 @@ struct ExpandReq {
     int32_t depth;
 };
 
-template <bool FILL, class Stack>
+template <int MODE, class Stack>
 __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, const ExpandReq* __restrict__ q,
                                                      uint32_t n, int gmd, ExpandOut o, TierArgs ta) {
+    constexpr bool FILL = MODE != EXP_COUNT, STAGE = MODE == EXP_STAGE;
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     // a tree's map: its first REG_VIDS + LDS_VIDS sets in registers and the lane's LDS column (one
@@ -1828,34 +1876,116 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         st.n = ta.gstack_n;
     }
     const uint32_t total = ta.in_list ? *ta.in_count : n;
+    const uint64_t stage0 = (uint64_t)slot * o.stage_cap;    // STAGE: this lane's region
+    uint64_t used = 0;
+    uint32_t nr = 0;                                          // this lane's queued runs
+    if (FILL && o.runs) o.runs += (uint64_t)slot * RUNS_PER_LANE;
     for (uint32_t j = slot; j < total; j += stride) {
         const uint32_t i = ta.in_list ? ta.in_list[j] : j;
-        if (FILL && o.status[i] != EXP_TREE) continue;   // nil / error roots own no output
+        // nil / error roots own no output; a staged tree is already written
+        if (MODE == EXP_FILL && (o.status[i] != EXP_TREE || (o.stage_pos && o.stage_pos[i] != NOT_STAGED))) continue;
         const ExpandReq rq = q[i];
         int d = rq.depth;
         if (d <= 0 || gmd < d) d = gmd;
         uint64_t cnt = 0;
-        keto_tree_node* out = FILL ? o.nodes + o.offset[i] : nullptr;
-        int r = expand_one<FILL, Stack>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, st, o);
+        keto_tree_node* out = !FILL ? nullptr : STAGE ? o.stage + stage0 + used : o.nodes + o.offset[i];
+        const uint64_t cap = STAGE ? o.stage_cap - used : ~0ull;
+        uint64_t qend = 0;
+        int r = expand_one<FILL, Stack>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, st, o, nr, qend);
+        const bool staged = STAGE && r == EXP_TREE && cnt <= cap;
+        // a tree not staged (too big, or left to the next tier) may have queued runs into the region:
+        // that part stays dead, so the copies cannot land on the next tree
+        if (STAGE && !staged) used += qend;
         if (r == EXP_OVERFLOW) {
             uint32_t at = atomicAdd(ta.out_count, 1u);
             ta.out_list[at] = i;
-        } else if (!FILL) {
+        } else if (MODE != EXP_FILL) {
             o.count[i] = r == EXP_TREE ? cnt : 0;
             o.status[i] = (uint8_t)r;
+            if (staged) {
+                o.stage_pos[i] = stage0 + used;
+                used += cnt;
+            }
         }
     }
+    if (FILL && o.runs) o.lane_runs[slot] = nr;
     ta.slot_epoch[slot] = V.V.epoch;
 }
 
-// The queued id runs of a fill pass, a block per run (grid-stride over runs).  A run queued twice (a
-// root that overflowed a tier and was filled again on the next) is copied twice, to the same bytes.
-__global__ void __launch_bounds__(256) copy_runs(const CopyRun* __restrict__ runs, const uint32_t* __restrict__ n_runs,
-                                                 uint32_t cap) {
+// The staged trees of the one-pass expand, copied to their offsets in the node arena: a wave per
+// root (grid-stride over roots), lanes over its nodes.
+__global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict__ nodes,
+                                                     const keto_tree_node* __restrict__ stage,
+                                                     const uint64_t* __restrict__ stage_pos,
+                                                     const uint64_t* __restrict__ offset, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += waves) {
+        const uint64_t sp = stage_pos[i];
+        if (sp == NOT_STAGED) continue;
+        const uint64_t b = offset[i], c = offset[i + 1] - b;
+        for (uint64_t k = lane; k < c; k += 64) nodes[b + k] = stage[sp + k];
+    }
+}
+
+// The queued id runs of a fill pass.  A run queued twice (a root that overflowed a tier and was
+// filled again on the next) is copied twice, to the same bytes.
+//   copy_lane_runs: a wave per tier-0 lane; its runs' ids are laid end to end and the wave copies 64
+//     of them per round (lane k: flat position base + k, its run found by a search over the runs'
+//     exclusive prefix, read across lanes)
+//   copy_big_runs: a wave per BIG_RUN-id piece
+__global__ void __launch_bounds__(256) copy_lane_runs(const CopyRun* __restrict__ runs,
+                                                      const uint32_t* __restrict__ lane_runs, uint32_t lanes) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < lanes; l += waves) {
+        const uint32_t m = lane_runs[l];
+        if (m == 0) continue;
+        CopyRun c{nullptr, nullptr, 0};
+        if ((uint32_t)lane < m) c = runs[(uint64_t)l * RUNS_PER_LANE + lane];
+        const uint32_t len = (uint32_t)lane < m ? (uint32_t)c.len : 0u;
+        uint32_t incl = len;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        const uint32_t excl = incl - len;
+        const uint64_t src = (uint64_t)c.src, dst = (uint64_t)c.dst;
+        for (uint32_t base = 0; base < total; base += 64) {     // every lane takes part in the shuffles
+            const uint32_t f = base + (uint32_t)lane;
+            int j = 0;
+            for (int step = 16; step > 0; step >>= 1) {
+                const uint32_t e = __shfl(excl, j + step < 64 ? j + step : 63);
+                if ((uint32_t)(j + step) < m && e <= f) j += step;
+            }
+            const uint32_t ej = __shfl(excl, j);
+            const uint32_t slo = __shfl((uint32_t)src, j), shi = __shfl((uint32_t)(src >> 32), j);
+            const uint32_t dlo = __shfl((uint32_t)dst, j), dhi = __shfl((uint32_t)(dst >> 32), j);
+            if (f < total) {
+                const uint32_t* sp = reinterpret_cast<const uint32_t*>(((uint64_t)shi << 32) | slo);
+                keto_tree_node* dp = reinterpret_cast<keto_tree_node*>(((uint64_t)dhi << 32) | dlo);
+                dp[f - ej] = keto_tree_node{sp[f - ej], 0x80000000u};
+            }
+        }
+    }
+}
+__global__ void __launch_bounds__(256) copy_big_runs(const CopyRun* __restrict__ runs, const uint32_t* __restrict__ n_runs,
+                                                     uint32_t cap) {
     const uint32_t n = min(*n_runs, cap);
-    for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += waves) {
         const CopyRun c = runs[r];
-        for (uint64_t i = threadIdx.x; i < c.len; i += blockDim.x) c.dst[i] = keto_tree_node{c.src[i], 0x80000000u};
+        uint64_t i = lane;
+        for (; i + 192 < c.len; i += 256) {                  // four loads in flight per lane
+            const uint32_t v0 = c.src[i], v1 = c.src[i + 64], v2 = c.src[i + 128], v3 = c.src[i + 192];
+            c.dst[i] = keto_tree_node{v0, 0x80000000u};
+            c.dst[i + 64] = keto_tree_node{v1, 0x80000000u};
+            c.dst[i + 128] = keto_tree_node{v2, 0x80000000u};
+            c.dst[i + 192] = keto_tree_node{v3, 0x80000000u};
+        }
+        for (; i < c.len; i += 64) c.dst[i] = keto_tree_node{c.src[i], 0x80000000u};
     }
 }
 
@@ -1903,13 +2033,18 @@ struct DeviceState {
     uint32_t* row_handle = nullptr;   // row id -> handle (NO_UNIT: another part's root row), lazily
     uint32_t* layout_units = nullptr; // handles in arena order (increasing) and their rows, lazily:
     uint32_t* rows_by_unit = nullptr; //   expand output handle -> row id on the device
+    uint32_t* unit_row = nullptr;     // handle -> row id, direct (n_units entries; lazily, when <= 8 GiB)
     void* ex_buf = nullptr;           // expand workspace (requests, counts, statuses, offsets)
     uint64_t ex_cap = 0;
     keto_tree_node* ex_nodes = nullptr;
     uint64_t ex_nodes_cap = 0;
     CopyRun* ex_runs = nullptr;       // the fill pass's queued id runs | their count (last 8 B)
     uint32_t ex_runs_cap = 0;
-    hipEvent_t ex_ev[2] = {};         // copy_runs timing (added to tier 0 of the batch timing)
+    CopyRun* ex_big = nullptr;        // pieces of long id runs | their count (last 8 B)
+    uint32_t ex_big_cap = 0;
+    keto_tree_node* ex_stage = nullptr;   // one-pass expand: the lanes' staging regions
+    uint64_t ex_stage_nodes = 0;
+    hipEvent_t ex_ev[4] = {};         // copy_runs / gather timing (added to tier 0 of the batch timing)
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
     // host-buffer calls (device_check_host): a pipeline of chunks over two device slots, H2D on
@@ -2650,7 +2785,7 @@ void device_apply(Snapshot& S) {
         S.layout_units.swap(lu);
         S.rows_by_unit.swap(rbu);
     }
-    for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit})
+    for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit, &D.unit_row})
         if (*p) {
             (void)hipFree(*p);
             *p = nullptr;
@@ -2682,10 +2817,13 @@ void device_release(Snapshot& S) {
     if (D.coll) (void)hipFree(D.coll);
     if (D.row_handle) (void)hipFree(D.row_handle);
     if (D.layout_units) (void)hipFree(D.layout_units);
+    if (D.unit_row) (void)hipFree(D.unit_row);
     if (D.rows_by_unit) (void)hipFree(D.rows_by_unit);
     if (D.ex_buf) (void)hipFree(D.ex_buf);
     if (D.ex_nodes) (void)hipFree(D.ex_nodes);
     if (D.ex_runs) (void)hipFree(D.ex_runs);
+    if (D.ex_stage) (void)hipFree(D.ex_stage);
+    if (D.ex_big) (void)hipFree(D.ex_big);
     for (hipEvent_t e : D.ex_ev)
         if (e) (void)hipEventDestroy(e);
     if (D.xlate) (void)hipFree(D.xlate);
@@ -3596,6 +3734,22 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
 
 // Expand output: set nodes carry row handles; map them to row ids on the device (binary search in
 // the arena-order handle list; overlay handles >= ov_units_base are left for the host).
+// the direct handle -> row map: every row header's unit gets its row (other units are never looked up)
+__global__ void __launch_bounds__(256) scatter_unit_rows(uint32_t* __restrict__ unit_row, const uint32_t* __restrict__ units,
+                                                         const uint32_t* __restrict__ rows, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) unit_row[units[i]] = rows[i];
+}
+__global__ void __launch_bounds__(256) handles_to_rows_direct(keto_tree_node* __restrict__ nodes, uint64_t n,
+                                                              const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = nodes[i].subject;
+    if (!(x & EDGE_SET)) return;
+    const uint32_t h = x & EDGE_VAL;
+    if (h >= ov_units_base) return;
+    nodes[i].subject = EDGE_SET | unit_row[h];
+}
 __global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restrict__ nodes, uint64_t n,
                                                        const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
                                                        uint32_t n_rows, uint32_t ov_units_base) {
@@ -3705,8 +3859,9 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     };
     OverlayBuf ov(S, ovh);
     uint64_t acc = 0;
-    // workspace, reused across calls: requests | counts (n + 1) | offsets (n + 1) | statuses
-    const uint64_t need = (uint64_t)n * sizeof(ExpandReq) + 2ull * (n + 1) * sizeof(uint64_t) + n + 64;
+    // workspace, reused across calls: requests | counts (n + 1) | offsets (n + 1) | stage positions
+    // (n) | statuses
+    const uint64_t need = (uint64_t)n * sizeof(ExpandReq) + 3ull * (n + 1) * sizeof(uint64_t) + n + 64;
     if (D.ex_cap < need) {
         if (D.ex_buf) (void)hipFree(D.ex_buf);
         D.ex_cap = std::max<uint64_t>(need, 1 << 20);
@@ -3715,7 +3870,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     uint8_t* base = (uint8_t*)D.ex_buf;
     uint64_t* dcount = reinterpret_cast<uint64_t*>(base);
     uint64_t* doff = dcount + (n + 1);
-    ExpandReq* dq = reinterpret_cast<ExpandReq*>(doff + (n + 1));
+    uint64_t* dstage = doff + (n + 1);
+    ExpandReq* dq = reinterpret_cast<ExpandReq*>(dstage + (n + 1));
     uint8_t* dstatus = reinterpret_cast<uint8_t*>(dq + n);
     {
         std::vector<ExpandReq> hq(n);
@@ -3727,8 +3883,53 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     Plan p = make_plan(D, n, gmd);            // expand holds at most gmd frames
     DevSnap sv = D.view();
     DevOverlay dov = ov.v;
-    ExpandOut o{nullptr, nullptr, dcount, dstatus, nullptr, nullptr, 0};
-    // (the batch timing sums both passes' tiers: keto_last_batch_timing after an expand)
+    // One pass (default): tier 0 writes every tree into its lane's staging region while it counts it;
+    // the host scans the counts; a wave per root copies the staged trees to their offsets.  Trees that
+    // did not fit (or that a later tier decided, counting only) are filled by a second pass over just
+    // them.  KETO_EXPAND_STAGE=0: count pass + fill pass over every root (the two-pass form); =N > 1:
+    // N nodes of staging per lane.
+    const char* se = getenv("KETO_EXPAND_STAGE");
+    const bool staged = !se || atoi(se) != 0;
+    uint64_t stage_cap = 0;
+    if (staged) {
+        const uint64_t budget = 1ull << 29;                               // staging nodes (4 GiB)
+        stage_cap = std::min<uint64_t>(16384, std::max<uint64_t>(64, budget / p.slots[0]));
+        if (se && atoi(se) > 1) stage_cap = (uint64_t)atoi(se);            // tests: small regions spill
+        const uint64_t nodes = stage_cap * p.slots[0];
+        if (D.ex_stage_nodes < nodes) {
+            if (D.ex_stage) (void)hipFree(D.ex_stage);
+            D.ex_stage = nullptr;
+            D.ex_stage_nodes = 0;
+            D.ex_stage = dmalloc<keto_tree_node>(nodes, acc);
+            D.ex_stage_nodes = nodes;
+        }
+    }
+    // the id-run queues of tier 0's lanes (RUNS_PER_LANE entries each) | runs queued per lane
+    const char* ri = getenv("KETO_EXPAND_RUN_INLINE");
+    const uint32_t run_inline = ri ? (uint32_t)atoi(ri) : RUN_INLINE_DEFAULT;
+    if (D.ex_runs_cap < p.slots[0]) {
+        if (D.ex_runs) (void)hipFree(D.ex_runs);
+        D.ex_runs = nullptr;
+        D.ex_runs_cap = 0;
+        D.ex_runs = reinterpret_cast<CopyRun*>(
+            dmalloc<uint8_t>((uint64_t)p.slots[0] * (RUNS_PER_LANE * sizeof(CopyRun) + sizeof(uint32_t)), acc));
+        D.ex_runs_cap = p.slots[0];
+    }
+    uint32_t* d_lane_runs = reinterpret_cast<uint32_t*>(D.ex_runs + (uint64_t)D.ex_runs_cap * RUNS_PER_LANE);
+    // the big-run pieces: nodes / BIG_RUN bounds them, plus slack for roots filled again on a later
+    // tier (a full queue copies in place)
+    auto ensure_big = [&](uint64_t nodes) {
+        const uint32_t cap = (uint32_t)std::min<uint64_t>(nodes / BIG_RUN + 4096, 1u << 26);
+        if (D.ex_big_cap >= cap) return;
+        if (D.ex_big) (void)hipFree(D.ex_big);
+        D.ex_big = nullptr;
+        D.ex_big_cap = 0;
+        D.ex_big = reinterpret_cast<CopyRun*>(dmalloc<uint8_t>((uint64_t)cap * sizeof(CopyRun) + 8, acc));
+        D.ex_big_cap = cap;
+    };
+    for (int e = 0; e < 4; ++e)
+        if (!D.ex_ev[e]) HIP_OK(hipEventCreate(&D.ex_ev[e]));
+    // (the batch timing sums the passes' tiers: keto_last_batch_timing after an expand)
     auto launch_pass = [&](bool fill, const ExpandOut& eo) {
         run_tiers(D, D.ews, n, p, st,
                   [&](int level, Tier& t, const uint32_t* il, const uint32_t* ic, uint32_t* ol, uint32_t* oc,
@@ -3737,35 +3938,80 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                       const uint32_t bs = std::min<uint32_t>(256, slots);
                       dim3 grid(slots / bs), block(bs);
                       const bool local = p.frames[level] == 0;
-                      if (!fill && local)
-                          hipLaunchKernelGGL((expand_kernel<false, LocalStack<16>>), grid, block, 0, st, sv, dov, dq,
-                                             n, gmd, eo, a);
-                      else if (!fill)
-                          hipLaunchKernelGGL((expand_kernel<false, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
-                                             gmd, eo, a);
+                      const int mode = fill ? EXP_FILL : (eo.stage && level == 0) ? EXP_STAGE : EXP_COUNT;
+                      ExpandOut e = eo;
+                      if (level > 0) e.runs = nullptr;         // later tiers copy their runs in place
+                      if (mode == EXP_COUNT && local)
+                          hipLaunchKernelGGL((expand_kernel<EXP_COUNT, LocalStack<16>>), grid, block, 0, st, sv, dov,
+                                             dq, n, gmd, e, a);
+                      else if (mode == EXP_COUNT)
+                          hipLaunchKernelGGL((expand_kernel<EXP_COUNT, GlobalStack>), grid, block, 0, st, sv, dov, dq,
+                                             n, gmd, e, a);
+                      else if (mode == EXP_STAGE && local)
+                          hipLaunchKernelGGL((expand_kernel<EXP_STAGE, LocalStack<16>>), grid, block, 0, st, sv, dov,
+                                             dq, n, gmd, e, a);
+                      else if (mode == EXP_STAGE)
+                          hipLaunchKernelGGL((expand_kernel<EXP_STAGE, GlobalStack>), grid, block, 0, st, sv, dov, dq,
+                                             n, gmd, e, a);
                       else if (local)
-                          hipLaunchKernelGGL((expand_kernel<true, LocalStack<16>>), grid, block, 0, st, sv, dov, dq,
-                                             n, gmd, eo, a);
+                          hipLaunchKernelGGL((expand_kernel<EXP_FILL, LocalStack<16>>), grid, block, 0, st, sv, dov,
+                                             dq, n, gmd, e, a);
                       else
-                          hipLaunchKernelGGL((expand_kernel<true, GlobalStack>), grid, block, 0, st, sv, dov, dq, n,
-                                             gmd, eo, a);
+                          hipLaunchKernelGGL((expand_kernel<EXP_FILL, GlobalStack>), grid, block, 0, st, sv, dov, dq,
+                                             n, gmd, e, a);
                       HIP_OK(hipGetLastError());
                   },
                   Undecided{dstatus, fill ? nullptr : dcount, (uint8_t)EXP_OVERFLOW}, fill);
     };
-    // count pass, exclusive scan on the host, fill pass (same tier plan: a root overflows on the
-    // same tiers both times, and a partial pre-order is a prefix of the full one)
-    launch_pass(false, o);
+    uint32_t* d_nbig = nullptr;
+    auto copy_queued = [&]() {
+        hipLaunchKernelGGL(copy_lane_runs, dim3((p.slots[0] + 3) / 4), dim3(256), 0, st,
+                           D.ex_runs, d_lane_runs, p.slots[0]);
+        hipLaunchKernelGGL(copy_big_runs, dim3(std::min<uint32_t>((D.ex_big_cap + 3) / 4, 4096)), dim3(256), 0, st,
+                           D.ex_big, d_nbig, D.ex_big_cap);
+        HIP_OK(hipGetLastError());
+    };
+    auto big_queue = [&](uint64_t nodes) {
+        ensure_big(nodes);
+        d_nbig = reinterpret_cast<uint32_t*>(D.ex_big + D.ex_big_cap);
+        HIP_OK(hipMemsetAsync(d_nbig, 0, sizeof(uint32_t), st));
+    };
+    // pass 1: count (and stage), then the staged trees' queued id runs
+    HIP_OK(hipMemsetAsync(dstage, 0xFF, (uint64_t)n * sizeof(uint64_t), st));
+    if (staged) big_queue(stage_cap * p.slots[0]);
+    launch_pass(false, ExpandOut{nullptr, nullptr, dcount, dstatus, staged ? D.ex_runs : nullptr, d_lane_runs,
+                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage});
+    float extra_ms = 0;
+    if (staged) {
+        HIP_OK(hipEventRecord(D.ex_ev[0], st));
+        copy_queued();
+        HIP_OK(hipEventRecord(D.ex_ev[1], st));
+    }
     lap("count");
-    std::vector<uint64_t> cnt(n);
+    std::vector<uint64_t> cnt(n), spos;
     HIP_OK(hipMemcpyAsync(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(out.status.data(), dstatus, n, hipMemcpyDeviceToHost, st));
+    if (staged) {
+        spos.resize(n);
+        HIP_OK(hipMemcpyAsync(spos.data(), dstage, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    }
     HIP_OK(hipStreamSynchronize(st));
-    for (uint32_t i = 0; i < n; ++i) out.offset[i + 1] = out.offset[i] + cnt[i];
+    if (staged) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, D.ex_ev[0], D.ex_ev[1]) == hipSuccess) extra_ms += ms;
+    }
+    uint32_t unstaged = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        out.offset[i + 1] = out.offset[i] + cnt[i];
+        unstaged += (!staged || spos[i] == NOT_STAGED) && out.status[i] == EXP_TREE && cnt[i];
+    }
     const uint64_t total = out.offset[n];
     out.nodes.resize(total);
     lap("scan");
-    if (total == 0) return;
+    if (total == 0) {
+        D.last.tier_ms[0] += extra_ms;
+        return;
+    }
     if (D.ex_nodes_cap < total) {
         if (D.ex_nodes) (void)hipFree(D.ex_nodes);
         D.ex_nodes_cap = std::max<uint64_t>(total, 1 << 16);
@@ -3779,31 +4025,38 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                          hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(D.rows_by_unit, S.rows_by_unit.data(), S.rows_by_unit.size() * sizeof(uint32_t),
                          hipMemcpyHostToDevice));
+        // the direct map (one word per arena unit) when it is small next to the arena; else the
+        // handle -> row translation binary-searches the handle list
+        if (S.n_units && S.n_units * sizeof(uint32_t) <= (8ull << 30)) {
+            D.unit_row = dmalloc<uint32_t>(S.n_units, acc);
+            const uint32_t m32 = (uint32_t)S.layout_units.size();
+            if (m32)
+                hipLaunchKernelGGL(scatter_unit_rows, dim3((m32 + 255) / 256), dim3(256), 0, st, D.unit_row,
+                                   D.layout_units, D.rows_by_unit, m32);
+            HIP_OK(hipGetLastError());
+        }
     }
     HIP_OK(hipMemcpyAsync(doff, out.offset.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    // id runs longer than RUN_INLINE hold more than RUN_INLINE nodes each: total / (RUN_INLINE + 1)
-    // bounds them (slack for roots filled again on a later tier; a full queue copies in place)
-    const uint32_t runs_cap = (uint32_t)std::min<uint64_t>(total / (RUN_INLINE + 1) + 4096, 1u << 30);
-    if (D.ex_runs_cap < runs_cap) {
-        if (D.ex_runs) (void)hipFree(D.ex_runs);
-        D.ex_runs = nullptr;
-        D.ex_runs_cap = 0;
-        D.ex_runs = reinterpret_cast<CopyRun*>(dmalloc<uint8_t>((uint64_t)runs_cap * sizeof(CopyRun) + 8, acc));
-        D.ex_runs_cap = runs_cap;
+    // pass 2: the trees not staged, filled at their offsets (every root when not staging)
+    if (unstaged) {
+        big_queue(total);
+        launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_lane_runs, run_inline, D.ex_big,
+                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr});
     }
-    uint32_t* d_nruns = reinterpret_cast<uint32_t*>(D.ex_runs + D.ex_runs_cap);
-    HIP_OK(hipMemsetAsync(d_nruns, 0, sizeof(uint32_t), st));
-    launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_nruns, D.ex_runs_cap});
-    for (int e = 0; e < 2; ++e)
-        if (!D.ex_ev[e]) HIP_OK(hipEventCreate(&D.ex_ev[e]));
-    HIP_OK(hipEventRecord(D.ex_ev[0], st));
-    hipLaunchKernelGGL(copy_runs, dim3(std::min<uint32_t>(D.ex_runs_cap, 8192)), dim3(256), 0, st, D.ex_runs, d_nruns,
-                       D.ex_runs_cap);
+    HIP_OK(hipEventRecord(D.ex_ev[2], st));
+    if (unstaged) copy_queued();
+    if (staged)
+        hipLaunchKernelGGL(gather_staged, dim3((unsigned)std::min<uint64_t>((n + 3) / 4, 16384)), dim3(256), 0, st,
+                           D.ex_nodes, D.ex_stage, dstage, doff, n);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(D.ex_ev[1], st));
+    HIP_OK(hipEventRecord(D.ex_ev[3], st));
     lap("fill");
-    hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
-                       D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
+    if (D.unit_row)
+        hipLaunchKernelGGL(handles_to_rows_direct, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes,
+                           total, D.unit_row, (uint32_t)S.n_units);
+    else
+        hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
+                           D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
     HIP_OK(hipGetLastError());
     lap("h2rows");
     HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
@@ -3811,8 +4064,10 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     lap("d2h");
     {
         float ms = 0;
-        if (hipEventElapsedTime(&ms, D.ex_ev[0], D.ex_ev[1]) == hipSuccess) D.last.tier_ms[0] += ms;
+        if (hipEventElapsedTime(&ms, D.ex_ev[2], D.ex_ev[3]) == hipSuccess) extra_ms += ms;
+        D.last.tier_ms[0] += extra_ms;
     }
+    if (trace) fprintf(stderr, "[expand] %u of %u trees filled by the second pass\n", unstaged, n);
     // overlay handles -> ovh->base + overlay index (batch-local wildcard roots only)
     if (ovh && !ovh->empty())
         host_parallel_for(total, [&](uint64_t i) {

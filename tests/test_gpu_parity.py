@@ -69,6 +69,45 @@ def test_random_graphs_match_oracle(seed, wide):
             assert (have, js) == want, (seed, s, d, g)
 
 
+STAGE_ENVS = {
+    "two_pass": {"KETO_EXPAND_STAGE": "0"},
+    "tiny_regions": {"KETO_EXPAND_STAGE": "3"},                    # most trees spill to the second pass
+    "shared_regions": {"KETO_EXPAND_STAGE": "40", "KETO_SLOTS": "256"},   # many roots per lane's region
+    "default_few_slots": {"KETO_SLOTS": "256"},                   # lanes' run queues fill: runs copied in place
+    "inline_runs": {"KETO_EXPAND_RUN_INLINE": "32"},
+}
+
+
+@pytest.mark.parametrize("env", sorted(STAGE_ENVS))
+@pytest.mark.parametrize("seed", range(3300, 3330))
+def test_expand_staging_modes_match_oracle(monkeypatch, env, seed):
+    """The one-pass expand (trees staged in per-lane regions while counted, then gathered to their
+    offsets; trees that do not fit filled by a second pass) in every regime: the two-pass form,
+    regions so small that most trees spill, many roots sharing one lane's region, the default
+    regions with few lanes (whose id-run queues fill up), and short id runs copied in place.  Trees
+    equal the oracle's, child order included."""
+    from keto_amd.capi import EXPAND_NIL, EXPAND_NOT_FOUND, EXPAND_TREE
+    for k, v in STAGE_ENVS[env].items():
+        monkeypatch.setenv(k, v)
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=seed % 3 == 0)
+    snap = _snapshot(ns, rows_from_tuples(ns, tuples, raw), ps)
+    exps = random_expands(seed, alph, k=600)
+    for g in sorted({e[2] for e in exps}):
+        grp = [e for e in exps if e[2] == g]
+        got = snap.expand_batch([(subj(s), d) for s, d, _ in grp], g)
+        want_cache = {}
+        for (s, d, _), (st, js) in zip(grp, got):
+            key = (repr(s), d)
+            if key not in want_cache:
+                try:
+                    t = ExpandEngine(store, g).build_tree(s, d)
+                    want_cache[key] = ("tree", t.to_json()) if t is not None else ("nil", None)
+                except NotFoundError:
+                    want_cache[key] = ("error", None)
+            have = {EXPAND_TREE: "tree", EXPAND_NIL: "nil", EXPAND_NOT_FOUND: "error"}[st]
+            assert (have, js) == want_cache[key], (env, seed, s, d, g)
+
+
 @pytest.mark.parametrize("seed", range(2100, 2160))
 def test_random_expand_proto_device_equals_host(seed):
     """keto_tree_proto_all_device on quirk-heavy random graphs (wildcard roots answered by batch-local

@@ -307,8 +307,10 @@ def config5(a, g=None):
     return {"config": "#5 expand (100k roots on the #3 graph, max-depth 5)", "tuples": int(g.n_edges), "roots": n,
             "gpu": {"trees_per_s": round(n / best, 1), "wall_ms": round(best * 1e3, 3),
                     "kernel_ms": round(kern, 3),
-                    "what": "keto_expand_batch_ids: H2D roots, count pass, host scan, fill pass, D2H tree arena; "
-                            "kernel_ms = both passes' tier kernels and the fill pass's id-run copies (HIP events)"},
+                    "what": "keto_expand_batch_ids: H2D roots, one pass (trees counted and staged in per-lane "
+                            "regions), host scan, second pass for trees that did not fit, id-run copies, gather to "
+                            "offsets, handle -> row ids, D2H tree arena; kernel_ms = the passes' tier kernels, the "
+                            "id-run copies and the gather (HIP events; not the handle -> row map)"},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern, 3),
                          "alg_bytes_per_root": round(per, 1),
