@@ -179,6 +179,14 @@ int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespac
 
 void keto_snapshot_release(keto_snapshot* s);
 
+/* A replica of an unpartitioned snapshot for another device (device = -1: host only), at the source's
+ * current version, without scanning or sorting the table again: the host tables are copied and laid
+ * out afresh, then uploaded.  One server process serving the node's GPUs keeps one replica per
+ * device, deals batches among them and applies every write transaction to each (the reference serves
+ * every request from one process, internal/driver/daemon.go:62-69, on engines built once per registry,
+ * internal/driver/registry_default.go:159-171).  Replicas are independent snapshots afterwards. */
+int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot** out);
+
 /* Snapshot lifecycle: apply one write transaction the way TransactRelationTuples does
  * (internal/persistence/sql/relationtuples.go:289-297): the inserts first (each after every equal
  * tuple, as commit_time orders them, :128-149), then the deletes (every tuple equal in namespace,
@@ -358,16 +366,31 @@ void keto_host_free(void* p);
 int keto_check_batch_device(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, int32_t global_max_depth,
                             uint8_t* d_allowed_out, void* stream);
 
-/* ---- Multi-GPU over RCCL (xGMI), one process per GPU (repo:keto_amd/csrc/comm.cpp) ----
+/* ---- Multi-GPU: communicators (repo:keto_amd/csrc/comm.cpp) ----
  * The exchanges of SURVEY.md 8(e) inside the library, for callers without Python (the Go server
  * process, internal/driver/daemon.go:62-69, calling check.(*Engine).SubjectIsAllowed per request,
- * internal/check/engine.go:116-123).  keto_comm_id makes a communicator id on one rank; the caller
- * hands its KETO_COMM_ID_BYTES to every rank (its own channel), and every rank calls
- * keto_comm_init with it.  Every call below is collective: all ranks of the communicator call it. */
+ * internal/check/engine.go:116-123).  Every call below taking a keto_comm is collective: all ranks of
+ * the communicator call it.  Errors are agreed: a rank whose own part fails (a bad argument, a
+ * request it cannot route, an allocation or kernel error) still takes part in the status exchange
+ * that precedes every data exchange, and every rank then returns the same code (that of the lowest
+ * failing rank; keto_last_error says which rank failed), so a local error never leaves the peers
+ * waiting.  Only a failing transport (RCCL, or a local rank that does not arrive within
+ * KETO_COMM_TIMEOUT_MS, default 600000) returns KETO_E_HIP without agreement.
+ *
+ * Two transports:
+ *   keto_comm_init        one process per GPU over RCCL (xGMI).  keto_comm_id makes a communicator id
+ *                         on one rank; the caller hands its KETO_COMM_ID_BYTES to every rank (its own
+ *                         channel), and every rank calls keto_comm_init with it.
+ *   keto_comm_init_local  the ranks are threads of ONE process (one server process driving several
+ *                         GPUs, or several parts on one GPU), each rank's calls made from its own
+ *                         thread; the exchanges are device copies (peer copies between GPUs).  The id
+ *                         is any KETO_COMM_ID_BYTES the caller chooses (the same for every rank of the
+ *                         communicator, unique among the process's live local communicators). */
 #define KETO_COMM_ID_BYTES 128
 typedef struct keto_comm keto_comm;
 int keto_comm_id(uint8_t* id_out);
 int keto_comm_init(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, keto_comm** out);
+int keto_comm_init_local(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, keto_comm** out);
 void keto_comm_free(keto_comm* c);
 /* Replicated snapshot (every rank uploaded the whole graph): every rank passes the same n named
  * requests (keto_check_batch's form); rank r decides the r-th contiguous shard, and one all-gather

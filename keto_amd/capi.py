@@ -38,7 +38,7 @@ EXPORTS = [
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
     "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
     "keto_comm_id", "keto_comm_init", "keto_comm_free", "keto_check_batch_sharded", "keto_check_batch_routed",
-    "keto_comm_close_filters",
+    "keto_comm_close_filters", "keto_comm_init_local", "keto_snapshot_clone",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -46,7 +46,9 @@ FILTER_WORDS = 22
 
 
 class KetoError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class KStr(C.Structure):
@@ -172,7 +174,7 @@ def load():
 
 def _check(rc):
     if rc != KETO_OK:
-        raise KetoError(f"keto error {rc}: {load().keto_last_error().decode(errors='replace')}")
+        raise KetoError(f"keto error {rc}: {load().keto_last_error().decode(errors='replace')}", rc)
 
 
 def route_work_bytes(n: int, n_parts: int) -> int:
@@ -309,6 +311,12 @@ class Snapshot:
         opts = KOpts(page_size, device, 0)
         _check(lib.keto_snapshot_build(ns, len(namespaces), tt, C.c_uint64(len(rows)), C.byref(opts), C.byref(h)))
         return cls(h, lib)
+
+    def clone(self, device: int = 0) -> "Snapshot":
+        """keto_snapshot_clone: a replica of this snapshot (current version) on another device."""
+        h = C.c_void_p()
+        _check(self.lib.keto_snapshot_clone(self.h, C.c_int32(device), C.byref(h)))
+        return Snapshot(h, self.lib)
 
     def upload_part(self, part: int, n_parts: int, device: int = 0, mode: int = PART_SHARED, hot_bytes: int = 0):
         """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part_mode; a migrating
@@ -738,11 +746,14 @@ class Comm:
         _check(load().keto_comm_id(buf))
         return bytes(buf)
 
-    def __init__(self, comm_id: bytes, n_ranks: int, rank: int, device: int = 0):
+    def __init__(self, comm_id: bytes, n_ranks: int, rank: int, device: int = 0, local: bool = False):
+        """local: keto_comm_init_local (the ranks are threads of this process; comm_id any 128 bytes)."""
         self.lib = load()
         self.h = C.c_void_p()
-        idb = (C.c_uint8 * 128).from_buffer_copy(comm_id)
-        _check(self.lib.keto_comm_init(idb, C.c_int32(n_ranks), C.c_int32(rank), C.c_int32(device), C.byref(self.h)))
+        self.rank, self.n_ranks = rank, n_ranks
+        idb = (C.c_uint8 * 128).from_buffer_copy(comm_id.ljust(128, b"\0")[:128])
+        init = self.lib.keto_comm_init_local if local else self.lib.keto_comm_init
+        _check(init(idb, C.c_int32(n_ranks), C.c_int32(rank), C.c_int32(device), C.byref(self.h)))
 
     def close(self):
         if self.h:

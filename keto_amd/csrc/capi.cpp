@@ -364,6 +364,21 @@ int keto_snapshot_from_csr(const keto_namespace* namespaces, uint32_t n_namespac
     });
 }
 
+int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot** out) {
+    return guarded([&] {
+        if (!src || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        *out = nullptr;
+        auto h = std::make_unique<keto_snapshot>();
+        {
+            std::shared_lock<std::shared_mutex> lk(src->s->rw);      // one version: no apply copies under us
+            h->s = clone_host(*src->s);
+        }
+        if (device >= 0) device_upload(*h->s, device);
+        *out = h.release();
+        return KETO_OK;
+    });
+}
+
 void keto_snapshot_release(keto_snapshot* s) { delete s; }
 
 int keto_snapshot_get_stats(const keto_snapshot* h, keto_snapshot_stats* out) {

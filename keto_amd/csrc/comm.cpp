@@ -1,7 +1,6 @@
-// Multi-GPU check batches over RCCL (xGMI), behind the C-ABI: one process per GPU, the exchanges
-// keto_amd/multi.py runs over torch.distributed, here in the library so that a caller without
-// Python -- the Go server, one process per GPU (internal/driver/daemon.go:62-69) -- can use every
-// multi-GPU mode:
+// Multi-GPU check batches behind the C-ABI: the exchanges keto_amd/multi.py runs over
+// torch.distributed, here in the library so that a caller without Python -- the Go server
+// (internal/driver/daemon.go:62-69) -- can use every multi-GPU mode:
 //
 //   keto_check_batch_sharded    replicated snapshot: rank r checks the r-th contiguous shard of the
 //                               batch, one all-gather returns every decision to every rank
@@ -9,17 +8,36 @@
 //                               rank's own batch is routed to the parts owning the requests' rows
 //                               (one all-to-all), decided there, and the decisions come back (a
 //                               second all-to-all); on a migrating partition the owners run the
-//                               continuation-record rounds (an all-reduce and all-to-alls a round)
+//                               continuation-record rounds (an all-gather and all-to-alls a round)
 //   keto_comm_close_filters     a migrating partition's closure-filter exchange after upload
 //
-// All collectives run on the communicator's own stream with device buffers that are kept across
-// calls.  The reference serves each check on one goroutine against one database
+// Two transports carry the collectives:
+//   RCCL  (keto_comm_init)        one process per GPU over xGMI: grouped ncclSend / ncclRecv
+//                                 all-to-alls and all-gathers on the communicator's stream
+//   local (keto_comm_init_local)  the ranks are threads of one process, each with its own stream
+//                                 (on one GPU or several): a rendezvous in host memory and device
+//                                 copies (peer copies over xGMI between GPUs).  One server process
+//                                 can serve a partitioned graph over the node's GPUs this way, and
+//                                 the multi-rank logic runs on a one-GPU box.
+//
+// Errors never leave a peer waiting: a rank-local failure (a bad argument, a request that cannot be
+// routed, an allocation, a kernel error) is caught, and before every data exchange the ranks agree
+// on their status (an all-gather of error codes, folded into the count exchanges where there is
+// one).  If any rank failed, every rank returns the code of the lowest failing rank.  Only a failure
+// of the transport itself (RCCL, or a local peer that never arrives: KETO_COMM_TIMEOUT_MS, default
+// 10 minutes) ends a call without agreement, and it marks the communicator broken.
+//
+// The reference serves each check on one goroutine against one database
 // (internal/check/handler.go:108-184); batching across GPUs is this engine's.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -63,23 +81,230 @@ struct DBuf {                     // grow-only device buffer
     }
 };
 
+// ------------------------------------------------------------------ transports
+// Collectives over the ranks of one communicator.  Device-buffer calls are enqueued on `st` and
+// complete before they return (the callers read the results on the host or launch on `st`).
+struct Transport {
+    virtual ~Transport() = default;
+    // bytes: send[sdisp(p), +scount[p]) to rank p; recv[rdisp(p), +rcount[p]) from rank p (device)
+    virtual void alltoallv(const void* send, const std::vector<uint64_t>& scount, void* recv,
+                           const std::vector<uint64_t>& rcount, hipStream_t st) = 0;
+    // every rank's `bytes` at send -> recv + p * bytes (device)
+    virtual void allgather(const void* send, void* recv, uint64_t bytes, hipStream_t st) = 0;
+    // host words: in[p * k + j] goes to rank p, arriving as out[src * k + j]
+    virtual std::vector<uint64_t> alltoall_u64(const std::vector<uint64_t>& in, int k, hipStream_t st) = 0;
+    // host words: every rank's `in` (the same length on every rank), in rank order
+    virtual std::vector<uint64_t> allgather_u64(const std::vector<uint64_t>& in, hipStream_t st) = 0;
+};
+
+struct RcclTransport final : Transport {
+    ncclComm_t comm = nullptr;
+    int n = 1;
+    DBuf small;
+    ~RcclTransport() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    void alltoallv(const void* send, const std::vector<uint64_t>& scount, void* recv, const std::vector<uint64_t>& rcount,
+                   hipStream_t st) override {
+        uint64_t so = 0, ro = 0;
+        NCCL_OK(ncclGroupStart());
+        for (int p = 0; p < n; ++p) {
+            if (scount[p]) NCCL_OK(ncclSend(static_cast<const uint8_t*>(send) + so, scount[p], ncclUint8, p, comm, st));
+            if (rcount[p]) NCCL_OK(ncclRecv(static_cast<uint8_t*>(recv) + ro, rcount[p], ncclUint8, p, comm, st));
+            so += scount[p];
+            ro += rcount[p];
+        }
+        NCCL_OK(ncclGroupEnd());
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    void allgather(const void* send, void* recv, uint64_t bytes, hipStream_t st) override {
+        if (bytes) NCCL_OK(ncclAllGather(send, recv, bytes, ncclUint8, comm, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    std::vector<uint64_t> alltoall_u64(const std::vector<uint64_t>& in, int k, hipStream_t st) override {
+        uint64_t* d_in = small.get<uint64_t>((uint64_t)n * k * 2);
+        uint64_t* d_out = d_in + (uint64_t)n * k;
+        HIP_OK(hipMemcpyAsync(d_in, in.data(), in.size() * 8, hipMemcpyHostToDevice, st));
+        NCCL_OK(ncclGroupStart());
+        for (int p = 0; p < n; ++p) {
+            NCCL_OK(ncclSend(d_in + (uint64_t)p * k, k, ncclUint64, p, comm, st));
+            NCCL_OK(ncclRecv(d_out + (uint64_t)p * k, k, ncclUint64, p, comm, st));
+        }
+        NCCL_OK(ncclGroupEnd());
+        std::vector<uint64_t> out((uint64_t)n * k);
+        HIP_OK(hipMemcpyAsync(out.data(), d_out, out.size() * 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        return out;
+    }
+    std::vector<uint64_t> allgather_u64(const std::vector<uint64_t>& in, hipStream_t st) override {
+        const uint64_t k = in.size();
+        uint64_t* d_in = small.get<uint64_t>(k * (n + 1));
+        uint64_t* d_out = d_in + k;
+        HIP_OK(hipMemcpyAsync(d_in, in.data(), k * 8, hipMemcpyHostToDevice, st));
+        NCCL_OK(ncclAllGather(d_in, d_out, k, ncclUint64, comm, st));
+        std::vector<uint64_t> out(k * n);
+        HIP_OK(hipMemcpyAsync(out.data(), d_out, out.size() * 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        return out;
+    }
+};
+
+// The rendezvous of a local communicator: what each rank posted for the current collective, and a
+// generation barrier.  Ranks find it by the caller's 128-B id (a process-wide registry).
+struct LocalHub {
+    int n = 0;
+    int refs = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;
+    int arrived = 0;
+    bool broken = false;
+    std::string why;
+    struct Post {
+        const void* dsend = nullptr;
+        int device = 0;
+        std::vector<uint64_t> sdisp, scount, host;
+    };
+    std::vector<Post> post;
+};
+std::mutex g_hubs_mu;
+std::map<std::string, std::shared_ptr<LocalHub>> g_hubs;
+
+int64_t timeout_ms() {
+    const char* e = getenv("KETO_COMM_TIMEOUT_MS");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? v : 600000;
+}
+
+struct LocalTransport final : Transport {
+    std::shared_ptr<LocalHub> hub;
+    std::string key;
+    int rank = 0, n = 1, device = 0;
+    ~LocalTransport() override {
+        std::lock_guard<std::mutex> g(g_hubs_mu);
+        if (hub && --hub->refs == 0) g_hubs.erase(key);
+    }
+    [[noreturn]] void fail(const std::string& why) {
+        {
+            std::lock_guard<std::mutex> lk(hub->mu);
+            if (!hub->broken) {
+                hub->broken = true;
+                hub->why = why;
+            }
+        }
+        hub->cv.notify_all();
+        throw Error{KETO_E_HIP, "local communicator broken: " + why};
+    }
+    // every rank arrives before any leaves; a peer that does not arrive within the timeout, or a
+    // broken hub, fails the call on every rank still waiting
+    void barrier() {
+        std::unique_lock<std::mutex> lk(hub->mu);
+        if (hub->broken) throw Error{KETO_E_HIP, "local communicator broken: " + hub->why};
+        const uint64_t g = hub->gen;
+        if (++hub->arrived == n) {
+            hub->arrived = 0;
+            ++hub->gen;
+            lk.unlock();
+            hub->cv.notify_all();
+            return;
+        }
+        const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms());
+        if (!hub->cv.wait_until(lk, until, [&] { return hub->gen != g || hub->broken; })) {
+            lk.unlock();
+            fail("rank " + std::to_string(rank) + " timed out waiting for its peers");
+        }
+        if (hub->gen == g) throw Error{KETO_E_HIP, "local communicator broken: " + hub->why};
+    }
+    void put(const void* dsend, const std::vector<uint64_t>& scount, std::vector<uint64_t> host) {
+        std::lock_guard<std::mutex> lk(hub->mu);
+        LocalHub::Post& p = hub->post[rank];
+        p.dsend = dsend;
+        p.device = device;
+        p.scount = scount;
+        p.sdisp.assign(scount.size(), 0);
+        for (size_t q = 1; q < scount.size(); ++q) p.sdisp[q] = p.sdisp[q - 1] + scount[q - 1];
+        p.host = std::move(host);
+    }
+    void alltoallv(const void* send, const std::vector<uint64_t>& scount, void* recv, const std::vector<uint64_t>& rcount,
+                   hipStream_t st) override {
+        HIP_OK(hipStreamSynchronize(st));            // this rank's send data is complete
+        put(send, scount, {});
+        barrier();
+        uint64_t ro = 0;
+        for (int p = 0; p < n; ++p) {
+            const LocalHub::Post& src = hub->post[p];
+            if (src.scount[rank] != rcount[p])
+                fail("rank " + std::to_string(rank) + " expected " + std::to_string(rcount[p]) + " bytes from rank " +
+                     std::to_string(p) + ", which sends " + std::to_string(src.scount[rank]));
+            if (rcount[p]) {
+                const void* from = static_cast<const uint8_t*>(src.dsend) + src.sdisp[rank];
+                void* to = static_cast<uint8_t*>(recv) + ro;
+                if (src.device == device) HIP_OK(hipMemcpyAsync(to, from, rcount[p], hipMemcpyDeviceToDevice, st));
+                else HIP_OK(hipMemcpyPeerAsync(to, device, from, src.device, rcount[p], st));
+            }
+            ro += rcount[p];
+        }
+        HIP_OK(hipStreamSynchronize(st));
+        barrier();                                  // every copy out of the send buffers is done
+    }
+    void allgather(const void* send, void* recv, uint64_t bytes, hipStream_t st) override {
+        HIP_OK(hipStreamSynchronize(st));
+        put(send, std::vector<uint64_t>(n, 0), {});
+        barrier();
+        for (int p = 0; p < n; ++p) {
+            const LocalHub::Post& src = hub->post[p];
+            void* to = static_cast<uint8_t*>(recv) + (uint64_t)p * bytes;
+            if (!bytes) continue;
+            if (src.device == device) HIP_OK(hipMemcpyAsync(to, src.dsend, bytes, hipMemcpyDeviceToDevice, st));
+            else HIP_OK(hipMemcpyPeerAsync(to, device, src.dsend, src.device, bytes, st));
+        }
+        HIP_OK(hipStreamSynchronize(st));
+        barrier();
+    }
+    std::vector<uint64_t> alltoall_u64(const std::vector<uint64_t>& in, int k, hipStream_t) override {
+        put(nullptr, std::vector<uint64_t>(n, 0), in);
+        barrier();
+        std::vector<uint64_t> out((uint64_t)n * k);
+        for (int p = 0; p < n; ++p) {
+            const std::vector<uint64_t>& h = hub->post[p].host;
+            if (h.size() != (uint64_t)n * k) fail("all-to-all of words with different sizes");
+            std::copy(h.begin() + (uint64_t)rank * k, h.begin() + (uint64_t)(rank + 1) * k, out.begin() + (uint64_t)p * k);
+        }
+        barrier();
+        return out;
+    }
+    std::vector<uint64_t> allgather_u64(const std::vector<uint64_t>& in, hipStream_t) override {
+        put(nullptr, std::vector<uint64_t>(n, 0), in);
+        barrier();
+        std::vector<uint64_t> out;
+        out.reserve(in.size() * n);
+        for (int p = 0; p < n; ++p) {
+            const std::vector<uint64_t>& h = hub->post[p].host;
+            if (h.size() != in.size()) fail("all-gather of words with different sizes");
+            out.insert(out.end(), h.begin(), h.end());
+        }
+        barrier();
+        return out;
+    }
+};
+
 }  // namespace
 
 struct keto_comm {
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<Transport> t;
     int rank = 0, n = 1, device = 0;
     hipStream_t stream = nullptr;
     // device buffers, kept across calls: a requests, b their order, c routing workspace / output,
-    // d routed requests out, e / f small collectives, g routed requests in, h their decisions,
-    // i decisions back, k / l the migrating rounds' records and offsets
-    DBuf a, b, c, d, e, f, g, h, i, k, l;
+    // d routed requests out, g routed requests in, h their decisions, i decisions back, k / l the
+    // migrating rounds' records and offsets
+    DBuf a, b, c, d, g, h, i, k, l;
     // owner part per row id (int16, -1 = every part) of the last routed snapshot
     const Snapshot* owner_of = nullptr;
     uint64_t owner_version = ~0ull;
     DBuf owner;
     ~keto_comm() {
         (void)hipSetDevice(device);
-        if (comm) (void)ncclCommDestroy(comm);
+        t.reset();
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -88,45 +313,55 @@ namespace {
 
 void sync(keto_comm& c) { HIP_OK(hipStreamSynchronize(c.stream)); }
 
-// variable all-to-all of bytes: send[sdisp[p], +scount[p]) to rank p, receive recv[rdisp[p], +rcount[p])
-void alltoallv(keto_comm& c, const void* send, const std::vector<uint64_t>& scount, void* recv,
-               const std::vector<uint64_t>& rcount) {
-    uint64_t so = 0, ro = 0;
-    NCCL_OK(ncclGroupStart());
-    for (int p = 0; p < c.n; ++p) {
-        if (scount[p]) NCCL_OK(ncclSend(static_cast<const uint8_t*>(send) + so, scount[p], ncclUint8, p, c.comm, c.stream));
-        if (rcount[p]) NCCL_OK(ncclRecv(static_cast<uint8_t*>(recv) + ro, rcount[p], ncclUint8, p, c.comm, c.stream));
-        so += scount[p];
-        ro += rcount[p];
+// A rank's status before an exchange: the first error of its local work.
+struct Local {
+    int code = KETO_OK;
+    std::string msg;
+    template <class F>
+    void run(F&& f) {
+        if (code != KETO_OK) return;
+        try {
+            f();
+        } catch (const Error& e) {
+            code = e.code;
+            msg = e.msg;
+        } catch (const std::bad_alloc&) {
+            code = KETO_E_NOMEM;
+            msg = "out of host memory";
+        } catch (const std::exception& e) {
+            code = KETO_E_INVALID;
+            msg = e.what();
+        }
     }
-    NCCL_OK(ncclGroupEnd());
+};
+
+// KETO_COMM_INJECT="<rank>:<point>" fails that rank's local work at that point (tests of the
+// agreement): resolve, check, mig_begin, mig_round, filters
+void injected(const keto_comm& c, const char* point) {
+    const char* e = getenv("KETO_COMM_INJECT");
+    if (!e) return;
+    const char* colon = strchr(e, ':');
+    if (!colon || atoi(e) != c.rank || strcmp(colon + 1, point) != 0) return;
+    throw Error{KETO_E_INVALID, std::string("injected failure at ") + point};
 }
 
-// every rank's `k` 64-bit words to every rank: out[p * k + j] = rank p's in[j]... per destination:
-// in[p * k + j] goes to rank p, arriving as out[src * k + j]
-std::vector<uint64_t> alltoall_u64(keto_comm& c, const std::vector<uint64_t>& in, int k) {
-    uint64_t* d_in = c.e.get<uint64_t>((uint64_t)c.n * k * 2);
-    uint64_t* d_out = d_in + (uint64_t)c.n * k;
-    HIP_OK(hipMemcpyAsync(d_in, in.data(), in.size() * 8, hipMemcpyHostToDevice, c.stream));
-    NCCL_OK(ncclGroupStart());
+// the agreed outcome of every rank's codes (rank order): the lowest failing rank's code on every
+// rank; this rank's own message when it failed, else the failing peer's rank
+void settle(const keto_comm& c, const Local& mine, const std::vector<int64_t>& codes) {
     for (int p = 0; p < c.n; ++p) {
-        NCCL_OK(ncclSend(d_in + (uint64_t)p * k, k, ncclUint64, p, c.comm, c.stream));
-        NCCL_OK(ncclRecv(d_out + (uint64_t)p * k, k, ncclUint64, p, c.comm, c.stream));
+        if (codes[p] == KETO_OK) continue;
+        if (p == c.rank) throw Error{mine.code, mine.msg};
+        std::string msg = "rank " + std::to_string(p) + " failed with code " + std::to_string(codes[p]) +
+                          "; every rank of the collective call returns it";
+        if (mine.code != KETO_OK) msg += " (this rank failed too: " + mine.msg + ")";
+        throw Error{(int)codes[p], msg};
     }
-    NCCL_OK(ncclGroupEnd());
-    std::vector<uint64_t> out((uint64_t)c.n * k);
-    HIP_OK(hipMemcpyAsync(out.data(), d_out, out.size() * 8, hipMemcpyDeviceToHost, c.stream));
-    sync(c);
-    return out;
 }
 
-uint64_t allreduce_sum(keto_comm& c, uint64_t v) {
-    uint64_t* d = c.f.get<uint64_t>(1);
-    HIP_OK(hipMemcpyAsync(d, &v, 8, hipMemcpyHostToDevice, c.stream));
-    NCCL_OK(ncclAllReduce(d, d, 1, ncclUint64, ncclSum, c.comm, c.stream));
-    HIP_OK(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, c.stream));
-    sync(c);
-    return v;
+void agree(keto_comm& c, const Local& mine) {
+    const std::vector<uint64_t> all = c.t->allgather_u64({(uint64_t)(int64_t)mine.code}, c.stream);
+    std::vector<int64_t> codes(all.begin(), all.end());
+    settle(c, mine, codes);
 }
 
 void shard(uint32_t n, int rank, int world, uint32_t& lo, uint32_t& hi) {
@@ -149,22 +384,36 @@ const int16_t* owner_table(keto_comm& c, const Snapshot& S) {
 }
 
 // the migrating partition's record rounds for the requests routed to this part (decisions into
-// d_dec, in routed order); every rank calls it collectively
-void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_dec) {
+// d_dec, in routed order); every rank calls it collectively, `mine` carrying its status so far
+void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_dec,
+                Local& mine) {
     MigOut out{};
-    mig_begin(S, d_reqs, n, gmd, d_dec, c.stream, out);
     const int P = c.n;
+    mine.run([&] {
+        injected(c, "mig_begin");
+        mig_begin(S, d_reqs, n, gmd, d_dec, c.stream, out);
+    });
     for (uint32_t rounds = 0;; ++rounds) {
-        uint64_t mine = 0;
-        for (int q = 0; q < P; ++q) mine += out.records[q];
-        if (allreduce_sum(c, mine) == 0) return;
+        // one all-gather per round: every rank's status and the records it emitted
+        uint64_t emitted = 0;
+        if (mine.code == KETO_OK)
+            for (int q = 0; q < P; ++q) emitted += out.records[q];
+        const std::vector<uint64_t> all = c.t->allgather_u64({(uint64_t)(int64_t)mine.code, emitted}, c.stream);
+        std::vector<int64_t> codes(P);
+        uint64_t total = 0;
+        for (int p = 0; p < P; ++p) {
+            codes[p] = (int64_t)all[2 * p];
+            total += all[2 * p + 1];
+        }
+        settle(c, mine, codes);
+        if (total == 0) return;
         if (rounds >= (1u << 20)) throw Error{KETO_E_RANGE, "migrating check did not finish in 2^20 rounds"};
         std::vector<uint64_t> cnt((uint64_t)P * 2);
         for (int q = 0; q < P; ++q) {
             cnt[2 * q] = out.units[q];
             cnt[2 * q + 1] = out.records[q];
         }
-        const std::vector<uint64_t> in = alltoall_u64(c, cnt, 2);
+        const std::vector<uint64_t> in = c.t->alltoall_u64(cnt, 2, c.stream);
         std::vector<uint64_t> su(P), sr(P), ru(P), rr(P);
         std::vector<uint32_t> in_recs(MIG_MAX_PARTS, 0);
         std::vector<uint64_t> in_units(MIG_MAX_PARTS, 0);
@@ -179,14 +428,33 @@ void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_
             tu += in[2 * q];
             tr += in[2 * q + 1];
         }
-        uint8_t* rbuf = c.k.get<uint8_t>(tu * 16);
-        uint32_t* roff = c.l.get<uint32_t>(tr);
-        alltoallv(c, out.d_buf, su, rbuf, ru);
-        alltoallv(c, out.d_off, sr, roff, rr);
-        sync(c);
+        uint8_t* rbuf = nullptr;
+        uint32_t* roff = nullptr;
+        mine.run([&] {
+            rbuf = c.k.get<uint8_t>(tu * 16);
+            roff = c.l.get<uint32_t>(tr);
+        });
+        agree(c, mine);
+        c.t->alltoallv(out.d_buf, su, rbuf, ru, c.stream);
+        c.t->alltoallv(out.d_off, sr, roff, rr, c.stream);
         out = MigOut{};
-        mig_round(S, rbuf, roff, in_recs.data(), in_units.data(), c.stream, out);
+        mine.run([&] {
+            injected(c, "mig_round");
+            mig_round(S, rbuf, roff, in_recs.data(), in_units.data(), c.stream, out);
+        });
     }
+}
+
+std::unique_ptr<keto_comm> new_comm(int32_t n_ranks, int32_t rank, int32_t device) {
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks || n_ranks > (int32_t)MIG_MAX_PARTS)
+        throw Error{KETO_E_INVALID, "bad rank / rank count"};
+    HIP_OK(hipSetDevice(device));
+    auto c = std::make_unique<keto_comm>();
+    c->rank = rank;
+    c->n = n_ranks;
+    c->device = device;
+    HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return c;
 }
 
 }  // namespace
@@ -206,17 +474,49 @@ int keto_comm_id(uint8_t* id_out) {
 int keto_comm_init(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, keto_comm** out) {
     return guarded([&] {
         if (!id || !out) throw Error{KETO_E_INVALID, "NULL argument"};
-        if (n_ranks < 1 || rank < 0 || rank >= n_ranks || n_ranks > (int32_t)MIG_MAX_PARTS)
-            throw Error{KETO_E_INVALID, "bad rank / rank count"};
-        HIP_OK(hipSetDevice(device));
-        auto c = std::make_unique<keto_comm>();
-        c->rank = rank;
-        c->n = n_ranks;
-        c->device = device;
-        HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        auto c = new_comm(n_ranks, rank, device);
+        auto t = std::make_unique<RcclTransport>();
+        t->n = n_ranks;
         ncclUniqueId uid;
         std::memcpy(uid.internal, id, KETO_COMM_ID_BYTES);
-        NCCL_OK(ncclCommInitRank(&c->comm, n_ranks, uid, rank));
+        NCCL_OK(ncclCommInitRank(&t->comm, n_ranks, uid, rank));
+        c->t = std::move(t);
+        *out = c.release();
+        return KETO_OK;
+    });
+}
+
+int keto_comm_init_local(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, keto_comm** out) {
+    return guarded([&] {
+        if (!id || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        auto c = new_comm(n_ranks, rank, device);
+        auto t = std::make_unique<LocalTransport>();
+        t->key.assign(reinterpret_cast<const char*>(id), KETO_COMM_ID_BYTES);
+        t->rank = rank;
+        t->n = n_ranks;
+        t->device = device;
+        {
+            std::lock_guard<std::mutex> g(g_hubs_mu);
+            std::shared_ptr<LocalHub>& h = g_hubs[t->key];
+            if (!h) {
+                h = std::make_shared<LocalHub>();
+                h->n = n_ranks;
+                h->post.resize(n_ranks);
+            }
+            if (h->n != n_ranks) throw Error{KETO_E_INVALID, "local communicator id in use with another rank count"};
+            ++h->refs;
+            t->hub = h;
+        }
+        // peer copies between the ranks' GPUs over xGMI (already enabled, or one GPU: nothing to do)
+        int nd = 0;
+        if (hipGetDeviceCount(&nd) == hipSuccess)
+            for (int d = 0; d < nd; ++d)
+                if (d != device) {
+                    int ok = 0;
+                    if (hipDeviceCanAccessPeer(&ok, device, d) == hipSuccess && ok) (void)hipDeviceEnablePeerAccess(d, 0);
+                }
+        (void)hipGetLastError();
+        c->t = std::move(t);
         *out = c.release();
         return KETO_OK;
     });
@@ -227,23 +527,30 @@ void keto_comm_free(keto_comm* c) { delete c; }
 int keto_check_batch_sharded(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, uint32_t n,
                              int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
-        if (!c || !h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        if (h->s->n_parts > 1) throw Error{KETO_E_INVALID, "a partitioned snapshot: keto_check_batch_routed"};
+        if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
         HIP_OK(hipSetDevice(c->device));
-        uint32_t lo, hi, w0, w1;
+        Local mine;
+        uint32_t lo = 0, hi = 0, w0 = 0, w1 = 0;
         shard(n, c->rank, c->n, lo, hi);
         shard(n, 0, c->n, w0, w1);
         const uint32_t width = w1 - w0;          // the largest shard; every shard is padded to it
-        std::vector<uint8_t> mine(2ull * std::max<uint32_t>(width, 1), 0);
-        if (hi > lo) {
-            const int rc = keto_check_batch(h, reqs + lo, hi - lo, global_max_depth, mine.data(), mine.data() + width);
-            if (rc != KETO_OK) return rc;
-        }
+        std::vector<uint8_t> part(2ull * std::max<uint32_t>(width, 1), 0);
+        uint8_t *d_send = nullptr, *d_recv = nullptr;
+        mine.run([&] {
+            if (!h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+            if (h->s->n_parts > 1) throw Error{KETO_E_INVALID, "a partitioned snapshot: keto_check_batch_routed"};
+            injected(*c, "check");
+            if (hi > lo) {
+                const int rc = keto_check_batch(h, reqs + lo, hi - lo, global_max_depth, part.data(), part.data() + width);
+                if (rc != KETO_OK) throw Error{rc, g_err};
+            }
+            d_send = c->a.get<uint8_t>(2ull * std::max<uint32_t>(width, 1));
+            d_recv = c->b.get<uint8_t>(2ull * std::max<uint32_t>(width, 1) * c->n);
+            HIP_OK(hipMemcpyAsync(d_send, part.data(), 2ull * width, hipMemcpyHostToDevice, c->stream));
+        });
+        agree(*c, mine);
         // decisions and statuses of every shard, all-gathered as [allowed (width) | status (width)]
-        uint8_t* d_send = c->a.get<uint8_t>(2ull * std::max<uint32_t>(width, 1));
-        uint8_t* d_recv = c->b.get<uint8_t>(2ull * std::max<uint32_t>(width, 1) * c->n);
-        HIP_OK(hipMemcpyAsync(d_send, mine.data(), 2ull * width, hipMemcpyHostToDevice, c->stream));
-        if (width) NCCL_OK(ncclAllGather(d_send, d_recv, 2ull * width, ncclUint8, c->comm, c->stream));
+        c->t->allgather(d_send, d_recv, 2ull * width, c->stream);
         std::vector<uint8_t> all(2ull * width * c->n);
         HIP_OK(hipMemcpyAsync(all.data(), d_recv, all.size(), hipMemcpyDeviceToHost, c->stream));
         sync(*c);
@@ -261,49 +568,84 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* h, const keto_check_re
 int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, uint32_t n,
                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
-        if (!c || !h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        Snapshot& S = *h->s;
-        std::shared_lock<std::shared_mutex> lk(S.rw);
-        if ((int)S.n_parts != c->n || (int)S.part != c->rank)
-            throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with part = "
-                                            "rank and n_parts = ranks)"};
+        if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
         HIP_OK(hipSetDevice(c->device));
-        // names -> row ids (routing needs rows, not this part's handles)
-        std::vector<keto_check_ids> ids(std::max<uint32_t>(n, 1));
-        const auto wild = resolve_all(S, reqs, n, ids.data(), status_out, true);
-        if (!wild.empty())
-            throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
-                                            " is a wildcard query that no stored subject set uses: not routable on a "
-                                            "partitioned snapshot"};
-        keto_check_ids* d_reqs = c->a.get<keto_check_ids>(n);
-        HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice, c->stream));
-        const int16_t* d_owner = owner_table(*c, S);
-        const uint64_t wb = route_work_bytes(n, c->n);
-        uint8_t* work = c->c.get<uint8_t>(wb);
-        keto_check_ids* d_send = c->d.get<keto_check_ids>(n);
-        uint32_t* d_order = c->b.get<uint32_t>(n);
-        std::vector<uint32_t> cs(c->n);
-        route_rows(d_reqs, n, d_owner, S.n_rows(), c->rank, c->n, work, wb, d_send, d_order, cs.data(), c->stream);
-        // counts, then the requests, to their owners
-        std::vector<uint64_t> cnt(cs.begin(), cs.end());
-        const std::vector<uint64_t> in = alltoall_u64(*c, cnt, 1);
+        Local mine;
+        Snapshot* Sp = nullptr;
+        std::shared_lock<std::shared_mutex> lk;
+        std::vector<uint64_t> cnt(c->n, 0);
+        keto_check_ids* d_send = nullptr;
+        uint32_t* d_order = nullptr;
+        uint64_t wb = 0;
+        mine.run([&] {
+            if (!h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+            Sp = h->s.get();
+            lk = std::shared_lock<std::shared_mutex>(Sp->rw);
+            if ((int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
+                throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
+                                            "part = rank and n_parts = ranks)"};
+            injected(*c, "resolve");
+            // names -> row ids (routing needs rows, not this part's handles)
+            std::vector<keto_check_ids> ids(std::max<uint32_t>(n, 1));
+            const auto wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
+            if (!wild.empty())
+                throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
+                                                " is a wildcard query that no stored subject set uses: not routable "
+                                                "on a partitioned snapshot"};
+            keto_check_ids* d_reqs = c->a.get<keto_check_ids>(n);
+            HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice,
+                                  c->stream));
+            const int16_t* d_owner = owner_table(*c, *Sp);
+            wb = route_work_bytes(n, c->n);
+            uint8_t* work = c->c.get<uint8_t>(std::max<uint64_t>(wb, n));
+            d_send = c->d.get<keto_check_ids>(n);
+            d_order = c->b.get<uint32_t>(n);
+            std::vector<uint32_t> cs(c->n);
+            route_rows(d_reqs, n, d_owner, Sp->n_rows(), c->rank, c->n, work, wb, d_send, d_order, cs.data(), c->stream);
+            cnt.assign(cs.begin(), cs.end());
+        });
+        // the counts to their owners, each with this rank's status: the exchange is the agreement
+        std::vector<uint64_t> cw(2ull * c->n);
+        for (int p = 0; p < c->n; ++p) {
+            cw[2 * p] = mine.code == KETO_OK ? cnt[p] : 0;
+            cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
+        }
+        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
+        std::vector<int64_t> codes(c->n);
+        std::vector<uint64_t> in(c->n);
+        for (int p = 0; p < c->n; ++p) {
+            in[p] = inw[2 * p];
+            codes[p] = (int64_t)inw[2 * p + 1];
+        }
+        settle(*c, mine, codes);
+        Snapshot& S = *Sp;
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
-        if (m >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "more than 2^32 - 1 requests routed to one part"};
-        keto_check_ids* d_recv = c->g.get<keto_check_ids>(std::max<uint64_t>(m, 1));
+        keto_check_ids* d_recv = nullptr;
+        uint8_t *d_dec = nullptr, *d_back = nullptr;
+        mine.run([&] {
+            if (m >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "more than 2^32 - 1 requests routed to one part"};
+            d_recv = c->g.get<keto_check_ids>(std::max<uint64_t>(m, 1));
+            d_dec = c->h.get<uint8_t>(std::max<uint64_t>(m, 1));
+            d_back = c->i.get<uint8_t>(std::max<uint32_t>(n, 1));
+        });
+        agree(*c, mine);
         std::vector<uint64_t> sb(c->n), rb(c->n);
         for (int p = 0; p < c->n; ++p) {
             sb[p] = cnt[p] * sizeof(keto_check_ids);
             rb[p] = in[p] * sizeof(keto_check_ids);
         }
-        alltoallv(*c, d_send, sb, d_recv, rb);
-        sync(*c);
-        uint8_t* d_dec = c->h.get<uint8_t>(std::max<uint64_t>(m, 1));
-        if (S.part_mode == PART_MIGRATE) mig_rounds(*c, S, d_recv, (uint32_t)m, global_max_depth, d_dec);
-        else device_check_rows(S, d_recv, (uint32_t)m, global_max_depth, d_dec, c->stream);
+        c->t->alltoallv(d_send, sb, d_recv, rb, c->stream);
+        if (S.part_mode == PART_MIGRATE) {
+            mig_rounds(*c, S, d_recv, (uint32_t)m, global_max_depth, d_dec, mine);   // agreed inside
+        } else {
+            mine.run([&] {
+                injected(*c, "check");
+                device_check_rows(S, d_recv, (uint32_t)m, global_max_depth, d_dec, c->stream);
+            });
+            agree(*c, mine);
+        }
         // decisions back to their origins, in the origin's order
-        uint8_t* d_back = c->i.get<uint8_t>(std::max<uint32_t>(n, 1));
-        std::vector<uint64_t> sb2(in.begin(), in.end()), rb2(cnt.begin(), cnt.end());
-        alltoallv(*c, d_dec, sb2, d_back, rb2);
+        c->t->alltoallv(d_dec, in, d_back, cnt, c->stream);
         uint8_t* d_out = c->c.get<uint8_t>(std::max<uint64_t>(wb, n));
         unroute_rows(d_back, d_order, n, d_out, c->stream);
         if (n) HIP_OK(hipMemcpyAsync(allowed_out, d_out, n, hipMemcpyDeviceToHost, c->stream));
@@ -319,41 +661,62 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
 
 int keto_comm_close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out) {
     return guarded([&] {
-        if (!c || !h) throw Error{KETO_E_INVALID, "NULL argument"};
-        Snapshot& S = *h->s;
-        if (S.part_mode != PART_MIGRATE || (int)S.n_parts != c->n || (int)S.part != c->rank)
-            throw Error{KETO_E_INVALID, "not this rank's migrating part"};
+        if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
         HIP_OK(hipSetDevice(c->device));
-        // this part's stubs, grouped by owner; the owners learn once which of their rows to answer for
-        std::vector<uint32_t> stubs;
-        for (uint32_t r = 0; r < S.n_rows(); ++r)
-            if (!S.stub.empty() && S.stub[r]) stubs.push_back(r);
         const int P = c->n;
+        Local mine;
+        Snapshot* Sp = nullptr;
+        std::vector<uint32_t> stubs;
         std::vector<uint64_t> cnt(P, 0);
-        std::vector<std::vector<uint32_t>> by(P);
-        for (uint32_t r : stubs) by[S.root_owner(r, P)].push_back(r);
-        stubs.clear();
+        mine.run([&] {
+            if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+            Sp = h->s.get();
+            if (Sp->part_mode != PART_MIGRATE || (int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
+                throw Error{KETO_E_INVALID, "not this rank's migrating part"};
+            // this part's stubs, grouped by owner; the owners learn once which of their rows to answer for
+            for (uint32_t r = 0; r < Sp->n_rows(); ++r)
+                if (!Sp->stub.empty() && Sp->stub[r]) stubs.push_back(r);
+            std::vector<std::vector<uint32_t>> by(P);
+            for (uint32_t r : stubs) by[Sp->root_owner(r, P)].push_back(r);
+            stubs.clear();
+            for (int p = 0; p < P; ++p) {
+                cnt[p] = by[p].size();
+                stubs.insert(stubs.end(), by[p].begin(), by[p].end());
+            }
+        });
+        std::vector<uint64_t> cw(2ull * P);
         for (int p = 0; p < P; ++p) {
-            cnt[p] = by[p].size();
-            stubs.insert(stubs.end(), by[p].begin(), by[p].end());
+            cw[2 * p] = mine.code == KETO_OK ? cnt[p] : 0;
+            cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
         }
-        const std::vector<uint64_t> in = alltoall_u64(*c, cnt, 1);
+        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
+        std::vector<int64_t> codes(P);
+        std::vector<uint64_t> in(P);
+        for (int p = 0; p < P; ++p) {
+            in[p] = inw[2 * p];
+            codes[p] = (int64_t)inw[2 * p + 1];
+        }
+        settle(*c, mine, codes);
+        Snapshot& S = *Sp;
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
-        uint32_t* d_stubs = c->a.get<uint32_t>(std::max<uint64_t>(stubs.size(), 1));
-        uint32_t* d_asked = c->b.get<uint32_t>(std::max<uint64_t>(m, 1));
-        HIP_OK(hipMemcpyAsync(d_stubs, stubs.data(), stubs.size() * 4, hipMemcpyHostToDevice, c->stream));
+        uint32_t *d_stubs = nullptr, *d_asked = nullptr, *d_ans = nullptr, *d_got = nullptr;
+        std::vector<uint32_t> asked(m), ans(m * CF_WORDS), got(stubs.size() * CF_WORDS);
+        mine.run([&] {
+            d_stubs = c->a.get<uint32_t>(std::max<uint64_t>(stubs.size(), 1));
+            d_asked = c->b.get<uint32_t>(std::max<uint64_t>(m, 1));
+            d_ans = c->c.get<uint32_t>(std::max<uint64_t>(ans.size(), 1));
+            d_got = c->d.get<uint32_t>(std::max<uint64_t>(got.size(), 1));
+            HIP_OK(hipMemcpyAsync(d_stubs, stubs.data(), stubs.size() * 4, hipMemcpyHostToDevice, c->stream));
+        });
+        agree(*c, mine);
         std::vector<uint64_t> sb(P), rb(P);
         for (int p = 0; p < P; ++p) {
             sb[p] = cnt[p] * 4;
             rb[p] = in[p] * 4;
         }
-        alltoallv(*c, d_stubs, sb, d_asked, rb);
-        std::vector<uint32_t> asked(m);
+        c->t->alltoallv(d_stubs, sb, d_asked, rb, c->stream);
         HIP_OK(hipMemcpyAsync(asked.data(), d_asked, m * 4, hipMemcpyDeviceToHost, c->stream));
         sync(*c);
-        std::vector<uint32_t> ans(m * CF_WORDS), got(stubs.size() * CF_WORDS);
-        uint32_t* d_ans = c->c.get<uint32_t>(std::max<uint64_t>(ans.size(), 1));
-        uint32_t* d_got = c->d.get<uint32_t>(std::max<uint64_t>(got.size(), 1));
         for (int p = 0; p < P; ++p) {
             sb[p] = in[p] * 4 * CF_WORDS;        // answers go back to the askers
             rb[p] = cnt[p] * 4 * CF_WORDS;
@@ -361,12 +724,26 @@ int keto_comm_close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out
         uint64_t changed = 1;
         uint32_t rounds = 0;
         while (changed && rounds < 256) {
-            part_filters(S, asked.data(), m, ans.data());
-            HIP_OK(hipMemcpyAsync(d_ans, ans.data(), ans.size() * 4, hipMemcpyHostToDevice, c->stream));
-            alltoallv(*c, d_ans, sb, d_got, rb);
-            HIP_OK(hipMemcpyAsync(got.data(), d_got, got.size() * 4, hipMemcpyDeviceToHost, c->stream));
-            sync(*c);
-            changed = allreduce_sum(*c, part_close(S, stubs.data(), stubs.size(), got.data()));
+            mine.run([&] {
+                injected(*c, "filters");
+                part_filters(S, asked.data(), m, ans.data());
+                HIP_OK(hipMemcpyAsync(d_ans, ans.data(), ans.size() * 4, hipMemcpyHostToDevice, c->stream));
+            });
+            agree(*c, mine);
+            c->t->alltoallv(d_ans, sb, d_got, rb, c->stream);
+            uint64_t mine_changed = 0;
+            mine.run([&] {
+                HIP_OK(hipMemcpyAsync(got.data(), d_got, got.size() * 4, hipMemcpyDeviceToHost, c->stream));
+                sync(*c);
+                mine_changed = part_close(S, stubs.data(), stubs.size(), got.data());
+            });
+            const std::vector<uint64_t> all = c->t->allgather_u64({(uint64_t)(int64_t)mine.code, mine_changed}, c->stream);
+            changed = 0;
+            for (int p = 0; p < P; ++p) {
+                codes[p] = (int64_t)all[2 * p];
+                changed += all[2 * p + 1];
+            }
+            settle(*c, mine, codes);
             ++rounds;
         }
         part_closure_done(S, changed == 0);

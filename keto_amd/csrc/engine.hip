@@ -1791,9 +1791,20 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
                             o.runs[nr++] = CopyRun{a + cur.pos, out + cnt, cur.left};   // (o.runs: this lane's)
                             queued = true;
                         } else if (cur.left > BIG_RUN) {
+                            // reserve the pieces only if all of them fit: a slot below the count
+                            // is always written, so copy_big_runs never reads a stale entry
                             const uint32_t pieces = (cur.left + BIG_RUN - 1) / BIG_RUN;
-                            const uint32_t at = atomicAdd(o.n_big, pieces);
-                            if ((uint64_t)at + pieces <= o.big_cap) {
+                            uint32_t at = __hip_atomic_load(o.n_big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            bool got = false;
+                            while ((uint64_t)at + pieces <= o.big_cap) {
+                                const uint32_t prev = atomicCAS(o.n_big, at, at + pieces);
+                                if (prev == at) {
+                                    got = true;
+                                    break;
+                                }
+                                at = prev;
+                            }
+                            if (got) {
                                 for (uint32_t k = 0; k < pieces; ++k)
                                     o.big[at + k] = CopyRun{a + cur.pos + (uint64_t)k * BIG_RUN, out + cnt + (uint64_t)k * BIG_RUN,
                                                             min(BIG_RUN, cur.left - k * BIG_RUN)};
@@ -3916,10 +3927,19 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         D.ex_runs_cap = p.slots[0];
     }
     uint32_t* d_lane_runs = reinterpret_cast<uint32_t*>(D.ex_runs + (uint64_t)D.ex_runs_cap * RUNS_PER_LANE);
-    // the big-run pieces: nodes / BIG_RUN bounds them, plus slack for roots filled again on a later
-    // tier (a full queue copies in place)
+    // the big-run pieces: a run of L > BIG_RUN ids takes ceil(L / BIG_RUN) < 2 L / BIG_RUN pieces, so
+    // 2 nodes / BIG_RUN bounds a pass, plus slack for roots that overflowed tier 0 part way (their
+    // pieces are queued again); a queue that is full anyway copies the run in place
     auto ensure_big = [&](uint64_t nodes) {
-        const uint32_t cap = (uint32_t)std::min<uint64_t>(nodes / BIG_RUN + 4096, 1u << 26);
+        uint32_t cap = (uint32_t)std::min<uint64_t>(2 * nodes / BIG_RUN + 4096, 1u << 26);
+        if (const char* bc = getenv("KETO_EXPAND_BIG_CAP")) {          // tests: a queue that fills
+            cap = std::max(1, atoi(bc));
+            if (D.ex_big_cap != cap && D.ex_big) {
+                (void)hipFree(D.ex_big);
+                D.ex_big = nullptr;
+                D.ex_big_cap = 0;
+            }
+        }
         if (D.ex_big_cap >= cap) return;
         if (D.ex_big) (void)hipFree(D.ex_big);
         D.ex_big = nullptr;

@@ -828,4 +828,43 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
     return Sp;
 }
 
+// A host copy of a snapshot for another device (keto_snapshot_clone): every host table the engine
+// reads, at the snapshot's current version, laid out afresh (as a host-only snapshot is after writes,
+// delta.cpp).  The resolution indexes are rebuilt on the copy's first lookup.
+std::unique_ptr<Snapshot> clone_host(const Snapshot& S) {
+    if (S.n_parts > 1) throw Error{KETO_E_INVALID, "a part of a partitioned snapshot cannot be cloned"};
+    auto Cp = std::make_unique<Snapshot>();
+    Snapshot& C = *Cp;
+    C.ns_ids = S.ns_ids;
+    C.ns_names = S.ns_names;
+    C.ns_by_name = S.ns_by_name;
+    C.ns_by_id = S.ns_by_id;
+    for (uint32_t i = 0; i < (uint32_t)C.ns_names.size(); ++i) C.ns_view.emplace(C.ns_names[i], (int)i);
+    C.page_size = S.page_size;
+    C.strs = S.strs;
+    C.empty_str = S.empty_str;
+    C.n_real_rows = S.n_real_rows;
+    C.n_wild_rows = S.n_wild_rows;
+    C.wild_rows = S.wild_rows;
+    C.row_key = S.row_key;
+    C.row_of = S.row_of;
+    C.rows = S.rows;
+    C.row_pp = S.row_pp;
+    C.edges = S.edges;
+    C.row_has_coll = S.row_has_coll;
+    C.coll = S.coll;
+    C.n_coll_keys = S.n_coll_keys;
+    C.coll_dirty = false;
+    C.n_tuples = S.n_tuples;
+    C.n_poisoned_rows = S.n_poisoned_rows;
+    C.n_seq_rows = S.n_seq_rows;
+    C.version = S.version;
+    C.n_sorted_strs = S.n_sorted_strs;
+    C.added_str = S.added_str;
+    C.n_base_rows = S.n_base_rows;
+    C.row_over = S.row_over;
+    compute_layout(C);
+    return Cp;
+}
+
 }  // namespace keto

@@ -363,6 +363,9 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
                                              const uint32_t* edges, const keto_str* strings, uint32_t n_strings,
                                              uint32_t page_size);
 
+// host copy of an unpartitioned snapshot at its current version, laid out afresh (snapshot.cpp)
+std::unique_ptr<Snapshot> clone_host(const Snapshot& s);
+
 // Batch-local rows for wildcard requests that no stored subject set materialized: they can only
 // be top-level (check) or root (expand) rows, never edge targets.  Row ids >= base.
 struct Overlay {

@@ -1,8 +1,20 @@
-"""The library's own RCCL layer (keto_amd/csrc/comm.cpp: keto_comm_*, keto_check_batch_sharded,
-keto_check_batch_routed, keto_comm_close_filters) on the box's one GPU, as a one-rank communicator:
-the collectives run through RCCL for real (all-gather, grouped send/recv all-to-alls, all-reduce),
-and every decision must equal the replicated snapshot's and the SQL oracle's.  Runs with more ranks
-are the driver's multi-GPU node; the same exchanges over gloo are tests/test_multi_cpu.py."""
+"""The library's own multi-GPU layer (keto_amd/csrc/comm.cpp: keto_comm_*, keto_check_batch_sharded,
+keto_check_batch_routed, keto_comm_close_filters) on the box's one GPU.
+
+* RCCL, as a one-rank communicator: the collectives run through RCCL for real.
+* The local transport (keto_comm_init_local) with P = 2 and 3 ranks, each a thread of this process
+  with its own stream and its own part on the one GPU: requests cross parts, migrating searches
+  travel as continuation records between parts, the filter exchange converges across parts.  Every
+  decision must equal the replicated snapshot's and the SQL oracle's
+  (internal/check/engine.go:36-123).
+* Error agreement: a failure on one rank (an injected one at every local phase, a NULL argument, a
+  request it cannot route) makes every rank return the same code instead of leaving its peers
+  waiting, and the communicator stays usable afterwards.
+The same exchanges over gloo (multi.py) are tests/test_multi_cpu.py."""
+import ctypes as C
+import os
+import threading
+
 import pytest
 
 from oracle.oracle_sql import CheckEngine
@@ -20,9 +32,55 @@ def comm():
     c.close()
 
 
+@pytest.fixture(autouse=True)
+def _short_timeout(monkeypatch):
+    # a rank that never arrives fails its peers' calls after 60 s instead of hanging the run
+    monkeypatch.setenv("KETO_COMM_TIMEOUT_MS", "60000")
+
+
 def _reqs(seed, alph):
     checks = random_checks(seed, alph, k=48)
     return [(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in checks], checks
+
+
+def _local_comms(P):
+    from keto_amd.capi import Comm
+    cid = os.urandom(32)
+    return [Comm(cid, P, r, 0, local=True) for r in range(P)]
+
+
+def _ranks(P, fn):
+    """fn(rank) on P threads at once (a collective call per rank); [(ok, result or exception)]."""
+    res = [None] * P
+
+    def run(r):
+        try:
+            res[r] = (True, fn(r))
+        except Exception as e:          # noqa: BLE001 -- reported per rank
+            res[r] = (False, e)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a rank is still waiting"
+    return res
+
+
+def _ok(res):
+    bad = [(r, v) for r, (ok, v) in enumerate(res) if not ok]
+    assert not bad, bad
+    return [v for _, v in res]
+
+
+def _parts(ns, rows, ps, P, mode):
+    import keto_amd
+    return [keto_amd.Snapshot.build(ns, rows, page_size=ps, device=-1).upload_part(r, P, 0, mode=mode) for r in range(P)]
+
+
+def _wild(req):
+    return req[0] == "" or req[1] == "" or req[2] == ""
 
 
 @pytest.mark.parametrize("seed", range(4000, 4030))
@@ -77,3 +135,190 @@ def test_routed_powerlaw_matches_replicated(comm):
         part.close()
     full.close()
     g.close()
+
+
+# ------------------------------------------------------------------ local transport, P > 1
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("seed", range(4100, 4120))
+def test_local_ranks_match_oracle(P, seed):
+    """P ranks on one GPU over the local transport: sharded on a shared replicated snapshot, routed on
+    a shared-rows and a migrating partition (each rank its own part and its own batch; the last
+    rank's batch is empty on odd seeds), every decision against the replicated snapshot and the SQL
+    oracle."""
+    import keto_amd
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED
+    store, ns, tuples, raw, ps, alph = random_store(seed)
+    rows = rows_from_tuples(ns, tuples, raw)
+    full = keto_amd.Snapshot.build(ns, rows, page_size=ps, device=0)
+    reqs, checks = _reqs(seed, alph)
+    g = 5
+    want, want_st = full.check_batch(reqs, g)
+    for (t, d, _), a in zip(checks, want):
+        assert bool(a) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, t, d)
+    comms = _local_comms(P)
+    for r, (got, st) in enumerate(_ok(_ranks(P, lambda r: comms[r].check_batch_sharded(full, reqs, g)))):
+        assert (got == want).all() and (st == want_st).all(), (seed, r)
+    routable = [i for i, q in enumerate(reqs) if not _wild(q)]
+    ranks = P - (seed % 2)                          # odd seeds: the last rank passes no request
+    mine = [routable[r::ranks] if r < ranks else [] for r in range(P)]
+    for mode in (PART_SHARED, PART_MIGRATE):
+        parts = _parts(ns, rows, ps, P, mode)
+        if mode == PART_MIGRATE:
+            _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+        res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], [reqs[i] for i in mine[r]], g)))
+        for r, (got, st) in enumerate(res):
+            for k, i in enumerate(mine[r]):
+                assert got[k] == want[i] and st[k] == want_st[i], (seed, mode, r, reqs[i])
+        for p in parts:
+            p.close()
+    for c in comms:
+        c.close()
+    full.close()
+
+
+@pytest.fixture(scope="module")
+def powerlaw_strings():
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 256), threads=16)
+    st = g.string_tuples(seed=5)
+    full, _ = g.snapshot_from_strings(st, device=0)
+    q = g.queries(240_000, seed=12, depth=5)
+    arr = g.string_requests(st, q)
+    want, want_st = full.check_batch_reqs(arr, len(q), 5)
+    yield g, st, full, arr, len(q), want, want_st
+    full.close()
+    g.close()
+
+
+def _slice(arr, lo, hi):
+    from keto_amd.capi import KCheckReq
+    return (KCheckReq * max(1, hi - lo)).from_address(C.addressof(arr) + lo * C.sizeof(KCheckReq))
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("mode", ["shared", "migrate"])
+def test_local_routed_powerlaw_matches_replicated(powerlaw_strings, P, mode):
+    """The power-law graph (1/256 scale, from string tuples) on P parts over the local transport: each
+    rank passes its own 240,000 / P named requests, most of which belong to other parts; on the
+    migrating partition searches cross parts as records (many rounds).  Decisions equal the
+    replicated snapshot's."""
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED
+    g, st, full, arr, n, want, want_st = powerlaw_strings
+    m = PART_MIGRATE if mode == "migrate" else PART_SHARED
+    parts = []
+    for r in range(P):
+        part, _ = g.snapshot_from_strings(st, device=-1)
+        parts.append(part.upload_part(r, P, 0, mode=m))
+    comms = _local_comms(P)
+    if m == PART_MIGRATE:
+        rounds = _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+        assert len(set(rounds)) == 1 and rounds[0] >= 1
+    bounds = [(r * n // P, (r + 1) * n // P) for r in range(P)]
+    res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], _slice(arr, *bounds[r]), 5,
+                                                              n=bounds[r][1] - bounds[r][0])))
+    for r, (got, gst) in enumerate(res):
+        lo, hi = bounds[r]
+        assert (got == want[lo:hi]).all(), (mode, P, r, int((got != want[lo:hi]).sum()))
+        assert (gst == want_st[lo:hi]).all()
+    # the sharded path on the replicated snapshot, every rank the whole batch
+    res = _ok(_ranks(P, lambda r: comms[r].check_batch_sharded(full, arr, 5, n=n)))
+    for got, gst in res:
+        assert (got == want).all() and (gst == want_st).all()
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+
+
+# ------------------------------------------------------------------ error agreement
+def _agreed_failure(res, bad_rank, needle):
+    codes = set()
+    for r, (ok, v) in enumerate(res):
+        assert not ok, f"rank {r} returned normally while rank {bad_rank} failed"
+        codes.add(v.code)
+        if r == bad_rank:
+            assert needle in str(v), (r, v)
+        else:
+            assert f"rank {bad_rank} failed" in str(v), (r, v)
+    assert len(codes) == 1, codes
+
+
+@pytest.mark.parametrize("point", ["resolve", "check", "mig_begin", "mig_round", "filters", "sharded"])
+def test_local_error_agreement(powerlaw_strings, monkeypatch, point):
+    """A failure injected on rank 1 of 3 (KETO_COMM_INJECT) at each local phase: every rank returns
+    the same code, rank 1 its own message, the others name rank 1; no rank waits.  The communicator
+    and the parts then answer the next call exactly."""
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED
+    g, st, full, arr, n, want, want_st = powerlaw_strings
+    P = 3
+    m = PART_SHARED if point in ("check", "resolve", "sharded") else PART_MIGRATE
+    parts = []
+    for r in range(P):
+        part, _ = g.snapshot_from_strings(st, device=-1)
+        parts.append(part.upload_part(r, P, 0, mode=m))
+    comms = _local_comms(P)
+    k = 30_000
+    bounds = [(r * k, (r + 1) * k) for r in range(P)]
+
+    def routed(r):
+        return comms[r].check_batch_routed(parts[r], _slice(arr, *bounds[r]), 5, n=k)
+
+    if point == "filters":
+        monkeypatch.setenv("KETO_COMM_INJECT", "1:filters")
+        _agreed_failure(_ranks(P, lambda r: comms[r].close_filters(parts[r])), 1, "injected")
+        monkeypatch.delenv("KETO_COMM_INJECT")
+    if m == PART_MIGRATE:
+        _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+    monkeypatch.setenv("KETO_COMM_INJECT", f"1:{'check' if point == 'sharded' else point}")
+    if point == "sharded":
+        _agreed_failure(_ranks(P, lambda r: comms[r].check_batch_sharded(full, _slice(arr, 0, k), 5, n=k)), 1,
+                        "injected")
+    elif point != "filters":
+        _agreed_failure(_ranks(P, routed), 1, "injected")
+    monkeypatch.delenv("KETO_COMM_INJECT")
+    for r, (got, gst) in enumerate(_ok(_ranks(P, routed))):
+        lo, hi = bounds[r]
+        assert (got == want[lo:hi]).all() and (gst == want_st[lo:hi]).all(), (point, r)
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+
+
+def test_local_error_agreement_bad_arguments(powerlaw_strings):
+    """Real rank-local errors, no injection: rank 2 passes a NULL request array with n > 0; rank 0
+    passes a wildcard query (empty object) that no stored set uses.  Every rank returns the code."""
+    from keto_amd.capi import PART_SHARED, KCheckReq
+    g, st, full, arr, n, want, want_st = powerlaw_strings
+    P = 3
+    parts = []
+    for r in range(P):
+        part, _ = g.snapshot_from_strings(st, device=-1)
+        parts.append(part.upload_part(r, P, 0, mode=PART_SHARED))
+    comms = _local_comms(P)
+    k = 1000
+
+    def null_on_2(r):
+        c = comms[r]
+        if r == 2:
+            from keto_amd.capi import _check
+            import numpy as np
+            a = np.zeros(k, dtype=np.uint8)
+            _check(c.lib.keto_check_batch_routed(c.h, parts[r].h, None, C.c_uint32(k), C.c_int32(5),
+                                                 a.ctypes.data_as(C.c_void_p), a.ctypes.data_as(C.c_void_p)))
+        return c.check_batch_routed(parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)
+
+    _agreed_failure(_ranks(P, null_on_2), 2, "NULL")
+    wild = (KCheckReq * k)()
+    C.memmove(wild, _slice(arr, 0, k), C.sizeof(wild))
+    wild[7].object.n = 0                                  # docs:#view@u -- a wildcard query
+
+    def wild_on_0(r):
+        return comms[r].check_batch_routed(parts[r], wild if r == 0 else _slice(arr, r * k, (r + 1) * k), 5, n=k)
+
+    _agreed_failure(_ranks(P, wild_on_0), 0, "wildcard")
+    _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)))
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()

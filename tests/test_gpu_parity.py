@@ -218,3 +218,38 @@ def test_random_expand_via_fields_matches_json(seed):
         for st, js, tf in snap.expand_batch(grp, g, via_fields=True):
             assert (st == EXPAND_TREE) == (tf is not None)
             assert tf == js, (seed, g)
+
+
+@pytest.mark.parametrize("env", [{}, {"KETO_EXPAND_BIG_CAP": "7"}, {"KETO_EXPAND_BIG_CAP": "64"},
+                                 {"KETO_EXPAND_STAGE": "0"}, {"KETO_SLOTS": "256"}],
+                         ids=["default", "big_cap_7", "big_cap_64", "two_pass", "few_slots"])
+def test_expand_many_big_runs(monkeypatch, env):
+    """Trees too big for a staging region (20 subject sets of 1,025-1,044 ids each: every set's id
+    run is longer than BIG_RUN and takes 2 pieces) go through the second pass, whose shared queue of
+    big-run pieces fills up when it is small: a run whose pieces do not all fit is copied in place
+    and no queue slot is left unwritten.  The trees are written out here and compared whole
+    (internal/expand/engine.go:33-102: sets before ids, both in ORDER BY order)."""
+    from keto_amd.capi import EXPAND_TREE
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    roots, sets = 16, 20
+    ns = [(1, "n")]
+    rows, want = [], []
+    for i in range(roots):
+        kids = []
+        for j in range(sets):
+            c = f"c{i:02d}_{j:02d}"
+            rows.append((1, f"r{i:02d}", "m", None, 1, c, "m"))
+            ids = [f"u{(i * 7919 + j * 104729 + k) % 1000003:07d}" for k in range(1025 + j)]
+            ids = sorted(set(ids))
+            for u in ids:
+                rows.append((1, c, "m", u))
+            kids.append({"type": "union", "subject_set": {"namespace": "n", "object": c, "relation": "m"},
+                         "children": [{"type": "leaf", "subject_id": u} for u in ids]})
+        want.append({"type": "union", "subject_set": {"namespace": "n", "object": f"r{i:02d}", "relation": "m"},
+                     "children": kids})
+    snap = _snapshot(ns, rows, 100)
+    got = snap.expand_batch([(("set", "n", f"r{i:02d}", "m"), 0) for i in range(roots)] * 3, 5)
+    for k, (st, js) in enumerate(got):
+        assert st == EXPAND_TREE
+        assert js == want[k % roots], (env, k)
