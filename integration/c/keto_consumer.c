@@ -12,8 +12,14 @@
  * cases (tests/golden/reference_cases.json) and seeded write / check / expand sequences compared with
  * the SQL oracle.
  *
+ * Several GPUs in the one server process (registry_gpu.go EnableGPU over a device list): with an
+ * "R" line the consumer keeps one replica per listed device -- the first built from the table, the
+ * others made by keto_snapshot_clone -- deals its check and expand batches over them round-robin,
+ * applies every write transaction to each replica, and rebuilds them all when one answers
+ * KETO_E_REBUILD.
+ *
  * Input (tab-separated lines; empty fields allowed), executed in order:
- *   P <page_size>        V <device>
+ *   P <page_size>        V <device>        R <device> <device> ...   (replicas; default: V's device)
  *   N <ns id> <name>
  *   T <ns id> <object> <relation> I <subject id>                          (a row of the initial table)
  *   T <ns id> <object> <relation> S <set ns id> <set object> <set relation>
@@ -248,6 +254,18 @@ static keto_snapshot* build(const keto_namespace* ns, size_t n_ns, const table_t
     return snap;
 }
 
+#define MAX_REPLICAS 8
+
+/* one replica per device: the table sorted and uploaded once, cloned to the other devices */
+static void build_replicas(const keto_namespace* ns, size_t n_ns, const table_t* tb, uint32_t page_size,
+                           const int* devices, int n, keto_snapshot** reps) {
+    reps[0] = build(ns, n_ns, tb, page_size, devices[0]);
+    for (int k = 1; k < n; ++k) {
+        const int rc = keto_snapshot_clone(reps[0], devices[k], &reps[k]);
+        if (rc != KETO_OK) fail("keto_snapshot_clone", rc);
+    }
+}
+
 static void subject_of(line_t* l, int* k, keto_subject* s) {
     memset(s, 0, sizeof *s);
     if (!strcmp(l->f[(*k)++], "I")) {
@@ -277,11 +295,14 @@ int main(int argc, char** argv) {
     char buf[1 << 16];
     uint32_t page_size = 100;
     int device = -1;
+    int devices[MAX_REPLICAS], n_reps = 0;
     while (fgets(buf, sizeof buf, in)) {
         line_t* l = (line_t*)calloc(1, sizeof(line_t));
         if (!l || split(buf, l) < 1) return 1;
         if (!strcmp(l->f[0], "P")) page_size = (uint32_t)atoi(l->f[1]);
         else if (!strcmp(l->f[0], "V")) device = atoi(l->f[1]);
+        else if (!strcmp(l->f[0], "R"))
+            for (int k = 1; k < l->n && n_reps < MAX_REPLICAS; ++k) devices[n_reps++] = atoi(l->f[k]);
         lines = (line_t**)xrealloc(lines, (n_lines + 1) * sizeof(line_t*));
         lines[n_lines++] = l;
     }
@@ -301,7 +322,11 @@ int main(int argc, char** argv) {
             table_insert(&table, tuple_of(l, 1));
         }
     }
-    keto_snapshot* snap = build(ns, n_ns, &table, page_size, device);
+    if (n_reps == 0) devices[n_reps++] = device;
+    keto_snapshot* reps[MAX_REPLICAS];
+    build_replicas(ns, n_ns, &table, page_size, devices, n_reps, reps);
+    keto_snapshot* snap = reps[0];
+    int batches = 0;                          /* batches dealt round-robin over the replicas */
     keto_snapshot_stats st;
     int rc = keto_snapshot_get_stats(snap, &st);
     if (rc != KETO_OK) fail("keto_snapshot_get_stats", rc);
@@ -334,6 +359,7 @@ int main(int argc, char** argv) {
                 subject_of(c, &f, &q[k].subject);
                 q[k].max_depth = atoi(c->f[f]);
             }
+            snap = reps[batches++ % n_reps];
             rc = keto_check_batch(snap, q, (uint32_t)m, gmd, allowed, status);
             if (device < 0) {
                 printf("nodevice %d\n", rc);
@@ -361,6 +387,7 @@ int main(int argc, char** argv) {
                 r[k].max_depth = atoi(lines[i + k]->f[f]);
             }
             keto_tree_arena* ar = NULL;
+            snap = reps[batches++ % n_reps];
             rc = keto_expand_batch(snap, r, (uint32_t)m, gmd, &ar);
             if (rc != KETO_OK) fail("keto_expand_batch", rc);
             if (keto_tree_count(ar) != m) return 5;
@@ -419,29 +446,35 @@ int main(int argc, char** argv) {
             /* the transaction committed in SQL: the table changes, then the snapshot follows */
             for (size_t k = 0; k < n_ins; ++k) table_insert(&table, ins[k]);
             for (size_t k = 0; k < n_del; ++k) table_delete(&table, &del[k]);
-            uint64_t v0 = keto_snapshot_version(snap), v = 0;
-            rc = keto_snapshot_apply(snap, ins, n_ins, del, n_del, &v);
+            /* every replica follows the transaction; one refusal rebuilds them all */
+            uint64_t v0 = keto_snapshot_version(reps[0]), v = 0;
             int rebuilt = 0;
+            rc = KETO_OK;
+            for (int k = 0; k < n_reps && rc == KETO_OK; ++k) {
+                uint64_t vk = 0;
+                rc = keto_snapshot_apply(reps[k], ins, n_ins, del, n_del, &vk);
+                if (rc == KETO_OK && (vk != v0 + 1 || keto_snapshot_version(reps[k]) != vk)) return 12;
+                if (rc == KETO_E_REBUILD && keto_snapshot_version(reps[k]) != v0) return 11; /* left unchanged */
+                v = vk;
+            }
             if (rc == KETO_E_REBUILD) {
-                if (keto_snapshot_version(snap) != v0) return 11; /* a refused write leaves it unchanged */
-                keto_snapshot_release(snap);
-                snap = build(ns, n_ns, &table, page_size, device);
+                for (int k = 0; k < n_reps; ++k) keto_snapshot_release(reps[k]);
+                build_replicas(ns, n_ns, &table, page_size, devices, n_reps, reps);
                 rebuilt = 1;
-                v = keto_snapshot_version(snap);
+                v = keto_snapshot_version(reps[0]);
             } else if (rc != KETO_OK) {
                 fail("keto_snapshot_apply", rc);
-            } else if (v != v0 + 1 || keto_snapshot_version(snap) != v) {
-                return 12;
             }
+            snap = reps[0];
             printf("apply\t%d\t%llu\t%d\n", rc, (unsigned long long)v, rebuilt);
             n_ins = n_del = 0;
         }
         ++i;
     }
     /* an error path: a NULL argument must fail with a message, not crash */
-    rc = keto_check_batch(snap, NULL, 1, 5, NULL, NULL);
+    rc = keto_check_batch(reps[0], NULL, 1, 5, NULL, NULL);
     if (rc != KETO_E_INVALID || !keto_last_error()[0]) return 8;
-    keto_snapshot_release(snap);
+    for (int k = 0; k < n_reps; ++k) keto_snapshot_release(reps[k]);
     for (size_t i = 0; i < n_lines; ++i) {
         for (int k = 0; k < lines[i]->n; ++k) free(lines[i]->f[k]);
         free(lines[i]);

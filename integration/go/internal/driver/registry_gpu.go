@@ -8,6 +8,7 @@ import (
 	"errors"
 	"os"
 	"strconv"
+	"strings"
 	"sync"
 
 	"github.com/ory/keto/internal/gpu"
@@ -20,24 +21,35 @@ import (
 //
 //	reg, err := driver.NewDefaultRegistry(cmd.Context(), cmd.Flags(), false)
 //	...
-//	if err := driver.EnableGPU(cmd.Context(), reg, driver.GPUDeviceFromEnv()); err != nil {
+//	if err := driver.EnableGPU(cmd.Context(), reg, driver.GPUDevicesFromEnv()); err != nil {
 //		return err
 //	}
 //	return reg.ServeAllSQA(cmd)
 //
-// EnableGPU builds the snapshot from one full scan of the table, starts the check and expand
-// batchers over it, and wraps the persister so that every committed write transaction is applied to
-// the snapshot before the write returns.  The engines find the batchers through GPUCheckBatcher /
+// The server stays one process (internal/driver/daemon.go:62-69) and drives every GPU of the node
+// itself: EnableGPU builds one snapshot replica per device from one full scan of the table (sorted
+// and uploaded once, cloned to the other devices, gpu.BuildReplicas), starts the check and expand
+// batchers, which deal each batch to a GPU with no batch in flight, and wraps the persister so that
+// every committed write transaction is applied to every replica before the write returns.  The engines find the batchers through GPUCheckBatcher /
 // GPUExpandBatcher (internal/check/engine_gpu.go, internal/expand/engine_gpu.go) and answer on SQL
 // whenever those return nil: no GPU, or a snapshot that is behind the table while it is rebuilt.
 
-// GPUDeviceFromEnv is the HIP device of the GPU path: KETO_GPU_DEVICE (unset or negative: off).
-func GPUDeviceFromEnv() int {
-	v, err := strconv.Atoi(os.Getenv("KETO_GPU_DEVICE"))
-	if err != nil {
-		return -1
+// GPUDevicesFromEnv is the HIP devices of the GPU path: KETO_GPU_DEVICES, a comma-separated list
+// ("0,1,2,3,4,5,6,7"), or the single KETO_GPU_DEVICE; unset, empty or negative: off (nil).
+func GPUDevicesFromEnv() []int {
+	v := os.Getenv("KETO_GPU_DEVICES")
+	if v == "" {
+		v = os.Getenv("KETO_GPU_DEVICE")
 	}
-	return v
+	var out []int
+	for _, f := range strings.Split(v, ",") {
+		d, err := strconv.Atoi(strings.TrimSpace(f))
+		if err != nil || d < 0 {
+			continue
+		}
+		out = append(out, d)
+	}
+	return out
 }
 
 // gpuRowSource is the persister's full scan (internal/persistence/sql/snapshot_gpu.go).
@@ -46,14 +58,14 @@ type gpuRowSource interface {
 }
 
 type gpuState struct {
-	r      *RegistryDefault
-	device int
-	check  *gpu.Batcher
-	expand *gpu.ExpandBatcher
+	r       *RegistryDefault
+	devices []int
+	check   *gpu.Batcher
+	expand  *gpu.ExpandBatcher
 
 	mu    sync.RWMutex
-	snap  *gpu.Snapshot
-	stale bool // the snapshot is behind the table: the engines answer on SQL until the rebuild lands
+	snaps []*gpu.Snapshot // one replica per device, all at the same version
+	stale bool            // the replicas are behind the table: the engines answer on SQL until the rebuild lands
 
 	wmu        sync.Mutex // one write transaction (SQL commit + Apply) at a time; the rebuild's scan holds it too
 	rebuilding bool
@@ -71,24 +83,24 @@ func gpuOf(r *RegistryDefault) *gpuState {
 	return nil
 }
 
-// EnableGPU loads the GPU snapshot for HIP device `device` (< 0: leave the registry on SQL).
-func EnableGPU(ctx context.Context, reg Registry, device int) error {
+// EnableGPU loads one snapshot replica per HIP device of `devices` (none: leave the registry on SQL).
+func EnableGPU(ctx context.Context, reg Registry, devices []int) error {
 	r, ok := reg.(*RegistryDefault)
-	if !ok || device < 0 {
+	if !ok || len(devices) == 0 {
 		return nil
 	}
 	if err := r.Init(ctx); err != nil {
 		return err
 	}
-	st := &gpuState{r: r, device: device}
-	snap, err := st.build(ctx)
+	st := &gpuState{r: r, devices: append([]int(nil), devices...)}
+	snaps, err := st.build(ctx)
 	if err != nil {
 		return err
 	}
-	st.snap = snap
+	st.snaps = snaps
 	globalMax := func() int { return r.Config().ReadAPIMaxDepth() }
-	st.check = gpu.NewBatcher(snap, globalMax, r.PermissionEngine().Fallback())
-	st.expand = gpu.NewExpandBatcher(snap, globalMax)
+	st.check = gpu.NewBatcher(snaps, globalMax, r.PermissionEngine().Fallback())
+	st.expand = gpu.NewExpandBatcher(snaps, globalMax)
 	r.p = &gpuPersister{Persister: r.p, g: st}
 	gpuStates.Store(r, st)
 	return nil
@@ -123,7 +135,7 @@ func (r *RegistryDefault) GPUExpandBatcher() *gpu.ExpandBatcher {
 }
 
 // build scans the table (caller holds wmu when it must be consistent with writes) and uploads.
-func (g *gpuState) build(ctx context.Context) (*gpu.Snapshot, error) {
+func (g *gpuState) build(ctx context.Context) ([]*gpu.Snapshot, error) {
 	src, ok := g.r.p.(gpuRowSource) // EnableGPU builds before it wraps the persister
 	if !ok {
 		return nil, errors.New("gpu: the persister has no full-scan source")
@@ -135,7 +147,7 @@ func (g *gpuState) build(ctx context.Context) (*gpu.Snapshot, error) {
 	return g.buildFrom(ctx, rows)
 }
 
-func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) (*gpu.Snapshot, error) {
+func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) ([]*gpu.Snapshot, error) {
 	nm, err := g.r.Config().NamespaceManager()
 	if err != nil {
 		return nil, err
@@ -144,11 +156,11 @@ func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) (*gpu.Snapshot
 	if err != nil {
 		return nil, err
 	}
-	return gpu.Build(nss, rows, g.device)
+	return gpu.BuildReplicas(nss, rows, g.devices)
 }
 
-// applyLocked runs after a write committed, with wmu held: the snapshot follows the table one
-// transaction at a time, or goes stale and is rebuilt.
+// applyLocked runs after a write committed, with wmu held: every replica follows the table one
+// transaction at a time, or the set goes stale and is rebuilt.
 func (g *gpuState) applyLocked(ctx context.Context, ins, del []*relationtuple.InternalRelationTuple) {
 	nm, err := g.r.Config().NamespaceManager()
 	var iRows, dRows []gpu.Row
@@ -167,16 +179,16 @@ func (g *gpuState) applyLocked(ctx context.Context, ins, del []*relationtuple.In
 		return
 	}
 	g.mu.RLock()
-	snap, stale := g.snap, g.stale
+	snaps, stale := g.snaps, g.stale
 	g.mu.RUnlock()
-	if stale { // an earlier rebuild failed: the snapshot is behind, try again
+	if stale { // an earlier rebuild failed: the replicas are behind, try again
 		g.startRebuildLocked()
 		return
 	}
 	if err == nil {
-		err = snap.Apply(iRows, dRows)
+		err = gpu.ApplyAll(snaps, iRows, dRows)
 	}
-	if err != nil { // gpu.ErrRebuild (or a failed write to the device): serve SQL until rebuilt
+	if err != nil { // gpu.ErrRebuild (or a failed write to a device): serve SQL until rebuilt
 		g.startRebuildLocked()
 	}
 }
@@ -214,17 +226,15 @@ func (g *gpuState) rebuild() {
 			rows, err = src.SnapshotRows(ctx)
 		}
 		g.wmu.Unlock()
-		var snap *gpu.Snapshot
+		var snaps []*gpu.Snapshot
 		if err == nil {
-			snap, err = g.buildFrom(ctx, rows)
+			snaps, err = g.buildFrom(ctx, rows)
 		}
 		rows = nil
 		g.wmu.Lock()
 		if err != nil || g.rescan {
 			g.wmu.Unlock()
-			if snap != nil {
-				snap.Close()
-			}
+			gpu.CloseAll(snaps)
 			if err != nil { // stay stale (SQL answers); a later write retries the rebuild
 				g.wmu.Lock()
 				g.rebuilding = false
@@ -235,26 +245,26 @@ func (g *gpuState) rebuild() {
 		}
 		replayed := true
 		for _, w := range g.pending {
-			if snap.Apply(w[0], w[1]) != nil {
+			if gpu.ApplyAll(snaps, w[0], w[1]) != nil {
 				replayed = false
 				break
 			}
 		}
 		if !replayed { // a replayed write needs a rebuild itself: scan again
 			g.wmu.Unlock()
-			snap.Close()
+			gpu.CloseAll(snaps)
 			continue
 		}
-		old := g.check.Swap(snap) // waits for batches running on the old version
-		g.expand.Swap(snap)
+		old := g.check.Swap(snaps) // waits for batches running on the old versions
+		g.expand.Swap(snaps)
 		g.mu.Lock()
-		g.snap = snap
+		g.snaps = snaps
 		g.stale = false
 		g.mu.Unlock()
 		g.pending = nil
 		g.rebuilding = false
 		g.wmu.Unlock()
-		old.Close()
+		gpu.CloseAll(old)
 		return
 	}
 }

@@ -135,11 +135,51 @@ func (c *coalescer) loop() {
 // requests still queued when the batcher closes.
 type Fallback func(ctx context.Context, r *relationtuple.InternalRelationTuple, restDepth int) (bool, error)
 
+// replicas deals batches to the snapshots of a replica set, one per GPU (BuildReplicas): a batch goes
+// to a replica with no batch in flight, so the GPUs of a node work on consecutive batches at once and
+// the dealing follows their load; when every replica is busy the flush loop waits (back-pressure).
+type replicas struct {
+	mu    sync.RWMutex // held shared by a running batch, exclusively by Swap
+	snaps []*Snapshot
+	idle  chan int
+}
+
+func newReplicas(snaps []*Snapshot) *replicas {
+	r := &replicas{snaps: snaps, idle: make(chan int, len(snaps))}
+	for k := range snaps {
+		r.idle <- k
+	}
+	return r
+}
+
+// run takes an idle replica, then runs fn on it in its own goroutine.
+func (r *replicas) run(fn func(s *Snapshot)) {
+	k := <-r.idle
+	go func() {
+		defer func() { r.idle <- k }()
+		r.mu.RLock()
+		defer r.mu.RUnlock()
+		fn(r.snaps[k])
+	}()
+}
+
+// swap installs a new replica set of the same size (a rebuild); it returns the old one once no batch
+// uses it.
+func (r *replicas) swap(snaps []*Snapshot) []*Snapshot {
+	r.mu.Lock()
+	defer r.mu.Unlock()
+	if len(snaps) != len(r.snaps) {
+		panic("gpu: a replica set is swapped for one of another size")
+	}
+	old := r.snaps
+	r.snaps = snaps
+	return old
+}
+
 // Batcher coalesces concurrent SubjectIsAllowed calls into keto_check_batch calls (defaults: 65,536
-// requests or 200 µs per batch).
+// requests or 200 µs per batch), dealt over the replica set's GPUs.
 type Batcher struct {
-	mu        sync.RWMutex
-	snap      *Snapshot
+	rep       *replicas
 	GlobalMax func() int // config.ReadAPIMaxDepth (internal/driver/config/provider.go:143-145)
 	Fallback  Fallback
 	c         *coalescer
@@ -150,21 +190,15 @@ type checkReq struct {
 	depth int
 }
 
-// NewBatcher starts the flush loop.
-func NewBatcher(s *Snapshot, globalMax func() int, fb Fallback) *Batcher {
-	b := &Batcher{snap: s, GlobalMax: globalMax, Fallback: fb}
+// NewBatcher starts the flush loop over one snapshot per GPU.
+func NewBatcher(snaps []*Snapshot, globalMax func() int, fb Fallback) *Batcher {
+	b := &Batcher{rep: newReplicas(snaps), GlobalMax: globalMax, Fallback: fb}
 	b.c = newCoalescer(1<<16, 200*time.Microsecond, b.flush, b.fallbackAll)
 	return b
 }
 
-// Swap installs a new snapshot version (a rebuild); it returns once no batch uses the old one.
-func (b *Batcher) Swap(s *Snapshot) *Snapshot {
-	b.mu.Lock()
-	defer b.mu.Unlock()
-	old := b.snap
-	b.snap = s
-	return old
-}
+// Swap installs a new replica set (a rebuild); it returns the old one once no batch uses it.
+func (b *Batcher) Swap(snaps []*Snapshot) []*Snapshot { return b.rep.swap(snaps) }
 
 // Close stops the loop; queued requests are answered by the fallback, later ones too.
 func (b *Batcher) Close() { b.c.close() }
@@ -198,31 +232,32 @@ func (b *Batcher) flush(batch []*pending) {
 		q := p.req.(checkReq)
 		reqs[i], depths[i] = q.r, q.depth
 	}
-	b.mu.RLock()
-	allowed, status, err := b.snap.CheckBatch(reqs, depths, b.GlobalMax())
-	b.mu.RUnlock()
-	if err != nil {
-		b.fallbackAll(batch)
-		return
-	}
-	var undecided []*pending
-	for i, p := range batch {
-		if status[i] == StatusUndecided {
-			undecided = append(undecided, p) // this one request goes to the reference engine
-			continue
+	globalMax := b.GlobalMax()
+	b.rep.run(func(s *Snapshot) {
+		allowed, status, err := s.CheckBatch(reqs, depths, globalMax)
+		if err != nil {
+			b.fallbackAll(batch)
+			return
 		}
-		// StatusUnknownNamespace is allowed = false, nil like the reference (engine.go:98-100)
-		p.done <- result{allowed[i], nil}
-	}
-	b.fallbackAll(undecided)
+		var undecided []*pending
+		for i, p := range batch {
+			if status[i] == StatusUndecided {
+				undecided = append(undecided, p) // this one request goes to the reference engine
+				continue
+			}
+			// StatusUnknownNamespace is allowed = false, nil like the reference (engine.go:98-100)
+			p.done <- result{allowed[i], nil}
+		}
+		b.fallbackAll(undecided)
+	})
 }
 
 // ExpandBatcher coalesces concurrent BuildTree calls into keto_expand_batch calls (defaults: 4,096
-// roots or 200 µs per batch).  Trees come back as pre-order Nodes; errors per root are ErrNotFound,
-// ErrUndecided, a wrapped ErrBatchFailed or ErrClosed (the last three: answer on the SQL engine).
+// roots or 200 µs per batch), dealt over the replica set's GPUs.  Trees come back as pre-order Nodes;
+// errors per root are ErrNotFound, ErrUndecided, a wrapped ErrBatchFailed or ErrClosed (the last
+// three: answer on the SQL engine).
 type ExpandBatcher struct {
-	mu        sync.RWMutex
-	snap      *Snapshot
+	rep       *replicas
 	GlobalMax func() int
 	c         *coalescer
 }
@@ -232,9 +267,9 @@ type expandReq struct {
 	depth int
 }
 
-// NewExpandBatcher starts the flush loop.
-func NewExpandBatcher(s *Snapshot, globalMax func() int) *ExpandBatcher {
-	b := &ExpandBatcher{snap: s, GlobalMax: globalMax}
+// NewExpandBatcher starts the flush loop over one snapshot per GPU.
+func NewExpandBatcher(snaps []*Snapshot, globalMax func() int) *ExpandBatcher {
+	b := &ExpandBatcher{rep: newReplicas(snaps), GlobalMax: globalMax}
 	b.c = newCoalescer(1<<12, 200*time.Microsecond, b.flush, func(ps []*pending) {
 		for _, p := range ps {
 			p.done <- result{nil, ErrClosed}
@@ -243,14 +278,8 @@ func NewExpandBatcher(s *Snapshot, globalMax func() int) *ExpandBatcher {
 	return b
 }
 
-// Swap installs a new snapshot version; it returns once no batch uses the old one.
-func (b *ExpandBatcher) Swap(s *Snapshot) *Snapshot {
-	b.mu.Lock()
-	defer b.mu.Unlock()
-	old := b.snap
-	b.snap = s
-	return old
-}
+// Swap installs a new replica set; it returns the old one once no batch uses it.
+func (b *ExpandBatcher) Swap(snaps []*Snapshot) []*Snapshot { return b.rep.swap(snaps) }
 
 // Close stops the loop; queued and later requests get ErrClosed.
 func (b *ExpandBatcher) Close() { b.c.close() }
@@ -272,17 +301,18 @@ func (b *ExpandBatcher) flush(batch []*pending) {
 		q := p.req.(expandReq)
 		subs[i], depths[i] = q.sub, q.depth
 	}
-	b.mu.RLock()
-	trees, errs, err := b.snap.ExpandBatch(subs, depths, b.GlobalMax())
-	b.mu.RUnlock()
-	for i, p := range batch {
-		switch {
-		case err != nil:
-			p.done <- result{nil, fmt.Errorf("%w: %v", ErrBatchFailed, err)}
-		case errs[i] != nil:
-			p.done <- result{nil, errs[i]}
-		default:
-			p.done <- result{trees[i], nil}
+	globalMax := b.GlobalMax()
+	b.rep.run(func(s *Snapshot) {
+		trees, errs, err := s.ExpandBatch(subs, depths, globalMax)
+		for i, p := range batch {
+			switch {
+			case err != nil:
+				p.done <- result{nil, fmt.Errorf("%w: %v", ErrBatchFailed, err)}
+			case errs[i] != nil:
+				p.done <- result{nil, errs[i]}
+			default:
+				p.done <- result{trees[i], nil}
+			}
 		}
-	}
+	})
 }

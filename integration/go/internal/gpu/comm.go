@@ -16,9 +16,10 @@ import (
 	"github.com/ory/keto/internal/relationtuple"
 )
 
-// Comm is the library's RCCL communicator (keto_comm, include/keto_mi355x.h): one Keto server
-// process per GPU (internal/driver/daemon.go:62-69 serves one process), the processes of a node
-// joined by one communicator.  Every method is collective: all ranks call it.
+// Comm is the library's communicator (keto_comm, include/keto_mi355x.h): over RCCL between processes
+// (NewComm, one process per GPU), or between goroutines of one server process (NewLocalComm; the
+// reference serves from one process, internal/driver/daemon.go:62-69).  Every method is collective:
+// all ranks call it, an empty batch included; an error on one rank is returned by every rank.
 type Comm struct {
 	h *C.keto_comm
 }
@@ -48,6 +49,24 @@ func NewComm(id []byte, ranks, rank, device int) (*Comm, error) {
 	return &Comm{h: h}, nil
 }
 
+// NewLocalComm joins an in-process communicator (keto_comm_init_local): the ranks are goroutines of
+// this one server process, each rank's collective calls made from its own goroutine (a blocked cgo
+// call holds its own OS thread) and driving its own part of an edge-partitioned snapshot on GPU
+// device; the exchanges are device copies (peer copies over xGMI).
+// id is any KETO_COMM_ID_BYTES the process chooses, the same for every rank.
+func NewLocalComm(id []byte, ranks, rank, device int) (*Comm, error) {
+	if len(id) != C.KETO_COMM_ID_BYTES {
+		return nil, fmt.Errorf("gpu: communicator id of %d bytes, want %d", len(id), C.KETO_COMM_ID_BYTES)
+	}
+	cid := C.CBytes(id)
+	defer C.free(cid)
+	var h *C.keto_comm
+	if rc := C.keto_comm_init_local((*C.uint8_t)(cid), C.int32_t(ranks), C.int32_t(rank), C.int32_t(device), &h); rc != C.KETO_OK {
+		return nil, lastErr(rc)
+	}
+	return &Comm{h: h}, nil
+}
+
 // Close frees the communicator (keto_comm_free).
 func (c *Comm) Close() {
 	if c.h != nil {
@@ -60,7 +79,7 @@ func (c *Comm) Close() {
 // rank checks its contiguous shard, one all-gather returns every decision to every rank
 // (keto_check_batch_sharded).
 func (c *Comm) CheckBatchSharded(s *Snapshot, reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
-	return checkWith(reqs, depths, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
+	return checkWith(reqs, depths, true, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
 		return C.keto_check_batch_sharded(c.h, s.h, cr, n, C.int32_t(globalMax), allowed, status)
 	})
 }
@@ -68,7 +87,7 @@ func (c *Comm) CheckBatchSharded(s *Snapshot, reqs []*relationtuple.InternalRela
 // CheckBatchRouted decides this rank's own batch on an edge-partitioned snapshot: requests travel
 // to the parts owning their rows and their decisions come back (keto_check_batch_routed).
 func (c *Comm) CheckBatchRouted(s *Snapshot, reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
-	return checkWith(reqs, depths, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
+	return checkWith(reqs, depths, true, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
 		return C.keto_check_batch_routed(c.h, s.h, cr, n, C.int32_t(globalMax), allowed, status)
 	})
 }

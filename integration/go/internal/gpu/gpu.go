@@ -183,6 +183,56 @@ func Build(nss []*namespace.Namespace, rows []Row, device int) (*Snapshot, error
 	return &Snapshot{h: h}, nil
 }
 
+// Clone makes a replica of the snapshot at its current version on another HIP device
+// (keto_snapshot_clone): the host tables are copied and uploaded, nothing is scanned or sorted again.
+func (s *Snapshot) Clone(device int) (*Snapshot, error) {
+	var h *C.keto_snapshot
+	if rc := C.keto_snapshot_clone(s.h, C.int32_t(device), &h); rc != C.KETO_OK {
+		return nil, lastErr(rc)
+	}
+	return &Snapshot{h: h, Version: s.Version}, nil
+}
+
+// BuildReplicas builds one snapshot per device of a node (one server process driving every GPU):
+// the rows are sorted and uploaded once by Build on devices[0], the other devices get clones.
+func BuildReplicas(nss []*namespace.Namespace, rows []Row, devices []int) ([]*Snapshot, error) {
+	if len(devices) == 0 {
+		return nil, errors.New("gpu: no device")
+	}
+	first, err := Build(nss, rows, devices[0])
+	if err != nil {
+		return nil, err
+	}
+	out := []*Snapshot{first}
+	for _, d := range devices[1:] {
+		c, err := first.Clone(d)
+		if err != nil {
+			CloseAll(out)
+			return nil, err
+		}
+		out = append(out, c)
+	}
+	return out, nil
+}
+
+// CloseAll closes every snapshot of a replica set.
+func CloseAll(snaps []*Snapshot) {
+	for _, s := range snaps {
+		s.Close()
+	}
+}
+
+// ApplyAll applies one transaction to every replica (see Apply).  An error from any replica leaves
+// the set inconsistent: the caller rebuilds it (gpu.ErrRebuild or a device error alike).
+func ApplyAll(snaps []*Snapshot, inserts, deletes []Row) error {
+	for _, s := range snaps {
+		if err := s.Apply(inserts, deletes); err != nil {
+			return err
+		}
+	}
+	return nil
+}
+
 // Close releases the host tables and the device arena.
 func (s *Snapshot) Close() {
 	if s.h != nil {
@@ -215,17 +265,18 @@ func (m *cmem) subject(sub relationtuple.Subject) C.keto_subject {
 // CheckBatch = check.(*Engine).SubjectIsAllowed (internal/check/engine.go:116-123) for many
 // requests: allowed[i] and status[i] (StatusUndecided: ask the SQL engine for request i).
 func (s *Snapshot) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
-	return checkWith(reqs, depths, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
+	return checkWith(reqs, depths, false, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
 		return C.keto_check_batch(s.h, cr, n, C.int32_t(globalMax), allowed, status)
 	})
 }
 
 // checkWith marshals the requests into C memory, runs call (one of the keto_check_batch* entry
-// points taking keto_check_req) and unpacks its decisions and statuses.
-func checkWith(reqs []*relationtuple.InternalRelationTuple, depths []int,
+// points taking keto_check_req) and unpacks its decisions and statuses.  collective: the call is a
+// collective one (comm.go) and is made even for an empty batch, since the other ranks wait for it.
+func checkWith(reqs []*relationtuple.InternalRelationTuple, depths []int, collective bool,
 	call func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int) ([]bool, []uint8, error) {
 	n := len(reqs)
-	if n == 0 {
+	if n == 0 && !collective {
 		return nil, nil, nil
 	}
 	if len(depths) != n {

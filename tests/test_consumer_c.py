@@ -27,10 +27,10 @@ def consumer(tmp_path_factory):
     return exe
 
 
-def _input(case, device):
+def _input(case, device, replicas=1):
     ns = case_namespaces(case)
     ids = {n: i for i, n in reversed(ns)}
-    lines = [f"P\t{case.get('page_size', 100)}", f"V\t{device}"]
+    lines = [f"P\t{case.get('page_size', 100)}", f"V\t{device}", "R" + f"\t{device}" * replicas]
     lines += [f"N\t{i}\t{n}" for i, n in ns]
     for t in case_tuples(case):
         if isinstance(t.subject, SubjectID):
@@ -52,9 +52,9 @@ def _input(case, device):
     return "\n".join(lines) + "\n"
 
 
-def _run(exe, tmp_path, case, device):
+def _run(exe, tmp_path, case, device, replicas=1):
     p = tmp_path / "in.tsv"
-    p.write_text(_input(case, device))
+    p.write_text(_input(case, device, replicas))
     r = subprocess.run([exe, str(p)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     return r.stdout.splitlines()
@@ -62,7 +62,7 @@ def _run(exe, tmp_path, case, device):
 
 @pytest.mark.parametrize("case", [c for c in load_cases() if c.get("checks")][:6], ids=lambda c: c["name"])
 def test_consumer_host_only(consumer, tmp_path, case):
-    out = _run(consumer, tmp_path, case, -1)
+    out = _run(consumer, tmp_path, case, -1, replicas=2)      # host-only replicas clone too
     assert out[0].startswith("stats tuples=")
     assert out[1] == "nodevice -2"                      # KETO_E_HIP: no compute without a device
     assert out[-1] == "done"
@@ -98,12 +98,15 @@ def _tuple_fields(ids, t):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("replicas", [1, 2, 3])
 @pytest.mark.parametrize("seed", range(24))
-def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed):
+def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed, replicas):
     """The whole Go call sequence from C: build -> check / expand micro-batches -> write transactions
     applied after they commit (KETO_E_REBUILD -> rebuild from the consumer's table, as the registry's
     persister wrapper does) -> checks and expands again; trees also rebuilt from keto_tree_nodes +
-    keto_subject_fields (the Go shim's path) and re-encoded byte-equal.  Every decision and tree is
+    keto_subject_fields (the Go shim's path) and re-encoded byte-equal.  With replicas > 1 the consumer
+    is one server process over several devices (here all device 0): replicas cloned from the first
+    build, batches dealt round-robin, every write applied to each.  Every decision and tree is
     compared with the SQL oracle replaying the same transactions."""
     import random
     from oracle.oracle_sql import CheckEngine, ExpandEngine, NotFoundError, SQLStore
@@ -118,7 +121,8 @@ def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed):
         pytest.skip("only a namespace named ''")
     ids = {n: i for i, n in reversed(ns)}
     store = SQLStore(ns, tuples, page_size=ps)
-    lines = [f"P\t{ps}", "V\t0"] + [f"N\t{i}\t{n}" for i, n in ns] + [f"T\t{_tuple_fields(ids, t)}" for t in tuples]
+    lines = [f"P\t{ps}", "V\t0", "R" + "\t0" * replicas]
+    lines += [f"N\t{i}\t{n}" for i, n in ns] + [f"T\t{_tuple_fields(ids, t)}" for t in tuples]
     want = []                                  # expected output lines, in order
     rng = random.Random(seed)
     for step in range(6):

@@ -96,3 +96,30 @@ def test_engine_dispatch_hooks_match_the_registry():
     # (internal/relationtuple/definitions.go:28-34)
     for m in ("WriteRelationTuples", "DeleteRelationTuples", "DeleteAllRelationTuples", "TransactRelationTuples"):
         assert re.search(r"func \(p \*gpuPersister\) " + m + r"\(", reg), m
+
+
+def test_multi_gpu_server_process():
+    """One server process drives every GPU (the reference is one process, internal/driver/daemon.go:62-69):
+    EnableGPU takes the device list, builds one replica per device (sorted once, the others cloned
+    with keto_snapshot_clone), the batchers deal batches over the replica set, and every write
+    transaction reaches every replica before it returns."""
+    reg = _code(open(os.path.join(GO, "internal", "driver", "registry_gpu.go")).read())
+    assert re.search(r"func EnableGPU\(ctx context\.Context, reg Registry, devices \[\]int\) error", reg)
+    assert "gpu.BuildReplicas(" in reg and "gpu.ApplyAll(" in reg and "func GPUDevicesFromEnv() []int" in reg
+    gpu_go = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
+    assert "C.keto_snapshot_clone(" in gpu_go
+    assert re.search(r"func BuildReplicas\(nss \[\]\*namespace\.Namespace, rows \[\]Row, devices \[\]int\)", gpu_go)
+    bat = _code(open(os.path.join(GO, "internal", "gpu", "batcher.go")).read())
+    assert re.search(r"func NewBatcher\(snaps \[\]\*Snapshot,", bat)
+    assert re.search(r"func NewExpandBatcher\(snaps \[\]\*Snapshot,", bat)
+    assert "r.idle" in bat                              # a batch goes to a replica with none in flight
+
+
+def test_collective_calls_never_skip_an_empty_batch():
+    """keto_check_batch_sharded / _routed are collective: a rank with no request must still call them,
+    or its peers wait (checkWith's collective flag)."""
+    comm = _code(open(os.path.join(GO, "internal", "gpu", "comm.go")).read())
+    gpu_go = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
+    assert len(re.findall(r"checkWith\(reqs, depths, true,", comm)) == 2
+    assert "if n == 0 && !collective {" in gpu_go
+    assert "C.keto_comm_init_local(" in comm
