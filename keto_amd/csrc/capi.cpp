@@ -327,6 +327,33 @@ std::vector<WildReq> keto::resolve_all(const Snapshot& S, const keto_check_req* 
     return all;
 }
 
+namespace keto {
+// keto_check_batch's body (the caller holds the snapshot's lock shared); comm.cpp answers a
+// partitioned batch's wildcard requests with it
+void check_named(Snapshot& S, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth, uint8_t* allowed_out,
+                 uint8_t* status_out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    // resolution (whereQuery on the snapshot) on host threads into uninitialized buffers (every
+    // entry is written); wildcard requests that need a batch-local overlay row are materialized
+    // afterwards, in request order
+    std::vector<keto_check_ids, NoInitAlloc<keto_check_ids>> ids(n);
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> st(status_out ? 0 : n);
+    uint8_t* status = status_out ? status_out : st.data();
+    Overlay ov;
+    ov.base = S.n_rows();
+    for (const WildReq& w : resolve_all(S, reqs, n, ids.data(), status))
+        ids[w.i].row = handle_of(S, &ov, overlay_row(S, ov, w.key));
+    S.last_resolve_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    device_check_host(S, ids.data(), n, global_max_depth, allowed_out, FORM_HANDLES, 0, &ov);
+    if (status_out)
+        for (uint32_t i = 0; i < n; ++i)
+            if (allowed_out[i] == KETO_UNDECIDED) {
+                allowed_out[i] = 0;
+                status_out[i] = KETO_CHECK_UNDECIDED;
+            }
+}
+}  // namespace keto
+
 extern "C" {
 
 int keto_abi_version(void) { return KETO_ABI_VERSION; }
@@ -415,31 +442,13 @@ int keto_resolve_checks(const keto_snapshot* h, const keto_check_req* reqs, uint
     });
 }
 
+
 int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth,
                      uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
         std::shared_lock<std::shared_mutex> lk(h->s->rw);
-        Snapshot& S = *h->s;
-        const auto t0 = std::chrono::steady_clock::now();
-        // resolution (whereQuery on the snapshot) on host threads into uninitialized buffers (every
-        // entry is written); wildcard requests that need a batch-local overlay row are materialized
-        // afterwards, in request order
-        std::vector<keto_check_ids, NoInitAlloc<keto_check_ids>> ids(n);
-        std::vector<uint8_t, NoInitAlloc<uint8_t>> st(status_out ? 0 : n);
-        uint8_t* status = status_out ? status_out : st.data();
-        Overlay ov;
-        ov.base = S.n_rows();
-        for (const WildReq& w : resolve_all(S, reqs, n, ids.data(), status))
-            ids[w.i].row = handle_of(S, &ov, overlay_row(S, ov, w.key));
-        S.last_resolve_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        device_check_host(S, ids.data(), n, global_max_depth, allowed_out, FORM_HANDLES, 0, &ov);
-        if (status_out)
-            for (uint32_t i = 0; i < n; ++i)
-                if (allowed_out[i] == KETO_UNDECIDED) {
-                    allowed_out[i] = 0;
-                    status_out[i] = KETO_CHECK_UNDECIDED;
-                }
+        check_named(*h->s, reqs, n, global_max_depth, allowed_out, status_out);
         return KETO_OK;
     });
 }

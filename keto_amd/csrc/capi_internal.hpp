@@ -41,4 +41,8 @@ auto guarded(F&& f) -> decltype(f()) {
 std::vector<WildReq> resolve_all(const Snapshot& S, const keto_check_req* reqs, uint32_t n, keto_check_ids* ids,
                                  uint8_t* st, bool by_row = false);
 
+// keto_check_batch's body, the caller holding the snapshot's lock shared (capi.cpp)
+void check_named(Snapshot& S, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth, uint8_t* allowed_out,
+                 uint8_t* status_out);
+
 }  // namespace keto

@@ -574,6 +574,7 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         Snapshot* Sp = nullptr;
         std::shared_lock<std::shared_mutex> lk;
         std::vector<uint64_t> cnt(c->n, 0);
+        std::vector<WildReq> wild;     // wildcard queries no stored set uses: answered here (below)
         keto_check_ids* d_send = nullptr;
         uint32_t* d_order = nullptr;
         uint64_t wb = 0;
@@ -587,11 +588,11 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             injected(*c, "resolve");
             // names -> row ids (routing needs rows, not this part's handles)
             std::vector<keto_check_ids> ids(std::max<uint32_t>(n, 1));
-            const auto wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
-            if (!wild.empty())
+            wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
+            if (!wild.empty() && Sp->part_mode == PART_MIGRATE)
                 throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
-                                                " is a wildcard query that no stored subject set uses: not routable "
-                                                "on a partitioned snapshot"};
+                                                " is a wildcard query that no stored subject set uses: not "
+                                                "answered on a migrating partition"};
             keto_check_ids* d_reqs = c->a.get<keto_check_ids>(n);
             HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice,
                                   c->stream));
@@ -655,6 +656,21 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
                 allowed_out[i] = 0;
                 if (status_out[i] == KETO_CHECK_OK) status_out[i] = KETO_CHECK_UNDECIDED;
             }
+        // A wildcard query that no stored subject set uses (whereQuery with an empty field,
+        // relationtuples.go:178-198) has no row to route by; it went to this part as a request without
+        // a row.  Every part holds the whole graph's host tables, so this part builds its batch-local
+        // row (every matching row's tuples in ORDER BY order, as keto_check_batch does) and answers
+        // it: below its top level a search only enters subject-set targets, which every part holds.
+        if (!wild.empty()) {
+            std::vector<keto_check_req> wq(wild.size());
+            for (size_t k = 0; k < wild.size(); ++k) wq[k] = reqs[wild[k].i];
+            std::vector<uint8_t> wa(wild.size()), ws(wild.size());
+            check_named(S, wq.data(), (uint32_t)wq.size(), global_max_depth, wa.data(), ws.data());
+            for (size_t k = 0; k < wild.size(); ++k) {
+                allowed_out[wild[k].i] = wa[k];
+                status_out[wild[k].i] = ws[k];
+            }
+        }
         return KETO_OK;
     });
 }

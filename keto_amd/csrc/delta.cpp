@@ -21,8 +21,10 @@
 // a row some wildcard row matches re-materializes the wildcard row from the staged edges.  Writes
 // outside this delta path throw KETO_E_REBUILD and leave the snapshot unchanged; the caller rebuilds
 // it (keto_snapshot_build from the table): a write that touches a poisoned row (one whose pages hold
-// a tuple of an unknown namespace), or a wildcard row that matches one.  A partitioned snapshot takes
-// no writes.
+// a tuple of an unknown namespace), or a wildcard row that matches one.  A part of an
+// edge-partitioned snapshot (KETO_PART_SHARED) takes every transaction: its host tables are the whole
+// graph's, and device_apply writes the rows the part holds (every subject-set target and its own root
+// rows); a migrating part takes none.
 #include <algorithm>
 #include <cstring>
 
@@ -253,7 +255,11 @@ std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {     /
 }  // namespace
 
 void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del) {
-    if (S.n_parts > 1 || S.part_mode == PART_MIGRATE) throw Error{KETO_E_INVALID, "writes need a replicated snapshot (not an edge-partitioned part)"};
+    // a shared-rows part holds the whole graph's host tables: every part applies every transaction
+    // and device_apply writes the rows this part holds; a migrating part's stubs carry their owners'
+    // filters and handles, which a local write cannot follow
+    if (S.part_mode == PART_MIGRATE)
+        throw Error{KETO_E_INVALID, "writes need a replicated snapshot or a shared-rows part (not a migrating part)"};
     if ((n_ins && !ins) || (n_del && !del)) throw Error{KETO_E_INVALID, "NULL tuples"};
     Txn T(S);
     // ---- inserts (commit order: after every equal tuple), then deletes (every equal tuple)

@@ -2674,16 +2674,26 @@ void device_apply(Snapshot& S) {
         w.img = {to, 0u, HDR_FWD | (cb ? HDR_CLOSURE : 0u), 0u};
         writes.push_back(std::move(w));
     };
+    // a part of an edge-partitioned snapshot (PART_SHARED) holds every row some subject set points at
+    // and its own root rows: another part's root row has no place here, whatever a write did to it
+    // (that part's apply writes it), and a root row that became a target joins every part
+    const bool parted = S.n_parts > 1;
+    auto elsewhere = [&](uint32_t r) { return parted && S.is_root[r] && S.root_owner(r, S.n_parts) != S.part; };
     // 1. new identities first: edges name targets by identity handle
     std::vector<std::pair<uint32_t, uint32_t>> moved;        // (row, old identity)
     std::vector<uint32_t> fresh;
     for (uint32_t r : S.dirty)
-        if (S.unit_of_row[r] == NO_UNIT) fresh.push_back(r);
-    for (uint32_t r : S.needs_cb)
+        if (S.unit_of_row[r] == NO_UNIT && !elsewhere(r)) fresh.push_back(r);
+    for (uint32_t r : S.needs_cb) {
         if (S.unit_of_row[r] != NO_UNIT && !S.row_cb[r]) {
             moved.push_back({r, S.unit_of_row[r]});
             fresh.push_back(r);
+        } else if (S.unit_of_row[r] == NO_UNIT) {
+            fresh.push_back(r);                                   // another part's root row until now
         }
+    }
+    std::sort(fresh.begin(), fresh.end());
+    fresh.erase(std::unique(fresh.begin(), fresh.end()), fresh.end());
     for (uint32_t r : fresh) {
         uint64_t tw = 0;
         const uint32_t u = tail_place(S, S.row_hlog2(r), true, S.row_edges(r).second, tw);
@@ -2697,8 +2707,10 @@ void device_apply(Snapshot& S) {
     // 2. every changed row's content
     std::vector<uint8_t> is_fresh(S.n_rows(), 0);
     for (uint32_t r : fresh) is_fresh[r] = 1;
-    std::vector<uint32_t> todo(S.dirty);
-    for (auto& m : moved) todo.push_back(m.first);
+    std::vector<uint32_t> todo;
+    for (uint32_t r : S.dirty)
+        if (S.unit_of_row[r] != NO_UNIT) todo.push_back(r);    // (elsewhere: not on this part)
+    for (uint32_t r : fresh) todo.push_back(r);
     std::sort(todo.begin(), todo.end());
     todo.erase(std::unique(todo.begin(), todo.end()), todo.end());
     for (uint32_t r : todo) {

@@ -158,10 +158,12 @@ def test_local_ranks_match_oracle(P, seed):
     comms = _local_comms(P)
     for r, (got, st) in enumerate(_ok(_ranks(P, lambda r: comms[r].check_batch_sharded(full, reqs, g)))):
         assert (got == want).all() and (st == want_st).all(), (seed, r)
-    routable = [i for i, q in enumerate(reqs) if not _wild(q)]
     ranks = P - (seed % 2)                          # odd seeds: the last rank passes no request
-    mine = [routable[r::ranks] if r < ranks else [] for r in range(P)]
     for mode in (PART_SHARED, PART_MIGRATE):
+        # wildcard queries no stored set uses: answered by the requesting shared-rows part; a migrating
+        # partition refuses them (test_local_error_agreement_bad_arguments)
+        routable = [i for i, q in enumerate(reqs) if mode == PART_SHARED or not _wild(q)]
+        mine = [routable[r::ranks] if r < ranks else [] for r in range(P)]
         parts = _parts(ns, rows, ps, P, mode)
         if mode == PART_MIGRATE:
             _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
@@ -286,38 +288,123 @@ def test_local_error_agreement(powerlaw_strings, monkeypatch, point):
 
 
 def test_local_error_agreement_bad_arguments(powerlaw_strings):
-    """Real rank-local errors, no injection: rank 2 passes a NULL request array with n > 0; rank 0
-    passes a wildcard query (empty object) that no stored set uses.  Every rank returns the code."""
-    from keto_amd.capi import PART_SHARED, KCheckReq
+    """Real rank-local errors, no injection: rank 2 passes a NULL request array with n > 0 (shared-rows
+    parts); on a migrating partition rank 0 passes a wildcard query (empty object) that no stored set
+    uses, which a migrating part does not answer.  Every rank returns the code; the same wildcard
+    query on the shared-rows parts is answered by rank 0 like the replicated snapshot answers it."""
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED, KCheckReq
     g, st, full, arr, n, want, want_st = powerlaw_strings
     P = 3
-    parts = []
-    for r in range(P):
-        part, _ = g.snapshot_from_strings(st, device=-1)
-        parts.append(part.upload_part(r, P, 0, mode=PART_SHARED))
-    comms = _local_comms(P)
     k = 1000
-
-    def null_on_2(r):
-        c = comms[r]
-        if r == 2:
-            from keto_amd.capi import _check
-            import numpy as np
-            a = np.zeros(k, dtype=np.uint8)
-            _check(c.lib.keto_check_batch_routed(c.h, parts[r].h, None, C.c_uint32(k), C.c_int32(5),
-                                                 a.ctypes.data_as(C.c_void_p), a.ctypes.data_as(C.c_void_p)))
-        return c.check_batch_routed(parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)
-
-    _agreed_failure(_ranks(P, null_on_2), 2, "NULL")
     wild = (KCheckReq * k)()
     C.memmove(wild, _slice(arr, 0, k), C.sizeof(wild))
     wild[7].object.n = 0                                  # docs:#view@u -- a wildcard query
+    wild_want, wild_st = full.check_batch_reqs(wild, k, 5)
+    for mode in (PART_SHARED, PART_MIGRATE):
+        parts = []
+        for r in range(P):
+            part, _ = g.snapshot_from_strings(st, device=-1)
+            parts.append(part.upload_part(r, P, 0, mode=mode))
+        comms = _local_comms(P)
+        if mode == PART_MIGRATE:
+            _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
 
-    def wild_on_0(r):
-        return comms[r].check_batch_routed(parts[r], wild if r == 0 else _slice(arr, r * k, (r + 1) * k), 5, n=k)
+        def null_on_2(r):
+            c = comms[r]
+            if r == 2:
+                from keto_amd.capi import _check
+                import numpy as np
+                a = np.zeros(k, dtype=np.uint8)
+                _check(c.lib.keto_check_batch_routed(c.h, parts[r].h, None, C.c_uint32(k), C.c_int32(5),
+                                                     a.ctypes.data_as(C.c_void_p), a.ctypes.data_as(C.c_void_p)))
+            return c.check_batch_routed(parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)
 
-    _agreed_failure(_ranks(P, wild_on_0), 0, "wildcard")
-    _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)))
+        _agreed_failure(_ranks(P, null_on_2), 2, "NULL")
+
+        def wild_on_0(r):
+            return comms[r].check_batch_routed(parts[r], wild if r == 0 else _slice(arr, r * k, (r + 1) * k), 5, n=k)
+
+        res = _ranks(P, wild_on_0)
+        if mode == PART_MIGRATE:
+            _agreed_failure(res, 0, "wildcard")
+        else:
+            got, gst = _ok(res)[0]
+            assert (got == wild_want).all() and (gst == wild_st).all()
+        for r, (got, gst) in enumerate(_ok(_ranks(P, lambda r: comms[r].check_batch_routed(
+                parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)))):
+            assert (got == want[r * k:(r + 1) * k]).all(), (mode, r)
+        for c in comms:
+            c.close()
+        for p in parts:
+            p.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("seed", range(4200, 4216))
+def test_local_shared_parts_follow_writes(P, seed):
+    """Write transactions on an edge-partitioned snapshot (KETO_PART_SHARED): every part applies every
+    transaction (its host tables are the whole graph's) and writes the rows it holds -- subject-set
+    targets on every part, root rows on their owner, a root row that becomes a target joins every part.
+    After each write the routed checks of every rank (wildcard queries included) and the expands of
+    each part's own roots equal the SQL oracle's (relationtuples.go:128-149,200-223,
+    check/engine.go:36-123, expand/engine.go:33-102)."""
+    import random
+    from oracle.oracle_sql import ExpandEngine, NotFoundError, SQLStore
+    from tests.randgraph import random_expands, random_graph
+    from tests.test_gpu_lifecycle import _random_write, _row
+    import keto_amd
+    from keto_amd.capi import PART_SHARED
+    ns, tuples, raw, ps, alph = random_graph(seed, wide=seed % 4 == 3, allow_wildcards=seed % 3 == 0,
+                                             allow_poison=False, allow_collisions=seed % 2 == 0)
+    names, objs, rels, users = alph
+    set_names = list(names)
+    names = [n_ for n_ in names if n_]
+    if not names:
+        pytest.skip("only a namespace named ''")
+    store = SQLStore(ns, tuples, page_size=ps)
+    rows = rows_from_tuples(ns, tuples)
+    parts = [keto_amd.Snapshot.build(ns, rows, page_size=ps, device=-1).upload_part(r, P, 0, mode=PART_SHARED)
+             for r in range(P)]
+    comms = _local_comms(P)
+    rng = random.Random(seed)
+    g = 5
+    for step in range(6):
+        cur = store.tuples()
+        ins = [_random_write(rng, names, objs, rels, users, set_names, 0.1) for _ in range(rng.randint(1, 8))]
+        dels = [rng.choice(cur) for _ in range(rng.randint(0, 3))] if cur else []
+        for p in parts:
+            p.apply([_row(ns, t) for t in ins], [_row(ns, t) for t in dels])
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+        checks = random_checks(seed * 41 + step, (names, objs + ["new1", "a0"], rels + ["q"], users + ["w001"]), k=60)
+        reqs = [(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in checks]
+        mine = [list(range(r, len(reqs), P)) for r in range(P)]
+        res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], [reqs[i] for i in mine[r]], g)))
+        for r, (got, _) in enumerate(res):
+            for k, i in enumerate(mine[r]):
+                t, d, _ = checks[i]
+                assert bool(got[k]) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, step, r, t, d)
+        # expands of set roots on the part owning the root row (any part for a subject-set target)
+        exps = random_expands(seed * 23 + step, (names, objs + ["new3"], rels + ["q"], users), k=10)
+        for s_, d, _ in exps:
+            if not hasattr(s_, "namespace") or "" in (s_.namespace, s_.object, s_.relation):
+                continue
+            try:
+                tr = ExpandEngine(store, g).build_tree(s_, d)
+                want_t = ("tree", tr.to_json()) if tr is not None else ("nil", None)
+            except NotFoundError:
+                want_t = ("error", None)
+            answered = False
+            for p in parts:
+                try:
+                    (st_, js), = p.expand_batch([(subj(s_), d)], g)
+                except keto_amd.KetoError:
+                    continue                                # another part's root row
+                answered = True
+                assert ({0: "tree", 1: "nil", 2: "error"}[st_], js) == want_t, (seed, step, s_, d)
+            assert answered, s_
     for c in comms:
         c.close()
     for p in parts:
