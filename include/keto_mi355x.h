@@ -192,11 +192,14 @@ int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot*
  * tuple, as commit_time orders them, :128-149), then the deletes (every tuple equal in namespace,
  * object, relation and subject, :200-223).  The changed rows are rewritten in the device arena in
  * place (forwards when a row outgrows its place; the tail grows on demand) and closure filters are
- * re-closed, between batches; later batches see the new version.  An unknown namespace id fails the
- * whole transaction (KETO_E_INVALID), like GetNamespaceByName.  KETO_E_REBUILD: this write changes
- * what the build derives globally (a new Subject.String() collision, a stored subject set with an
- * empty field, a row a stored wildcard set materializes, a poisoned row, a partitioned snapshot); the
- * snapshot is unchanged and the caller rebuilds it from the table.  Row handles (keto_row_handles,
+ * re-closed, between batches; later batches see the new version.  New Subject.String() collisions
+ * (collision classes, ROW_SEQ rows) and stored subject sets with an empty field (their materialized
+ * rows, re-materialized when a row they match changes) are patched in place too.  A part of an
+ * edge-partitioned snapshot (KETO_PART_SHARED) takes every transaction and writes the rows it holds;
+ * a migrating part takes none (KETO_E_INVALID).  An unknown namespace id fails the whole transaction
+ * (KETO_E_INVALID), like GetNamespaceByName.  KETO_E_REBUILD: the write touches a poisoned row (a
+ * tuple of an unconfigured namespace) or a wildcard row that matches one; the snapshot is unchanged
+ * and the caller rebuilds it from the table.  Row handles (keto_row_handles,
  * keto_resolve_checks) are per version: resolve again after a write.  *version_out (may be NULL)
  * gets the new version: the snaptoken the reference leaves "not yet implemented"
  * (internal/check/handler.go:182). */

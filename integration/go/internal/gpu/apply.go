@@ -16,9 +16,10 @@ import (
 	"github.com/ory/keto/internal/relationtuple"
 )
 
-// ErrRebuild: the write touches what the snapshot derives globally (wildcard subject sets, a new
-// Subject.String() collision, a poisoned row, a partitioned snapshot).  The snapshot is unchanged;
-// build a new one from the table (keto_snapshot_apply, KETO_E_REBUILD).
+// ErrRebuild: the write touches a poisoned row (a tuple of an unconfigured namespace) or a wildcard
+// row that matches one.  The snapshot is unchanged; build a new one from the table
+// (keto_snapshot_apply, KETO_E_REBUILD).  New Subject.String() collisions, wildcard subject sets and
+// writes to a shared-rows part of an edge-partitioned snapshot are applied in place.
 var ErrRebuild = errors.New("keto_mi355x: write needs a snapshot rebuild")
 
 // Apply patches the snapshot with one transaction of TransactRelationTuples

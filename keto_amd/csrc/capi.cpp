@@ -27,7 +27,7 @@ struct keto_tree_arena {
     // for the filling call that follows it, so a size-then-fill pair encodes once
     mutable std::mutex enc_mu;
     mutable int enc_kind = 0;              // 0 none, 1 JSON, 2 protobuf
-    mutable const void* enc_snap = nullptr;
+    mutable uint64_t enc_uid = 0;          // the snapshot the encodings were made with (Snapshot::uid)
     mutable uint64_t enc_version = 0;
     mutable std::vector<std::string> enc;
 };
@@ -907,7 +907,7 @@ int64_t encode_all(const keto_snapshot* h, const keto_tree_arena* a, int kind, c
     std::shared_lock<std::shared_mutex> rlk(h->s->rw);      // before enc_mu: apply takes rw alone
     std::lock_guard<std::mutex> lk(a->enc_mu);
     std::vector<std::string>& enc = a->enc;
-    if (!(a->enc_kind == kind && a->enc_snap == h && a->enc_version == h->s->version && enc.size() == n)) {
+    if (!(a->enc_kind == kind && a->enc_uid == h->s->uid && a->enc_version == h->s->version && enc.size() == n)) {
         enc.assign(n, std::string());
         std::vector<std::thread> ts;
         std::atomic<uint32_t> next{0};
@@ -932,7 +932,7 @@ int64_t encode_all(const keto_snapshot* h, const keto_tree_arena* a, int kind, c
         a->enc_kind = 0;
     } else {
         a->enc_kind = kind;
-        a->enc_snap = h;
+        a->enc_uid = h->s->uid;
         a->enc_version = h->s->version;
     }
     return total;

@@ -298,9 +298,9 @@ struct keto_comm {
     // d routed requests out, g routed requests in, h their decisions, i decisions back, k / l the
     // migrating rounds' records and offsets
     DBuf a, b, c, d, g, h, i, k, l;
-    // owner part per row id (int16, -1 = every part) of the last routed snapshot
-    const Snapshot* owner_of = nullptr;
-    uint64_t owner_version = ~0ull;
+    // owner part per row id (int16, -1 = every part) of the last routed snapshot (its uid, version,
+    // partitioning: a snapshot freed and another allocated at its address is not mistaken for it)
+    uint64_t owner_uid = 0, owner_version = ~0ull, owner_layout = ~0ull;
     DBuf owner;
     ~keto_comm() {
         (void)hipSetDevice(device);
@@ -371,14 +371,16 @@ void shard(uint32_t n, int rank, int world, uint32_t& lo, uint32_t& hi) {
 }
 
 const int16_t* owner_table(keto_comm& c, const Snapshot& S) {
-    if (c.owner_of != &S || c.owner_version != S.version) {
+    const uint64_t layout = ((uint64_t)S.part_mode << 40) | ((uint64_t)S.n_parts << 20) | S.part;
+    if (c.owner_uid != S.uid || c.owner_version != S.version || c.owner_layout != layout) {
         const uint32_t R = S.n_rows();
         std::vector<int16_t> own(std::max<uint32_t>(R, 1), -1);
         for (uint32_t r = 0; r < R; ++r) own[r] = (int16_t)S.row_owner(r, S.n_parts);
         int16_t* d = c.owner.get<int16_t>(own.size());
         HIP_OK(hipMemcpy(d, own.data(), own.size() * 2, hipMemcpyHostToDevice));
-        c.owner_of = &S;
+        c.owner_uid = S.uid;
         c.owner_version = S.version;
+        c.owner_layout = layout;
     }
     return static_cast<const int16_t*>(c.owner.p);
 }

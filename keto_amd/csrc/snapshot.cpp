@@ -43,6 +43,8 @@ struct PhaseClock {
     }
 };
 
+std::atomic<uint64_t> g_snapshot_uid{0};
+
 inline std::string_view sv(const keto_str& s) { return std::string_view(s.p ? s.p : "", s.n); }
 
 void load_namespaces(Snapshot& S, const keto_namespace* ns, uint32_t n_ns) {
@@ -255,6 +257,8 @@ void finalize_rows(Snapshot& S, const std::vector<uint64_t>& row_ptr, const std:
 }
 
 }  // namespace
+
+uint64_t next_snapshot_uid() { return ++g_snapshot_uid; }
 
 int Snapshot::key_cmp_bytes(const RowKey& a, const RowKey& b) const {
     if (a.ns != b.ns) return a.ns < b.ns ? -1 : 1;

@@ -170,7 +170,10 @@ struct ReachStateDeleter {
     void operator()(ReachState* r) const;    // reach.hip
 };
 
+uint64_t next_snapshot_uid();   // snapshot.cpp: a process-wide counter
+
 struct Snapshot {
+    const uint64_t uid = next_snapshot_uid();   // never reused (caches keyed by snapshot use it, not its address)
     // ---- config
     std::vector<int32_t> ns_ids;
     std::vector<std::string> ns_names;
