@@ -1719,6 +1719,10 @@ struct ExpandOut {
     keto_tree_node* stage;
     uint64_t stage_cap;
     uint64_t* stage_pos;
+    // the snapshot has no poisoned row: a subject set at remaining depth <= 1 is a leaf whatever its
+    // row holds (engine.go:72-75; only a failing first page would make it an error), so its row is
+    // not loaded
+    uint32_t leaf_sets_blind;
 };
 // expand kernel modes: count the trees' nodes; write them at their offsets; write them to staging
 constexpr int EXP_COUNT = 0, EXP_FILL = 1, EXP_STAGE = 2;
@@ -1749,9 +1753,37 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     // has edges (a child whose parent is exhausted returns straight to the grandparent)
     int sp = 0;
     Frame cur{0, 0, 0, 0};
+    // the current frame's window: its first WINDOW_WORDS edge words, read with the header from the
+    // same line (a main-arena row's header and window share one; the arena has slack at its end), so
+    // the edges a row holds there cost no load of their own; wbeg = their first word (~0: none held,
+    // e.g. after a pop)
+    uint4 win = make_uint4(0, 0, 0, 0);
+    uint64_t wbeg = ~0ull;
     // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union entered
     auto open = [&](uint32_t h, int k) -> int {
-        const RowView rv = load_row(s, ov, h);
+        RowView rv;
+        uint4 w4 = make_uint4(0, 0, 0, 0);
+        if (h >= ov.base) {
+            rv = load_row(s, ov, h);
+        } else {
+            uint64_t w = (uint64_t)h * HDR_WORDS;
+            uint4 v = *reinterpret_cast<const uint4*>(s.arena + w);
+            w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
+            while (v.z & HDR_FWD) {                         // a row a write moved (delta.cpp)
+                w = (uint64_t)v.x * HDR_WORDS;
+                v = *reinterpret_cast<const uint4*>(s.arena + w);
+                w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
+            }
+            rv.a = s.arena;
+            rv.beg = w + HDR_WORDS;
+            rv.n_sets = v.x;
+            rv.n_ids = v.y;
+            rv.seq = (v.z & HDR_SEQ) != 0;
+            rv.hlog2 = (v.z >> 8) & 31u;
+            rv.poison = (v.z & HDR_POISON) != 0;
+            rv.poison0 = (v.z & HDR_POISON0) != 0;
+            rv.closure = (v.z & HDR_CLOSURE) != 0;
+        }
         const uint32_t n_all = rv.n_sets + rv.n_ids;
         if (!rv.poison && n_all == 0) return EXP_NIL;
         if (rv.poison0) return EXP_ERROR;                   // the first page fails toInternal
@@ -1767,6 +1799,8 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         }
         emit(out, cnt, FILL, cap, EDGE_SET | h, n_all);
         cur = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
+        win = w4;
+        wbeg = rv.a != s.arena ? ~0ull : rv.beg;
         return EXP_TREE;
     };
     int r0 = open(root, d);
@@ -1776,10 +1810,12 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             if (sp == 0) break;
             --sp;
             cur = st[sp];
+            wbeg = ~0ull;
             continue;
         }
         const uint32_t* const a = (cur.fl & FR_OV) ? ov.arena : s.arena;
-        const uint32_t e = a[cur.pos];
+        const uint64_t wo = cur.pos - wbeg;                 // (huge when no window is held)
+        const uint32_t e = wo == 0 ? win.x : wo == 1 ? win.y : wo == 2 ? win.z : wo == 3 ? win.w : a[cur.pos];
         if (!(e & EDGE_SET) && !(cur.fl & FR_SEQ)) {
             // a normal row keeps its subject sets first: every edge left is a subject id, and each
             // is a leaf (:97-101) -- counted at once, copied in one pass
@@ -1847,7 +1883,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         const uint16_t k = cur.k - 1;
         int t = V.test_add(vid, nw);
         if (t == 2) return EXP_OVERFLOW;
-        if (t == 1) {                                       // visited -> nil -> Leaf(set)
+        if (t == 1 || (k <= 1 && o.leaf_sets_blind)) {      // visited -> nil -> Leaf(set); or :72-75
             emit(out, cnt, FILL, cap, e, 0x80000000u);
             continue;
         }
@@ -1921,22 +1957,6 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
     }
     if (FILL && o.runs) o.lane_runs[slot] = nr;
     ta.slot_epoch[slot] = V.V.epoch;
-}
-
-// The staged trees of the one-pass expand, copied to their offsets in the node arena: a wave per
-// root (grid-stride over roots), lanes over its nodes.
-__global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict__ nodes,
-                                                     const keto_tree_node* __restrict__ stage,
-                                                     const uint64_t* __restrict__ stage_pos,
-                                                     const uint64_t* __restrict__ offset, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += waves) {
-        const uint64_t sp = stage_pos[i];
-        if (sp == NOT_STAGED) continue;
-        const uint64_t b = offset[i], c = offset[i + 1] - b;
-        for (uint64_t k = lane; k < c; k += 64) nodes[b + k] = stage[sp + k];
-    }
 }
 
 // The queued id runs of a fill pass.  A run queued twice (a root that overflowed a tier and was
@@ -2767,7 +2787,8 @@ void device_apply(Snapshot& S) {
     const uint64_t need = S.n_units * HDR_WORDS;
     if (need > (2ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^33 words (32 GiB)"};
     if (need > D.arena_words) {
-        const uint64_t cap = std::min<uint64_t>(2ull << 32, std::max<uint64_t>(need, D.arena_words + D.arena_words / 4));
+        // (slack past the last row: the kernels read a header's 32-B slot, window included)
+        const uint64_t cap = std::min<uint64_t>(2ull << 32, std::max<uint64_t>(need + 1024, D.arena_words + D.arena_words / 4));
         uint64_t acc = 0;
         uint32_t* na = dmalloc<uint32_t>(cap, acc);
         HIP_OK(hipMemcpy(na, D.arena, D.arena_words * sizeof(uint32_t), hipMemcpyDeviceToDevice));
@@ -3763,32 +3784,49 @@ __global__ void __launch_bounds__(256) scatter_unit_rows(uint32_t* __restrict__ 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) unit_row[units[i]] = rows[i];
 }
-__global__ void __launch_bounds__(256) handles_to_rows_direct(keto_tree_node* __restrict__ nodes, uint64_t n,
-                                                              const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t x = nodes[i].subject;
-    if (!(x & EDGE_SET)) return;
-    const uint32_t h = x & EDGE_VAL;
-    if (h >= ov_units_base) return;
-    nodes[i].subject = EDGE_SET | unit_row[h];
-}
-__global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restrict__ nodes, uint64_t n,
-                                                       const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
-                                                       uint32_t n_rows, uint32_t ov_units_base) {
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t x = nodes[i].subject;
-    if (!(x & EDGE_SET)) return;
-    const uint32_t h = x & EDGE_VAL;
-    if (h >= ov_units_base) return;
-    uint32_t lo = 0, hi = n_rows;                  // first unit >= h
-    while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (units[m] < h) lo = m + 1;
-        else hi = m;
+// The last pass of an expand batch, a wave per root: a staged tree is copied from its lane's staging
+// region to its offset in the node arena, a tree filled in place is read there, and on the way every
+// set node's row handle becomes its row id (the direct handle -> row map, else a binary search over
+// the arena-order handle list).  One pass over the nodes instead of a gather and a translation pass.
+template <bool DIRECT>
+__global__ void __launch_bounds__(256) finish_trees(keto_tree_node* __restrict__ nodes,
+                                                    const keto_tree_node* __restrict__ stage,
+                                                    const uint64_t* __restrict__ stage_pos,
+                                                    const uint64_t* __restrict__ offset, uint32_t n,
+                                                    const uint32_t* __restrict__ unit_row,
+                                                    const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
+                                                    uint32_t n_map, uint32_t ov_units_base) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += waves) {
+        const uint64_t b = offset[i], c = offset[i + 1] - b;
+        if (c == 0) continue;
+        const uint64_t sp = stage_pos ? stage_pos[i] : NOT_STAGED;
+        const bool staged = sp != NOT_STAGED;
+        const keto_tree_node* src = staged ? stage + sp : nodes + b;
+        for (uint64_t k = lane; k < c; k += 64) {
+            keto_tree_node x = src[k];
+            const uint32_t h = x.subject & EDGE_VAL;
+            if ((x.subject & EDGE_SET) && h < ov_units_base) {
+                uint32_t r;
+                if constexpr (DIRECT) {
+                    r = unit_row[h];
+                } else {
+                    uint32_t lo = 0, hi = n_map;                  // first unit >= h
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (units[m] < h) lo = m + 1;
+                        else hi = m;
+                    }
+                    r = rows[lo];
+                }
+                x.subject = EDGE_SET | r;
+            } else if (!staged) {
+                continue;                                         // in place: nothing changes
+            }
+            nodes[b + k] = x;
+        }
     }
-    nodes[i].subject = EDGE_SET | rows[lo];
 }
 
 // ---- the pinned block pool behind PinnedAlloc (snapshot.hpp); never destroyed, so an arena freed
@@ -4011,8 +4049,9 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     // pass 1: count (and stage), then the staged trees' queued id runs
     HIP_OK(hipMemsetAsync(dstage, 0xFF, (uint64_t)n * sizeof(uint64_t), st));
     if (staged) big_queue(stage_cap * p.slots[0]);
+    const uint32_t blind = S.n_poisoned_rows == 0 && getenv("KETO_EXPAND_LOAD_LEAVES") == nullptr;
     launch_pass(false, ExpandOut{nullptr, nullptr, dcount, dstatus, staged ? D.ex_runs : nullptr, d_lane_runs,
-                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage});
+                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, blind});
     float extra_ms = 0;
     if (staged) {
         HIP_OK(hipEventRecord(D.ex_ev[0], st));
@@ -4073,24 +4112,24 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (unstaged) {
         big_queue(total);
         launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_lane_runs, run_inline, D.ex_big,
-                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr});
+                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, blind});
     }
     HIP_OK(hipEventRecord(D.ex_ev[2], st));
     if (unstaged) copy_queued();
-    if (staged)
-        hipLaunchKernelGGL(gather_staged, dim3((unsigned)std::min<uint64_t>((n + 3) / 4, 16384)), dim3(256), 0, st,
-                           D.ex_nodes, D.ex_stage, dstage, doff, n);
+    // the staged trees to their offsets and every tree's set handles to row ids, in one pass
+    {
+        const dim3 grid((unsigned)std::min<uint64_t>((n + 3) / 4, 16384));
+        const uint64_t* sp = staged ? dstage : nullptr;
+        if (D.unit_row)
+            hipLaunchKernelGGL(finish_trees<true>, grid, dim3(256), 0, st, D.ex_nodes, D.ex_stage, sp, doff, n, D.unit_row,
+                               nullptr, nullptr, 0u, (uint32_t)S.n_units);
+        else
+            hipLaunchKernelGGL(finish_trees<false>, grid, dim3(256), 0, st, D.ex_nodes, D.ex_stage, sp, doff, n, nullptr,
+                               D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(D.ex_ev[3], st));
-    lap("fill");
-    if (D.unit_row)
-        hipLaunchKernelGGL(handles_to_rows_direct, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes,
-                           total, D.unit_row, (uint32_t)S.n_units);
-    else
-        hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
-                           D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
-    HIP_OK(hipGetLastError());
-    lap("h2rows");
+    lap("fill+finish");
     HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     lap("d2h");
