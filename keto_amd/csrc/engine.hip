@@ -191,6 +191,30 @@ struct Work<true> {
     }
 };
 // ------------------------------------------------------------------ visited maps
+// Probe sequence of the hashed maps: 32-B buckets of four entries (epoch << 32 | visit id), read
+// with two 16-B loads from one line, bucket after bucket; the entries of a bucket are taken in
+// order.  Entries are never removed, so an id is always found before the first empty entry of its
+// sequence.  A deep search's map lives mostly here (tens of thousands of ids at depth 32), so a
+// test is one line round trip instead of a dependent chain of 8-B probes.  Returns 1 if vid is
+// present; else 0 and *slot = the first empty entry.
+__device__ inline int probe_bucketed(const uint64_t* tab, uint32_t mask, uint32_t epoch, uint32_t vid, uint32_t* slot) {
+    uint32_t i = mix32(vid) & mask & ~3u;
+    for (;;) {
+        const uint4 a = *reinterpret_cast<const uint4*>(tab + i);
+        const uint4 b = *reinterpret_cast<const uint4*>(tab + i + 2);
+        const uint32_t lo[4] = {a.x, a.z, b.x, b.z}, hi[4] = {a.y, a.w, b.y, b.w};
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            if (hi[k] != epoch) {
+                *slot = i + k;
+                return 0;
+            }
+            if (lo[k] == vid) return 1;
+        }
+        i = (i + 4) & mask;
+    }
+}
+
 struct Visited {
     uint64_t* tab;
     uint32_t mask;
@@ -207,8 +231,17 @@ struct Visited {
     // 0 = newly added, 1 = already present, 2 = table too full (request must move up a tier)
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
-        uint32_t i = mix32(vid) & mask;
         const uint64_t want = ((uint64_t)epoch << 32) | vid;
+        if (mask >= 3) {                   // tables of >= 4 entries (every tier's): bucketed
+            uint32_t at = 0;
+            w.vprobe();
+            if (probe_bucketed(tab, mask, epoch, vid, &at)) return 1;
+            if ((++count) * 2u > mask + 1u) return 2;
+            tab[at] = want;
+            w.vinsert();
+            return 0;
+        }
+        uint32_t i = mix32(vid) & mask;
         for (;;) {
             uint64_t e = tab[i];
             w.vprobe();
@@ -220,6 +253,19 @@ struct Visited {
             }
             if (e == want) return 1;
             i = (i + 1) & mask;
+        }
+    }
+    // read-only membership (a borrowing map's earlier ids)
+    __device__ inline bool has(uint32_t vid) const {
+        if (mask >= 3) {
+            uint32_t at = 0;
+            return probe_bucketed(tab, mask, epoch, vid, &at) == 1;
+        }
+        const uint64_t want = ((uint64_t)epoch << 32) | vid;
+        for (uint32_t i = mix32(vid) & mask;; i = (i + 1) & mask) {
+            const uint64_t e = tab[i];
+            if ((uint32_t)(e >> 32) != epoch) return false;
+            if (e == want) return true;
         }
     }
     __device__ inline void release() {}
@@ -346,15 +392,8 @@ struct PromoVisited {
             if (t != 2 || pool_n == 0 || !borrow()) return t;
             live = true;                             // vid is in neither table: add it below
         } else if (live) {
-            uint32_t i = mix32(vid) & mask;          // earlier ids of this map (table <= half full)
-            const uint64_t want = ((uint64_t)epoch << 32) | vid;
-            for (;;) {
-                const uint64_t e = tab[i];
-                w.vprobe();
-                if ((uint32_t)(e >> 32) != epoch) break;
-                if (e == want) return 1;
-                i = (i + 1) & mask;
-            }
+            w.vprobe();                              // earlier ids of this map (table <= half full)
+            if (hashed().has(vid)) return 1;
         }
         BT B = borrowed();
         const int t = B.test_add(vid, w);
@@ -1723,6 +1762,10 @@ struct ExpandOut {
     // row holds (engine.go:72-75; only a failing first page would make it an error), so its row is
     // not loaded
     uint32_t leaf_sets_blind;
+    // entering a union, start the header loads of the subject sets in its window (the children it will
+    // open) at once: global_load_lds into a per-wave scratch word (no register, no wait), so the
+    // lines are in the caches when the walk reaches those children one after another
+    uint32_t prefetch;
 };
 // expand kernel modes: count the trees' nodes; write them at their offsets; write them to staging
 constexpr int EXP_COUNT = 0, EXP_FILL = 1, EXP_STAGE = 2;
@@ -1740,7 +1783,7 @@ __device__ inline void emit(keto_tree_node* out, uint64_t& cnt, bool fill, uint6
 template <bool FILL, class Stack, class VT>
 __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
                           uint32_t root_vid, int d, VT& V, keto_tree_node* out, uint64_t& cnt, uint64_t cap,
-                          Stack& st, const ExpandOut& o, uint32_t& nr, uint64_t& qend) {
+                          Stack& st, const ExpandOut& o, uint32_t& nr, uint64_t& qend, uint32_t* pf_lds) {
     if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
         emit(out, cnt, FILL, cap, root, 0x80000000u);
         return EXP_TREE;
@@ -1801,6 +1844,16 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         cur = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
         win = w4;
         wbeg = rv.a != s.arena ? ~0ull : rv.beg;
+        if (o.prefetch && wbeg != ~0ull && (k - 1 >= 2 || !o.leaf_sets_blind)) {
+            // the window's subject sets (set edges always target main-arena rows)
+#pragma unroll
+            for (uint32_t j = 0; j < WINDOW_WORDS; ++j) {
+                const uint32_t e = win_at(w4, j);
+                if (j < n_all && (e & EDGE_SET))
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(s.arena + (uint64_t)(e & EDGE_VAL) * HDR_WORDS),
+                                                     reinterpret_cast<void*>(pf_lds), 4, 0, 0);
+            }
+        }
         return EXP_TREE;
     };
     int r0 = open(root, d);
@@ -1910,6 +1963,7 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
     // a tree's map: its first REG_VIDS + LDS_VIDS sets in registers and the lane's LDS column (one
     // tree at max-depth 5 marks a handful of sets), the rest in the lane's HBM table
     __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
+    __shared__ uint32_t lds_pf[256];                          // the waves' prefetch scratch (never read)
     VisitedRS<LDS_VIDS, Visited> V;
     V.n = 0;
     V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
@@ -1938,7 +1992,8 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         keto_tree_node* out = !FILL ? nullptr : STAGE ? o.stage + stage0 + used : o.nodes + o.offset[i];
         const uint64_t cap = STAGE ? o.stage_cap - used : ~0ull;
         uint64_t qend = 0;
-        int r = expand_one<FILL, Stack>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, st, o, nr, qend);
+        int r = expand_one<FILL, Stack>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, st, o, nr, qend,
+                                        lds_pf + (threadIdx.x & ~63u));
         const bool staged = STAGE && r == EXP_TREE && cnt <= cap;
         // a tree not staged (too big, or left to the next tier) may have queued runs into the region:
         // that part stays dead, so the copies cannot land on the next tree
@@ -1957,6 +2012,22 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
     }
     if (FILL && o.runs) o.lane_runs[slot] = nr;
     ta.slot_epoch[slot] = V.V.epoch;
+}
+
+// The staged trees of the one-pass expand, copied to their offsets in the node arena: a wave per
+// root (grid-stride over roots), lanes over its nodes.
+__global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict__ nodes,
+                                                     const keto_tree_node* __restrict__ stage,
+                                                     const uint64_t* __restrict__ stage_pos,
+                                                     const uint64_t* __restrict__ offset, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += waves) {
+        const uint64_t sp = stage_pos[i];
+        if (sp == NOT_STAGED) continue;
+        const uint64_t b = offset[i], c = offset[i + 1] - b;
+        for (uint64_t k = lane; k < c; k += 64) nodes[b + k] = stage[sp + k];
+    }
 }
 
 // The queued id runs of a fill pass.  A run queued twice (a root that overflowed a tier and was
@@ -3784,49 +3855,32 @@ __global__ void __launch_bounds__(256) scatter_unit_rows(uint32_t* __restrict__ 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) unit_row[units[i]] = rows[i];
 }
-// The last pass of an expand batch, a wave per root: a staged tree is copied from its lane's staging
-// region to its offset in the node arena, a tree filled in place is read there, and on the way every
-// set node's row handle becomes its row id (the direct handle -> row map, else a binary search over
-// the arena-order handle list).  One pass over the nodes instead of a gather and a translation pass.
-template <bool DIRECT>
-__global__ void __launch_bounds__(256) finish_trees(keto_tree_node* __restrict__ nodes,
-                                                    const keto_tree_node* __restrict__ stage,
-                                                    const uint64_t* __restrict__ stage_pos,
-                                                    const uint64_t* __restrict__ offset, uint32_t n,
-                                                    const uint32_t* __restrict__ unit_row,
-                                                    const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
-                                                    uint32_t n_map, uint32_t ov_units_base) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += waves) {
-        const uint64_t b = offset[i], c = offset[i + 1] - b;
-        if (c == 0) continue;
-        const uint64_t sp = stage_pos ? stage_pos[i] : NOT_STAGED;
-        const bool staged = sp != NOT_STAGED;
-        const keto_tree_node* src = staged ? stage + sp : nodes + b;
-        for (uint64_t k = lane; k < c; k += 64) {
-            keto_tree_node x = src[k];
-            const uint32_t h = x.subject & EDGE_VAL;
-            if ((x.subject & EDGE_SET) && h < ov_units_base) {
-                uint32_t r;
-                if constexpr (DIRECT) {
-                    r = unit_row[h];
-                } else {
-                    uint32_t lo = 0, hi = n_map;                  // first unit >= h
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (units[m] < h) lo = m + 1;
-                        else hi = m;
-                    }
-                    r = rows[lo];
-                }
-                x.subject = EDGE_SET | r;
-            } else if (!staged) {
-                continue;                                         // in place: nothing changes
-            }
-            nodes[b + k] = x;
-        }
+__global__ void __launch_bounds__(256) handles_to_rows_direct(keto_tree_node* __restrict__ nodes, uint64_t n,
+                                                              const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = nodes[i].subject;
+    if (!(x & EDGE_SET)) return;
+    const uint32_t h = x & EDGE_VAL;
+    if (h >= ov_units_base) return;
+    nodes[i].subject = EDGE_SET | unit_row[h];
+}
+__global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restrict__ nodes, uint64_t n,
+                                                       const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
+                                                       uint32_t n_rows, uint32_t ov_units_base) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = nodes[i].subject;
+    if (!(x & EDGE_SET)) return;
+    const uint32_t h = x & EDGE_VAL;
+    if (h >= ov_units_base) return;
+    uint32_t lo = 0, hi = n_rows;                  // first unit >= h
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (units[m] < h) lo = m + 1;
+        else hi = m;
     }
+    nodes[i].subject = EDGE_SET | rows[lo];
 }
 
 // ---- the pinned block pool behind PinnedAlloc (snapshot.hpp); never destroyed, so an arena freed
@@ -4033,9 +4087,14 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                   },
                   Undecided{dstatus, fill ? nullptr : dcount, (uint8_t)EXP_OVERFLOW}, fill);
     };
+    // grids of the grid-stride copy kernels (a wave per lane / per root): capped, so that a launch is
+    // not mostly the dispatch of waves with nothing to copy; KETO_EXPAND_COPY_BLOCKS overrides (tuning)
+    const char* cbe = getenv("KETO_EXPAND_COPY_BLOCKS");
+    const uint32_t cb_cap = cbe ? (uint32_t)std::max(1, atoi(cbe)) : 16384u;
+    auto copy_blocks = [&](uint64_t want) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cb_cap)); };
     uint32_t* d_nbig = nullptr;
     auto copy_queued = [&]() {
-        hipLaunchKernelGGL(copy_lane_runs, dim3((p.slots[0] + 3) / 4), dim3(256), 0, st,
+        hipLaunchKernelGGL(copy_lane_runs, dim3(copy_blocks((p.slots[0] + 3) / 4)), dim3(256), 0, st,
                            D.ex_runs, d_lane_runs, p.slots[0]);
         hipLaunchKernelGGL(copy_big_runs, dim3(std::min<uint32_t>((D.ex_big_cap + 3) / 4, 4096)), dim3(256), 0, st,
                            D.ex_big, d_nbig, D.ex_big_cap);
@@ -4050,8 +4109,10 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     HIP_OK(hipMemsetAsync(dstage, 0xFF, (uint64_t)n * sizeof(uint64_t), st));
     if (staged) big_queue(stage_cap * p.slots[0]);
     const uint32_t blind = S.n_poisoned_rows == 0 && getenv("KETO_EXPAND_LOAD_LEAVES") == nullptr;
+    const char* pfe = getenv("KETO_EXPAND_PREFETCH");
+    const uint32_t pf = pfe ? (uint32_t)(atoi(pfe) != 0) : 1u;
     launch_pass(false, ExpandOut{nullptr, nullptr, dcount, dstatus, staged ? D.ex_runs : nullptr, d_lane_runs,
-                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, blind});
+                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, blind, pf});
     float extra_ms = 0;
     if (staged) {
         HIP_OK(hipEventRecord(D.ex_ev[0], st));
@@ -4112,24 +4173,26 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (unstaged) {
         big_queue(total);
         launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_lane_runs, run_inline, D.ex_big,
-                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, blind});
+                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, blind, pf});
     }
     HIP_OK(hipEventRecord(D.ex_ev[2], st));
     if (unstaged) copy_queued();
-    // the staged trees to their offsets and every tree's set handles to row ids, in one pass
-    {
-        const dim3 grid((unsigned)std::min<uint64_t>((n + 3) / 4, 16384));
-        const uint64_t* sp = staged ? dstage : nullptr;
-        if (D.unit_row)
-            hipLaunchKernelGGL(finish_trees<true>, grid, dim3(256), 0, st, D.ex_nodes, D.ex_stage, sp, doff, n, D.unit_row,
-                               nullptr, nullptr, 0u, (uint32_t)S.n_units);
-        else
-            hipLaunchKernelGGL(finish_trees<false>, grid, dim3(256), 0, st, D.ex_nodes, D.ex_stage, sp, doff, n, nullptr,
-                               D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
-    }
+    if (staged)
+        hipLaunchKernelGGL(gather_staged, dim3(copy_blocks((n + 3) / 4)), dim3(256), 0, st,
+                           D.ex_nodes, D.ex_stage, dstage, doff, n);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(D.ex_ev[3], st));
-    lap("fill+finish");
+    lap("fill");
+    // set handles -> row ids, a thread per node (a wave-per-tree pass, fused with the gather, was 2.5x
+    // slower: its random gathers into the 4-B-per-unit map wait one after another per wave)
+    if (D.unit_row)
+        hipLaunchKernelGGL(handles_to_rows_direct, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes,
+                           total, D.unit_row, (uint32_t)S.n_units);
+    else
+        hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
+                           D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
+    HIP_OK(hipGetLastError());
+    lap("h2rows");
     HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     lap("d2h");
