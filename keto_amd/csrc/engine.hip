@@ -2014,56 +2014,59 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
     ta.slot_epoch[slot] = V.V.epoch;
 }
 
-// The staged trees of the one-pass expand, copied to their offsets in the node arena: a wave per
-// root (grid-stride over roots), lanes over its nodes.
+// The staged trees of the one-pass expand, copied to their offsets in the node arena: 16 lanes per
+// root (four roots per wave, grid-stride), whose position and offsets are loaded together (a tree
+// is ~37 nodes on average: a wave per root waited three dependent loads for one short copy).
 __global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict__ nodes,
                                                      const keto_tree_node* __restrict__ stage,
                                                      const uint64_t* __restrict__ stage_pos,
                                                      const uint64_t* __restrict__ offset, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += waves) {
-        const uint64_t sp = stage_pos[i];
+    const uint32_t gl = threadIdx.x & 15u;
+    const uint32_t groups = gridDim.x * (blockDim.x >> 4);
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; i < n; i += groups) {
+        const uint64_t sp = stage_pos[i], b = offset[i], e = offset[i + 1];
         if (sp == NOT_STAGED) continue;
-        const uint64_t b = offset[i], c = offset[i + 1] - b;
-        for (uint64_t k = lane; k < c; k += 64) nodes[b + k] = stage[sp + k];
+        for (uint64_t k = gl; k < e - b; k += 16) nodes[b + k] = stage[sp + k];
     }
 }
 
 // The queued id runs of a fill pass.  A run queued twice (a root that overflowed a tier and was
 // filled again on the next) is copied twice, to the same bytes.
-//   copy_lane_runs: a wave per tier-0 lane; its runs' ids are laid end to end and the wave copies 64
-//     of them per round (lane k: flat position base + k, its run found by a search over the runs'
-//     exclusive prefix, read across lanes)
+//   copy_lane_runs: half a wave per tier-0 lane (one queue entry per thread: RUNS_PER_LANE = 32);
+//     its runs' ids are laid end to end and the half-wave copies 32 of them per round (thread k:
+//     flat position base + k, its run found by a search over the runs' exclusive prefix, read
+//     across the half-wave)
 //   copy_big_runs: a wave per BIG_RUN-id piece
+static_assert(RUNS_PER_LANE == 32, "copy_lane_runs holds one queue entry per thread of a half-wave");
 __global__ void __launch_bounds__(256) copy_lane_runs(const CopyRun* __restrict__ runs,
                                                       const uint32_t* __restrict__ lane_runs, uint32_t lanes) {
-    const int lane = (int)(threadIdx.x & 63u);
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < lanes; l += waves) {
+    constexpr int G = 32;
+    const int t = (int)(threadIdx.x & (G - 1));
+    const uint32_t groups = gridDim.x * (blockDim.x / G);
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) / G; l < lanes; l += groups) {
         const uint32_t m = lane_runs[l];
         if (m == 0) continue;
         CopyRun c{nullptr, nullptr, 0};
-        if ((uint32_t)lane < m) c = runs[(uint64_t)l * RUNS_PER_LANE + lane];
-        const uint32_t len = (uint32_t)lane < m ? (uint32_t)c.len : 0u;
+        if ((uint32_t)t < m) c = runs[(uint64_t)l * RUNS_PER_LANE + t];
+        const uint32_t len = (uint32_t)t < m ? (uint32_t)c.len : 0u;
         uint32_t incl = len;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
+        for (int off = 1; off < G; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, G);
+            if (t >= off) incl += y;
         }
-        const uint32_t total = __shfl(incl, 63);
+        const uint32_t total = __shfl(incl, G - 1, G);
         const uint32_t excl = incl - len;
         const uint64_t src = (uint64_t)c.src, dst = (uint64_t)c.dst;
-        for (uint32_t base = 0; base < total; base += 64) {     // every lane takes part in the shuffles
-            const uint32_t f = base + (uint32_t)lane;
+        for (uint32_t base = 0; base < total; base += G) {      // every thread takes part in the shuffles
+            const uint32_t f = base + (uint32_t)t;
             int j = 0;
-            for (int step = 16; step > 0; step >>= 1) {
-                const uint32_t e = __shfl(excl, j + step < 64 ? j + step : 63);
-                if ((uint32_t)(j + step) < m && e <= f) j += step;
+            for (int step = G / 2; step > 0; step >>= 1) {
+                const uint32_t ev = __shfl(excl, j + step < G ? j + step : G - 1, G);
+                if ((uint32_t)(j + step) < m && ev <= f) j += step;
             }
-            const uint32_t ej = __shfl(excl, j);
-            const uint32_t slo = __shfl((uint32_t)src, j), shi = __shfl((uint32_t)(src >> 32), j);
-            const uint32_t dlo = __shfl((uint32_t)dst, j), dhi = __shfl((uint32_t)(dst >> 32), j);
+            const uint32_t ej = __shfl(excl, j, G);
+            const uint32_t slo = __shfl((uint32_t)src, j, G), shi = __shfl((uint32_t)(src >> 32), j, G);
+            const uint32_t dlo = __shfl((uint32_t)dst, j, G), dhi = __shfl((uint32_t)(dst >> 32), j, G);
             if (f < total) {
                 const uint32_t* sp = reinterpret_cast<const uint32_t*>(((uint64_t)shi << 32) | slo);
                 keto_tree_node* dp = reinterpret_cast<keto_tree_node*>(((uint64_t)dhi << 32) | dlo);
@@ -4007,8 +4010,11 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     const bool staged = !se || atoi(se) != 0;
     uint64_t stage_cap = 0;
     if (staged) {
-        const uint64_t budget = 1ull << 29;                               // staging nodes (4 GiB)
-        stage_cap = std::min<uint64_t>(16384, std::max<uint64_t>(64, budget / p.slots[0]));
+        // staging nodes: 8 GiB (config #5's 100k roots get 10.7K-node regions; 2 trees of 100k need
+        // the second pass), KETO_EXPAND_STAGE_GIB overrides
+        const char* sg = getenv("KETO_EXPAND_STAGE_GIB");
+        const uint64_t budget = (sg ? (uint64_t)std::max(1, atoi(sg)) : 8ull) << 27;
+        stage_cap = std::min<uint64_t>(32768, std::max<uint64_t>(64, budget / p.slots[0]));
         if (se && atoi(se) > 1) stage_cap = (uint64_t)atoi(se);            // tests: small regions spill
         const uint64_t nodes = stage_cap * p.slots[0];
         if (D.ex_stage_nodes < nodes) {
@@ -4094,9 +4100,10 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     auto copy_blocks = [&](uint64_t want) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, cb_cap)); };
     uint32_t* d_nbig = nullptr;
     auto copy_queued = [&]() {
-        hipLaunchKernelGGL(copy_lane_runs, dim3(copy_blocks((p.slots[0] + 3) / 4)), dim3(256), 0, st,
+        hipLaunchKernelGGL(copy_lane_runs, dim3(copy_blocks((p.slots[0] + 7) / 8)), dim3(256), 0, st,
                            D.ex_runs, d_lane_runs, p.slots[0]);
-        hipLaunchKernelGGL(copy_big_runs, dim3(std::min<uint32_t>((D.ex_big_cap + 3) / 4, 4096)), dim3(256), 0, st,
+        // (usually empty: a small grid-stride grid, not a wave per possible piece)
+        hipLaunchKernelGGL(copy_big_runs, dim3(std::min<uint32_t>((D.ex_big_cap + 3) / 4, 512)), dim3(256), 0, st,
                            D.ex_big, d_nbig, D.ex_big_cap);
         HIP_OK(hipGetLastError());
     };
@@ -4178,7 +4185,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     HIP_OK(hipEventRecord(D.ex_ev[2], st));
     if (unstaged) copy_queued();
     if (staged)
-        hipLaunchKernelGGL(gather_staged, dim3(copy_blocks((n + 3) / 4)), dim3(256), 0, st,
+        hipLaunchKernelGGL(gather_staged, dim3(copy_blocks((n + 15) / 16)), dim3(256), 0, st,
                            D.ex_nodes, D.ex_stage, dstage, doff, n);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(D.ex_ev[3], st));
