@@ -4010,11 +4010,13 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     const bool staged = !se || atoi(se) != 0;
     uint64_t stage_cap = 0;
     if (staged) {
-        // staging nodes: 8 GiB (config #5's 100k roots get 10.7K-node regions; 2 trees of 100k need
-        // the second pass), KETO_EXPAND_STAGE_GIB overrides
-        const char* sg = getenv("KETO_EXPAND_STAGE_GIB");
-        const uint64_t budget = (sg ? (uint64_t)std::max(1, atoi(sg)) : 8ull) << 27;
-        stage_cap = std::min<uint64_t>(32768, std::max<uint64_t>(64, budget / p.slots[0]));
+        // staging nodes: KETO_EXPAND_STAGE_MB (default 1024 MB).  Bigger regions let fewer trees
+        // spill to the second pass, but the lanes' regions then lie far apart and the copies into and
+        // out of them miss the TLB page by page: the gather of config #5's 100k staged trees took
+        // 34 us from 4 GiB of regions, 143 us from 8 GiB and 298 us from 16 GiB
+        const char* sg = getenv("KETO_EXPAND_STAGE_MB");
+        const uint64_t budget = (sg ? (uint64_t)std::max(16, atoi(sg)) : 1024ull) << 17;
+        stage_cap = std::min<uint64_t>(16384, std::max<uint64_t>(64, budget / p.slots[0]));
         if (se && atoi(se) > 1) stage_cap = (uint64_t)atoi(se);            // tests: small regions spill
         const uint64_t nodes = stage_cap * p.slots[0];
         if (D.ex_stage_nodes < nodes) {

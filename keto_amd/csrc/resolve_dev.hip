@@ -1,0 +1,399 @@
+// Check requests resolved on the GPU: the role of whereQuery (internal/persistence/sql/
+// relationtuples.go:178-198) for every request of a batch, on the device, against the snapshot's
+// string and row indexes uploaded once per version -- instead of on host threads (resolve.cpp),
+// where a request costs ~6 dependent host-memory misses (16.7M requests: 175-195 ms on 16 EPYC
+// threads, profiles/r03d_resolve.log).
+//
+// The batch comes packed (keto_check_batch_packed, include/keto_mi355x.h): every request's
+// strings back to back in one buffer -- the Go batcher already copies a batch's strings into one C
+// arena -- and a 24-B record per request with their offset and lengths.  The library copies both to
+// the device, and one thread per request:
+//   namespace name -> config namespace id      (a compare over the few configured names)
+//   object, relation, subject id -> string ids (the host's open-addressing string index, same hash
+//                                               and 16-B slots: length + first 11 bytes verify a
+//                                               short string in the slot; a longer one compares its
+//                                               bytes; strings a write added: a second table)
+//   (namespace, object, relation) -> row id    (the real-row index; empty rows subject sets point
+//                                               at and rows a write added: a second table)
+//   subject set -> its row id (the target), flags
+// exactly as Snapshot::resolve_query / resolve_general do; the row-id requests then go through
+// device_check_rows (row ids -> handles, the check).  A request with an empty namespace, object or
+// relation (a wildcard query, also in its subject set) is left to the host path (check_named: it
+// may need a batch-local row); so is a field longer than 65535 bytes, which the record cannot
+// hold (the caller passes those through keto_check_batch).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "parallel.hpp"
+#include "snapshot.hpp"
+
+namespace keto {
+
+namespace {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t err__ = (x);                                                                     \
+        if (err__ != hipSuccess)                                                                    \
+            throw Error{KETO_E_HIP, std::string(#x) + ": " + hipGetErrorString(err__)};             \
+    } while (0)
+
+struct RBuf {                      // grow-only device buffer
+    void* p = nullptr;
+    uint64_t cap = 0;
+    RBuf() = default;
+    RBuf(const RBuf&) = delete;
+    RBuf& operator=(const RBuf&) = delete;
+    template <class T>
+    T* get(uint64_t n) {
+        const uint64_t want = std::max<uint64_t>(64, n * sizeof(T));
+        if (want > cap) {
+            release();
+            const uint64_t c = std::max<uint64_t>(want, cap + cap / 4);
+            const hipError_t e = hipMalloc(&p, c);
+            if (e != hipSuccess) {
+                p = nullptr;
+                throw Error{KETO_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+            }
+            cap = c;
+        }
+        return static_cast<T*>(p);
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    ~RBuf() { release(); }
+};
+
+using StrSlot = Snapshot::StrSlot;
+using RowSlot = Snapshot::RowSlot;
+constexpr uint32_t INLINE = sizeof(StrSlot::b);
+constexpr uint8_t ST_HOST = 0xFF;                   // resolved on the host (wildcards)
+
+// ---- hashing, mirrored bit for bit from parallel.hpp (hash_bytes, mix64) and resolve.cpp (row_hash)
+__device__ inline uint64_t d_mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__device__ inline uint64_t d_load(const uint8_t* p, int n) {        // n little-endian bytes
+    uint64_t w = 0;
+    for (int i = 0; i < n; ++i) w |= (uint64_t)p[i] << (8 * i);
+    return w;
+}
+__device__ inline uint64_t d_hash_bytes(const uint8_t* p, uint32_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xC2B2AE3D27D4EB4Full);
+    uint64_t a, b;
+    if (n <= 16) {
+        if (n >= 8) {
+            a = d_load(p, 8);
+            b = d_load(p + n - 8, 8);
+        } else if (n >= 4) {
+            a = d_load(p, 4);
+            b = d_load(p + n - 4, 4);
+        } else if (n > 0) {
+            a = (uint64_t)p[0] | (uint64_t)p[n / 2] << 8 | (uint64_t)p[n - 1] << 16;
+            b = 0;
+        } else {
+            a = b = 0;
+        }
+        return d_mix64(d_mix64(h ^ a) * 0x9E3779B97F4A7C15ull ^ b);
+    }
+    uint32_t i = 0;
+    for (; i + 8 < n; i += 8) h = d_mix64(h ^ d_load(p + i, 8)) * 0x9E3779B97F4A7C15ull;
+    return d_mix64(h ^ d_load(p + n - 8, 8));
+}
+__host__ __device__ inline uint64_t row_hash_hd(int64_t ns, uint32_t obj, uint32_t rel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return d_mix64((uint64_t)ns * 0x9E3779B97F4A7C15ull ^ d_mix64(((uint64_t)obj << 32) | rel));
+#else
+    return mix64((uint64_t)ns * 0x9E3779B97F4A7C15ull ^ mix64(((uint64_t)obj << 32) | rel));
+#endif
+}
+
+struct StrIndex {                  // an open-addressing string table and the bytes behind it
+    const StrSlot* slot;
+    uint64_t mask;                 // 0 with slot == nullptr: empty
+    const uint8_t* bytes;          // every string of the snapshot back to back (id order)
+    const uint64_t* off;
+};
+struct RowIndex {
+    const RowSlot* slot;
+    uint64_t mask;
+};
+struct ResolveDev {
+    StrIndex base, added;          // the build's strings; strings writes added (after the build's)
+    RowIndex real, extra;          // the build's real rows; empty rows and rows writes added
+    const uint8_t* ns_bytes;       // configured namespace names back to back (config order)
+    const uint64_t* ns_off;
+    const int32_t* ns_id;
+    uint32_t n_ns;
+};
+
+__device__ inline bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+__device__ int64_t find_str_dev(const StrIndex& T, const uint8_t* s, uint32_t n, uint64_t h) {
+    if (!T.slot) return -1;
+    const uint8_t n8 = (uint8_t)min(n, 255u);
+    for (uint64_t j = h & T.mask;; j = (j + 1) & T.mask) {
+        const StrSlot x = T.slot[j];
+        if (!x.id1) return -1;
+        if (x.n != n8) continue;
+        if (!bytes_eq(reinterpret_cast<const uint8_t*>(x.b), s, min(n, INLINE))) continue;
+        if (n <= INLINE) return x.id1 - 1;
+        const uint64_t b = T.off[x.id1 - 1], e = T.off[x.id1];
+        if (e - b == n && bytes_eq(T.bytes + b, s, n)) return x.id1 - 1;
+    }
+}
+__device__ inline int64_t lookup_str_dev(const ResolveDev& R, const uint8_t* s, uint32_t n) {
+    const uint64_t h = d_hash_bytes(s, n);
+    const int64_t id = find_str_dev(R.base, s, n, h);
+    return id >= 0 ? id : find_str_dev(R.added, s, n, h);
+}
+__device__ int64_t find_row_dev(const RowIndex& T, int32_t ns, uint32_t obj, uint32_t rel) {
+    if (!T.slot) return -1;
+    for (uint64_t j = row_hash_hd(ns, obj, rel) & T.mask;; j = (j + 1) & T.mask) {
+        const RowSlot x = T.slot[j];
+        if (!x.row1) return -1;
+        if (x.ns == ns && x.obj == obj && x.rel == rel) return x.row1 - 1;
+    }
+}
+__device__ inline int ns_index_dev(const ResolveDev& R, const uint8_t* s, uint32_t n) {
+    for (uint32_t c = 0; c < R.n_ns; ++c) {
+        const uint64_t b = R.ns_off[c], e = R.ns_off[c + 1];
+        if (e - b == n && bytes_eq(R.ns_bytes + b, s, n)) return (int)c;
+    }
+    return -1;
+}
+// RelationQuery (namespace, object, relation), every field set -> row id; -1 none, -2 unknown namespace
+__device__ int64_t query_row_dev(const ResolveDev& R, const uint8_t* f, uint32_t l_ns, uint32_t l_obj, uint32_t l_rel) {
+    const int c = ns_index_dev(R, f, l_ns);
+    if (c < 0) return -2;                                                  // ErrNotFound
+    const int64_t o = lookup_str_dev(R, f + l_ns, l_obj);
+    if (o < 0) return -1;                                                  // no row can match an unknown string
+    const int64_t r = lookup_str_dev(R, f + l_ns + l_obj, l_rel);
+    if (r < 0) return -1;
+    const int32_t ns = R.ns_id[c];
+    const int64_t row = find_row_dev(R.real, ns, (uint32_t)o, (uint32_t)r);
+    return row >= 0 ? row : find_row_dev(R.extra, ns, (uint32_t)o, (uint32_t)r);
+}
+
+__global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_t* __restrict__ blob,
+                                                      const keto_check_packed* __restrict__ q, uint32_t n,
+                                                      keto_check_ids* __restrict__ out, uint8_t* __restrict__ status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const keto_check_packed p = q[i];
+    const uint8_t* f = blob + p.off;
+    keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0u, p.max_depth};
+    uint8_t st = KETO_CHECK_OK;
+    const bool set = p.kind != 0;
+    if (!p.len[0] || !p.len[1] || !p.len[2] || (set && (!p.len[3] || !p.len[4] || !p.len[5]))) {
+        st = ST_HOST;                                                      // a wildcard query: the host
+    } else {
+        const int64_t row = query_row_dev(R, f, p.len[0], p.len[1], p.len[2]);
+        if (row == -2) st = KETO_CHECK_UNKNOWN_NAMESPACE;
+        else if (row >= 0) r.row = (uint32_t)row;
+        const uint8_t* g = f + p.len[0] + p.len[1] + p.len[2];
+        if (!set) {
+            const int64_t sid = lookup_str_dev(R, g, p.len[3]);
+            if (sid >= 0) r.target = (uint32_t)sid;
+        } else {
+            const int64_t t = query_row_dev(R, g, p.len[3], p.len[4], p.len[5]);
+            if (t >= 0) {
+                r.target = (uint32_t)t;                                    // row-id form: translated below
+                r.flags = 1;
+            }
+        }
+    }
+    out[i] = r;
+    status[i] = st;
+}
+
+template <class T>
+T* upload(RBuf& b, const T* src, uint64_t n, hipStream_t st) {
+    T* d = b.get<T>(std::max<uint64_t>(n, 1));
+    if (n) HIP_OK(hipMemcpyAsync(d, src, n * sizeof(T), hipMemcpyHostToDevice, st));
+    return d;
+}
+
+}  // namespace
+
+// The device copies of the indexes (per snapshot version) and the per-call buffers.
+struct RDevState {
+    int device = 0;
+    uint64_t version = ~0ull;
+    std::mutex mu;                 // one packed batch at a time per snapshot
+    hipStream_t stream = nullptr;
+    RBuf str_slots, str_bytes, str_off, add_slots, row_slots, extra_slots, ns_bytes, ns_off, ns_id;
+    ResolveDev view{};
+    RBuf blob, reqs, ids, status, dec;
+    ~RDevState() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+void RDevStateDeleter::operator()(RDevState* r) const { delete r; }
+
+namespace {
+
+// an open-addressing table over (hash, fill) pairs, the host's layout and probing (resolve.cpp)
+template <class Slot, class Fill>
+std::vector<Slot> build_table(uint64_t n, uint64_t& mask, Fill fill) {
+    uint64_t cap = 16;
+    while (cap < n + n / 3 + 1) cap <<= 1;                               // load <= 3/4
+    std::vector<Slot> t(cap);
+    std::memset(t.data(), 0, cap * sizeof(Slot));
+    mask = cap - 1;
+    fill(t);
+    return t;
+}
+
+RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
+    if (!S.rdev) {
+        S.rdev.reset(new RDevState);
+        S.rdev->device = device;
+        HIP_OK(hipStreamCreateWithFlags(&S.rdev->stream, hipStreamNonBlocking));
+    }
+    RDevState& R = *S.rdev;
+    *st_out = R.stream;
+    if (R.version == S.version) return R;
+    hipStream_t st = R.stream;
+    S.ensure_index();
+    ResolveDev v{};
+    // the build's strings: the host index as it is, and every string's bytes (long-string checks)
+    v.base.slot = upload(R.str_slots, static_cast<const StrSlot*>(S.str_idx.p), S.str_mask + 1, st);
+    v.base.mask = S.str_mask;
+    {
+        const uint64_t ns = S.strs.size();
+        std::vector<uint64_t> off(ns + 1, 0);
+        for (uint64_t i = 0; i < ns; ++i) off[i + 1] = off[i] + S.strs[i].size();
+        std::vector<uint8_t> bytes(std::max<uint64_t>(1, off[ns]));
+        par_chunks(ns, ns >= par_min() ? build_threads() : 1u, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t i = b; i < e; ++i)
+                if (!S.strs[i].empty()) std::memcpy(bytes.data() + off[i], S.strs[i].data(), S.strs[i].size());
+        });
+        v.base.bytes = upload(R.str_bytes, bytes.data(), bytes.size(), st);
+        v.base.off = upload(R.str_off, off.data(), off.size(), st);
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    v.added = StrIndex{nullptr, 0, v.base.bytes, v.base.off};
+    if (!S.added_str.empty()) {
+        uint64_t mask = 0;
+        auto t = build_table<StrSlot>(S.added_str.size(), mask, [&](std::vector<StrSlot>& tab) {
+            const uint64_t m = tab.size() - 1;
+            for (const auto& kv : S.added_str) {
+                const std::string& s = kv.first;
+                for (uint64_t j = hash_bytes(s) & m;; j = (j + 1) & m) {
+                    if (tab[j].id1) continue;
+                    tab[j].id1 = kv.second + 1;
+                    tab[j].n = (uint8_t)std::min<size_t>(s.size(), 255);
+                    std::memcpy(tab[j].b, s.data(), std::min<size_t>(s.size(), INLINE));
+                    break;
+                }
+            }
+        });
+        v.added.slot = upload(R.add_slots, t.data(), t.size(), st);
+        v.added.mask = mask;
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    // the build's real rows: the host index; every other row a query can name (empty rows subject
+    // sets point at, rows writes added; not the wildcard rows): a second table
+    v.real.slot = upload(R.row_slots, static_cast<const RowSlot*>(S.row_idx.p), S.row_mask + 1, st);
+    v.real.mask = S.row_mask;
+    v.extra = RowIndex{nullptr, 0};
+    {
+        std::vector<std::pair<RowKey, uint32_t>> rows;
+        for (const auto& kv : S.row_of)
+            if (kv.first.ns != ANY_NS && kv.first.obj != ANY && kv.first.rel != ANY && kv.first.ns >= INT32_MIN &&
+                kv.first.ns <= INT32_MAX)
+                rows.push_back(kv);
+        if (!rows.empty()) {
+            uint64_t mask = 0;
+            auto t = build_table<RowSlot>(rows.size(), mask, [&](std::vector<RowSlot>& tab) {
+                const uint64_t m = tab.size() - 1;
+                for (const auto& kv : rows) {
+                    const RowKey& k = kv.first;
+                    for (uint64_t j = row_hash_hd(k.ns, k.obj, k.rel) & m;; j = (j + 1) & m) {
+                        if (tab[j].row1) continue;
+                        tab[j] = RowSlot{(int32_t)k.ns, k.obj, k.rel, kv.second + 1};
+                        break;
+                    }
+                }
+            });
+            v.extra.slot = upload(R.extra_slots, t.data(), t.size(), st);
+            v.extra.mask = mask;
+            HIP_OK(hipStreamSynchronize(st));
+        }
+    }
+    {
+        const uint32_t nn = (uint32_t)S.ns_names.size();
+        std::vector<uint64_t> off(nn + 1, 0);
+        std::string bytes;
+        for (uint32_t c = 0; c < nn; ++c) {
+            bytes += S.ns_names[c];
+            off[c + 1] = bytes.size();
+        }
+        v.ns_bytes = upload(R.ns_bytes, reinterpret_cast<const uint8_t*>(bytes.data()), bytes.size(), st);
+        v.ns_off = upload(R.ns_off, off.data(), off.size(), st);
+        v.ns_id = upload(R.ns_id, S.ns_ids.data(), S.ns_ids.size(), st);
+        v.n_ns = nn;
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    R.view = v;
+    R.version = S.version;
+    return R;
+}
+
+}  // namespace
+
+void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs, uint32_t n,
+                         int32_t gmd, uint8_t* allowed, uint8_t* status, std::vector<uint32_t>& host) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    const DevView dv = device_view(S);
+    HIP_OK(hipSetDevice(dv.device));
+    for (uint32_t i = 0; i < n; ++i) {
+        const keto_check_packed& p = reqs[i];
+        const uint64_t len = (uint64_t)p.len[0] + p.len[1] + p.len[2] + p.len[3] + (p.kind ? (uint64_t)p.len[4] + p.len[5] : 0);
+        if (p.off + len > blob_len) throw Error{KETO_E_INVALID, "request " + std::to_string(i) + "'s fields lie outside the blob"};
+    }
+    hipStream_t st = nullptr;
+    RDevState& R = rdev_state(S, dv.device, &st);
+    std::lock_guard<std::mutex> lk(R.mu);
+    const uint8_t* d_blob = upload(R.blob, blob, blob_len, st);
+    const keto_check_packed* d_q = upload(R.reqs, reqs, n, st);
+    keto_check_ids* d_ids = R.ids.get<keto_check_ids>(n);
+    uint8_t* d_st = R.status.get<uint8_t>(n);
+    uint8_t* d_dec = R.dec.get<uint8_t>(n);
+    hipLaunchKernelGGL(resolve_packed, dim3((n + 255) / 256), dim3(256), 0, st, R.view, d_blob, d_q, n, d_ids, d_st);
+    HIP_OK(hipGetLastError());
+    device_check_rows(S, d_ids, n, gmd, d_dec, st);                        // row ids -> handles, the check
+    HIP_OK(hipMemcpyAsync(allowed, d_dec, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (status[i] == ST_HOST) {
+            host.push_back(i);
+            continue;
+        }
+        if (allowed[i] > 1) {                                              // KETO_UNDECIDED
+            allowed[i] = 0;
+            if (status[i] == KETO_CHECK_OK) status[i] = KETO_CHECK_UNDECIDED;
+        }
+    }
+}
+
+void rdev_release(Snapshot& S) { S.rdev.reset(); }
+
+}  // namespace keto

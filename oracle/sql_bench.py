@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from oracle.oracle_sql import CheckEngine, Namespaces, RelationTuple, SQLStore, SubjectID  # noqa: E402
+from oracle.oracle_sql import CheckEngine, Namespaces, RelationTuple, SQLStore, SubjectID, SubjectSet  # noqa: E402
 
 
 def open_store(db, namespaces, page_size):
@@ -46,7 +46,9 @@ def _work(args):
     while time.time() < t_start:          # start together
         time.sleep(0.001)
     t0 = time.perf_counter()
-    out = [int(eng.subject_is_allowed(RelationTuple(ns, o, r, SubjectID(s)), d)) for ns, o, r, s, d in reqs]
+    # a request's subject: a subject id (string) or a subject set [namespace, object, relation]
+    out = [int(eng.subject_is_allowed(RelationTuple(ns, o, r, SubjectID(s) if isinstance(s, str) else SubjectSet(*s)), d))
+           for ns, o, r, s, d in reqs]
     st.requested_pages = []
     return out, time.perf_counter() - t0
 

@@ -87,6 +87,32 @@ def config1(a):
         sub = SubjectID(u[1]) if u[0] == "id" else SubjectSet(*u[1:])
         ref.append(eng.subject_is_allowed(RelationTuple(n_, o, r, sub), d))
     t_sql = time.perf_counter() - t0
+    # the same requests with one worker process per core (oracle/sql_bench.py, as bench.py's ref_sql)
+    import json as _json
+    import subprocess
+    import tempfile
+    fd, db = tempfile.mkstemp(prefix="keto_c1_", suffix=".sqlite", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    os.close(fd)
+    fd, rq = tempfile.mkstemp(prefix="keto_c1_", suffix=".json")
+    os.close(fd)
+    try:
+        dst = __import__("sqlite3").connect(db)
+        store.conn.backup(dst)
+        dst.close()
+        _json.dump({"namespaces": ns, "requests": [(n_, o, r, u[1] if u[0] == "id" else list(u[1:]), d)
+                                                  for n_, o, r, u, d in reqs]}, open(rq, "w"))
+        pr = subprocess.run([sys.executable, "-m", "oracle.sql_bench", "--db", db, "--requests", rq, "--workers",
+                             str(a.threads), "--gmd", "5"], capture_output=True, text=True, cwd=ROOT, timeout=600)
+        if pr.returncode != 0:
+            raise RuntimeError(pr.stderr[-2000:])
+        par = _json.loads(pr.stdout.strip().splitlines()[-1])
+    finally:
+        for f in (db, rq):
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+    par_mism = int(sum(int(x) != int(y) for x, y in zip(par["decisions"], ref)))
     snap = Snapshot.build(ns, rows_from_tuples(ns, tuples), device=0)
     t0 = time.perf_counter()
     allowed, _ = snap.check_batch(reqs, 5)
@@ -96,6 +122,10 @@ def config1(a):
             "ref_sql": {"checks_per_s": round(len(reqs) / t_sql, 1), "cores": 1,
                         "what": "oracle/oracle_sql.py: the reference engine's recursion issuing its SQL "
                                 "(ORDER BY, LIMIT 100 OFFSET, page count) against in-memory SQLite"},
+            "ref_sql_parallel": {"checks_per_s": par["checks_per_s"], "cores": par["workers"],
+                                 "mismatches_vs_serial": par_mism,
+                                 "what": "the same, one worker process per core (oracle/sql_bench.py), each with its "
+                                         "own in-memory copy of the database"},
             "gpu_host_api": {"checks_per_s": round(len(reqs) / t_gpu, 1),
                              "what": "keto_check_batch with string requests (resolution + H2D + kernel + D2H)"},
             "mismatches": mism}
