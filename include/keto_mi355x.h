@@ -333,6 +333,28 @@ int keto_resolve_checks(const keto_snapshot* s, const keto_check_req* reqs, uint
 int keto_check_batch(keto_snapshot* s, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth,
                      uint8_t* allowed_out, uint8_t* status_out);
 
+/* Check requests with their strings packed back to back in one buffer, resolved on the GPU.  Request
+ * i's fields start at blob + reqs[i].off: namespace, object, relation, then the subject id (kind 0)
+ * or the subject set's namespace, object and relation (kind 1), with their byte lengths in
+ * reqs[i].len -- the form a caller that already copies a batch's strings into one arena (the Go
+ * batcher's C memory) hands over without building keto_check_req structs.  The library copies blob
+ * and records to the device and resolves every request there against the snapshot's string and row
+ * indexes (whereQuery, internal/persistence/sql/relationtuples.go:178-198; the indexes are uploaded
+ * once per snapshot version), then checks them (check.(*Engine).SubjectIsAllowed,
+ * internal/check/engine.go:116-123): decisions and statuses equal keto_check_batch's on the same
+ * requests.  Requests with an empty namespace, object or relation (wildcard queries, in the subject
+ * set too) are resolved on the host as keto_check_batch does.  blob_len < 2^32; fields of up to
+ * 65535 bytes (longer ones: keto_check_batch). */
+typedef struct {
+    uint32_t off;               /* byte offset of the request's first field in blob */
+    uint16_t len[6];            /* namespace, object, relation, subject id | set namespace, set object, set relation */
+    uint8_t kind;               /* 0 = subject id (len[0..3]), 1 = subject set (len[0..5]) */
+    uint8_t reserved;
+    int32_t max_depth;          /* <= 0 or > global -> global (engine.go:118-120) */
+} keto_check_packed;
+int keto_check_batch_packed(keto_snapshot* s, const char* blob, uint64_t blob_len, const keto_check_packed* reqs,
+                            uint32_t n, int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
+
 /* Same with pre-resolved requests in host memory (decision bytes as above, KETO_UNDECIDED
  * included).  Host-buffer calls run as a pipeline of chunks: the H2D copy of the next chunk and the
  * D2H copy of the previous one overlap the check of the current one.  Buffers from keto_host_alloc

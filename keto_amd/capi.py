@@ -38,7 +38,7 @@ EXPORTS = [
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_snapshot_upload_part_migrate",
     "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
     "keto_comm_id", "keto_comm_init", "keto_comm_free", "keto_check_batch_sharded", "keto_check_batch_routed",
-    "keto_comm_close_filters", "keto_comm_init_local", "keto_snapshot_clone",
+    "keto_comm_close_filters", "keto_comm_init_local", "keto_snapshot_clone", "keto_check_batch_packed",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -81,6 +81,28 @@ class KCheckIds(C.Structure):
 
 CHECK_IDS_DTYPE = np.dtype([("row", "<u4"), ("target", "<u4"), ("flags", "<u4"), ("max_depth", "<i4")])
 CHECK_PAIR_DTYPE = np.dtype([("row", "<u4"), ("subject", "<u4")])
+# keto_check_packed: a request's fields back to back in a blob (offset, six lengths, kind, depth)
+CHECK_PACKED_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2", (6,)), ("kind", "u1"), ("reserved", "u1"),
+                               ("max_depth", "<i4")], align=True)
+assert CHECK_PACKED_DTYPE.itemsize == 24
+
+
+def pack_requests(reqs):
+    """reqs as in Snapshot.check_batch -> (blob bytes, CHECK_PACKED_DTYPE array) for
+    keto_check_batch_packed: every request's strings back to back."""
+    parts, out = [], np.zeros(len(reqs), dtype=CHECK_PACKED_DTYPE)
+    off = 0
+    for i, (ns, obj, rel, sub, depth) in enumerate(reqs):
+        fields = [ns, obj, rel] + ([sub[1]] if sub[0] == "id" else list(sub[1:4]))
+        enc = [f.encode() for f in fields]
+        out[i]["off"] = off
+        out[i]["len"][:len(enc)] = [len(x) for x in enc]
+        out[i]["kind"] = 0 if sub[0] == "id" else 1
+        out[i]["max_depth"] = depth
+        for x in enc:
+            parts.append(x)
+            off += len(x)
+    return b"".join(parts), out
 
 
 def pairs_of(q: np.ndarray) -> np.ndarray:
@@ -448,6 +470,26 @@ class Snapshot:
         status = np.zeros(max(1, n), dtype=np.uint8)
         _check(self.lib.keto_check_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth),
                                          allowed.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
+        return allowed[:n], status[:n]
+
+    def check_batch_packed(self, blob, packed: np.ndarray, global_max_depth=5, n=None, allowed=None, status=None):
+        """keto_check_batch_packed: requests resolved on the GPU from one string blob (bytes, a numpy
+        uint8 array or a HostBuffer array) and CHECK_PACKED_DTYPE records.  Returns (allowed, status)."""
+        n = len(packed) if n is None else n
+        packed = np.ascontiguousarray(packed, dtype=CHECK_PACKED_DTYPE)
+        if isinstance(blob, (bytes, bytearray)):
+            blob = np.frombuffer(blob, dtype=np.uint8) if len(blob) else np.zeros(1, dtype=np.uint8)
+            blen = len(blob) if blob.size else 0
+        else:
+            blen = blob.nbytes
+        if allowed is None:
+            allowed = np.zeros(max(1, n), dtype=np.uint8)
+        if status is None:
+            status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch_packed(self.h, blob.ctypes.data_as(C.c_void_p), C.c_uint64(blen),
+                                                packed.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                                C.c_int32(global_max_depth), allowed.ctypes.data_as(C.c_void_p),
+                                                status.ctypes.data_as(C.c_void_p)))
         return allowed[:n], status[:n]
 
     def check_batch(self, reqs, global_max_depth=5):

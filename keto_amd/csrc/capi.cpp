@@ -453,6 +453,55 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
     });
 }
 
+int keto_check_batch_packed(keto_snapshot* h, const char* blob, uint64_t blob_len, const keto_check_packed* reqs,
+                            uint32_t n, int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
+    return guarded([&] {
+        if (!h || (n && (!reqs || !allowed_out)) || (blob_len && !blob)) throw Error{KETO_E_INVALID, "NULL argument"};
+        if (blob_len >= (1ull << 32)) throw Error{KETO_E_RANGE, "a packed batch's strings must stay below 4 GiB"};
+        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        Snapshot& S = *h->s;
+        if (n == 0) return KETO_OK;
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<uint8_t> st_local(status_out ? 0 : n);
+        uint8_t* status = status_out ? status_out : st_local.data();
+        std::vector<uint32_t> host;
+        device_check_packed(S, reinterpret_cast<const uint8_t*>(blob), blob_len, reqs, n, global_max_depth,
+                            allowed_out, status, host);
+        if (!host.empty()) {
+            // wildcard queries: the host path (keto_check_batch), which may need batch-local rows
+            std::vector<keto_check_req> q(host.size());
+            for (size_t k = 0; k < host.size(); ++k) {
+                const keto_check_packed& p = reqs[host[k]];
+                const char* f = blob + p.off;
+                keto_check_req& r = q[k];
+                std::memset(&r, 0, sizeof r);
+                r.namespace_ = keto_str{f, p.len[0]};
+                r.object = keto_str{f + p.len[0], p.len[1]};
+                r.relation = keto_str{f + p.len[0] + p.len[1], p.len[2]};
+                const char* g = f + p.len[0] + p.len[1] + p.len[2];
+                if (p.kind == 0) {
+                    r.subject.kind = 0;
+                    r.subject.id = keto_str{g, p.len[3]};
+                } else {
+                    r.subject.kind = 1;
+                    r.subject.set_namespace = keto_str{g, p.len[3]};
+                    r.subject.set_object = keto_str{g + p.len[3], p.len[4]};
+                    r.subject.set_relation = keto_str{g + p.len[3] + p.len[4], p.len[5]};
+                }
+                r.max_depth = p.max_depth;
+            }
+            std::vector<uint8_t> a(host.size()), st(host.size());
+            check_named(S, q.data(), (uint32_t)q.size(), global_max_depth, a.data(), st.data());
+            for (size_t k = 0; k < host.size(); ++k) {
+                allowed_out[host[k]] = a[k];
+                status[host[k]] = st[k];
+            }
+        }
+        S.last_resolve_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return KETO_OK;
+    });
+}
+
 int keto_check_batch_ids(keto_snapshot* h, const keto_check_ids* reqs, uint32_t n, int32_t global_max_depth,
                          uint8_t* allowed_out) {
     return guarded([&] {

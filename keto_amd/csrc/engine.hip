@@ -2919,6 +2919,7 @@ void device_release(Snapshot& S) {
     mig_release(S);
     S.proto.reset();
     S.reach.reset();
+    rdev_release(S);
     for (auto& W : D.ws) {
         for (auto& t : W.tiers) free_tier(t);
         if (W.lists) (void)hipFree(W.lists);

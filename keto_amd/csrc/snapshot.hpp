@@ -169,6 +169,10 @@ struct ReachState;       // reach.hip
 struct ReachStateDeleter {
     void operator()(ReachState* r) const;    // reach.hip
 };
+struct RDevState;        // resolve_dev.hip
+struct RDevStateDeleter {
+    void operator()(RDevState* r) const;     // resolve_dev.hip
+};
 
 uint64_t next_snapshot_uid();   // snapshot.cpp: a process-wide counter
 
@@ -278,6 +282,7 @@ struct Snapshot {
     std::unique_ptr<MigState, MigStateDeleter> mig;      // migrating-partition batches (migrate.hip)
     std::unique_ptr<ProtoState, ProtoStateDeleter> proto; // strings on the device for tree encoding (proto.hip)
     std::unique_ptr<ReachState, ReachStateDeleter> reach; // reverse / postings index of deep batches (reach.hip)
+    std::unique_ptr<RDevState, RDevStateDeleter> rdev;    // string / row indexes on the device (resolve_dev.hip)
     std::mutex mu;
 
     ~Snapshot();
@@ -477,6 +482,11 @@ uint64_t device_tree_proto(Snapshot& s, const keto_tree_node* nodes, uint64_t n_
                            uint32_t n_trees, uint32_t ov_base, const std::vector<RowKey>& ov_keys, uint32_t extra_base,
                            const std::vector<std::string>& extra, uint8_t* buf, uint64_t cap, uint64_t* offsets);
 void device_copy(void* dst, const void* src, uint64_t bytes, void* stream);   // D2D, synchronous
+// packed string requests resolved and checked on the device (resolve_dev.hip); the indexes of the
+// requests left to the host (wildcard queries) are appended to `host`
+void device_check_packed(Snapshot& s, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs, uint32_t n,
+                         int32_t gmd, uint8_t* allowed, uint8_t* status, std::vector<uint32_t>& host);
+void rdev_release(Snapshot& s);
 // An allocator whose resize() leaves new elements default-initialized (no zero fill): the expand
 // node arena is sized, then overwritten by one D2H copy.
 template <class T>

@@ -1,0 +1,142 @@
+"""Requests resolved on the GPU (keto_check_batch_packed, keto_amd/csrc/resolve_dev.hip): the same
+decisions and statuses as keto_check_batch (host resolution, resolve.cpp) and as the SQL oracle
+(whereQuery, internal/persistence/sql/relationtuples.go:178-198; check/engine.go:36-123) -- on
+quirk-heavy random graphs (unknown namespaces and strings, subject sets, wildcard queries left to the
+host, collisions, poisoned rows), on strings longer than a slot's 11 inline bytes that share their
+first 11 bytes, after writes that add strings and rows, and on the power-law graph built from its
+string tuples."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle.oracle_sql import CheckEngine, RelationTuple, SQLStore, SubjectID, SubjectSet
+from tests.engine_util import rows_from_tuples, subj
+from tests.randgraph import random_checks, random_store
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_as_host(snap, reqs, g):
+    from keto_amd.capi import pack_requests
+    want, want_st = snap.check_batch(reqs, g)
+    blob, packed = pack_requests(reqs)
+    got, st = snap.check_batch_packed(blob, packed, g)
+    assert (got == want).all(), [(r, int(a), int(b)) for r, a, b in zip(reqs, got, want) if a != b][:5]
+    assert (st == want_st).all(), [(r, int(a), int(b)) for r, a, b in zip(reqs, st, want_st) if a != b][:5]
+    return got
+
+
+@pytest.mark.parametrize("seed", range(5000, 5060))
+def test_random_graphs_packed_equals_host(seed):
+    import keto_amd
+    store, ns, tuples, raw, ps, alph = random_store(seed, wide=seed % 4 == 0)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples, raw), page_size=ps, device=0)
+    checks = random_checks(seed, alph, k=80)
+    for g in sorted({c[2] for c in checks}):
+        grp = [c for c in checks if c[2] == g]
+        reqs = [(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in grp]
+        got = _same_as_host(snap, reqs, g)
+        for (t, d, _), a in zip(grp, got):
+            assert bool(a) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, t, d, g)
+    snap.close()
+
+
+def test_long_strings_sharing_a_prefix():
+    """Objects, relations and subject ids longer than a string slot's 11 inline bytes, many sharing
+    their first 11 bytes (the slot matches, the device compares the rest), and requests naming
+    strings the snapshot does not hold but whose prefix it does."""
+    import keto_amd
+    rng = random.Random(7)
+    ns = [(1, "files"), (2, "groups")]
+    pre = "0123456789abcdef"
+    objs = [pre + f"/doc/{i:05d}" for i in range(60)] + ["short"]
+    users = [pre + f"user-{i}" * (1 + i % 5) for i in range(40)] + ["u"]
+    grps = [pre + f"g{i:03d}" for i in range(20)]
+    tuples = []
+    for _ in range(600):
+        if rng.random() < 0.6:
+            tuples.append(RelationTuple("files", rng.choice(objs), "view", SubjectID(rng.choice(users))))
+        elif rng.random() < 0.5:
+            tuples.append(RelationTuple("files", rng.choice(objs), "view", SubjectSet("groups", rng.choice(grps), "member")))
+        else:
+            tuples.append(RelationTuple("groups", rng.choice(grps), "member", SubjectID(rng.choice(users))))
+    store = SQLStore(ns, tuples)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), device=0)
+    reqs, exp = [], []
+    for _ in range(400):
+        o = rng.choice(objs + [pre + "/doc/99999", pre])
+        if rng.random() < 0.8:
+            s = rng.choice(users + [pre + "user-", pre + "nobody"])
+            reqs.append(("files", o, "view", ("id", s), 0))
+            exp.append(RelationTuple("files", o, "view", SubjectID(s)))
+        else:
+            gname = rng.choice(grps + [pre + "g999"])
+            reqs.append(("files", o, "view", ("set", "groups", gname, "member"), 0))
+            exp.append(RelationTuple("files", o, "view", SubjectSet("groups", gname, "member")))
+    got = _same_as_host(snap, reqs, 5)
+    for t, a in zip(exp, got):
+        assert bool(a) == CheckEngine(store, 5).subject_is_allowed(t, 0), t
+    snap.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_packed_after_writes(seed):
+    """Writes add strings and rows the build's indexes do not hold (added_str, row_of): the device
+    indexes are rebuilt for the new version and still resolve exactly like the host."""
+    import keto_amd
+    from tests.test_gpu_lifecycle import _random_write, _row
+    from tests.randgraph import random_graph
+    ns, tuples, raw, ps, alph = random_graph(seed + 700, allow_poison=False)
+    names, objs, rels, users = alph
+    names = [n for n in names if n]
+    if not names:
+        pytest.skip("only a namespace named ''")
+    store = SQLStore(ns, tuples, page_size=ps)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), page_size=ps, device=0)
+    rng = random.Random(seed)
+    for step in range(4):
+        ins = [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(2, 10))]
+        snap.apply([_row(ns, t) for t in ins], [])
+        for t in ins:
+            store.insert(t)
+        checks = random_checks(seed * 5 + step, (names, objs + ["new1", "new7", "a0", "Z"], rels + ["q"],
+                                                 users + ["w001", "a", "zz"]), k=60)
+        for g in sorted({c[2] for c in checks}):
+            grp = [c for c in checks if c[2] == g]
+            reqs = [(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in grp]
+            got = _same_as_host(snap, reqs, g)
+            for (t, d, _), a in zip(grp, got):
+                assert bool(a) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, step, t, d)
+    snap.close()
+
+
+def test_powerlaw_packed_matches_host():
+    """200,000 named requests on the power-law graph (1/256 scale) built from its string tuples,
+    packed by the generator's packer, against keto_check_batch on the same snapshot."""
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 256), threads=16)
+    st = g.string_tuples(seed=5)
+    snap, _ = g.snapshot_from_strings(st, device=0)
+    q = g.queries(200_000, seed=11, depth=5)
+    arr = g.string_requests(st, q)
+    want, want_st = snap.check_batch_reqs(arr, len(q), 5)
+    blob, rec, used = g.pack_requests(arr, len(q))
+    got, got_st = snap.check_batch_packed(blob.array[:used], rec.array, 5, n=len(q))
+    assert (got == want).all() and (got_st == want_st).all()
+    assert 0.05 < got.mean() < 0.95
+    snap.close()
+    g.close()
+
+
+def test_packed_empty_batch_and_bad_offsets():
+    import keto_amd
+    from keto_amd.capi import CHECK_PACKED_DTYPE, KetoError, pack_requests
+    snap = keto_amd.Snapshot.build([(1, "n")], [(1, "a", "r", "u")], device=0)
+    got, st = snap.check_batch_packed(b"", np.zeros(0, dtype=CHECK_PACKED_DTYPE), 5)
+    assert len(got) == 0
+    blob, packed = pack_requests([("n", "a", "r", ("id", "u"), 0)])
+    packed["off"][0] = 1000
+    with pytest.raises(KetoError):
+        snap.check_batch_packed(blob, packed, 5)
+    snap.close()

@@ -663,6 +663,63 @@ int synth_check_reqs(const synth_graph* g, const synth_strings* st, const keto_c
     return 0;
 }
 
+// keto_check_req -> keto_check_packed: every request's fields back to back in blob (which holds
+// cap bytes); returns the bytes used, or -1 when blob is too small or a field exceeds 65535 bytes.
+// Offsets are a prefix sum over the requests' field lengths (threads: per-chunk sums, then copies).
+int64_t synth_pack_reqs(const keto_check_req* q, uint64_t n, uint8_t* blob, uint64_t cap, keto_check_packed* out,
+                        int threads) {
+    auto fields = [&](const keto_check_req& r, keto_str* f) {
+        f[0] = r.namespace_;
+        f[1] = r.object;
+        f[2] = r.relation;
+        if (r.subject.kind == 0) {
+            f[3] = r.subject.id;
+            f[4] = f[5] = keto_str{nullptr, 0};
+            return 4;
+        }
+        f[3] = r.subject.set_namespace;
+        f[4] = r.subject.set_object;
+        f[5] = r.subject.set_relation;
+        return 6;
+    };
+    const uint64_t T = (uint64_t)std::max(1, threads);
+    const uint64_t chunk = (n + T - 1) / T;
+    std::vector<uint64_t> sum(T + 1, 0);
+    std::atomic<int> bad{0};
+    parallel_for(T, threads, [&](uint64_t t) {
+        uint64_t s = 0;
+        for (uint64_t i = t * chunk; i < std::min(n, (t + 1) * chunk); ++i) {
+            keto_str f[6];
+            const int k = fields(q[i], f);
+            for (int j = 0; j < k; ++j) {
+                if (f[j].n > 65535) bad = 1;
+                s += f[j].n;
+            }
+        }
+        sum[t + 1] = s;
+    });
+    for (uint64_t t = 0; t < T; ++t) sum[t + 1] += sum[t];
+    if (bad || sum[T] > cap || sum[T] >= (1ull << 32)) return -1;
+    parallel_for(T, threads, [&](uint64_t t) {
+        uint64_t at = sum[t];
+        for (uint64_t i = t * chunk; i < std::min(n, (t + 1) * chunk); ++i) {
+            keto_str f[6];
+            const int k = fields(q[i], f);
+            keto_check_packed& p = out[i];
+            memset(&p, 0, sizeof p);
+            p.off = (uint32_t)at;
+            p.kind = q[i].subject.kind;
+            p.max_depth = q[i].max_depth;
+            for (int j = 0; j < k; ++j) {
+                p.len[j] = (uint16_t)f[j].n;
+                if (f[j].n) memcpy(blob + at, f[j].p, f[j].n);
+                at += f[j].n;
+            }
+        }
+    });
+    return (int64_t)sum[T];
+}
+
 void synth_strings_free(synth_strings* s) {
     free(s->tuples);
     free(s->names);

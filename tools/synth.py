@@ -65,6 +65,7 @@ def lib():
     if _lib is None:
         build()
         _lib = C.CDLL(LIB)
+        _lib.synth_pack_reqs.restype = C.c_int64
     return _lib
 
 
@@ -251,6 +252,32 @@ class SynthGraph:
                                out, C.c_int(threads))
         out._keep = (na, names)
         return out
+
+    @staticmethod
+    def pack_requests(arr, n, threads=16, pinned=True):
+        """A keto_check_req array -> (blob, keto_check_packed records, bytes used) for
+        keto_check_batch_packed, packed on host threads; pinned: both in page-locked memory
+        (keto_host_alloc, .array holds the numpy view), else plain numpy arrays."""
+        from keto_amd.capi import CHECK_PACKED_DTYPE, HostBuffer
+
+        class _Plain:
+            def __init__(self, k, dt):
+                self.array = np.zeros(k, dtype=dt)
+        buf = HostBuffer if pinned else _Plain
+        total = 0
+        cap = max(1, n) * 64
+        while True:
+            blob = buf(cap, np.uint8)
+            rec = buf(max(1, n), CHECK_PACKED_DTYPE)
+            used = lib().synth_pack_reqs(arr, C.c_uint64(n), blob.array.ctypes.data_as(C.c_void_p), C.c_uint64(cap),
+                                         rec.array.ctypes.data_as(C.c_void_p), C.c_int(threads))
+            if used >= 0:
+                total = used
+                break
+            if cap >= (1 << 32):
+                raise ValueError("requests do not pack below 4 GiB (or a field exceeds 65535 bytes)")
+            cap = min(cap * 2, 1 << 32)
+        return blob, rec, int(total)
 
     def free_strings(self, st):
         lib().synth_strings_free(C.byref(st))
