@@ -367,6 +367,50 @@ int main(int argc, char** argv) {
                 break;
             }
             if (rc != KETO_OK) fail("keto_check_batch", rc);
+            {
+                /* the Go shim's path: the same batch packed in one string blob, resolved on the GPU
+                   (keto_check_batch_packed); decisions and statuses must equal keto_check_batch's */
+                size_t total = 0;
+                for (size_t k = 0; k < m; ++k) {
+                    const keto_check_req* r = &q[k];
+                    total += r->namespace_.n + r->object.n + r->relation.n;
+                    total += r->subject.kind == 0 ? r->subject.id.n
+                                                  : r->subject.set_namespace.n + r->subject.set_object.n + r->subject.set_relation.n;
+                }
+                char* blob = (char*)xrealloc(NULL, total);
+                keto_check_packed* pk = (keto_check_packed*)calloc(m, sizeof(keto_check_packed));
+                uint8_t* pa = (uint8_t*)malloc(m);
+                uint8_t* ps = (uint8_t*)malloc(m);
+                if (!pk || !pa || !ps) return 3;
+                size_t at = 0;
+                for (size_t k = 0; k < m; ++k) {
+                    const keto_check_req* r = &q[k];
+                    keto_str f[6] = {r->namespace_, r->object, r->relation, r->subject.id, {NULL, 0}, {NULL, 0}};
+                    int nf = 4;
+                    if (r->subject.kind == 1) {
+                        f[3] = r->subject.set_namespace;
+                        f[4] = r->subject.set_object;
+                        f[5] = r->subject.set_relation;
+                        nf = 6;
+                    }
+                    pk[k].off = (uint32_t)at;
+                    pk[k].kind = r->subject.kind;
+                    pk[k].max_depth = r->max_depth;
+                    for (int j = 0; j < nf; ++j) {
+                        pk[k].len[j] = (uint16_t)f[j].n;
+                        if (f[j].n) memcpy(blob + at, f[j].p, f[j].n);
+                        at += f[j].n;
+                    }
+                }
+                rc = keto_check_batch_packed(snap, blob, total, pk, (uint32_t)m, gmd, pa, ps);
+                if (rc != KETO_OK) fail("keto_check_batch_packed", rc);
+                for (size_t k = 0; k < m; ++k)
+                    if (pa[k] != allowed[k] || ps[k] != status[k]) return 13;
+                free(blob);
+                free(pk);
+                free(pa);
+                free(ps);
+            }
             for (size_t k = 0; k < m; ++k) printf("check\t%d\t%u\t%u\n", checks++, allowed[k], status[k]);
             free(q);
             free(allowed);

@@ -263,11 +263,85 @@ func (m *cmem) subject(sub relationtuple.Subject) C.keto_subject {
 }
 
 // CheckBatch = check.(*Engine).SubjectIsAllowed (internal/check/engine.go:116-123) for many
-// requests: allowed[i] and status[i] (StatusUndecided: ask the SQL engine for request i).
+// requests: allowed[i] and status[i] (StatusUndecided: ask the SQL engine for request i).  The
+// batch's strings go to the library packed back to back in one C buffer and are resolved on the GPU
+// (keto_check_batch_packed); a batch holding a field longer than 65535 bytes takes keto_check_batch,
+// which resolves on host threads.
 func (s *Snapshot) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	if out, st, ok, err := s.checkPacked(reqs, depths, globalMax); ok {
+		return out, st, err
+	}
 	return checkWith(reqs, depths, false, func(cr *C.keto_check_req, n C.uint32_t, allowed, status *C.uint8_t) C.int {
 		return C.keto_check_batch(s.h, cr, n, C.int32_t(globalMax), allowed, status)
 	})
+}
+
+// packedFields are a request's fields in keto_check_packed order: namespace, object, relation, then
+// the subject id or the subject set's namespace, object and relation.
+func packedFields(r *relationtuple.InternalRelationTuple) ([6]string, int, uint8) {
+	f := [6]string{r.Namespace, r.Object, r.Relation}
+	switch v := r.Subject.(type) {
+	case *relationtuple.SubjectID:
+		f[3] = v.ID
+		return f, 4, 0
+	case *relationtuple.SubjectSet:
+		f[3], f[4], f[5] = v.Namespace, v.Object, v.Relation
+		return f, 6, 1
+	}
+	return f, 4, 0 // nil subject: an empty subject id, which matches nothing
+}
+
+// checkPacked runs the batch through keto_check_batch_packed; ok = false when a field does not fit
+// a record (then nothing ran).
+func (s *Snapshot) checkPacked(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, bool, error) {
+	n := len(reqs)
+	if n == 0 {
+		return nil, nil, true, nil
+	}
+	if len(depths) != n {
+		return nil, nil, true, fmt.Errorf("gpu: %d requests, %d depths", n, len(depths))
+	}
+	total := 0
+	for _, r := range reqs {
+		f, k, _ := packedFields(r)
+		for j := 0; j < k; j++ {
+			if len(f[j]) > 65535 {
+				return nil, nil, false, nil
+			}
+			total += len(f[j])
+		}
+	}
+	if total >= 1<<32 {
+		return nil, nil, false, nil
+	}
+	var m cmem
+	defer m.free()
+	m.strings(total)
+	rec := (*C.keto_check_packed)(m.alloc(n * int(C.sizeof_keto_check_packed)))
+	rs := unsafe.Slice(rec, n)
+	for i, r := range reqs {
+		f, k, kind := packedFields(r)
+		p := C.keto_check_packed{off: C.uint32_t(m.used), kind: C.uint8_t(kind), max_depth: C.int32_t(depths[i])}
+		for j := 0; j < k; j++ {
+			p.len[j] = C.uint16_t(len(f[j]))
+			m.s(f[j])
+		}
+		rs[i] = p
+	}
+	allowed := (*C.uint8_t)(m.alloc(n))
+	status := (*C.uint8_t)(m.alloc(n))
+	if rc := C.keto_check_batch_packed(s.h, (*C.char)(m.str), C.uint64_t(m.used), rec, C.uint32_t(n),
+		C.int32_t(globalMax), allowed, status); rc != C.KETO_OK {
+		return nil, nil, true, lastErr(rc)
+	}
+	out := make([]bool, n)
+	st := make([]uint8, n)
+	as, ss := unsafe.Slice(allowed, n), unsafe.Slice(status, n)
+	for i := range out {
+		out[i] = as[i] == 1
+		st[i] = uint8(ss[i])
+	}
+	return out, st, true, nil
 }
 
 // checkWith marshals the requests into C memory, runs call (one of the keto_check_batch* entry
