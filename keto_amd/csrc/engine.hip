@@ -543,6 +543,21 @@ struct TierArgs {
     // check_kernel: non-NULL = requests handed out one at a time from this counter after each lane's
     // first (a lane never holds a run of long searches back to back); NULL = contiguous runs
     uint32_t* next;
+    // streamed host batch (tier-0 wave kernel, STREAM): 8-B keto_check_pair requests by row id that
+    // land in chunks of 2^chunk_log2 behind the running launch; ready[c] != 0 once chunk c has
+    // landed (written in copy order, so it also vouches for every earlier chunk).  Row ids become
+    // handles through row_handle (n_rows entries, NO_UNIT: another part's root row, counted in
+    // *misrouted); a lane that waits more than wait_ticks (100 MHz) for a chunk sets *stalled and
+    // stops, and the caller checks the batch again without streaming
+    const keto_check_pair* pairs;
+    const uint32_t* ready;
+    uint32_t chunk_log2;
+    const uint32_t* row_handle;
+    uint32_t n_rows;
+    int32_t pair_depth;
+    uint32_t* misrouted;
+    uint32_t* stalled;
+    uint64_t wait_ticks;
 };
 
 // ------------------------------------------------------------------ check
@@ -978,7 +993,25 @@ struct LaneVisited {
 #define KETO_WAVE_WAVES 8
 #endif
 
-template <int F, bool WIN, int LV, int RV, bool COUNT>
+// streamed batches: wait (bounded) until chunk word `p` says the chunk has landed.  Relaxed is
+// enough: the requests are only read after the word's value came back (program order), and the
+// launch started with caches holding none of this batch's lines (tools/dev/stream_probe.hip)
+__device__ inline bool chunk_wait(const uint32_t* p, uint64_t ticks) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return true;
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return true;
+        if (wall_clock64() - t0 > ticks) return false;
+    }
+}
+
+#ifndef KETO_STREAM_CPOL
+#define KETO_STREAM_CPOL 0            // cache policy of the streamed request loads
+#endif
+constexpr uint32_t P_XLT = 5;          // streamed: the request's row id (and set target) -> handles
+
+template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM = false>
 __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
                       uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
@@ -1001,11 +1034,18 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
     // runs on XCD b % 8); a lane's first run covers its share of part of its XCD's range, then it takes
     // runs of ta.dyn requests from its XCD's head (one returning atomic per wave and grab), so lanes
     // that drew long searches do not hold up the end of the launch
+    // Streamed batches (STREAM): dynamic runs only, dealt interleaved over the XCDs (run g of the
+    // batch goes to XCD g % 8) so that every XCD works near the front where the chunks have landed
     const uint32_t R = ta.dyn & 0xFFFFu;
     uint32_t j, j_end, xe = n, dyn_base = 0;
     uint32_t* head = nullptr;
     bool whole_groups = true;                                  // runs are 4-aligned multiples of 4
-    if (R == 0) {
+    uint32_t known = 0;                                        // STREAM: chunks [0, known) have landed
+    if (STREAM) {
+        const uint32_t nx = min(8u, gridDim.x);
+        j = j_end = 0;
+        head = ta.heads + 32u * ((blockIdx.x % nx) << ((ta.dyn >> 20) & 15u));
+    } else if (R == 0) {
         // batches under 4 requests per lane: runs of 1-3 requests (every lane busy; decisions are
         // then stored byte by byte); otherwise runs rounded up to a multiple of 4
         uint32_t per = (n + stride - 1) / stride;
@@ -1055,6 +1095,24 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             const uint4 nq = lds_nq[tid];
             const uint32_t qi = j++;
             uint32_t keep = 0;                                    // the pair's second request moves up
+            if constexpr (STREAM) {
+                // {row id, subject} x 2; the batch's request depth; P_XLT looks the handles up
+                if (c & C_NQ2) {
+                    lds_nq[tid] = make_uint4(nq.z, nq.w, 0u, 0u);
+                    keep = C_NQ;
+                }
+                int d = ta.pair_depth;
+                if (d <= 0 || gmd < d) d = gmd;                   // engine.go:118-120
+                if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
+                    decide(qi, 0);
+                    c = keep;
+                    continue;
+                }
+                T = nq.y;                                         // bit 31: a subject set's row id
+                eh = nq.x;
+                c = P_XLT | ((uint32_t)d << C_K) | ((nq.y & EDGE_SET) ? C_TSET : 0u) | keep;
+                return;
+            }
             if (c & C_NQ2) {
                 lds_nq[tid] = lds_nq[LDS_STRIDE + tid];
                 keep = C_NQ;
@@ -1089,7 +1147,9 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 if ((tid & 63u) == leader) base = atomicAdd(head + 32u * h, (uint32_t)__popcll(m));
                 base = __shfl(base, (int)leader);
                 const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                const uint64_t st = (uint64_t)dyn_base + (((uint64_t)(base + below) << hl2) + h) * R;
+                const uint64_t run = ((uint64_t)(base + below) << hl2) + h;
+                const uint64_t st = STREAM ? (run * min(8u, gridDim.x) + blockIdx.x % min(8u, gridDim.x)) * R
+                                           : (uint64_t)dyn_base + run * R;
                 if (st < xe) {
                     j = (uint32_t)st;
                     j_end = (uint32_t)min<uint64_t>(xe, st + R);
@@ -1098,6 +1158,17 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 }
             }
             if (!got) break;
+            if constexpr (STREAM) {
+                // the run's chunk (runs never straddle one) must have landed
+                const uint32_t ck = j >> ta.chunk_log2;
+                if (ck >= known) {
+                    if (!chunk_wait(ta.ready + ck, ta.wait_ticks)) {
+                        atomicOr(ta.stalled, 1u);
+                        break;
+                    }
+                    known = ck + 1u;
+                }
+            }
         }
         w.simt(0);
         // ---- the iteration's global accesses: one per lane (selected without branches), plus the
@@ -1125,13 +1196,26 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             w.edge_at(a0);
         }
         if (!(c & C_NQ) && j < j_end) {                           // prefetch the next pair
-            prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
+            if constexpr (STREAM) {
+                // requests j, j + 1 (j is even: runs are 4-aligned) in one 16-B load
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ta.pairs + j),
+                                                 reinterpret_cast<void*>(lds_nq + (tid & ~63u)), 16, 0, KETO_STREAM_CPOL);
+            } else {
+                prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
+            }
             c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
             w.request();
         }
         uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
         uint32_t cbw = NONE32, sgw = NONE32;
-        if (ph != P_REQ && ph != P_WALK) v0 = a0[0];
+        uint32_t xr = NO_UNIT, xt = NO_UNIT;                      // STREAM, P_XLT: the handles
+        if constexpr (STREAM) {
+            if (ph == P_XLT) {
+                if (eh < ta.n_rows) xr = ta.row_handle[eh];
+                if ((c & C_TSET) && (T & EDGE_VAL) < ta.n_rows) xt = ta.row_handle[T & EDGE_VAL];
+            }
+        }
+        if (ph != P_REQ && ph != P_WALK && (!STREAM || ph != P_XLT)) v0 = a0[0];
         if (hdr) v1 = a0[1];
         if (cbq) {
             // T's closure-filter word and T's child-signature word (both in the header's line)
@@ -1142,6 +1226,27 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         if (ph == P_REQ) {
             start_next();
             continue;
+        }
+        if constexpr (STREAM) {
+            if (ph == P_XLT) {                                    // as pairs_to_handles
+                const uint32_t qi = j - 1;
+                bool drop = false;
+                if (xr == NO_UNIT) {                              // another part's root row
+                    atomicAdd(ta.misrouted, 1u);
+                    drop = true;
+                } else if (c & C_TSET) {
+                    drop = xt == NO_UNIT;                         // no tuple has it as subject
+                    T = xt;
+                }
+                if (drop) {
+                    decide(qi, 0);
+                    start_next();
+                } else {
+                    eh = xr;
+                    c = bf_set(c, C_PH, 3, P_HDR);
+                }
+                continue;
+            }
         }
         w.simt(1);
         int res = -1;
@@ -2169,6 +2274,13 @@ struct DeviceState {
     uint32_t* ps_count = nullptr;     // [0] stashed, [1] tier-1 requests
     uint64_t ps_cap = 0;
     std::vector<hipEvent_t> ps_ev;    // per chunk: 3 timing events
+    // streamed host batches (device_check_stream): the whole batch's pairs, its chunks' ready words,
+    // its decisions and the handle form of the requests tier 0 hands up
+    keto_check_pair* st_pairs = nullptr;
+    uint8_t* st_dec = nullptr;
+    keto_check_ids* st_x = nullptr;
+    uint32_t* st_ready = nullptr;
+    uint64_t st_cap = 0;
 
     DevSnap view() const { return DevSnap{arena, coll, coll_mask, n_units}; }
 };
@@ -2275,6 +2387,15 @@ TierArgs tier_args(Tier& t, const uint32_t* in_list, const uint32_t* in_count, u
     a.in_count = in_count;
     a.out_list = out_list;
     a.out_count = out_count;
+    a.pairs = nullptr;
+    a.ready = nullptr;
+    a.chunk_log2 = 0;
+    a.row_handle = nullptr;
+    a.n_rows = 0;
+    a.pair_depth = 0;
+    a.misrouted = nullptr;
+    a.stalled = nullptr;
+    a.wait_ticks = 0;
     return a;
 }
 
@@ -2946,6 +3067,10 @@ void device_release(Snapshot& S) {
     for (hipEvent_t e : D.ex_ev)
         if (e) (void)hipEventDestroy(e);
     if (D.xlate) (void)hipFree(D.xlate);
+    if (D.st_pairs) (void)hipFree(D.st_pairs);
+    if (D.st_dec) (void)hipFree(D.st_dec);
+    if (D.st_x) (void)hipFree(D.st_x);
+    if (D.st_ready) (void)hipFree(D.st_ready);
     for (int i = 0; i < 2; ++i) {
         if (D.slot_q[i]) (void)hipFree(D.slot_q[i]);
         if (D.slot_x[i]) (void)hipFree(D.slot_x[i]);
@@ -2995,6 +3120,8 @@ Plan make_plan(const DeviceState& D, uint32_t n, int frames_needed) {
     p.slots[0] = (uint32_t)std::min<uint64_t>((uint64_t)hw_slots(), ((uint64_t)n + 255) / 256 * 256);
     if (p.slots[0] == 0) p.slots[0] = 256;
     p.cap[0] = std::min<uint32_t>(256, full);
+    if (const char* e = getenv("KETO_TEST_T0_CAP"))      // test hook: push shallow requests up the tiers
+        p.cap[0] = std::min<uint32_t>(full, pow2_at_least((uint32_t)std::max(16, atoi(e))));
     p.slots[1] = (uint32_t)std::min<uint64_t>(4096, ((uint64_t)n + 255) / 256 * 256);
     p.cap[1] = std::min<uint32_t>(1u << 15, full);
     // tier 2: tables that hold every visit id of the snapshot, as many lanes as 8 GiB allows (>= 1)
@@ -3217,6 +3344,15 @@ uint32_t t0_dyn(uint64_t n, uint64_t lanes) {
     while ((1 << (hl2 + 1)) <= heads) ++hl2;
     return v > 0 ? (std::min<uint32_t>((uint32_t)v + 3u, 0xFFFCu) & ~3u) | ((uint32_t)st << 16) | (hl2 << 20) : 0u;
 }
+// streamed batches: runs of 4 (a power of two, so no run straddles a chunk), all of them dealt by
+// the heads (no static part: a lane's static run could lie in the last chunk)
+uint32_t t0_stream_dyn() {
+    const char* hs = getenv("KETO_T0_HEADS");
+    const int heads = hs ? std::min(16, atoi(hs)) : 4;
+    uint32_t hl2 = 0;
+    while ((1 << (hl2 + 1)) <= heads) ++hl2;
+    return 4u | (hl2 << 20);
+}
 const char* t0_kernel_name(int var) {
     switch (var) {
         case 0: return "keto::check_wave_kernel<4, false, 4, 16, false>";
@@ -3236,6 +3372,7 @@ CheckKernelFn t0_kernel(int var, bool count) {
         default: return count ? check_wave_kernel<8, false, 8, 8, true> : check_wave_kernel<8, false, 8, 8, false>;
     }
 }
+CheckKernelFn t0_stream_kernel() { return check_wave_kernel<4, false, 4, 16, false, true>; }
 }  // namespace
 
 // deep batches (global max-depth 10..64) take deep_wave_kernel as tier 0 only with KETO_DEEP_WAVE=1:
@@ -3256,11 +3393,58 @@ const char* device_check_kernel_name(int32_t gmd) {
 
 namespace {
 
+// A streamed host batch (device_check_stream): tier 0 reads the 8-B pairs as their chunks land; the
+// requests it hands up are translated into `xlate` (at their batch index) for tiers 1 and 2
+struct StreamSrc {
+    const keto_check_pair* pairs = nullptr;
+    const uint32_t* ready = nullptr;
+    uint32_t chunk_log2 = 0;
+    int32_t depth = 0;
+    uint32_t* stalled = nullptr;
+    uint64_t wait_ticks = 0;
+    keto_check_ids* xlate = nullptr;
+};
+
+__device__ inline keto_check_ids pair_to_ids(const keto_check_pair p, int32_t depth, const uint32_t* __restrict__ table,
+                                             uint32_t n_rows, bool& misrouted) {
+    keto_check_ids q{KETO_NO_ROW, KETO_NO_TARGET, 0u, depth};
+    misrouted = false;
+    if (p.row != KETO_NO_ROW) {
+        const uint32_t h = p.row < n_rows ? table[p.row] : NO_UNIT;
+        misrouted = h == NO_UNIT;
+        q.row = h == NO_UNIT ? KETO_NO_ROW : h;
+    }
+    if (p.subject != KETO_NO_TARGET) {
+        if (p.subject & EDGE_SET) {
+            const uint32_t r = p.subject & EDGE_VAL;
+            const uint32_t h = r < n_rows ? table[r] : NO_UNIT;
+            q.target = h == NO_UNIT ? KETO_NO_TARGET : h;
+            q.flags = 1u;
+        } else {
+            q.target = p.subject;
+        }
+    }
+    return q;
+}
+
+// the streamed requests tier 0 handed up (list[0 .. *count)), translated in place of the batch
+__global__ void __launch_bounds__(256) list_pairs_to_handles(const keto_check_pair* __restrict__ in,
+                                                             const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                             keto_check_ids* __restrict__ out, int32_t depth,
+                                                             const uint32_t* __restrict__ table, uint32_t n_rows) {
+    const uint32_t m = *count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint32_t qi = list[i];
+        bool mis;
+        out[qi] = pair_to_ids(in[qi], depth, table, n_rows, mis);
+    }
+}
+
 // The check of one device-resident batch: the tier plan and the kernel launches.  The caller holds
-// D.mu and has set the device; `dq` / `da` are device buffers.
+// D.mu and has set the device; `dq` / `da` are device buffers (`ss`: a streamed batch, dq unused).
 void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t n, int32_t gmd, uint8_t* da,
                 hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate, uint32_t* d_steps,
-                PipeStash* stash, int wsi, const ItemWork* items) {
+                PipeStash* stash, int wsi, const ItemWork* items, const StreamSrc* ss = nullptr) {
     WorkSet& W = D.ws[wsi];
     if (S.part_mode == PART_MIGRATE)
         throw Error{KETO_E_INVALID, "a migrating part answers checks through keto_mig_begin / keto_mig_round"};
@@ -3291,11 +3475,15 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
         p.slots[2] = s2;
     }
     const bool dw = kind == 2 && deep_wave(gmd);
-    const int var = kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
+    if (ss && kind != 0) throw Error{KETO_E_INVALID, "streamed batches need max-depth <= 5"};
+    const int var = ss ? T0_VARIANTS + 3
+                       : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
-        if (dw)
+        if (ss)
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_stream_kernel(), 256, 0));
+        else if (dw)
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, deep_wave_kernel<8, 8, false>, 256, 0));
         else if (kind == 2)
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_kernel<GlobalStack, false, 0>, 256, 0));
@@ -3389,11 +3577,38 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
                   }
                   const uint32_t bs = std::min<uint32_t>(256, slots);
                   const dim3 grid(slots / bs), block(bs);
+                  const keto_check_ids* q = dq;
+                  if (ss && level == 1) {
+                      // the streamed requests tier 0 handed up, in the handle form the next tiers read
+                      hipLaunchKernelGGL(list_pairs_to_handles, dim3(1024), dim3(256), 0, st, ss->pairs, il, ic, ss->xlate,
+                                         ss->depth, D.row_handle, S.n_rows());
+                      HIP_OK(hipGetLastError());
+                  }
+                  if (ss && level >= 1) q = ss->xlate;
                   auto go = [&](auto kern) {
-                      hipLaunchKernelGGL(kern, grid, block, 0, st, sv, dov, dq, n, gmd, da, a, dwork);
+                      hipLaunchKernelGGL(kern, grid, block, 0, st, sv, dov, q, n, gmd, da, a, dwork);
                   };
                   const bool local = p.frames[level] == 0;
-                  if (level == 0 && kind < 2) {
+                  if (level == 0 && ss) {
+                      a.pairs = ss->pairs;
+                      a.ready = ss->ready;
+                      a.chunk_log2 = ss->chunk_log2;
+                      a.row_handle = D.row_handle;
+                      a.n_rows = S.n_rows();
+                      a.pair_depth = ss->depth;
+                      a.misrouted = W.counters + 4;
+                      a.stalled = ss->stalled;
+                      a.wait_ticks = ss->wait_ticks;
+                      a.dyn = t0_stream_dyn();
+                      if (!W.heads) {
+                          uint64_t acc = 0;
+                          W.heads = dmalloc<uint32_t>(KETO_HEAD_WORDS, acc);
+                      }
+                      HIP_OK(hipMemsetAsync(W.heads, 0, KETO_HEAD_WORDS * sizeof(uint32_t), st));
+                      a.heads = W.heads;
+                      go(t0_stream_kernel());
+                  }
+                  else if (level == 0 && kind < 2) {
                       a.dyn = t0_dyn(n, slots);
                       if (const char* wc = getenv("KETO_T0_WALK"))
                           if (atoi(wc) > 0) a.walk_cap = (uint32_t)atoi(wc);
@@ -3612,6 +3827,85 @@ void device_check(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t
     check_locked(S, D, d_reqs, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, work_out, false, d_steps);
 }
 
+namespace {
+
+// Streamed host batches: FORM_PAIRS from pinned memory, no overlay, max-depth <= 5, at least
+// KETO_STREAM_MIN requests (default 1M); KETO_STREAM=0 turns it off
+bool stream_ok(const Snapshot& S, uint32_t n, int32_t gmd, const Overlay* ovh) {
+    const char* e = getenv("KETO_STREAM");
+    if (e && atoi(e) == 0) return false;
+    const char* m = getenv("KETO_STREAM_MIN");
+    const uint64_t lo = m ? strtoull(m, nullptr, 10) : (1ull << 20);
+    return n >= std::max<uint64_t>(lo, 1) && !(ovh && !ovh->empty()) && std::max(1, std::min(gmd, 65535) - 1) <= 4 &&
+           S.part_mode != PART_MIGRATE;
+}
+
+// One tier-0 launch over the whole host batch, started before the requests have landed: the copy
+// stream moves chunks of 2^KETO_STREAM_CHUNK_LOG2 pairs (default 2^20 = 8 MB) in and marks each
+// landed with hipStreamWriteValue32; the kernel deals runs in batch order, waits for a run's chunk
+// and turns row ids into handles itself (P_XLT).  The chunked pipeline below pays a launch tail
+// and a translation pass per chunk (4 launches summed to 3.5 ms against 2.6 ms for one,
+// DESIGN.md "Measurement").  Returns false, with nothing decided, if a lane waited longer than
+// KETO_STREAM_WAIT_MS (default 1000) for a chunk: the caller then runs the chunked pipeline.
+bool check_streamed(Snapshot& S, DeviceState& D, const keto_check_pair* reqs, uint32_t n, int32_t gmd, uint8_t* allowed,
+                    int32_t depth) {
+    uint64_t acc = 0;
+    const char* ec = getenv("KETO_STREAM_CHUNK_LOG2");
+    const uint32_t cl = (uint32_t)std::min(26, std::max(16, ec ? atoi(ec) : 20));
+    const uint64_t chunks = ((uint64_t)n + (1ull << cl) - 1) >> cl;
+    if (D.st_cap < n) {
+        for (void* p : {(void*)D.st_pairs, (void*)D.st_dec, (void*)D.st_x, (void*)D.st_ready})
+            if (p) (void)hipFree(p);
+        D.st_pairs = nullptr;
+        D.st_dec = nullptr;
+        D.st_x = nullptr;
+        D.st_ready = nullptr;
+        D.st_cap = 0;
+        D.st_pairs = dmalloc<keto_check_pair>((uint64_t)n + 4, acc);       // + the pair a 16-B load reads past an odd end
+        D.st_dec = dmalloc<uint8_t>(((uint64_t)n + 3) & ~3ull, acc);
+        D.st_x = dmalloc<keto_check_ids>(n, acc);
+        D.st_ready = dmalloc<uint32_t>(((uint64_t)n >> 16) + 2, acc);
+        D.st_cap = n;
+    }
+    WorkSet& W = D.ws[0];
+    ensure_lists(W, n);
+    uint32_t* d_bad = W.counters + 4;                                         // [4] misrouted, [5] stalled
+    translate_rows_locked(S, D, nullptr, nullptr, 0, D.stream, d_bad);      // the row -> handle table
+    HIP_OK(hipMemsetAsync(W.counters + 4, 0, 2 * sizeof(uint32_t), D.stream));
+    HIP_OK(hipMemsetAsync(D.st_ready, 0, chunks * sizeof(uint32_t), D.stream));
+    HIP_OK(hipEventRecord(D.pev[6], D.stream));
+    HIP_OK(hipStreamWaitEvent(D.copy_in, D.pev[6], 0));
+    const bool drop = getenv("KETO_STREAM_TEST_DROP") != nullptr;           // test hook: the last chunk is never marked
+    for (uint64_t c = 0; c < chunks; ++c) {
+        const uint64_t lo = c << cl, len = std::min<uint64_t>(n, lo + (1ull << cl)) - lo;
+        HIP_OK(hipMemcpyAsync(D.st_pairs + lo, reqs + lo, len * sizeof(keto_check_pair), hipMemcpyHostToDevice, D.copy_in));
+        if (!(drop && c + 1 == chunks)) HIP_OK(hipStreamWriteValue32(D.copy_in, D.st_ready + c, 1u, 0));
+    }
+    const char* ew = getenv("KETO_STREAM_WAIT_MS");
+    StreamSrc ss;
+    ss.pairs = D.st_pairs;
+    ss.ready = D.st_ready;
+    ss.chunk_log2 = cl;
+    ss.depth = depth;
+    ss.stalled = W.counters + 5;
+    ss.wait_ticks = (uint64_t)std::max(1, ew ? atoi(ew) : 1000) * 100000ull;   // wall clock: 100 MHz
+    ss.xlate = D.st_x;
+    check_core(S, D, nullptr, n, gmd, D.st_dec, D.stream, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, false, nullptr,
+               nullptr, 0, nullptr, &ss);
+    HIP_OK(hipStreamSynchronize(D.copy_in));
+    uint32_t flags[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(flags, W.counters + 4, sizeof(flags), hipMemcpyDeviceToHost, D.stream));
+    HIP_OK(hipStreamSynchronize(D.stream));
+    if (flags[1]) return false;
+    if (flags[0]) throw Error{KETO_E_INVALID, std::to_string(flags[0]) + " requests name root rows another part owns"};
+    HIP_OK(hipMemcpyAsync(allowed, D.st_dec, n, hipMemcpyDeviceToHost, D.stream));
+    HIP_OK(hipStreamSynchronize(D.stream));
+    D.last.chunks = (uint32_t)chunks;
+    return true;
+}
+
+}  // namespace
+
 // Host-buffer batches: the requests go to the device in chunks of KETO_CHUNK (default 4M), so the
 // H2D copy of chunk c + 1 (copy_in stream) and the D2H copy of chunk c - 1 (copy_out) overlap the
 // check of chunk c (the check stream).  Two device slots alternate.  Pinned caller buffers
@@ -3630,6 +3924,13 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     const auto t_start = std::chrono::steady_clock::now();
     D.last = keto_batch_timing{};
     if (n == 0) return;
+    if (form == FORM_PAIRS && stream_ok(S, n, gmd, ovh) && host_pinned(reqs) && host_pinned(allowed)) {
+        if (check_streamed(S, D, reinterpret_cast<const keto_check_pair*>(reqs), n, gmd, allowed, pair_depth)) {
+            D.last.wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+            return;
+        }
+        D.last = keto_batch_timing{};                    // a chunk did not land in time: the pipeline below
+    }
     OverlayBuf ov(S, ovh);
     const uint64_t C = std::min<uint64_t>(n, chunk_requests());
     const uint64_t C0 = first_chunk_requests(C);        // chunk 0; then chunks of C
