@@ -636,9 +636,9 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
     V.V.count = 0;
-    if constexpr (TIER == 2) V.V.base = s.n_units;
+    if constexpr (TIER == 2) V.V.base = min(s.n_units, EDGE_VAL);   // set visit ids are targets' handles (< 2^31)
     if constexpr (TIER < 2) {
-        V.V.base = s.n_units;
+        V.V.base = min(s.n_units, EDGE_VAL);   // set visit ids are targets' handles (< 2^31)
         V.V.hint = slot;
         V.V.dcount = 0;
         V.V.pool = ta.pool;
@@ -702,7 +702,8 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             w.request();
             int d = qq.max_depth;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            if (qq.row == KETO_NO_ROW || d <= 0 || qq.target == KETO_NO_TARGET) {
+            // (a subject set no tuple has as subject -- past 2^31 units, not a target -- is never allowed)
+            if (qq.row == KETO_NO_ROW || d <= 0 || qq.target == KETO_NO_TARGET || ((qq.flags & 1u) && qq.target >= EDGE_VAL)) {
                 allowed[qi] = 0;
                 continue;
             }
@@ -907,17 +908,22 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
 // A request needing more than F saved frames, or a row with more than WF_LEFT_MAX edges left when
 // saved, overflows to the next tier (check_kernel).  Lane control state is one packed word.
 constexpr uint32_t P_REQ = 0, P_HDR = 1, P_IDQ = 2, P_EDGE = 3, P_WALK = 4;
-constexpr uint32_t WF_LEFT_MAX = (1u << 19) - 1u;   // saved lkf = left | skip << 19 | k << 23 | seg << 27 | fl << 28
+constexpr uint32_t WF_LEFT_MAX = (1u << 18) - 1u;   // saved lkf = left | skip << 18 | k << 22 | seg << 26 | fl << 28
 // control word: phase 0..2 | k 3..7 | fl 8..11 | sp 12..15 | have 16 | nq 17 | tset 18 | hl 19..23 | nq2 24
 // | cb 25 (the current row has a closure filter, so its id table starts CB_WORDS further down)
-// | seg 26 (the current row lies in arena segment 1: positions are 32-bit words within a segment)
+// | seg 26, 31 (bits 0 and 1 of the current row's arena segment: positions are 32-bit words within
+//   a segment)
 // | skip 27..30 (window slot i's subject set is ruled out by the row's child signatures; cleared
 //   when the walk leaves the row's first block)
 constexpr uint32_t C_PH = 0, C_K = 3, C_FL = 8, C_SP = 12, C_HL = 19, C_MK = 27;
 constexpr uint32_t C_HAVE = 1u << 16, C_NQ = 1u << 17, C_TSET = 1u << 18, C_NQ2 = 1u << 24, C_CB = 1u << 25;
-constexpr uint32_t C_SEG = 1u << 26, C_MKS = 15u << C_MK;
-// saved frame word: left 0..18 | skip 19..22 | k 23..26 (tier 0 runs max-depth <= 9) | seg 27 | fl 28..31
+constexpr uint32_t C_SEG = 1u << 26, C_SEG2 = 1u << 31, C_MKS = 15u << C_MK;
+// saved frame word: left 0..17 | skip 18..21 | k 22..25 (tier 0 runs max-depth <= 9) | seg 26..27 | fl 28..31
 __device__ inline uint32_t bf(uint32_t c, uint32_t off, uint32_t wd) { return (c >> off) & ((1u << wd) - 1u); }
+__device__ inline uint32_t c_seg(uint32_t c) { return ((c >> 26) & 1u) | ((c >> 30) & 2u); }
+__device__ inline uint32_t c_with_seg(uint32_t c, uint32_t seg) {
+    return (c & ~(C_SEG | C_SEG2)) | ((seg & 1u) << 26) | ((seg & 2u) << 30);
+}
 __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_t v) {
     const uint32_t m = ((1u << wd) - 1u) << off;
     return (c & ~m) | ((v << off) & m);
@@ -1119,7 +1125,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             }
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
+            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET || ((nq.z & 1u) && nq.y >= EDGE_VAL)) {
                 decide(qi, 0);
                 c = keep;
                 continue;
@@ -1175,8 +1181,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         // next request pair's prefetch
         const bool hdr = ph == P_HDR;
         const bool in_ov = hdr ? eh >= ov.base : (bf(c, C_FL, 4) & FR_OV) != 0;
-        const bool hi = hdr ? ((eh >> SEG_SHIFT) & 1u) != 0 : (c & C_SEG) != 0;
-        const uint32_t* const ar = (in_ov ? ov.arena : s.arena) + ((hi && !in_ov) ? (1ull << 32) : 0ull);
+        const uint32_t seg = in_ov ? 0u : hdr ? (eh >> SEG_SHIFT) : c_seg(c);
+        const uint32_t* const ar = (in_ov ? ov.arena : s.arena) + ((uint64_t)seg << 32);
         const uint32_t hl = bf(c, C_HL, 5);
         const uint32_t word = hdr ? (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS
                                   : ph == P_IDQ ? pos - HDR_WORDS - ((c & C_CB) ? CB_WORDS : 0u) - (1u << hl) +
@@ -1235,7 +1241,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                     atomicAdd(ta.misrouted, 1u);
                     drop = true;
                 } else if (c & C_TSET) {
-                    drop = xt == NO_UNIT;                         // no tuple has it as subject
+                    drop = xt >= EDGE_VAL;                        // no tuple has it as subject (NO_UNIT too)
                     T = xt;
                 }
                 if (drop) {
@@ -1282,8 +1288,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                     // the window's skip bits go with it (a saved single edge: its own, as slot 0)
                     const uint32_t mk = !WIN && (fl & FR_WV) && left == 1 ? (c >> (C_MK + (pos & 3u))) & 1u : bf(c, C_MK, 4);
                     sf_pk[sp * LDS_STRIDE + tid] =
-                        make_uint2(px, left | (mk << 19) | (bf(c, C_K, 5) << 23) | ((c & C_SEG) ? (1u << 27) : 0u) |
-                                           (fl << 28));
+                        make_uint2(px, left | (mk << 18) | (bf(c, C_K, 5) << 22) | (c_seg(c) << 26) | (fl << 28));
                     if constexpr (WIN) sf_win[sp * LDS_STRIDE + tid] = win;
                     c = bf_set(c, C_SP, 4, sp + 1);
                     w.push();
@@ -1300,7 +1305,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 win = v1;
                 c = bf_set(bf_set(bf_set(bf_set(c, C_K, 5, k), C_FL, 4, fl), C_HL, 5, hl), C_PH, 3, P_WALK) | C_HAVE;
                 c = (v0.z & HDR_CLOSURE) ? (c | C_CB) : (c & ~C_CB);
-                c = (!is_ov && ((eh >> SEG_SHIFT) & 1u)) ? (c | C_SEG) : (c & ~C_SEG);
+                c = c_with_seg(c, is_ov ? 0u : eh >> SEG_SHIFT);
                 // window slots whose subject set cannot reach T (child signatures, read entering a
                 // subject set; never for a subject-set request)
                 const uint32_t skip = (have && !tset && (v0.z & HDR_CLOSURE)) ? ~(sgw >> ((cbit & 7u) * 4u)) & 15u : 0u;
@@ -1372,9 +1377,9 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                     pos = pk.x;
                 }
                 left = pk.y & WF_LEFT_MAX;
-                c = bf_set(bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 23) & 15u), C_FL, 4, pk.y >> 28), C_MK,
-                           4, pk.y >> 19);
-                c = ((pk.y >> 27) & 1u) ? (c | C_SEG) : (c & ~C_SEG);
+                c = bf_set(bf_set(bf_set(bf_set(c, C_SP, 4, sp), C_K, 5, (pk.y >> 22) & 15u), C_FL, 4, pk.y >> 28), C_MK,
+                           4, pk.y >> 18);
+                c = c_with_seg(c, (pk.y >> 26) & 3u);
                 w.pop();
                 continue;
             }
@@ -1555,7 +1560,7 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             }
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
+            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET || ((nq.z & 1u) && nq.y >= EDGE_VAL)) {
                 decide(qi, 0);
                 c = keep;
                 continue;
@@ -2417,8 +2422,9 @@ void host_parallel_for(uint64_t n, F f) {
 // closure filter starts as the row's own ids (all bits for a ROW_SEQ row); closure_pass adds the
 // closures of its subject sets on the device, then sig_pass its child signatures.
 void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uint32_t hlog2, const uint32_t* edges,
-             uint64_t n_stored, const std::vector<uint32_t>& unit_of_row, bool closure) {
-    uint64_t h = (uint64_t)unit * HDR_WORDS;
+             uint64_t n_stored, const std::vector<uint32_t>& unit_of_row, bool closure, uint64_t base = 0) {
+    // `arena` holds the arena's words from `base` on
+    uint64_t h = (uint64_t)unit * HDR_WORDS - base;
     const bool seq = ((rec.hi_flags >> 8) & ROW_SEQ) != 0;
     arena[h + 0] = rec.n_sets;
     arena[h + 1] = rec.n_ids;
@@ -2679,8 +2685,12 @@ void device_upload(Snapshot& S, int device) {
     D->device = device;
     uint64_t acc = 0;
     const uint64_t words = S.n_units * HDR_WORDS;
-    if (words > (2ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^33 words (32 GiB)"};
-    std::vector<uint32_t> arena(std::max<uint64_t>(words, 4));
+    if (words > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
+    // a split layout's reserve [tgt_tail, roots_at) is not built on the host: the targets below it
+    // and the roots above it are two host pieces
+    const bool split = S.tgt_end > 0;
+    const uint64_t lo_words = split ? S.tgt_tail : words, hi_base = split ? S.roots_at : words;
+    std::vector<uint32_t> arena(std::max<uint64_t>(lo_words, 4)), arena_hi(split ? words - hi_base : 0);
     const uint32_t R = S.n_rows();
     host_parallel_for(R, [&](uint64_t r) {
         if (!S.mapped((uint32_t)r)) return;                  // another part's row
@@ -2696,13 +2706,20 @@ void device_upload(Snapshot& S, int device) {
             return;
         }
         const auto ed = S.row_edges((uint32_t)r);
-        put_row(arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r), ed.first, ed.second,
-                S.unit_of_row, S.row_cb[r] != 0);
+        const bool hi = split && (uint64_t)S.unit_of_row[r] * HDR_WORDS >= hi_base;
+        put_row(hi ? arena_hi.data() : arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r),
+                ed.first, ed.second, S.unit_of_row, S.row_cb[r] != 0, hi ? hi_base : 0);
     });
     // room at the tail for rows writes move (keto_snapshot_apply; grown on demand)
-    D->arena_words = std::min<uint64_t>(2ull << 32, arena.size() + std::max<uint64_t>(arena.size() / 16, 1ull << 20));
+    const uint64_t used = std::max<uint64_t>(words, 4);
+    D->arena_words = std::min<uint64_t>(ARENA_MAX_WORDS, used + std::max<uint64_t>(used / 16, 1ull << 20));
     D->arena = dmalloc<uint32_t>(D->arena_words, acc);
     HIP_OK(hipMemcpy(D->arena, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (split) {
+        HIP_OK(hipMemcpy(D->arena + hi_base, arena_hi.data(), arena_hi.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        // the reserve's slots are read 32 B at a time like any header slot once writes fill them
+        HIP_OK(hipMemset(D->arena + lo_words, 0, (hi_base - lo_words) * sizeof(uint32_t)));
+    }
     build_closures(S, D->arena);
     S.mig_ready = !(S.part_mode == PART_MIGRATE && S.n_parts > 1);   // else after the filter exchange
     upload_coll(S, *D, acc);
@@ -2824,28 +2841,27 @@ void part_closure_done(Snapshot& S, bool converged) {
 }
 
 namespace {
-// A tail place for a row (the same line rules as compute_layout): returns its header unit.
+// A tail place for a row (the same line and segment rules as compute_layout): returns its header
+// unit.  A subject-set target (cb) needs a handle below 2^31: in a split layout it goes into the
+// target reserve, else to the tail while that is low enough; without room the caller must rebuild
+// (compute_layout places it among the targets).
 uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint64_t& total_words) {
     const uint64_t table = hlog2 ? (1ull << hlog2) : 0;
     const uint64_t c = cb ? CB_WORDS : 0;
-    const uint64_t slot = c + HDR_WORDS + WINDOW_WORDS;
-    const uint64_t total = table + c + HDR_WORDS + ((n_edges + 3) & ~3ull);
-    const uint64_t fit = std::max(total, table + slot);
-    auto align = [&](uint64_t x) {
-        if (fit <= LINE_WORDS) {
-            if (x % LINE_WORDS + fit > LINE_WORDS) x = (x + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
-        } else {
-            const uint64_t o = (x + table) % LINE_WORDS;
-            if (o + slot > LINE_WORDS) x += LINE_WORDS - o;
-        }
-        return x;
-    };
-    uint64_t w = align(S.n_units * HDR_WORDS);
-    if (w < (1ull << 32) && w + fit > (1ull << 32)) w = align(1ull << 32);
+    if (cb && S.tgt_end) {
+        const uint64_t w = arena_fit(S.tgt_tail, table, c, n_edges, total_words);
+        if (w + total_words > S.tgt_end)
+            throw Error{KETO_E_REBUILD, "the arena's reserve for new subject-set targets is full: rebuild the snapshot"};
+        S.tgt_tail = w + total_words;
+        return (uint32_t)((w + table + c) / HDR_WORDS);
+    }
+    const uint64_t w = arena_fit(S.n_units * HDR_WORDS, table, c, n_edges, total_words);
     const uint64_t unit = (w + table + c) / HDR_WORDS;
-    if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
-    S.n_units = (w + total) / HDR_WORDS;
-    total_words = total;
+    if (cb && unit >= (uint64_t)EDGE_VAL)
+        throw Error{KETO_E_REBUILD, "a new subject-set target would lie past 2^31 16-byte units: rebuild the snapshot"};
+    if (w + total_words > ARENA_MAX_WORDS || unit >= HANDLE_MAX)
+        throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
+    S.n_units = (w + total_words) / HDR_WORDS;
     return (uint32_t)unit;
 }
 }  // namespace
@@ -2858,8 +2874,10 @@ uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint
 // resolved before.  Closure filters are then re-closed on the device from their rows' own ids
 // (filters of other rows only ever lose precision: a deleted id's bit may stay, never a needed one
 // go missing).  Runs under the snapshot's device lock, between batches.
-void device_apply(Snapshot& S) {
-    if (!S.dev) return;
+namespace {
+// device_apply in place; false (nothing written to the device yet) when a new subject-set target
+// finds no place below 2^31 units
+bool apply_in_place(Snapshot& S) {
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));
@@ -2909,13 +2927,22 @@ void device_apply(Snapshot& S) {
     }
     std::sort(fresh.begin(), fresh.end());
     fresh.erase(std::unique(fresh.begin(), fresh.end()), fresh.end());
+    // a fresh row some subject set points at gets a closure block and a handle below 2^31 (a target);
+    // one nothing points at yet (a new root row) goes to the tail like a root of the build, and
+    // moves to a target's place once a set points at it (needs_cb)
     for (uint32_t r : fresh) {
+        const bool tgt = !S.is_root[r];
         uint64_t tw = 0;
-        const uint32_t u = tail_place(S, S.row_hlog2(r), true, S.row_edges(r).second, tw);
+        uint32_t u = 0;
+        try {
+            u = tail_place(S, S.row_hlog2(r), tgt, S.row_edges(r).second, tw);
+        } catch (const Error& e) {
+            if (e.code == KETO_E_REBUILD) return false;
+            throw;
+        }
         S.unit_of_row[r] = u;
-        S.row_cb[r] = 1;
-        S.is_root[r] = 0;
-        S.row_place[r] = Snapshot::RowPlace{u, S.row_hlog2(r), (S.row_edges(r).second + 3) & ~3ull, true};
+        S.row_cb[r] = tgt;
+        S.row_place[r] = Snapshot::RowPlace{u, S.row_hlog2(r), (S.row_edges(r).second + 3) & ~3ull, tgt};
         S.layout_units.push_back(u);
         S.rows_by_unit.push_back(r);
     }
@@ -2934,7 +2961,7 @@ void device_apply(Snapshot& S) {
         const uint64_t cap = (S.row_edges(r).second + 3) & ~3ull;
         Snapshot::RowPlace& pl = S.row_place[r];
         if (is_fresh[r]) {
-            image(r, id, true);
+            image(r, id, S.row_cb[r] != 0);
         } else if (pl.hlog2 == hl && pl.edge_cap >= cap) {
             image(r, pl.unit, pl.cb);                         // fits where it is
             if (pl.unit != id && S.row_cb[r]) {               // a forwarded row: re-seed the identity filter
@@ -2980,10 +3007,10 @@ void device_apply(Snapshot& S) {
     for (auto& m : moved) forward(m.second, S.unit_of_row[m.first], false);   // stale top-level handles
     // 3. room: grow the arena if the tail outgrew it (handles are word offsets: copied as is)
     const uint64_t need = S.n_units * HDR_WORDS;
-    if (need > (2ull << 32)) throw Error{KETO_E_RANGE, "device arena exceeds 2^33 words (32 GiB)"};
+    if (need > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
     if (need > D.arena_words) {
         // (slack past the last row: the kernels read a header's 32-B slot, window included)
-        const uint64_t cap = std::min<uint64_t>(2ull << 32, std::max<uint64_t>(need + 1024, D.arena_words + D.arena_words / 4));
+        const uint64_t cap = std::min<uint64_t>(ARENA_MAX_WORDS, std::max<uint64_t>(need + 1024, D.arena_words + D.arena_words / 4));
         uint64_t acc = 0;
         uint32_t* na = dmalloc<uint32_t>(cap, acc);
         HIP_OK(hipMemcpy(na, D.arena, D.arena_words * sizeof(uint32_t), hipMemcpyDeviceToDevice));
@@ -3029,6 +3056,22 @@ void device_apply(Snapshot& S) {
             (void)hipFree(*p);
             *p = nullptr;
         }
+    S.dirty.clear();
+    S.needs_cb.clear();
+    return true;
+}
+}  // namespace
+
+void device_apply(Snapshot& S) {
+    if (!S.dev) return;
+    if (apply_in_place(S)) return;
+    // a new subject-set target found no place below 2^31 units (the split layout's reserve is full,
+    // or an unsplit arena's tail is past it): lay the arena out afresh, as a build would, and upload
+    // it again (handles are per version)
+    const int dev = S.dev->device;
+    device_release(S);
+    compute_layout(S);
+    device_upload(S, dev);
     S.dirty.clear();
     S.needs_cb.clear();
 }
@@ -3464,7 +3507,7 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     {
         // tier 2 keeps one 16-bit epoch per possible visit id (DirectVisited): 2 B per arena unit
         // and collision class, as many lanes (<= 256, a power of two) as 16 GiB allows
-        const uint64_t ids = (uint64_t)D.n_units + D.n_coll + 1;
+        const uint64_t ids = (uint64_t)std::min<uint32_t>(D.n_units, EDGE_VAL) + D.n_coll + 1;
         if ((ids + 3) / 4 > 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "tier-2 visited table exceeds 2^32 words"};
         p.cap[2] = (uint32_t)((ids + 3) / 4);
         const uint64_t per = (uint64_t)p.cap[2] * sizeof(uint64_t);
@@ -3474,7 +3517,8 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
         while (s2 * 2 <= want) s2 *= 2;
         p.slots[2] = s2;
     }
-    const bool dw = kind == 2 && deep_wave(gmd);
+    // (deep_wave_kernel keeps one segment bit: arenas of up to 2 segments)
+    const bool dw = kind == 2 && deep_wave(gmd) && (uint64_t)D.n_units <= (1ull << 31);
     if (ss && kind != 0) throw Error{KETO_E_INVALID, "streamed batches need max-depth <= 5"};
     const int var = ss ? T0_VARIANTS + 3
                        : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
@@ -3668,7 +3712,10 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                   hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
                   uint32_t* d_steps = nullptr, PipeStash* stash = nullptr, int wsi = 0) {
     const int32_t g = std::min<int32_t>(gmd, 65535);
-    const bool deep = n > 0 && g - 1 > 8 && !deep_wave(g) && S.part_mode != PART_MIGRATE;
+    // (the reachability pretest's indexes keep handles in 31 bits: arenas whose roots lie past 2^31
+    // units check deep batches without it)
+    const bool deep = n > 0 && g - 1 > 8 && !(deep_wave(g) && (uint64_t)D.n_units <= (1ull << 31)) &&
+                      S.part_mode != PART_MIGRATE && (uint64_t)D.n_units <= (uint64_t)EDGE_VAL;
     ItemWork iw;
     if (!deep || !reach_split(S, dq, n, gmd, da, dov.base, st, d_steps != nullptr, iw)) {
         check_core(S, D, dq, n, gmd, da, st, dov, work_out, accumulate, d_steps, stash, wsi, nullptr);
@@ -4170,6 +4217,15 @@ __global__ void __launch_bounds__(256) handles_to_rows_direct(keto_tree_node* __
     if (h >= ov_units_base) return;
     nodes[i].subject = EDGE_SET | unit_row[h];
 }
+// arenas with root rows past 2^31 units: a tree's root node lost its handle's bit 31 to EDGE_SET, so
+// it takes its row from the request (overlay roots: the host, below)
+__global__ void __launch_bounds__(256) root_rows_of_trees(keto_tree_node* __restrict__ nodes, const uint64_t* __restrict__ off,
+                                                          const ExpandReq* __restrict__ q, const uint32_t* __restrict__ unit_row,
+                                                          uint32_t n, uint32_t n_units) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !(q[i].flags & 1u) || off[i + 1] == off[i] || q[i].root >= n_units) return;
+    nodes[off[i]].subject = EDGE_SET | unit_row[q[i].root];
+}
 __global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restrict__ nodes, uint64_t n,
                                                        const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
                                                        uint32_t n_rows, uint32_t ov_units_base) {
@@ -4470,7 +4526,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                          hipMemcpyHostToDevice));
         // the direct map (one word per arena unit) when it is small next to the arena; else the
         // handle -> row translation binary-searches the handle list
-        if (S.n_units && S.n_units * sizeof(uint32_t) <= (8ull << 30)) {
+        if (S.n_units && S.n_units <= (1ull << 32)) {
             D.unit_row = dmalloc<uint32_t>(S.n_units, acc);
             const uint32_t m32 = (uint32_t)S.layout_units.size();
             if (m32)
@@ -4503,6 +4559,13 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         hipLaunchKernelGGL(handles_to_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes, total,
                            D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
     HIP_OK(hipGetLastError());
+    const bool high_roots = S.n_units > (uint64_t)EDGE_VAL;
+    if (high_roots) {
+        if (!D.unit_row) throw Error{KETO_E_RANGE, "expand over an arena past 2^31 units needs the direct unit map"};
+        hipLaunchKernelGGL(root_rows_of_trees, dim3((n + 255) / 256), dim3(256), 0, st, D.ex_nodes, doff, dq, D.unit_row,
+                           n, (uint32_t)S.n_units);
+        HIP_OK(hipGetLastError());
+    }
     lap("h2rows");
     HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -4514,7 +4577,13 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     }
     if (trace) fprintf(stderr, "[expand] %u of %u trees filled by the second pass\n", unstaged, n);
     // overlay handles -> ovh->base + overlay index (batch-local wildcard roots only)
-    if (ovh && !ovh->empty())
+    if (ovh && !ovh->empty() && high_roots) {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (!root_flags[i] || out.offset[i + 1] == out.offset[i] || root[i] < S.n_units) continue;
+            auto it = std::lower_bound(ovh->unit.begin(), ovh->unit.end(), (uint32_t)(root[i] - S.n_units));
+            out.nodes[out.offset[i]].subject = EDGE_SET | (ovh->base + (uint32_t)(it - ovh->unit.begin()));
+        }
+    } else if (ovh && !ovh->empty())
         host_parallel_for(total, [&](uint64_t i) {
             keto_tree_node& x = out.nodes[i];
             if (!(x.subject & EDGE_SET)) return;

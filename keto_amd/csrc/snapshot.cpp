@@ -322,7 +322,7 @@ uint32_t overlay_row(const Snapshot& S, Overlay& ov, const RowKey& k) {
     ov.map.emplace(k, id);
     ov.unit.push_back((uint32_t)ov.n_units);                  // overlay rows: header + edges, no table
     ov.n_units += 1 + (n + 3) / 4;
-    if (S.n_units + ov.n_units >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "overlay exceeds the handle space"};
+    if (S.n_units + ov.n_units >= (uint64_t)HANDLE_MAX) throw Error{KETO_E_RANGE, "overlay exceeds the handle space"};
     return id;
 }
 
@@ -342,12 +342,34 @@ uint32_t Snapshot::row_hlog2(uint32_t r) const {
     return std::max<uint32_t>(2, ceil_log2(2ull * x.n_ids));                      // load <= 1/2, >= 1 bucket
 }
 
+uint64_t arena_fit(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, uint64_t& total) {
+    // line placement: a row that fits in a 128-B line never straddles one (closure filter, header,
+    // window and id table come in with one miss); a bigger row keeps closure filter + header +
+    // window in one line
+    const uint64_t slot = cb + HDR_WORDS + WINDOW_WORDS;         // read together on a visit
+    total = table + cb + HDR_WORDS + ((n_edges + 3) & ~3ull);
+    const uint64_t fit = std::max(total, table + slot);          // a short row's window included
+    auto align = [&](uint64_t x) {
+        if (fit <= LINE_WORDS) {
+            if (x % LINE_WORDS + fit > LINE_WORDS) x = (x + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
+        } else {
+            const uint64_t o = (x + table) % LINE_WORDS;         // closure filter + header + window
+            if (o + slot > LINE_WORDS) x += LINE_WORDS - o;
+        }
+        return x;
+    };
+    w = align(w);
+    if ((w >> 32) != ((w + fit - 1) >> 32)) w = align(((w >> 32) + 1) << 32);   // rows stay in a segment
+    return w;
+}
+
 namespace {
 // The arena layout of one part: which rows it holds, where, and (PART_MIGRATE) its stubs.
 struct PartLayout {
     std::vector<uint32_t> unit_of_row, rows_by_unit, layout_units;
     std::vector<uint8_t> stub;
     uint64_t n_units = 0, shared_words = 0, n_stubs = 0, hot_words = 0, hot_rows = 0;
+    uint64_t tgt_tail = 0, tgt_end = 0, roots_at = 0;
 };
 
 // hot_band (PART_MIGRATE): rows of in-degree band >= hot_band are kept on every part; sorted
@@ -404,32 +426,44 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
     // segment boundary at 2^32 words (tests/test_gpu_synth.py)
     uint64_t w = 0;
     if (const char* base = getenv("KETO_TEST_ARENA_BASE")) w = strtoull(base, nullptr, 0) & ~(uint64_t)(LINE_WORDS - 1);
+    // test hook: a split layout whose root rows start at this word (tests/test_gpu_arena_split.py)
+    const char* root_base = getenv("KETO_TEST_ROOT_BASE");
+    // the root rows' words, to see whether the layout must split (roots come last)
+    uint64_t root_words = 0;
+    for (uint64_t x = 0; x < kept; ++x) {
+        const uint32_t r = L.rows_by_unit[x];
+        if (!S.is_root[r] || !keep[r]) continue;
+        const uint32_t h = S.row_hlog2(r);
+        root_words += (h ? (1ull << h) : 0) + HDR_WORDS + ((row_size(S, r) + 3) & ~3ull) + LINE_WORDS;   // + alignment
+    }
+    L.tgt_tail = L.tgt_end = L.roots_at = 0;
+    // test hook: the target reserve's size in words (a small one fills after a few writes)
+    const char* reserve_words = getenv("KETO_TEST_TGT_RESERVE");
+    bool in_roots = false;
     for (uint64_t x = 0; x < kept; ++x) {
         const uint32_t r = L.rows_by_unit[x];
         const bool stub = !keep[r];                                  // header + closure block only
+        if (S.is_root[r] && !stub && !in_roots) {
+            in_roots = true;
+            if (root_base || w + root_words > TARGET_MAX_WORDS) {
+                // split: targets end here; a reserve for targets writes add, then the roots
+                if (mode == PART_MIGRATE) throw Error{KETO_E_RANGE, "a migrating part's arena exceeds 2^31 16-byte units"};
+                L.tgt_tail = w;
+                const uint64_t reserve = reserve_words ? strtoull(reserve_words, nullptr, 0) : std::max<uint64_t>(1ull << 20, w / 8);
+                L.tgt_end = std::min<uint64_t>(TARGET_MAX_WORDS, w + reserve);
+                L.roots_at = std::max<uint64_t>(L.tgt_end, root_base ? strtoull(root_base, nullptr, 0) & ~(uint64_t)(LINE_WORDS - 1) : 0);
+                w = L.roots_at;
+            }
+        }
         const uint32_t h = stub ? 0 : S.row_hlog2(r);
         const uint64_t table = h ? (1ull << h) : 0;
-        const uint64_t n = stub ? 0 : row_size(S, r);
-        // line placement: a row that fits in a 128-B line never straddles one (closure filter,
-        // header, window and id table come in with one miss); a bigger row keeps closure filter +
-        // header + window in one line
         const uint64_t cb = S.is_root[r] ? 0 : CB_WORDS;          // closure filter
-        const uint64_t slot = cb + HDR_WORDS + WINDOW_WORDS;         // read together on a visit
-        const uint64_t total = table + cb + HDR_WORDS + ((n + 3) & ~3ull);
-        const uint64_t fit = std::max(total, table + slot);          // a short row's window included
-        auto align = [&](uint64_t x) {
-            if (fit <= LINE_WORDS) {
-                if (x % LINE_WORDS + fit > LINE_WORDS) x = (x + LINE_WORDS - 1) / LINE_WORDS * LINE_WORDS;
-            } else {
-                const uint64_t o = (x + table) % LINE_WORDS;         // closure filter + header + window
-                if (o + slot > LINE_WORDS) x += LINE_WORDS - o;
-            }
-            return x;
-        };
-        w = align(w);
-        if (w < (1ull << 32) && w + fit > (1ull << 32)) w = align(1ull << 32);   // rows stay in a segment
+        uint64_t total = 0;
+        w = arena_fit(w, table, cb, stub ? 0 : row_size(S, r), total);
         const uint64_t unit = (w + table + cb) / HDR_WORDS;
-        if (unit >= (uint64_t)EDGE_VAL) throw Error{KETO_E_RANGE, "device arena exceeds 2^31 16-byte units"};
+        if (!S.is_root[r] || stub ? unit >= (uint64_t)EDGE_VAL : unit >= HANDLE_MAX)
+            throw Error{KETO_E_RANGE, S.is_root[r] && !stub ? "device arena exceeds 2^32 16-byte units"
+                                                            : "subject-set targets exceed 2^31 16-byte units"};
         L.unit_of_row[r] = (uint32_t)unit;
         L.layout_units[x] = (uint32_t)unit;
         if (!S.is_root[r] && !stub) L.shared_words += total;
@@ -439,6 +473,9 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
             ++L.hot_rows;
         }
     }
+    if (w > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
+    if (mode == PART_MIGRATE && w > TARGET_MAX_WORDS)
+        throw Error{KETO_E_RANGE, "a migrating part's arena exceeds 2^31 16-byte units"};
     L.n_units = w / HDR_WORDS;
 }
 }  // namespace
@@ -490,6 +527,9 @@ void compute_layout(Snapshot& S) {
     S.stub = std::move(L.stub);
     S.n_stubs = L.n_stubs;
     S.n_units = L.n_units;
+    S.tgt_tail = L.tgt_tail;
+    S.tgt_end = L.tgt_end;
+    S.roots_at = L.roots_at;
     S.shared_words = L.shared_words;
     S.hot_units = (uint32_t)(L.hot_words / HDR_WORDS);
     S.hot_rows = L.hot_rows;
@@ -535,9 +575,14 @@ uint32_t handle_of(const Snapshot& S, const Overlay* ov, uint32_t row) {
 }
 
 uint32_t Snapshot::vid_of_row(uint32_t row) const {
-    if (coll.empty()) return unit_of_row[row];
-    auto it = coll.find(EDGE_SET | row);
-    return it == coll.end() ? unit_of_row[row] : it->second;
+    if (!coll.empty()) {
+        auto it = coll.find(EDGE_SET | row);
+        if (it != coll.end()) return it->second;
+    }
+    // a root row past 2^31 units (split layout): no subject set points at it, so nothing in its own
+    // tree can be it; its handle could read as a collision class's visit id (VID_CLASS | c)
+    const uint32_t u = unit_of_row[row];
+    return u != NO_UNIT && u >= EDGE_VAL ? 0xFFFFFFF0u : u;
 }
 
 std::string Snapshot::row_field_ns(uint32_t row) const {

@@ -63,11 +63,21 @@ constexpr uint32_t HDR_WORDS = 4;
 constexpr uint32_t WINDOW_WORDS = 4;            // edge words read together with the header
 constexpr uint32_t LINE_WORDS = 32;             // 128-B cache line
 constexpr uint32_t BUCKET_WORDS = 4;            // id tables are probed one 16-B bucket at a time
-// The arena is two segments of 2^32 words (16 GiB); no row (id table to last edge) crosses from one
-// to the other, so a position inside a row is a 32-bit word index within its segment.  Handles
-// (31-bit 16-B units) with bit SEG_SHIFT set lie in segment 1.
+// The arena is up to four segments of 2^32 words (16 GiB each, 64 GiB in all); no row (id table to
+// last edge) crosses from one to the next, so a position inside a row is a 32-bit word index within
+// its segment.  A handle (a 16-B unit, 32 bits) lies in segment handle >> SEG_SHIFT.
+//
+// Edges hold a subject set's handle in 31 bits, so every row some subject set points at (a
+// target) has a handle below 2^31 (the first 32 GiB); root rows -- rows no subject set points at,
+// reached only as a request's row -- may lie anywhere below 2^32 - 16.  The layout puts targets
+// first anyway (hottest first, roots last); when the arena outgrows 2^33 words it leaves a reserve
+// for the targets later writes add between the targets and the roots ("split" layout:
+// [0, tgt_tail) targets, [tgt_tail, tgt_end) reserve, [roots_at >= tgt_end, ...) roots).
 constexpr uint32_t SEG_SHIFT = 30;
 constexpr uint32_t SEG_MASK = (1u << SEG_SHIFT) - 1u;
+constexpr uint64_t ARENA_MAX_WORDS = 1ull << 34;
+constexpr uint64_t TARGET_MAX_WORDS = 1ull << 33;     // target rows' headers lie below this word
+constexpr uint32_t HANDLE_MAX = 0xFFFFFFF0u;          // handles (and overlay handles) stay below
 // header word 2: bits 0..7 flags, 8..12 hlog2, 13..31 bloom bits 32..50; word 3: bloom bits 0..31.
 // The 51-bit bloom filter (2 bits per subject id) summarizes the ids of a row with an id table,
 // so most absent ids are rejected with the header and the table is never probed for them.
@@ -214,6 +224,10 @@ struct Snapshot {
     std::vector<uint32_t> unit_of_row;    // NO_UNIT: a root row another part owns (not on this device)
     std::vector<uint32_t> rows_by_unit;   // rows in arena order (most-referenced first)
     std::vector<uint32_t> layout_units;   // their units, increasing
+    // split layout (arenas past 2^33 words, see SEG_SHIFT): the target reserve [tgt_tail, tgt_end)
+    // in words, filled by writes from tgt_tail up, and the first root row's word roots_at (>=
+    // tgt_end); tgt_end == 0: not split
+    uint64_t tgt_tail = 0, tgt_end = 0, roots_at = 0;
     // edge partitioning (keto_snapshot_upload_part): rows that are some subject set's target are
     // kept on every part; root rows (never a subject set) only on part hash(ns, object) % n_parts
     std::vector<uint8_t> is_root;
@@ -393,6 +407,10 @@ uint32_t overlay_row(const Snapshot& s, Overlay& ov, const RowKey& k);
 uint32_t handle_of(const Snapshot& s, const Overlay* ov, uint32_t row);
 // arena layout of every row (called by the builders)
 void compute_layout(Snapshot& s);
+// arena placement of one row (compute_layout, device_apply): the first word at or after w where a
+// row of `table` id-table words, `cb` closure-block words and n_edges edges keeps the line and
+// segment rules; total = the row's words from there
+uint64_t arena_fit(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, uint64_t& total);
 // snapshot lifecycle (delta.cpp): apply an insert / delete transaction to the host tables
 // (TransactRelationTuples, internal/persistence/sql/relationtuples.go:289-297); throws KETO_E_REBUILD
 // for writes outside the delta path; device_apply then patches the device arena

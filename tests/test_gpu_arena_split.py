@@ -1,0 +1,155 @@
+"""Arenas past 32 GiB (snapshot.hpp SEG_SHIFT): subject-set targets keep handles below 2^31, root rows
+lie above, in arena segments 2 and 3.  KETO_TEST_ROOT_BASE lays a small graph out that way (the
+roots from just below 3 x 2^32 words on, a ~48 GiB arena on the device whose gap is never built on
+the host); KETO_TEST_TGT_RESERVE shrinks the reserve for targets later writes add, so that a write
+overflows it and the snapshot lays its arena out afresh inside keto_snapshot_apply.
+
+Every decision and tree is compared with the oracle (or with the same graph in an ordinary layout):
+checks at max-depth 5 (tier 0), 9 (the 8-frame tier 0) and 16 (check_kernel; the reachability
+pretest is off past 2^31 units), subject-set requests naming root rows (handles past 2^31, never
+allowed: no tuple has them as subject), expand trees rooted at high rows, the streamed pair form, and
+writes interleaved with checks and expands against the SQL oracle."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT_BASE = 3 * (1 << 32) - (1 << 16)        # words: roots straddle segments 2 and 3
+
+
+@pytest.fixture(scope="module")
+def split():
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 4096), threads=16)
+    plain = g.snapshot(device=0)
+    os.environ["KETO_TEST_ROOT_BASE"] = str(ROOT_BASE)
+    try:
+        snap = g.snapshot(device=0)
+    finally:
+        del os.environ["KETO_TEST_ROOT_BASE"]
+    yield g, snap, plain
+    snap.close()
+    plain.close()
+    g.close()
+
+
+def test_split_layout_places_roots_high(split):
+    g, snap, _ = split
+    h = snap.row_handles(np.arange(g.n_rows, dtype=np.uint32)).astype(np.int64)
+    assert (h < (1 << 31)).any()                               # the targets
+    assert (h >= (1 << 31)).mean() > 0.5                       # the roots
+    assert (h >= 3 << 30).any() and ((h >= 1 << 31) & (h < 3 << 30)).any()   # both segments 2 and 3
+
+
+@pytest.mark.parametrize("gmd", [5, 9, 16])
+def test_split_checks_match_oracle(split, gmd):
+    g, snap, _ = split
+    q = g.queries(20000, seed=700 + gmd, depth=gmd)
+    gpu = snap.check_batch_ids(snap.with_handles(q), gmd)
+    tab = g.oracle_table(q, gmd)
+    ref = tab.check_batch_reqs(g.oracle_requests(tab, q), gmd, threads=16)
+    assert (gpu == ref).all(), f"{int((gpu != ref).sum())} mismatches of {len(q)}"
+    assert 0.05 < gpu.mean() < 0.95
+
+
+def test_split_subject_set_requests_equal_plain_layout(split):
+    """Subject-set requests whose target is any row -- root rows included, whose handles do not fit
+    an edge -- decide like the same graph in the ordinary layout (rows by row id, both forms)."""
+    from keto_amd.capi import pairs_of
+    g, snap, plain = split
+    q = g.queries(30000, seed=71, depth=5)
+    rng = np.random.default_rng(71)
+    sets = rng.random(len(q)) < 0.5
+    q["target"][sets] = rng.integers(0, g.n_rows, size=int(sets.sum()))
+    q["flags"][sets] = 1
+    want = plain.check_batch_rows(q, 5)
+    assert (snap.check_batch_rows(q, 5) == want).all()
+    q["max_depth"] = 0
+    assert (snap.check_batch_pairs(pairs_of(q), 0, 5) == plain.check_batch_pairs(pairs_of(q), 0, 5)).all()
+
+
+def test_split_streamed_pairs_equal_plain_layout(split, monkeypatch):
+    from keto_amd.capi import HostBuffer, pairs_of
+    g, snap, plain = split
+    monkeypatch.setenv("KETO_STREAM_MIN", "1")
+    monkeypatch.setenv("KETO_STREAM_CHUNK_LOG2", "16")
+    q = g.queries(200_000, seed=72, depth=5)
+    q["max_depth"] = 0
+    p = pairs_of(q)
+    hq, ho = HostBuffer(len(q), p.dtype), HostBuffer(len(q), np.uint8)
+    hq.array[:] = p
+    got = snap.check_batch_pairs(hq.array, 0, 5, out=ho.array).copy()
+    assert snap.last_timing_full()["chunks"] == -(-len(q) // 65536)
+    assert (got == plain.check_batch_pairs(p, 0, 5)).all()
+
+
+def test_split_expand_matches_oracle(split):
+    from tests.test_gpu_synth import _expand_matches_oracle
+    g, snap, _ = split
+    _expand_matches_oracle(g, snap)
+
+
+def test_split_expand_trees_equal_plain_layout(split):
+    g, snap, plain = split
+    rng = np.random.default_rng(8)
+    rows = rng.integers(0, g.n_rows, size=4000).astype(np.uint32) | np.uint32(0x80000000)
+    depths = rng.integers(0, 6, size=4000).astype(np.int32)
+    a = snap.expand_batch_ids(rows, depths, 5)
+    b = plain.expand_batch_ids(rows, depths, 5)
+    for x, y in zip(a, b):
+        assert (np.asarray(x) == np.asarray(y)).all()
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_split_writes_interleaved_with_checks(seed, monkeypatch):
+    """Writes on a split layout whose target reserve holds a few rows: new targets fill it, then a
+    write lays the arena out afresh (no KETO_E_REBUILD reaches the caller); every check and tree
+    after every write equals the SQL oracle's."""
+    import keto_amd
+    from oracle.oracle_sql import CheckEngine, ExpandEngine, NotFoundError, SQLStore
+    from tests.engine_util import rows_from_tuples, subj
+    from tests.randgraph import random_checks, random_expands, random_graph
+    from tests.test_gpu_lifecycle import _random_write, _row
+    monkeypatch.setenv("KETO_TEST_ROOT_BASE", str(ROOT_BASE))
+    monkeypatch.setenv("KETO_TEST_TGT_RESERVE", "256")
+    ns, tuples, raw, ps, alph = random_graph(seed + 900, wide=seed % 3 == 2, allow_poison=False,
+                                             allow_collisions=seed % 2 == 0)
+    names, objs, rels, users = alph
+    names = [n for n in names if n]
+    if not names:
+        pytest.skip("only a namespace named ''")
+    store = SQLStore(ns, tuples, page_size=ps)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), page_size=ps, device=0)
+    rng = random.Random(seed)
+    for step in range(8):
+        ins = [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(1, 12))]
+        cur = store.tuples()
+        dels = [rng.choice(cur) for _ in range(rng.randint(0, 3))] if cur else []
+        v0 = snap.version()
+        assert snap.apply([_row(ns, t) for t in ins], [_row(ns, t) for t in dels]) == v0 + 1
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+        checks = random_checks(seed * 13 + step, (names, objs + ["new1", "new7", "a0"], rels + ["q"],
+                                                  users + ["w001", "a"]), k=40)
+        for gm in sorted({c[2] for c in checks}):
+            grp = [c for c in checks if c[2] == gm]
+            allowed, _ = snap.check_batch([(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in grp], gm)
+            for (t, d, _), a in zip(grp, allowed):
+                assert bool(a) == CheckEngine(store, gm).subject_is_allowed(t, d), (seed, step, t, d, gm)
+        exps = random_expands(seed * 7 + step, (names, objs + ["new3"], rels + ["q"], users), k=8)
+        for gm in sorted({e[2] for e in exps}):
+            grp = [e for e in exps if e[2] == gm]
+            got = snap.expand_batch([(subj(s), d) for s, d, _ in grp], gm)
+            for (s, d, _), (st, js) in zip(grp, got):
+                try:
+                    tr = ExpandEngine(store, gm).build_tree(s, d)
+                    want = ("tree", tr.to_json()) if tr is not None else ("nil", None)
+                except NotFoundError:
+                    want = ("error", None)
+                assert ({0: "tree", 1: "nil", 2: "error"}[st], js) == want, (seed, step, s, d, gm)
+    snap.close()
