@@ -561,6 +561,10 @@ struct TierArgs {
 };
 
 // ------------------------------------------------------------------ check
+// T_NEVER: a subject-set request's target past 2^31 units is a root row (snapshot.hpp SEG_SHIFT):
+// no tuple has it as subject, and no edge could hold its handle.  Its target is clamped to EDGE_VAL,
+// whose set-edge value EDGE_SET | EDGE_VAL no edge has (targets lie below EDGE_VAL), so the search
+// runs as the reference's does and never matches: false.
 __device__ inline uint32_t win_at(const uint4& w, uint32_t i) {
     const uint32_t lo = (i & 1u) ? w.y : w.x;              // two-level select: no branches
     const uint32_t hi = (i & 1u) ? w.w : w.z;
@@ -702,15 +706,14 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             w.request();
             int d = qq.max_depth;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            // (a subject set no tuple has as subject -- past 2^31 units, not a target -- is never allowed)
-            if (qq.row == KETO_NO_ROW || d <= 0 || qq.target == KETO_NO_TARGET || ((qq.flags & 1u) && qq.target >= EDGE_VAL)) {
+            if (qq.row == KETO_NO_ROW || d <= 0 || qq.target == KETO_NO_TARGET) {
                 allowed[qi] = 0;
                 continue;
             }
             busy = true;
             if constexpr (COUNT) it = 1;
             tset = (qq.flags & 1u) != 0;
-            T = qq.target;
+            T = (qq.flags & 1u) ? min(qq.target, EDGE_VAL) : qq.target;   // see T_NEVER
             {
                 uint32_t cwd, cbit;
                 closure_bit(T, cwd, cbit);
@@ -1125,12 +1128,12 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             }
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET || ((nq.z & 1u) && nq.y >= EDGE_VAL)) {
+            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
                 decide(qi, 0);
                 c = keep;
                 continue;
             }
-            T = nq.y;
+            T = (nq.z & 1u) ? min(nq.y, EDGE_VAL) : nq.y;   // see T_NEVER
             eh = nq.x;
             c = P_HDR | ((uint32_t)d << C_K) | ((nq.z & 1u) ? C_TSET : 0u) | keep;   // sp 0, no frame
             return;
@@ -1560,12 +1563,12 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             }
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
-            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET || ((nq.z & 1u) && nq.y >= EDGE_VAL)) {
+            if (nq.x == KETO_NO_ROW || d <= 0 || nq.y == KETO_NO_TARGET) {
                 decide(qi, 0);
                 c = keep;
                 continue;
             }
-            T = nq.y;
+            T = (nq.z & 1u) ? min(nq.y, EDGE_VAL) : nq.y;   // see T_NEVER
             eh = nq.x;
             if constexpr (COUNT) it = 0;
             c = P_HDR | ((uint32_t)d << D_K) | ((nq.z & 1u) ? D_TSET : 0u) | keep;
