@@ -1208,9 +1208,11 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             if constexpr (STREAM) {
                 // requests j, j + 1 (j is even: runs are 4-aligned) in one 16-B load
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ta.pairs + j),
-                                                 reinterpret_cast<void*>(lds_nq + (tid & ~63u)), 16, 0, KETO_STREAM_CPOL);
+                                                 reinterpret_cast<void*>(lds_nq + (__builtin_amdgcn_readfirstlane(tid) & ~63u)),
+                                                 16, 0, KETO_STREAM_CPOL);
             } else {
-                prefetch_pair(q, j, j_end, lds_nq + (tid & ~63u));
+                // (the wave's LDS base from a scalar: a vector copy of it was spilled to scratch)
+                prefetch_pair(q, j, j_end, lds_nq + (__builtin_amdgcn_readfirstlane(tid) & ~63u));
             }
             c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
             w.request();
