@@ -26,6 +26,9 @@
 // graph's, and device_apply writes the rows the part holds (every subject-set target and its own root
 // rows); a migrating part takes none.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "parallel.hpp"
@@ -332,20 +335,58 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
         // they walk): a parallel scan of every row's current edges
         const uint32_t R = S.n_rows();
         std::vector<uint8_t> hit(R, 0);
+        // a transaction classes a handful of values: a branch-free compare against each of them per
+        // edge (many values: a 64-bit prefilter before the hash lookup).  The whole scan is one pass
+        // over the edge array: 15-24 ms of the write at 15.6M tuples on 8 threads
+        // (profiles/r04_apply_latency_cpu.log), linear in the tuples
+        std::vector<uint32_t> vals;
+        for (auto& kv : new_coll) vals.push_back(kv.first);
+        uint64_t mask = 0;
+        for (uint32_t v : vals) mask |= 1ull << ((v * 0x9E3779B1u) >> 26);
         auto holds = [&](const uint32_t* e, uint64_t n) {
+            if (vals.size() <= 8) {
+                uint32_t v8[8];
+                for (int k = 0; k < 8; ++k) v8[k] = vals[(size_t)k < vals.size() ? k : 0];
+                for (uint64_t i = 0; i < n; ++i) {
+                    bool any = false;
+                    for (int k = 0; k < 8; ++k) any |= e[i] == v8[k];
+                    if (any) return true;
+                }
+                return false;
+            }
             for (uint64_t i = 0; i < n; ++i)
-                if (new_coll.count(e[i])) return true;
+                if (((mask >> ((e[i] * 0x9E3779B1u) >> 26)) & 1u) && new_coll.count(e[i])) return true;
             return false;
         };
-        par_chunks(R, R >= par_min() ? build_threads() : 1u, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
-            for (uint64_t r = b; r < e; ++r) {
-                if (S.row_flags((uint32_t)r) & ROW_SEQ) continue;
-                auto st = T.rows.find((uint32_t)r);
-                if (st != T.rows.end()) continue;        // staged rows: checked below
-                const auto ed = S.row_edges((uint32_t)r);
-                if (holds(ed.first, ed.second)) hit[r] = 1;
+        // one streaming pass over the base edge array (no per-row lookups); a match is mapped to its
+        // row by binary search, and rows a write overrode are checked on their current edges
+        const unsigned th = S.edges.size() >= par_min() ? build_threads() : 1u;
+        std::vector<std::vector<uint64_t>> found(std::max(1u, th));
+        par_chunks(S.edges.size(), th, 1 << 20, [&](uint64_t b, uint64_t e, unsigned t) {
+            for (uint64_t i = b; i < e;) {
+                const uint64_t n = std::min<uint64_t>(e - i, 256);
+                if (holds(S.edges.data() + i, n))
+                    for (uint64_t x = i; x < i + n; ++x)
+                        if (holds(S.edges.data() + x, 1)) found[t].push_back(x);
+                i += n;
             }
         });
+        const uint32_t NB = S.n_base_rows;
+        for (auto& f : found)
+            for (uint64_t x : f) {
+                uint32_t lo = 0, hi = NB;                    // the last base row starting at or before x
+                while (hi - lo > 1) {
+                    const uint32_t m = lo + (hi - lo) / 2;
+                    if (S.row_begin(m) <= x) lo = m;
+                    else hi = m;
+                }
+                if (lo < R && !S.row_over.count(lo) && !(S.row_flags(lo) & ROW_SEQ)) hit[lo] = 1;
+            }
+        for (auto& kv : S.row_over)
+            if (kv.first < R && !(S.row_flags(kv.first) & ROW_SEQ) && holds(kv.second.data(), kv.second.size()))
+                hit[kv.first] = 1;
+        for (auto& kv : T.rows)
+            if (kv.first < R) hit[kv.first] = 0;         // staged rows: checked below
         for (uint32_t r = 0; r < R; ++r)
             if (hit[r]) T.edges(r);                      // re-imaged with the new flag (poisoned: rebuild)
     }
@@ -451,7 +492,13 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
     std::sort(S.needs_cb.begin(), S.needs_cb.end());
     S.needs_cb.erase(std::unique(S.needs_cb.begin(), S.needs_cb.end()), S.needs_cb.end());
     S.version += 1;
-    if (!S.dev) compute_layout(S);            // host-only: a later upload lays everything out afresh
+    if (!S.dev) {                             // host-only: a later upload lays everything out afresh
+        const auto t0 = std::chrono::steady_clock::now();
+        compute_layout(S);
+        if (getenv("KETO_APPLY_TRACE"))
+            fprintf(stderr, "[apply] host-only layout %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
 }
 
 }  // namespace keto
