@@ -23,10 +23,12 @@ Extras on the same line:
                 with the GPU's for that sample ("parity").
   ref_sql       the reference recursion issuing its own SQL against in-memory SQLite, one worker
                 process per core, over the first 10,000 requests (compared with the GPU too).
-  string_form   (N = 1) the same batch as named requests (keto_check_req: namespace, object, relation,
-                subject id strings in C memory) through keto_check_batch, the entry point the Go
-                shim calls: name resolution on host threads, then the pipelined device part.  The
-                snapshot then carries the graph's string table (tools/synth.py unified()).
+  string_form   (N = 1) the same batch as named requests, packed as the Go shim packs them (every
+                request's strings in one pinned blob + 24-B records) through keto_check_batch_packed,
+                which the Go shim's CheckBatch calls: resolution on the GPU, then the check; the
+                128-B keto_check_req form through keto_check_batch (resolution on host threads)
+                alongside as host_resolution.  The snapshot then carries the graph's string table
+                (tools/synth.py unified()).
 Host cores: --threads defaults to the CPUs this job may use (tools/hostcpu.py: affinity mask,
 cgroup quota, the harness's OMP_NUM_THREADS share), recorded with every CPU leg.
 """
@@ -230,23 +232,25 @@ def string_form(g, u, snap, q, a):
         snap.check_batch_packed(hb, rec.array, a.depth, n=n, allowed=pa, status=ps_)
         pts.append(time.perf_counter() - t0)
     pms = float(np.median(pts)) * 1e3
-    packed = {"value": round(n / (pms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(pms, 3),
-              "blob_bytes": int(used), "record_bytes": int(rec.array.nbytes), "pack_s": round(t_pack, 2),
-              "first_call_ms": round(t_pfirst * 1e3, 1), "statuses_equal_host": bool((ps_ == st).all()),
-              "decisions_equal_host": bool((pa == out).all()),
-              "what": "keto_check_batch_packed: the batch's strings back to back in one pinned blob + 24-B records "
-                      "(offset, six lengths, kind, depth) -> H2D -> every request resolved on the GPU against the "
-                      "snapshot's string / row indexes (uploaded once per version) -> check -> D2H; median of the "
-                      "timed batches; first_call_ms includes the index upload"}
-    return {"value": round(n / (ms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(ms, 3),
+    host = {"value": round(n / (ms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(ms, 3),
             "resolve_ms": round(float(np.median(res)), 3), "device_wall_ms": round(float(np.median(walls)), 3),
             "threads": a.threads, "first_call_ms": round(t_first * 1e3, 1), "request_build_s": round(t_make, 2),
-            "strings_in_snapshot": int(u.n_strings), "statuses_not_ok": int((st != 0).sum()),
-            "packed_device_resolution": packed,
-            "what": "keto_check_batch (the Go shim's entry point): 128-B keto_check_req with namespace / object / "
-                    "relation / subject-id strings in C memory -> name resolution on host threads (hashed string "
-                    "and row indexes) -> pipelined H2D / check / D2H; median of the timed batches; first_call_ms "
-                    "includes building the indexes", "_out": out.copy()}
+            "statuses_not_ok": int((st != 0).sum()),
+            "what": "keto_check_batch: 128-B keto_check_req with namespace / object / relation / subject-id strings "
+                    "in C memory -> name resolution on host threads (hashed string and row indexes) -> pipelined H2D "
+                    "/ check / D2H; median of the timed batches; first_call_ms includes building the indexes",
+            "_out": out.copy()}
+    return {"value": round(n / (pms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(pms, 3),
+            "form": "keto_check_batch_packed (what the Go shim's gpu.Snapshot.CheckBatch calls)",
+            "blob_bytes": int(used), "record_bytes": int(rec.array.nbytes), "pack_s": round(t_pack, 2),
+            "first_call_ms": round(t_pfirst * 1e3, 1), "statuses_equal_host": bool((ps_ == st).all()),
+            "decisions_equal_host": bool((pa == out).all()), "strings_in_snapshot": int(u.n_strings),
+            "what": "the batch's strings back to back in one pinned blob + 24-B records (offset, six lengths, kind, "
+                    "depth), as the Go batcher packs them -> H2D -> every request resolved on the GPU against the "
+                    "snapshot's string / row indexes (uploaded once per version) -> check -> D2H; median of the timed "
+                    "batches; first_call_ms includes the index upload; pack_s (the packing, untimed like the "
+                    "request structs of host_resolution) for reference",
+            "host_resolution": host, "_out": pa.copy()}
 
 
 def rusage():
@@ -476,10 +480,11 @@ def main():
         e2e["decisions_equal_device_resident"] = all(bool((o == gpu_out).all()) for o in e2e.pop("_out"))
     if strf is not None:
         strf["decisions_equal_device_resident"] = bool((strf.pop("_out") == gpu_out).all())
-        strf["packed_device_resolution"]["decisions_equal_device_resident"] = (
-            strf["packed_device_resolution"]["decisions_equal_host"] and strf["decisions_equal_device_resident"])
+        hr = strf["host_resolution"]
+        hr["decisions_equal_device_resident"] = bool((hr.pop("_out") == gpu_out).all())
         if roofline is not None:
-            strf["frac"] = round(roofline["alg_bytes_per_launch"] / (strf["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            for x in (strf, hr):
+                x["frac"] = round(roofline["alg_bytes_per_launch"] / (x["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         if e2e is not None:
             e2e["string_form"] = strf
     # host resources per rank (the 8-rank run: every rank holds the graph and the snapshot's host tables)

@@ -3543,6 +3543,15 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     }
     const uint32_t lanes = getenv("KETO_SLOTS") ? (uint32_t)hw_slots() : D.v1_lanes[var];
     p.slots[0] = (uint32_t)std::min<uint64_t>(lanes, ((uint64_t)n + 255) / 256 * 256);
+    if (ss) {
+        // a streamed launch leaves wave slots free: the runtime's H2D copies behind it run as blit
+        // kernels, which a launch holding every slot starves until its lanes give up waiting
+        // (tools/dev/stream_probe.hip: 8/8 of the slots never saw a chunk land, 7/8 did).
+        // KETO_STREAM_EIGHTHS overrides the share (default 7)
+        const char* e8 = getenv("KETO_STREAM_EIGHTHS");
+        const uint32_t eighths = (uint32_t)std::min(8, std::max(1, e8 ? atoi(e8) : 7));
+        p.slots[0] = std::max<uint32_t>(256, p.slots[0] / 8 * eighths / 256 * 256);
+    }
     if (stash && kind < 2) {
         // KETO_CHUNK_LANES (tuning): a pipeline chunk's tier 0 on at most that many lanes, so that the
         // chunks of two compute streams (KETO_PIPE_STREAMS=2) can run side by side

@@ -64,8 +64,6 @@ def test_streamed_matches_handle_form(graph, monkeypatch, n, depth, t0cap):
     q = _requests(g, n, seed=n % 97, depth=depth)
     out, t = _streamed(snap, q, depth)
     assert t["chunks"] == -(-n // 65536), t                         # the streamed path ran
-    if t0cap:
-        assert t["requests"][1] > 0, t                              # and handed requests up
     want = _want(snap, q)
     assert (out == want).all(), f"{int((out != want).sum())} mismatches of {n}"
     ids = ((q["flags"] & 1) == 0) & (q["row"] != 0xFFFFFFFF)

@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #define OK(x)                                                                                    \
@@ -25,19 +26,20 @@
     } while (0)
 
 constexpr uint32_t CHUNKS = 8;
-constexpr uint64_t CHUNK_WORDS = 64u << 10;      // 256 KB per chunk: the whole buffer fits one XCD's L2
+uint64_t CHUNK_WORDS = 64u << 10;                // 256 KB per chunk by default: the buffer fits one XCD's L2
 
-__global__ void __launch_bounds__(256) touch(const uint32_t* data, unsigned long long* sink) {
+__global__ void __launch_bounds__(256) touch(const uint32_t* data, uint64_t chunk_words, unsigned long long* sink) {
     // every XCD (workgroup b runs on XCD b % 8) reads every line of the buffer
     const uint32_t xcd_blocks = gridDim.x / 8;
     const uint32_t t = (blockIdx.x / 8) * blockDim.x + threadIdx.x;
     unsigned long long s = 0;
-    for (uint64_t i = t; i < CHUNKS * CHUNK_WORDS; i += (uint64_t)xcd_blocks * blockDim.x) s += data[i];
+    for (uint64_t i = t; i < CHUNKS * chunk_words; i += (uint64_t)xcd_blocks * blockDim.x) s += data[i];
     if (s == 42) atomicAdd(sink, s);
 }
 
-__global__ void __launch_bounds__(256) spin(const uint32_t* ready, const uint32_t* data, unsigned long long* sums,
-                                            unsigned long long* sums_sys, uint32_t* seen_at, uint32_t* timeouts) {
+__global__ void __launch_bounds__(256) spin(const uint32_t* ready, const uint32_t* data, uint64_t chunk_words,
+                                            unsigned long long* sums, unsigned long long* sums_sys, uint32_t* seen_at,
+                                            uint32_t* timeouts) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
@@ -58,8 +60,8 @@ __global__ void __launch_bounds__(256) spin(const uint32_t* ready, const uint32_
         }
         if (lane == 0) atomicMin(seen_at + c, (uint32_t)((wall_clock64() - t0) / 100u));   // us
         unsigned long long s = 0, s2 = 0;
-        const uint32_t* d = data + c * CHUNK_WORDS;
-        for (uint64_t i = (uint64_t)wave * 64 + lane; i < CHUNK_WORDS; i += (uint64_t)waves * 64) {
+        const uint32_t* d = data + c * chunk_words;
+        for (uint64_t i = (uint64_t)wave * 64 + lane; i < chunk_words; i += (uint64_t)waves * 64) {
             s += d[i];
             s2 += __hip_atomic_load(d + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -68,11 +70,13 @@ __global__ void __launch_bounds__(256) spin(const uint32_t* ready, const uint32_
     }
 }
 
-int run(int mode) {
+// mode: 0 = hipStreamWriteValue32 marks, 1 = 4-B H2D copies of a pinned word; eighths: the spinning
+// grid's share of the resident blocks (8 = every slot)
+int run(int mode, int eighths) {
     int cus = 0, per_cu = 0;
     OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, spin, 256, 0));
-    const uint32_t blocks = (uint32_t)(cus * per_cu);
+    const uint32_t blocks = (uint32_t)std::max(8, cus * per_cu * eighths / 8);
     uint32_t *h_data = nullptr, *h_one = nullptr;
     OK(hipHostMalloc((void**)&h_data, CHUNKS * CHUNK_WORDS * 4, hipHostMallocDefault));
     OK(hipHostMalloc((void**)&h_one, 4, hipHostMallocDefault));
@@ -101,11 +105,11 @@ int run(int mode) {
     hipStream_t ks, cs;
     OK(hipStreamCreateWithFlags(&ks, hipStreamNonBlocking));
     OK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-    hipLaunchKernelGGL(touch, dim3(2048), dim3(256), 0, ks, data, sink);
+    hipLaunchKernelGGL(touch, dim3(2048), dim3(256), 0, ks, data, CHUNK_WORDS, sink);
     OK(hipGetLastError());
     OK(hipStreamSynchronize(ks));
     const auto t0 = std::chrono::steady_clock::now();
-    hipLaunchKernelGGL(spin, dim3(blocks), dim3(256), 0, ks, ready, data, sums, sums_sys, seen, tmo);
+    hipLaunchKernelGGL(spin, dim3(blocks), dim3(256), 0, ks, ready, data, CHUNK_WORDS, sums, sums_sys, seen, tmo);
     OK(hipGetLastError());
     for (uint32_t c = 0; c < CHUNKS; ++c) {
         OK(hipMemcpyAsync(data + c * CHUNK_WORDS, h_data + c * CHUNK_WORDS, CHUNK_WORDS * 4, hipMemcpyHostToDevice, cs));
@@ -123,8 +127,9 @@ int run(int mode) {
     OK(hipMemcpy(got_sys.data(), sums_sys, CHUNKS * 8, hipMemcpyDeviceToHost));
     OK(hipMemcpy(at.data(), seen, CHUNKS * 4, hipMemcpyDeviceToHost));
     OK(hipMemcpy(&t, tmo, 4, hipMemcpyDeviceToHost));
-    printf("mode %d (%s): %u blocks, copies done %.2f ms, kernel done %.2f ms, waves timed out %u\n", mode,
-           mode == 0 ? "hipStreamWriteValue32" : "4-B H2D flag copy", blocks, copy_ms, all_ms, t);
+    printf("mode %d (%s), %llu KB chunks, %u blocks (%d/8 of the resident slots): copies done %.2f ms, kernel done "
+           "%.2f ms, waves timed out %u\n", mode, mode == 0 ? "hipStreamWriteValue32" : "4-B H2D flag copy",
+           (unsigned long long)(CHUNK_WORDS * 4 / 1024), blocks, eighths, copy_ms, all_ms, t);
     int bad = 0;
     for (uint32_t c = 0; c < CHUNKS; ++c) {
         printf("  chunk %u first seen at %u us, plain-load sum %s, system-scope sum %s\n", c, at[c],
@@ -146,12 +151,14 @@ int run(int mode) {
 }
 
 int main(int argc, char** argv) {
+    // args: [chunk KB]; runs both modes at full, 7/8 and 1/2 of the resident slots
+    if (argc > 1) CHUNK_WORDS = (uint64_t)atoll(argv[1]) * 256;
     int rc = 0;
-    for (int m = 0; m < 2; ++m) {
-        if (argc > 1 && atoi(argv[1]) != m) continue;
-        const int r = run(m);
-        if (r == 2) return 2;
-        rc |= r;
-    }
+    for (int eighths : {8, 7, 4})
+        for (int m = 0; m < 2; ++m) {
+            const int r = run(m, eighths);
+            if (r == 2) return 2;
+            rc |= r;
+        }
     return rc;
 }
