@@ -126,6 +126,7 @@ def sql_leg(g, q, a, gpu_out):
     os.close(fd)
     try:
         dst = __import__("sqlite3").connect(db)
+        store.conn.commit()                   # a pending write transaction stalls the backup
         store.conn.backup(dst)
         dst.close()
         store.conn.close()

@@ -97,6 +97,7 @@ def config1(a):
     os.close(fd)
     try:
         dst = __import__("sqlite3").connect(db)
+        store.conn.commit()                   # a pending write transaction stalls the backup
         store.conn.backup(dst)
         dst.close()
         _json.dump({"namespaces": ns, "requests": [(n_, o, r, u[1] if u[0] == "id" else list(u[1:]), d)
