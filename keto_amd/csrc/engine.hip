@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1881,6 +1882,10 @@ struct ExpandOut {
     // open) at once: global_load_lds into a per-wave scratch word (no register, no wait), so the
     // lines are in the caches when the walk reaches those children one after another
     uint32_t prefetch;
+    // edges past the window read a 16-B block at a time (KETO_EXPAND_EDGE_BLOCKS=0: a word at a time)
+    uint32_t edge_blocks;
+    // tooling (KETO_EXPAND_CLOCKS=1): each root's walk time in wall-clock ticks (100 MHz), or NULL
+    uint32_t* clocks;
 };
 // expand kernel modes: count the trees' nodes; write them at their offsets; write them to staging
 constexpr int EXP_COUNT = 0, EXP_FILL = 1, EXP_STAGE = 2;
@@ -1917,6 +1922,10 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     // e.g. after a pop)
     uint4 win = make_uint4(0, 0, 0, 0);
     uint64_t wbeg = ~0ull;
+    // past the window, the current frame's edges are read a 16-B block at a time (rows are padded to
+    // 16 B): one dependent load per four set edges instead of one per edge (ExpandOut::edge_blocks)
+    uint4 blk = make_uint4(0, 0, 0, 0);
+    uint64_t blk_at = ~0ull;
     // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union entered
     auto open = [&](uint32_t h, int k) -> int {
         RowView rv;
@@ -1959,6 +1968,7 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
         cur = Frame{rv.beg, n_all, (uint16_t)k, (uint16_t)((rv.seq ? FR_SEQ : 0) | (rv.a != s.arena ? FR_OV : 0))};
         win = w4;
         wbeg = rv.a != s.arena ? ~0ull : rv.beg;
+        blk_at = ~0ull;
         if (o.prefetch && wbeg != ~0ull && (k - 1 >= 2 || !o.leaf_sets_blind)) {
             // the window's subject sets (set edges always target main-arena rows)
 #pragma unroll
@@ -1979,11 +1989,24 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             --sp;
             cur = st[sp];
             wbeg = ~0ull;
+            blk_at = ~0ull;
             continue;
         }
         const uint32_t* const a = (cur.fl & FR_OV) ? ov.arena : s.arena;
         const uint64_t wo = cur.pos - wbeg;                 // (huge when no window is held)
-        const uint32_t e = wo == 0 ? win.x : wo == 1 ? win.y : wo == 2 ? win.z : wo == 3 ? win.w : a[cur.pos];
+        uint32_t e;
+        if (wo < WINDOW_WORDS) {
+            e = win_at(win, (uint32_t)wo);
+        } else if (o.edge_blocks) {
+            const uint64_t bw = cur.pos & ~3ull;
+            if (bw != blk_at) {
+                blk = *reinterpret_cast<const uint4*>(a + bw);
+                blk_at = bw;
+            }
+            e = win_at(blk, (uint32_t)cur.pos & 3u);
+        } else {
+            e = a[cur.pos];
+        }
         if (!(e & EDGE_SET) && !(cur.fl & FR_SEQ)) {
             // a normal row keeps its subject sets first: every edge left is a subject id, and each
             // is a leaf (:97-101) -- counted at once, copied in one pass
@@ -2062,6 +2085,196 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     return EXP_TREE;
 }
 
+// The same walk as expand_one, restructured like the tier-0 check kernel (round 4): each loop
+// iteration issues ONE global access per lane, from one place in the loop -- a subject set's header
+// and window (with the forward followed on the next iteration), or the next 16-B block of the
+// current row's edges -- and the walk in between needs no memory: window and block edges, visited
+// tests in registers / LDS, node stores, queued id runs, and the saved frames in LDS.  expand_one
+// waited on each lane's loads where they occurred, so a wave of 64 trees paid one round trip per
+// load of any of its lanes (every wave of config #5 lived ~110-150 us, KETO_EXPAND_CLOCKS).
+// SmFrames selects it (tier 0, max-depth <= SM_FRAMES); the visited map gets SM_LDS_VIDS LDS
+// entries per lane (config #5's trees mark at most 25 sets; 16 made 4.5 % of them probe HBM).
+struct SmFrames {};
+constexpr int SM_FRAMES = 8;
+constexpr int SM_LDS_VIDS = 24;
+
+template <bool FILL, class VT>
+__device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
+                         uint32_t root_vid, int d, VT& V, keto_tree_node* out, uint64_t& cnt, uint64_t cap,
+                         uint4* frames, const ExpandOut& o, uint32_t& nr, uint64_t& qend, uint32_t* pf_lds,
+                         uint32_t& iters) {
+    if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
+        emit(out, cnt, FILL, cap, root, 0x80000000u);
+        return EXP_TREE;
+    }
+    if (root == KETO_NO_ROW) return EXP_NIL;                // no tuples at all (:68-70)
+    V.fresh();
+    Work<false> nw;
+    V.test_add(root_vid, nw);                               // :40-43 (root marked too)
+    int sp = 0;
+    Frame cur{0, 0, 0, 0};
+    uint4 win = make_uint4(0, 0, 0, 0), blk = make_uint4(0, 0, 0, 0);
+    uint64_t wbeg = ~0ull, blk_at = ~0ull;
+    // the pending open: identity handle oh (what its node names), the handle its header is read at
+    // (ol: a forward moves it), remaining depth od, and its edge in the parent (oe; NONE32 = the root)
+    bool opening = true;
+    uint32_t oh = root, ol = root, oe = NONE32;
+    int od = d;
+    for (;;) {
+        ++iters;
+        // ---- the iteration's access
+        uint4 v = make_uint4(0, 0, 0, 0), w4 = make_uint4(0, 0, 0, 0), b4 = make_uint4(0, 0, 0, 0);
+        const bool in_ov = ol >= ov.base;
+        const uint32_t* const ha = in_ov ? ov.arena : s.arena;
+        const uint64_t hw = (uint64_t)(in_ov ? ol - ov.base : ol) * HDR_WORDS;
+        if (opening) {
+            // header, window and the next edge block together (the arena has slack past its end)
+            v = *reinterpret_cast<const uint4*>(ha + hw);
+            if (!in_ov) {
+                w4 = *reinterpret_cast<const uint4*>(ha + hw + HDR_WORDS);
+                if (o.edge_blocks) b4 = *reinterpret_cast<const uint4*>(ha + hw + 2 * HDR_WORDS);
+            }
+        } else {
+            const uint32_t* const a = (cur.fl & FR_OV) ? ov.arena : s.arena;
+            blk_at = cur.pos & ~3ull;                       // (rows are padded to 16 B)
+            blk = *reinterpret_cast<const uint4*>(a + blk_at);
+        }
+        if (opening) {
+            if (v.z & HDR_FWD) {                            // a row a write moved (delta.cpp)
+                ol = v.x;
+                continue;
+            }
+            opening = false;
+            const uint32_t n_all = v.x + v.y;
+            const bool poison = (v.z & HDR_POISON) != 0, poison0 = (v.z & HDR_POISON0) != 0;
+            if (!poison && n_all == 0) {                    // nil (:68-70)
+                if (oe == NONE32) return EXP_NIL;
+                emit(out, cnt, FILL, cap, oe, 0x80000000u);     // a nil child -> Leaf(set)
+            } else if (poison0) {
+                return EXP_ERROR;                           // the first page fails toInternal
+            } else if (od <= 1) {                           // :72-75
+                emit(out, cnt, FILL, cap, EDGE_SET | oh, 0x80000000u);
+            } else if (poison) {
+                return EXP_ERROR;                           // a later page fails
+            } else {                                        // a union: enter it
+                if (cur.left > 0) {
+                    if (sp == SM_FRAMES) return EXP_OVERFLOW;
+                    frames[sp * LDS_STRIDE] = make_uint4((uint32_t)cur.pos, (uint32_t)(cur.pos >> 32), cur.left,
+                                                         (uint32_t)cur.k | ((uint32_t)cur.fl << 16));
+                    ++sp;
+                }
+                emit(out, cnt, FILL, cap, EDGE_SET | oh, n_all);
+                const uint64_t beg = hw + HDR_WORDS;
+                cur = Frame{beg, n_all, (uint16_t)od, (uint16_t)(((v.z & HDR_SEQ) ? FR_SEQ : 0) | (in_ov ? FR_OV : 0))};
+                win = w4;
+                wbeg = in_ov ? ~0ull : beg;
+                blk = b4;
+                blk_at = in_ov || !o.edge_blocks ? ~0ull : beg + WINDOW_WORDS;
+                if (o.prefetch && !in_ov && (od - 1 >= 2 || !o.leaf_sets_blind)) {
+                    // the window's subject sets: their header lines start loading now (no register)
+#pragma unroll
+                    for (uint32_t j = 0; j < WINDOW_WORDS; ++j) {
+                        const uint32_t e = win_at(w4, j);
+                        if (j < n_all && (e & EDGE_SET))
+                            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(s.arena + (uint64_t)(e & EDGE_VAL) * HDR_WORDS),
+                                                             reinterpret_cast<void*>(pf_lds), 4, 0, 0);
+                    }
+                }
+            }
+        }
+        // ---- walk until the next access is needed
+        for (;;) {
+            if (cur.left == 0) {
+                if (sp == 0) return EXP_TREE;
+                --sp;
+                const uint4 f = frames[sp * LDS_STRIDE];
+                cur = Frame{(uint64_t)f.x | ((uint64_t)f.y << 32), f.z, (uint16_t)(f.w & 0xFFFFu), (uint16_t)(f.w >> 16)};
+                wbeg = ~0ull;
+                blk_at = ~0ull;
+                continue;
+            }
+            const uint64_t wo = cur.pos - wbeg;             // (huge when no window is held)
+            uint32_t e;
+            if (wo < WINDOW_WORDS) e = win_at(win, (uint32_t)wo);
+            else if ((cur.pos & ~3ull) == blk_at) e = win_at(blk, (uint32_t)cur.pos & 3u);
+            else break;                                     // next: this edge's block
+            const uint32_t* const a = (cur.fl & FR_OV) ? ov.arena : s.arena;
+            if (!(e & EDGE_SET) && !(cur.fl & FR_SEQ)) {
+                // the rest of a normal row are subject ids, all leaves: queued (or copied) at once
+                if constexpr (FILL) {
+                    if (cnt + cur.left <= cap) {
+                        bool queued = false;
+                        if (cur.left > o.run_inline && o.runs) {
+                            if (cur.left <= BIG_RUN && nr < RUNS_PER_LANE) {
+                                o.runs[nr++] = CopyRun{a + cur.pos, out + cnt, cur.left};
+                                queued = true;
+                            } else if (cur.left > BIG_RUN) {
+                                const uint32_t pieces = (cur.left + BIG_RUN - 1) / BIG_RUN;
+                                uint32_t at = __hip_atomic_load(o.n_big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                bool got = false;
+                                while ((uint64_t)at + pieces <= o.big_cap) {
+                                    const uint32_t prev = atomicCAS(o.n_big, at, at + pieces);
+                                    if (prev == at) {
+                                        got = true;
+                                        break;
+                                    }
+                                    at = prev;
+                                }
+                                if (got) {
+                                    for (uint32_t k = 0; k < pieces; ++k)
+                                        o.big[at + k] = CopyRun{a + cur.pos + (uint64_t)k * BIG_RUN, out + cnt + (uint64_t)k * BIG_RUN,
+                                                                min(BIG_RUN, cur.left - k * BIG_RUN)};
+                                    queued = true;
+                                }
+                            }
+                            if (queued) qend = max(qend, cnt + cur.left);
+                        }
+                        if (!queued) {
+                            const uint32_t* src = a + cur.pos;
+                            keto_tree_node* dst = out + cnt;
+                            for (uint32_t i = 0; i < cur.left; i += 8) {
+                                uint32_t x[8];
+#pragma unroll
+                                for (int j = 0; j < 8; ++j) x[j] = i + j < cur.left ? src[i + j] : 0u;
+#pragma unroll
+                                for (int j = 0; j < 8; ++j)
+                                    if (i + j < cur.left) dst[i + j] = keto_tree_node{x[j], 0x80000000u};
+                            }
+                        }
+                    }
+                }
+                cnt += cur.left;
+                cur.left = 0;
+                continue;
+            }
+            cur.pos++;
+            cur.left--;
+            if (!(e & EDGE_SET)) {
+                emit(out, cnt, FILL, cap, e, 0x80000000u);     // subject id child -> Leaf
+                continue;
+            }
+            const uint32_t c = e & EDGE_VAL;
+            uint32_t vid = c;
+            if (cur.fl & FR_SEQ) {
+                const uint32_t cv = coll_lookup(s, e);
+                if (cv != NONE32) vid = cv;
+            }
+            const int k = (int)cur.k - 1;
+            const int t = V.test_add(vid, nw);
+            if (t == 2) return EXP_OVERFLOW;
+            if (t == 1 || (k <= 1 && o.leaf_sets_blind)) {  // visited -> nil -> Leaf(set); or :72-75
+                emit(out, cnt, FILL, cap, e, 0x80000000u);
+                continue;
+            }
+            opening = true;                                 // next: the child's header
+            oh = ol = c;
+            oe = e;
+            od = k;
+            break;
+        }
+    }
+}
+
 struct ExpandReq {
     uint32_t root;
     uint32_t flags;
@@ -2073,20 +2286,23 @@ template <int MODE, class Stack>
 __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, const ExpandReq* __restrict__ q,
                                                      uint32_t n, int gmd, ExpandOut o, TierArgs ta) {
     constexpr bool FILL = MODE != EXP_COUNT, STAGE = MODE == EXP_STAGE;
+    constexpr bool SM = std::is_same<Stack, SmFrames>::value;  // expand_sm (saved frames in LDS)
+    constexpr int LV = SM ? SM_LDS_VIDS : LDS_VIDS;
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
-    // a tree's map: its first REG_VIDS + LDS_VIDS sets in registers and the lane's LDS column (one
+    // a tree's map: its first REG_VIDS + LV sets in registers and the lane's LDS column (one
     // tree at max-depth 5 marks a handful of sets), the rest in the lane's HBM table
-    __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
+    __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
     __shared__ uint32_t lds_pf[256];                          // the waves' prefetch scratch (never read)
-    VisitedRS<LDS_VIDS, Visited> V;
+    __shared__ uint4 lds_fr[SM ? SM_FRAMES * LDS_STRIDE : 1];   // SM: the lane's saved frames
+    VisitedRS<LV, Visited> V;
     V.n = 0;
-    V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
+    V.lds = LV > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
     V.V.count = 0;
-    Stack st;
+    typename std::conditional<SM, LocalStack<1>, Stack>::type st;
     if constexpr (std::is_same<Stack, GlobalStack>::value) {
         st.f = ta.gstack + (uint64_t)slot * ta.gstack_n;
         st.n = ta.gstack_n;
@@ -2107,8 +2323,19 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         keto_tree_node* out = !FILL ? nullptr : STAGE ? o.stage + stage0 + used : o.nodes + o.offset[i];
         const uint64_t cap = STAGE ? o.stage_cap - used : ~0ull;
         uint64_t qend = 0;
-        int r = expand_one<FILL, Stack>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, st, o, nr, qend,
-                                        lds_pf + (threadIdx.x & ~63u));
+        const uint64_t t_tree = o.clocks ? wall_clock64() : 0;
+        int r;
+        uint32_t iters = 0;
+        if constexpr (SM)
+            r = expand_sm<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, lds_fr + threadIdx.x, o, nr, qend,
+                                lds_pf + (threadIdx.x & ~63u), iters);
+        else
+            r = expand_one<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, st, o, nr, qend,
+                                 lds_pf + (threadIdx.x & ~63u));
+        if (o.clocks) {
+            o.clocks[i] = (uint32_t)(wall_clock64() - t_tree);
+            o.clocks[n + i] = iters;                       // (expand_sm: its accesses)
+        }
         const bool staged = STAGE && r == EXP_TREE && cnt <= cap;
         // a tree not staged (too big, or left to the next tier) may have queued runs into the region:
         // that part stays dead, so the copies cannot land on the next tree
@@ -4433,6 +4660,10 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     };
     for (int e = 0; e < 4; ++e)
         if (!D.ex_ev[e]) HIP_OK(hipEventCreate(&D.ex_ev[e]));
+    // tier 0 walks with expand_sm (one access per iteration, frames in LDS) when the saved frames
+    // fit its LDS stack; KETO_EXPAND_SM=0: expand_one (tooling)
+    const char* sme = getenv("KETO_EXPAND_SM");
+    const bool sm = gmd <= SM_FRAMES && !(sme && atoi(sme) == 0);
     // (the batch timing sums the passes' tiers: keto_last_batch_timing after an expand)
     auto launch_pass = [&](bool fill, const ExpandOut& eo) {
         run_tiers(D, D.ews, n, p, st,
@@ -4445,7 +4676,15 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                       const int mode = fill ? EXP_FILL : (eo.stage && level == 0) ? EXP_STAGE : EXP_COUNT;
                       ExpandOut e = eo;
                       if (level > 0) e.runs = nullptr;         // later tiers copy their runs in place
-                      if (mode == EXP_COUNT && local)
+                      if (level == 0 && local && sm) {
+                          if (mode == EXP_COUNT)
+                              hipLaunchKernelGGL((expand_kernel<EXP_COUNT, SmFrames>), grid, block, 0, st, sv, dov, dq, n, gmd, e, a);
+                          else if (mode == EXP_STAGE)
+                              hipLaunchKernelGGL((expand_kernel<EXP_STAGE, SmFrames>), grid, block, 0, st, sv, dov, dq, n, gmd, e, a);
+                          else
+                              hipLaunchKernelGGL((expand_kernel<EXP_FILL, SmFrames>), grid, block, 0, st, sv, dov, dq, n, gmd, e, a);
+                      }
+                      else if (mode == EXP_COUNT && local)
                           hipLaunchKernelGGL((expand_kernel<EXP_COUNT, LocalStack<16>>), grid, block, 0, st, sv, dov,
                                              dq, n, gmd, e, a);
                       else if (mode == EXP_COUNT)
@@ -4492,8 +4731,17 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     const uint32_t blind = S.n_poisoned_rows == 0 && getenv("KETO_EXPAND_LOAD_LEAVES") == nullptr;
     const char* pfe = getenv("KETO_EXPAND_PREFETCH");
     const uint32_t pf = pfe ? (uint32_t)(atoi(pfe) != 0) : 1u;
+    const char* ebe = getenv("KETO_EXPAND_EDGE_BLOCKS");
+    const uint32_t eb = ebe ? (uint32_t)(atoi(ebe) != 0) : 1u;
+    // KETO_EXPAND_CLOCKS=1 (tooling): the first pass's per-root walk times, summarized on stderr
+    uint32_t* d_clocks = nullptr;
+    if (getenv("KETO_EXPAND_CLOCKS")) {
+        d_clocks = dmalloc<uint32_t>(2ull * n, acc);
+        HIP_OK(hipMemsetAsync(d_clocks, 0, 2ull * n * sizeof(uint32_t), st));
+    }
     launch_pass(false, ExpandOut{nullptr, nullptr, dcount, dstatus, staged ? D.ex_runs : nullptr, d_lane_runs,
-                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, blind, pf});
+                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, blind, pf, eb,
+                                 d_clocks});
     float extra_ms = 0;
     if (staged) {
         HIP_OK(hipEventRecord(D.ex_ev[0], st));
@@ -4512,6 +4760,30 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (staged) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, D.ex_ev[0], D.ex_ev[1]) == hipSuccess) extra_ms += ms;
+    }
+    if (d_clocks) {
+        std::vector<uint32_t> ck(2ull * n);
+        HIP_OK(hipMemcpy(ck.data(), d_clocks, 2ull * n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        {
+            // per wave (64 consecutive roots of a lane block): the most accesses of one lane
+            std::vector<uint32_t> it(ck.begin() + n, ck.end()), wmax;
+            for (uint32_t b = 0; b < n; b += 64) wmax.push_back(*std::max_element(it.begin() + b, it.begin() + std::min(n, b + 64)));
+            std::sort(it.begin(), it.end());
+            std::sort(wmax.begin(), wmax.end());
+            fprintf(stderr, "[expand clocks] accesses per root: p50 %u p90 %u p99 %u max %u; per wave (max lane): p50 %u p90 %u max %u\n",
+                    it[n / 2], it[n * 9 / 10], it[n * 99 / 100], it[n - 1], wmax[wmax.size() / 2], wmax[wmax.size() * 9 / 10],
+                    wmax.back());
+        }
+        (void)hipFree(d_clocks);
+        std::vector<uint32_t> idx(n);
+        std::iota(idx.begin(), idx.end(), 0u);
+        std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return ck[x] > ck[y]; });
+        auto q = [&](double f) { return ck[idx[std::min<size_t>(n - 1, (size_t)(f * n))]] / 100.0; };
+        fprintf(stderr, "[expand clocks] walk us per root: max %.1f p0.1%% %.1f p1%% %.1f p10%% %.1f p50 %.1f\n",
+                ck[idx[0]] / 100.0, q(0.001), q(0.01), q(0.1), q(0.5));
+        for (uint32_t k = 0; k < std::min<uint32_t>(n, 12); ++k)
+            fprintf(stderr, "[expand clocks]   root %u (handle %u): %.1f us, %llu nodes, %u accesses\n", idx[k], root[idx[k]],
+                    ck[idx[k]] / 100.0, (unsigned long long)cnt[idx[k]], ck[n + idx[k]]);
     }
     uint32_t unstaged = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -4554,7 +4826,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (unstaged) {
         big_queue(total);
         launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_lane_runs, run_inline, D.ex_big,
-                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, blind, pf});
+                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, blind, pf, eb, nullptr});
     }
     HIP_OK(hipEventRecord(D.ex_ev[2], st));
     if (unstaged) copy_queued();
