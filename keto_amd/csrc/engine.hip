@@ -2091,7 +2091,10 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
 // current row's edges -- and the walk in between needs no memory: window and block edges, visited
 // tests in registers / LDS, node stores, queued id runs, and the saved frames in LDS.  expand_one
 // waited on each lane's loads where they occurred, so a wave of 64 trees paid one round trip per
-// load of any of its lanes (every wave of config #5 lived ~110-150 us, KETO_EXPAND_CLOCKS).
+// load of any of its lanes.  Measured on config #5 it takes the same time (profiles/r04o_expand_sm.txt):
+// a wave lives as long as its slowest lane's chain of dependent accesses -- 25 per wave at the
+// median, 39 at most (KETO_EXPAND_CLOCKS counts them) -- at ~4 us each with 1.5 waves per SIMD, so
+// the pass is that chain's latency, not where the waits sit.  Kept: no scratch, fewer waits.
 // SmFrames selects it (tier 0, max-depth <= SM_FRAMES); the visited map gets SM_LDS_VIDS LDS
 // entries per lane (config #5's trees mark at most 25 sets; 16 made 4.5 % of them probe HBM).
 struct SmFrames {};
@@ -2123,17 +2126,13 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
     for (;;) {
         ++iters;
         // ---- the iteration's access
-        uint4 v = make_uint4(0, 0, 0, 0), w4 = make_uint4(0, 0, 0, 0), b4 = make_uint4(0, 0, 0, 0);
+        uint4 v = make_uint4(0, 0, 0, 0), w4 = make_uint4(0, 0, 0, 0);
         const bool in_ov = ol >= ov.base;
         const uint32_t* const ha = in_ov ? ov.arena : s.arena;
         const uint64_t hw = (uint64_t)(in_ov ? ol - ov.base : ol) * HDR_WORDS;
         if (opening) {
-            // header, window and the next edge block together (the arena has slack past its end)
             v = *reinterpret_cast<const uint4*>(ha + hw);
-            if (!in_ov) {
-                w4 = *reinterpret_cast<const uint4*>(ha + hw + HDR_WORDS);
-                if (o.edge_blocks) b4 = *reinterpret_cast<const uint4*>(ha + hw + 2 * HDR_WORDS);
-            }
+            if (!in_ov) w4 = *reinterpret_cast<const uint4*>(ha + hw + HDR_WORDS);   // (the arena has slack)
         } else {
             const uint32_t* const a = (cur.fl & FR_OV) ? ov.arena : s.arena;
             blk_at = cur.pos & ~3ull;                       // (rows are padded to 16 B)
@@ -2168,8 +2167,7 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
                 cur = Frame{beg, n_all, (uint16_t)od, (uint16_t)(((v.z & HDR_SEQ) ? FR_SEQ : 0) | (in_ov ? FR_OV : 0))};
                 win = w4;
                 wbeg = in_ov ? ~0ull : beg;
-                blk = b4;
-                blk_at = in_ov || !o.edge_blocks ? ~0ull : beg + WINDOW_WORDS;
+                blk_at = ~0ull;
                 if (o.prefetch && !in_ov && (od - 1 >= 2 || !o.leaf_sets_blind)) {
                     // the window's subject sets: their header lines start loading now (no register)
 #pragma unroll
