@@ -3628,11 +3628,11 @@ uint32_t t0_stream_dyn() {
 }
 const char* t0_kernel_name(int var) {
     switch (var) {
-        case 0: return "keto::check_wave_kernel<4, false, 4, 16, false>";
-        case 1: return "keto::check_wave_kernel<4, false, 4, 8, false>";
-        case 2: return "keto::check_wave_kernel<4, false, 12, 4, false>";
-        case 3: return "keto::check_wave_kernel<4, false, 8, 8, false>";
-        default: return "keto::check_wave_kernel<8, false, 8, 8, false>";
+        case 0: return "keto::check_wave_kernel<4, false, 4, 16, false, false>";
+        case 1: return "keto::check_wave_kernel<4, false, 4, 8, false, false>";
+        case 2: return "keto::check_wave_kernel<4, false, 12, 4, false, false>";
+        case 3: return "keto::check_wave_kernel<4, false, 8, 8, false, false>";
+        default: return "keto::check_wave_kernel<8, false, 8, 8, false, false>";
     }
 }
 CheckKernelFn t0_kernel(int var, bool count) {
