@@ -187,6 +187,20 @@ void keto_snapshot_release(keto_snapshot* s);
  * internal/driver/registry_default.go:159-171).  Replicas are independent snapshots afterwards. */
 int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot** out);
 
+/* Persisted snapshot (the optional on-disk CSR): keto_snapshot_save writes the
+ * host tables of an unpartitioned snapshot at its current version (the interned strings, the rows in
+ * ORDER BY order with their page cuts and edges, the collision classes, the rows writes changed) to
+ * `path` (through <path>.tmp and a rename, so an interrupted save leaves an older file intact), with
+ * the caller's 64-bit `tag` -- e.g. the table's last commit covered, so that a restarting server
+ * replays only later transactions (the reference re-reads the table on every query,
+ * internal/persistence/sql/relationtuples.go:249-251; a GPU server otherwise rebuilds the snapshot
+ * from a full scan and sort).  keto_snapshot_load reads it back, lays it out and uploads it to
+ * `device` (-1: host only); *tag_out (may be NULL) gets the tag.  The loaded snapshot answers every
+ * call exactly as the saved one did and has its version.  A file that is not a snapshot, has another
+ * format, is truncated or fails a section checksum: KETO_E_INVALID. */
+int keto_snapshot_save(const keto_snapshot* s, const char* path, uint64_t tag);
+int keto_snapshot_load(const char* path, int32_t device, keto_snapshot** out, uint64_t* tag_out);
+
 /* Snapshot lifecycle: apply one write transaction the way TransactRelationTuples does
  * (internal/persistence/sql/relationtuples.go:289-297): the inserts first (each after every equal
  * tuple, as commit_time orders them, :128-149), then the deletes (every tuple equal in namespace,

@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libketo_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["snapshot.cpp", "resolve.cpp", "delta.cpp", "capi.cpp", "engine.hip", "route.hip", "migrate.hip", "proto.hip", "reach.hip", "resolve_dev.hip", "comm.cpp"]
+SOURCES = ["snapshot.cpp", "resolve.cpp", "delta.cpp", "persist.cpp", "capi.cpp", "engine.hip", "route.hip", "migrate.hip", "proto.hip", "reach.hip", "resolve_dev.hip", "comm.cpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 HOST_HIP = ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]   # host-only sources using the HIP / RCCL APIs
 

@@ -39,6 +39,7 @@ EXPORTS = [
     "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
     "keto_comm_id", "keto_comm_init", "keto_comm_free", "keto_check_batch_sharded", "keto_check_batch_routed",
     "keto_comm_close_filters", "keto_comm_init_local", "keto_snapshot_clone", "keto_check_batch_packed",
+    "keto_snapshot_save", "keto_snapshot_load",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -339,6 +340,20 @@ class Snapshot:
         h = C.c_void_p()
         _check(self.lib.keto_snapshot_clone(self.h, C.c_int32(device), C.byref(h)))
         return Snapshot(h, self.lib)
+
+    def save(self, path, tag: int = 0) -> None:
+        """keto_snapshot_save: the host tables at the current version to `path`, with the caller's tag."""
+        _check(self.lib.keto_snapshot_save(self.h, os.fsencode(path), C.c_uint64(tag)))
+
+    @classmethod
+    def load(cls, path, device: int = 0):
+        """keto_snapshot_load: a snapshot read back from `path` (device -1: host only); returns
+        (snapshot, tag)."""
+        lib = load()
+        h = C.c_void_p()
+        tag = C.c_uint64()
+        _check(lib.keto_snapshot_load(os.fsencode(path), C.c_int32(device), C.byref(h), C.byref(tag)))
+        return cls(h, lib), tag.value
 
     def upload_part(self, part: int, n_parts: int, device: int = 0, mode: int = PART_SHARED, hot_bytes: int = 0):
         """Edge-partitioned upload of a host-only snapshot (keto_snapshot_upload_part_mode; a migrating

@@ -406,6 +406,27 @@ int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot*
     });
 }
 
+int keto_snapshot_save(const keto_snapshot* s, const char* path, uint64_t tag) {
+    return guarded([&] {
+        if (!s || !path) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<std::shared_mutex> lk(s->s->rw);        // one version: no apply under us
+        save_snapshot(*s->s, path, tag);
+        return KETO_OK;
+    });
+}
+
+int keto_snapshot_load(const char* path, int32_t device, keto_snapshot** out, uint64_t* tag_out) {
+    return guarded([&] {
+        if (!path || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        *out = nullptr;
+        auto h = std::make_unique<keto_snapshot>();
+        h->s = load_snapshot(path, tag_out);
+        if (device >= 0) device_upload(*h->s, device);
+        *out = h.release();
+        return KETO_OK;
+    });
+}
+
 void keto_snapshot_release(keto_snapshot* s) { delete s; }
 
 int keto_snapshot_get_stats(const keto_snapshot* h, keto_snapshot_stats* out) {

@@ -428,22 +428,36 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
     if (const char* base = getenv("KETO_TEST_ARENA_BASE")) w = strtoull(base, nullptr, 0) & ~(uint64_t)(LINE_WORDS - 1);
     // test hook: a split layout whose root rows start at this word (tests/test_gpu_arena_split.py)
     const char* root_base = getenv("KETO_TEST_ROOT_BASE");
-    // the root rows' words, to see whether the layout must split (roots come last)
+    // what the placement needs of each row, gathered in arena order on the builder's threads (the
+    // rows come in band order, so these are random reads): edge count (bits 0..39), id-table log2
+    // (40..45), closure filter (46), stub (47), root row (48)
+    constexpr uint64_t P_CB = 1ull << 46, P_STUB = 1ull << 47, P_ROOT = 1ull << 48;
+    std::vector<uint64_t> pk(kept);
+    std::vector<uint64_t> root_part(std::max(1u, build_threads()), 0);
+    const unsigned th = kept >= par_min() ? build_threads() : 1u;
+    par_chunks(kept, th, 1 << 14, [&](uint64_t b, uint64_t e, unsigned t) {
+        uint64_t rw = 0;
+        for (uint64_t x = b; x < e; ++x) {
+            const uint32_t r = L.rows_by_unit[x];
+            const bool stub = !keep[r], root = S.is_root[r] != 0;
+            const uint64_t h = stub ? 0 : S.row_hlog2(r), n = stub ? 0 : row_size(S, r);
+            pk[x] = n | (h << 40) | (root ? P_ROOT : P_CB) | (stub ? P_STUB : 0);
+            // the root rows' words, to see whether the layout must split (roots come last)
+            if (root && !stub) rw += (h ? (1ull << h) : 0) + HDR_WORDS + ((n + 3) & ~3ull) + LINE_WORDS;   // + alignment
+        }
+        root_part[t] += rw;
+    });
     uint64_t root_words = 0;
-    for (uint64_t x = 0; x < kept; ++x) {
-        const uint32_t r = L.rows_by_unit[x];
-        if (!S.is_root[r] || !keep[r]) continue;
-        const uint32_t h = S.row_hlog2(r);
-        root_words += (h ? (1ull << h) : 0) + HDR_WORDS + ((row_size(S, r) + 3) & ~3ull) + LINE_WORDS;   // + alignment
-    }
+    for (uint64_t v : root_part) root_words += v;
     L.tgt_tail = L.tgt_end = L.roots_at = 0;
     // test hook: the target reserve's size in words (a small one fills after a few writes)
     const char* reserve_words = getenv("KETO_TEST_TGT_RESERVE");
     bool in_roots = false;
     for (uint64_t x = 0; x < kept; ++x) {
-        const uint32_t r = L.rows_by_unit[x];
-        const bool stub = !keep[r];                                  // header + closure block only
-        if (S.is_root[r] && !stub && !in_roots) {
+        const uint64_t p = pk[x];
+        const bool stub = (p & P_STUB) != 0;                         // header + closure block only
+        const bool root = (p & P_ROOT) != 0;
+        if (root && !stub && !in_roots) {
             in_roots = true;
             if (root_base || w + root_words > TARGET_MAX_WORDS) {
                 // split: targets end here; a reserve for targets writes add, then the roots
@@ -455,24 +469,26 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
                 w = L.roots_at;
             }
         }
-        const uint32_t h = stub ? 0 : S.row_hlog2(r);
+        const uint32_t h = (uint32_t)(p >> 40) & 63u;
         const uint64_t table = h ? (1ull << h) : 0;
-        const uint64_t cb = S.is_root[r] ? 0 : CB_WORDS;          // closure filter
+        const uint64_t cb = (p & P_CB) ? CB_WORDS : 0;              // closure filter
         uint64_t total = 0;
-        w = arena_fit(w, table, cb, stub ? 0 : row_size(S, r), total);
+        w = arena_fit(w, table, cb, p & ((1ull << 40) - 1), total);
         const uint64_t unit = (w + table + cb) / HDR_WORDS;
-        if (!S.is_root[r] || stub ? unit >= (uint64_t)EDGE_VAL : unit >= HANDLE_MAX)
-            throw Error{KETO_E_RANGE, S.is_root[r] && !stub ? "device arena exceeds 2^32 16-byte units"
-                                                            : "subject-set targets exceed 2^31 16-byte units"};
-        L.unit_of_row[r] = (uint32_t)unit;
+        if (!root || stub ? unit >= (uint64_t)EDGE_VAL : unit >= HANDLE_MAX)
+            throw Error{KETO_E_RANGE, root && !stub ? "device arena exceeds 2^32 16-byte units"
+                                                    : "subject-set targets exceed 2^31 16-byte units"};
         L.layout_units[x] = (uint32_t)unit;
-        if (!S.is_root[r] && !stub) L.shared_words += total;
+        if (!root && !stub) L.shared_words += total;
         w += total;
-        if (mode == PART_MIGRATE && band[r] >= hot_band) {          // the replicated prefix so far
+        if (mode == PART_MIGRATE && band[L.rows_by_unit[x]] >= hot_band) {   // the replicated prefix so far
             L.hot_words = w;
             ++L.hot_rows;
         }
     }
+    par_chunks(kept, th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+        for (uint64_t x = b; x < e; ++x) L.unit_of_row[L.rows_by_unit[x]] = L.layout_units[x];
+    });
     if (w > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
     if (mode == PART_MIGRATE && w > TARGET_MAX_WORDS)
         throw Error{KETO_E_RANGE, "a migrating part's arena exceeds 2^31 16-byte units"};
@@ -488,18 +504,24 @@ void compute_layout(Snapshot& S) {
     std::vector<uint8_t> band(R, 0);
     {
         std::vector<uint32_t> indeg(R, 0);
-        for (uint32_t r = 0; r < R; ++r) {
-            const auto ed = S.row_edges(r);
-            for (uint64_t i = 0; i < ed.second; ++i) {
-                const uint32_t e = ed.first[i];
-                if ((e & EDGE_SET) && e != EDGE_POISON && (e & EDGE_VAL) < R) ++indeg[e & EDGE_VAL];
+        const unsigned th = R >= par_min() ? build_threads() : 1u;
+        par_chunks(R, th, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t r = b; r < e; ++r) {
+                const auto ed = S.row_edges((uint32_t)r);
+                for (uint64_t i = 0; i < ed.second; ++i) {
+                    const uint32_t x = ed.first[i];
+                    if ((x & EDGE_SET) && x != EDGE_POISON && (x & EDGE_VAL) < R)
+                        __atomic_fetch_add(&indeg[x & EDGE_VAL], 1u, __ATOMIC_RELAXED);
+                }
             }
-        }
+        });
         S.is_root.assign(R, 0);
-        for (uint32_t r = 0; r < R; ++r) {
-            band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
-            S.is_root[r] = indeg[r] == 0;
-        }
+        par_chunks(R, th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
+            for (uint64_t r = b; r < e; ++r) {
+                band[r] = indeg[r] ? (uint8_t)(32 - __builtin_clz(indeg[r])) : 0;
+                S.is_root[r] = indeg[r] == 0;
+            }
+        });
     }
     if (S.part_mode == PART_MIGRATE && S.n_parts > MIG_MAX_PARTS)
         throw Error{KETO_E_INVALID, "a migrating partition has at most 30 parts"};

@@ -387,6 +387,10 @@ std::unique_ptr<Snapshot> build_snapshot_csr(const keto_namespace* ns, uint32_t 
 
 // host copy of an unpartitioned snapshot at its current version, laid out afresh (snapshot.cpp)
 std::unique_ptr<Snapshot> clone_host(const Snapshot& s);
+// persist.cpp: the host tables of an unpartitioned snapshot to / from one file (keto_snapshot_save /
+// keto_snapshot_load); the loaded snapshot is laid out afresh, as a clone is
+void save_snapshot(const Snapshot& s, const char* path, uint64_t tag);
+std::unique_ptr<Snapshot> load_snapshot(const char* path, uint64_t* tag_out);
 
 // Batch-local rows for wildcard requests that no stored subject set materialized: they can only
 // be top-level (check) or root (expand) rows, never edge targets.  Row ids >= base.
