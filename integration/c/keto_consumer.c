@@ -18,6 +18,10 @@
  * applies every write transaction to each replica, and rebuilds them all when one answers
  * KETO_E_REBUILD.
  *
+ * A restart ("S" line): the server saves the first replica (keto_snapshot_save, tagged with its
+ * version), releases every replica, loads the file back onto the first device (keto_snapshot_load)
+ * and clones it to the others, as registry_gpu.go's loadFile does when the table has not changed.
+ *
  * Input (tab-separated lines; empty fields allowed), executed in order:
  *   P <page_size>        V <device>        R <device> <device> ...   (replicas; default: V's device)
  *   N <ns id> <name>
@@ -28,10 +32,11 @@
  *   E I <subject id> <max depth> <global max depth>
  *   E S <ns> <object> <relation> <max depth> <global max depth>
  *   A+ <tuple as after T>   A- <tuple as after T>   A!   (one write transaction: inserts, deletes, commit)
+ *   S <path>             (restart from a persisted snapshot)
  * Consecutive C lines with one global max depth form one keto_check_batch; consecutive E lines one
  * keto_expand_batch.  Output (tab-separated): "check <i> <allowed> <status>",
  * "expand <i> <status> <json|null|error> <proto hex|->", "apply <rc> <version> <rebuilt>", "stats ...",
- * "nodevice <rc>", "done".
+ * "restart <version> <tag>", "nodevice <rc>", "done".
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -512,6 +517,21 @@ int main(int argc, char** argv) {
             snap = reps[0];
             printf("apply\t%d\t%llu\t%d\n", rc, (unsigned long long)v, rebuilt);
             n_ins = n_del = 0;
+        } else if (!strcmp(l->f[0], "S")) {
+            const uint64_t v0 = keto_snapshot_version(reps[0]);
+            rc = keto_snapshot_save(reps[0], l->f[1], v0);
+            if (rc != KETO_OK) fail("keto_snapshot_save", rc);
+            for (int k = 0; k < n_reps; ++k) keto_snapshot_release(reps[k]);
+            uint64_t tag = 0;
+            rc = keto_snapshot_load(l->f[1], devices[0], &reps[0], &tag);
+            if (rc != KETO_OK) fail("keto_snapshot_load", rc);
+            if (tag != v0 || keto_snapshot_version(reps[0]) != v0) return 13;
+            for (int k = 1; k < n_reps; ++k) {
+                rc = keto_snapshot_clone(reps[0], devices[k], &reps[k]);
+                if (rc != KETO_OK) fail("keto_snapshot_clone", rc);
+            }
+            snap = reps[0];
+            printf("restart\t%llu\t%llu\n", (unsigned long long)v0, (unsigned long long)tag);
         }
         ++i;
     }

@@ -55,7 +55,14 @@ func GPUDevicesFromEnv() []int {
 // gpuRowSource is the persister's full scan (internal/persistence/sql/snapshot_gpu.go).
 type gpuRowSource interface {
 	SnapshotRows(ctx context.Context) ([]gpu.Row, error)
+	SnapshotFingerprint(ctx context.Context) (uint64, error)
 }
+
+// GPUSnapshotFileFromEnv is where the GPU path keeps its persisted snapshot (KETO_GPU_SNAPSHOT_FILE;
+// empty: none).  A server that starts with a file saved under the table's current fingerprint loads
+// it (gpu.Load: about 15 s for 1B tuples) instead of scanning and sorting the table; every build
+// from a scan writes the file again.
+func GPUSnapshotFileFromEnv() string { return os.Getenv("KETO_GPU_SNAPSHOT_FILE") }
 
 type gpuState struct {
 	r       *RegistryDefault
@@ -140,11 +147,49 @@ func (g *gpuState) build(ctx context.Context) ([]*gpu.Snapshot, error) {
 	if !ok {
 		return nil, errors.New("gpu: the persister has no full-scan source")
 	}
+	path := GPUSnapshotFileFromEnv()
+	var fp uint64
+	if path != "" {
+		var err error
+		if fp, err = src.SnapshotFingerprint(ctx); err != nil {
+			return nil, err
+		}
+		if snaps, ok := g.loadFile(path, fp); ok {
+			return snaps, nil
+		}
+	}
 	rows, err := src.SnapshotRows(ctx)
 	if err != nil {
 		return nil, err
 	}
-	return g.buildFrom(ctx, rows)
+	snaps, err := g.buildFrom(ctx, rows)
+	if err == nil && path != "" {
+		_ = snaps[0].Save(path, fp) // best effort: without the file the next start scans again
+	}
+	return snaps, err
+}
+
+// loadFile: the persisted snapshot at path, if it was saved under fingerprint fp, on the first
+// device and cloned to the others; ok is false (and nothing is kept) otherwise.
+func (g *gpuState) loadFile(path string, fp uint64) ([]*gpu.Snapshot, bool) {
+	first, tag, err := gpu.Load(path, g.devices[0])
+	if err != nil {
+		return nil, false
+	}
+	if tag != fp {
+		first.Close()
+		return nil, false
+	}
+	out := []*gpu.Snapshot{first}
+	for _, d := range g.devices[1:] {
+		c, err := first.Clone(d)
+		if err != nil {
+			gpu.CloseAll(out)
+			return nil, false
+		}
+		out = append(out, c)
+	}
+	return out, true
 }
 
 func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) ([]*gpu.Snapshot, error) {

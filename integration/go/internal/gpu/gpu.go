@@ -193,6 +193,33 @@ func (s *Snapshot) Clone(device int) (*Snapshot, error) {
 	return &Snapshot{h: h, Version: s.Version}, nil
 }
 
+// Save writes the snapshot's host tables at its current version to path (keto_snapshot_save),
+// with the caller's tag: typically the table's last commit the snapshot covers, so that a restarting
+// server loads the file and replays only the transactions committed after it instead of scanning
+// and sorting the whole table again (internal/persistence/sql/relationtuples.go:249-251).
+func (s *Snapshot) Save(path string, tag uint64) error {
+	cp := C.CString(path)
+	defer C.free(unsafe.Pointer(cp))
+	if rc := C.keto_snapshot_save(s.h, cp, C.uint64_t(tag)); rc != C.KETO_OK {
+		return lastErr(rc)
+	}
+	return nil
+}
+
+// Load reads a snapshot written by Save and uploads it to HIP device `device` (-1: host only);
+// it returns the snapshot and the tag it was saved with.  A damaged, truncated or foreign file is
+// an error (the caller rebuilds from the table).
+func Load(path string, device int) (*Snapshot, uint64, error) {
+	cp := C.CString(path)
+	defer C.free(unsafe.Pointer(cp))
+	var h *C.keto_snapshot
+	var tag C.uint64_t
+	if rc := C.keto_snapshot_load(cp, C.int32_t(device), &h, &tag); rc != C.KETO_OK {
+		return nil, 0, lastErr(rc)
+	}
+	return &Snapshot{h: h, Version: uint64(C.keto_snapshot_version(h))}, uint64(tag), nil
+}
+
 // BuildReplicas builds one snapshot per device of a node (one server process driving every GPU):
 // the rows are sorted and uploaded once by Build on devices[0], the other devices get clones.
 func BuildReplicas(nss []*namespace.Namespace, rows []Row, devices []int) ([]*Snapshot, error) {

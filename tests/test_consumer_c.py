@@ -153,11 +153,15 @@ def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed, replica
             store.insert(t)
         for t in dels:
             store.delete(t)
+        if step in (2, 4):                             # a server restart from its persisted snapshot
+            lines.append(f"S\t{tmp_path / 'snap.keto'}")
     p = tmp_path / "in.tsv"
     p.write_text("\n".join(lines) + "\n")
     r = subprocess.run([consumer, str(p)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     got = [ln.split("\t") for ln in r.stdout.splitlines() if ln.split("\t")[0] in ("check", "expand", "apply")]
+    restarts = [ln.split("\t") for ln in r.stdout.splitlines() if ln.startswith("restart")]
+    assert len(restarts) == 2 and all(x[1] == x[2] for x in restarts)
     # the consumer runs a batch of checks before the expands of a step: same order as `want`
     assert [g[0] for g in got] == [w[0] for w in want]
     versions = 0

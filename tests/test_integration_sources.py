@@ -115,6 +115,24 @@ def test_multi_gpu_server_process():
     assert "r.idle" in bat                              # a batch goes to a replica with none in flight
 
 
+def test_persisted_snapshot_at_startup():
+    """A server started with KETO_GPU_SNAPSHOT_FILE loads the persisted snapshot (keto_snapshot_load)
+    when its tag is the table's current fingerprint (row count + newest commit_time), clones it to
+    the other devices, and otherwise scans, builds and saves the file again (keto_snapshot_save)."""
+    reg = _code(open(os.path.join(GO, "internal", "driver", "registry_gpu.go")).read())
+    gpu_go = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
+    sql = _code(open(os.path.join(GO, "internal", "persistence", "sql", "snapshot_gpu.go")).read())
+    assert "C.keto_snapshot_save(" in gpu_go and "C.keto_snapshot_load(" in gpu_go
+    assert re.search(r"func \(s \*Snapshot\) Save\(path string, tag uint64\) error", gpu_go)
+    assert re.search(r"func Load\(path string, device int\) \(\*Snapshot, uint64, error\)", gpu_go)
+    assert re.search(r"func \(p \*Persister\) SnapshotFingerprint\(ctx context\.Context\) \(uint64, error\)", sql)
+    assert "SnapshotFingerprint(ctx context.Context) (uint64, error)" in reg      # part of the row source
+    load_at = reg.index("g.loadFile(path, fp)")
+    scan_at = reg.index("src.SnapshotRows(ctx)")
+    assert load_at < scan_at                                                    # the file first
+    assert ".Save(path, fp)" in reg and "tag != fp" in reg
+
+
 def test_collective_calls_never_skip_an_empty_batch():
     """keto_check_batch_sharded / _routed are collective: a rank with no request must still call them,
     or its peers wait (checkWith's collective flag)."""
