@@ -440,9 +440,18 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* s, const keto_check_re
  * n_parts = ranks): every rank passes its own batch; requests go to the parts owning their rows
  * (one all-to-all), are decided there -- on a migrating part by continuation-record rounds with an
  * all-reduce and all-to-alls per round -- and the decisions come back (a second all-to-all).  A
- * wildcard query that no stored subject set uses has no row to route by: KETO_E_INVALID. */
+ * wildcard query that no stored subject set uses has no row to route by: a shared-rows part answers
+ * it itself (its batch-local row from the whole graph's host tables); a migrating part returns
+ * KETO_E_INVALID.  Every rank returns the same code when any rank fails. */
 int keto_check_batch_routed(keto_comm* c, keto_snapshot* s, const keto_check_req* reqs, uint32_t n,
                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
+/* BuildTree (internal/expand/engine.go:33-102) over an edge-partitioned snapshot of shared-rows
+ * parts (KETO_PART_SHARED; this rank's part as above): every rank passes its own roots; a root row
+ * another part owns is expanded on that part (one all-to-all of roots, one of trees), every other
+ * root here, as keto_expand_batch does.  *out: one arena in request order, read with keto_tree_*
+ * against this rank's snapshot.  Migrating parts: KETO_E_INVALID.  Errors are agreed as above. */
+int keto_expand_batch_routed(keto_comm* c, keto_snapshot* s, const keto_expand_req* reqs, uint32_t n,
+                             int32_t global_max_depth, keto_tree_arena** out);
 /* A migrating partition's closure-filter exchange, once after every rank uploaded its part (before
  * the first keto_check_batch_routed; replaces the keto_part_filters / keto_part_close /
  * keto_part_closure_done loop a caller would otherwise run). */

@@ -92,6 +92,15 @@ func (c *Comm) CheckBatchRouted(s *Snapshot, reqs []*relationtuple.InternalRelat
 	})
 }
 
+// ExpandBatchRouted is BuildTree (internal/expand/engine.go:33-102) for this rank's roots over an
+// edge-partitioned snapshot of shared-rows parts (keto_expand_batch_routed): a root row another
+// part owns is expanded there.  Collective: every rank calls it, with an empty batch too.
+func (c *Comm) ExpandBatchRouted(s *Snapshot, subs []relationtuple.Subject, depths []int, globalMax int) ([][]Node, []error, error) {
+	return s.expandWith(subs, depths, func(cr *C.keto_expand_req, n C.uint32_t, a **C.keto_tree_arena) C.int {
+		return C.keto_expand_batch_routed(c.h, s.h, cr, n, C.int32_t(globalMax), a)
+	})
+}
+
 // CloseFilters runs a migrating partition's closure-filter exchange once after upload
 // (keto_comm_close_filters); it returns the rounds it took.
 func (c *Comm) CloseFilters(s *Snapshot) (int, error) {

@@ -424,10 +424,19 @@ type Node struct {
 // ErrUndecided per root.  Subjects are built from the node arena and keto_subject_fields: no text
 // codec on the way.
 func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([][]Node, []error, error) {
-	n := len(subs)
-	if n == 0 {
+	if len(subs) == 0 {
 		return nil, nil, nil
 	}
+	return s.expandWith(subs, depths, func(cr *C.keto_expand_req, n C.uint32_t, a **C.keto_tree_arena) C.int {
+		return C.keto_expand_batch(s.h, cr, n, C.int32_t(globalMax), a)
+	})
+}
+
+// expandWith runs one expand entry point over the roots and reads its arena (an empty batch still
+// makes the call: the routed form is collective).
+func (s *Snapshot) expandWith(subs []relationtuple.Subject, depths []int,
+	run func(cr *C.keto_expand_req, n C.uint32_t, a **C.keto_tree_arena) C.int) ([][]Node, []error, error) {
+	n := len(subs)
 	if len(depths) != n {
 		return nil, nil, fmt.Errorf("gpu: %d roots, %d depths", n, len(depths))
 	}
@@ -438,13 +447,13 @@ func (s *Snapshot) ExpandBatch(subs []relationtuple.Subject, depths []int, globa
 		total += subjectLen(sub)
 	}
 	m.strings(total)
-	cr := (*C.keto_expand_req)(m.alloc(n * int(C.sizeof_keto_expand_req)))
+	cr := (*C.keto_expand_req)(m.alloc((n + 1) * int(C.sizeof_keto_expand_req)))
 	cs := unsafe.Slice(cr, n)
 	for i, sub := range subs {
 		cs[i] = C.keto_expand_req{subject: m.subject(sub), max_depth: C.int32_t(depths[i])}
 	}
 	var a *C.keto_tree_arena
-	if rc := C.keto_expand_batch(s.h, cr, C.uint32_t(n), C.int32_t(globalMax), &a); rc != C.KETO_OK {
+	if rc := run(cr, C.uint32_t(n), &a); rc != C.KETO_OK {
 		return nil, nil, lastErr(rc)
 	}
 	defer C.keto_tree_arena_free(a)

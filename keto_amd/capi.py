@@ -39,7 +39,7 @@ EXPORTS = [
     "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
     "keto_comm_id", "keto_comm_init", "keto_comm_free", "keto_check_batch_sharded", "keto_check_batch_routed",
     "keto_comm_close_filters", "keto_comm_init_local", "keto_snapshot_clone", "keto_check_batch_packed",
-    "keto_snapshot_save", "keto_snapshot_load",
+    "keto_snapshot_save", "keto_snapshot_load", "keto_expand_batch_routed",
 ]
 PART_SHARED, PART_MIGRATE = 0, 1
 MIG_MAX_PARTS = 30
@@ -750,12 +750,22 @@ class Snapshot:
         from its nodes and keto_subject_fields (the Go shim's path), as a dict."""
         keep = _Keep()
         n = len(reqs)
-        arr = (KExpandReq * max(1, n))()
+        arr = self._expand_reqs(keep, reqs)
+        a = C.c_void_p()
+        _check(self.lib.keto_expand_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth), C.byref(a)))
+        return self._arena_results(a, n, want_nodes, want_proto, proto_all, json_all, via_fields)
+
+    @staticmethod
+    def _expand_reqs(keep, reqs):
+        arr = (KExpandReq * max(1, len(reqs)))()
         for k, (sub, depth) in enumerate(reqs):
             arr[k].subject = subject_struct(keep, sub)
             arr[k].max_depth = depth
-        a = C.c_void_p()
-        _check(self.lib.keto_expand_batch(self.h, arr, C.c_uint32(n), C.c_int32(global_max_depth), C.byref(a)))
+        return arr
+
+    def _arena_results(self, a, n, want_nodes=False, want_proto=False, proto_all=None, json_all=False,
+                       via_fields=False):
+        """The trees of arena `a` (freed here) as expand_batch returns them."""
         out = []
         try:
             for i in range(n):
@@ -844,6 +854,16 @@ class Comm:
     def check_batch_routed(self, snap, reqs, global_max_depth=5, n=None):
         """keto_check_batch_routed (this rank's part of an edge-partitioned snapshot)."""
         return self._batch(self.lib.keto_check_batch_routed, snap, reqs, global_max_depth, n)
+
+    def expand_batch_routed(self, snap, reqs, global_max_depth=5, **kw):
+        """keto_expand_batch_routed (this rank's shared-rows part): reqs and results as in
+        Snapshot.expand_batch."""
+        keep = _Keep()
+        arr = snap._expand_reqs(keep, reqs)
+        a = C.c_void_p()
+        _check(self.lib.keto_expand_batch_routed(self.h, snap.h, arr, C.c_uint32(len(reqs)),
+                                                 C.c_int32(global_max_depth), C.byref(a)))
+        return snap._arena_results(a, len(reqs), **kw)
 
     def close_filters(self, snap) -> int:
         rounds = C.c_uint32(0)

@@ -17,21 +17,6 @@
 using namespace keto;
 
 
-struct keto_tree_arena {
-    ExpandResult r;
-    uint32_t ov_base = 0xFFFFFFFFu;
-    std::vector<RowKey> ov_keys;           // overlay roots (wildcard queries)
-    uint32_t extra_base = 0;               // subject-id strings not in the snapshot
-    std::vector<std::string> extra;
-    // keto_tree_json_all / keto_tree_proto_all: the encodings of a sizing call (buf too small), kept
-    // for the filling call that follows it, so a size-then-fill pair encodes once
-    mutable std::mutex enc_mu;
-    mutable int enc_kind = 0;              // 0 none, 1 JSON, 2 protobuf
-    mutable uint64_t enc_uid = 0;          // the snapshot the encodings were made with (Snapshot::uid)
-    mutable uint64_t enc_version = 0;
-    mutable std::vector<std::string> enc;
-};
-
 thread_local std::string keto::g_err;
 
 namespace {
@@ -850,57 +835,73 @@ int keto_check_steps_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
     });
 }
 
+extern "C++" {
+namespace keto {
+// keto_expand_batch's body (the caller holds the snapshot's lock shared); skip[i] != 0: request i is
+// answered elsewhere (comm.cpp routes it to the part owning its root row) and gets an empty slot
+void expand_named(Snapshot& S, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth, keto_tree_arena& A,
+                  const uint8_t* skip) {
+    keto_tree_arena* a = &A;
+    Overlay ov;
+    ov.base = S.n_rows();
+    a->ov_base = ov.base;
+    a->extra_base = (uint32_t)S.strs.size();
+    std::vector<uint32_t> root(n), flags(n), vid(n, 0);
+    std::vector<int32_t> depth(n);
+    std::vector<uint8_t> not_found(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        const keto_subject& sj = reqs[i].subject;
+        depth[i] = reqs[i].max_depth;
+        if (skip && skip[i]) {                                          // answered on another part
+            root[i] = KETO_NO_ROW;
+            flags[i] = 1;
+            continue;
+        }
+        if (sj.kind == 0) {                                             // SubjectID -> Leaf
+            int64_t sid = S.lookup_str(sv(sj.id));
+            if (sid < 0) {
+                sid = a->extra_base + a->extra.size();
+                a->extra.emplace_back(sv(sj.id));
+            }
+            root[i] = (uint32_t)sid;
+            flags[i] = 0;
+            continue;
+        }
+        flags[i] = 1;
+        RowKey k;
+        int64_t r = S.resolve_query(sv(sj.set_namespace), sv(sj.set_object), sv(sj.set_relation), &k);
+        if (r == -2) {
+            not_found[i] = 1;
+            root[i] = KETO_NO_ROW;
+        } else if (r == -1) {
+            root[i] = KETO_NO_ROW;
+        } else if (r == -3) {
+            root[i] = handle_of(S, &ov, overlay_row(S, ov, k));
+            std::string key = std::string(sv(sj.set_namespace)) + ":" + std::string(sv(sj.set_object)) + "#" +
+                              std::string(sv(sj.set_relation));
+            vid[i] = S.vid_of_key(key);
+        } else {
+            if (!S.present((uint32_t)r)) throw Error{KETO_E_INVALID, "expand root is owned by another part"};
+            root[i] = S.handle((uint32_t)r);
+            vid[i] = S.vid_of_row((uint32_t)r);
+        }
+    }
+    a->ov_keys = ov.keys;
+    device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r);
+    for (uint32_t i = 0; i < n; ++i)
+        if (not_found[i]) a->r.status[i] = KETO_EXPAND_NOT_FOUND;
+}
+}  // namespace keto
+}  // extern "C++"
+
 int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth,
                       keto_tree_arena** out) {
     return guarded([&] {
         if (!h || !out || (n && !reqs)) throw Error{KETO_E_INVALID, "NULL argument"};
         std::shared_lock<std::shared_mutex> lk(h->s->rw);
         *out = nullptr;
-        Snapshot& S = *h->s;
         auto a = std::make_unique<keto_tree_arena>();
-        Overlay ov;
-        ov.base = S.n_rows();
-        a->ov_base = ov.base;
-        a->extra_base = (uint32_t)S.strs.size();
-        std::vector<uint32_t> root(n), flags(n), vid(n, 0);
-        std::vector<int32_t> depth(n);
-        std::vector<uint8_t> not_found(n, 0);
-        for (uint32_t i = 0; i < n; ++i) {
-            const keto_subject& sj = reqs[i].subject;
-            depth[i] = reqs[i].max_depth;
-            if (sj.kind == 0) {                                             // SubjectID -> Leaf
-                int64_t sid = S.lookup_str(sv(sj.id));
-                if (sid < 0) {
-                    sid = a->extra_base + a->extra.size();
-                    a->extra.emplace_back(sv(sj.id));
-                }
-                root[i] = (uint32_t)sid;
-                flags[i] = 0;
-                continue;
-            }
-            flags[i] = 1;
-            RowKey k;
-            int64_t r = S.resolve_query(sv(sj.set_namespace), sv(sj.set_object), sv(sj.set_relation), &k);
-            if (r == -2) {
-                not_found[i] = 1;
-                root[i] = KETO_NO_ROW;
-            } else if (r == -1) {
-                root[i] = KETO_NO_ROW;
-            } else if (r == -3) {
-                root[i] = handle_of(S, &ov, overlay_row(S, ov, k));
-                std::string key = std::string(sv(sj.set_namespace)) + ":" + std::string(sv(sj.set_object)) + "#" +
-                                  std::string(sv(sj.set_relation));
-                vid[i] = S.vid_of_key(key);
-            } else {
-                if (!S.present((uint32_t)r)) throw Error{KETO_E_INVALID, "expand root is owned by another part"};
-                root[i] = S.handle((uint32_t)r);
-                vid[i] = S.vid_of_row((uint32_t)r);
-            }
-        }
-        a->ov_keys = ov.keys;
-        device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r);
-        for (uint32_t i = 0; i < n; ++i)
-            if (not_found[i]) a->r.status[i] = KETO_EXPAND_NOT_FOUND;
+        expand_named(*h->s, reqs, n, global_max_depth, *a, nullptr);
         *out = a.release();
         return KETO_OK;
     });

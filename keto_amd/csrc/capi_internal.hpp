@@ -3,6 +3,7 @@
 #pragma once
 
 #include <memory>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -12,6 +13,21 @@
 
 struct keto_snapshot {
     std::unique_ptr<keto::Snapshot> s;
+};
+
+struct keto_tree_arena {
+    keto::ExpandResult r;
+    uint32_t ov_base = 0xFFFFFFFFu;
+    std::vector<keto::RowKey> ov_keys;     // overlay roots (wildcard queries)
+    uint32_t extra_base = 0;               // subject-id strings not in the snapshot
+    std::vector<std::string> extra;
+    // keto_tree_json_all / keto_tree_proto_all: the encodings of a sizing call (buf too small), kept
+    // for the filling call that follows it, so a size-then-fill pair encodes once
+    mutable std::mutex enc_mu;
+    mutable int enc_kind = 0;              // 0 none, 1 JSON, 2 protobuf
+    mutable uint64_t enc_uid = 0;          // the snapshot the encodings were made with (Snapshot::uid)
+    mutable uint64_t enc_version = 0;
+    mutable std::vector<std::string> enc;
 };
 
 namespace keto {
@@ -44,5 +60,10 @@ std::vector<WildReq> resolve_all(const Snapshot& S, const keto_check_req* reqs, 
 // keto_check_batch's body, the caller holding the snapshot's lock shared (capi.cpp)
 void check_named(Snapshot& S, const keto_check_req* reqs, uint32_t n, int32_t global_max_depth, uint8_t* allowed_out,
                  uint8_t* status_out);
+
+// keto_expand_batch's body, the caller holding the snapshot's lock shared (capi.cpp); skip[i] != 0:
+// request i is answered by another part (an empty slot here)
+void expand_named(Snapshot& S, const keto_expand_req* reqs, uint32_t n, int32_t global_max_depth, keto_tree_arena& a,
+                  const uint8_t* skip);
 
 }  // namespace keto

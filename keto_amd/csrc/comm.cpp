@@ -9,6 +9,9 @@
 //                               (one all-to-all), decided there, and the decisions come back (a
 //                               second all-to-all); on a migrating partition the owners run the
 //                               continuation-record rounds (an all-gather and all-to-alls a round)
+//   keto_expand_batch_routed    edge-partitioned snapshot (shared rows): every rank's expand roots
+//                               whose root row another part owns go to that part (one all-to-all),
+//                               are expanded there, and their trees come back (a second all-to-all)
 //   keto_comm_close_filters     a migrating partition's closure-filter exchange after upload
 //
 // Two transports carry the collectives:
@@ -673,6 +676,179 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
                 status_out[wild[k].i] = ws[k];
             }
         }
+        return KETO_OK;
+    });
+}
+
+// BuildTree (internal/expand/engine.go:33-102) for every rank's own roots over an edge-partitioned
+// snapshot of shared-rows parts.  A root whose row this part holds (a subject-set target, which
+// every part keeps, or one of this part's own root rows), a subject id, an unknown namespace, a
+// missing row or a wildcard query is expanded here, exactly as keto_expand_batch does it.  A root
+// row another part owns goes there as one word (row id, max depth); the owner expands it -- every
+// row below a root is a subject-set target, which the owner holds -- and returns the tree as
+// {status, node count, nodes}.  Node subjects are row and string ids of the whole graph, which every
+// part's host tables share, so a returned tree reads like a local one.  Both exchanges carry each
+// rank's status, so a failure anywhere ends the call with the same code on every rank.
+int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_req* reqs, uint32_t n,
+                             int32_t global_max_depth, keto_tree_arena** out) {
+    return guarded([&] {
+        if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
+        HIP_OK(hipSetDevice(c->device));
+        const int P = c->n;
+        Local mine;
+        Snapshot* Sp = nullptr;
+        std::shared_lock<std::shared_mutex> lk;
+        std::vector<uint8_t> routed(std::max<uint32_t>(n, 1), 0);
+        std::vector<std::vector<uint32_t>> to(P);        // request indices per owner part, in request order
+        std::vector<uint64_t> words;                     // (row id | max depth << 32), grouped by owner
+        auto local = std::make_unique<keto_tree_arena>();
+        if (out) *out = nullptr;
+        mine.run([&] {
+            if (!h || !out || (n && !reqs)) throw Error{KETO_E_INVALID, "NULL argument"};
+            Sp = h->s.get();
+            lk = std::shared_lock<std::shared_mutex>(Sp->rw);
+            if ((int)Sp->n_parts != P || (int)Sp->part != c->rank)
+                throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
+                                            "part = rank and n_parts = ranks)"};
+            if (P > 1 && Sp->part_mode != PART_SHARED)
+                throw Error{KETO_E_INVALID, "expand needs shared-rows parts (KETO_PART_SHARED)"};
+            injected(*c, "resolve");
+            const Snapshot& S = *Sp;
+            for (uint32_t i = 0; i < n; ++i) {
+                const keto_subject& sj = reqs[i].subject;
+                if (sj.kind != 1) continue;
+                const int64_t r = S.resolve_query(std::string_view(sj.set_namespace.p ? sj.set_namespace.p : "", sj.set_namespace.n),
+                                                  std::string_view(sj.set_object.p ? sj.set_object.p : "", sj.set_object.n),
+                                                  std::string_view(sj.set_relation.p ? sj.set_relation.p : "", sj.set_relation.n));
+                if (r < 0 || S.present((uint32_t)r)) continue;
+                const int32_t o = S.row_owner((uint32_t)r, (uint32_t)P);
+                if (o < 0 || o >= P || o == c->rank) throw Error{KETO_E_INVALID, "expand root " + std::to_string(i) + " has no owner part"};
+                routed[i] = 1;
+                to[o].push_back(i);
+            }
+            for (int p = 0; p < P; ++p)
+                for (uint32_t i : to[p]) {
+                    const keto_subject& sj = reqs[i].subject;
+                    const int64_t r = S.resolve_query(std::string_view(sj.set_namespace.p ? sj.set_namespace.p : "", sj.set_namespace.n),
+                                                      std::string_view(sj.set_object.p ? sj.set_object.p : "", sj.set_object.n),
+                                                      std::string_view(sj.set_relation.p ? sj.set_relation.p : "", sj.set_relation.n));
+                    words.push_back((uint64_t)(uint32_t)r | ((uint64_t)(uint32_t)reqs[i].max_depth << 32));
+                }
+            injected(*c, "expand");
+            if (n) expand_named(*Sp, reqs, n, global_max_depth, *local, routed.data());
+        });
+        // the roots to their owners, each count with this rank's status (the exchange is the agreement)
+        std::vector<uint64_t> cw(2ull * P);
+        for (int p = 0; p < P; ++p) {
+            cw[2 * p] = mine.code == KETO_OK ? to[p].size() : 0;
+            cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
+        }
+        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
+        std::vector<int64_t> codes(P);
+        std::vector<uint64_t> in(P), sb(P), rb(P);
+        for (int p = 0; p < P; ++p) {
+            in[p] = inw[2 * p];
+            codes[p] = (int64_t)inw[2 * p + 1];
+            sb[p] = to[p].size() * 8;
+            rb[p] = in[p] * 8;
+        }
+        settle(*c, mine, codes);
+        const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
+        uint64_t* d_words = c->a.get<uint64_t>(std::max<uint64_t>(words.size(), 1));
+        uint64_t* d_in = c->b.get<uint64_t>(std::max<uint64_t>(m, 1));
+        if (!words.empty())
+            HIP_OK(hipMemcpyAsync(d_words, words.data(), words.size() * 8, hipMemcpyHostToDevice, c->stream));
+        c->t->alltoallv(d_words, sb, d_in, rb, c->stream);
+        std::vector<uint64_t> got(m);
+        if (m) HIP_OK(hipMemcpyAsync(got.data(), d_in, m * 8, hipMemcpyDeviceToHost, c->stream));
+        sync(*c);
+        // expand the roots this part owns for the other ranks; pack the trees per origin rank
+        std::vector<uint64_t> pack, pb(P, 0);            // 8-B words: {status | nodes << 8}, nodes...
+        mine.run([&] {
+            if (!m) return;
+            injected(*c, "owner");
+            Snapshot& S = *Sp;
+            std::vector<uint32_t> root(m), flags(m, 1u), vid(m);
+            std::vector<int32_t> depth(m);
+            for (uint64_t k = 0; k < m; ++k) {
+                const uint32_t r = (uint32_t)got[k];
+                if (r >= S.n_rows() || !S.present(r)) throw Error{KETO_E_INVALID, "a routed expand root is not on its owner part"};
+                root[k] = S.handle(r);
+                vid[k] = S.vid_of_row(r);
+                depth[k] = (int32_t)(uint32_t)(got[k] >> 32);
+            }
+            ExpandResult er;
+            device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, er);
+            uint64_t k = 0;
+            for (int p = 0; p < P; ++p) {
+                const uint64_t w0 = pack.size();
+                for (uint64_t j = 0; j < in[p]; ++j, ++k) {
+                    const uint64_t nn = er.status[k] == KETO_EXPAND_TREE ? er.offset[k + 1] - er.offset[k] : 0;
+                    pack.push_back((uint64_t)er.status[k] | (nn << 8));
+                    const keto_tree_node* nd = er.nodes.data() + er.offset[k];
+                    for (uint64_t q = 0; q < nn; ++q) pack.push_back((uint64_t)nd[q].subject | ((uint64_t)nd[q].info << 32));
+                }
+                pb[p] = (pack.size() - w0) * 8;
+            }
+        });
+        std::vector<uint64_t> bw(2ull * P);
+        for (int p = 0; p < P; ++p) {
+            bw[2 * p] = mine.code == KETO_OK ? pb[p] : 0;
+            bw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
+        }
+        const std::vector<uint64_t> backw = c->t->alltoall_u64(bw, 2, c->stream);
+        std::vector<uint64_t> back(P);
+        for (int p = 0; p < P; ++p) {
+            back[p] = backw[2 * p];
+            codes[p] = (int64_t)backw[2 * p + 1];
+        }
+        settle(*c, mine, codes);
+        const uint64_t tot = std::accumulate(back.begin(), back.end(), 0ull);
+        uint64_t* d_pack = c->d.get<uint64_t>(std::max<uint64_t>(pack.size(), 1));
+        uint64_t* d_back = c->g.get<uint64_t>(std::max<uint64_t>(tot / 8, 1));
+        if (!pack.empty())
+            HIP_OK(hipMemcpyAsync(d_pack, pack.data(), pack.size() * 8, hipMemcpyHostToDevice, c->stream));
+        c->t->alltoallv(d_pack, pb, d_back, back, c->stream);
+        std::vector<uint64_t> trees(tot / 8);
+        if (tot) HIP_OK(hipMemcpyAsync(trees.data(), d_back, tot, hipMemcpyDeviceToHost, c->stream));
+        sync(*c);
+        // one arena in request order: the local trees, and the routed ones from their owners
+        ExpandResult& L = local->r;
+        ExpandResult R;
+        R.status.resize(n);
+        R.offset.assign((uint64_t)n + 1, 0);
+        std::vector<uint64_t> at(n, ~0ull);               // a routed tree's header word in `trees`
+        uint64_t w = 0;
+        for (int p = 0; p < P; ++p) {
+            const uint64_t end = w + back[p] / 8;
+            for (uint32_t i : to[p]) {
+                if (w >= end) throw Error{KETO_E_HIP, "expand trees missing from part " + std::to_string(p)};
+                at[i] = w;
+                w += 1 + (trees[w] >> 8);
+            }
+            if (w != end) throw Error{KETO_E_HIP, "expand trees from part " + std::to_string(p) + " do not match"};
+        }
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint64_t nn = routed[i] ? (trees[at[i]] >> 8) : L.offset[i + 1] - L.offset[i];
+            R.status[i] = routed[i] ? (uint8_t)(trees[at[i]] & 0xFF) : L.status[i];
+            R.offset[i + 1] = R.offset[i] + nn;
+        }
+        R.nodes.resize(R.offset[n]);
+        for (uint32_t i = 0; i < n; ++i) {
+            keto_tree_node* dst = R.nodes.data() + R.offset[i];
+            const uint64_t nn = R.offset[i + 1] - R.offset[i];
+            if (!routed[i]) {
+                if (nn) std::memcpy(dst, L.nodes.data() + L.offset[i], nn * sizeof(keto_tree_node));
+                continue;
+            }
+            for (uint64_t q = 0; q < nn; ++q) {
+                const uint64_t x = trees[at[i] + 1 + q];
+                dst[q].subject = (uint32_t)x;
+                dst[q].info = (uint32_t)(x >> 32);
+            }
+        }
+        local->r = std::move(R);
+        *out = local.release();
         return KETO_OK;
     });
 }

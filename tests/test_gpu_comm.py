@@ -405,7 +405,123 @@ def test_local_shared_parts_follow_writes(P, seed):
                 answered = True
                 assert ({0: "tree", 1: "nil", 2: "error"}[st_], js) == want_t, (seed, step, s_, d)
             assert answered, s_
+        # the same roots and more (subject ids, wildcard queries, unknown rows) from every rank through
+        # keto_expand_batch_routed: each rank's share, root rows expanded on their owners
+        shares = [exps[r::P] for r in range(P)]
+        res = _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], [(subj(s_), d) for s_, d, _ in shares[r]], g)))
+        for r, got in enumerate(res):
+            for (s_, d, _), (st_, js) in zip(shares[r], got):
+                try:
+                    tr = ExpandEngine(store, g).build_tree(s_, d)
+                    want_t = ("tree", tr.to_json()) if tr is not None else ("nil", None)
+                except NotFoundError:
+                    want_t = ("error", None)
+                assert ({0: "tree", 1: "nil", 2: "error"}[st_], js) == want_t, (seed, step, r, s_, d)
     for c in comms:
         c.close()
     for p in parts:
         p.close()
+
+
+@pytest.fixture(scope="module")
+def powerlaw_parts():
+    """The power-law graph (1/1024 scale) with its strings: a replicated snapshot, shared-rows parts
+    for P = 3, and expand roots of every kind (folders and groups, which every part keeps, and docs,
+    which one part owns)."""
+    from keto_amd.capi import PART_SHARED
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 1024), threads=8)
+    st = g.string_tuples(seed=3, threads=8)
+    full, _ = g.snapshot_from_strings(st, device=0)
+    P = 3
+    parts = []
+    for r in range(P):
+        part, _ = g.snapshot_from_strings(st, device=-1)
+        parts.append(part.upload_part(r, P, 0, mode=PART_SHARED))
+    q = g.queries(600, seed=17, depth=5, threads=8)
+    arr = g.string_requests(st, q, threads=8)
+
+    def text(k):
+        return k.p[:k.n].decode() if k.n else ""
+
+    roots = [(("set", text(arr[i].namespace_), text(arr[i].object), text(arr[i].relation)), 1 + i % 5)
+             for i in range(len(q))]
+    user = text(arr[0].subject.id)
+    roots += [(("id", user), 3), (("set", "nope", "x", "y"), 3), (("set", roots[0][0][1], "no such object", roots[0][0][3]), 3)]
+    yield g, st, full, parts, roots
+    full.close()
+    for p in parts:
+        p.close()
+    g.free_strings(st)
+    g.close()
+
+
+def test_local_expand_routed_powerlaw(powerlaw_parts):
+    """Three ranks' expand batches over shared-rows parts: every tree (nodes in pre-order, status)
+    equals the replicated snapshot's; roots owned by other parts cross."""
+    g, st, full, parts, roots = powerlaw_parts
+    P = len(parts)
+    want = full.expand_batch(roots, 5, want_nodes=True)
+    comms = _local_comms(P)
+    shares = [list(range(r, len(roots), P)) for r in range(P)]
+    res = _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], [roots[i] for i in shares[r]], 5,
+                                                               want_nodes=True)))
+    crossed = 0
+    for r, got in enumerate(res):
+        for k, i in enumerate(shares[r]):
+            assert got[k] == want[i], (r, i, roots[i])
+            crossed += 1
+    assert crossed == len(roots)
+    # an empty batch on one rank still takes part
+    res = _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], [] if r == 1 else roots[:50], 5)))
+    assert res[1] == [] and res[0] == res[2] == [w[:2] for w in want[:50]]
+    for c in comms:
+        c.close()
+
+
+@pytest.mark.parametrize("point", ["resolve", "expand", "owner"])
+def test_local_expand_error_agreement(powerlaw_parts, monkeypatch, point):
+    """A failure injected on rank 1 before the roots leave (resolve, local expand) or while it expands
+    other ranks' roots (owner): every rank returns the same code; the next call answers exactly."""
+    g, st, full, parts, roots = powerlaw_parts
+    P = len(parts)
+    comms = _local_comms(P)
+    monkeypatch.setenv("KETO_COMM_INJECT", f"1:{point}")
+    _agreed_failure(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], roots[r::P], 5)), 1, "injected")
+    monkeypatch.delenv("KETO_COMM_INJECT")
+    want = full.expand_batch(roots, 5)
+    res = _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], roots[r::P], 5)))
+    for r, got in enumerate(res):
+        assert got == want[r::P], r
+    for c in comms:
+        c.close()
+
+
+def test_expand_routed_refuses_migrating_parts(powerlaw_parts):
+    """Migrating parts do not expand: every rank returns KETO_E_INVALID, none waits."""
+    from keto_amd.capi import PART_MIGRATE
+    g, st, full, parts, roots = powerlaw_parts
+    P = 2
+    mig = []
+    for r in range(P):
+        sn = g.snapshot(device=-1)
+        mig.append(sn.upload_part(r, P, 0, mode=PART_MIGRATE))
+    comms = _local_comms(P)
+    _ok(_ranks(P, lambda r: comms[r].close_filters(mig[r])))
+    res = _ranks(P, lambda r: comms[r].expand_batch_routed(mig[r], [], 5))
+    for r, (ok, v) in enumerate(res):
+        assert not ok and v.code == -1, (r, v)
+    for c in comms:
+        c.close()
+    for p in mig:
+        p.close()
+
+
+def test_expand_routed_one_rank(comm, powerlaw_parts):
+    """Over RCCL with one rank and one shared-rows part (P = 1): the trees equal keto_expand_batch's."""
+    from keto_amd.capi import PART_SHARED
+    g, st, full, parts, roots = powerlaw_parts
+    one, _ = g.snapshot_from_strings(st, device=-1)
+    one = one.upload_part(0, 1, 0, mode=PART_SHARED)
+    assert comm.expand_batch_routed(one, roots, 5, want_nodes=True) == full.expand_batch(roots, 5, want_nodes=True)
+    one.close()
