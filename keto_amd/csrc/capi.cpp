@@ -599,15 +599,26 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
     return guarded([&] {
         if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
         Snapshot& S = *h->s;
-        std::unique_lock<std::shared_mutex> lk(S.rw);
+        // writes one at a time; a transaction is staged (parsed, merged into its rows' current edges,
+        // collision and wildcard effects found -- reads only) under the shared lock, so batches keep
+        // running, and committed to the host tables and the device arena under the exclusive one
+        std::lock_guard<std::mutex> wl(S.apply_mu);
+        std::shared_lock<std::shared_mutex> rl(S.rw);
+        std::unique_lock<std::shared_mutex> xl(S.rw, std::defer_lock);
         const auto t0 = std::chrono::steady_clock::now();
-        apply_writes(S, inserts, n_inserts, deletes, n_deletes);
-        const auto t1 = std::chrono::steady_clock::now();
+        auto t1 = t0;
+        apply_writes(S, inserts, n_inserts, deletes, n_deletes, [&] {
+            t1 = std::chrono::steady_clock::now();
+            rl.unlock();
+            xl.lock();
+        });
+        const auto t2 = std::chrono::steady_clock::now();
         device_apply(S);
-        if (getenv("KETO_APPLY_TRACE"))             // tooling: the exclusive lock's two halves
-            fprintf(stderr, "[apply] host delta %.3f ms, device %.3f ms\n",
+        if (getenv("KETO_APPLY_TRACE"))             // tooling: staged (shared lock), then the exclusive part
+            fprintf(stderr, "[apply] staged %.3f ms, lock wait %.3f ms, host commit + device %.3f ms\n",
                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+                    std::chrono::duration<double, std::milli>(t2 - t1).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
         if (version_out) *version_out = S.version;
         return KETO_OK;
     });

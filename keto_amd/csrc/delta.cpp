@@ -257,7 +257,8 @@ std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {     /
 
 }  // namespace
 
-void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del) {
+void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del,
+                  const std::function<void()>& commit) {
     // a shared-rows part holds the whole graph's host tables: every part applies every transaction
     // and device_apply writes the rows this part holds; a migrating part's stubs carry their owners'
     // filters and handles, which a local write cannot follow
@@ -422,6 +423,7 @@ void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto
     for (uint32_t r : T.order)
         if (r < S.rows.size() && S.row_pp[r] != NO_PAGE) throw Error{KETO_E_REBUILD, "a write touches a poisoned row"};
     // ---- commit
+    if (commit) commit();
     const uint32_t R0 = S.n_rows();
     if (!new_coll.empty()) {
         for (auto& kv : new_coll) S.coll[kv.first] = kv.second;

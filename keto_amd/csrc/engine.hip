@@ -2479,6 +2479,16 @@ struct DeviceState {
     uint32_t* layout_units = nullptr; // handles in arena order (increasing) and their rows, lazily:
     uint32_t* rows_by_unit = nullptr; //   expand output handle -> row id on the device
     uint32_t* unit_row = nullptr;     // handle -> row id, direct (n_units entries; lazily, when <= 8 GiB)
+    uint64_t row_handle_cap = 0;      // entries allocated (a write patches the maps in place while its rows fit)
+    uint64_t unit_row_cap = 0;
+    // the closure rows of the last write (device_apply): the rows with a filter and subject sets
+    // (closure_pass) and every row with a filter (sig_pass), kept while a write changes neither set
+    uint32_t* cl_list = nullptr;
+    uint32_t* cl_all = nullptr;
+    uint32_t* cl_changed = nullptr;
+    uint64_t cl_list_n = 0, cl_all_n = 0, cl_list_cap = 0, cl_all_cap = 0;
+    std::vector<uint8_t> cl_in;       // per row: in cl_list
+    bool cl_valid = false;
     void* ex_buf = nullptr;           // expand workspace (requests, counts, statuses, offsets)
     uint64_t ex_cap = 0;
     keto_tree_node* ex_nodes = nullptr;
@@ -3096,6 +3106,72 @@ uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint
 }
 }  // namespace
 
+// Closure filters after a write (device_apply): rounds of closure_pass over the rows with a filter
+// and subject sets until one changes nothing, then the child signatures of every row with a filter
+// -- as build_closures, on the snapshot's stream, over row lists kept on the device from the last
+// write: they are rebuilt only when this write gave a row a new identity (fresh) or changed whether
+// a row takes part (its first subject set, or its last, or the ordered path)
+void apply_closures(Snapshot& S, DeviceState& D, bool fresh) {
+    const uint32_t R = S.n_rows();
+    auto in_list = [&](uint32_t r) {
+        return S.row_cb[r] && S.present(r) && S.rows[r].n_sets > 0 && !(S.row_flags(r) & ROW_SEQ);
+    };
+    bool valid = D.cl_valid && !fresh && D.cl_in.size() == R;
+    for (uint32_t r : S.dirty) {
+        if (!valid) break;
+        if (r >= R || (uint8_t)in_list(r) != D.cl_in[r]) valid = false;
+    }
+    if (!valid) {
+        std::vector<uint32_t> list, all;
+        closure_rows(S, list, all);
+        D.cl_in.assign(R, 0);
+        for (uint32_t r = 0; r < R; ++r) D.cl_in[r] = S.mapped(r) ? (uint8_t)in_list(r) : 0;
+        auto put = [&](uint32_t*& d, uint64_t& cap, const std::vector<uint32_t>& v) {
+            if (v.size() > cap) {
+                if (d) (void)hipFree(d);
+                d = nullptr;
+                cap = v.size() + v.size() / 8 + 1024;
+                HIP_OK(hipMalloc(&d, cap * sizeof(uint32_t)));
+            }
+            if (!v.empty())
+                HIP_OK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice, D.stream));
+        };
+        put(D.cl_list, D.cl_list_cap, list);
+        put(D.cl_all, D.cl_all_cap, all);
+        D.cl_list_n = list.size();
+        D.cl_all_n = all.size();
+        if (!D.cl_changed) HIP_OK(hipMalloc(&D.cl_changed, sizeof(uint32_t)));
+        HIP_OK(hipStreamSynchronize(D.stream));
+        D.cl_valid = true;
+    }
+    if (!D.cl_all_n) return;
+    bool done = D.cl_list_n == 0;
+    const uint32_t n = (uint32_t)D.cl_list_n, m = (uint32_t)D.cl_all_n;
+    for (int round = 0; round < CLOSURE_MAX_ROUNDS && !done; ++round) {
+        HIP_OK(hipMemsetAsync(D.cl_changed, 0, sizeof(uint32_t), D.stream));
+        hipLaunchKernelGGL(closure_pass, dim3((n + 255) / 256), dim3(256), 0, D.stream, D.arena, D.cl_list, n, D.cl_changed);
+        HIP_OK(hipGetLastError());
+        uint32_t ch = 0;
+        HIP_OK(hipMemcpyAsync(&ch, D.cl_changed, sizeof(uint32_t), hipMemcpyDeviceToHost, D.stream));
+        HIP_OK(hipStreamSynchronize(D.stream));
+        done = ch == 0;
+    }
+    if (!done) {
+        hipLaunchKernelGGL(closure_fill, dim3((m + 255) / 256), dim3(256), 0, D.stream, D.arena, D.cl_all, m);
+        HIP_OK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(sig_pass, dim3((m + 255) / 256), dim3(256), 0, D.stream, D.arena, D.cl_all, m);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(D.stream));
+}
+
+// dst[pairs[2k]] = pairs[2k + 1]: the map entries a write changed
+__global__ void __launch_bounds__(256) scatter_pairs(uint32_t* __restrict__ dst, const uint32_t* __restrict__ pairs,
+                                                     uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) dst[pairs[2 * k]] = pairs[2 * k + 1];
+}
+
 // Patch the device arena after apply_writes (delta.cpp): every changed row is rewritten where it is
 // if its new content fits there, else placed at the arena's tail with a forward at its identity
 // handle (the handle subject sets hold; its closure filter stays in front of it).  New rows, and
@@ -3111,6 +3187,17 @@ bool apply_in_place(Snapshot& S) {
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));
+    const bool trace = getenv("KETO_APPLY_TRACE") != nullptr;          // tooling: phase times
+    auto t_lap = std::chrono::steady_clock::now();
+    std::string laps;
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        const auto t = std::chrono::steady_clock::now();
+        char b[64];
+        snprintf(b, sizeof b, " %s %.3f", what, std::chrono::duration<double, std::milli>(t - t_lap).count());
+        laps += b;
+        t_lap = t;
+    };
     struct Write {
         uint64_t word;                    // first word of the image in the arena
         std::vector<uint32_t> img;
@@ -3235,6 +3322,7 @@ bool apply_in_place(Snapshot& S) {
         }
     }
     for (auto& m : moved) forward(m.second, S.unit_of_row[m.first], false);   // stale top-level handles
+    lap("images");
     // 3. room: grow the arena if the tail outgrew it (handles are word offsets: copied as is)
     const uint64_t need = S.n_units * HDR_WORDS;
     if (need > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
@@ -3253,8 +3341,10 @@ bool apply_in_place(Snapshot& S) {
         HIP_OK(hipMemcpyAsync(D.arena + w.word, w.img.data(), w.img.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                               D.stream));
     HIP_OK(hipStreamSynchronize(D.stream));
+    lap("copies");
     // 4. closure filters of every row with one (from their own ids up)
-    build_closures(S, D.arena);
+    apply_closures(S, D, !fresh.empty());
+    lap("closures");
     // 5. what the kernels and expand output read next: the collision table when a write added
     // classes or gave a classed row a new identity handle
     if (!moved.empty() && !S.coll.empty()) S.coll_dirty = true;
@@ -3281,11 +3371,46 @@ bool apply_in_place(Snapshot& S) {
         S.layout_units.swap(lu);
         S.rows_by_unit.swap(rbu);
     }
-    for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit, &D.unit_row})
-        if (*p) {
-            (void)hipFree(*p);
-            *p = nullptr;
+    // 6. the lazily built maps: the rows with a fresh identity are patched in (row -> handle,
+    // handle -> row) while they fit; past their room, or with no direct handle map, the maps are
+    // rebuilt by the next batch that needs them.  (An old identity keeps its stale entry: only
+    // top-level handles resolved before the write reach it, through its forward.)
+    const bool patch = !fresh.empty() && D.row_handle && S.n_rows() <= D.row_handle_cap && D.unit_row &&
+                       S.n_units <= D.unit_row_cap && fresh.size() <= (1u << 20);
+    if (!fresh.empty() && !patch) {
+        for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit, &D.unit_row})
+            if (*p) {
+                (void)hipFree(*p);
+                *p = nullptr;
+            }
+        D.row_handle_cap = D.unit_row_cap = 0;
+    } else if (patch) {
+        std::vector<uint32_t> pr(4 * fresh.size());         // (row, handle) for row_handle, (handle, row) for unit_row
+        for (size_t k = 0; k < fresh.size(); ++k) {
+            const uint32_t r = fresh[k], u = S.unit_of_row[r];
+            pr[2 * k] = r;
+            pr[2 * k + 1] = u;
+            pr[2 * fresh.size() + 2 * k] = u;
+            pr[2 * fresh.size() + 2 * k + 1] = r;
         }
+        uint32_t* d_pr = nullptr;
+        HIP_OK(hipMalloc(&d_pr, pr.size() * sizeof(uint32_t)));
+        HIP_OK(hipMemcpyAsync(d_pr, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, D.stream));
+        const uint32_t nf = (uint32_t)fresh.size();
+        hipLaunchKernelGGL(scatter_pairs, dim3((nf + 255) / 256), dim3(256), 0, D.stream, D.row_handle, d_pr, nf);
+        hipLaunchKernelGGL(scatter_pairs, dim3((nf + 255) / 256), dim3(256), 0, D.stream, D.unit_row, d_pr + 2 * nf, nf);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipStreamSynchronize(D.stream));
+        (void)hipFree(d_pr);
+        // the device handle lists are used only without the direct map: leave them to a rebuild
+        for (uint32_t** p : {&D.layout_units, &D.rows_by_unit})
+            if (*p) {
+                (void)hipFree(*p);
+                *p = nullptr;
+            }
+    }
+    lap("maps");
+    if (trace) fprintf(stderr, "[apply] device phases (ms):%s\n", laps.c_str());
     S.dirty.clear();
     S.needs_cb.clear();
     return true;
@@ -3329,6 +3454,8 @@ void device_release(Snapshot& S) {
     if (D.arena) (void)hipFree(D.arena);
     if (D.coll) (void)hipFree(D.coll);
     if (D.row_handle) (void)hipFree(D.row_handle);
+    for (uint32_t* p : {D.cl_list, D.cl_all, D.cl_changed})
+        if (p) (void)hipFree(p);
     if (D.layout_units) (void)hipFree(D.layout_units);
     if (D.unit_row) (void)hipFree(D.unit_row);
     if (D.rows_by_unit) (void)hipFree(D.rows_by_unit);
@@ -4030,7 +4157,9 @@ void translate_rows_locked(Snapshot& S, DeviceState& D, const keto_check_ids* d_
                            hipStream_t st, uint32_t* d_bad) {
     uint64_t acc = 0;
     if (!D.row_handle) {
-        D.row_handle = dmalloc<uint32_t>(S.n_rows(), acc);
+        // room for the rows writes add (device_apply patches the map while they fit)
+        D.row_handle_cap = (uint64_t)S.n_rows() + S.n_rows() / 64 + 4096;
+        D.row_handle = dmalloc<uint32_t>(D.row_handle_cap, acc);
         HIP_OK(hipMemcpy(D.row_handle, S.unit_of_row.data(), (uint64_t)S.n_rows() * sizeof(uint32_t),
                          hipMemcpyHostToDevice));
     }
@@ -4800,7 +4929,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         D.ex_nodes_cap = std::max<uint64_t>(total, 1 << 16);
         D.ex_nodes = dmalloc<keto_tree_node>(D.ex_nodes_cap, acc);
     }
-    if (!D.layout_units) {
+    if (!D.layout_units && !D.unit_row) {             // (a write patches the direct map in place)
         const uint64_t m = std::max<uint64_t>(1, S.layout_units.size());
         D.layout_units = dmalloc<uint32_t>(m, acc);
         D.rows_by_unit = dmalloc<uint32_t>(m, acc);
@@ -4811,7 +4940,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         // the direct map (one word per arena unit) when it is small next to the arena; else the
         // handle -> row translation binary-searches the handle list
         if (S.n_units && S.n_units <= (1ull << 32)) {
-            D.unit_row = dmalloc<uint32_t>(S.n_units, acc);
+            D.unit_row_cap = std::min<uint64_t>(1ull << 32, S.n_units + S.n_units / 64 + 4096);
+            D.unit_row = dmalloc<uint32_t>(D.unit_row_cap, acc);
             const uint32_t m32 = (uint32_t)S.layout_units.size();
             if (m32)
                 hipLaunchKernelGGL(scatter_unit_rows, dim3((m32 + 255) / 256), dim3(256), 0, st, D.unit_row,

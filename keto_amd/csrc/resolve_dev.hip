@@ -121,8 +121,9 @@ __host__ __device__ inline uint64_t row_hash_hd(int64_t ns, uint32_t obj, uint32
 struct StrIndex {                  // an open-addressing string table and the bytes behind it
     const StrSlot* slot;
     uint64_t mask;                 // 0 with slot == nullptr: empty
-    const uint8_t* bytes;          // every string of the snapshot back to back (id order)
-    const uint64_t* off;
+    const uint8_t* bytes;          // the table's strings back to back (id order)
+    const uint64_t* off;           // string id - id0 -> offset in bytes
+    uint64_t id0;                  // the table's first string id
 };
 struct RowIndex {
     const RowSlot* slot;
@@ -151,7 +152,7 @@ __device__ int64_t find_str_dev(const StrIndex& T, const uint8_t* s, uint32_t n,
         if (x.n != n8) continue;
         if (!bytes_eq(reinterpret_cast<const uint8_t*>(x.b), s, min(n, INLINE))) continue;
         if (n <= INLINE) return x.id1 - 1;
-        const uint64_t b = T.off[x.id1 - 1], e = T.off[x.id1];
+        const uint64_t b = T.off[x.id1 - 1 - T.id0], e = T.off[x.id1 - T.id0];
         if (e - b == n && bytes_eq(T.bytes + b, s, n)) return x.id1 - 1;
     }
 }
@@ -233,9 +234,10 @@ T* upload(RBuf& b, const T* src, uint64_t n, hipStream_t st) {
 struct RDevState {
     int device = 0;
     uint64_t version = ~0ull;
+    bool base_ready = false;       // the build's string and row indexes and the namespaces (fixed after the build)
     std::mutex mu;                 // one packed batch at a time per snapshot
     hipStream_t stream = nullptr;
-    RBuf str_slots, str_bytes, str_off, add_slots, row_slots, extra_slots, ns_bytes, ns_off, ns_id;
+    RBuf str_slots, str_bytes, str_off, add_slots, add_bytes, add_off, row_slots, extra_slots, ns_bytes, ns_off, ns_id;
     ResolveDev view{};
     RBuf blob, reqs, ids, status, dec;
     ~RDevState() {
@@ -270,13 +272,16 @@ RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
     *st_out = R.stream;
     if (R.version == S.version) return R;
     hipStream_t st = R.stream;
-    S.ensure_index();
-    ResolveDev v{};
-    // the build's strings: the host index as it is, and every string's bytes (long-string checks)
-    v.base.slot = upload(R.str_slots, static_cast<const StrSlot*>(S.str_idx.p), S.str_mask + 1, st);
-    v.base.mask = S.str_mask;
-    {
-        const uint64_t ns = S.strs.size();
+    ResolveDev v = R.view;
+    // the build's strings (strs[0, n_sorted_strs): the host index covers exactly them), its real rows
+    // and the namespaces never change after the build: uploaded once per snapshot.  A write adds
+    // strings and rows to the small second tables, rebuilt per version.
+    if (!R.base_ready) {
+        S.ensure_index();
+        v.base.slot = upload(R.str_slots, static_cast<const StrSlot*>(S.str_idx.p), S.str_mask + 1, st);
+        v.base.mask = S.str_mask;
+        v.base.id0 = 0;
+        const uint64_t ns = S.n_sorted_strs;
         std::vector<uint64_t> off(ns + 1, 0);
         for (uint64_t i = 0; i < ns; ++i) off[i + 1] = off[i] + S.strs[i].size();
         std::vector<uint8_t> bytes(std::max<uint64_t>(1, off[ns]));
@@ -286,10 +291,31 @@ RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
         });
         v.base.bytes = upload(R.str_bytes, bytes.data(), bytes.size(), st);
         v.base.off = upload(R.str_off, off.data(), off.size(), st);
+        v.real.slot = upload(R.row_slots, static_cast<const RowSlot*>(S.row_idx.p), S.row_mask + 1, st);
+        v.real.mask = S.row_mask;
+        const uint32_t nn = (uint32_t)S.ns_names.size();
+        std::vector<uint64_t> noff(nn + 1, 0);
+        std::string nbytes;
+        for (uint32_t c = 0; c < nn; ++c) {
+            nbytes += S.ns_names[c];
+            noff[c + 1] = nbytes.size();
+        }
+        v.ns_bytes = upload(R.ns_bytes, reinterpret_cast<const uint8_t*>(nbytes.data()), nbytes.size(), st);
+        v.ns_off = upload(R.ns_off, noff.data(), noff.size(), st);
+        v.ns_id = upload(R.ns_id, S.ns_ids.data(), S.ns_ids.size(), st);
+        v.n_ns = nn;
         HIP_OK(hipStreamSynchronize(st));
+        R.base_ready = true;
     }
-    v.added = StrIndex{nullptr, 0, v.base.bytes, v.base.off};
+    // strings writes added: ids n_sorted_strs and up, their own table and bytes
+    v.added = StrIndex{nullptr, 0, nullptr, nullptr, S.n_sorted_strs};
     if (!S.added_str.empty()) {
+        const uint64_t id0 = S.n_sorted_strs, na = S.strs.size() - id0;
+        std::vector<uint64_t> off(na + 1, 0);
+        for (uint64_t i = 0; i < na; ++i) off[i + 1] = off[i] + S.strs[id0 + i].size();
+        std::vector<uint8_t> bytes(std::max<uint64_t>(1, off[na]));
+        for (uint64_t i = 0; i < na; ++i)
+            if (!S.strs[id0 + i].empty()) std::memcpy(bytes.data() + off[i], S.strs[id0 + i].data(), S.strs[id0 + i].size());
         uint64_t mask = 0;
         auto t = build_table<StrSlot>(S.added_str.size(), mask, [&](std::vector<StrSlot>& tab) {
             const uint64_t m = tab.size() - 1;
@@ -306,12 +332,12 @@ RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
         });
         v.added.slot = upload(R.add_slots, t.data(), t.size(), st);
         v.added.mask = mask;
+        v.added.bytes = upload(R.add_bytes, bytes.data(), bytes.size(), st);
+        v.added.off = upload(R.add_off, off.data(), off.size(), st);
         HIP_OK(hipStreamSynchronize(st));
     }
-    // the build's real rows: the host index; every other row a query can name (empty rows subject
-    // sets point at, rows writes added; not the wildcard rows): a second table
-    v.real.slot = upload(R.row_slots, static_cast<const RowSlot*>(S.row_idx.p), S.row_mask + 1, st);
-    v.real.mask = S.row_mask;
+    // every other row a query can name (empty rows subject sets point at, rows writes added; not the
+    // wildcard rows): a second table
     v.extra = RowIndex{nullptr, 0};
     {
         std::vector<std::pair<RowKey, uint32_t>> rows;
@@ -336,20 +362,6 @@ RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
             v.extra.mask = mask;
             HIP_OK(hipStreamSynchronize(st));
         }
-    }
-    {
-        const uint32_t nn = (uint32_t)S.ns_names.size();
-        std::vector<uint64_t> off(nn + 1, 0);
-        std::string bytes;
-        for (uint32_t c = 0; c < nn; ++c) {
-            bytes += S.ns_names[c];
-            off[c + 1] = bytes.size();
-        }
-        v.ns_bytes = upload(R.ns_bytes, reinterpret_cast<const uint8_t*>(bytes.data()), bytes.size(), st);
-        v.ns_off = upload(R.ns_off, off.data(), off.size(), st);
-        v.ns_id = upload(R.ns_id, S.ns_ids.data(), S.ns_ids.size(), st);
-        v.n_ns = nn;
-        HIP_OK(hipStreamSynchronize(st));
     }
     R.view = v;
     R.version = S.version;

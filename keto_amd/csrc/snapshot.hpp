@@ -15,6 +15,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -260,6 +261,7 @@ struct Snapshot {
 
     // ---- lifecycle (delta.cpp): writes applied since the build
     std::shared_mutex rw;                      // calls read the host tables shared; keto_snapshot_apply exclusive
+    std::mutex apply_mu;                       // one keto_snapshot_apply at a time (it stages under rw shared)
     uint64_t version = 0;                      // bumped by every keto_snapshot_apply
     uint32_t n_sorted_strs = 0;                // strs[0, n) are in byte order (id = rank); later ones were added
     std::unordered_map<std::string, uint32_t> added_str;
@@ -418,7 +420,11 @@ uint64_t arena_fit(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, ui
 // snapshot lifecycle (delta.cpp): apply an insert / delete transaction to the host tables
 // (TransactRelationTuples, internal/persistence/sql/relationtuples.go:289-297); throws KETO_E_REBUILD
 // for writes outside the delta path; device_apply then patches the device arena
-void apply_writes(Snapshot& s, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del);
+// commit: called once the transaction is staged (every check passed, nothing of the snapshot changed
+// yet) and before it changes anything; keto_snapshot_apply stages under the shared lock and takes the
+// exclusive one there, so batches run while a write is staged
+void apply_writes(Snapshot& s, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del,
+                  const std::function<void()>& commit = {});
 void device_apply(Snapshot& s);
 
 // device engine (engine.hip)

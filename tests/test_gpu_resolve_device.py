@@ -82,8 +82,9 @@ def test_long_strings_sharing_a_prefix():
 
 @pytest.mark.parametrize("seed", range(6))
 def test_packed_after_writes(seed):
-    """Writes add strings and rows the build's indexes do not hold (added_str, row_of): the device
-    indexes are rebuilt for the new version and still resolve exactly like the host."""
+    """Writes add strings and rows the build's indexes do not hold (added_str, row_of): the build's
+    device indexes stay, the tables of added strings and rows are rebuilt for each new version, and
+    every version resolves exactly like the host."""
     import keto_amd
     from tests.test_gpu_lifecycle import _random_write, _row
     from tests.randgraph import random_graph
@@ -95,7 +96,10 @@ def test_packed_after_writes(seed):
     store = SQLStore(ns, tuples, page_size=ps)
     snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), page_size=ps, device=0)
     rng = random.Random(seed)
-    for step in range(4):
+    # long names (past a slot's 11 inline bytes): an added string is verified against its own bytes
+    objs = objs + ["an_object_name_longer_than_a_slot"]
+    users = users + ["a_subject_id_longer_than_a_slot_0", "a_subject_id_longer_than_a_slot_1"]
+    for step in range(8):
         ins = [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(2, 10))]
         snap.apply([_row(ns, t) for t in ins], [])
         for t in ins:

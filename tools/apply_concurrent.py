@@ -2,8 +2,9 @@
 requests back to back while another applies TransactRelationTuples of K tuples (keto_snapshot_apply)
 every `--gap-ms`, on config #2's snapshot built from its 10M string tuples.  Reports the check
 batches' latency with and without the writer, the writes' latency under read load, and that the
-untouched requests keep their decisions throughout.  keto_snapshot_apply holds the snapshot's lock
-exclusively, so a write waits for the running batch and the next batch waits for the write.
+untouched requests keep their decisions throughout.  keto_snapshot_apply stages a transaction under
+the snapshot's shared lock (batches keep running) and commits it under the exclusive one, so a write
+waits for the running batch only to commit, and the next batch waits only for the commit.
 
   python tools/apply_concurrent.py [--k 100] [--gap-ms 20] [--seconds 5]
 """
@@ -30,6 +31,8 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--gap-ms", type=float, default=20.0)
     ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--packed", action="store_true",
+                    help="reads through keto_check_batch_packed (GPU resolution, the Go batcher's call)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -39,7 +42,15 @@ def main():
     snap, t_build = g.snapshot_from_strings(st, device=0)
     q = g.queries(1_000_000, seed=2, depth=5, threads=a.threads)
     reqs = g.string_requests(st, q, threads=a.threads)
-    before, _ = snap.check_batch_reqs(reqs, len(q), 5)
+    if a.packed:
+        blob, packed, used = g.pack_requests(reqs, len(q), threads=a.threads)
+
+        def batch():
+            return snap.check_batch_packed(blob.array[:used], packed.array, 5, n=len(q))[0]
+    else:
+        def batch():
+            return snap.check_batch_reqs(reqs, len(q), 5)[0]
+    before = batch().copy()
     hx = lambda v: f"{int(v):08x}"
     files_view = np.flatnonzero((g.row_ns == 1) & (g.row_rel == 2))
     rng = np.random.default_rng(7)
@@ -48,7 +59,7 @@ def main():
         t_end = time.perf_counter() + seconds
         while time.perf_counter() < t_end:
             t0 = time.perf_counter()
-            out, _ = snap.check_batch_reqs(reqs, len(q), 5)
+            out = batch()
             lat.append(time.perf_counter() - t0)
             bad.append(int((out != before).sum()))
 
@@ -75,6 +86,7 @@ def main():
     stop.set()
     w.join()
     out = {"graph": "drive10m (config #2, built from string tuples)", "tuples": int(g.n_edges),
+           "reads": "keto_check_batch_packed (GPU resolution)" if a.packed else "keto_check_batch (host resolution)",
            "requests_per_batch": len(q), "write_tuples": a.k, "write_gap_ms": a.gap_ms,
            "batch_ms_quiet": {"p50": pct(quiet, 50), "p99": pct(quiet, 99), "n": len(quiet)},
            "batch_ms_with_writes": {"p50": pct(loaded, 50), "p99": pct(loaded, 99), "n": len(loaded)},
