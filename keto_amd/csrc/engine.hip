@@ -4307,14 +4307,15 @@ bool check_streamed(Snapshot& S, DeviceState& D, const keto_check_pair* reqs, ui
     ss.xlate = D.st_x;
     check_core(S, D, nullptr, n, gmd, D.st_dec, D.stream, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, false, nullptr,
                nullptr, 0, nullptr, &ss);
-    HIP_OK(hipStreamSynchronize(D.copy_in));
+    // the decisions and the two flags come back behind the check in one round trip; a stalled or
+    // misrouted batch discards what was copied
     uint32_t flags[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(flags, W.counters + 4, sizeof(flags), hipMemcpyDeviceToHost, D.stream));
-    HIP_OK(hipStreamSynchronize(D.stream));
-    if (flags[1]) return false;
-    if (flags[0]) throw Error{KETO_E_INVALID, std::to_string(flags[0]) + " requests name root rows another part owns"};
     HIP_OK(hipMemcpyAsync(allowed, D.st_dec, n, hipMemcpyDeviceToHost, D.stream));
     HIP_OK(hipStreamSynchronize(D.stream));
+    HIP_OK(hipStreamSynchronize(D.copy_in));
+    if (flags[1]) return false;
+    if (flags[0]) throw Error{KETO_E_INVALID, std::to_string(flags[0]) + " requests name root rows another part owns"};
     D.last.chunks = (uint32_t)chunks;
     return true;
 }
