@@ -3713,14 +3713,17 @@ struct DevFree {
 namespace {
 using CheckKernelFn = void (*)(DevSnap, DevOverlay, const keto_check_ids*, uint32_t, int, uint8_t*, TierArgs,
                                unsigned long long*);
-// tier-0 variants for max-depth <= 5 (4 saved frames): {save windows, LDS visit ids}; then the
-// max-depth <= 9 kernel (8 frames).  KETO_T0 picks a variant (tuning); 0 is the default.
-constexpr int T0_VARIANTS = 4;
+// tier-0 variants for max-depth <= 5 (4 saved frames): {LDS visit ids, register visit ids}; then the
+// max-depth <= 9 kernel (8 frames).  KETO_T0 picks a variant (tuning).  The default is 3 (8 + 8
+// visit ids): on one box, 2.53-2.55 ms per 16.7M batch on the 1B graph against 2.97-3.01 ms for
+// variant 0 (4 + 16), the round-3 default, with identical decisions (profiles/r04ae_tier0_variants.log;
+// it runs 6 waves per SIMD against 8: its LDS columns hold 8 ids).  Variant 7 (12 + 8) ties.
+constexpr int T0_VARIANTS = 8;
 constexpr uint32_t KETO_HEAD_WORDS = 8 * 16 * 32;
 int t0_variant() {
     const char* e = getenv("KETO_T0");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v < T0_VARIANTS ? v : 0;
+    const int v = e ? atoi(e) : 3;
+    return v >= 0 && v < T0_VARIANTS ? v : 3;
 }
 // request runs handed out per grab by the tier-0 wave kernel (TierArgs::dyn) for a batch of n
 // requests over `lanes` lanes: runs of 4 after a static first quarter, dealt by 4 heads per XCD,
@@ -3759,6 +3762,10 @@ const char* t0_kernel_name(int var) {
         case 1: return "keto::check_wave_kernel<4, false, 4, 8, false, false>";
         case 2: return "keto::check_wave_kernel<4, false, 12, 4, false, false>";
         case 3: return "keto::check_wave_kernel<4, false, 8, 8, false, false>";
+        case 4: return "keto::check_wave_kernel<4, false, 8, 4, false, false>";
+        case 5: return "keto::check_wave_kernel<4, false, 16, 4, false, false>";
+        case 6: return "keto::check_wave_kernel<4, false, 16, 8, false, false>";
+        case 7: return "keto::check_wave_kernel<4, false, 12, 8, false, false>";
         default: return "keto::check_wave_kernel<8, false, 8, 8, false, false>";
     }
 }
@@ -3769,10 +3776,21 @@ CheckKernelFn t0_kernel(int var, bool count) {
         case 1: return count ? check_wave_kernel<4, false, 4, 8, true> : check_wave_kernel<4, false, 4, 8, false>;
         case 2: return count ? check_wave_kernel<4, false, 12, 4, true> : check_wave_kernel<4, false, 12, 4, false>;
         case 3: return count ? check_wave_kernel<4, false, 8, 8, true> : check_wave_kernel<4, false, 8, 8, false>;
+        case 4: return count ? check_wave_kernel<4, false, 8, 4, true> : check_wave_kernel<4, false, 8, 4, false>;
+        case 5: return count ? check_wave_kernel<4, false, 16, 4, true> : check_wave_kernel<4, false, 16, 4, false>;
+        case 6: return count ? check_wave_kernel<4, false, 16, 8, true> : check_wave_kernel<4, false, 16, 8, false>;
+        case 7: return count ? check_wave_kernel<4, false, 12, 8, true> : check_wave_kernel<4, false, 12, 8, false>;
         default: return count ? check_wave_kernel<8, false, 8, 8, true> : check_wave_kernel<8, false, 8, 8, false>;
     }
 }
-CheckKernelFn t0_stream_kernel() { return check_wave_kernel<4, false, 4, 16, false, true>; }
+// the streamed launch: the default variant's geometry (KETO_T0_STREAM=0: variant 0's)
+bool t0_stream_v0() {
+    const char* e = getenv("KETO_T0_STREAM");
+    return e && atoi(e) == 0;
+}
+CheckKernelFn t0_stream_kernel() {
+    return t0_stream_v0() ? check_wave_kernel<4, false, 4, 16, false, true> : check_wave_kernel<4, false, 8, 8, false, true>;
+}
 }  // namespace
 
 // deep batches (global max-depth 10..64) take deep_wave_kernel as tier 0 only with KETO_DEEP_WAVE=1:
@@ -3877,7 +3895,7 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     // (deep_wave_kernel keeps one segment bit: arenas of up to 2 segments)
     const bool dw = kind == 2 && deep_wave(gmd) && (uint64_t)D.n_units <= (1ull << 31);
     if (ss && kind != 0) throw Error{KETO_E_INVALID, "streamed batches need max-depth <= 5"};
-    const int var = ss ? T0_VARIANTS + 3
+    const int var = ss ? T0_VARIANTS + 3 + (t0_stream_v0() ? 1 : 0)
                        : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
