@@ -3762,10 +3762,10 @@ const char* t0_kernel_name(int var) {
         case 1: return "keto::check_wave_kernel<4, false, 4, 8, false, false>";
         case 2: return "keto::check_wave_kernel<4, false, 12, 4, false, false>";
         case 3: return "keto::check_wave_kernel<4, false, 8, 8, false, false>";
-        case 4: return "keto::check_wave_kernel<4, false, 8, 4, false, false>";
-        case 5: return "keto::check_wave_kernel<4, false, 16, 4, false, false>";
-        case 6: return "keto::check_wave_kernel<4, false, 16, 8, false, false>";
-        case 7: return "keto::check_wave_kernel<4, false, 12, 8, false, false>";
+        case 4: return "keto::check_wave_kernel<4, false, 8, 6, false, false>";
+        case 5: return "keto::check_wave_kernel<4, false, 12, 6, false, false>";
+        case 6: return "keto::check_wave_kernel<4, false, 6, 8, false, false>";
+        case 7: return "keto::check_wave_kernel<4, true, 8, 8, false, false>";
         default: return "keto::check_wave_kernel<8, false, 8, 8, false, false>";
     }
 }
@@ -3776,10 +3776,10 @@ CheckKernelFn t0_kernel(int var, bool count) {
         case 1: return count ? check_wave_kernel<4, false, 4, 8, true> : check_wave_kernel<4, false, 4, 8, false>;
         case 2: return count ? check_wave_kernel<4, false, 12, 4, true> : check_wave_kernel<4, false, 12, 4, false>;
         case 3: return count ? check_wave_kernel<4, false, 8, 8, true> : check_wave_kernel<4, false, 8, 8, false>;
-        case 4: return count ? check_wave_kernel<4, false, 8, 4, true> : check_wave_kernel<4, false, 8, 4, false>;
-        case 5: return count ? check_wave_kernel<4, false, 16, 4, true> : check_wave_kernel<4, false, 16, 4, false>;
-        case 6: return count ? check_wave_kernel<4, false, 16, 8, true> : check_wave_kernel<4, false, 16, 8, false>;
-        case 7: return count ? check_wave_kernel<4, false, 12, 8, true> : check_wave_kernel<4, false, 12, 8, false>;
+        case 4: return count ? check_wave_kernel<4, false, 8, 6, true> : check_wave_kernel<4, false, 8, 6, false>;
+        case 5: return count ? check_wave_kernel<4, false, 12, 6, true> : check_wave_kernel<4, false, 12, 6, false>;
+        case 6: return count ? check_wave_kernel<4, false, 6, 8, true> : check_wave_kernel<4, false, 6, 8, false>;
+        case 7: return count ? check_wave_kernel<4, true, 8, 8, true> : check_wave_kernel<4, true, 8, 8, false>;
         default: return count ? check_wave_kernel<8, false, 8, 8, true> : check_wave_kernel<8, false, 8, 8, false>;
     }
 }
