@@ -999,8 +999,12 @@ struct LaneVisited {
     }
 };
 
+// waves per SIMD the wave kernels are compiled for (__launch_bounds__' second argument).  6, not 8:
+// at 8 the compiler squeezed tier 0 into 64 VGPRs with spills and extra moves; at 6 it may use up
+// to 80, and the 16.7M batch on the 1B graph runs 2.48 ms against 2.55 ms (8 + 8 visit ids) and
+// 2.99 ms (4 + 16) on one box (profiles/r04aj_wave_waves.log)
 #ifndef KETO_WAVE_WAVES
-#define KETO_WAVE_WAVES 8
+#define KETO_WAVE_WAVES 6
 #endif
 
 // streamed batches: wait (bounded) until chunk word `p` says the chunk has landed.  Relaxed is
