@@ -159,7 +159,7 @@ struct Reader {
         io_all(fd, reinterpret_cast<char*>(&h), sizeof h, off, false, "a section header");
         off += sizeof h;
         if (h.id != id) throw Error{KETO_E_INVALID, "snapshot file: section " + std::to_string(id) + " expected, found " + std::to_string(h.id)};
-        if (h.bytes % sizeof(T) || off + h.bytes > size)
+        if (h.bytes > size || h.bytes % sizeof(T) || off + h.bytes > size)
             throw Error{KETO_E_INVALID, "snapshot file: section " + std::to_string(id) + " has a bad size"};
         out.resize(h.bytes / sizeof(T));
         if (h.bytes) io_par(fd, reinterpret_cast<char*>(out.data()), h.bytes, off, false, threads, "section " + std::to_string(id));

@@ -145,6 +145,13 @@ def test_damaged_files_refused(tmp_path):
             assert x.code == -1
         else:                                            # a section's padding bytes carry no checksum
             s.close()
+    import struct
+    huge = bytearray(data)
+    struct.pack_into("<Q", huge, 64 + 8, (1 << 64) - 8)  # a section's byte count near 2^64
+    bad.write_bytes(bytes(huge))
+    with pytest.raises(keto_amd.KetoError) as e:
+        keto_amd.Snapshot.load(bad, device=-1)
+    assert e.value.code == -1
     flip = bytearray(data)
     flip[0] ^= 1                                         # magic
     bad.write_bytes(bytes(flip))
