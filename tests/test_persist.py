@@ -253,3 +253,54 @@ def test_power_law_decisions_survive_round_trip(tmp_path):
     for s in (snap, got):
         s.close()
     g.close()
+
+
+def test_writes_staged_beside_readers_host():
+    """keto_snapshot_apply stages a transaction under the shared lock and commits under the exclusive
+    one (capi.cpp): readers resolving requests at the same time keep working and see versions only
+    move forward, and every write lands.  Host-only snapshot, one writer thread, two reader threads."""
+    import threading
+    import keto_amd
+    ns = [(1, "doc"), (2, "grp")]
+    rows = [(1, f"d{i}", "view", None, 2, f"g{i % 7}", "member") for i in range(200)]
+    rows += [(2, f"g{j}", "member", f"u{j}") for j in range(7)]
+    snap = keto_amd.Snapshot.build(ns, rows, device=-1)
+    reqs = [("doc", f"d{i}", "view", ("id", f"u{i % 7}"), 0) for i in range(200)]
+    reqs += [("doc", "dnew", "view", ("id", "unew"), 0), ("grp", "gnew", "member", ("id", "unew"), 0)]
+    stop = threading.Event()
+    errors = []
+
+    def writer():
+        try:
+            for k in range(150):
+                t = [(1, "dnew", "view", "unew"), (2, "gnew", "member", "unew")]
+                snap.apply(inserts=t)
+                snap.apply(deletes=t)
+        except Exception as e:            # noqa: BLE001 -- reported below
+            errors.append(e)
+        finally:
+            stop.set()
+
+    def reader():
+        try:
+            seen = 0
+            while not stop.is_set():
+                v0 = snap.version()
+                out, st = snap.resolve_checks(reqs)
+                assert (st == 0).all()
+                assert v0 >= seen                     # versions only move forward
+                seen = v0
+                # the build's rows keep their handles through every write
+                assert (out[:200]["row"] != 0xFFFFFFFF).all()
+        except Exception as e:            # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=writer)] + [threading.Thread(target=reader) for _ in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
+    assert snap.version() == 300
+    snap.close()
