@@ -1025,10 +1025,10 @@ __device__ inline bool chunk_wait(const uint32_t* p, uint64_t ticks) {
 #endif
 constexpr uint32_t P_XLT = 5;          // streamed: the request's row id (and set target) -> handles
 
-template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM>
-__device__ __forceinline__ void
-    check_wave_body(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
-                    uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM = false>
+__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
+    check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                      uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
     const uint32_t tid = threadIdx.x;
     const uint32_t slot = blockIdx.x * blockDim.x + tid;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1455,21 +1455,6 @@ __device__ __forceinline__ void
         for (int i = 0; i < 16; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
         for (int i = 0; i < 8; ++i) atomicAdd(work + 16 + i, (unsigned long long)w.s[i]);
     }
-}
-template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM = false>
-__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
-    check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
-                      uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
-    check_wave_body<F, WIN, LV, RV, COUNT, STREAM>(s, ov, q, n, gmd, allowed, ta, work);
-}
-// the same walk compiled for 8 waves per SIMD (64 VGPRs), for batches of fewer than 16 requests per
-// lane: there the lanes a launch holds matter more than the instructions per iteration (config #2,
-// 1M requests: 0.149 ms against 0.160-0.164 ms at 6 waves, profiles/r04al_small_batch_waves.log)
-template <int F, int LV, int RV>
-__global__ void __launch_bounds__(256, 8)
-    check_wave_kernel_w8(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
-                         uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
-    check_wave_body<F, false, LV, RV, false, false>(s, ov, q, n, gmd, allowed, ta, work);
 }
 
 // ------------------------------------------------------------------ check, deep requests
@@ -3914,20 +3899,8 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     // (deep_wave_kernel keeps one segment bit: arenas of up to 2 segments)
     const bool dw = kind == 2 && deep_wave(gmd) && (uint64_t)D.n_units <= (1ull << 31);
     if (ss && kind != 0) throw Error{KETO_E_INVALID, "streamed batches need max-depth <= 5"};
-    int var = ss ? T0_VARIANTS + 3 + (t0_stream_v0() ? 1 : 0)
-                 : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
-    // batches of fewer than 16 requests per lane of the 8-wave build take check_wave_kernel_w8
-    // (variant 0's geometry at 8 waves per SIMD); KETO_T0 (tuning) or KETO_T0_W8=0 keep the variant
-    constexpr int VAR_W8 = T0_VARIANTS + 5;
-    if (kind == 0 && !ss && !work_out && !getenv("KETO_T0") && !(getenv("KETO_T0_W8") && atoi(getenv("KETO_T0_W8")) == 0)) {
-        if (!D.v1_lanes[VAR_W8]) {
-            int per_cu = 0, cus = 0;
-            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_wave_kernel_w8<4, 4, 16>, 256, 0));
-            HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
-            D.v1_lanes[VAR_W8] = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
-        }
-        if ((uint64_t)n < 16ull * D.v1_lanes[VAR_W8]) var = VAR_W8;
-    }
+    const int var = ss ? T0_VARIANTS + 3 + (t0_stream_v0() ? 1 : 0)
+                       : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
@@ -4079,8 +4052,7 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
                           HIP_OK(hipMemsetAsync(W.heads, 0, KETO_HEAD_WORDS * sizeof(uint32_t), st));
                           a.heads = W.heads;
                       }
-                      if (var == VAR_W8) go(check_wave_kernel_w8<4, 4, 16>);
-                      else go(t0_kernel(var, dwork != nullptr));
+                      go(t0_kernel(var, dwork != nullptr));
                   }
                   else if (level == 0 && dw) {
                       // frames: the tier's GlobalStack area as [frame][lane] 8-B words (DF per lane)
