@@ -2484,6 +2484,7 @@ struct DeviceState {
     uint32_t* rows_by_unit = nullptr; //   expand output handle -> row id on the device
     uint32_t* unit_row = nullptr;     // handle -> row id, direct (n_units entries; lazily, when <= 8 GiB)
     uint64_t row_handle_cap = 0;      // entries allocated (a write patches the maps in place while its rows fit)
+    uint64_t row_handle_rows = 0;     // entries written (rows below it hold their handle or NO_UNIT)
     uint64_t unit_row_cap = 0;
     // the closure rows of the last write (device_apply): the rows with a filter and subject sets
     // (closure_pass) and every row with a filter (sig_pass), kept while a write changes neither set
@@ -3379,30 +3380,41 @@ bool apply_in_place(Snapshot& S) {
     // handle -> row) while they fit; past their room, or with no direct handle map, the maps are
     // rebuilt by the next batch that needs them.  (An old identity keeps its stale entry: only
     // top-level handles resolved before the write reach it, through its forward.)
-    const bool patch = !fresh.empty() && D.row_handle && S.n_rows() <= D.row_handle_cap && D.unit_row &&
-                       S.n_units <= D.unit_row_cap && fresh.size() <= (1u << 20);
-    if (!fresh.empty() && !patch) {
+    // rows the write added that got no handle here (another part's root rows) still need their
+    // NO_UNIT entry in the row -> handle map: the map's slack past its rows is uninitialized
+    const bool grew = D.row_handle && S.n_rows() > D.row_handle_rows;
+    const bool patch = (!fresh.empty() || grew) && D.row_handle && S.n_rows() <= D.row_handle_cap && D.unit_row &&
+                       S.n_units <= D.unit_row_cap && fresh.size() + (S.n_rows() - D.row_handle_rows) <= (1u << 20);
+    if ((!fresh.empty() || grew) && !patch) {
         for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit, &D.unit_row})
             if (*p) {
                 (void)hipFree(*p);
                 *p = nullptr;
             }
-        D.row_handle_cap = D.unit_row_cap = 0;
+        D.row_handle_cap = D.unit_row_cap = D.row_handle_rows = 0;
     } else if (patch) {
-        std::vector<uint32_t> pr(4 * fresh.size());         // (row, handle) for row_handle, (handle, row) for unit_row
-        for (size_t k = 0; k < fresh.size(); ++k) {
-            const uint32_t r = fresh[k], u = S.unit_of_row[r];
-            pr[2 * k] = r;
-            pr[2 * k + 1] = u;
-            pr[2 * fresh.size() + 2 * k] = u;
-            pr[2 * fresh.size() + 2 * k + 1] = r;
+        // (row, handle) for row_handle: the fresh rows and every row the write added; (handle, row)
+        // for unit_row: the fresh rows
+        std::vector<uint32_t> rh, hr;
+        for (uint32_t r : fresh) {
+            rh.push_back(r);
+            rh.push_back(S.unit_of_row[r]);
+            hr.push_back(S.unit_of_row[r]);
+            hr.push_back(r);
         }
+        for (uint64_t r = D.row_handle_rows; r < S.n_rows(); ++r) {
+            rh.push_back((uint32_t)r);
+            rh.push_back(S.unit_of_row[r]);
+        }
+        D.row_handle_rows = S.n_rows();
+        std::vector<uint32_t> pr(rh);
+        pr.insert(pr.end(), hr.begin(), hr.end());
         uint32_t* d_pr = nullptr;
-        HIP_OK(hipMalloc(&d_pr, pr.size() * sizeof(uint32_t)));
+        HIP_OK(hipMalloc(&d_pr, std::max<size_t>(1, pr.size()) * sizeof(uint32_t)));
         HIP_OK(hipMemcpyAsync(d_pr, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, D.stream));
-        const uint32_t nf = (uint32_t)fresh.size();
-        hipLaunchKernelGGL(scatter_pairs, dim3((nf + 255) / 256), dim3(256), 0, D.stream, D.row_handle, d_pr, nf);
-        hipLaunchKernelGGL(scatter_pairs, dim3((nf + 255) / 256), dim3(256), 0, D.stream, D.unit_row, d_pr + 2 * nf, nf);
+        const uint32_t n1 = (uint32_t)(rh.size() / 2), n2 = (uint32_t)(hr.size() / 2);
+        if (n1) hipLaunchKernelGGL(scatter_pairs, dim3((n1 + 255) / 256), dim3(256), 0, D.stream, D.row_handle, d_pr, n1);
+        if (n2) hipLaunchKernelGGL(scatter_pairs, dim3((n2 + 255) / 256), dim3(256), 0, D.stream, D.unit_row, d_pr + rh.size(), n2);
         HIP_OK(hipGetLastError());
         HIP_OK(hipStreamSynchronize(D.stream));
         (void)hipFree(d_pr);
@@ -4181,6 +4193,7 @@ void translate_rows_locked(Snapshot& S, DeviceState& D, const keto_check_ids* d_
     if (!D.row_handle) {
         // room for the rows writes add (device_apply patches the map while they fit)
         D.row_handle_cap = (uint64_t)S.n_rows() + S.n_rows() / 64 + 4096;
+        D.row_handle_rows = S.n_rows();
         D.row_handle = dmalloc<uint32_t>(D.row_handle_cap, acc);
         HIP_OK(hipMemcpy(D.row_handle, S.unit_of_row.data(), (uint64_t)S.n_rows() * sizeof(uint32_t),
                          hipMemcpyHostToDevice));
