@@ -308,6 +308,11 @@ int keto_mig_begin(keto_snapshot* s, const keto_check_ids* d_reqs, uint32_t n, i
                    uint8_t* d_allowed_out, void* stream, keto_mig_out* out);
 int keto_mig_round(keto_snapshot* s, const void* d_records, const uint32_t* d_offsets, const uint32_t* in_records,
                    const uint64_t* in_units, void* stream, keto_mig_out* out);
+/* Free and total device memory of HIP device `device` (hipMemGetInfo): the Go server sizes its
+ * placement with it -- replicas while the replicated arena (keto_snapshot_part_stats_mode with
+ * n_parts = 1) and the engine's workspaces fit every device, else shared-rows parts over the devices
+ * (the reference serves any table size from one process, internal/driver/daemon.go:62-69). */
+int keto_device_memory(int32_t device, uint64_t* free_out, uint64_t* total_out);
 /* Device-to-device copy on `stream`, returning when it is done: for callers whose exchange layer
  * needs the records in buffers of its own (e.g. torch.distributed tensors). */
 int keto_device_copy(void* dst, const void* src, uint64_t bytes, void* stream);

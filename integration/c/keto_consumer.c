@@ -18,12 +18,22 @@
  * applies every write transaction to each replica, and rebuilds them all when one answers
  * KETO_E_REBUILD.
  *
+ * A graph partitioned over the server's GPUs ("Q" line, registry_gpu.go when the replicated arena does
+ * not fit a device): the table is built once host-only, cloned host-only per part, and each clone is
+ * uploaded as one shared-rows part (keto_snapshot_upload_part_mode, KETO_PART_SHARED) on its device;
+ * one keto_comm_init_local rank per part, each driven by its own thread.  A check batch is split over
+ * the ranks and every rank calls keto_check_batch_routed with its slice (an empty slice too); an
+ * expand batch the same way through keto_expand_batch_routed; every write transaction is applied to
+ * every part.  A restart in this mode builds a host-only snapshot from the table, saves it, loads the
+ * file host-only and partitions it again (the Go server's persisted-file path).
+ *
  * A restart ("S" line): the server saves the first replica (keto_snapshot_save, tagged with its
  * version), releases every replica, loads the file back onto the first device (keto_snapshot_load)
  * and clones it to the others, as registry_gpu.go's loadFile does when the table has not changed.
  *
  * Input (tab-separated lines; empty fields allowed), executed in order:
  *   P <page_size>        V <device>        R <device> <device> ...   (replicas; default: V's device)
+ *   Q <device> <device> ...   (instead of replicas: one shared-rows part per listed device)
  *   N <ns id> <name>
  *   T <ns id> <object> <relation> I <subject id>                          (a row of the initial table)
  *   T <ns id> <object> <relation> S <set ns id> <set object> <set relation>
@@ -38,6 +48,8 @@
  * "expand <i> <status> <json|null|error> <proto hex|->", "apply <rc> <version> <rebuilt>", "stats ...",
  * "restart <version> <tag>", "nodevice <rc>", "done".
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -271,6 +283,133 @@ static void build_replicas(const keto_namespace* ns, size_t n_ns, const table_t*
     }
 }
 
+/* ---- a graph partitioned over the devices: one shared-rows part and one local rank per device */
+typedef struct {
+    int n;
+    int devices[MAX_REPLICAS];
+    keto_snapshot* parts[MAX_REPLICAS];
+    keto_comm* comms[MAX_REPLICAS];
+    uint8_t id[KETO_COMM_ID_BYTES];
+} partition_t;
+
+/* one rank's share of a collective call, run on its own thread */
+typedef struct {
+    partition_t* pt;
+    int rank;
+    int op;                                   /* 0 init, 1 check, 2 expand */
+    const keto_check_req* q;
+    const keto_expand_req* e;
+    uint32_t n;
+    int32_t gmd;
+    uint8_t* allowed;
+    uint8_t* status;
+    keto_tree_arena* ar;
+    int rc;
+} rank_call_t;
+
+static void* rank_main(void* arg) {
+    rank_call_t* c = (rank_call_t*)arg;
+    partition_t* pt = c->pt;
+    if (c->op == 0)
+        c->rc = keto_comm_init_local(pt->id, pt->n, c->rank, pt->devices[c->rank], &pt->comms[c->rank]);
+    else if (c->op == 1)
+        c->rc = keto_check_batch_routed(pt->comms[c->rank], pt->parts[c->rank], c->q, c->n, c->gmd, c->allowed, c->status);
+    else
+        c->rc = keto_expand_batch_routed(pt->comms[c->rank], pt->parts[c->rank], c->e, c->n, c->gmd, &c->ar);
+    return NULL;
+}
+
+/* every rank's call at once (collective); calls[k] are filled by the caller; returns the first rc */
+static int ranks_run(partition_t* pt, rank_call_t* calls) {
+    pthread_t th[MAX_REPLICAS];
+    for (int k = 0; k < pt->n; ++k) {
+        calls[k].pt = pt;
+        calls[k].rank = k;
+        if (pthread_create(&th[k], NULL, rank_main, &calls[k]) != 0) exit(3);
+    }
+    int rc = KETO_OK;
+    for (int k = 0; k < pt->n; ++k) {
+        pthread_join(th[k], NULL);
+        if (rc == KETO_OK) rc = calls[k].rc;
+    }
+    for (int k = 1; k < pt->n; ++k)
+        if (calls[k].rc != calls[0].rc) return 14;       /* an error must be agreed by every rank */
+    return rc;
+}
+
+/* parts from a host-only snapshot `base` (consumed: it becomes part 0), one per device, and the ranks */
+static void partition_from(keto_snapshot* base, partition_t* pt) {
+    static int generation = 0;
+    pt->parts[0] = base;
+    for (int k = 1; k < pt->n; ++k) {
+        const int rc = keto_snapshot_clone(base, -1, &pt->parts[k]);
+        if (rc != KETO_OK) fail("keto_snapshot_clone", rc);
+    }
+    for (int k = 0; k < pt->n; ++k) {
+        const int rc = keto_snapshot_upload_part_mode(pt->parts[k], (uint32_t)k, (uint32_t)pt->n, pt->devices[k],
+                                                      KETO_PART_SHARED);
+        if (rc != KETO_OK) fail("keto_snapshot_upload_part_mode", rc);
+    }
+    memset(pt->id, 0, sizeof pt->id);
+    snprintf((char*)pt->id, sizeof pt->id, "keto_consumer partition %d", generation++);
+    rank_call_t calls[MAX_REPLICAS];
+    memset(calls, 0, sizeof calls);
+    for (int k = 0; k < pt->n; ++k) calls[k].op = 0;
+    const int rc = ranks_run(pt, calls);
+    if (rc != KETO_OK) fail("keto_comm_init_local", rc);
+}
+
+static void partition_release(partition_t* pt) {
+    for (int k = 0; k < pt->n; ++k) {
+        keto_comm_free(pt->comms[k]);
+        keto_snapshot_release(pt->parts[k]);
+    }
+}
+
+/* prints the m trees of arena ar ("expand" lines): per-tree and batch JSON, protobuf, and the tree
+   rebuilt from nodes + subject fields re-encoded; returns 0, or the exit code of a mismatch */
+static int print_trees(keto_snapshot* snap, keto_tree_arena* ar, uint32_t m, int* expands) {
+    if (keto_tree_count(ar) != m) return 5;
+    /* the batch JSON (size query, then fill) */
+    uint64_t* offs = (uint64_t*)xrealloc(NULL, (m + 1) * sizeof(uint64_t));
+    const int64_t an = keto_tree_json_all(snap, ar, NULL, 0, offs);
+    if (an < 0) fail("keto_tree_json_all", (int)an);
+    char* all = (char*)xrealloc(NULL, (size_t)an + 1);
+    if (keto_tree_json_all(snap, ar, all, (uint64_t)an, offs) != an) return 6;
+    for (uint32_t k = 0; k < m; ++k) {
+        const int s = keto_tree_status(ar, k);
+        const int64_t jn = keto_tree_json(snap, ar, k, NULL, 0);
+        char* js = NULL;
+        if (jn >= 0) {
+            js = (char*)malloc((size_t)jn + 1);
+            if (!js || keto_tree_json(snap, ar, k, js, (uint64_t)jn + 1) != jn) return 6;
+        }
+        const uint64_t tl = offs[k + 1] - offs[k];
+        if (js ? (tl != (uint64_t)jn || memcmp(all + offs[k], js, tl) != 0) : tl != 0) return 6;
+        const int64_t pn = keto_tree_proto(snap, ar, k, NULL, 0);
+        printf("expand\t%d\t%d\t%s\t", (*expands)++, s, js ? js : "error");
+        buf_t via = {0, 0, 0};
+        if (tree_via_fields(snap, ar, k, &via)) return 9;
+        if (pn > 0) {
+            uint8_t* pb = (uint8_t*)malloc((size_t)pn);
+            if (!pb || keto_tree_proto(snap, ar, k, pb, (uint64_t)pn) != pn) return 7;
+            /* the tree the Go shim builds from nodes + fields encodes to the same bytes */
+            if (via.n != (size_t)pn || memcmp(via.p, pb, (size_t)pn) != 0) return 10;
+            for (int64_t x = 0; x < pn; ++x) printf("%02x", pb[x]);
+            free(pb);
+        } else {
+            if (via.n != 0) return 10;
+            printf("-");
+        }
+        free(via.p);
+        printf("\n");
+        free(js);
+    }
+    free(all);
+    free(offs);
+    return 0;
+}
+
 static void subject_of(line_t* l, int* k, keto_subject* s) {
     memset(s, 0, sizeof *s);
     if (!strcmp(l->f[(*k)++], "I")) {
@@ -301,6 +440,8 @@ int main(int argc, char** argv) {
     uint32_t page_size = 100;
     int device = -1;
     int devices[MAX_REPLICAS], n_reps = 0;
+    partition_t part;
+    memset(&part, 0, sizeof part);
     while (fgets(buf, sizeof buf, in)) {
         line_t* l = (line_t*)calloc(1, sizeof(line_t));
         if (!l || split(buf, l) < 1) return 1;
@@ -308,6 +449,8 @@ int main(int argc, char** argv) {
         else if (!strcmp(l->f[0], "V")) device = atoi(l->f[1]);
         else if (!strcmp(l->f[0], "R"))
             for (int k = 1; k < l->n && n_reps < MAX_REPLICAS; ++k) devices[n_reps++] = atoi(l->f[k]);
+        else if (!strcmp(l->f[0], "Q"))
+            for (int k = 1; k < l->n && part.n < MAX_REPLICAS; ++k) part.devices[part.n++] = atoi(l->f[k]);
         lines = (line_t**)xrealloc(lines, (n_lines + 1) * sizeof(line_t*));
         lines[n_lines++] = l;
     }
@@ -329,7 +472,15 @@ int main(int argc, char** argv) {
     }
     if (n_reps == 0) devices[n_reps++] = device;
     keto_snapshot* reps[MAX_REPLICAS];
-    build_replicas(ns, n_ns, &table, page_size, devices, n_reps, reps);
+    const int parted = part.n > 0;
+    if (parted) {
+        device = part.devices[0];
+        partition_from(build(ns, n_ns, &table, page_size, -1), &part);
+        n_reps = 1;
+        reps[0] = part.parts[0];
+    } else {
+        build_replicas(ns, n_ns, &table, page_size, devices, n_reps, reps);
+    }
     keto_snapshot* snap = reps[0];
     int batches = 0;                          /* batches dealt round-robin over the replicas */
     keto_snapshot_stats st;
@@ -365,6 +516,28 @@ int main(int argc, char** argv) {
                 q[k].max_depth = atoi(c->f[f]);
             }
             snap = reps[batches++ % n_reps];
+            if (parted) {
+                /* every rank its slice of the batch (the last ranks' slices may be empty) */
+                rank_call_t calls[MAX_REPLICAS];
+                memset(calls, 0, sizeof calls);
+                for (int k = 0; k < part.n; ++k) {
+                    const size_t lo = m * (size_t)k / (size_t)part.n, hi = m * (size_t)(k + 1) / (size_t)part.n;
+                    calls[k].op = 1;
+                    calls[k].q = q + lo;
+                    calls[k].n = (uint32_t)(hi - lo);
+                    calls[k].gmd = gmd;
+                    calls[k].allowed = allowed + lo;
+                    calls[k].status = status + lo;
+                }
+                rc = ranks_run(&part, calls);
+                if (rc != KETO_OK) fail("keto_check_batch_routed", rc);
+                for (size_t k = 0; k < m; ++k) printf("check\t%d\t%u\t%u\n", checks++, allowed[k], status[k]);
+                free(q);
+                free(allowed);
+                free(status);
+                i = j;
+                continue;
+            }
             rc = keto_check_batch(snap, q, (uint32_t)m, gmd, allowed, status);
             if (device < 0) {
                 printf("nodevice %d\n", rc);
@@ -435,49 +608,33 @@ int main(int argc, char** argv) {
                 subject_of(lines[i + k], &f, &r[k].subject);
                 r[k].max_depth = atoi(lines[i + k]->f[f]);
             }
-            keto_tree_arena* ar = NULL;
-            snap = reps[batches++ % n_reps];
-            rc = keto_expand_batch(snap, r, (uint32_t)m, gmd, &ar);
-            if (rc != KETO_OK) fail("keto_expand_batch", rc);
-            if (keto_tree_count(ar) != m) return 5;
-            /* the batch JSON (size query, then fill) */
-            uint64_t* offs = (uint64_t*)xrealloc(NULL, (m + 1) * sizeof(uint64_t));
-            const int64_t an = keto_tree_json_all(snap, ar, NULL, 0, offs);
-            if (an < 0) fail("keto_tree_json_all", (int)an);
-            char* all = (char*)xrealloc(NULL, (size_t)an + 1);
-            if (keto_tree_json_all(snap, ar, all, (uint64_t)an, offs) != an) return 6;
-            for (uint32_t k = 0; k < m; ++k) {
-                const int s = keto_tree_status(ar, k);
-                const int64_t jn = keto_tree_json(snap, ar, k, NULL, 0);
-                char* js = NULL;
-                if (jn >= 0) {
-                    js = (char*)malloc((size_t)jn + 1);
-                    if (!js || keto_tree_json(snap, ar, k, js, (uint64_t)jn + 1) != jn) return 6;
+            if (parted) {
+                rank_call_t calls[MAX_REPLICAS];
+                memset(calls, 0, sizeof calls);
+                for (int k = 0; k < part.n; ++k) {
+                    const size_t lo = m * (size_t)k / (size_t)part.n, hi = m * (size_t)(k + 1) / (size_t)part.n;
+                    calls[k].op = 2;
+                    calls[k].e = r + lo;
+                    calls[k].n = (uint32_t)(hi - lo);
+                    calls[k].gmd = gmd;
                 }
-                const uint64_t tl = offs[k + 1] - offs[k];
-                if (js ? (tl != (uint64_t)jn || memcmp(all + offs[k], js, tl) != 0) : tl != 0) return 6;
-                const int64_t pn = keto_tree_proto(snap, ar, k, NULL, 0);
-                printf("expand\t%d\t%d\t%s\t", expands++, s, js ? js : "error");
-                buf_t via = {0, 0, 0};
-                if (tree_via_fields(snap, ar, k, &via)) return 9;
-                if (pn > 0) {
-                    uint8_t* pb = (uint8_t*)malloc((size_t)pn);
-                    if (!pb || keto_tree_proto(snap, ar, k, pb, (uint64_t)pn) != pn) return 7;
-                    /* the tree the Go shim builds from nodes + fields encodes to the same bytes */
-                    if (via.n != (size_t)pn || memcmp(via.p, pb, (size_t)pn) != 0) return 10;
-                    for (int64_t x = 0; x < pn; ++x) printf("%02x", pb[x]);
-                    free(pb);
-                } else {
-                    if (via.n != 0) return 10;
-                    printf("-");
+                rc = ranks_run(&part, calls);
+                if (rc != KETO_OK) fail("keto_expand_batch_routed", rc);
+                for (int k = 0; k < part.n; ++k) {
+                    /* each rank's trees, in request order, read through its own part's host tables */
+                    const int e = print_trees(part.parts[k], calls[k].ar, calls[k].n, &expands);
+                    keto_tree_arena_free(calls[k].ar);
+                    if (e) return e;
                 }
-                free(via.p);
-                printf("\n");
-                free(js);
+            } else {
+                keto_tree_arena* ar = NULL;
+                snap = reps[batches++ % n_reps];
+                rc = keto_expand_batch(snap, r, (uint32_t)m, gmd, &ar);
+                if (rc != KETO_OK) fail("keto_expand_batch", rc);
+                const int e = print_trees(snap, ar, (uint32_t)m, &expands);
+                keto_tree_arena_free(ar);
+                if (e) return e;
             }
-            free(all);
-            free(offs);
-            keto_tree_arena_free(ar);
             free(r);
             i = j;
             continue;
@@ -496,17 +653,26 @@ int main(int argc, char** argv) {
             for (size_t k = 0; k < n_ins; ++k) table_insert(&table, ins[k]);
             for (size_t k = 0; k < n_del; ++k) table_delete(&table, &del[k]);
             /* every replica follows the transaction; one refusal rebuilds them all */
-            uint64_t v0 = keto_snapshot_version(reps[0]), v = 0;
+            /* (a partitioned graph: every part applies every transaction) */
+            keto_snapshot** tgt = parted ? part.parts : reps;
+            const int n_tgt = parted ? part.n : n_reps;
+            uint64_t v0 = keto_snapshot_version(tgt[0]), v = 0;
             int rebuilt = 0;
             rc = KETO_OK;
-            for (int k = 0; k < n_reps && rc == KETO_OK; ++k) {
+            for (int k = 0; k < n_tgt && rc == KETO_OK; ++k) {
                 uint64_t vk = 0;
-                rc = keto_snapshot_apply(reps[k], ins, n_ins, del, n_del, &vk);
-                if (rc == KETO_OK && (vk != v0 + 1 || keto_snapshot_version(reps[k]) != vk)) return 12;
-                if (rc == KETO_E_REBUILD && keto_snapshot_version(reps[k]) != v0) return 11; /* left unchanged */
+                rc = keto_snapshot_apply(tgt[k], ins, n_ins, del, n_del, &vk);
+                if (rc == KETO_OK && (vk != v0 + 1 || keto_snapshot_version(tgt[k]) != vk)) return 12;
+                if (rc == KETO_E_REBUILD && keto_snapshot_version(tgt[k]) != v0) return 11; /* left unchanged */
                 v = vk;
             }
-            if (rc == KETO_E_REBUILD) {
+            if (rc == KETO_E_REBUILD && parted) {
+                partition_release(&part);
+                partition_from(build(ns, n_ns, &table, page_size, -1), &part);
+                reps[0] = part.parts[0];
+                rebuilt = 1;
+                v = keto_snapshot_version(reps[0]);
+            } else if (rc == KETO_E_REBUILD) {
                 for (int k = 0; k < n_reps; ++k) keto_snapshot_release(reps[k]);
                 build_replicas(ns, n_ns, &table, page_size, devices, n_reps, reps);
                 rebuilt = 1;
@@ -517,6 +683,22 @@ int main(int argc, char** argv) {
             snap = reps[0];
             printf("apply\t%d\t%llu\t%d\n", rc, (unsigned long long)v, rebuilt);
             n_ins = n_del = 0;
+        } else if (!strcmp(l->f[0], "S") && parted) {
+            /* the partitioned server's restart: a host-only snapshot of the table saved, the parts
+               released, the file loaded host-only and partitioned again */
+            keto_snapshot* base = build(ns, n_ns, &table, page_size, -1);
+            const uint64_t v0 = keto_snapshot_version(base);
+            rc = keto_snapshot_save(base, l->f[1], v0);
+            if (rc != KETO_OK) fail("keto_snapshot_save", rc);
+            keto_snapshot_release(base);
+            partition_release(&part);
+            uint64_t tag = 0;
+            rc = keto_snapshot_load(l->f[1], -1, &base, &tag);
+            if (rc != KETO_OK) fail("keto_snapshot_load", rc);
+            if (tag != v0 || keto_snapshot_version(base) != v0) return 13;
+            partition_from(base, &part);
+            snap = reps[0] = part.parts[0];
+            printf("restart\t%llu\t%llu\n", (unsigned long long)v0, (unsigned long long)tag);
         } else if (!strcmp(l->f[0], "S")) {
             const uint64_t v0 = keto_snapshot_version(reps[0]);
             rc = keto_snapshot_save(reps[0], l->f[1], v0);
@@ -538,7 +720,10 @@ int main(int argc, char** argv) {
     /* an error path: a NULL argument must fail with a message, not crash */
     rc = keto_check_batch(reps[0], NULL, 1, 5, NULL, NULL);
     if (rc != KETO_E_INVALID || !keto_last_error()[0]) return 8;
-    for (int k = 0; k < n_reps; ++k) keto_snapshot_release(reps[k]);
+    if (parted)
+        partition_release(&part);
+    else
+        for (int k = 0; k < n_reps; ++k) keto_snapshot_release(reps[k]);
     for (size_t i = 0; i < n_lines; ++i) {
         for (int k = 0; k < lines[i]->n; ++k) free(lines[i]->f[k]);
         free(lines[i]);

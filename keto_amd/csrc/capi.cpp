@@ -771,6 +771,15 @@ int keto_mig_begin(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, i
     });
 }
 
+int keto_device_memory(int32_t device, uint64_t* free_out, uint64_t* total_out) {
+    return guarded([&] {
+        if (!free_out || !total_out) throw Error{KETO_E_INVALID, "NULL argument"};
+        if (device < 0) throw Error{KETO_E_INVALID, "no device " + std::to_string(device)};
+        device_memory(device, *free_out, *total_out);
+        return KETO_OK;
+    });
+}
+
 int keto_device_copy(void* dst, const void* src, uint64_t bytes, void* stream) {
     return guarded([&] {
         if (bytes && (!dst || !src)) throw Error{KETO_E_INVALID, "NULL argument"};

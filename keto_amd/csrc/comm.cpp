@@ -754,10 +754,17 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
         }
         settle(*c, mine, codes);
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
-        uint64_t* d_words = c->a.get<uint64_t>(std::max<uint64_t>(words.size(), 1));
-        uint64_t* d_in = c->b.get<uint64_t>(std::max<uint64_t>(m, 1));
-        if (!words.empty())
-            HIP_OK(hipMemcpyAsync(d_words, words.data(), words.size() * 8, hipMemcpyHostToDevice, c->stream));
+        // the exchange buffers are allocated inside the agreement: a rank whose allocation fails still
+        // meets its peers, and every rank returns that rank's code instead of waiting in the all-to-all
+        uint64_t *d_words = nullptr, *d_in = nullptr;
+        mine.run([&] {
+            injected(*c, "roots_alloc");
+            d_words = c->a.get<uint64_t>(std::max<uint64_t>(words.size(), 1));
+            d_in = c->b.get<uint64_t>(std::max<uint64_t>(m, 1));
+            if (!words.empty())
+                HIP_OK(hipMemcpyAsync(d_words, words.data(), words.size() * 8, hipMemcpyHostToDevice, c->stream));
+        });
+        agree(*c, mine);
         c->t->alltoallv(d_words, sb, d_in, rb, c->stream);
         std::vector<uint64_t> got(m);
         if (m) HIP_OK(hipMemcpyAsync(got.data(), d_in, m * 8, hipMemcpyDeviceToHost, c->stream));
@@ -804,10 +811,15 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
         }
         settle(*c, mine, codes);
         const uint64_t tot = std::accumulate(back.begin(), back.end(), 0ull);
-        uint64_t* d_pack = c->d.get<uint64_t>(std::max<uint64_t>(pack.size(), 1));
-        uint64_t* d_back = c->g.get<uint64_t>(std::max<uint64_t>(tot / 8, 1));
-        if (!pack.empty())
-            HIP_OK(hipMemcpyAsync(d_pack, pack.data(), pack.size() * 8, hipMemcpyHostToDevice, c->stream));
+        uint64_t *d_pack = nullptr, *d_back = nullptr;
+        mine.run([&] {
+            injected(*c, "trees_alloc");
+            d_pack = c->d.get<uint64_t>(std::max<uint64_t>(pack.size(), 1));
+            d_back = c->g.get<uint64_t>(std::max<uint64_t>(tot / 8, 1));
+            if (!pack.empty())
+                HIP_OK(hipMemcpyAsync(d_pack, pack.data(), pack.size() * 8, hipMemcpyHostToDevice, c->stream));
+        });
+        agree(*c, mine);
         c->t->alltoallv(d_pack, pb, d_back, back, c->stream);
         std::vector<uint64_t> trees(tot / 8);
         if (tot) HIP_OK(hipMemcpyAsync(trees.data(), d_back, tot, hipMemcpyDeviceToHost, c->stream));

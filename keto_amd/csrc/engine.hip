@@ -1025,10 +1025,10 @@ __device__ inline bool chunk_wait(const uint32_t* p, uint64_t ticks) {
 #endif
 constexpr uint32_t P_XLT = 5;          // streamed: the request's row id (and set target) -> handles
 
-template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM = false>
-__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
-    check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
-                      uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM>
+__device__ __forceinline__ void
+    check_wave_body(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                    uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
     const uint32_t tid = threadIdx.x;
     const uint32_t slot = blockIdx.x * blockDim.x + tid;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1455,6 +1455,21 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         for (int i = 0; i < 16; ++i) atomicAdd(work + i, (unsigned long long)w.c[i]);
         for (int i = 0; i < 8; ++i) atomicAdd(work + 16 + i, (unsigned long long)w.s[i]);
     }
+}
+template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM = false>
+__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
+    check_wave_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                      uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+    check_wave_body<F, WIN, LV, RV, COUNT, STREAM>(s, ov, q, n, gmd, allowed, ta, work);
+}
+// the same walk compiled for 8 waves per SIMD (64 VGPRs), for batches of fewer than 16 requests per
+// lane: there the lanes a launch holds matter more than the instructions per iteration (config #2,
+// 1M requests: 0.149 ms against 0.160-0.164 ms at 6 waves, profiles/r04al_small_batch_waves.log)
+template <int F, int LV, int RV>
+__global__ void __launch_bounds__(256, 8)
+    check_wave_kernel_w8(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                         uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+    check_wave_body<F, false, LV, RV, false, false>(s, ov, q, n, gmd, allowed, ta, work);
 }
 
 // ------------------------------------------------------------------ check, deep requests
@@ -2544,6 +2559,13 @@ T* dmalloc(uint64_t n, uint64_t& acc) {
     hipError_t e = hipMalloc(&p, n * sizeof(T));
     if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
     acc += n * sizeof(T);
+    // KETO_DEBUG_FILL=<u32>: every fresh allocation starts as that word (tests pick a plausible handle),
+    // so a read of memory nothing wrote gives the same wrong answer on every run instead of by chance
+    if (const char* f = getenv("KETO_DEBUG_FILL"); f && *f) {
+        const uint64_t words = n * sizeof(T) / 4;
+        if (words) HIP_OK(hipMemsetD32((hipDeviceptr_t)p, (int)strtoul(f, nullptr, 0), words));
+        HIP_OK(hipDeviceSynchronize());
+    }
     return (T*)p;
 }
 
@@ -3911,8 +3933,20 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     // (deep_wave_kernel keeps one segment bit: arenas of up to 2 segments)
     const bool dw = kind == 2 && deep_wave(gmd) && (uint64_t)D.n_units <= (1ull << 31);
     if (ss && kind != 0) throw Error{KETO_E_INVALID, "streamed batches need max-depth <= 5"};
-    const int var = ss ? T0_VARIANTS + 3 + (t0_stream_v0() ? 1 : 0)
-                       : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
+    int var = ss ? T0_VARIANTS + 3 + (t0_stream_v0() ? 1 : 0)
+                 : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
+    // batches of fewer than 16 requests per lane of the 8-wave build take check_wave_kernel_w8
+    // (variant 0's geometry at 8 waves per SIMD); KETO_T0 (tuning) or KETO_T0_W8=0 keep the variant
+    constexpr int VAR_W8 = T0_VARIANTS + 5;
+    if (kind == 0 && !ss && !work_out && !getenv("KETO_T0") && !(getenv("KETO_T0_W8") && atoi(getenv("KETO_T0_W8")) == 0)) {
+        if (!D.v1_lanes[VAR_W8]) {
+            int per_cu = 0, cus = 0;
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_wave_kernel_w8<4, 4, 16>, 256, 0));
+            HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
+            D.v1_lanes[VAR_W8] = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
+        }
+        if ((uint64_t)n < 16ull * D.v1_lanes[VAR_W8]) var = VAR_W8;
+    }
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
@@ -4064,7 +4098,8 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
                           HIP_OK(hipMemsetAsync(W.heads, 0, KETO_HEAD_WORDS * sizeof(uint32_t), st));
                           a.heads = W.heads;
                       }
-                      go(t0_kernel(var, dwork != nullptr));
+                      if (var == VAR_W8) go(check_wave_kernel_w8<4, 4, 16>);
+                      else go(t0_kernel(var, dwork != nullptr));
                   }
                   else if (level == 0 && dw) {
                       // frames: the tier's GlobalStack area as [frame][lane] 8-B words (DF per lane)
@@ -4197,6 +4232,8 @@ void translate_rows_locked(Snapshot& S, DeviceState& D, const keto_check_ids* d_
         D.row_handle = dmalloc<uint32_t>(D.row_handle_cap, acc);
         HIP_OK(hipMemcpy(D.row_handle, S.unit_of_row.data(), (uint64_t)S.n_rows() * sizeof(uint32_t),
                          hipMemcpyHostToDevice));
+        // the slack rows writes add stays NO_UNIT until device_apply patches it
+        HIP_OK(hipMemset(D.row_handle + S.n_rows(), 0xFF, (D.row_handle_cap - S.n_rows()) * sizeof(uint32_t)));
     }
     if (n) {
         hipLaunchKernelGGL(rows_to_handles, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, d_out, n, D.row_handle,
@@ -4978,6 +5015,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         if (S.n_units && S.n_units <= (1ull << 32)) {
             D.unit_row_cap = std::min<uint64_t>(1ull << 32, S.n_units + S.n_units / 64 + 4096);
             D.unit_row = dmalloc<uint32_t>(D.unit_row_cap, acc);
+            // units that start no row (and the slack) read NO_UNIT, never a stale row id
+            HIP_OK(hipMemsetAsync(D.unit_row, 0xFF, D.unit_row_cap * sizeof(uint32_t), st));
             const uint32_t m32 = (uint32_t)S.layout_units.size();
             if (m32)
                 hipLaunchKernelGGL(scatter_unit_rows, dim3((m32 + 255) / 256), dim3(256), 0, st, D.unit_row,

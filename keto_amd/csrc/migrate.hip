@@ -1008,6 +1008,18 @@ void mig_round(Snapshot& S, const void* d_in, const uint32_t* d_in_off, const ui
               out);
 }
 
+void device_memory(int device, uint64_t& free_bytes, uint64_t& total_bytes) {
+    int cur = 0;
+    HIP_OK(hipGetDevice(&cur));
+    HIP_OK(hipSetDevice(device));
+    size_t f = 0, t = 0;
+    const hipError_t e = hipMemGetInfo(&f, &t);
+    (void)hipSetDevice(cur);
+    if (e != hipSuccess) throw Error{KETO_E_HIP, std::string("hipMemGetInfo: ") + hipGetErrorString(e)};
+    free_bytes = f;
+    total_bytes = t;
+}
+
 void device_copy(void* dst, const void* src, uint64_t bytes, void* stream) {
     if (bytes == 0) return;
     HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));

@@ -262,15 +262,24 @@ std::vector<Slot> build_table(uint64_t n, uint64_t& mask, Fill fill) {
     return t;
 }
 
-RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
+// The state is created once per snapshot under a process-wide mutex: concurrent packed batches hold
+// only the snapshot's shared lock, and two of them must not both create (and free) it.
+RDevState& rdev_get(Snapshot& S, int device) {
+    static std::mutex create_mu;
+    std::lock_guard<std::mutex> lk(create_mu);
     if (!S.rdev) {
-        S.rdev.reset(new RDevState);
-        S.rdev->device = device;
-        HIP_OK(hipStreamCreateWithFlags(&S.rdev->stream, hipStreamNonBlocking));
+        std::unique_ptr<RDevState, RDevStateDeleter> r(new RDevState);
+        r->device = device;
+        HIP_OK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+        S.rdev = std::move(r);
     }
-    RDevState& R = *S.rdev;
-    *st_out = R.stream;
-    if (R.version == S.version) return R;
+    return *S.rdev;
+}
+
+// Brings R's tables to the snapshot's version.  The caller holds R.mu, so no packed batch's kernel
+// reads a table while it is rebuilt (the grow-only buffers free their old storage when they grow).
+void rdev_refresh(Snapshot& S, RDevState& R) {
+    if (R.version == S.version) return;
     hipStream_t st = R.stream;
     ResolveDev v = R.view;
     // the build's strings (strs[0, n_sorted_strs): the host index covers exactly them), its real rows
@@ -365,7 +374,6 @@ RDevState& rdev_state(Snapshot& S, int device, hipStream_t* st_out) {
     }
     R.view = v;
     R.version = S.version;
-    return R;
 }
 
 }  // namespace
@@ -380,9 +388,10 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
         const uint64_t len = (uint64_t)p.len[0] + p.len[1] + p.len[2] + p.len[3] + (p.kind ? (uint64_t)p.len[4] + p.len[5] : 0);
         if (p.off + len > blob_len) throw Error{KETO_E_INVALID, "request " + std::to_string(i) + "'s fields lie outside the blob"};
     }
-    hipStream_t st = nullptr;
-    RDevState& R = rdev_state(S, dv.device, &st);
-    std::lock_guard<std::mutex> lk(R.mu);
+    RDevState& R = rdev_get(S, dv.device);
+    std::lock_guard<std::mutex> lk(R.mu);                                   // held through the last copy
+    rdev_refresh(S, R);
+    hipStream_t st = R.stream;
     const uint8_t* d_blob = upload(R.blob, blob, blob_len, st);
     const keto_check_packed* d_q = upload(R.reqs, reqs, n, st);
     keto_check_ids* d_ids = R.ids.get<keto_check_ids>(n);

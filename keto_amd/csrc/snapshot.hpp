@@ -510,6 +510,7 @@ uint64_t device_tree_proto(Snapshot& s, const keto_tree_node* nodes, uint64_t n_
                            uint32_t n_trees, uint32_t ov_base, const std::vector<RowKey>& ov_keys, uint32_t extra_base,
                            const std::vector<std::string>& extra, uint8_t* buf, uint64_t cap, uint64_t* offsets);
 void device_copy(void* dst, const void* src, uint64_t bytes, void* stream);   // D2D, synchronous
+void device_memory(int device, uint64_t& free_bytes, uint64_t& total_bytes);
 // packed string requests resolved and checked on the device (resolve_dev.hip); the indexes of the
 // requests left to the host (wildcard queries) are appended to `host`
 void device_check_packed(Snapshot& s, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs, uint32_t n,

@@ -98,7 +98,7 @@ def _tuple_fields(ids, t):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("replicas", [1, 2, 3])
+@pytest.mark.parametrize("replicas", [1, 2, 3, "parts2", "parts3"])
 @pytest.mark.parametrize("seed", range(24))
 def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed, replicas):
     """The whole Go call sequence from C: build -> check / expand micro-batches -> write transactions
@@ -106,8 +106,12 @@ def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed, replica
     persister wrapper does) -> checks and expands again; trees also rebuilt from keto_tree_nodes +
     keto_subject_fields (the Go shim's path) and re-encoded byte-equal.  With replicas > 1 the consumer
     is one server process over several devices (here all device 0): replicas cloned from the first
-    build, batches dealt round-robin, every write applied to each.  Every decision and tree is
-    compared with the SQL oracle replaying the same transactions."""
+    build, batches dealt round-robin, every write applied to each.  With "partsP" the graph is
+    partitioned instead (the server's mode for a graph past one device's memory): P shared-rows parts,
+    one local rank per part on its own thread, every batch split over the ranks and routed
+    (keto_check_batch_routed / keto_expand_batch_routed), every write applied to every part, restarts
+    through a host-only saved snapshot partitioned again.  Every decision and tree is compared with the
+    SQL oracle replaying the same transactions."""
     import random
     from oracle.oracle_sql import CheckEngine, ExpandEngine, NotFoundError, SQLStore
     from tests.proto_util import tree_json_to_proto
@@ -121,7 +125,8 @@ def test_consumer_writes_checks_expands_on_gpu(consumer, tmp_path, seed, replica
         pytest.skip("only a namespace named ''")
     ids = {n: i for i, n in reversed(ns)}
     store = SQLStore(ns, tuples, page_size=ps)
-    lines = [f"P\t{ps}", "V\t0", "R" + "\t0" * replicas]
+    topo = ("Q" + "\t0" * int(replicas[5:])) if isinstance(replicas, str) else ("R" + "\t0" * replicas)
+    lines = [f"P\t{ps}", "V\t0", topo]
     lines += [f"N\t{i}\t{n}" for i, n in ns] + [f"T\t{_tuple_fields(ids, t)}" for t in tuples]
     want = []                                  # expected output lines, in order
     rng = random.Random(seed)

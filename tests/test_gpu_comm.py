@@ -423,6 +423,73 @@ def test_local_shared_parts_follow_writes(P, seed):
         p.close()
 
 
+@pytest.mark.parametrize("P", [2, 3])
+def test_shared_parts_new_root_rows_never_read_stale_handles(P, monkeypatch):
+    """The write-path bug behind r04f6 / r04f7, made deterministic.  A write that adds root rows owned
+    by another part gives them no handle on this part; their row -> handle entries must read NO_UNIT.
+    KETO_DEBUG_FILL fills every fresh device allocation with the handle of groups:g#member (the set
+    every docs:yJ row points at), so an entry nothing wrote names that set: a subject-set request
+    docs:yJ#view@(docs:nK#view) would then be allowed on every run, where the reference denies it
+    (check/engine.go:36-80: typed equality of the subject set).  Then the new rows become subject-set
+    targets (they join every part) and requests reach them through groups:g.  An expand runs first on
+    every part, so both lazily built maps exist and the write patches them in place (the path of the
+    bug).  The same test on the library built from before the fix fails every run
+    (profiles/r05b_slack_prefix.log)."""
+    from oracle.oracle_sql import RelationTuple, SQLStore, SubjectID, SubjectSet
+    import keto_amd
+    from keto_amd.capi import PART_SHARED
+    ns = [(0, "docs"), (1, "groups")]
+    tuples = [RelationTuple("groups", "g", "member", SubjectID("alice"))]
+    tuples += [RelationTuple("docs", f"y{j}", "view", SubjectSet("groups", "g", "member")) for j in range(8)]
+    tuples += [RelationTuple("docs", f"d{j}", "view", SubjectID("carol")) for j in range(8)]
+    store = SQLStore(ns, tuples)
+    rows = rows_from_tuples(ns, tuples)
+    parts = [keto_amd.Snapshot.build(ns, rows, device=-1).upload_part(r, P, 0, mode=PART_SHARED) for r in range(P)]
+    # the handle of groups:g#member on every part (a subject-set target: every part holds it, same layout)
+    hs = {int(p.resolve_checks([("groups", "g", "member", ("id", "alice"), 0)])[0]["row"][0]) for p in parts}
+    assert len(hs) == 1, hs
+    monkeypatch.setenv("KETO_DEBUG_FILL", str(hs.pop()))
+    comms = _local_comms(P)
+    g = 5
+
+    def routed_vs_oracle(reqs, step):
+        mine = [list(range(r, len(reqs), P)) for r in range(P)]
+        res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], [reqs[i] for i in mine[r]], g)))
+        for r, (got, st) in enumerate(res):
+            for k, i in enumerate(mine[r]):
+                ns_, o, rel, s_, d = reqs[i]
+                sub = SubjectID(s_[1]) if s_[0] == "id" else SubjectSet(*s_[1:])
+                want = CheckEngine(store, g).subject_is_allowed(RelationTuple(ns_, o, rel, sub), d)
+                assert bool(got[k]) == want and st[k] == 0, (P, step, r, reqs[i])
+
+    news = [f"n{k}" for k in range(16)]
+    probe = [("docs", f"y{j}", "view", ("set", "docs", nk, "view"), 0) for j in range(8) for nk in news]
+    probe += [("docs", f"y{j}", "view", ("id", u), 0) for j in range(8) for u in ("alice", "bob")]
+    probe += [("docs", nk, "view", ("id", "bob"), 0) for nk in news]
+    routed_vs_oracle(probe, "before")                 # allocates each part's row -> handle map
+    # an expand builds each part's handle -> row map: with both maps present a write patches them in
+    # place (without it the maps were dropped and rebuilt whole, which hid the bug)
+    roots = [(("set", "docs", f"y{j}", "view"), 3) for j in range(8)]
+    _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], roots[r::P], g)))
+    ins = [RelationTuple("docs", nk, "view", SubjectID("bob")) for nk in news]
+    for p in parts:
+        p.apply([rows_from_tuples(ns, [t])[0] for t in ins], [])
+    for t in ins:
+        store.insert(t)
+    routed_vs_oracle(probe, "new root rows")
+    # the new rows become subject-set targets: every part now holds them, reached through groups:g
+    sets = [RelationTuple("groups", "g", "member", SubjectSet("docs", nk, "view")) for nk in news[::3]]
+    for p in parts:
+        p.apply([rows_from_tuples(ns, [t])[0] for t in sets], [])
+    for t in sets:
+        store.insert(t)
+    routed_vs_oracle(probe, "new targets")
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+
+
 @pytest.fixture(scope="module")
 def powerlaw_parts():
     """The power-law graph (1/1024 scale) with its strings: a replicated snapshot, shared-rows parts
@@ -479,10 +546,11 @@ def test_local_expand_routed_powerlaw(powerlaw_parts):
         c.close()
 
 
-@pytest.mark.parametrize("point", ["resolve", "expand", "owner"])
+@pytest.mark.parametrize("point", ["resolve", "expand", "roots_alloc", "owner", "trees_alloc"])
 def test_local_expand_error_agreement(powerlaw_parts, monkeypatch, point):
-    """A failure injected on rank 1 before the roots leave (resolve, local expand) or while it expands
-    other ranks' roots (owner): every rank returns the same code; the next call answers exactly."""
+    """A failure injected on rank 1 before the roots leave (resolve, local expand, the roots' exchange
+    buffers) or while it expands other ranks' roots (owner) or sets up the trees' exchange: every rank
+    returns the same code; the next call answers exactly."""
     g, st, full, parts, roots = powerlaw_parts
     P = len(parts)
     comms = _local_comms(P)

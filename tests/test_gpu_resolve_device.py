@@ -144,3 +144,59 @@ def test_packed_empty_batch_and_bad_offsets():
     with pytest.raises(KetoError):
         snap.check_batch_packed(blob, packed, 5)
     snap.close()
+
+
+def test_packed_batches_concurrent_with_writes():
+    """Several threads run packed batches on one snapshot (its shared lock only) while writes add
+    strings and rows: the device resolver's state is created once and its per-version tables are
+    rebuilt under its own lock, never under a running resolve kernel (resolve_dev.hip rdev_get /
+    rdev_refresh).  The requests name rows and strings the writes never touch, so every batch must
+    decide exactly as before the first write; the written rows are checked after."""
+    import threading
+    import keto_amd
+    from keto_amd.capi import pack_requests
+    rng = random.Random(11)
+    ns = [(1, "docs"), (2, "groups")]
+    tuples = []
+    for _ in range(3000):
+        if rng.random() < 0.5:
+            tuples.append(RelationTuple("docs", f"d{rng.randrange(400)}", "view", SubjectID(f"u{rng.randrange(300)}")))
+        elif rng.random() < 0.5:
+            tuples.append(RelationTuple("docs", f"d{rng.randrange(400)}", "view", SubjectSet("groups", f"g{rng.randrange(60)}", "member")))
+        else:
+            tuples.append(RelationTuple("groups", f"g{rng.randrange(60)}", "member", SubjectID(f"u{rng.randrange(300)}")))
+    store = SQLStore(ns, tuples)
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), device=0)
+    reqs = [("docs", f"d{rng.randrange(420)}", "view", ("id", f"u{rng.randrange(320)}"), 0) for _ in range(4000)]
+    blob, packed = pack_requests(reqs)
+    want, want_st = snap.check_batch(reqs, 5)
+    errors, stop = [], threading.Event()
+
+    def reader():
+        try:
+            while not stop.is_set():
+                got, st = snap.check_batch_packed(blob, packed, 5)
+                if not ((got == want).all() and (st == want_st).all()):
+                    errors.append(int((got != want).sum()))
+        except Exception as e:          # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=reader) for _ in range(4)]
+    for t in ts:
+        t.start()
+    written = []
+    for k in range(40):
+        ins = [RelationTuple("docs", f"w{k}_{j}", "view", SubjectID(f"wu{k}_{j}_with_a_long_suffix")) for j in range(5)]
+        snap.apply(rows_from_tuples(ns, ins), [])
+        written += ins
+    stop.set()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:5]
+    for t in written:
+        store.insert(t)
+    wreq = [(t.namespace, t.object, t.relation, ("id", t.subject.id), 0) for t in written[::7]]
+    got = _same_as_host(snap, wreq, 5)
+    assert got.all()
+    snap.close()
