@@ -27,10 +27,13 @@ import (
 //	return reg.ServeAllSQA(cmd)
 //
 // The server stays one process (internal/driver/daemon.go:62-69) and drives every GPU of the node
-// itself: EnableGPU builds one snapshot replica per device from one full scan of the table (sorted
-// and uploaded once, cloned to the other devices, gpu.BuildReplicas), starts the check and expand
-// batchers, which deal each batch to a GPU with no batch in flight, and wraps the persister so that
-// every committed write transaction is applied to every replica before the write returns.  The engines find the batchers through GPUCheckBatcher /
+// itself: EnableGPU builds the snapshot from one full scan of the table (sorted once, host-only) and
+// places it (gpu.Place): one replica per device while the replicated arena fits each of them, else
+// one edge-partitioned snapshot over all of them (gpu.Partition: shared-rows parts, one in-process
+// communicator rank per part), so a table of any size is served from this one process, as the
+// reference serves it.  It starts the check and expand batchers, which deal each batch to an engine
+// with no batch in flight, and wraps the persister so that every committed write transaction is
+// applied to every replica or part before the write returns.  The engines find the batchers through GPUCheckBatcher /
 // GPUExpandBatcher (internal/check/engine_gpu.go, internal/expand/engine_gpu.go) and answer on SQL
 // whenever those return nil: no GPU, or a snapshot that is behind the table while it is rebuilt.
 
@@ -55,13 +58,18 @@ func GPUDevicesFromEnv() []int {
 // gpuRowSource is the persister's full scan (internal/persistence/sql/snapshot_gpu.go).
 type gpuRowSource interface {
 	SnapshotRows(ctx context.Context) ([]gpu.Row, error)
-	SnapshotFingerprint(ctx context.Context) (uint64, error)
 }
+
+// GPUPlacementFromEnv is how the snapshot is placed on the devices (KETO_GPU_PLACEMENT): "auto" (the
+// default: replicas while the replicated arena fits every device, else a partition), "replicate" or
+// "partition".
+func GPUPlacementFromEnv() string { return os.Getenv("KETO_GPU_PLACEMENT") }
 
 // GPUSnapshotFileFromEnv is where the GPU path keeps its persisted snapshot (KETO_GPU_SNAPSHOT_FILE;
 // empty: none).  A server that starts with a file saved under the table's current fingerprint loads
-// it (gpu.Load: about 15 s for 1B tuples) instead of scanning and sorting the table; every build
-// from a scan writes the file again.
+// it (gpu.Load: about 15 s for 1B tuples) instead of sorting the table; every build writes the file
+// again.  The fingerprint is a hash of the scanned rows' contents (gpu.Fingerprint), so the scan
+// still runs; what the file saves is the sort, the interning and the layout.
 func GPUSnapshotFileFromEnv() string { return os.Getenv("KETO_GPU_SNAPSHOT_FILE") }
 
 type gpuState struct {
@@ -70,9 +78,9 @@ type gpuState struct {
 	check   *gpu.Batcher
 	expand  *gpu.ExpandBatcher
 
-	mu    sync.RWMutex
-	snaps []*gpu.Snapshot // one replica per device, all at the same version
-	stale bool            // the replicas are behind the table: the engines answer on SQL until the rebuild lands
+	mu      sync.RWMutex
+	engines []gpu.Engine // one replica per device, or one partition over them, at one version
+	stale   bool         // the engines are behind the table: SQL answers until the rebuild lands
 
 	wmu        sync.Mutex // one write transaction (SQL commit + Apply) at a time; the rebuild's scan holds it too
 	rebuilding bool
@@ -90,7 +98,7 @@ func gpuOf(r *RegistryDefault) *gpuState {
 	return nil
 }
 
-// EnableGPU loads one snapshot replica per HIP device of `devices` (none: leave the registry on SQL).
+// EnableGPU loads the snapshot onto the HIP devices of `devices` (none: leave the registry on SQL).
 func EnableGPU(ctx context.Context, reg Registry, devices []int) error {
 	r, ok := reg.(*RegistryDefault)
 	if !ok || len(devices) == 0 {
@@ -100,14 +108,14 @@ func EnableGPU(ctx context.Context, reg Registry, devices []int) error {
 		return err
 	}
 	st := &gpuState{r: r, devices: append([]int(nil), devices...)}
-	snaps, err := st.build(ctx)
+	engines, err := st.build(ctx)
 	if err != nil {
 		return err
 	}
-	st.snaps = snaps
+	st.engines = engines
 	globalMax := func() int { return r.Config().ReadAPIMaxDepth() }
-	st.check = gpu.NewBatcher(snaps, globalMax, r.PermissionEngine().Fallback())
-	st.expand = gpu.NewExpandBatcher(snaps, globalMax)
+	st.check = gpu.NewBatcher(engines, globalMax, r.PermissionEngine().Fallback())
+	st.expand = gpu.NewExpandBatcher(engines, globalMax)
 	r.p = &gpuPersister{Persister: r.p, g: st}
 	gpuStates.Store(r, st)
 	return nil
@@ -141,58 +149,46 @@ func (r *RegistryDefault) GPUExpandBatcher() *gpu.ExpandBatcher {
 	return st.expand
 }
 
-// build scans the table (caller holds wmu when it must be consistent with writes) and uploads.
-func (g *gpuState) build(ctx context.Context) ([]*gpu.Snapshot, error) {
+// build scans the table (caller holds wmu when it must be consistent with writes) and places the
+// snapshot: from the persisted file when it was saved from these exact rows, else built from them.
+func (g *gpuState) build(ctx context.Context) ([]gpu.Engine, error) {
 	src, ok := g.r.p.(gpuRowSource) // EnableGPU builds before it wraps the persister
 	if !ok {
 		return nil, errors.New("gpu: the persister has no full-scan source")
-	}
-	path := GPUSnapshotFileFromEnv()
-	var fp uint64
-	if path != "" {
-		var err error
-		if fp, err = src.SnapshotFingerprint(ctx); err != nil {
-			return nil, err
-		}
-		if snaps, ok := g.loadFile(path, fp); ok {
-			return snaps, nil
-		}
 	}
 	rows, err := src.SnapshotRows(ctx)
 	if err != nil {
 		return nil, err
 	}
-	snaps, err := g.buildFrom(ctx, rows)
-	if err == nil && path != "" {
-		_ = snaps[0].Save(path, fp) // best effort: without the file the next start scans again
+	if path := GPUSnapshotFileFromEnv(); path != "" {
+		if es, ok := g.loadFile(path, gpu.Fingerprint(rows)); ok {
+			return es, nil
+		}
 	}
-	return snaps, err
+	return g.buildFrom(ctx, rows)
 }
 
-// loadFile: the persisted snapshot at path, if it was saved under fingerprint fp, on the first
-// device and cloned to the others; ok is false (and nothing is kept) otherwise.
-func (g *gpuState) loadFile(path string, fp uint64) ([]*gpu.Snapshot, bool) {
-	first, tag, err := gpu.Load(path, g.devices[0])
+// loadFile: the persisted snapshot at path, if it was saved under fingerprint fp, loaded host-only
+// and placed on the devices; ok is false (and nothing is kept) otherwise.
+func (g *gpuState) loadFile(path string, fp uint64) ([]gpu.Engine, bool) {
+	base, tag, err := gpu.Load(path, -1)
 	if err != nil {
 		return nil, false
 	}
 	if tag != fp {
-		first.Close()
+		base.Close()
 		return nil, false
 	}
-	out := []*gpu.Snapshot{first}
-	for _, d := range g.devices[1:] {
-		c, err := first.Clone(d)
-		if err != nil {
-			gpu.CloseAll(out)
-			return nil, false
-		}
-		out = append(out, c)
+	es, err := gpu.Place(base, g.devices, GPUPlacementFromEnv())
+	if err != nil {
+		return nil, false
 	}
-	return out, true
+	return es, true
 }
 
-func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) ([]*gpu.Snapshot, error) {
+// buildFrom sorts the rows once, host-only, saves the persisted file (best effort: without it the
+// next start sorts again) and places the snapshot on the devices.
+func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) ([]gpu.Engine, error) {
 	nm, err := g.r.Config().NamespaceManager()
 	if err != nil {
 		return nil, err
@@ -201,7 +197,14 @@ func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) ([]*gpu.Snapsh
 	if err != nil {
 		return nil, err
 	}
-	return gpu.BuildReplicas(nss, rows, g.devices)
+	base, err := gpu.Build(nss, rows, -1)
+	if err != nil {
+		return nil, err
+	}
+	if path := GPUSnapshotFileFromEnv(); path != "" {
+		_ = base.Save(path, gpu.Fingerprint(rows))
+	}
+	return gpu.Place(base, g.devices, GPUPlacementFromEnv())
 }
 
 // applyLocked runs after a write committed, with wmu held: every replica follows the table one
@@ -224,14 +227,14 @@ func (g *gpuState) applyLocked(ctx context.Context, ins, del []*relationtuple.In
 		return
 	}
 	g.mu.RLock()
-	snaps, stale := g.snaps, g.stale
+	engines, stale := g.engines, g.stale
 	g.mu.RUnlock()
 	if stale { // an earlier rebuild failed: the replicas are behind, try again
 		g.startRebuildLocked()
 		return
 	}
 	if err == nil {
-		err = gpu.ApplyAll(snaps, iRows, dRows)
+		err = gpu.ApplyEngines(engines, iRows, dRows)
 	}
 	if err != nil { // gpu.ErrRebuild (or a failed write to a device): serve SQL until rebuilt
 		g.startRebuildLocked()
@@ -271,15 +274,15 @@ func (g *gpuState) rebuild() {
 			rows, err = src.SnapshotRows(ctx)
 		}
 		g.wmu.Unlock()
-		var snaps []*gpu.Snapshot
+		var engines []gpu.Engine
 		if err == nil {
-			snaps, err = g.buildFrom(ctx, rows)
+			engines, err = g.buildFrom(ctx, rows)
 		}
 		rows = nil
 		g.wmu.Lock()
 		if err != nil || g.rescan {
 			g.wmu.Unlock()
-			gpu.CloseAll(snaps)
+			gpu.CloseEngines(engines)
 			if err != nil { // stay stale (SQL answers); a later write retries the rebuild
 				g.wmu.Lock()
 				g.rebuilding = false
@@ -290,26 +293,26 @@ func (g *gpuState) rebuild() {
 		}
 		replayed := true
 		for _, w := range g.pending {
-			if gpu.ApplyAll(snaps, w[0], w[1]) != nil {
+			if gpu.ApplyEngines(engines, w[0], w[1]) != nil {
 				replayed = false
 				break
 			}
 		}
 		if !replayed { // a replayed write needs a rebuild itself: scan again
 			g.wmu.Unlock()
-			gpu.CloseAll(snaps)
+			gpu.CloseEngines(engines)
 			continue
 		}
-		old := g.check.Swap(snaps) // waits for batches running on the old versions
-		g.expand.Swap(snaps)
+		old := g.check.Swap(engines) // waits for batches running on the old versions
+		g.expand.Swap(engines)
 		g.mu.Lock()
-		g.snaps = snaps
+		g.engines = engines
 		g.stale = false
 		g.mu.Unlock()
 		g.pending = nil
 		g.rebuilding = false
 		g.wmu.Unlock()
-		gpu.CloseAll(old)
+		gpu.CloseEngines(old)
 		return
 	}
 }

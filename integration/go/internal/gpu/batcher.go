@@ -135,44 +135,51 @@ func (c *coalescer) loop() {
 // requests still queued when the batcher closes.
 type Fallback func(ctx context.Context, r *relationtuple.InternalRelationTuple, restDepth int) (bool, error)
 
-// replicas deals batches to the snapshots of a replica set, one per GPU (BuildReplicas): a batch goes
-// to a replica with no batch in flight, so the GPUs of a node work on consecutive batches at once and
-// the dealing follows their load; when every replica is busy the flush loop waits (back-pressure).
+// replicas deals batches to the engines of a set: one snapshot replica per GPU (BuildReplicas), or
+// one Partition over all of them (a graph past one GPU's memory).  A batch goes to an engine with no
+// batch in flight, so the GPUs of a node work on consecutive batches at once and the dealing follows
+// their load; when every engine is busy the flush loop waits (back-pressure).
 type replicas struct {
-	mu    sync.RWMutex // held shared by a running batch, exclusively by Swap
-	snaps []*Snapshot
-	idle  chan int
+	mu  sync.RWMutex // held shared by a running batch (from dealing to its end), exclusively by swap
+	cur *engineSet
 }
 
-func newReplicas(snaps []*Snapshot) *replicas {
-	r := &replicas{snaps: snaps, idle: make(chan int, len(snaps))}
+type engineSet struct {
+	snaps []Engine
+	idle  chan int // indices of the engines with no batch in flight
+}
+
+func newEngineSet(snaps []Engine) *engineSet {
+	s := &engineSet{snaps: snaps, idle: make(chan int, len(snaps))}
 	for k := range snaps {
-		r.idle <- k
+		s.idle <- k
 	}
-	return r
+	return s
 }
 
-// run takes an idle replica, then runs fn on it in its own goroutine.
-func (r *replicas) run(fn func(s *Snapshot)) {
-	k := <-r.idle
+func newReplicas(snaps []Engine) *replicas { return &replicas{cur: newEngineSet(snaps)} }
+
+// run takes an idle engine of the current set, then runs fn on it in its own goroutine.  The shared
+// lock is held from here until fn returns (another goroutine may release it), so a swap waits for
+// the batches in flight and no batch sees two sets.
+func (r *replicas) run(fn func(s Engine)) {
+	r.mu.RLock()
+	set := r.cur
+	k := <-set.idle
 	go func() {
-		defer func() { r.idle <- k }()
-		r.mu.RLock()
 		defer r.mu.RUnlock()
-		fn(r.snaps[k])
+		defer func() { set.idle <- k }()
+		fn(set.snaps[k])
 	}()
 }
 
-// swap installs a new replica set of the same size (a rebuild); it returns the old one once no batch
-// uses it.
-func (r *replicas) swap(snaps []*Snapshot) []*Snapshot {
+// swap installs a new engine set (a rebuild, which may also change the placement: replicas <-> a
+// partition); it returns the old one once no batch uses it.
+func (r *replicas) swap(snaps []Engine) []Engine {
 	r.mu.Lock()
 	defer r.mu.Unlock()
-	if len(snaps) != len(r.snaps) {
-		panic("gpu: a replica set is swapped for one of another size")
-	}
-	old := r.snaps
-	r.snaps = snaps
+	old := r.cur.snaps
+	r.cur = newEngineSet(snaps)
 	return old
 }
 
@@ -190,15 +197,15 @@ type checkReq struct {
 	depth int
 }
 
-// NewBatcher starts the flush loop over one snapshot per GPU.
-func NewBatcher(snaps []*Snapshot, globalMax func() int, fb Fallback) *Batcher {
+// NewBatcher starts the flush loop over the engines (one snapshot per GPU, or a partition).
+func NewBatcher(snaps []Engine, globalMax func() int, fb Fallback) *Batcher {
 	b := &Batcher{rep: newReplicas(snaps), GlobalMax: globalMax, Fallback: fb}
 	b.c = newCoalescer(1<<16, 200*time.Microsecond, b.flush, b.fallbackAll)
 	return b
 }
 
-// Swap installs a new replica set (a rebuild); it returns the old one once no batch uses it.
-func (b *Batcher) Swap(snaps []*Snapshot) []*Snapshot { return b.rep.swap(snaps) }
+// Swap installs a new engine set (a rebuild); it returns the old one once no batch uses it.
+func (b *Batcher) Swap(snaps []Engine) []Engine { return b.rep.swap(snaps) }
 
 // Close stops the loop; queued requests are answered by the fallback, later ones too.
 func (b *Batcher) Close() { b.c.close() }
@@ -233,7 +240,7 @@ func (b *Batcher) flush(batch []*pending) {
 		reqs[i], depths[i] = q.r, q.depth
 	}
 	globalMax := b.GlobalMax()
-	b.rep.run(func(s *Snapshot) {
+	b.rep.run(func(s Engine) {
 		allowed, status, err := s.CheckBatch(reqs, depths, globalMax)
 		if err != nil {
 			b.fallbackAll(batch)
@@ -267,8 +274,8 @@ type expandReq struct {
 	depth int
 }
 
-// NewExpandBatcher starts the flush loop over one snapshot per GPU.
-func NewExpandBatcher(snaps []*Snapshot, globalMax func() int) *ExpandBatcher {
+// NewExpandBatcher starts the flush loop over the engines (one snapshot per GPU, or a partition).
+func NewExpandBatcher(snaps []Engine, globalMax func() int) *ExpandBatcher {
 	b := &ExpandBatcher{rep: newReplicas(snaps), GlobalMax: globalMax}
 	b.c = newCoalescer(1<<12, 200*time.Microsecond, b.flush, func(ps []*pending) {
 		for _, p := range ps {
@@ -278,8 +285,8 @@ func NewExpandBatcher(snaps []*Snapshot, globalMax func() int) *ExpandBatcher {
 	return b
 }
 
-// Swap installs a new replica set; it returns the old one once no batch uses it.
-func (b *ExpandBatcher) Swap(snaps []*Snapshot) []*Snapshot { return b.rep.swap(snaps) }
+// Swap installs a new engine set; it returns the old one once no batch uses it.
+func (b *ExpandBatcher) Swap(snaps []Engine) []Engine { return b.rep.swap(snaps) }
 
 // Close stops the loop; queued and later requests get ErrClosed.
 func (b *ExpandBatcher) Close() { b.c.close() }
@@ -302,7 +309,7 @@ func (b *ExpandBatcher) flush(batch []*pending) {
 		subs[i], depths[i] = q.sub, q.depth
 	}
 	globalMax := b.GlobalMax()
-	b.rep.run(func(s *Snapshot) {
+	b.rep.run(func(s Engine) {
 		trees, errs, err := s.ExpandBatch(subs, depths, globalMax)
 		for i, p := range batch {
 			switch {

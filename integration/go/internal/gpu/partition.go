@@ -1,0 +1,334 @@
+//go:build keto_gpu
+// +build keto_gpu
+
+package gpu
+
+/*
+#include "keto_mi355x.h"
+*/
+import "C"
+
+import (
+	"crypto/rand"
+	"errors"
+	"sync"
+
+	"github.com/ory/keto/internal/relationtuple"
+)
+
+// Engine is what the check and expand batchers deal a batch to: one snapshot replica on one GPU, or
+// a whole partition over several GPUs.  Apply follows one committed write transaction; Close
+// releases it.
+type Engine interface {
+	CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error)
+	ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([][]Node, []error, error)
+	Apply(inserts, deletes []Row) error
+	Close()
+}
+
+// Engines views a replica set as engines.
+func Engines(snaps []*Snapshot) []Engine {
+	out := make([]Engine, len(snaps))
+	for i, s := range snaps {
+		out[i] = s
+	}
+	return out
+}
+
+// DeviceMemory is the free and total memory of HIP device d (keto_device_memory).
+func DeviceMemory(d int) (free, total uint64, err error) {
+	var f, t C.uint64_t
+	if rc := C.keto_device_memory(C.int32_t(d), &f, &t); rc != C.KETO_OK {
+		return 0, 0, lastErr(rc)
+	}
+	return uint64(f), uint64(t), nil
+}
+
+// PartArenaBytes is the device arena part `part` of nParts shared-rows parts of this host-only
+// snapshot would take (keto_snapshot_part_stats_mode); nParts = 1 is the replicated arena.
+func (s *Snapshot) PartArenaBytes(part, nParts int) (uint64, error) {
+	var st C.keto_part_stats
+	if rc := C.keto_snapshot_part_stats_mode(s.h, C.uint32_t(part), C.uint32_t(nParts), C.KETO_PART_SHARED, &st); rc != C.KETO_OK {
+		return 0, lastErr(rc)
+	}
+	return uint64(st.arena_bytes), nil
+}
+
+// UploadPart uploads this host-only snapshot as part `part` of nParts shared-rows parts on HIP
+// device `device` (keto_snapshot_upload_part_mode, KETO_PART_SHARED): the rows subject sets point at
+// on every part, each root row on the part hash(namespace, object) picks.
+func (s *Snapshot) UploadPart(part, nParts, device int) error {
+	if rc := C.keto_snapshot_upload_part_mode(s.h, C.uint32_t(part), C.uint32_t(nParts), C.int32_t(device), C.KETO_PART_SHARED); rc != C.KETO_OK {
+		return lastErr(rc)
+	}
+	return nil
+}
+
+// workspaceBytes is what a device keeps beside its arena for the engine's tiers, visited tables,
+// expand staging and request buffers (the deep tiers and the expand staging pool take the most).
+const workspaceBytes = 12 << 30
+
+// Fits reports whether an arena of `arena` bytes and the engine's workspaces fit on every device.
+func Fits(arena uint64, devices []int) (bool, error) {
+	for _, d := range devices {
+		free, _, err := DeviceMemory(d)
+		if err != nil {
+			return false, err
+		}
+		if arena+arena/8+workspaceBytes > free { // + room for the rows writes add
+			return false, nil
+		}
+	}
+	return true, nil
+}
+
+// Partition is a graph too large for one GPU, edge-partitioned over the devices of the server
+// process: one shared-rows part per device (subject-set targets on every part, root rows by hash)
+// and one in-process communicator rank per part (keto_comm_init_local).  It answers batches like a
+// snapshot does: a batch is split over the ranks and every rank calls the collective routed entry
+// point with its slice -- an empty slice too -- on its own goroutine, so each request travels to
+// the part owning its row and its decision (or tree) comes back.  Batches run one at a time; every
+// write transaction is applied to every part (each holds the whole graph's host tables).
+type Partition struct {
+	mu    sync.Mutex
+	parts []*Snapshot
+	comms []*Comm
+}
+
+// NewPartition partitions the host-only snapshot base over devices; base becomes part 0 (the
+// partition owns it), the other parts are host-only clones of it.
+func NewPartition(base *Snapshot, devices []int) (*Partition, error) {
+	if len(devices) == 0 {
+		return nil, errors.New("gpu: no device")
+	}
+	p := &Partition{parts: []*Snapshot{base}}
+	for range devices[1:] {
+		c, err := base.Clone(-1)
+		if err != nil {
+			p.Close()
+			return nil, err
+		}
+		p.parts = append(p.parts, c)
+	}
+	for k, d := range devices {
+		if err := p.parts[k].UploadPart(k, len(devices), d); err != nil {
+			p.Close()
+			return nil, err
+		}
+	}
+	id := make([]byte, C.KETO_COMM_ID_BYTES)
+	if _, err := rand.Read(id); err != nil {
+		p.Close()
+		return nil, err
+	}
+	p.comms = make([]*Comm, len(devices))
+	errs := p.ranks(func(k int) error {
+		c, err := NewLocalComm(id, len(devices), k, devices[k])
+		p.comms[k] = c
+		return err
+	})
+	if err := firstErr(errs); err != nil {
+		p.Close()
+		return nil, err
+	}
+	return p, nil
+}
+
+// ranks runs fn(k) for every rank at once, each on its own goroutine (a collective call blocks its
+// OS thread until every rank has arrived), and returns each rank's error.
+func (p *Partition) ranks(fn func(k int) error) []error {
+	errs := make([]error, len(p.parts))
+	var wg sync.WaitGroup
+	for k := range p.parts {
+		wg.Add(1)
+		go func(k int) {
+			defer wg.Done()
+			errs[k] = fn(k)
+		}(k)
+	}
+	wg.Wait()
+	return errs
+}
+
+func firstErr(errs []error) error {
+	for _, e := range errs {
+		if e != nil {
+			return e
+		}
+	}
+	return nil
+}
+
+// slice bounds of rank k's share of n requests
+func share(n, k, ranks int) (int, int) { return n * k / ranks, n * (k + 1) / ranks }
+
+// CheckBatch = SubjectIsAllowed for many requests over the partition (keto_check_batch_routed).
+func (p *Partition) CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	p.mu.Lock()
+	defer p.mu.Unlock()
+	allowed := make([]bool, len(reqs))
+	status := make([]uint8, len(reqs))
+	errs := p.ranks(func(k int) error {
+		lo, hi := share(len(reqs), k, len(p.parts))
+		a, st, err := p.comms[k].CheckBatchRouted(p.parts[k], reqs[lo:hi], depths[lo:hi], globalMax)
+		if err != nil {
+			return err
+		}
+		copy(allowed[lo:hi], a)
+		copy(status[lo:hi], st)
+		return nil
+	})
+	if err := firstErr(errs); err != nil { // agreed: every rank returned the failing rank's code
+		return nil, nil, err
+	}
+	return allowed, status, nil
+}
+
+// ExpandBatch = BuildTree for many roots over the partition (keto_expand_batch_routed).
+func (p *Partition) ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([][]Node, []error, error) {
+	p.mu.Lock()
+	defer p.mu.Unlock()
+	trees := make([][]Node, len(subs))
+	terrs := make([]error, len(subs))
+	errs := p.ranks(func(k int) error {
+		lo, hi := share(len(subs), k, len(p.parts))
+		t, e, err := p.comms[k].ExpandBatchRouted(p.parts[k], subs[lo:hi], depths[lo:hi], globalMax)
+		if err != nil {
+			return err
+		}
+		copy(trees[lo:hi], t)
+		copy(terrs[lo:hi], e)
+		return nil
+	})
+	if err := firstErr(errs); err != nil {
+		return nil, nil, err
+	}
+	return trees, terrs, nil
+}
+
+// Apply follows one committed write transaction on every part (see Snapshot.Apply).  An error
+// leaves the parts inconsistent: the caller rebuilds the partition.
+func (p *Partition) Apply(inserts, deletes []Row) error {
+	p.mu.Lock()
+	defer p.mu.Unlock()
+	for _, s := range p.parts {
+		if err := s.Apply(inserts, deletes); err != nil {
+			return err
+		}
+	}
+	return nil
+}
+
+// Close releases the communicators and the parts.
+func (p *Partition) Close() {
+	for _, c := range p.comms {
+		if c != nil {
+			c.Close()
+		}
+	}
+	for _, s := range p.parts {
+		s.Close()
+	}
+	p.comms, p.parts = nil, nil
+}
+
+// Place builds the engines for a host-only snapshot base (consumed) on devices: replicas -- base
+// cloned to every device -- when the replicated arena fits each of them (mode "" or "auto") or when
+// mode is "replicate"; else (or with mode "partition") one Partition over all of them.
+func Place(base *Snapshot, devices []int, mode string) ([]Engine, error) {
+	if len(devices) == 0 {
+		base.Close()
+		return nil, errors.New("gpu: no device")
+	}
+	replicate := mode == "replicate"
+	if mode == "" || mode == "auto" {
+		arena, err := base.PartArenaBytes(0, 1)
+		if err != nil {
+			base.Close()
+			return nil, err
+		}
+		if replicate, err = Fits(arena, devices); err != nil {
+			base.Close()
+			return nil, err
+		}
+	}
+	if !replicate {
+		p, err := NewPartition(base, devices)
+		if err != nil {
+			return nil, err
+		}
+		return []Engine{p}, nil
+	}
+	var out []*Snapshot
+	for _, d := range devices {
+		c, err := base.Clone(d)
+		if err != nil {
+			CloseAll(out)
+			base.Close()
+			return nil, err
+		}
+		out = append(out, c)
+	}
+	base.Close()
+	return Engines(out), nil
+}
+
+// ApplyEngines applies one transaction to every engine of a set (see Snapshot.Apply).  An error
+// leaves the set inconsistent: the caller rebuilds it (gpu.ErrRebuild or a device error alike).
+func ApplyEngines(es []Engine, inserts, deletes []Row) error {
+	for _, e := range es {
+		if err := e.Apply(inserts, deletes); err != nil {
+			return err
+		}
+	}
+	return nil
+}
+
+// CloseEngines closes every engine of a set.
+func CloseEngines(es []Engine) {
+	for _, e := range es {
+		e.Close()
+	}
+}
+
+// Fingerprint identifies the table's contents for a persisted snapshot (Snapshot.Save's tag): an
+// order-independent hash of the multiset of rows (a sum of per-row hashes) mixed with their count.
+// Any committed write changes it -- an insert adds a row's hash, a delete removes one (duplicates
+// included) -- whatever the rows' commit_time (the reference sets it from the app clock,
+// relationtuples.go:137, and a MySQL TIMESTAMP keeps whole seconds only), so a restarting server
+// never loads a file whose contents differ from the table's.
+func Fingerprint(rows []Row) uint64 {
+	var sum uint64
+	for i := range rows {
+		r := &rows[i]
+		h := uint64(1469598103934665603)
+		add := func(b string) {
+			for k := 0; k < len(b); k++ {
+				h = (h ^ uint64(b[k])) * 1099511628211
+			}
+			h = (h ^ uint64(len(b))) * 1099511628211 // field boundaries: "ab","c" != "a","bc"
+		}
+		h = (h ^ uint64(uint32(r.NamespaceID))) * 1099511628211
+		add(r.Object)
+		add(r.Relation)
+		if r.SubjectID != nil {
+			h = (h ^ 1) * 1099511628211
+			add(*r.SubjectID)
+		} else {
+			h = (h ^ 2 ^ uint64(uint32(r.SetNamespaceID))<<8) * 1099511628211
+			add(r.SetObject)
+			add(r.SetRelation)
+		}
+		sum += mix64(h)
+	}
+	return mix64(sum ^ mix64(uint64(len(rows))+0x9E3779B97F4A7C15))
+}
+
+func mix64(x uint64) uint64 {
+	x ^= x >> 31
+	x *= 0xBF58476D1CE4E5B9
+	x ^= x >> 29
+	x *= 0x94D049BB133111EB
+	return x ^ x>>32
+}
+

@@ -49,27 +49,3 @@ func (p *Persister) SnapshotRows(ctx context.Context) ([]gpu.Row, error) {
 		last = res[len(res)-1]
 	}
 }
-
-// SnapshotFingerprint identifies the table's current contents for a persisted GPU snapshot
-// (gpu.Snapshot.Save / gpu.Load): this network's row count and its newest commit_time.  Every
-// insert gets a newer commit_time (relationtuples.go:128-149) and every delete lowers the count
-// (:200-223), so any committed write transaction changes the pair; a file saved under another
-// fingerprint is not loaded.
-func (p *Persister) SnapshotFingerprint(ctx context.Context) (uint64, error) {
-	n, err := p.QueryWithNetwork(ctx).Count(&RelationTuple{})
-	if err != nil {
-		return 0, sqlcon.HandleError(err)
-	}
-	var newest int64
-	if n > 0 {
-		var last RelationTuple
-		if err := p.QueryWithNetwork(ctx).Order("commit_time DESC, shard_id DESC").First(&last); err != nil {
-			return 0, sqlcon.HandleError(err)
-		}
-		newest = last.CommitTime.UnixNano()
-	}
-	h := uint64(n)*0x9E3779B97F4A7C15 ^ uint64(newest)
-	h ^= h >> 31
-	h *= 0xBF58476D1CE4E5B9
-	return h ^ h>>29, nil
-}

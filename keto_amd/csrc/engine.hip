@@ -429,6 +429,10 @@ struct VisitedRS {
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
         const uint32_t lcap = lds ? (uint32_t)LV : 0u;
+        // a map past registers + LDS lives wholly in the table (its first ids were copied there at
+        // the overflow), so a deep search's test is one table probe: the register compares and the
+        // serial LDS scan cost a long chain ~0.3 us per step (tools/dev/chain_probe.py)
+        if (n > (uint32_t)REG_VIDS + lcap) return V.test_add(vid, w);
         const uint32_t m = min(n, (uint32_t)REG_VIDS + lcap);
         bool hit = false;
 #pragma unroll
@@ -447,10 +451,14 @@ struct VisitedRS {
             ++n;
             return 0;
         }
-        if (n == (uint32_t)REG_VIDS + lcap) {            // first overflow of this map
-            V.fresh();
-            ++n;
-        }
+        // first overflow of this map: the table takes every id so far (all distinct), then vid
+        V.fresh();
+        ++n;
+#pragma unroll
+        for (int i = 0; i < REG_VIDS; ++i)
+            if (V.test_add(r[i], w) == 2) return 2;
+        for (uint32_t i = 0; i < lcap; ++i)
+            if (V.test_add(lds[i * LDS_STRIDE], w) == 2) return 2;
         return V.test_add(vid, w);
     }
 };

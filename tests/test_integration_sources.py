@@ -100,37 +100,113 @@ def test_engine_dispatch_hooks_match_the_registry():
 
 def test_multi_gpu_server_process():
     """One server process drives every GPU (the reference is one process, internal/driver/daemon.go:62-69):
-    EnableGPU takes the device list, builds one replica per device (sorted once, the others cloned
-    with keto_snapshot_clone), the batchers deal batches over the replica set, and every write
-    transaction reaches every replica before it returns."""
+    EnableGPU takes the device list and places the snapshot (gpu.Place): one replica per device while
+    the replicated arena fits each of them (sized with keto_snapshot_part_stats_mode and
+    keto_device_memory), else one Partition over all of them; the batchers deal batches over the
+    engine set, and every write transaction reaches every replica or part before it returns."""
     reg = _code(open(os.path.join(GO, "internal", "driver", "registry_gpu.go")).read())
     assert re.search(r"func EnableGPU\(ctx context\.Context, reg Registry, devices \[\]int\) error", reg)
-    assert "gpu.BuildReplicas(" in reg and "gpu.ApplyAll(" in reg and "func GPUDevicesFromEnv() []int" in reg
+    assert "gpu.Place(" in reg and "gpu.ApplyEngines(" in reg and "func GPUDevicesFromEnv() []int" in reg
+    assert "func GPUPlacementFromEnv() string" in reg
     gpu_go = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
     assert "C.keto_snapshot_clone(" in gpu_go
-    assert re.search(r"func BuildReplicas\(nss \[\]\*namespace\.Namespace, rows \[\]Row, devices \[\]int\)", gpu_go)
+    part = _code(open(os.path.join(GO, "internal", "gpu", "partition.go")).read())
+    assert re.search(r"func Place\(base \*Snapshot, devices \[\]int, mode string\) \(\[\]Engine, error\)", part)
+    assert "C.keto_device_memory(" in part and "C.keto_snapshot_part_stats_mode(" in part
     bat = _code(open(os.path.join(GO, "internal", "gpu", "batcher.go")).read())
-    assert re.search(r"func NewBatcher\(snaps \[\]\*Snapshot,", bat)
-    assert re.search(r"func NewExpandBatcher\(snaps \[\]\*Snapshot,", bat)
-    assert "r.idle" in bat                              # a batch goes to a replica with none in flight
+    assert re.search(r"func NewBatcher\(snaps \[\]Engine,", bat)
+    assert re.search(r"func NewExpandBatcher\(snaps \[\]Engine,", bat)
+    assert "set.idle" in bat                            # a batch goes to an engine with none in flight
+    # both engine kinds answer the batchers: a replica and a partition
+    for recv in (r"\(s \*Snapshot\)", r"\(p \*Partition\)"):
+        for m in ("CheckBatch", "ExpandBatch", "Apply", "Close"):
+            assert re.search(r"^func " + recv + " " + m + r"\(", gpu_go + "\n" + part + "\n" +
+                             _code(open(os.path.join(GO, "internal", "gpu", "apply.go")).read()), re.M), (recv, m)
+
+
+def test_partitioned_serving():
+    """A graph past one GPU's memory is served partitioned from the same process: shared-rows parts
+    (keto_snapshot_upload_part_mode, KETO_PART_SHARED) on the devices, one in-process communicator
+    rank per part (NewLocalComm), every batch split over the ranks and routed collectively -- every
+    rank calls, an empty slice too -- and every write applied to every part."""
+    part = _code(open(os.path.join(GO, "internal", "gpu", "partition.go")).read())
+    assert "C.keto_snapshot_upload_part_mode(" in part and "C.KETO_PART_SHARED" in part
+    assert "NewLocalComm(" in part
+    assert ".CheckBatchRouted(p.parts[k], reqs[lo:hi]" in part          # every rank, its slice
+    assert ".ExpandBatchRouted(p.parts[k], subs[lo:hi]" in part
+    assert "wg.Wait()" in part                                           # the ranks' calls run at once
+    apply_at = part.index("func (p *Partition) Apply(")
+    assert "s.Apply(inserts, deletes)" in part[apply_at:apply_at + 400]
 
 
 def test_persisted_snapshot_at_startup():
-    """A server started with KETO_GPU_SNAPSHOT_FILE loads the persisted snapshot (keto_snapshot_load)
-    when its tag is the table's current fingerprint (row count + newest commit_time), clones it to
-    the other devices, and otherwise scans, builds and saves the file again (keto_snapshot_save)."""
+    """A server started with KETO_GPU_SNAPSHOT_FILE scans the table, and loads the persisted snapshot
+    (keto_snapshot_load, host-only, then placed) when its tag is the fingerprint of the scanned rows'
+    contents (gpu.Fingerprint: an order-independent hash of the row multiset, so no committed write
+    leaves it unchanged); otherwise it builds and saves the file again (keto_snapshot_save)."""
     reg = _code(open(os.path.join(GO, "internal", "driver", "registry_gpu.go")).read())
     gpu_go = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
-    sql = _code(open(os.path.join(GO, "internal", "persistence", "sql", "snapshot_gpu.go")).read())
+    part = _code(open(os.path.join(GO, "internal", "gpu", "partition.go")).read())
     assert "C.keto_snapshot_save(" in gpu_go and "C.keto_snapshot_load(" in gpu_go
     assert re.search(r"func \(s \*Snapshot\) Save\(path string, tag uint64\) error", gpu_go)
     assert re.search(r"func Load\(path string, device int\) \(\*Snapshot, uint64, error\)", gpu_go)
-    assert re.search(r"func \(p \*Persister\) SnapshotFingerprint\(ctx context\.Context\) \(uint64, error\)", sql)
-    assert "SnapshotFingerprint(ctx context.Context) (uint64, error)" in reg      # part of the row source
-    load_at = reg.index("g.loadFile(path, fp)")
+    assert re.search(r"func Fingerprint\(rows \[\]Row\) uint64", part)
     scan_at = reg.index("src.SnapshotRows(ctx)")
-    assert load_at < scan_at                                                    # the file first
-    assert ".Save(path, fp)" in reg and "tag != fp" in reg
+    load_at = reg.index("g.loadFile(path, gpu.Fingerprint(rows))")
+    assert scan_at < load_at                                                    # the rows' contents first
+    assert ".Save(path, gpu.Fingerprint(rows))" in reg and "tag != fp" in reg
+    assert "gpu.Load(path, -1)" in reg
+
+
+def test_fingerprint_is_order_independent_and_content_sensitive():
+    """gpu.Fingerprint restated in Python (FNV-1a per field with length separators, a splitmix64
+    finalizer, a wrapping sum over rows): the same multiset in another order gives the same value;
+    deleting a tuple and inserting another (same count) changes it; a duplicate counts."""
+    M = (1 << 64) - 1
+
+    def mix64(x):
+        x ^= x >> 31
+        x = (x * 0xBF58476D1CE4E5B9) & M
+        x ^= x >> 29
+        x = (x * 0x94D049BB133111EB) & M
+        return x ^ (x >> 32)
+
+    def row_hash(r):
+        h = 1469598103934665603
+
+        def step(v):
+            nonlocal h
+            h = ((h ^ v) * 1099511628211) & M
+
+        def add(b):
+            for c in b.encode():
+                step(c)
+            step(len(b.encode()))
+        step(r[0] & 0xFFFFFFFF)
+        add(r[1])
+        add(r[2])
+        if r[3] is not None:
+            step(1)
+            add(r[3])
+        else:
+            step(2 ^ ((r[4] & 0xFFFFFFFF) << 8))
+            add(r[5])
+            add(r[6])
+        return h
+
+    def fp(rows):
+        s = sum(mix64(row_hash(r)) for r in rows) & M
+        return mix64(s ^ mix64((len(rows) + 0x9E3779B97F4A7C15) & M))
+
+    a = [(1, "d", "view", "u1"), (1, "d", "view", None, 2, "g", "member"), (2, "g", "member", "u2")]
+    assert fp(a) == fp(list(reversed(a)))
+    assert fp(a) != fp(a[:2] + [(2, "g", "member", "u3")])
+    assert fp(a) != fp(a + [a[0]])
+    assert fp([(1, "ab", "c", "x")]) != fp([(1, "a", "bc", "x")])
+    part = open(os.path.join(GO, "internal", "gpu", "partition.go")).read()
+    for const in ("1469598103934665603", "1099511628211", "0xBF58476D1CE4E5B9", "0x94D049BB133111EB",
+                  "0x9E3779B97F4A7C15"):
+        assert const in part, const
 
 
 def test_collective_calls_never_skip_an_empty_batch():

@@ -72,6 +72,23 @@ def main():
                               "us_per_step_tier0": round(deep_ms * 1e3 / max(1, int(steps[i])), 3),
                               "us_per_step_wall": round(best * 1e3 / max(1, int(steps[i])), 3)})
         log(json.dumps(res["single"][-1]))
+    # the whole batch, and the batch without its longest searches: how much of the batch is the chain
+    for drop in (0, 16, 256):
+        keep = np.sort(order[drop:])
+        sub = torch.from_numpy(qd[keep].copy().view(np.uint8)).to("cuda:0")
+        o = torch.empty(len(keep), dtype=torch.uint8, device="cuda:0")
+        best = 1e9
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            snap.check_batch_device(sub.data_ptr(), len(keep), o.data_ptr(), 32, sp)
+            torch.cuda.synchronize()
+            best = min(best, (time.perf_counter() - t0) * 1e3)
+        full = snap.last_timing_full()
+        res[f"batch_without_top_{drop}"] = {"wall_ms": round(best, 3), "tier_ms": [round(x, 3) for x in full["tier_ms"]],
+                                            "items_ms": round(full["items_ms"], 3),
+                                            "longest_steps_left": int(steps[order[drop]])}
+        log(json.dumps(res[f"batch_without_top_{drop}"]))
     print(json.dumps(res), flush=True)
 
 
