@@ -175,6 +175,7 @@ def end_to_end(snap, q, a, d_out):
         log(f"end-to-end leg ({form}): {a.e2e_steps} batches of {n} through the host API (pinned buffers)")
         call()                                                     # warm-up (slots, staging)
         ts, walls, tiers = [], [], []
+        streamed = stalls = fallbacks = 0
         for _ in range(a.e2e_steps):
             t0 = time.perf_counter()
             call()
@@ -182,13 +183,19 @@ def end_to_end(snap, q, a, d_out):
             t = snap.last_timing_full()
             walls.append(t["wall_ms"])
             tiers.append(t["tier_ms"][0])
+            streamed += t["streamed"]
+            stalls += t["stream_stalls"]
+            fallbacks += t["stream_fallbacks"]
         ms = float(np.median(ts)) * 1e3
         pcie = n * (size + 1)
         legs[form] = {"value": round(n / (ms * 1e-3), 1), "unit": "checks/s", "ms_per_batch": round(ms, 3),
                       "library_wall_ms": round(float(np.median(walls)), 3),
                       "tier0_ms_sum": round(float(np.median(tiers)), 3), "chunks": t["chunks"],
                       "request_bytes": size, "pcie_bytes_per_batch": pcie,
-                      "pcie_GBps": round(pcie / (ms * 1e-3) / 1e9, 1)}
+                      "pcie_GBps": round(pcie / (ms * 1e-3) / 1e9, 1),
+                      # over the timed batches: decided by the one streamed launch; lanes whose chunk
+                      # wait hit KETO_STREAM_WAIT_MS; batches that fell back to the chunked pipeline
+                      "streamed_batches": streamed, "stream_wait_timeouts": stalls, "stream_fallbacks": fallbacks}
         outs.append(ho.array.copy())
     best = legs["pairs"]
     return {**best, "form": "keto_check_batch_pairs (8-B row-id requests, batch depth)", "rows_form": legs["rows"],

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 4
+#define KETO_ABI_VERSION 5
 
 /* return codes */
 #define KETO_OK 0
@@ -477,6 +477,9 @@ typedef struct {
     uint32_t items_kept;        /* deep batches: of them, checked after the reachability pretest */
     float index_ms;             /* deep batches: reverse / postings index (re)built for this snapshot version
                                    before the batch (host threads + upload; 0 when it was current) */
+    uint32_t streamed;          /* pair batches from pinned memory: 1 = decided by the one streamed launch */
+    uint32_t stream_stalls;     /* of the streamed launch: lanes whose wait for a chunk hit KETO_STREAM_WAIT_MS */
+    uint32_t stream_fallbacks;  /* 1 = the streamed launch gave up (a stall) and the chunked pipeline decided */
 } keto_batch_timing;
 int keto_last_batch_timing(const keto_snapshot* s, keto_batch_timing* out);
 

@@ -131,7 +131,8 @@ class KTiming(C.Structure):
     _fields_ = [("tier_ms", C.c_float * 3), ("requests", C.c_uint32 * 3), ("undecided", C.c_uint32),
                 ("chunks", C.c_uint32), ("wall_ms", C.c_float), ("resolve_ms", C.c_float),
                 ("items_ms", C.c_float), ("items", C.c_uint32), ("items_kept", C.c_uint32),
-                ("index_ms", C.c_float)]
+                ("index_ms", C.c_float), ("streamed", C.c_uint32), ("stream_stalls", C.c_uint32),
+                ("stream_fallbacks", C.c_uint32)]
 
 
 class KPartStats(C.Structure):
@@ -601,7 +602,8 @@ class Snapshot:
         _check(self.lib.keto_last_batch_timing(self.h, C.byref(t)))
         return {"tier_ms": list(t.tier_ms), "requests": list(t.requests), "undecided": t.undecided,
                 "chunks": t.chunks, "wall_ms": t.wall_ms, "resolve_ms": t.resolve_ms,
-                "items_ms": t.items_ms, "items": t.items, "items_kept": t.items_kept, "index_ms": t.index_ms}
+                "items_ms": t.items_ms, "items": t.items, "items_kept": t.items_kept, "index_ms": t.index_ms,
+                "streamed": t.streamed, "stream_stalls": t.stream_stalls, "stream_fallbacks": t.stream_fallbacks}
 
     @staticmethod
     def check_kernel_name(global_max_depth=5) -> str:

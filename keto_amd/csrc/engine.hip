@@ -418,36 +418,51 @@ constexpr int LDS_VIDS = KETO_LDS_VIDS;
 constexpr int LDS_STRIDE = 256;          // lanes per block
 // A visited map of one lane: the first REG_VIDS ids in registers, the next LV in the lane's LDS
 // column, and only the ids beyond those in the lane's HBM table (started fresh on the first
-// overflow), so a test probes HBM only when a map has outgrown registers + LDS.
-template <int LV, class VT = Visited>
+// overflow), so a test probes HBM only when a map has outgrown registers + LDS.  A 64-bit filter of
+// hashed ids answers "new" for most tests of a small map with no scan; a scan reads the LDS slots
+// with independent loads (one LDS round trip, not one per slot).
+template <int LV, class VT = Visited, int RV = REG_VIDS>
 struct VisitedRS {
-    uint32_t r[REG_VIDS];
-    uint32_t n;          // ids held in r + lds; REG_VIDS + LV + 1 = the HBM table holds the rest
+    uint32_t r[RV > 0 ? RV : 1];
+    uint32_t n;          // ids held in r + lds; RV + LV + 1 = the HBM table holds the rest
+    uint32_t f0, f1;     // filter of the ids in r + lds: bit (vid * 0x9E3779B1) >> 26
     uint32_t* lds;       // this lane's LDS column (stride LDS_STRIDE), or nullptr
     VT V;
-    __device__ inline void fresh() { n = 0; }
+    __device__ inline void fresh() {
+        n = 0;
+        f0 = f1 = 0;
+    }
     template <class W>
     __device__ inline int test_add(uint32_t vid, W& w) {
         const uint32_t lcap = lds ? (uint32_t)LV : 0u;
         // a map past registers + LDS lives wholly in the table (its first ids were copied there at
         // the overflow), so a deep search's test is one table probe: the register compares and the
-        // serial LDS scan cost a long chain ~0.3 us per step (tools/dev/chain_probe.py)
-        if (n > (uint32_t)REG_VIDS + lcap) return V.test_add(vid, w);
-        const uint32_t m = min(n, (uint32_t)REG_VIDS + lcap);
-        bool hit = false;
+        // serial LDS scan cost a long chain ~0.5 us per step (tools/dev/chain_probe.py)
+        if (n > (uint32_t)RV + lcap) return V.test_add(vid, w);
+        const uint32_t b = (vid * 0x9E3779B1u) >> 26;
+        const uint32_t bit = 1u << (b & 31u);
+        if (((b < 32 ? f0 : f1) & bit) != 0) {             // the filter cannot rule vid out: scan
+            const uint32_t m = min(n, (uint32_t)RV + lcap);
+            bool hit = false;
 #pragma unroll
-        for (int i = 0; i < REG_VIDS; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
-        for (uint32_t i = REG_VIDS; i < m && !hit; ++i) hit = lds[(i - REG_VIDS) * LDS_STRIDE] == vid;
-        if (hit) return 1;
-        if (n < (uint32_t)REG_VIDS) {
+            for (int i = 0; i < RV; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
+            if (lcap) {
 #pragma unroll
-            for (int i = 0; i < REG_VIDS; ++i)
+                for (int i = 0; i < LV; ++i) hit |= ((uint32_t)(RV + i) < m) & (lds[i * LDS_STRIDE] == vid);
+            }
+            if (hit) return 1;
+        }
+        if (b < 32) f0 |= bit;
+        else f1 |= bit;
+        if (n < (uint32_t)RV) {
+#pragma unroll
+            for (int i = 0; i < RV; ++i)
                 if ((uint32_t)i == n) r[i] = vid;
             ++n;
             return 0;
         }
-        if (n < (uint32_t)REG_VIDS + lcap) {
-            lds[(n - REG_VIDS) * LDS_STRIDE] = vid;
+        if (n < (uint32_t)RV + lcap) {
+            lds[(n - RV) * LDS_STRIDE] = vid;
             ++n;
             return 0;
         }
@@ -455,7 +470,7 @@ struct VisitedRS {
         V.fresh();
         ++n;
 #pragma unroll
-        for (int i = 0; i < REG_VIDS; ++i)
+        for (int i = 0; i < RV; ++i)
             if (V.test_add(r[i], w) == 2) return 2;
         for (uint32_t i = 0; i < lcap; ++i)
             if (V.test_add(lds[i * LDS_STRIDE], w) == 2) return 2;
@@ -634,17 +649,23 @@ struct CheckStack<GlobalStack> {
 // the HBM visited probe are in flight together; edges are read a 16-B block at a time and saved
 // frames keep their block; the header bloom filter rules most absent ids out without the id table.
 // Only a subject set reached with remaining depth >= 2 is entered (engine.go:65-69,88-91).
+// check_kernel's visited map: KETO_CK_RV ids in registers, KETO_CK_LV in the lane's LDS column
+#ifndef KETO_CK_RV
+#define KETO_CK_RV REG_VIDS
+#endif
+#ifndef KETO_CK_LV
+#define KETO_CK_LV LDS_VIDS
+#endif
 template <class Stack, bool COUNT, int TIER>
 __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
                                                     uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
                                                     unsigned long long* __restrict__ work) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
-    __shared__ uint32_t lds_vis[(LDS_VIDS > 0 ? LDS_VIDS : 1) * LDS_STRIDE];
-    VisitedRS<LDS_VIDS, typename std::conditional<TIER == 2, DirectVisited,
-                                                  PromoVisited<TIER == 1>>::type> V;
-    V.n = 0;
-    V.lds = LDS_VIDS > 0 ? lds_vis + threadIdx.x : nullptr;
+    __shared__ uint32_t lds_vis[(KETO_CK_LV > 0 ? KETO_CK_LV : 1) * LDS_STRIDE];
+    VisitedRS<KETO_CK_LV, typename std::conditional<TIER == 2, DirectVisited, PromoVisited<TIER == 1>>::type, KETO_CK_RV> V;
+    V.fresh();
+    V.lds = KETO_CK_LV > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
@@ -1185,7 +1206,7 @@ __device__ __forceinline__ void
                 const uint32_t ck = j >> ta.chunk_log2;
                 if (ck >= known) {
                     if (!chunk_wait(ta.ready + ck, ta.wait_ticks)) {
-                        atomicOr(ta.stalled, 1u);
+                        atomicAdd(ta.stalled, 1u);                 // (counted: keto_batch_timing)
                         break;
                     }
                     known = ck + 1u;
@@ -2321,7 +2342,7 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
     __shared__ uint32_t lds_pf[256];                          // the waves' prefetch scratch (never read)
     __shared__ uint4 lds_fr[SM ? SM_FRAMES * LDS_STRIDE : 1];   // SM: the lane's saved frames
     VisitedRS<LV, Visited> V;
-    V.n = 0;
+    V.fresh();
     V.lds = LV > 0 ? lds_vis + threadIdx.x : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
     V.V.mask = ta.mask;
@@ -4394,6 +4415,7 @@ bool check_streamed(Snapshot& S, DeviceState& D, const keto_check_pair* reqs, ui
     HIP_OK(hipMemcpyAsync(allowed, D.st_dec, n, hipMemcpyDeviceToHost, D.stream));
     HIP_OK(hipStreamSynchronize(D.stream));
     HIP_OK(hipStreamSynchronize(D.copy_in));
+    D.last.stream_stalls = flags[1];
     if (flags[1]) return false;
     if (flags[0]) throw Error{KETO_E_INVALID, std::to_string(flags[0]) + " requests name root rows another part owns"};
     D.last.chunks = (uint32_t)chunks;
@@ -4423,9 +4445,13 @@ void device_check_host(Snapshot& S, const void* reqs_v, uint32_t n, int32_t gmd,
     if (form == FORM_PAIRS && stream_ok(S, n, gmd, ovh) && host_pinned(reqs) && host_pinned(allowed)) {
         if (check_streamed(S, D, reinterpret_cast<const keto_check_pair*>(reqs), n, gmd, allowed, pair_depth)) {
             D.last.wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+            D.last.streamed = 1;
             return;
         }
+        const uint32_t stalls = D.last.stream_stalls;
         D.last = keto_batch_timing{};                    // a chunk did not land in time: the pipeline below
+        D.last.stream_stalls = stalls;
+        D.last.stream_fallbacks = 1;
     }
     OverlayBuf ov(S, ovh);
     const uint64_t C = std::min<uint64_t>(n, chunk_requests());

@@ -333,6 +333,10 @@ std::unique_ptr<Snapshot> load_snapshot(const char* path, uint64_t* tag_out) {
     if (fh.format != FORMAT)
         throw Error{KETO_E_INVALID, "snapshot file format " + std::to_string(fh.format) + " (this library reads " +
                                         std::to_string(FORMAT) + ")"};
+    // a file from a newer library may carry records this one lays out differently
+    if (fh.abi > (uint32_t)KETO_ABI_VERSION)
+        throw Error{KETO_E_INVALID, "snapshot file written by library ABI " + std::to_string(fh.abi) + " (this is " +
+                                        std::to_string(KETO_ABI_VERSION) + ")"};
     Reader rd{f.fd, th, (uint64_t)st.st_size};
 
     LoadClock clk;
@@ -455,6 +459,25 @@ std::unique_ptr<Snapshot> load_snapshot(const char* path, uint64_t* tag_out) {
             if (x != EDGE_POISON && ((x & EDGE_SET) ? (x & ~EDGE_SET) >= R : x >= n_str)) bad = true;
     }
     if (bad) throw Error{KETO_E_INVALID, "snapshot file: an edge names a row or string out of range"};
+    // the scalars and ids compute_layout and the kernels index with (a damaged or foreign file must
+    // fail here, not index out of range later)
+    if (S.page_size == 0 || S.n_wild_rows != S.wild_rows.size() || S.n_seq_rows > R || S.n_poisoned_rows > R ||
+        (S.empty_str != ANY && S.empty_str >= n_str))
+        throw Error{KETO_E_INVALID, "snapshot file: bad scalars"};
+    for (uint64_t r = 0; r < R; ++r) {
+        const RowKey& k = S.row_key[r];
+        if ((k.obj != ANY && k.obj >= n_str) || (k.rel != ANY && k.rel >= n_str))
+            throw Error{KETO_E_INVALID, "snapshot file: a row key names a string out of range"};
+    }
+    for (const auto& kv : S.coll) {
+        const uint32_t key = kv.first, v = kv.second;
+        const bool key_ok = (key & EDGE_SET) ? (key & ~EDGE_SET) < R : key < n_str;
+        if (!key_ok || !(v & VID_CLASS) || (v & ~VID_CLASS) >= std::max<uint64_t>(S.n_coll_keys, S.coll.size()))
+            throw Error{KETO_E_INVALID, "snapshot file: bad collision class"};
+    }
+    for (const auto& kv : S.added_str)
+        if (kv.second < S.n_sorted_strs || kv.second >= S.strs.size())
+            throw Error{KETO_E_INVALID, "snapshot file: an added string's id is out of range"};
     clk.lap("tables checked");
     if (tag_out) *tag_out = fh.tag;
     compute_layout(S);

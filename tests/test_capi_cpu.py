@@ -22,7 +22,7 @@ def test_exports_match_header():
 
 
 def test_abi_version():
-    assert keto_amd.load().keto_abi_version() == 4
+    assert keto_amd.load().keto_abi_version() == 5
 
 
 def test_host_snapshot_stats():

@@ -64,6 +64,7 @@ def test_streamed_matches_handle_form(graph, monkeypatch, n, depth, t0cap):
     q = _requests(g, n, seed=n % 97, depth=depth)
     out, t = _streamed(snap, q, depth)
     assert t["chunks"] == -(-n // 65536), t                         # the streamed path ran
+    assert t["streamed"] == 1 and t["stream_stalls"] == 0 and t["stream_fallbacks"] == 0, t
     want = _want(snap, q)
     assert (out == want).all(), f"{int((out != want).sum())} mismatches of {n}"
     ids = ((q["flags"] & 1) == 0) & (q["row"] != 0xFFFFFFFF)
@@ -85,6 +86,19 @@ def test_lost_chunk_mark_falls_back(graph, monkeypatch):
     q = _requests(g, 150_000, seed=7, depth=0)
     out, t = _streamed(snap, q, 0)
     assert t["chunks"] == 1, t                                       # the pipeline's one chunk
+    assert t["streamed"] == 0 and t["stream_fallbacks"] == 1 and t["stream_stalls"] >= 1, t   # counted
+    assert (out == _want(snap, q)).all()
+
+
+def test_default_geometry_never_stalls(graph, monkeypatch):
+    """The default streamed geometry (chunks of 2^20 pairs, 7/8 of the lanes, 1 s waits) on a batch of
+    several chunks: one streamed launch, no lane's chunk wait hits the limit, no fallback."""
+    g, snap = graph
+    monkeypatch.setenv("KETO_STREAM_MIN", "1")
+    q = _requests(g, 3 * (1 << 20) + 17, seed=11, depth=0)
+    for _ in range(3):
+        out, t = _streamed(snap, q, 0)
+        assert t["streamed"] == 1 and t["stream_stalls"] == 0 and t["stream_fallbacks"] == 0, t
     assert (out == _want(snap, q)).all()
 
 

@@ -304,3 +304,68 @@ def test_writes_staged_beside_readers_host():
     assert not errors, errors
     assert snap.version() == 300
     snap.close()
+
+
+def _mix64(x):
+    M = (1 << 64) - 1
+    x ^= x >> 30
+    x = (x * 0xBF58476D1CE4E5B9) & M
+    x ^= x >> 27
+    x = (x * 0x94D049BB133111EB) & M
+    return x ^ (x >> 31)
+
+
+def _section_hash(data: bytes) -> int:
+    """persist.cpp section_hash restated (1-MiB blocks, four lanes per 32 B, folded in order)."""
+    import struct
+    M = (1 << 64) - 1
+    B = 1 << 20
+    hs = []
+    for k in range(0, max(1, -(-len(data) // B))):
+        p = data[k * B:(k + 1) * B]
+        n = len(p)
+        h = (k ^ ((n * 0x9E3779B97F4A7C15) & M)) & M
+        i = 0
+        while i + 32 <= n:
+            a, b, c, d = struct.unpack_from("<4Q", p, i)
+            h = (_mix64(h ^ a) + _mix64(b ^ 0x632BE59BD9B4E019) + _mix64((c + h) & M) + _mix64(d ^ (h >> 17))) & M
+            i += 32
+        while i + 8 <= n:
+            h = _mix64(h ^ struct.unpack_from("<Q", p, i)[0])
+            i += 8
+        t = int.from_bytes(p[i:] + b"\0" * (8 - (n - i)), "little") if i < n else 0
+        hs.append(_mix64(h ^ t ^ 0xD6E8FEB86659FD93))
+    if not data:
+        hs = []
+    h = _mix64(len(data) + 1)
+    for x in hs:
+        h = (_mix64(h ^ x) * 0x94D049BB133111EB) & M
+    return h
+
+
+def test_crafted_files_refused(tmp_path):
+    """Files whose checksums are right but whose contents are not: the ABI field of a newer library,
+    and a scalars section (page_size 0, then an empty-string id past the string table) rewritten with
+    a recomputed section hash.  Both fail with KETO_E_INVALID before anything indexes with them
+    (persist.cpp trusted these fields)."""
+    import struct
+    import keto_amd
+    path = _small(tmp_path)
+    data = bytearray(path.read_bytes())
+    bad = tmp_path / "crafted.keto"
+    newer = bytearray(data)
+    struct.pack_into("<I", newer, 12, 99)                # the header's abi
+    bad.write_bytes(bytes(newer))
+    with pytest.raises(keto_amd.KetoError) as e:
+        keto_amd.Snapshot.load(bad, device=-1)
+    assert "ABI" in str(e.value)
+    sid, nbytes, h = struct.unpack_from("<3Q", data, 64)  # the first section: the scalars
+    assert sid == 1 and _section_hash(bytes(data[88:88 + nbytes])) == h   # the restated hash is the library's
+    for field, value in ((0, 0), (1, 0x7FFFFFF0)):       # page_size = 0; empty_str far past the strings
+        crafted = bytearray(data)
+        struct.pack_into("<I", crafted, 88 + 4 * field, value)
+        struct.pack_into("<Q", crafted, 64 + 16, _section_hash(bytes(crafted[88:88 + nbytes])))
+        bad.write_bytes(bytes(crafted))
+        with pytest.raises(keto_amd.KetoError) as e:
+            keto_amd.Snapshot.load(bad, device=-1)
+        assert e.value.code == -1 and "bad scalars" in str(e.value), e.value

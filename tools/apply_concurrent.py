@@ -7,6 +7,11 @@ the snapshot's shared lock (batches keep running) and commits it under the exclu
 waits for the running batch only to commit, and the next batch waits only for the commit.
 
   python tools/apply_concurrent.py [--k 100] [--gap-ms 20] [--seconds 5]
+  python tools/apply_concurrent.py --graph powerlaw1b --packed [--requests 1000000]
+
+--graph powerlaw1b: the headline graph (config #4, 1B tuples) with its string table (the bench's
+string_form snapshot, keto_snapshot_from_csr + strings); writes add and remove direct
+docs:<object>#view@<new user> tuples.  KETO_APPLY_TRACE=1 prints each write's device phases.
 """
 import argparse
 import json
@@ -33,14 +38,27 @@ def main():
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--packed", action="store_true",
                     help="reads through keto_check_batch_packed (GPU resolution, the Go batcher's call)")
+    ap.add_argument("--graph", choices=["drive10m", "powerlaw1b"], default="drive10m")
+    ap.add_argument("--requests", type=int, default=1_000_000)
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     from tools import synth
-    g = synth.SynthGraph(dict(synth.DRIVE_10M), threads=a.threads, kind="drive")
-    st = g.string_tuples(seed=11, threads=a.threads)
-    snap, t_build = g.snapshot_from_strings(st, device=0)
-    q = g.queries(1_000_000, seed=2, depth=5, threads=a.threads)
+    t0 = time.perf_counter()
+    if a.graph == "drive10m":
+        g = synth.SynthGraph(dict(synth.DRIVE_10M), threads=a.threads, kind="drive")
+        st = g.string_tuples(seed=11, threads=a.threads)
+        snap, t_build = g.snapshot_from_strings(st, device=0)
+        doc_ns, label = 1, "drive10m (config #2, built from string tuples)"
+    else:
+        g = synth.SynthGraph(dict(synth.POWERLAW_1B), threads=a.threads)
+        st = g.unified(threads=a.threads)
+        snap = g.snapshot_unified(st, device=0)
+        st = st.names
+        doc_ns, label = 1, "powerlaw1b (config #4, 1B tuples, snapshot with its string table)"
+    t_setup = time.perf_counter() - t0
+    print(f"[apply] {a.graph}: {g.n_edges} tuples ready in {t_setup:.1f} s", file=sys.stderr, flush=True)
+    q = g.queries(a.requests, seed=2, depth=5, threads=a.threads)
     reqs = g.string_requests(st, q, threads=a.threads)
     if a.packed:
         blob, packed, used = g.pack_requests(reqs, len(q), threads=a.threads)
@@ -52,7 +70,7 @@ def main():
             return snap.check_batch_reqs(reqs, len(q), 5)[0]
     before = batch().copy()
     hx = lambda v: f"{int(v):08x}"
-    files_view = np.flatnonzero((g.row_ns == 1) & (g.row_rel == 2))
+    files_view = np.flatnonzero((g.row_ns == doc_ns) & (g.row_rel == g.relation_names().index("view")))
     rng = np.random.default_rng(7)
 
     def reads(seconds, lat, bad):
@@ -71,7 +89,7 @@ def main():
     def writer():
         while not stop.is_set():
             rows = rng.choice(files_view, size=a.k, replace=False)
-            ins = [(1, hx(g.row_obj[r]), "view", f"uw{serial[0] + i:08x}") for i, r in enumerate(rows)]
+            ins = [(doc_ns, hx(g.row_obj[r]), "view", f"uw{serial[0] + i:08x}") for i, r in enumerate(rows)]
             serial[0] += a.k
             t0 = time.perf_counter()
             snap.apply(inserts=ins)
@@ -85,7 +103,7 @@ def main():
     reads(a.seconds, loaded, loaded_bad)
     stop.set()
     w.join()
-    out = {"graph": "drive10m (config #2, built from string tuples)", "tuples": int(g.n_edges),
+    out = {"graph": label, "tuples": int(g.n_edges), "setup_s": round(t_setup, 1),
            "reads": "keto_check_batch_packed (GPU resolution)" if a.packed else "keto_check_batch (host resolution)",
            "requests_per_batch": len(q), "write_tuples": a.k, "write_gap_ms": a.gap_ms,
            "batch_ms_quiet": {"p50": pct(quiet, 50), "p99": pct(quiet, 99), "n": len(quiet)},
