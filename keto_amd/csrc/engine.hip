@@ -1582,10 +1582,15 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         dyn_base = xs + lanes_x * r0;
         head = ta.heads + 32u * xcd;
     }
-    const bool packed = ((uintptr_t)allowed & 3u) == 0 && whole_groups;
+    const bool packed = ((uintptr_t)allowed & 3u) == 0 && whole_groups && (R & 3u) == 0;
     uint32_t acc = 0;
 
     uint32_t c = P_REQ;
+    // top-level items (reach.hip, ta.items): the request a work request belongs to (its other items
+    // stop when one is allowed, polled every 256 iterations), and "the next header is the item's own
+    // set", entered below the top level with a map that already holds it (engine.go:47-48)
+    uint32_t own = NONE32, poll = 0;
+    bool item_entry = false;
     uint32_t T = 0;
     uint32_t pos = 0, left = 0;
     uint4 win = make_uint4(0, 0, 0, 0);
@@ -1623,6 +1628,20 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
             eh = nq.x;
             if constexpr (COUNT) it = 0;
             c = P_HDR | ((uint32_t)d << D_K) | ((nq.z & 1u) ? D_TSET : 0u) | keep;
+            own = ta.item_owner ? ta.item_owner[qi] : NONE32;
+            poll = 0;
+            item_entry = ta.items && (nq.z & KETO_ITEM_FLAG);
+            if (item_entry) {
+                // the item's set, entered at its depth with the fresh map of its top-level tuple, which
+                // holds the set itself (its root is not ROW_SEQ: its visit id is its handle)
+                vfresh();
+                const uint32_t b = (eh * 0x9E3779B1u) >> 26;       // vtest's insert into a fresh map
+                if (b < 32) vf0 |= 1u << b;
+                else vf1 |= 1u << (b & 31u);
+                vr[0] = eh;
+                vn = 1;
+                w.item();
+            }
             return;
         }
         c = (c & ~7u) | P_REQ;
@@ -1716,7 +1735,13 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
         }
         int res = -1;
         const bool tset = (c & D_TSET) != 0;
-        if (ph == P_VIS) {
+        if (own != NONE32 && ++poll >= 256u) {
+            // another item of this request allowed it (engine.go:73-75 returns there): stop
+            poll = 0;
+            if (__hip_atomic_load(ta.item_acc + own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u) res = RES_FALSE;
+        }
+        if (res >= 0) {
+        } else if (ph == P_VIS) {
             // one probe of the HBM table: empty (another epoch) -> the id is new, insert it here
             w.vprobe();
             const uint64_t want = ((uint64_t)epoch << 32) | vv;
@@ -1776,7 +1801,8 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 const bool seq = (v0.z & HDR_SEQ) != 0;
                 const uint32_t hln = (v0.z >> 8) & 31u;
                 const uint32_t k = have ? bf(c, D_K, 7) - 1u : bf(c, D_K, 7);
-                const uint32_t fl = (have ? 0u : (uint32_t)FR_TOP) | (seq ? FR_SEQ : 0u) | (is_ov ? FR_OV : 0u) | FR_WV;
+                const uint32_t fl = (have || item_entry ? 0u : (uint32_t)FR_TOP) | (seq ? FR_SEQ : 0u) | (is_ov ? FR_OV : 0u) | FR_WV;
+                item_entry = false;
                 pos = (is_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS + HDR_WORDS;
                 left = v0.x;
                 win = v1;
@@ -1876,7 +1902,9 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
                 decide(qi, 0);
             } else {
                 decide(qi, (uint32_t)res);
+                if (res == RES_TRUE && own != NONE32) atomicOr(ta.item_acc + own, 1u);
             }
+            own = NONE32;
             start_next();
         }
     }
@@ -4135,7 +4163,9 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
                       // (a search holds at most gmd - 1 saved frames)
                       if ((uint64_t)t.gstack_n * 2 < (uint64_t)std::max(1, gmd - 1))
                           throw Error{KETO_E_RANGE, "deep frame area too small"};
-                      a.dyn = getenv("KETO_T0_DYN_FORCE") ? t0_dyn(n, slots) : 0u;
+                      // items (one long search can take 30K+ iterations): every work request dealt one at a
+                      // time by the XCD heads, so no lane holds two long searches back to back
+                      a.dyn = items ? 1u : getenv("KETO_T0_DYN_FORCE") ? t0_dyn(n, slots) : 0u;
                       if (a.dyn) {
                           if (!W.heads) {
                               uint64_t acc = 0;
@@ -4178,8 +4208,7 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
     const int32_t g = std::min<int32_t>(gmd, 65535);
     // (the reachability pretest's indexes keep handles in 31 bits: arenas whose roots lie past 2^31
     // units check deep batches without it)
-    const bool deep = n > 0 && g - 1 > 8 && !(deep_wave(g) && (uint64_t)D.n_units <= (1ull << 31)) &&
-                      S.part_mode != PART_MIGRATE && (uint64_t)D.n_units <= (uint64_t)EDGE_VAL;
+    const bool deep = n > 0 && g - 1 > 8 && S.part_mode != PART_MIGRATE && (uint64_t)D.n_units <= (uint64_t)EDGE_VAL;
     ItemWork iw;
     if (!deep || !reach_split(S, dq, n, gmd, da, dov.base, st, d_steps != nullptr, iw)) {
         check_core(S, D, dq, n, gmd, da, st, dov, work_out, accumulate, d_steps, stash, wsi, nullptr);
