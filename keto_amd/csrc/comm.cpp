@@ -570,6 +570,8 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* h, const keto_check_re
     });
 }
 
+void close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out);
+
 int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, uint32_t n,
                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
@@ -610,20 +612,28 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             route_rows(d_reqs, n, d_owner, Sp->n_rows(), c->rank, c->n, work, wb, d_send, d_order, cs.data(), c->stream);
             cnt.assign(cs.begin(), cs.end());
         });
-        // the counts to their owners, each with this rank's status: the exchange is the agreement
-        std::vector<uint64_t> cw(2ull * c->n);
+        // the counts to their owners, each with this rank's status and whether writes left this
+        // (migrating) part's closure filters stale: the exchange is the agreement
+        const uint64_t stale = mine.code == KETO_OK && Sp->part_mode == PART_MIGRATE && !Sp->mig_ready ? 1u : 0u;
+        std::vector<uint64_t> cw(3ull * c->n);
         for (int p = 0; p < c->n; ++p) {
-            cw[2 * p] = mine.code == KETO_OK ? cnt[p] : 0;
-            cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
+            cw[3 * p] = mine.code == KETO_OK ? cnt[p] : 0;
+            cw[3 * p + 1] = (uint64_t)(int64_t)mine.code;
+            cw[3 * p + 2] = stale;
         }
-        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
+        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 3, c->stream);
         std::vector<int64_t> codes(c->n);
         std::vector<uint64_t> in(c->n);
+        bool any_stale = false;
         for (int p = 0; p < c->n; ++p) {
-            in[p] = inw[2 * p];
-            codes[p] = (int64_t)inw[2 * p + 1];
+            in[p] = inw[3 * p];
+            codes[p] = (int64_t)inw[3 * p + 1];
+            any_stale |= inw[3 * p + 2] != 0;
         }
         settle(*c, mine, codes);
+        // a write lays a migrating part out afresh (its stubs' filters start empty): every rank saw the
+        // same flags, so all of them run the exchange again before the batch's records travel
+        if (any_stale) close_filters(c, h, nullptr);
         Snapshot& S = *Sp;
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
         keto_check_ids* d_recv = nullptr;
@@ -865,95 +875,103 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
     });
 }
 
+// A migrating partition's closure-filter exchange (collective; every rank calls it): rounds of
+// "ask each stub's owner for its filter, OR the answers in, re-close locally" until no filter changes
+// anywhere, then the signatures.  Used after the upload (keto_comm_close_filters) and again before a
+// routed batch when writes laid a part out afresh.
+void close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out) {
+    const int P = c->n;
+    Local mine;
+    Snapshot* Sp = nullptr;
+    std::vector<uint32_t> stubs;
+    std::vector<uint64_t> cnt(P, 0);
+    mine.run([&] {
+        if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        Sp = h->s.get();
+        if (Sp->part_mode != PART_MIGRATE || (int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
+            throw Error{KETO_E_INVALID, "not this rank's migrating part"};
+        // this part's stubs, grouped by owner; the owners learn once which of their rows to answer for
+        for (uint32_t r = 0; r < Sp->n_rows(); ++r)
+            if (!Sp->stub.empty() && Sp->stub[r]) stubs.push_back(r);
+        std::vector<std::vector<uint32_t>> by(P);
+        for (uint32_t r : stubs) by[Sp->root_owner(r, P)].push_back(r);
+        stubs.clear();
+        for (int p = 0; p < P; ++p) {
+            cnt[p] = by[p].size();
+            stubs.insert(stubs.end(), by[p].begin(), by[p].end());
+        }
+    });
+    std::vector<uint64_t> cw(2ull * P);
+    for (int p = 0; p < P; ++p) {
+        cw[2 * p] = mine.code == KETO_OK ? cnt[p] : 0;
+        cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
+    }
+    const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
+    std::vector<int64_t> codes(P);
+    std::vector<uint64_t> in(P);
+    for (int p = 0; p < P; ++p) {
+        in[p] = inw[2 * p];
+        codes[p] = (int64_t)inw[2 * p + 1];
+    }
+    settle(*c, mine, codes);
+    Snapshot& S = *Sp;
+    const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
+    uint32_t *d_stubs = nullptr, *d_asked = nullptr, *d_ans = nullptr, *d_got = nullptr;
+    std::vector<uint32_t> asked(m), ans(m * CF_WORDS), got(stubs.size() * CF_WORDS);
+    mine.run([&] {
+        d_stubs = c->a.get<uint32_t>(std::max<uint64_t>(stubs.size(), 1));
+        d_asked = c->b.get<uint32_t>(std::max<uint64_t>(m, 1));
+        d_ans = c->c.get<uint32_t>(std::max<uint64_t>(ans.size(), 1));
+        d_got = c->d.get<uint32_t>(std::max<uint64_t>(got.size(), 1));
+        HIP_OK(hipMemcpyAsync(d_stubs, stubs.data(), stubs.size() * 4, hipMemcpyHostToDevice, c->stream));
+    });
+    agree(*c, mine);
+    std::vector<uint64_t> sb(P), rb(P);
+    for (int p = 0; p < P; ++p) {
+        sb[p] = cnt[p] * 4;
+        rb[p] = in[p] * 4;
+    }
+    c->t->alltoallv(d_stubs, sb, d_asked, rb, c->stream);
+    HIP_OK(hipMemcpyAsync(asked.data(), d_asked, m * 4, hipMemcpyDeviceToHost, c->stream));
+    sync(*c);
+    for (int p = 0; p < P; ++p) {
+        sb[p] = in[p] * 4 * CF_WORDS;        // answers go back to the askers
+        rb[p] = cnt[p] * 4 * CF_WORDS;
+    }
+    uint64_t changed = 1;
+    uint32_t rounds = 0;
+    while (changed && rounds < 256) {
+        mine.run([&] {
+            injected(*c, "filters");
+            part_filters(S, asked.data(), m, ans.data());
+            HIP_OK(hipMemcpyAsync(d_ans, ans.data(), ans.size() * 4, hipMemcpyHostToDevice, c->stream));
+        });
+        agree(*c, mine);
+        c->t->alltoallv(d_ans, sb, d_got, rb, c->stream);
+        uint64_t mine_changed = 0;
+        mine.run([&] {
+            HIP_OK(hipMemcpyAsync(got.data(), d_got, got.size() * 4, hipMemcpyDeviceToHost, c->stream));
+            sync(*c);
+            mine_changed = part_close(S, stubs.data(), stubs.size(), got.data());
+        });
+        const std::vector<uint64_t> all = c->t->allgather_u64({(uint64_t)(int64_t)mine.code, mine_changed}, c->stream);
+        changed = 0;
+        for (int p = 0; p < P; ++p) {
+            codes[p] = (int64_t)all[2 * p];
+            changed += all[2 * p + 1];
+        }
+        settle(*c, mine, codes);
+        ++rounds;
+    }
+    part_closure_done(S, changed == 0);
+    if (rounds_out) *rounds_out = rounds;
+}
+
 int keto_comm_close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out) {
     return guarded([&] {
         if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
         HIP_OK(hipSetDevice(c->device));
-        const int P = c->n;
-        Local mine;
-        Snapshot* Sp = nullptr;
-        std::vector<uint32_t> stubs;
-        std::vector<uint64_t> cnt(P, 0);
-        mine.run([&] {
-            if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
-            Sp = h->s.get();
-            if (Sp->part_mode != PART_MIGRATE || (int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
-                throw Error{KETO_E_INVALID, "not this rank's migrating part"};
-            // this part's stubs, grouped by owner; the owners learn once which of their rows to answer for
-            for (uint32_t r = 0; r < Sp->n_rows(); ++r)
-                if (!Sp->stub.empty() && Sp->stub[r]) stubs.push_back(r);
-            std::vector<std::vector<uint32_t>> by(P);
-            for (uint32_t r : stubs) by[Sp->root_owner(r, P)].push_back(r);
-            stubs.clear();
-            for (int p = 0; p < P; ++p) {
-                cnt[p] = by[p].size();
-                stubs.insert(stubs.end(), by[p].begin(), by[p].end());
-            }
-        });
-        std::vector<uint64_t> cw(2ull * P);
-        for (int p = 0; p < P; ++p) {
-            cw[2 * p] = mine.code == KETO_OK ? cnt[p] : 0;
-            cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
-        }
-        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
-        std::vector<int64_t> codes(P);
-        std::vector<uint64_t> in(P);
-        for (int p = 0; p < P; ++p) {
-            in[p] = inw[2 * p];
-            codes[p] = (int64_t)inw[2 * p + 1];
-        }
-        settle(*c, mine, codes);
-        Snapshot& S = *Sp;
-        const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
-        uint32_t *d_stubs = nullptr, *d_asked = nullptr, *d_ans = nullptr, *d_got = nullptr;
-        std::vector<uint32_t> asked(m), ans(m * CF_WORDS), got(stubs.size() * CF_WORDS);
-        mine.run([&] {
-            d_stubs = c->a.get<uint32_t>(std::max<uint64_t>(stubs.size(), 1));
-            d_asked = c->b.get<uint32_t>(std::max<uint64_t>(m, 1));
-            d_ans = c->c.get<uint32_t>(std::max<uint64_t>(ans.size(), 1));
-            d_got = c->d.get<uint32_t>(std::max<uint64_t>(got.size(), 1));
-            HIP_OK(hipMemcpyAsync(d_stubs, stubs.data(), stubs.size() * 4, hipMemcpyHostToDevice, c->stream));
-        });
-        agree(*c, mine);
-        std::vector<uint64_t> sb(P), rb(P);
-        for (int p = 0; p < P; ++p) {
-            sb[p] = cnt[p] * 4;
-            rb[p] = in[p] * 4;
-        }
-        c->t->alltoallv(d_stubs, sb, d_asked, rb, c->stream);
-        HIP_OK(hipMemcpyAsync(asked.data(), d_asked, m * 4, hipMemcpyDeviceToHost, c->stream));
-        sync(*c);
-        for (int p = 0; p < P; ++p) {
-            sb[p] = in[p] * 4 * CF_WORDS;        // answers go back to the askers
-            rb[p] = cnt[p] * 4 * CF_WORDS;
-        }
-        uint64_t changed = 1;
-        uint32_t rounds = 0;
-        while (changed && rounds < 256) {
-            mine.run([&] {
-                injected(*c, "filters");
-                part_filters(S, asked.data(), m, ans.data());
-                HIP_OK(hipMemcpyAsync(d_ans, ans.data(), ans.size() * 4, hipMemcpyHostToDevice, c->stream));
-            });
-            agree(*c, mine);
-            c->t->alltoallv(d_ans, sb, d_got, rb, c->stream);
-            uint64_t mine_changed = 0;
-            mine.run([&] {
-                HIP_OK(hipMemcpyAsync(got.data(), d_got, got.size() * 4, hipMemcpyDeviceToHost, c->stream));
-                sync(*c);
-                mine_changed = part_close(S, stubs.data(), stubs.size(), got.data());
-            });
-            const std::vector<uint64_t> all = c->t->allgather_u64({(uint64_t)(int64_t)mine.code, mine_changed}, c->stream);
-            changed = 0;
-            for (int p = 0; p < P; ++p) {
-                codes[p] = (int64_t)all[2 * p];
-                changed += all[2 * p + 1];
-            }
-            settle(*c, mine, codes);
-            ++rounds;
-        }
-        part_closure_done(S, changed == 0);
-        if (rounds_out) *rounds_out = rounds;
+        close_filters(c, h, rounds_out);
         return KETO_OK;
     });
 }

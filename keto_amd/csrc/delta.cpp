@@ -259,11 +259,11 @@ std::string key_string(const Snapshot& S, const Txn& T, const RowKey& k) {     /
 
 void apply_writes(Snapshot& S, const keto_tuple* ins, uint64_t n_ins, const keto_tuple* del, uint64_t n_del,
                   const std::function<void()>& commit) {
-    // a shared-rows part holds the whole graph's host tables: every part applies every transaction
-    // and device_apply writes the rows this part holds; a migrating part's stubs carry their owners'
-    // filters and handles, which a local write cannot follow
-    if (S.part_mode == PART_MIGRATE)
-        throw Error{KETO_E_INVALID, "writes need a replicated snapshot or a shared-rows part (not a migrating part)"};
+    // a part of an edge-partitioned snapshot holds the whole graph's host tables: every part applies
+    // every transaction.  A shared-rows part writes the rows it holds in place (device_apply); a
+    // migrating part's stubs carry their owners' handles and filters, which a write on the owner can
+    // move, so device_apply lays the part out afresh from the host tables (every part computes every
+    // part's layout the same way) and the next routed batch exchanges the closure filters again
     if ((n_ins && !ins) || (n_del && !del)) throw Error{KETO_E_INVALID, "NULL tuples"};
     Txn T(S);
     // ---- inserts (commit order: after every equal tuple), then deletes (every equal tuple)

@@ -446,9 +446,12 @@ struct VisitedRS {
             bool hit = false;
 #pragma unroll
             for (int i = 0; i < RV; ++i) hit |= ((uint32_t)i < m) & (r[i] == vid);
-            if (lcap) {
+            // the LDS slots in groups of four independent loads (one LDS round trip per group), up to
+            // the map's size: a map of a few ids reads one group, not all LV slots
+            static_assert(LV % 4 == 0, "LDS slots come in groups of four");
+            for (uint32_t i0 = 0; lcap && (uint32_t)RV + i0 < m && !hit; i0 += 4) {
 #pragma unroll
-                for (int i = 0; i < LV; ++i) hit |= ((uint32_t)(RV + i) < m) & (lds[i * LDS_STRIDE] == vid);
+                for (uint32_t k = 0; k < 4; ++k) hit |= ((uint32_t)RV + i0 + k < m) & (lds[(i0 + k) * LDS_STRIDE] == vid);
             }
             if (hit) return 1;
         }
@@ -656,12 +659,6 @@ struct CheckStack<GlobalStack> {
 #ifndef KETO_CK_LV
 #define KETO_CK_LV LDS_VIDS
 #endif
-// deep tier 0: entering a child, start loading the parent's next sibling's header line and visited
-// bucket (global_load_lds into scratch: no register, no wait), so that when the child's subtree is
-// done the step that reaches the sibling finds both in the caches
-#ifndef KETO_CK_PF
-#define KETO_CK_PF 0
-#endif
 template <class Stack, bool COUNT, int TIER>
 __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q,
                                                     uint32_t n, int gmd, uint8_t* __restrict__ allowed, TierArgs ta,
@@ -669,7 +666,6 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     __shared__ uint32_t lds_vis[(KETO_CK_LV > 0 ? KETO_CK_LV : 1) * LDS_STRIDE];
-    __shared__ uint32_t lds_pf[KETO_CK_PF ? 256 : 1];            // prefetch scratch (never read)
     VisitedRS<KETO_CK_LV, typename std::conditional<TIER == 2, DirectVisited, PromoVisited<TIER == 1>>::type, KETO_CK_RV> V;
     V.fresh();
     V.lds = KETO_CK_LV > 0 ? lds_vis + threadIdx.x : nullptr;
@@ -904,22 +900,6 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
                     sv.fl = (blk_at == (cur.pos & ~3ull)) ? (uint16_t)(cur.fl | FR_WV) : (uint16_t)(cur.fl & ~FR_WV);
                     st.save(sp - 1, sv, blk);
                     w.push();
-#if KETO_CK_PF
-                    if constexpr (TIER == 0) {
-                        if ((sv.fl & FR_WV) && cur.k >= 2 && !(cur.fl & FR_SEQ)) {
-                            const uint32_t e2 = win_at(blk, (uint32_t)cur.pos & 3u);
-                            if (e2 & EDGE_SET) {
-                                const uint32_t c2 = e2 & EDGE_VAL;
-                                uint32_t* const pf = lds_pf + (threadIdx.x & ~63u);
-                                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(s.arena + (uint64_t)c2 * HDR_WORDS),
-                                                                 reinterpret_cast<void*>(pf), 4, 0, 0);
-                                if (V.n > (uint32_t)(KETO_CK_RV + KETO_CK_LV) && V.V.d < 0)
-                                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(V.V.tab + (mix32(c2) & V.V.mask & ~3u)),
-                                                                     reinterpret_cast<void*>(pf), 4, 0, 0);
-                            }
-                        }
-                    }
-#endif
                 }
                 cur = Frame{beg, n_sets, enter_k,
                             (uint16_t)(enter_fl | (seq ? FR_SEQ : 0) | (ea != s.arena ? FR_OV : 0))};
@@ -2456,16 +2436,24 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
 // The staged trees of the one-pass expand, copied to their offsets in the node arena: 16 lanes per
 // root (four roots per wave, grid-stride), whose position and offsets are loaded together (a tree
 // is ~37 nodes on average: a wave per root waited three dependent loads for one short copy).
+// unit_row != NULL: set nodes' row handles become row ids on the way (handles_to_rows_direct's
+// translation, fused: the translated staged trees need no pass of their own)
 __global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict__ nodes,
                                                      const keto_tree_node* __restrict__ stage,
                                                      const uint64_t* __restrict__ stage_pos,
-                                                     const uint64_t* __restrict__ offset, uint32_t n) {
+                                                     const uint64_t* __restrict__ offset, uint32_t n,
+                                                     const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
     const uint32_t gl = threadIdx.x & 15u;
     const uint32_t groups = gridDim.x * (blockDim.x >> 4);
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; i < n; i += groups) {
         const uint64_t sp = stage_pos[i], b = offset[i], e = offset[i + 1];
         if (sp == NOT_STAGED) continue;
-        for (uint64_t k = gl; k < e - b; k += 16) nodes[b + k] = stage[sp + k];
+        for (uint64_t k = gl; k < e - b; k += 16) {
+            keto_tree_node v = stage[sp + k];
+            if (unit_row && (v.subject & EDGE_SET) && (v.subject & EDGE_VAL) < ov_units_base)
+                v.subject = EDGE_SET | unit_row[v.subject & EDGE_VAL];
+            nodes[b + k] = v;
+        }
     }
 }
 
@@ -3546,7 +3534,9 @@ bool apply_in_place(Snapshot& S) {
 
 void device_apply(Snapshot& S) {
     if (!S.dev) return;
-    if (apply_in_place(S)) return;
+    // a migrating part (see apply_writes): its stubs name rows by their owners' handles, so it is laid
+    // out afresh and uploaded, its filters stale until the next routed batch's exchange
+    if (!(S.part_mode == PART_MIGRATE && S.n_parts > 1) && apply_in_place(S)) return;
     // a new subject-set target found no place below 2^31 units (the split layout's reserve is full,
     // or an unsplit arena's tail is past it): lay the arena out afresh, as a build would, and upload
     // it again (handles are per version)
@@ -4753,6 +4743,21 @@ __global__ void __launch_bounds__(256) handles_to_rows_direct(keto_tree_node* __
     if (h >= ov_units_base) return;
     nodes[i].subject = EDGE_SET | unit_row[h];
 }
+// the same over the trees a fill pass wrote at their offsets (ranges[2r], ranges[2r + 1] = first node,
+// end): a wave per range
+__global__ void __launch_bounds__(256) handles_to_rows_ranges(keto_tree_node* __restrict__ nodes,
+                                                              const uint64_t* __restrict__ ranges, uint32_t n_ranges,
+                                                              const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n_ranges; r += waves) {
+        const uint64_t b = ranges[2 * r], e = ranges[2 * r + 1];
+        for (uint64_t i = b + lane; i < e; i += 64) {
+            const uint32_t x = nodes[i].subject;
+            if ((x & EDGE_SET) && (x & EDGE_VAL) < ov_units_base) nodes[i].subject = EDGE_SET | unit_row[x & EDGE_VAL];
+        }
+    }
+}
 // arenas with root rows past 2^31 units: a tree's root node lost its handle's bit 31 to EDGE_SET, so
 // it takes its row from the request (overlay roots: the host, below)
 __global__ void __launch_bounds__(256) root_rows_of_trees(keto_tree_node* __restrict__ nodes, const uint64_t* __restrict__ off,
@@ -5128,15 +5133,38 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     }
     HIP_OK(hipEventRecord(D.ex_ev[2], st));
     if (unstaged) copy_queued();
+    // staged trees: copied to their offsets with their set handles turned into row ids on the way (16
+    // lanes per root, their map loads independent); the trees a fill pass wrote at their offsets get
+    // the translation over just their ranges.  (Round 3's fused version, a wave per tree, waited its
+    // lanes' map loads one after another: 2.5x slower than a pass of its own.)
+    const bool fuse = staged && D.unit_row;
     if (staged)
         hipLaunchKernelGGL(gather_staged, dim3(copy_blocks((n + 15) / 16)), dim3(256), 0, st,
-                           D.ex_nodes, D.ex_stage, dstage, doff, n);
+                           D.ex_nodes, D.ex_stage, dstage, doff, n, fuse ? D.unit_row : nullptr, (uint32_t)S.n_units);
     HIP_OK(hipGetLastError());
+    std::vector<uint64_t> rg;                          // (alive until the stream is synchronized below)
+    if (fuse && unstaged) {
+        for (uint32_t i = 0; i < n; ++i)
+            if (spos[i] == NOT_STAGED && out.offset[i + 1] > out.offset[i]) {
+                rg.push_back(out.offset[i]);
+                rg.push_back(out.offset[i + 1]);
+            }
+        // (the big-run queue is free once the copies above ran: the ranges go through it, in pieces
+        // that fit it; the copy of a piece waits for the kernel that read the last one)
+        uint64_t* d_rg = reinterpret_cast<uint64_t*>(D.ex_big);
+        const uint64_t per = std::max<uint64_t>(1, (uint64_t)D.ex_big_cap * sizeof(CopyRun) / 16);
+        for (uint64_t r0 = 0; r0 < rg.size() / 2; r0 += per) {
+            const uint32_t nr = (uint32_t)std::min<uint64_t>(per, rg.size() / 2 - r0);
+            HIP_OK(hipMemcpyAsync(d_rg, rg.data() + 2 * r0, (uint64_t)nr * 16, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(handles_to_rows_ranges, dim3(std::min<uint32_t>((nr + 3) / 4, 4096)), dim3(256), 0, st,
+                               D.ex_nodes, d_rg, nr, D.unit_row, (uint32_t)S.n_units);
+        }
+        HIP_OK(hipGetLastError());
+    }
     HIP_OK(hipEventRecord(D.ex_ev[3], st));
     lap("fill");
-    // set handles -> row ids, a thread per node (a wave-per-tree pass, fused with the gather, was 2.5x
-    // slower: its random gathers into the 4-B-per-unit map wait one after another per wave)
-    if (D.unit_row)
+    if (fuse) {
+    } else if (D.unit_row)
         hipLaunchKernelGGL(handles_to_rows_direct, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D.ex_nodes,
                            total, D.unit_row, (uint32_t)S.n_units);
     else

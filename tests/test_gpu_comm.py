@@ -341,6 +341,62 @@ def test_local_error_agreement_bad_arguments(powerlaw_strings):
 
 @pytest.mark.parametrize("P", [2, 3])
 @pytest.mark.parametrize("seed", range(4200, 4216))
+def test_local_migrating_parts_follow_writes(P, seed):
+    """Write transactions on a migrating partition (KETO_PART_MIGRATE): every part applies every
+    transaction to its host tables (the whole graph's) and is laid out afresh, since its stubs name
+    rows by their owners' handles; the next routed batch sees the stale filters on some rank and every
+    rank runs the closure-filter exchange again before the records travel.  After each write the
+    routed checks of every rank equal the SQL oracle's (relationtuples.go:128-149,200-223,
+    check/engine.go:36-123).  Wildcard queries no stored set uses are not routable on a migrating
+    partition (test_local_error_agreement_bad_arguments); expand is refused there."""
+    import random
+    from oracle.oracle_sql import SQLStore
+    from tests.randgraph import random_graph
+    from tests.test_gpu_lifecycle import _random_write, _row
+    import keto_amd
+    from keto_amd.capi import PART_MIGRATE
+    ns, tuples, raw, ps, alph = random_graph(seed, wide=seed % 4 == 3, allow_wildcards=seed % 3 == 0,
+                                             allow_poison=False, allow_collisions=seed % 2 == 0)
+    names, objs, rels, users = alph
+    set_names = list(names)
+    names = [n_ for n_ in names if n_]
+    if not names:
+        pytest.skip("only a namespace named ''")
+    store = SQLStore(ns, tuples, page_size=ps)
+    rows = rows_from_tuples(ns, tuples)
+    parts = [keto_amd.Snapshot.build(ns, rows, page_size=ps, device=-1).upload_part(r, P, 0, mode=PART_MIGRATE)
+             for r in range(P)]
+    comms = _local_comms(P)
+    _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+    rng = random.Random(seed)
+    g = 5
+    for step in range(5):
+        cur = store.tuples()
+        ins = [_random_write(rng, names, objs, rels, users, set_names, 0.1) for _ in range(rng.randint(1, 8))]
+        dels = [rng.choice(cur) for _ in range(rng.randint(0, 3))] if cur else []
+        for p in parts:
+            p.apply([_row(ns, t) for t in ins], [_row(ns, t) for t in dels])
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+        checks = random_checks(seed * 41 + step, (names, objs + ["new1", "a0"], rels + ["q"], users + ["w001"]), k=60)
+        reqs = [(t.namespace, t.object, t.relation, subj(t.subject), d) for t, d, _ in checks]
+        keep = [i for i, q in enumerate(reqs) if not _wild(q)]
+        mine = [keep[r::P] for r in range(P)]
+        res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], [reqs[i] for i in mine[r]], g)))
+        for r, (got, _) in enumerate(res):
+            for k, i in enumerate(mine[r]):
+                t, d, _ = checks[i]
+                assert bool(got[k]) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, step, r, t, d)
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("seed", range(4200, 4216))
 def test_local_shared_parts_follow_writes(P, seed):
     """Write transactions on an edge-partitioned snapshot (KETO_PART_SHARED): every part applies every
     transaction (its host tables are the whole graph's) and writes the rows it holds -- subject-set
