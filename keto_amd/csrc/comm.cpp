@@ -585,21 +585,9 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         keto_check_ids* d_send = nullptr;
         uint32_t* d_order = nullptr;
         uint64_t wb = 0;
-        mine.run([&] {
-            if (!h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-            Sp = h->s.get();
-            lk = std::shared_lock<std::shared_mutex>(Sp->rw);
-            if ((int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
-                throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
-                                            "part = rank and n_parts = ranks)"};
-            injected(*c, "resolve");
-            // names -> row ids (routing needs rows, not this part's handles)
-            std::vector<keto_check_ids> ids(std::max<uint32_t>(n, 1));
-            wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
-            if (!wild.empty() && Sp->part_mode == PART_MIGRATE)
-                throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
-                                                " is a wildcard query that no stored subject set uses: not "
-                                                "answered on a migrating partition"};
+        std::vector<keto_check_ids> ids;
+        // row-id requests to the device, grouped by owner (d_send, d_order); counts per part
+        auto route = [&] {
             keto_check_ids* d_reqs = c->a.get<keto_check_ids>(n);
             HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice,
                                   c->stream));
@@ -611,6 +599,23 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             std::vector<uint32_t> cs(c->n);
             route_rows(d_reqs, n, d_owner, Sp->n_rows(), c->rank, c->n, work, wb, d_send, d_order, cs.data(), c->stream);
             cnt.assign(cs.begin(), cs.end());
+        };
+        mine.run([&] {
+            if (!h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+            Sp = h->s.get();
+            lk = std::shared_lock<std::shared_mutex>(Sp->rw);
+            if ((int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
+                throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
+                                            "part = rank and n_parts = ranks)"};
+            injected(*c, "resolve");
+            // names -> row ids (routing needs rows, not this part's handles)
+            ids.resize(std::max<uint32_t>(n, 1));
+            wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
+            if (!wild.empty() && Sp->part_mode == PART_MIGRATE)
+                throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
+                                                " is a wildcard query that no stored subject set uses: not "
+                                                "answered on a migrating partition"};
+            route();
         });
         // the counts to their owners, each with this rank's status and whether writes left this
         // (migrating) part's closure filters stale: the exchange is the agreement
@@ -633,7 +638,11 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         settle(*c, mine, codes);
         // a write lays a migrating part out afresh (its stubs' filters start empty): every rank saw the
         // same flags, so all of them run the exchange again before the batch's records travel
-        if (any_stale) close_filters(c, h, nullptr);
+        if (any_stale) {
+            close_filters(c, h, nullptr);
+            // the exchange used the communicator's scratch buffers: route again (same owners, same counts)
+            if (mine.code == KETO_OK) mine.run(route);
+        }
         Snapshot& S = *Sp;
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
         keto_check_ids* d_recv = nullptr;

@@ -5145,10 +5145,11 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     std::vector<uint64_t> rg;                          // (alive until the stream is synchronized below)
     if (fuse && unstaged) {
         for (uint32_t i = 0; i < n; ++i)
-            if (spos[i] == NOT_STAGED && out.offset[i + 1] > out.offset[i]) {
-                rg.push_back(out.offset[i]);
-                rg.push_back(out.offset[i + 1]);
-            }
+            if (spos[i] == NOT_STAGED)   // in pieces of at most 2048 nodes: a big tree is not one wave's
+                for (uint64_t b = out.offset[i]; b < out.offset[i + 1]; b += 2048) {
+                    rg.push_back(b);
+                    rg.push_back(std::min<uint64_t>(b + 2048, out.offset[i + 1]));
+                }
         // (the big-run queue is free once the copies above ran: the ranges go through it, in pieces
         // that fit it; the copy of a piece waits for the kernel that read the last one)
         uint64_t* d_rg = reinterpret_cast<uint64_t*>(D.ex_big);

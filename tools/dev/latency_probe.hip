@@ -264,6 +264,19 @@ int main(int argc, char** argv) {
 
     const std::string which = argc > 1 ? argv[1] : "all";
     const uint64_t GiB = 1ull << 30;
+    if (which == "busy") {
+        // the loaded regime only: does the allocation (page / fragment size) decide a miss's cost when
+        // every CU chases its own chains over the same footprint?
+        for (const char* how : {"malloc", "contig"})
+            for (uint64_t F : std::vector<uint64_t>{512ull << 20, 2 * GiB, 8 * GiB, 32 * GiB}) {
+                Buf b = alloc(F, how);
+                const std::string h(how);
+                run((h + " chase").c_str(), b, F, 0, 0, 0, 0, false, false);
+                run((h + " chase, chip busy").c_str(), b, F, 0, 0, 0, 0, true, false);
+                b.free();
+            }
+        return 0;
+    }
     const std::vector<uint64_t> sizes = {2ull << 20, 64ull << 20, 512ull << 20, 2 * GiB, 8 * GiB, 32 * GiB};
     for (const char* how : {"malloc", "contig", "frag"}) {
         if (which != "all" && which != how) continue;
