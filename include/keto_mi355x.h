@@ -454,7 +454,9 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* s, const keto_check_req
  * parts (KETO_PART_SHARED; this rank's part as above): every rank passes its own roots; a root row
  * another part owns is expanded on that part (one all-to-all of roots, one of trees), every other
  * root here, as keto_expand_batch does.  *out: one arena in request order, read with keto_tree_*
- * against this rank's snapshot.  Migrating parts: KETO_E_INVALID.  Errors are agreed as above. */
+ * against this rank's snapshot.  A migrating part (KETO_PART_MIGRATE) expands every root itself: the
+ * other parts' rows its trees reach are copied into the call's overlay from the host tables (which
+ * every part holds whole) in rounds of the count pass; nothing is routed.  Errors are agreed as above. */
 int keto_expand_batch_routed(keto_comm* c, keto_snapshot* s, const keto_expand_req* reqs, uint32_t n,
                              int32_t global_max_depth, keto_tree_arena** out);
 /* A migrating partition's closure-filter exchange, once after every rank uploaded its part (before

@@ -859,8 +859,8 @@ class Comm:
         return self._batch(self.lib.keto_check_batch_routed, snap, reqs, global_max_depth, n)
 
     def expand_batch_routed(self, snap, reqs, global_max_depth=5, **kw):
-        """keto_expand_batch_routed (this rank's shared-rows part): reqs and results as in
-        Snapshot.expand_batch."""
+        """keto_expand_batch_routed (this rank's shared-rows or migrating part): reqs and results as
+        in Snapshot.expand_batch."""
         keep = _Keep()
         arr = snap._expand_reqs(keep, reqs)
         a = C.c_void_p()

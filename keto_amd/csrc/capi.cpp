@@ -869,6 +869,7 @@ void expand_named(Snapshot& S, const keto_expand_req* reqs, uint32_t n, int32_t 
     std::vector<uint32_t> root(n), flags(n), vid(n, 0);
     std::vector<int32_t> depth(n);
     std::vector<uint8_t> not_found(n, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> remote;                  // (request, row) of other parts
     for (uint32_t i = 0; i < n; ++i) {
         const keto_subject& sj = reqs[i].subject;
         depth[i] = reqs[i].max_depth;
@@ -900,14 +901,20 @@ void expand_named(Snapshot& S, const keto_expand_req* reqs, uint32_t n, int32_t 
             std::string key = std::string(sv(sj.set_namespace)) + ":" + std::string(sv(sj.set_object)) + "#" +
                               std::string(sv(sj.set_relation));
             vid[i] = S.vid_of_key(key);
+        } else if (!S.present((uint32_t)r)) {
+            // another part's row: a migrating part copies it in (device_expand); a shared-rows part
+            // routes it to its owner (keto_expand_batch_routed) and never gets here with it
+            if (!(S.part_mode == PART_MIGRATE && S.n_parts > 1))
+                throw Error{KETO_E_INVALID, "expand root is owned by another part"};
+            remote.emplace_back(i, (uint32_t)r);
+            root[i] = KETO_NO_ROW;
         } else {
-            if (!S.present((uint32_t)r)) throw Error{KETO_E_INVALID, "expand root is owned by another part"};
             root[i] = S.handle((uint32_t)r);
             vid[i] = S.vid_of_row((uint32_t)r);
         }
     }
     a->ov_keys = ov.keys;
-    device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r);
+    device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r, &remote);
     for (uint32_t i = 0; i < n; ++i)
         if (not_found[i]) a->r.status[i] = KETO_EXPAND_NOT_FOUND;
 }

@@ -700,7 +700,8 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
 }
 
 // BuildTree (internal/expand/engine.go:33-102) for every rank's own roots over an edge-partitioned
-// snapshot of shared-rows parts.  A root whose row this part holds (a subject-set target, which
+// snapshot.  A migrating part expands all of them itself (device_expand copies the other parts' rows
+// a tree reaches into the call's overlay); on shared-rows parts:  A root whose row this part holds (a subject-set target, which
 // every part keeps, or one of this part's own root rows), a subject id, an unknown namespace, a
 // missing row or a wildcard query is expanded here, exactly as keto_expand_batch does it.  A root
 // row another part owns goes there as one word (row id, max depth); the owner expands it -- every
@@ -729,11 +730,13 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
             if ((int)Sp->n_parts != P || (int)Sp->part != c->rank)
                 throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
                                             "part = rank and n_parts = ranks)"};
-            if (P > 1 && Sp->part_mode != PART_SHARED)
-                throw Error{KETO_E_INVALID, "expand needs shared-rows parts (KETO_PART_SHARED)"};
             injected(*c, "resolve");
             const Snapshot& S = *Sp;
-            for (uint32_t i = 0; i < n; ++i) {
+            // a migrating part expands every root itself (device_expand copies the other parts' rows
+            // a tree needs from the host tables, which every part holds whole): nothing is routed,
+            // and the exchanges below carry only the agreement
+            const bool migrating = Sp->part_mode == PART_MIGRATE;
+            for (uint32_t i = 0; i < n && !migrating; ++i) {
                 const keto_subject& sj = reqs[i].subject;
                 if (sj.kind != 1) continue;
                 const int64_t r = S.resolve_query(std::string_view(sj.set_namespace.p ? sj.set_namespace.p : "", sj.set_namespace.n),

@@ -32,6 +32,7 @@
 #include <mutex>
 #include <new>
 #include <unordered_map>
+#include <unordered_set>
 #include <thread>
 #include <vector>
 
@@ -57,6 +58,9 @@ namespace keto {
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr int RES_FALSE = 0, RES_TRUE = 1, RES_OVERFLOW = 2;
 constexpr int EXP_TREE = 0, EXP_NIL = 1, EXP_ERROR = 2, EXP_OVERFLOW = 3;
+// (internal) the walk met a row another part owns with no copy in the call's overlay yet: the
+// migrating part copies the rows it recorded and runs the count pass again
+constexpr int EXP_RETRY = 4;
 
 struct DevSnap {
     const uint32_t* arena;    // main arena (u32 words; tier 0 adds 2^32 words for segment 1)
@@ -68,6 +72,11 @@ struct DevSnap {
 struct DevOverlay {           // batch-local wildcard rows (top-level / root only)
     const uint32_t* arena;
     uint32_t base;            // handles >= base live in this arena (unit = handle - base)
+    // expand on a migrating part: rows another part owns, copied into this arena for the call.  A
+    // stub (HDR_REMOTE) is looked up here by its handle -> the handle of its copy (key << 32 | value,
+    // ~0 = empty); NULL = no copies
+    const uint64_t* rmap = nullptr;
+    uint32_t rmask = 0;
 };
 
 __host__ __device__ inline uint32_t mix32(uint32_t k) {
@@ -77,6 +86,17 @@ __host__ __device__ inline uint32_t mix32(uint32_t k) {
     k *= 0x846ca68bU;
     k ^= k >> 16;
     return k;
+}
+// the copy of a remote row (rmap), or NONE32
+__device__ inline uint32_t rmap_find(const DevOverlay& ov, uint32_t h) {
+    if (!ov.rmap) return 0xFFFFFFFFu;
+    uint32_t i = mix32(h) & ov.rmask;
+    for (;;) {
+        const uint64_t e = ov.rmap[i];
+        if (e == ~0ull) return 0xFFFFFFFFu;
+        if ((uint32_t)(e >> 32) == h) return (uint32_t)e;
+        i = (i + 1) & ov.rmask;
+    }
 }
 
 __device__ inline uint32_t coll_lookup(const DevSnap& s, uint32_t key) {
@@ -98,6 +118,7 @@ struct RowView {
     bool poison, poison0;     // some page / the first page fails toInternal (expand)
     bool seq;
     bool closure;             // a closure filter precedes the header (the id table precedes that)
+    bool remote = false;      // a stub: the row lives on another part (migrating partition)
 };
 
 __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint32_t h) {
@@ -123,6 +144,7 @@ __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint3
     rv.poison = (v.z & HDR_POISON) != 0;
     rv.poison0 = (v.z & HDR_POISON0) != 0;
     rv.closure = (v.z & HDR_CLOSURE) != 0;
+    rv.remote = (v.z & HDR_REMOTE) != 0;
     return rv;
 }
 
@@ -421,12 +443,12 @@ constexpr int LDS_STRIDE = 256;          // lanes per block
 // overflow), so a test probes HBM only when a map has outgrown registers + LDS.  A 64-bit filter of
 // hashed ids answers "new" for most tests of a small map with no scan; a scan reads the LDS slots
 // with independent loads (one LDS round trip, not one per slot).
-template <int LV, class VT = Visited, int RV = REG_VIDS>
+template <int LV, class VT = Visited, int RV = REG_VIDS, int STRIDE = LDS_STRIDE>
 struct VisitedRS {
     uint32_t r[RV > 0 ? RV : 1];
     uint32_t n;          // ids held in r + lds; RV + LV + 1 = the HBM table holds the rest
     uint32_t f0, f1;     // filter of the ids in r + lds: bit (vid * 0x9E3779B1) >> 26
-    uint32_t* lds;       // this lane's LDS column (stride LDS_STRIDE), or nullptr
+    uint32_t* lds;       // this lane's LDS column (stride STRIDE), or nullptr
     VT V;
     __device__ inline void fresh() {
         n = 0;
@@ -451,7 +473,7 @@ struct VisitedRS {
             static_assert(LV % 4 == 0, "LDS slots come in groups of four");
             for (uint32_t i0 = 0; lcap && (uint32_t)RV + i0 < m && !hit; i0 += 4) {
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) hit |= ((uint32_t)RV + i0 + k < m) & (lds[(i0 + k) * LDS_STRIDE] == vid);
+                for (uint32_t k = 0; k < 4; ++k) hit |= ((uint32_t)RV + i0 + k < m) & (lds[(i0 + k) * STRIDE] == vid);
             }
             if (hit) return 1;
         }
@@ -465,7 +487,7 @@ struct VisitedRS {
             return 0;
         }
         if (n < (uint32_t)RV + lcap) {
-            lds[(n - RV) * LDS_STRIDE] = vid;
+            lds[(n - RV) * STRIDE] = vid;
             ++n;
             return 0;
         }
@@ -476,7 +498,7 @@ struct VisitedRS {
         for (int i = 0; i < RV; ++i)
             if (V.test_add(r[i], w) == 2) return 2;
         for (uint32_t i = 0; i < lcap; ++i)
-            if (V.test_add(lds[i * LDS_STRIDE], w) == 2) return 2;
+            if (V.test_add(lds[i * STRIDE], w) == 2) return 2;
         return V.test_add(vid, w);
     }
 };
@@ -1953,6 +1975,15 @@ struct ExpandOut {
     keto_tree_node* stage;
     uint64_t stage_cap;
     uint64_t* stage_pos;
+    // a tree that outgrows its lane's region goes on in an overflow chunk (ovf_chunk nodes taken from
+    // the pool at stage + ovf_base, *ovf_used of ovf_cap taken so far): its first split_at nodes stay
+    // in the region, the rest follow in the chunk, and segs[k] records both (stage_pos = SPLIT_POS | k).
+    // ovf_used = NULL: no overflow chunks (the tree is counted only and filled by the second pass)
+    unsigned long long* ovf_used;
+    uint64_t ovf_base, ovf_cap, ovf_chunk;
+    struct StageSeg* segs;
+    uint32_t* seg_n;
+    uint32_t seg_cap;
     // the snapshot has no poisoned row: a subject set at remaining depth <= 1 is a leaf whatever its
     // row holds (engine.go:72-75; only a failing first page would make it an error), so its row is
     // not loaded
@@ -1965,10 +1996,32 @@ struct ExpandOut {
     uint32_t edge_blocks;
     // tooling (KETO_EXPAND_CLOCKS=1): each root's walk time in wall-clock ticks (100 MHz), or NULL
     uint32_t* clocks;
+    // expand on a migrating part: the handles of rows another part owns that a walk met without a
+    // copy in the overlay (miss_cap entries, *n_miss recorded; the walk returns EXP_RETRY)
+    uint32_t* miss = nullptr;
+    uint32_t* n_miss = nullptr;
+    uint32_t miss_cap = 0;
 };
+__device__ inline void record_miss(const ExpandOut& o, uint32_t h) {
+    if (!o.n_miss) return;
+    const uint32_t at = atomicAdd(o.n_miss, 1u);
+    if (at < o.miss_cap) o.miss[at] = h;
+}
 // expand kernel modes: count the trees' nodes; write them at their offsets; write them to staging
 constexpr int EXP_COUNT = 0, EXP_FILL = 1, EXP_STAGE = 2;
 constexpr uint64_t NOT_STAGED = ~0ull;
+constexpr uint64_t SPLIT_POS = 1ull << 62;     // stage_pos of a tree staged in two pieces: | its StageSeg
+constexpr uint64_t NO_SPLIT = ~0ull;
+// a staged tree in two pieces: nodes [0, split_at) at region, the rest at chunk (stage positions)
+struct StageSeg {
+    uint64_t region, chunk, split_at;
+    uint32_t root, pad;
+};
+// a tree's overflow chunk while it is staged (expand_sm)
+struct SplitState {
+    uint64_t split_at = NO_SPLIT, chunk = 0;
+    bool tried = false;
+};
 
 // cnt < cap: the node is written (cap = ~0 in a fill pass; a staged tree past its region is only
 // counted, and filled again later)
@@ -2006,29 +2059,43 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
     uint4 blk = make_uint4(0, 0, 0, 0);
     uint64_t blk_at = ~0ull;
     // "open" a subject set at remaining depth k: NIL / ERROR / leaf written / union entered
+    bool retry = false;
     auto open = [&](uint32_t h, int k) -> int {
         RowView rv;
         uint4 w4 = make_uint4(0, 0, 0, 0);
-        if (h >= ov.base) {
-            rv = load_row(s, ov, h);
-        } else {
-            uint64_t w = (uint64_t)h * HDR_WORDS;
-            uint4 v = *reinterpret_cast<const uint4*>(s.arena + w);
-            w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
-            while (v.z & HDR_FWD) {                         // a row a write moved (delta.cpp)
-                w = (uint64_t)v.x * HDR_WORDS;
-                v = *reinterpret_cast<const uint4*>(s.arena + w);
+        // h names the set; hl is where its row is read: another part's row (a stub, migrating
+        // partition) is read from its copy in the call's overlay, or recorded as missing
+        uint32_t hl = h;
+        for (int hop = 0;; ++hop) {
+            if (hl >= ov.base) {
+                rv = load_row(s, ov, hl);
+            } else {
+                uint64_t w = (uint64_t)hl * HDR_WORDS;
+                uint4 v = *reinterpret_cast<const uint4*>(s.arena + w);
                 w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
+                while (v.z & HDR_FWD) {                     // a row a write moved (delta.cpp)
+                    w = (uint64_t)v.x * HDR_WORDS;
+                    v = *reinterpret_cast<const uint4*>(s.arena + w);
+                    w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
+                }
+                rv.a = s.arena;
+                rv.beg = w + HDR_WORDS;
+                rv.n_sets = v.x;
+                rv.n_ids = v.y;
+                rv.seq = (v.z & HDR_SEQ) != 0;
+                rv.hlog2 = (v.z >> 8) & 31u;
+                rv.poison = (v.z & HDR_POISON) != 0;
+                rv.poison0 = (v.z & HDR_POISON0) != 0;
+                rv.closure = (v.z & HDR_CLOSURE) != 0;
+                rv.remote = (v.z & HDR_REMOTE) != 0;
             }
-            rv.a = s.arena;
-            rv.beg = w + HDR_WORDS;
-            rv.n_sets = v.x;
-            rv.n_ids = v.y;
-            rv.seq = (v.z & HDR_SEQ) != 0;
-            rv.hlog2 = (v.z >> 8) & 31u;
-            rv.poison = (v.z & HDR_POISON) != 0;
-            rv.poison0 = (v.z & HDR_POISON0) != 0;
-            rv.closure = (v.z & HDR_CLOSURE) != 0;
+            if (!rv.remote) break;
+            const uint32_t to = rmap_find(ov, hl);
+            if (to == NONE32 || to == hl || hop > 1) {
+                record_miss(o, hl);
+                return EXP_RETRY;
+            }
+            hl = to;
         }
         const uint32_t n_all = rv.n_sets + rv.n_ids;
         if (!rv.poison && n_all == 0) return EXP_NIL;
@@ -2158,10 +2225,11 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             continue;
         }
         int r = open(c, k);
-        if (r == EXP_NIL) emit(out, cnt, FILL, cap, e, 0x80000000u);
+        if (r == EXP_RETRY) retry = true;                   // (a leaf for now: the walk goes on)
+        if (r == EXP_NIL || r == EXP_RETRY) emit(out, cnt, FILL, cap, e, 0x80000000u);
         else if (r != EXP_TREE) return r;
     }
-    return EXP_TREE;
+    return retry ? EXP_RETRY : EXP_TREE;
 }
 
 // The same walk as expand_one, restructured like the tier-0 check kernel (round 4): each loop
@@ -2180,12 +2248,30 @@ struct SmFrames {};
 constexpr int SM_FRAMES = 8;
 constexpr int SM_LDS_VIDS = 24;
 
-template <bool FILL, class VT>
+template <bool FILL, int COLS, class VT>
 __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, uint32_t root_flags,
-                         uint32_t root_vid, int d, VT& V, keto_tree_node* out, uint64_t& cnt, uint64_t cap,
+                         uint32_t root_vid, int d, VT& V, keto_tree_node*& out, uint64_t& cnt, uint64_t& cap,
                          uint4* frames, const ExpandOut& o, uint32_t& nr, uint64_t& qend, uint32_t* pf_lds,
-                         uint32_t& iters) {
+                         uint32_t& iters, SplitState& sg) {
+    // k more nodes past the staging region: go on in an overflow chunk (once per tree; out is then
+    // based so that out + cnt is the chunk's first node)
+    auto room = [&](uint64_t k) {
+        if constexpr (FILL) {
+            if (cnt + k > cap && o.ovf_used && !sg.tried) {
+                sg.tried = true;
+                const uint64_t at = atomicAdd(o.ovf_used, (unsigned long long)o.ovf_chunk);
+                if (at + o.ovf_chunk <= o.ovf_cap && k <= o.ovf_chunk) {
+                    sg.split_at = cnt;
+                    sg.chunk = o.ovf_base + at;
+                    out = reinterpret_cast<keto_tree_node*>(reinterpret_cast<uintptr_t>(o.stage + sg.chunk) -
+                                                            cnt * sizeof(keto_tree_node));
+                    cap = cnt + o.ovf_chunk;
+                }
+            }
+        }
+    };
     if (!(root_flags & 1u)) {                               // SubjectID -> Leaf (:97-101)
+        room(1);
         emit(out, cnt, FILL, cap, root, 0x80000000u);
         return EXP_TREE;
     }
@@ -2199,7 +2285,7 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
     uint64_t wbeg = ~0ull, blk_at = ~0ull;
     // the pending open: identity handle oh (what its node names), the handle its header is read at
     // (ol: a forward moves it), remaining depth od, and its edge in the parent (oe; NONE32 = the root)
-    bool opening = true;
+    bool opening = true, retry = false;
     uint32_t oh = root, ol = root, oe = NONE32;
     int od = d;
     for (;;) {
@@ -2222,25 +2308,44 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
                 ol = v.x;
                 continue;
             }
+            if (v.z & HDR_REMOTE) {                         // another part's row (migrating partition)
+                const uint32_t to = rmap_find(ov, ol);
+                if (to != NONE32 && to != ol) {             // its copy in the call's overlay
+                    ol = to;
+                    continue;
+                }
+                // no copy yet: recorded, and the walk goes on past it (a leaf for now) to find the
+                // tree's other missing rows in this round; the tree is counted again next round
+                record_miss(o, ol);
+                if (oe == NONE32) return EXP_RETRY;
+                retry = true;
+                opening = false;
+                room(1);
+                emit(out, cnt, FILL, cap, oe, 0x80000000u);
+                goto walk;
+            }
             opening = false;
             const uint32_t n_all = v.x + v.y;
             const bool poison = (v.z & HDR_POISON) != 0, poison0 = (v.z & HDR_POISON0) != 0;
             if (!poison && n_all == 0) {                    // nil (:68-70)
                 if (oe == NONE32) return EXP_NIL;
+                room(1);
                 emit(out, cnt, FILL, cap, oe, 0x80000000u);     // a nil child -> Leaf(set)
             } else if (poison0) {
                 return EXP_ERROR;                           // the first page fails toInternal
             } else if (od <= 1) {                           // :72-75
+                room(1);
                 emit(out, cnt, FILL, cap, EDGE_SET | oh, 0x80000000u);
             } else if (poison) {
                 return EXP_ERROR;                           // a later page fails
             } else {                                        // a union: enter it
                 if (cur.left > 0) {
                     if (sp == SM_FRAMES) return EXP_OVERFLOW;
-                    frames[sp * LDS_STRIDE] = make_uint4((uint32_t)cur.pos, (uint32_t)(cur.pos >> 32), cur.left,
+                    frames[sp * COLS] = make_uint4((uint32_t)cur.pos, (uint32_t)(cur.pos >> 32), cur.left,
                                                          (uint32_t)cur.k | ((uint32_t)cur.fl << 16));
                     ++sp;
                 }
+                room(1);
                 emit(out, cnt, FILL, cap, EDGE_SET | oh, n_all);
                 const uint64_t beg = hw + HDR_WORDS;
                 cur = Frame{beg, n_all, (uint16_t)od, (uint16_t)(((v.z & HDR_SEQ) ? FR_SEQ : 0) | (in_ov ? FR_OV : 0))};
@@ -2260,11 +2365,12 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
             }
         }
         // ---- walk until the next access is needed
+    walk:
         for (;;) {
             if (cur.left == 0) {
-                if (sp == 0) return EXP_TREE;
+                if (sp == 0) return retry ? EXP_RETRY : EXP_TREE;
                 --sp;
-                const uint4 f = frames[sp * LDS_STRIDE];
+                const uint4 f = frames[sp * COLS];
                 cur = Frame{(uint64_t)f.x | ((uint64_t)f.y << 32), f.z, (uint16_t)(f.w & 0xFFFFu), (uint16_t)(f.w >> 16)};
                 wbeg = ~0ull;
                 blk_at = ~0ull;
@@ -2279,6 +2385,7 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
             if (!(e & EDGE_SET) && !(cur.fl & FR_SEQ)) {
                 // the rest of a normal row are subject ids, all leaves: queued (or copied) at once
                 if constexpr (FILL) {
+                    room(cur.left);
                     if (cnt + cur.left <= cap) {
                         bool queued = false;
                         if (cur.left > o.run_inline && o.runs) {
@@ -2327,6 +2434,7 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
             cur.pos++;
             cur.left--;
             if (!(e & EDGE_SET)) {
+                room(1);
                 emit(out, cnt, FILL, cap, e, 0x80000000u);     // subject id child -> Leaf
                 continue;
             }
@@ -2340,6 +2448,7 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
             const int t = V.test_add(vid, nw);
             if (t == 2) return EXP_OVERFLOW;
             if (t == 1 || (k <= 1 && o.leaf_sets_blind)) {  // visited -> nil -> Leaf(set); or :72-75
+                room(1);
                 emit(out, cnt, FILL, cap, e, 0x80000000u);
                 continue;
             }
@@ -2359,22 +2468,30 @@ struct ExpandReq {
     int32_t depth;
 };
 
-template <int MODE, class Stack>
+// SPREAD > 1 (tier 0 of expand_sm, KETO_EXPAND_SPREAD): only 64 / SPREAD lanes of each wave walk a
+// tree, the rest exit at once, and the block's LDS columns are its active lanes' (256 / SPREAD): a
+// wave's instruction stream is the union of fewer lanes' paths, and with less LDS per block more
+// waves are resident to interleave their issue
+template <int MODE, class Stack, int SPREAD = 1>
 __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, const ExpandReq* __restrict__ q,
                                                      uint32_t n, int gmd, ExpandOut o, TierArgs ta) {
     constexpr bool FILL = MODE != EXP_COUNT, STAGE = MODE == EXP_STAGE;
     constexpr bool SM = std::is_same<Stack, SmFrames>::value;  // expand_sm (saved frames in LDS)
     constexpr int LV = SM ? SM_LDS_VIDS : LDS_VIDS;
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t stride = gridDim.x * blockDim.x;
+    constexpr int ACT = 64 / SPREAD, COLS = 256 / SPREAD;     // active lanes per wave, per block
+    static_assert(SPREAD == 1 || SM, "spread lanes: expand_sm only");
+    if (SPREAD > 1 && (threadIdx.x & 63u) >= (uint32_t)ACT) return;
+    const uint32_t col = SPREAD > 1 ? (threadIdx.x >> 6) * ACT + (threadIdx.x & 63u) : threadIdx.x;
+    const uint32_t slot = blockIdx.x * COLS + col;
+    const uint32_t stride = gridDim.x * COLS;
     // a tree's map: its first REG_VIDS + LV sets in registers and the lane's LDS column (one
     // tree at max-depth 5 marks a handful of sets), the rest in the lane's HBM table
-    __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
+    __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * COLS];
     __shared__ uint32_t lds_pf[256];                          // the waves' prefetch scratch (never read)
-    __shared__ uint4 lds_fr[SM ? SM_FRAMES * LDS_STRIDE : 1];   // SM: the lane's saved frames
-    VisitedRS<LV, Visited> V;
+    __shared__ uint4 lds_fr[SM ? SM_FRAMES * COLS : 1];       // SM: the lane's saved frames
+    VisitedRS<LV, Visited, REG_VIDS, COLS> V;
     V.fresh();
-    V.lds = LV > 0 ? lds_vis + threadIdx.x : nullptr;
+    V.lds = LV > 0 ? lds_vis + col : nullptr;
     V.V.tab = ta.vtab + (uint64_t)slot * (ta.mask + 1u);
     V.V.mask = ta.mask;
     V.V.epoch = ta.slot_epoch[slot];
@@ -2398,14 +2515,15 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
         if (d <= 0 || gmd < d) d = gmd;
         uint64_t cnt = 0;
         keto_tree_node* out = !FILL ? nullptr : STAGE ? o.stage + stage0 + used : o.nodes + o.offset[i];
-        const uint64_t cap = STAGE ? o.stage_cap - used : ~0ull;
+        uint64_t cap = STAGE ? o.stage_cap - used : ~0ull;
+        SplitState sg;
         uint64_t qend = 0;
         const uint64_t t_tree = o.clocks ? wall_clock64() : 0;
         int r;
         uint32_t iters = 0;
         if constexpr (SM)
-            r = expand_sm<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, lds_fr + threadIdx.x, o, nr, qend,
-                                lds_pf + (threadIdx.x & ~63u), iters);
+            r = expand_sm<FILL, COLS>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, lds_fr + col, o, nr, qend,
+                                lds_pf + (threadIdx.x & ~63u), iters, sg);
         else
             r = expand_one<FILL>(s, ov, rq.root, rq.flags, rq.vid, d, V, out, cnt, cap, st, o, nr, qend,
                                  lds_pf + (threadIdx.x & ~63u));
@@ -2414,16 +2532,24 @@ __global__ void __launch_bounds__(256) expand_kernel(DevSnap s, DevOverlay ov, c
             o.clocks[n + i] = iters;                       // (expand_sm: its accesses)
         }
         const bool staged = STAGE && r == EXP_TREE && cnt <= cap;
+        const bool split = sg.split_at != NO_SPLIT;
         // a tree not staged (too big, or left to the next tier) may have queued runs into the region:
-        // that part stays dead, so the copies cannot land on the next tree
-        if (STAGE && !staged) used += qend;
+        // that part stays dead, so the copies cannot land on the next tree (a split tree wrote the
+        // region below its split only)
+        if (STAGE && !staged) used += split ? sg.split_at : qend;
         if (r == EXP_OVERFLOW) {
             uint32_t at = atomicAdd(ta.out_count, 1u);
             ta.out_list[at] = i;
         } else if (MODE != EXP_FILL) {
             o.count[i] = r == EXP_TREE ? cnt : 0;
             o.status[i] = (uint8_t)r;
-            if (staged) {
+            if (staged && split) {
+                const uint32_t k = atomicAdd(o.seg_n, 1u);
+                // (one record per chunk taken, so k < seg_cap; a full list leaves the tree to pass 2)
+                o.stage_pos[i] = k < o.seg_cap ? SPLIT_POS | k : NOT_STAGED;
+                if (k < o.seg_cap) o.segs[k] = StageSeg{stage0 + used, sg.chunk, sg.split_at, i, 0u};
+                used += sg.split_at;
+            } else if (staged) {
                 o.stage_pos[i] = stage0 + used;
                 used += cnt;
             }
@@ -2447,12 +2573,32 @@ __global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict_
     const uint32_t groups = gridDim.x * (blockDim.x >> 4);
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; i < n; i += groups) {
         const uint64_t sp = stage_pos[i], b = offset[i], e = offset[i + 1];
-        if (sp == NOT_STAGED) continue;
+        if (sp >= SPLIT_POS) continue;                      // not staged, or in two pieces (copy_stage_pieces)
         for (uint64_t k = gl; k < e - b; k += 16) {
             keto_tree_node v = stage[sp + k];
             if (unit_row && (v.subject & EDGE_SET) && (v.subject & EDGE_VAL) < ov_units_base)
                 v.subject = EDGE_SET | unit_row[v.subject & EDGE_VAL];
             nodes[b + k] = v;
+        }
+    }
+}
+
+// The staged trees in two pieces (StageSeg): each piece of at most 2048 nodes {source in the staging
+// pool, destination in the node arena, length} copied by one wave, set handles turned into row ids on
+// the way as in gather_staged (unit_row != NULL)
+__global__ void __launch_bounds__(256) copy_stage_pieces(keto_tree_node* __restrict__ nodes,
+                                                         const keto_tree_node* __restrict__ stage,
+                                                         const uint64_t* __restrict__ pieces, uint32_t n_pieces,
+                                                         const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < n_pieces; w += waves) {
+        const uint64_t src = pieces[3 * w], dst = pieces[3 * w + 1], len = pieces[3 * w + 2];
+        for (uint64_t k = lane; k < len; k += 64) {
+            keto_tree_node v = stage[src + k];
+            if (unit_row && (v.subject & EDGE_SET) && (v.subject & EDGE_VAL) < ov_units_base)
+                v.subject = EDGE_SET | unit_row[v.subject & EDGE_VAL];
+            nodes[dst + k] = v;
         }
     }
 }
@@ -2585,8 +2731,12 @@ struct DeviceState {
     uint32_t ex_runs_cap = 0;
     CopyRun* ex_big = nullptr;        // pieces of long id runs | their count (last 8 B)
     uint32_t ex_big_cap = 0;
-    keto_tree_node* ex_stage = nullptr;   // one-pass expand: the lanes' staging regions
+    keto_tree_node* ex_stage = nullptr;   // one-pass expand: the lanes' staging regions | overflow chunks
     uint64_t ex_stage_nodes = 0;
+    uint8_t* ex_seg = nullptr;        // overflow chunks taken (8 B) | split trees (4 B + pad) | StageSeg list
+    uint32_t ex_seg_cap = 0;
+    uint64_t* ex_pieces = nullptr;    // copy_stage_pieces' {source, destination, length} triples
+    uint64_t ex_pieces_cap = 0;
     hipEvent_t ex_ev[4] = {};         // copy_runs / gather timing (added to tier 0 of the batch timing)
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
@@ -3580,6 +3730,8 @@ void device_release(Snapshot& S) {
     if (D.ex_nodes) (void)hipFree(D.ex_nodes);
     if (D.ex_runs) (void)hipFree(D.ex_runs);
     if (D.ex_stage) (void)hipFree(D.ex_stage);
+    if (D.ex_seg) (void)hipFree(D.ex_seg);
+    if (D.ex_pieces) (void)hipFree(D.ex_pieces);
     if (D.ex_big) (void)hipFree(D.ex_big);
     for (hipEvent_t e : D.ex_ev)
         if (e) (void)hipEventDestroy(e);
@@ -3824,6 +3976,149 @@ struct DevFree {
             if (q) (void)hipFree(q);
     }
 };
+
+// Expand on a migrating part (PART_MIGRATE, n_parts > 1): the part's arena holds its own rows, the
+// replicated hot rows and a stub (HDR_REMOTE) for every other part's row one of them points at.  A
+// tree that reaches another part's row needs that row's edges, and every part's host tables hold the
+// whole graph, so the call copies such rows into its overlay arena: the count pass records the rows
+// its walks met without a copy (ExpandOut::miss; the tree returns EXP_RETRY), they are copied in, and
+// the pass runs again until no tree needs one.  A row keeps one identity (the handle its node and
+// visit id carry): its stub's handle where this part has a stub, else an identity slot of the
+// overlay (a REMOTE header, allocated on first sight).  rmap maps an identity to the handle of the
+// row's copy.  Overlay layout: [the call's wildcard rows][identity slots][copies].
+struct PullSet {
+    const Snapshot& S;
+    const Overlay* wild;
+    uint64_t wild_units;
+    std::vector<uint32_t> id_row;                    // identity slot k -> row
+    std::unordered_map<uint32_t, uint32_t> ident;    // row -> identity handle (rows without a stub)
+    std::vector<uint32_t> pulled;                    // rows copied into the overlay, in order
+    std::unordered_set<uint32_t> have;
+    DevFree bufs;                                    // this round's device copies
+    PullSet(const Snapshot& s, const Overlay* w) : S(s), wild(w), wild_units(w && !w->empty() ? w->n_units : 0) {}
+    uint32_t identity(uint32_t r) {
+        if (S.mapped(r)) return S.unit_of_row[r];
+        auto it = ident.find(r);
+        if (it != ident.end()) return it->second;
+        const uint64_t h = S.n_units + wild_units + id_row.size();
+        if (h >= EDGE_VAL) throw Error{KETO_E_RANGE, "expand on a migrating part: identity handles past 2^31"};
+        id_row.push_back(r);
+        ident.emplace(r, (uint32_t)h);
+        return (uint32_t)h;
+    }
+    uint32_t vid(uint32_t r) {                        // Snapshot::vid_of_row with identities
+        if (!S.coll.empty()) {
+            auto it = S.coll.find(EDGE_SET | r);
+            if (it != S.coll.end()) return it->second;
+        }
+        return identity(r);
+    }
+    bool add(uint32_t r) {
+        if (r >= S.n_rows() || S.present(r) || !have.insert(r).second) return false;
+        pulled.push_back(r);
+        return true;
+    }
+    int64_t row_of(uint32_t h) const {                // the row a recorded handle names
+        if (h < S.n_units) return S.row_of_handle(h);
+        const uint64_t k = (uint64_t)h - S.n_units;
+        if (k < wild_units) return -1;
+        return k - wild_units < id_row.size() ? (int64_t)id_row[k - wild_units] : -1;
+    }
+    // the overlay arena, rmap and (with collision classes) a collision table keyed by identities, on
+    // the device for the next pass
+    void build(DevOverlay& dov, DevSnap& sv, const DevSnap& base) {
+        auto scan = [&](const uint32_t* ed, uint64_t m) {
+            for (uint64_t i = 0; i < m; ++i)
+                if ((ed[i] & EDGE_SET) && ed[i] != EDGE_POISON) (void)identity(ed[i] & EDGE_VAL);
+        };
+        auto wild_edges = [&](size_t i) {
+            const RowRec& rec = wild->rows[i];
+            const uint64_t b = (uint64_t)rec.edge_lo | ((uint64_t)(rec.hi_flags & 0xFFu) << 32);
+            const uint64_t e = i + 1 < wild->rows.size()
+                                   ? ((uint64_t)wild->rows[i + 1].edge_lo | ((uint64_t)(wild->rows[i + 1].hi_flags & 0xFFu) << 32))
+                                   : wild->edges.size();
+            return std::make_pair(wild->edges.data() + b, e - b);
+        };
+        const size_t n_wild = wild_units ? wild->rows.size() : 0;
+        for (size_t i = 0; i < n_wild; ++i) {
+            const auto ed = wild_edges(i);
+            scan(ed.first, ed.second);
+        }
+        for (uint32_t r : pulled) {
+            const auto ed = S.row_edges(r);
+            scan(ed.first, ed.second);
+        }
+        const uint64_t slots_at = wild_units, copies_at = wild_units + id_row.size();
+        std::vector<uint64_t> at(pulled.size());
+        uint64_t units = copies_at;
+        for (size_t k = 0; k < pulled.size(); ++k) {
+            at[k] = units;
+            units += 1 + (S.row_edges(pulled[k]).second + 3) / 4;
+        }
+        std::vector<uint32_t> arena(std::max<uint64_t>(units, 1) * HDR_WORDS, 0u);
+        auto patch = [&](uint64_t unit, const uint32_t* ed, uint64_t m) {   // set edges -> identities
+            uint32_t* e = arena.data() + unit * HDR_WORDS + HDR_WORDS;
+            for (uint64_t i = 0; i < m; ++i)
+                if ((ed[i] & EDGE_SET) && ed[i] != EDGE_POISON) e[i] = EDGE_SET | identity(ed[i] & EDGE_VAL);
+        };
+        for (size_t i = 0; i < n_wild; ++i) {
+            const auto ed = wild_edges(i);
+            put_row(arena.data(), wild->unit[i], wild->rows[i], wild->pp[i], 0, ed.first, ed.second, S.unit_of_row, false);
+            patch(wild->unit[i], ed.first, ed.second);
+        }
+        for (size_t k = 0; k < id_row.size(); ++k) arena[(slots_at + k) * HDR_WORDS + 2] = HDR_REMOTE;
+        for (size_t k = 0; k < pulled.size(); ++k) {
+            const uint32_t r = pulled[k];
+            const auto ed = S.row_edges(r);
+            put_row(arena.data(), (uint32_t)at[k], S.rows[r], S.row_pp[r], 0, ed.first, ed.second, S.unit_of_row, false);
+            patch(at[k], ed.first, ed.second);
+        }
+        for (void* q : bufs.p)
+            if (q) (void)hipFree(q);
+        bufs.p.clear();
+        uint64_t acc = 0;
+        uint32_t* a = dmalloc<uint32_t>(arena.size(), acc);
+        bufs.p.push_back(a);
+        HIP_OK(hipMemcpy(a, arena.data(), arena.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        const uint32_t cap = pow2_at_least(pulled.size() * 2 + 2);
+        std::vector<uint64_t> tab(cap, ~0ull);
+        for (size_t k = 0; k < pulled.size(); ++k) {
+            const uint32_t key = identity(pulled[k]);
+            uint32_t i = mix32(key) & (cap - 1);
+            while (tab[i] != ~0ull) i = (i + 1) & (cap - 1);
+            tab[i] = ((uint64_t)key << 32) | (uint32_t)(S.n_units + at[k]);
+        }
+        uint64_t* rm = dmalloc<uint64_t>(cap, acc);
+        bufs.p.push_back(rm);
+        HIP_OK(hipMemcpy(rm, tab.data(), cap * sizeof(uint64_t), hipMemcpyHostToDevice));
+        dov = DevOverlay{a, (uint32_t)S.n_units, rm, cap - 1};
+        sv = base;
+        if (!S.coll.empty() && !id_row.empty()) {
+            // the device table keys classes by handles of mapped rows (upload_coll); the identity
+            // slots' rows join it here
+            const uint32_t cc = pow2_at_least(S.coll.size() * 2 + 2);
+            std::vector<uint64_t> ct(cc, ~0ull);
+            for (const auto& kv : S.coll) {
+                uint32_t key = kv.first;
+                if (key & EDGE_SET) {
+                    const uint32_t r = key & EDGE_VAL;
+                    if (S.mapped(r)) key = EDGE_SET | S.unit_of_row[r];
+                    else if (auto it = ident.find(r); it != ident.end()) key = EDGE_SET | it->second;
+                    else continue;
+                }
+                uint32_t i = mix32(key) & (cc - 1);
+                while (ct[i] != ~0ull) i = (i + 1) & (cc - 1);
+                ct[i] = ((uint64_t)key << 32) | kv.second;
+            }
+            uint64_t* c = dmalloc<uint64_t>(cc, acc);
+            bufs.p.push_back(c);
+            HIP_OK(hipMemcpy(c, ct.data(), cc * sizeof(uint64_t), hipMemcpyHostToDevice));
+            sv.coll = c;
+            sv.coll_mask = cc - 1;
+        }
+    }
+};
+
 
 }  // namespace
 
@@ -4848,12 +5143,32 @@ void pinned_give(void* p) noexcept {
     (void)hipHostFree(p);
 }
 
-void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
-                   const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
-                   const Overlay* ovh, ExpandResult& out) {
+void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std::vector<uint32_t>& root_flags,
+                   const std::vector<uint32_t>& root_vid_in, const std::vector<int32_t>& depth, int32_t gmd,
+                   const Overlay* ovh, ExpandResult& out,
+                   const std::vector<std::pair<uint32_t, uint32_t>>* remote_roots) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
-    if (S.part_mode == PART_MIGRATE)
-        throw Error{KETO_E_INVALID, "expand needs a replicated snapshot or a shared-rows part (PART_SHARED)"};
+    // a migrating part holds its own rows and stubs for the others' rows it points at: the rows a
+    // tree needs from other parts are copied into the call's overlay (PullSet) from the host tables,
+    // which every part holds whole
+    const bool pulls = S.part_mode == PART_MIGRATE && S.n_parts > 1;
+    std::unique_ptr<PullSet> ps;
+    std::vector<uint32_t> root_m, vid_m;
+    if (pulls) {
+        ps = std::make_unique<PullSet>(S, ovh);
+        root_m = root_in;
+        vid_m = root_vid_in;
+        if (remote_roots)
+            for (const auto& rr : *remote_roots) {
+                root_m[rr.first] = ps->identity(rr.second);
+                vid_m[rr.first] = ps->vid(rr.second);
+                ps->add(rr.second);
+            }
+    } else if (remote_roots && !remote_roots->empty()) {
+        throw Error{KETO_E_INVALID, "expand root is owned by another part"};
+    }
+    const std::vector<uint32_t>& root = pulls ? root_m : root_in;
+    const std::vector<uint32_t>& root_vid = pulls ? vid_m : root_vid_in;
     DeviceState& D = *S.dev;
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));
@@ -4874,7 +5189,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         fprintf(stderr, "[expand] %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    OverlayBuf ov(S, ovh);
+    OverlayBuf ov(S, pulls ? nullptr : ovh);          // (a migrating part: the PullSet's overlay)
     uint64_t acc = 0;
     // workspace, reused across calls: requests | counts (n + 1) | offsets (n + 1) | stage positions
     // (n) | statuses
@@ -4907,7 +5222,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     // N nodes of staging per lane.
     const char* se = getenv("KETO_EXPAND_STAGE");
     const bool staged = !se || atoi(se) != 0;
-    uint64_t stage_cap = 0;
+    uint64_t stage_cap = 0, ovf_chunk = 0, ovf_cap = 0, ovf_base = 0;
     if (staged) {
         // staging nodes: KETO_EXPAND_STAGE_MB (default 1024 MB).  Bigger regions let fewer trees
         // spill to the second pass, but the lanes' regions then lie far apart and the copies into and
@@ -4917,7 +5232,16 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         const uint64_t budget = (sg ? (uint64_t)std::max(16, atoi(sg)) : 1024ull) << 17;
         stage_cap = std::min<uint64_t>(16384, std::max<uint64_t>(64, budget / p.slots[0]));
         if (se && atoi(se) > 1) stage_cap = (uint64_t)atoi(se);            // tests: small regions spill
-        const uint64_t nodes = stage_cap * p.slots[0];
+        // a tree past its region goes on in an overflow chunk of KETO_EXPAND_OVF_CHUNK nodes (default
+        // 256K) from a pool of KETO_EXPAND_OVF_NODES (default 32M nodes, 256 MB; 0: none, such trees
+        // are filled by the second pass)
+        const char* oc = getenv("KETO_EXPAND_OVF_CHUNK");
+        const char* on = getenv("KETO_EXPAND_OVF_NODES");
+        ovf_chunk = oc ? (uint64_t)std::max(1, atoi(oc)) : 262144ull;
+        ovf_cap = on ? (uint64_t)std::max(0ll, atoll(on)) : 32ull << 20;
+        ovf_cap -= ovf_cap % ovf_chunk;
+        ovf_base = stage_cap * p.slots[0];
+        const uint64_t nodes = ovf_base + ovf_cap;
         if (D.ex_stage_nodes < nodes) {
             if (D.ex_stage) (void)hipFree(D.ex_stage);
             D.ex_stage = nullptr;
@@ -4925,6 +5249,15 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
             D.ex_stage = dmalloc<keto_tree_node>(nodes, acc);
             D.ex_stage_nodes = nodes;
         }
+        const uint32_t seg_cap = (uint32_t)(ovf_cap / ovf_chunk) + 1;
+        if (D.ex_seg_cap < seg_cap) {
+            if (D.ex_seg) (void)hipFree(D.ex_seg);
+            D.ex_seg = nullptr;
+            D.ex_seg_cap = 0;
+            D.ex_seg = dmalloc<uint8_t>(16 + (uint64_t)seg_cap * sizeof(StageSeg), acc);
+            D.ex_seg_cap = seg_cap;
+        }
+        HIP_OK(hipMemsetAsync(D.ex_seg, 0, 16, st));
     }
     // the id-run queues of tier 0's lanes (RUNS_PER_LANE entries each) | runs queued per lane
     const char* ri = getenv("KETO_EXPAND_RUN_INLINE");
@@ -4964,6 +5297,9 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     // fit its LDS stack; KETO_EXPAND_SM=0: expand_one (tooling)
     const char* sme = getenv("KETO_EXPAND_SM");
     const bool sm = gmd <= SM_FRAMES && !(sme && atoi(sme) == 0);
+    // KETO_EXPAND_SPREAD=2|4 (A/B): tier 0's trees on 64 / spread lanes per wave
+    const char* spe = getenv("KETO_EXPAND_SPREAD");
+    const uint32_t spread = spe && (atoi(spe) == 2 || atoi(spe) == 4) ? (uint32_t)atoi(spe) : 1u;
     // (the batch timing sums the passes' tiers: keto_last_batch_timing after an expand)
     auto launch_pass = [&](bool fill, const ExpandOut& eo) {
         run_tiers(D, D.ews, n, p, st,
@@ -4975,8 +5311,27 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
                       const bool local = p.frames[level] == 0;
                       const int mode = fill ? EXP_FILL : (eo.stage && level == 0) ? EXP_STAGE : EXP_COUNT;
                       ExpandOut e = eo;
-                      if (level > 0) e.runs = nullptr;         // later tiers copy their runs in place
-                      if (level == 0 && local && sm) {
+                      if (level > 0) {
+                          e.runs = nullptr;                    // later tiers copy their runs in place
+                          e.ovf_used = nullptr;                // and stage no tree
+                      }
+                      if (level == 0 && local && sm && spread > 1 && bs == 256) {
+                          // (the same logical lanes, spread over spread x the waves)
+                          const dim3 g2(grid.x * spread);
+#define KETO_EXP_SPREAD(S)                                                                                          \
+    if (mode == EXP_COUNT)                                                                                        \
+        hipLaunchKernelGGL((expand_kernel<EXP_COUNT, SmFrames, S>), g2, block, 0, st, sv, dov, dq, n, gmd, e, a);  \
+    else if (mode == EXP_STAGE)                                                                                   \
+        hipLaunchKernelGGL((expand_kernel<EXP_STAGE, SmFrames, S>), g2, block, 0, st, sv, dov, dq, n, gmd, e, a);  \
+    else                                                                                                          \
+        hipLaunchKernelGGL((expand_kernel<EXP_FILL, SmFrames, S>), g2, block, 0, st, sv, dov, dq, n, gmd, e, a);
+                          if (spread == 2) {
+                              KETO_EXP_SPREAD(2)
+                          } else {
+                              KETO_EXP_SPREAD(4)
+                          }
+#undef KETO_EXP_SPREAD
+                      } else if (level == 0 && local && sm) {
                           if (mode == EXP_COUNT)
                               hipLaunchKernelGGL((expand_kernel<EXP_COUNT, SmFrames>), grid, block, 0, st, sv, dov, dq, n, gmd, e, a);
                           else if (mode == EXP_STAGE)
@@ -5025,6 +5380,41 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         d_nbig = reinterpret_cast<uint32_t*>(D.ex_big + D.ex_big_cap);
         HIP_OK(hipMemsetAsync(d_nbig, 0, sizeof(uint32_t), st));
     };
+    if (pulls) {
+        // rounds of the count pass over every root: each records the other parts' rows its walks met
+        // without a copy; they are copied into the overlay and the pass runs again until no tree
+        // needs one (a round finds every missing row a walk reaches through rows it has)
+        constexpr uint32_t MISS_CAP = 1u << 16;
+        DevBuf<uint32_t> miss(MISS_CAP + 1);
+        const DevSnap base = sv;
+        std::vector<uint8_t> stv(n);
+        std::vector<uint32_t> ml;
+        for (int round = 0;; ++round) {
+            ps->build(dov, sv, base);
+            HIP_OK(hipMemsetAsync(miss.p + MISS_CAP, 0, sizeof(uint32_t), st));
+            ExpandOut eo{nullptr, nullptr, dcount, dstatus, nullptr, d_lane_runs, run_inline, nullptr, nullptr, 0, nullptr,
+                         0, nullptr, nullptr, 0, 0, 0, nullptr, nullptr, 0, S.n_poisoned_rows == 0 ? 1u : 0u, 0u, 1u, nullptr};
+            eo.miss = miss.p;
+            eo.n_miss = miss.p + MISS_CAP;
+            eo.miss_cap = MISS_CAP;
+            launch_pass(false, eo);
+            uint32_t nm = 0;
+            HIP_OK(hipMemcpyAsync(stv.data(), dstatus, n, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipMemcpyAsync(&nm, miss.p + MISS_CAP, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            if (std::find(stv.begin(), stv.end(), (uint8_t)EXP_RETRY) == stv.end()) break;
+            ml.resize(std::min(nm, MISS_CAP));
+            if (!ml.empty()) HIP_OK(hipMemcpy(ml.data(), miss.p, ml.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            bool added = false;
+            for (uint32_t h : ml) {
+                const int64_t r = ps->row_of(h);
+                if (r >= 0) added |= ps->add((uint32_t)r);
+            }
+            if (!added) throw Error{KETO_E_HIP, "expand on a migrating part: a walk needs a row no part holds"};
+        }
+        if (trace) fprintf(stderr, "[expand] %zu rows of other parts copied\n", ps->pulled.size());
+        lap("pulls");
+    }
     // pass 1: count (and stage), then the staged trees' queued id runs
     HIP_OK(hipMemsetAsync(dstage, 0xFF, (uint64_t)n * sizeof(uint64_t), st));
     if (staged) big_queue(stage_cap * p.slots[0]);
@@ -5039,9 +5429,13 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         d_clocks = dmalloc<uint32_t>(2ull * n, acc);
         HIP_OK(hipMemsetAsync(d_clocks, 0, 2ull * n * sizeof(uint32_t), st));
     }
+    unsigned long long* d_ovf_used = staged && ovf_cap ? reinterpret_cast<unsigned long long*>(D.ex_seg) : nullptr;
+    uint32_t* d_seg_n = staged ? reinterpret_cast<uint32_t*>(D.ex_seg + 8) : nullptr;
+    StageSeg* d_segs = staged ? reinterpret_cast<StageSeg*>(D.ex_seg + 16) : nullptr;
     launch_pass(false, ExpandOut{nullptr, nullptr, dcount, dstatus, staged ? D.ex_runs : nullptr, d_lane_runs,
-                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, blind, pf, eb,
-                                 d_clocks});
+                                 run_inline, D.ex_big, d_nbig, D.ex_big_cap, D.ex_stage, stage_cap, dstage, d_ovf_used,
+                                 ovf_base, ovf_cap, ovf_chunk, d_segs, d_seg_n, staged ? D.ex_seg_cap : 0u, blind, pf,
+                                 eb, d_clocks});
     float extra_ms = 0;
     if (staged) {
         HIP_OK(hipEventRecord(D.ex_ev[0], st));
@@ -5052,11 +5446,16 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     std::vector<uint64_t> cnt(n), spos;
     HIP_OK(hipMemcpyAsync(cnt.data(), dcount, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(out.status.data(), dstatus, n, hipMemcpyDeviceToHost, st));
+    std::vector<uint8_t> segbuf;
     if (staged) {
         spos.resize(n);
         HIP_OK(hipMemcpyAsync(spos.data(), dstage, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        segbuf.resize(16 + (uint64_t)D.ex_seg_cap * sizeof(StageSeg));
+        HIP_OK(hipMemcpyAsync(segbuf.data(), D.ex_seg, segbuf.size(), hipMemcpyDeviceToHost, st));
     }
     HIP_OK(hipStreamSynchronize(st));
+    if (pulls && std::find(out.status.begin(), out.status.end(), (uint8_t)EXP_RETRY) != out.status.end())
+        throw Error{KETO_E_HIP, "expand on a migrating part: a tree still needs a row of another part"};
     if (staged) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, D.ex_ev[0], D.ex_ev[1]) == hipSuccess) extra_ms += ms;
@@ -5129,7 +5528,8 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
     if (unstaged) {
         big_queue(total);
         launch_pass(true, ExpandOut{D.ex_nodes, doff, dcount, dstatus, D.ex_runs, d_lane_runs, run_inline, D.ex_big,
-                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, blind, pf, eb, nullptr});
+                                    d_nbig, D.ex_big_cap, nullptr, 0, staged ? dstage : nullptr, nullptr, 0, 0, 0,
+                                    nullptr, nullptr, 0, blind, pf, eb, nullptr});
     }
     HIP_OK(hipEventRecord(D.ex_ev[2], st));
     if (unstaged) copy_queued();
@@ -5142,6 +5542,43 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         hipLaunchKernelGGL(gather_staged, dim3(copy_blocks((n + 15) / 16)), dim3(256), 0, st,
                            D.ex_nodes, D.ex_stage, dstage, doff, n, fuse ? D.unit_row : nullptr, (uint32_t)S.n_units);
     HIP_OK(hipGetLastError());
+    // staged trees in two pieces (a region, then an overflow chunk): copied piece by piece
+    std::vector<uint64_t> pc;                          // (alive until the stream is synchronized below)
+    uint32_t n_split = 0;
+    if (staged) {
+        uint32_t ns_ = 0;
+        std::memcpy(&ns_, segbuf.data() + 8, 4);
+        n_split = std::min<uint32_t>(ns_, D.ex_seg_cap);
+        const StageSeg* sgs = reinterpret_cast<const StageSeg*>(segbuf.data() + 16);
+        auto piece = [&](uint64_t src, uint64_t dst, uint64_t len) {
+            for (uint64_t b = 0; b < len; b += 2048) {
+                pc.push_back(src + b);
+                pc.push_back(dst + b);
+                pc.push_back(std::min<uint64_t>(2048, len - b));
+            }
+        };
+        for (uint32_t k = 0; k < n_split; ++k) {
+            const StageSeg& g = sgs[k];
+            if (g.root >= n || spos[g.root] != (SPLIT_POS | k)) continue;   // (a record of another call)
+            const uint64_t b = out.offset[g.root], len = out.offset[g.root + 1] - b;
+            piece(g.region, b, std::min(g.split_at, len));
+            if (len > g.split_at) piece(g.chunk, b + g.split_at, len - g.split_at);
+        }
+        if (!pc.empty()) {
+            const uint64_t m = pc.size() / 3;
+            if (D.ex_pieces_cap < m) {
+                if (D.ex_pieces) (void)hipFree(D.ex_pieces);
+                D.ex_pieces = nullptr;
+                D.ex_pieces_cap = 0;
+                D.ex_pieces = dmalloc<uint64_t>(3 * std::max<uint64_t>(m, 4096), acc);
+                D.ex_pieces_cap = std::max<uint64_t>(m, 4096);
+            }
+            HIP_OK(hipMemcpyAsync(D.ex_pieces, pc.data(), pc.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(copy_stage_pieces, dim3(copy_blocks((m + 3) / 4)), dim3(256), 0, st, D.ex_nodes,
+                               D.ex_stage, D.ex_pieces, (uint32_t)m, fuse ? D.unit_row : nullptr, (uint32_t)S.n_units);
+            HIP_OK(hipGetLastError());
+        }
+    }
     std::vector<uint64_t> rg;                          // (alive until the stream is synchronized below)
     if (fuse && unstaged) {
         for (uint32_t i = 0; i < n; ++i)
@@ -5188,9 +5625,34 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root, const std::ve
         if (hipEventElapsedTime(&ms, D.ex_ev[2], D.ex_ev[3]) == hipSuccess) extra_ms += ms;
         D.last.tier_ms[0] += extra_ms;
     }
-    if (trace) fprintf(stderr, "[expand] %u of %u trees filled by the second pass\n", unstaged, n);
-    // overlay handles -> ovh->base + overlay index (batch-local wildcard roots only)
-    if (ovh && !ovh->empty() && high_roots) {
+    if (trace) {
+        uint64_t big = 0, sum = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            if ((!staged || spos[i] == NOT_STAGED) && out.status[i] == EXP_TREE) {
+                big = std::max<uint64_t>(big, out.offset[i + 1] - out.offset[i]);
+                sum += out.offset[i + 1] - out.offset[i];
+            }
+        fprintf(stderr, "[expand] %u of %u trees filled by the second pass (%llu nodes, the largest %llu); %u staged in two pieces\n",
+                unstaged, n, (unsigned long long)sum, (unsigned long long)big, n_split);
+    }
+    // overlay handles -> ovh->base + overlay index (batch-local wildcard roots only); a migrating
+    // part's identity slots -> the rows they name
+    if (pulls) {
+        const uint64_t wu = ps->wild_units;
+        host_parallel_for(total, [&](uint64_t i) {
+            keto_tree_node& x = out.nodes[i];
+            if (!(x.subject & EDGE_SET)) return;
+            const uint32_t h = x.subject & EDGE_VAL;
+            if (h < S.n_units) return;
+            const uint64_t u = (uint64_t)h - S.n_units;
+            if (u < wu) {
+                auto it = std::lower_bound(ovh->unit.begin(), ovh->unit.end(), (uint32_t)u);
+                x.subject = EDGE_SET | (ovh->base + (uint32_t)(it - ovh->unit.begin()));
+            } else {
+                x.subject = EDGE_SET | ps->id_row[u - wu];
+            }
+        });
+    } else if (ovh && !ovh->empty() && high_roots) {
         for (uint32_t i = 0; i < n; ++i) {
             if (!root_flags[i] || out.offset[i + 1] == out.offset[i] || root[i] < S.n_units) continue;
             auto it = std::lower_bound(ovh->unit.begin(), ovh->unit.end(), (uint32_t)(root[i] - S.n_units));

@@ -565,9 +565,12 @@ struct ExpandResult {
     std::vector<uint64_t> offset;          // n+1
     std::vector<keto_tree_node, PinnedAlloc<keto_tree_node>> nodes;
 };
-// roots: row handles (root_flags bit0 = subject set) or string ids; out.nodes carry row ids
+// roots: row handles (root_flags bit0 = subject set) or string ids; out.nodes carry row ids.  On a
+// migrating part, remote_roots lists the roots (index, row id) whose rows this part does not hold
+// (their root / vid entries are ignored)
 void device_expand(Snapshot& s, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
                    const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
-                   const Overlay* ov, ExpandResult& out);
+                   const Overlay* ov, ExpandResult& out,
+                   const std::vector<std::pair<uint32_t, uint32_t>>* remote_roots = nullptr);
 
 }  // namespace keto

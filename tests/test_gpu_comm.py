@@ -347,10 +347,14 @@ def test_local_migrating_parts_follow_writes(P, seed):
     rows by their owners' handles; the next routed batch sees the stale filters on some rank and every
     rank runs the closure-filter exchange again before the records travel.  After each write the
     routed checks of every rank equal the SQL oracle's (relationtuples.go:128-149,200-223,
-    check/engine.go:36-123).  Wildcard queries no stored set uses are not routable on a migrating
-    partition (test_local_error_agreement_bad_arguments); expand is refused there."""
+    check/engine.go:36-123).  Wildcard check queries no stored set uses are not routable on a
+    migrating partition (test_local_error_agreement_bad_arguments).  Expands from every rank (set
+    roots any part owns, subject ids, wildcard queries, unknown rows) equal the oracle's trees: each
+    part copies the other parts' rows its trees reach into the call's overlay
+    (expand/engine.go:33-102)."""
     import random
-    from oracle.oracle_sql import SQLStore
+    from oracle.oracle_sql import ExpandEngine, NotFoundError, SQLStore
+    from tests.randgraph import random_expands
     from tests.randgraph import random_graph
     from tests.test_gpu_lifecycle import _random_write, _row
     import keto_amd
@@ -389,6 +393,17 @@ def test_local_migrating_parts_follow_writes(P, seed):
             for k, i in enumerate(mine[r]):
                 t, d, _ = checks[i]
                 assert bool(got[k]) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, step, r, t, d)
+        exps = random_expands(seed * 23 + step, (names, objs + ["new3"], rels + ["q"], users), k=12)
+        shares = [exps[r::P] for r in range(P)]
+        res = _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(parts[r], [(subj(s_), d) for s_, d, _ in shares[r]], g)))
+        for r, got in enumerate(res):
+            for (s_, d, _), (st_, js) in zip(shares[r], got):
+                try:
+                    tr = ExpandEngine(store, g).build_tree(s_, d)
+                    want_t = ("tree", tr.to_json()) if tr is not None else ("nil", None)
+                except NotFoundError:
+                    want_t = ("error", None)
+                assert ({0: "tree", 1: "nil", 2: "error"}[st_], js) == want_t, (seed, step, r, s_, d)
     for c in comms:
         c.close()
     for p in parts:
@@ -621,20 +636,23 @@ def test_local_expand_error_agreement(powerlaw_parts, monkeypatch, point):
         c.close()
 
 
-def test_expand_routed_refuses_migrating_parts(powerlaw_parts):
-    """Migrating parts do not expand: every rank returns KETO_E_INVALID, none waits."""
+@pytest.mark.parametrize("P", [2, 3])
+def test_expand_routed_migrating_parts(powerlaw_parts, P):
+    """Migrating parts expand every root themselves, copying the other parts' rows a tree reaches
+    into the call's overlay: each rank's share of the roots (folders and groups, docs of every part)
+    gives the replicated snapshot's trees, node for node (expand/engine.go:33-102)."""
     from keto_amd.capi import PART_MIGRATE
     g, st, full, parts, roots = powerlaw_parts
-    P = 2
     mig = []
     for r in range(P):
-        sn = g.snapshot(device=-1)
+        sn, _ = g.snapshot_from_strings(st, device=-1)
         mig.append(sn.upload_part(r, P, 0, mode=PART_MIGRATE))
     comms = _local_comms(P)
     _ok(_ranks(P, lambda r: comms[r].close_filters(mig[r])))
-    res = _ranks(P, lambda r: comms[r].expand_batch_routed(mig[r], [], 5))
-    for r, (ok, v) in enumerate(res):
-        assert not ok and v.code == -1, (r, v)
+    want = full.expand_batch(roots, 5, want_nodes=True)
+    res = _ok(_ranks(P, lambda r: comms[r].expand_batch_routed(mig[r], roots[r::P], 5, want_nodes=True)))
+    for r, got in enumerate(res):
+        assert got == want[r::P], r
     for c in comms:
         c.close()
     for p in mig:

@@ -71,10 +71,17 @@ def test_random_graphs_match_oracle(seed, wide):
 
 STAGE_ENVS = {
     "two_pass": {"KETO_EXPAND_STAGE": "0"},
-    "tiny_regions": {"KETO_EXPAND_STAGE": "3"},                    # most trees spill to the second pass
+    "tiny_regions": {"KETO_EXPAND_STAGE": "3"},                    # most trees go on in overflow chunks
     "shared_regions": {"KETO_EXPAND_STAGE": "40", "KETO_SLOTS": "256"},   # many roots per lane's region
     "default_few_slots": {"KETO_SLOTS": "256"},                   # lanes' run queues fill: runs copied in place
     "inline_runs": {"KETO_EXPAND_RUN_INLINE": "32"},
+    # trees past their region go on in overflow chunks: most trees in two pieces, the rest spill
+    "split_chunks": {"KETO_EXPAND_STAGE": "3", "KETO_EXPAND_OVF_CHUNK": "40"},
+    # the chunk pool runs out (4 chunks), with many roots per lane's region
+    "split_pool_full": {"KETO_EXPAND_STAGE": "8", "KETO_SLOTS": "256", "KETO_EXPAND_OVF_CHUNK": "64",
+                        "KETO_EXPAND_OVF_NODES": "256"},
+    # no overflow chunks: every tree past its region goes to the second pass
+    "no_chunks": {"KETO_EXPAND_STAGE": "5", "KETO_EXPAND_OVF_NODES": "0"},
 }
 
 
@@ -82,9 +89,11 @@ STAGE_ENVS = {
 @pytest.mark.parametrize("seed", range(3300, 3330))
 def test_expand_staging_modes_match_oracle(monkeypatch, env, seed):
     """The one-pass expand (trees staged in per-lane regions while counted, then gathered to their
-    offsets; trees that do not fit filled by a second pass) in every regime: the two-pass form,
-    regions so small that most trees spill, many roots sharing one lane's region, the default
-    regions with few lanes (whose id-run queues fill up), and short id runs copied in place.  Trees
+    offsets; a tree past its region goes on in an overflow chunk and is copied in two pieces; trees
+    that fit neither filled by a second pass) in every regime: the two-pass form, regions so small
+    that most trees spill, many roots sharing one lane's region, the default regions with few lanes
+    (whose id-run queues fill up), short id runs copied in place, most trees in two pieces, a chunk
+    pool that runs out, and no chunks.  Trees
     equal the oracle's, child order included."""
     from keto_amd.capi import EXPAND_NIL, EXPAND_NOT_FOUND, EXPAND_TREE
     for k, v in STAGE_ENVS[env].items():

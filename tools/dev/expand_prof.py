@@ -17,12 +17,16 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--roots", type=int, default=100_000)
     ap.add_argument("--check", type=int, default=0, help="trees compared with the C oracle")
+    ap.add_argument("--scale", type=int, default=0, help="the graph at 1/2^k size (same degrees): footprint study")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     from tools import synth
     t0 = time.time()
-    g = synth.SynthGraph(dict(synth.NESTED_100M), threads=16, kind="nested", chain=32)
+    prm = dict(synth.NESTED_100M)
+    for k in ("n_groups", "n_users", "target_edges"):
+        prm[k] >>= a.scale
+    g = synth.SynthGraph(prm, threads=16, kind="nested", chain=32)
     snap = g.snapshot(device=0)
     print(f"graph + upload {time.time() - t0:.1f} s", flush=True)
     rng = np.random.default_rng(5)
