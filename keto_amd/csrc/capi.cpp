@@ -382,7 +382,7 @@ int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot*
         *out = nullptr;
         auto h = std::make_unique<keto_snapshot>();
         {
-            std::shared_lock<std::shared_mutex> lk(src->s->rw);      // one version: no apply copies under us
+            std::shared_lock<RwGate> lk(src->s->rw);      // one version: no apply copies under us
             h->s = clone_host(*src->s);
         }
         if (device >= 0) device_upload(*h->s, device);
@@ -394,7 +394,7 @@ int keto_snapshot_clone(const keto_snapshot* src, int32_t device, keto_snapshot*
 int keto_snapshot_save(const keto_snapshot* s, const char* path, uint64_t tag) {
     return guarded([&] {
         if (!s || !path) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(s->s->rw);        // one version: no apply under us
+        std::shared_lock<RwGate> lk(s->s->rw);        // one version: no apply under us
         save_snapshot(*s->s, path, tag);
         return KETO_OK;
     });
@@ -417,7 +417,7 @@ void keto_snapshot_release(keto_snapshot* s) { delete s; }
 int keto_snapshot_get_stats(const keto_snapshot* h, keto_snapshot_stats* out) {
     return guarded([&] {
         if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         const Snapshot& S = *h->s;
         out->n_tuples = S.n_tuples;
         out->n_edges = S.edges.size();
@@ -437,7 +437,7 @@ int keto_resolve_checks(const keto_snapshot* h, const keto_check_req* reqs, uint
                         uint8_t* status_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         std::vector<uint8_t, NoInitAlloc<uint8_t>> st(status_out ? 0 : n);
         const auto wild = resolve_all(*h->s, reqs, n, out, status_out ? status_out : st.data());
         if (!wild.empty())
@@ -453,7 +453,7 @@ int keto_check_batch(keto_snapshot* h, const keto_check_req* reqs, uint32_t n, i
                      uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         check_named(*h->s, reqs, n, global_max_depth, allowed_out, status_out);
         return KETO_OK;
     });
@@ -464,7 +464,9 @@ int keto_check_batch_packed(keto_snapshot* h, const char* blob, uint64_t blob_le
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out)) || (blob_len && !blob)) throw Error{KETO_E_INVALID, "NULL argument"};
         if (blob_len >= (1ull << 32)) throw Error{KETO_E_RANGE, "a packed batch's strings must stay below 4 GiB"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        lock_trace("packed: waiting for rw shared");
+        std::shared_lock<RwGate> lk(h->s->rw);
+        lock_trace("packed: rw shared");
         Snapshot& S = *h->s;
         if (n == 0) return KETO_OK;
         const auto t0 = std::chrono::steady_clock::now();
@@ -512,7 +514,7 @@ int keto_check_batch_ids(keto_snapshot* h, const keto_check_ids* reqs, uint32_t 
                          uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_HANDLES, 0, nullptr);
         return KETO_OK;
     });
@@ -522,7 +524,7 @@ int keto_check_batch_rows(keto_snapshot* h, const keto_check_ids* reqs, uint32_t
                           uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_ROWS, 0, nullptr);
         return KETO_OK;
     });
@@ -532,7 +534,7 @@ int keto_check_batch_pairs(keto_snapshot* h, const keto_check_pair* reqs, uint32
                            int32_t global_max_depth, uint8_t* allowed_out) {
     return guarded([&] {
         if (!h || (n && (!reqs || !allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         device_check_host(*h->s, reqs, n, global_max_depth, allowed_out, FORM_PAIRS, max_depth, nullptr);
         return KETO_OK;
     });
@@ -552,7 +554,7 @@ int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
                             uint8_t* d_allowed_out, void* stream) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream);
         return KETO_OK;
     });
@@ -561,7 +563,7 @@ int keto_check_batch_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
 int keto_row_handles(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t* out) {
     return guarded([&] {
         if (!h || (n && (!rows || !out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         const Snapshot& S = *h->s;
         for (uint64_t i = 0; i < n; ++i) {
             if (rows[i] == KETO_NO_ROW) { out[i] = KETO_NO_ROW; continue; }
@@ -588,11 +590,22 @@ int keto_check_batch_rows_device(keto_snapshot* h, const keto_check_ids* d_reqs,
                                  uint8_t* d_allowed_out, void* stream) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         device_check_rows(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream);
         return KETO_OK;
     });
 }
+
+extern "C++" {
+namespace keto {
+void lock_trace(const char* what) {
+    static const bool on = getenv("KETO_TRACE_LOCKS") != nullptr;
+    if (!on) return;
+    const auto t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    fprintf(stderr, "[lk %.3f %zx] %s\n", t, std::hash<std::thread::id>{}(std::this_thread::get_id()) & 0xFFFFFF, what);
+}
+}  // namespace keto
+}  // extern "C++"
 
 int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_inserts, const keto_tuple* deletes,
                         uint64_t n_deletes, uint64_t* version_out) {
@@ -603,17 +616,22 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
         // collision and wildcard effects found -- reads only) under the shared lock, so batches keep
         // running, and committed to the host tables and the device arena under the exclusive one
         std::lock_guard<std::mutex> wl(S.apply_mu);
-        std::shared_lock<std::shared_mutex> rl(S.rw);
-        std::unique_lock<std::shared_mutex> xl(S.rw, std::defer_lock);
+        lock_trace("apply: apply_mu");
+        std::shared_lock<RwGate> rl(S.rw);
+        lock_trace("apply: rw shared");
+        std::unique_lock<RwGate> xl(S.rw, std::defer_lock);
         const auto t0 = std::chrono::steady_clock::now();
         auto t1 = t0;
         apply_writes(S, inserts, n_inserts, deletes, n_deletes, [&] {
             t1 = std::chrono::steady_clock::now();
             rl.unlock();
+            lock_trace("apply: staged, waiting for rw exclusive");
             xl.lock();
+            lock_trace("apply: rw exclusive");
         });
         const auto t2 = std::chrono::steady_clock::now();
         device_apply(S);
+        lock_trace("apply: device_apply done");
         if (getenv("KETO_APPLY_TRACE"))             // tooling: staged (shared lock), then the exclusive part
             fprintf(stderr, "[apply] staged %.3f ms, lock wait %.3f ms, host commit + device %.3f ms\n",
                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -838,7 +856,7 @@ int keto_check_work_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint3
                            uint8_t* d_allowed_out, uint64_t out[KETO_WORK_SLOTS]) {
     return guarded([&] {
         if (!h || !out || (n && (!d_reqs || !d_allowed_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, nullptr, out);
         return KETO_OK;
     });
@@ -848,7 +866,7 @@ int keto_check_steps_device(keto_snapshot* h, const keto_check_ids* d_reqs, uint
                             uint8_t* d_allowed_out, uint32_t* d_steps) {
     return guarded([&] {
         if (!h || (n && (!d_reqs || !d_allowed_out || !d_steps))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         uint64_t w[KETO_WORK_SLOTS];
         device_check(*h->s, d_reqs, n, global_max_depth, d_allowed_out, nullptr, w, d_steps);
         return KETO_OK;
@@ -925,7 +943,7 @@ int keto_expand_batch(keto_snapshot* h, const keto_expand_req* reqs, uint32_t n,
                       keto_tree_arena** out) {
     return guarded([&] {
         if (!h || !out || (n && !reqs)) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         *out = nullptr;
         auto a = std::make_unique<keto_tree_arena>();
         expand_named(*h->s, reqs, n, global_max_depth, *a, nullptr);
@@ -938,7 +956,7 @@ int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t
                           int32_t global_max_depth, keto_tree_arena** out) {
     return guarded([&] {
         if (!h || !out || (n && (!roots || !max_depth))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         *out = nullptr;
         Snapshot& S = *h->s;
         auto a = std::make_unique<keto_tree_arena>();
@@ -991,7 +1009,7 @@ int64_t keto_tree_json(const keto_snapshot* h, const keto_tree_arena* a, uint32_
         if (a->r.status[i] != KETO_EXPAND_TREE) {
             o = "null";
         } else {
-            std::shared_lock<std::shared_mutex> lk(h->s->rw);
+            std::shared_lock<RwGate> lk(h->s->rw);
             const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
             tree_json(*h->s, a, a->r.nodes.data() + b, e - b, o);
         }
@@ -1008,7 +1026,7 @@ int64_t encode_all(const keto_snapshot* h, const keto_tree_arena* a, int kind, c
                    uint64_t* offsets, One one) {
     const uint32_t n = (uint32_t)a->r.status.size();
     const unsigned th = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::shared_lock<std::shared_mutex> rlk(h->s->rw);      // before enc_mu: apply takes rw alone
+    std::shared_lock<RwGate> rlk(h->s->rw);      // before enc_mu: apply takes rw alone
     std::lock_guard<std::mutex> lk(a->enc_mu);
     std::vector<std::string>& enc = a->enc;
     if (!(a->enc_kind == kind && a->enc_uid == h->s->uid && a->enc_version == h->s->version && enc.size() == n)) {
@@ -1068,7 +1086,7 @@ int64_t keto_tree_proto(const keto_snapshot* h, const keto_tree_arena* a, uint32
         if (st != KETO_EXPAND_TREE) return 0;                     // nil tree: no message
         std::string o;
         {
-            std::shared_lock<std::shared_mutex> lk(h->s->rw);
+            std::shared_lock<RwGate> lk(h->s->rw);
             const uint64_t b = a->r.offset[i], e = a->r.offset[i + 1];
             tree_proto(*h->s, a, a->r.nodes.data() + b, e - b, o);
         }
@@ -1094,7 +1112,7 @@ int64_t keto_tree_proto_all_device(keto_snapshot* h, const keto_tree_arena* a, u
                                    uint64_t* offsets) {
     return guarded([&]() -> int64_t {
         if (!h || !a || !offsets) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> rlk(h->s->rw);    // strings / row keys (before S.mu)
+        std::shared_lock<RwGate> rlk(h->s->rw);    // strings / row keys (before S.mu)
         const uint32_t n = (uint32_t)a->r.status.size();
         // the nodes of the trees (other statuses have none), tree t = [toff[t], toff[t + 1])
         std::vector<uint64_t> toff(n + 1, 0);
@@ -1127,7 +1145,7 @@ int64_t keto_subject_fields(const keto_snapshot* h, const keto_tree_arena* a, co
                             char* buf, uint64_t cap, uint32_t* lens_out) {
     return guarded([&]() -> int64_t {
         if (!h || (n && (!subjects || !lens_out))) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         const Snapshot& S = *h->s;
         uint64_t total = 0;
         for (uint64_t i = 0; i < n; ++i) {
@@ -1171,7 +1189,7 @@ int64_t keto_subject_fields(const keto_snapshot* h, const keto_tree_arena* a, co
 int64_t keto_subject_string(const keto_snapshot* h, uint32_t subject, char* buf, uint64_t cap) {
     return guarded([&]() -> int64_t {
         if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
-        std::shared_lock<std::shared_mutex> lk(h->s->rw);
+        std::shared_lock<RwGate> lk(h->s->rw);
         SubjectFields f = fields_of(*h->s, nullptr, subject);
         return copy_out(f.set ? f.ns + ":" + f.obj + "#" + f.rel : f.id, buf, cap);
     });

@@ -579,7 +579,7 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         HIP_OK(hipSetDevice(c->device));
         Local mine;
         Snapshot* Sp = nullptr;
-        std::shared_lock<std::shared_mutex> lk;
+        std::shared_lock<RwGate> lk;
         std::vector<uint64_t> cnt(c->n, 0);
         std::vector<WildReq> wild;     // wildcard queries no stored set uses: answered here (below)
         keto_check_ids* d_send = nullptr;
@@ -603,7 +603,7 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         mine.run([&] {
             if (!h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
             Sp = h->s.get();
-            lk = std::shared_lock<std::shared_mutex>(Sp->rw);
+            lk = std::shared_lock<RwGate>(Sp->rw);
             if ((int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
                 throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
                                             "part = rank and n_parts = ranks)"};
@@ -717,7 +717,7 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
         const int P = c->n;
         Local mine;
         Snapshot* Sp = nullptr;
-        std::shared_lock<std::shared_mutex> lk;
+        std::shared_lock<RwGate> lk;
         std::vector<uint8_t> routed(std::max<uint32_t>(n, 1), 0);
         std::vector<std::vector<uint32_t>> to(P);        // request indices per owner part, in request order
         std::vector<uint64_t> words;                     // (row id | max depth << 32), grouped by owner
@@ -726,7 +726,7 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
         mine.run([&] {
             if (!h || !out || (n && !reqs)) throw Error{KETO_E_INVALID, "NULL argument"};
             Sp = h->s.get();
-            lk = std::shared_lock<std::shared_mutex>(Sp->rw);
+            lk = std::shared_lock<RwGate>(Sp->rw);
             if ((int)Sp->n_parts != P || (int)Sp->part != c->rank)
                 throw Error{KETO_E_INVALID, "the snapshot is not this rank's part (keto_snapshot_upload_part_mode with "
                                             "part = rank and n_parts = ranks)"};

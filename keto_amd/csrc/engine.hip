@@ -3440,12 +3440,15 @@ namespace {
 // finds no place below 2^31 units
 bool apply_in_place(Snapshot& S) {
     DeviceState& D = *S.dev;
+    lock_trace("apply: waiting for D.mu");
     std::lock_guard<std::mutex> lk(D.mu);
+    lock_trace("apply: D.mu");
     HIP_OK(hipSetDevice(D.device));
     const bool trace = getenv("KETO_APPLY_TRACE") != nullptr;          // tooling: phase times
     auto t_lap = std::chrono::steady_clock::now();
     std::string laps;
     auto lap = [&](const char* what) {
+        lock_trace(what);
         if (!trace) return;
         const auto t = std::chrono::steady_clock::now();
         char b[64];
@@ -5000,7 +5003,9 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
     // that produced the inputs (the snapshot's own stream is non-blocking and would not be)
     hipStream_t st = (hipStream_t)stream;
     // the lock is held from the translation through the check: D.xlate is shared by all callers
+    lock_trace("rows: waiting for D.mu");
     std::lock_guard<std::mutex> lk(D.mu);
+    lock_trace("rows: D.mu");
     HIP_OK(hipSetDevice(D.device));
     uint64_t acc = 0;
     if (D.xlate_cap < n) {
@@ -5016,8 +5021,10 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
     uint32_t bad = 0;
     HIP_OK(hipMemcpyAsync(&bad, D.ws[0].counters + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    lock_trace("rows: translated");
     if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
     check_locked(S, D, D.xlate, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, false);
+    lock_trace("rows: check launched");
 }
 
 // Expand output: set nodes carry row handles; map them to row ids on the device (binary search in
@@ -5233,12 +5240,13 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std:
         stage_cap = std::min<uint64_t>(16384, std::max<uint64_t>(64, budget / p.slots[0]));
         if (se && atoi(se) > 1) stage_cap = (uint64_t)atoi(se);            // tests: small regions spill
         // a tree past its region goes on in an overflow chunk of KETO_EXPAND_OVF_CHUNK nodes (default
-        // 256K) from a pool of KETO_EXPAND_OVF_NODES (default 32M nodes, 256 MB; 0: none, such trees
-        // are filled by the second pass)
+        // 256K) from a pool of KETO_EXPAND_OVF_NODES (default a quarter of the regions' nodes, at
+        // least 4 chunks, at most 32M nodes = 256 MB; 0: none, such trees are filled by the second pass)
         const char* oc = getenv("KETO_EXPAND_OVF_CHUNK");
         const char* on = getenv("KETO_EXPAND_OVF_NODES");
         ovf_chunk = oc ? (uint64_t)std::max(1, atoi(oc)) : 262144ull;
-        ovf_cap = on ? (uint64_t)std::max(0ll, atoll(on)) : 32ull << 20;
+        ovf_cap = on ? (uint64_t)std::max(0ll, atoll(on))
+                     : std::min<uint64_t>(32ull << 20, std::max<uint64_t>(4 * ovf_chunk, stage_cap * p.slots[0] / 4));
         ovf_cap -= ovf_cap % ovf_chunk;
         ovf_base = stage_cap * p.slots[0];
         const uint64_t nodes = ovf_base + ovf_cap;

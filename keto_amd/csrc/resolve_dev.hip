@@ -389,8 +389,11 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
         if (p.off + len > blob_len) throw Error{KETO_E_INVALID, "request " + std::to_string(i) + "'s fields lie outside the blob"};
     }
     RDevState& R = rdev_get(S, dv.device);
+    lock_trace("packed: waiting for R.mu");
     std::lock_guard<std::mutex> lk(R.mu);                                   // held through the last copy
+    lock_trace("packed: R.mu");
     rdev_refresh(S, R);
+    lock_trace("packed: refreshed");
     hipStream_t st = R.stream;
     const uint8_t* d_blob = upload(R.blob, blob, blob_len, st);
     const keto_check_packed* d_q = upload(R.reqs, reqs, n, st);
@@ -400,9 +403,11 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
     hipLaunchKernelGGL(resolve_packed, dim3((n + 255) / 256), dim3(256), 0, st, R.view, d_blob, d_q, n, d_ids, d_st);
     HIP_OK(hipGetLastError());
     device_check_rows(S, d_ids, n, gmd, d_dec, st);                        // row ids -> handles, the check
+    lock_trace("packed: checked");
     HIP_OK(hipMemcpyAsync(allowed, d_dec, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    lock_trace("packed: copied back");
     for (uint32_t i = 0; i < n; ++i) {
         if (status[i] == ST_HOST) {
             host.push_back(i);

@@ -187,6 +187,28 @@ struct RDevStateDeleter {
 
 uint64_t next_snapshot_uid();   // snapshot.cpp: a process-wide counter
 
+// The snapshot's reader / writer lock, writer-preferring: a waiting writer holds the turnstile
+// every reader passes before it takes the lock shared, so a stream of overlapping batches cannot
+// keep keto_snapshot_apply waiting forever (std::shared_mutex on glibc lets readers in while a writer
+// waits).  A thread never takes it shared twice, and never waits for another thread's call on the
+// same snapshot while it holds it.
+struct RwGate {
+    std::shared_mutex m;
+    std::mutex gate;
+    void lock() {
+        std::lock_guard<std::mutex> g(gate);
+        m.lock();
+    }
+    bool try_lock() { return m.try_lock(); }
+    void unlock() { m.unlock(); }
+    void lock_shared() {
+        { std::lock_guard<std::mutex> g(gate); }
+        m.lock_shared();
+    }
+    bool try_lock_shared() { return m.try_lock_shared(); }
+    void unlock_shared() { m.unlock_shared(); }
+};
+
 struct Snapshot {
     const uint64_t uid = next_snapshot_uid();   // never reused (caches keyed by snapshot use it, not its address)
     // ---- config
@@ -260,7 +282,7 @@ struct Snapshot {
     uint32_t row_hlog2(uint32_t r) const;         // 0 = no id table
 
     // ---- lifecycle (delta.cpp): writes applied since the build
-    std::shared_mutex rw;                      // calls read the host tables shared; keto_snapshot_apply exclusive
+    RwGate rw;                                 // calls read the host tables shared; keto_snapshot_apply exclusive
     std::mutex apply_mu;                       // one keto_snapshot_apply at a time (it stages under rw shared)
     uint64_t version = 0;                      // bumped by every keto_snapshot_apply
     uint32_t n_sorted_strs = 0;                // strs[0, n) are in byte order (id = rank); later ones were added
@@ -540,6 +562,9 @@ struct NoInitAlloc : std::allocator<T> {
 // Page-locked host memory for expand node arenas (engine.hip): blocks are recycled across arenas,
 // so the arena's D2H is one DMA at the link's rate without a hipHostMalloc per call.  Falls back to
 // malloc when no pinned memory can be had.
+// tooling (KETO_TRACE_LOCKS=1): one stderr line per lock / phase step of the calls that share a
+// snapshot (apply, packed batches), with the thread: where each thread waits when a run hangs
+void lock_trace(const char* what);
 void* pinned_take(size_t bytes);
 void pinned_give(void* p) noexcept;
 template <class T>
