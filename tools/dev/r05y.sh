@@ -1,0 +1,11 @@
+set -o pipefail
+tag=r05y
+o=gpurun_out/$tag; mkdir -p $o
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+echo "== smoke $(date +%T)"
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { tail -30 $o/smoke.log; exit 1; }
+tail -2 $o/smoke.log
+echo "== bench $(date +%T)"
+timeout -k 10 420 python -u bench.py > $o/bench.log 2>&1 || { tail -30 $o/bench.log; exit 1; }
+tail -1 $o/bench.log | cut -c1-600
+PROFILE_ONLY=1 bash tools/gpu_round.sh $tag
