@@ -5397,7 +5397,7 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std:
         const DevSnap base = sv;
         std::vector<uint8_t> stv(n);
         std::vector<uint32_t> ml;
-        for (int round = 0;; ++round) {
+        for (;;) {
             ps->build(dov, sv, base);
             HIP_OK(hipMemsetAsync(miss.p + MISS_CAP, 0, sizeof(uint32_t), st));
             ExpandOut eo{nullptr, nullptr, dcount, dstatus, nullptr, d_lane_runs, run_inline, nullptr, nullptr, 0, nullptr,
