@@ -4338,7 +4338,17 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.device));
         D.v1_lanes[var] = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus) * 256u;
     }
-    const uint32_t lanes = getenv("KETO_SLOTS") ? (uint32_t)hw_slots() : D.v1_lanes[var];
+    uint32_t lanes = getenv("KETO_SLOTS") ? (uint32_t)hw_slots() : D.v1_lanes[var];
+    // a batch of at most ~2 requests per resident lane (config #2: 1M requests) takes one lane per
+    // request: the grid is then more than the chip holds at once, and a wave that finishes makes room
+    // for the next instead of a lane walking its second request behind its first (0.158 -> 0.144
+    // ms, profiles/r05aa_config2_grid.log).  KETO_T0_ONE_PER_LANE = the requests-per-lane bound
+    // (default 2; 0 = off); tier-0 tables: 2 KB per lane
+    if (var == VAR_W8 && !getenv("KETO_SLOTS")) {
+        const char* e1 = getenv("KETO_T0_ONE_PER_LANE");
+        const uint64_t k = e1 ? (uint64_t)std::max(0, atoi(e1)) : 2u;
+        if ((uint64_t)n <= k * lanes) lanes = (uint32_t)(((uint64_t)n + 255) / 256 * 256);
+    }
     p.slots[0] = (uint32_t)std::min<uint64_t>(lanes, ((uint64_t)n + 255) / 256 * 256);
     if (ss) {
         // a streamed launch leaves wave slots free: the runtime's H2D copies behind it run as blit
