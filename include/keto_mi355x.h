@@ -446,8 +446,10 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* s, const keto_check_re
  * (one all-to-all), are decided there -- on a migrating part by continuation-record rounds with an
  * all-reduce and all-to-alls per round -- and the decisions come back (a second all-to-all).  A
  * wildcard query that no stored subject set uses has no row to route by: a shared-rows part answers
- * it itself (its batch-local row from the whole graph's host tables); a migrating part returns
- * KETO_E_INVALID.  Every rank returns the same code when any rank fails. */
+ * it itself (its batch-local row from the whole graph's host tables); a migrating part sends one
+ * request per matching row (each top-level tuple is searched with a fresh visited map, so the query
+ * is allowed iff one of those rows is) and returns KETO_E_INVALID only when one of them has a failing
+ * page.  Every rank returns the same code when any rank fails. */
 int keto_check_batch_routed(keto_comm* c, keto_snapshot* s, const keto_check_req* reqs, uint32_t n,
                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
 /* BuildTree (internal/expand/engine.go:33-102) over an edge-partitioned snapshot of shared-rows

@@ -586,18 +586,22 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         uint32_t* d_order = nullptr;
         uint64_t wb = 0;
         std::vector<keto_check_ids> ids;
+        // a migrating part's wildcard queries: one request per matching row after the batch's own
+        // (parent = the query's index), their decisions OR-ed into the query's below
+        std::vector<uint32_t> parent;
+        uint32_t N = n;                                  // requests routed: the batch's + those
         // row-id requests to the device, grouped by owner (d_send, d_order); counts per part
         auto route = [&] {
-            keto_check_ids* d_reqs = c->a.get<keto_check_ids>(n);
-            HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice,
+            keto_check_ids* d_reqs = c->a.get<keto_check_ids>(N);
+            HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)N * sizeof(keto_check_ids), hipMemcpyHostToDevice,
                                   c->stream));
             const int16_t* d_owner = owner_table(*c, *Sp);
-            wb = route_work_bytes(n, c->n);
-            uint8_t* work = c->c.get<uint8_t>(std::max<uint64_t>(wb, n));
-            d_send = c->d.get<keto_check_ids>(n);
-            d_order = c->b.get<uint32_t>(n);
+            wb = route_work_bytes(N, c->n);
+            uint8_t* work = c->c.get<uint8_t>(std::max<uint64_t>(wb, N));
+            d_send = c->d.get<keto_check_ids>(N);
+            d_order = c->b.get<uint32_t>(N);
             std::vector<uint32_t> cs(c->n);
-            route_rows(d_reqs, n, d_owner, Sp->n_rows(), c->rank, c->n, work, wb, d_send, d_order, cs.data(), c->stream);
+            route_rows(d_reqs, N, d_owner, Sp->n_rows(), c->rank, c->n, work, wb, d_send, d_order, cs.data(), c->stream);
             cnt.assign(cs.begin(), cs.end());
         };
         mine.run([&] {
@@ -611,10 +615,32 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             // names -> row ids (routing needs rows, not this part's handles)
             ids.resize(std::max<uint32_t>(n, 1));
             wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
-            if (!wild.empty() && Sp->part_mode == PART_MIGRATE)
-                throw Error{KETO_E_INVALID, "request " + std::to_string(wild[0].i) +
-                                                " is a wildcard query that no stored subject set uses: not "
-                                                "answered on a migrating partition"};
+            if (!wild.empty() && Sp->part_mode == PART_MIGRATE) {
+                // A wildcard query that no stored subject set uses has no row here, and its
+                // batch-local row would hold other parts' subject sets.  Its tuples are every
+                // matching row's, and each top-level tuple is searched with a fresh visited map
+                // (the shadowed ctx, internal/check/engine.go:47-48), so the query is allowed iff
+                // one of the matching rows is, checked as a request of its own at the same depth:
+                // those requests travel like any other.  A poisoned page would cut the query's
+                // ORDER BY sequence elsewhere than the rows' own (relationtuples.go:200-223): such
+                // queries are refused.
+                for (const WildReq& w : wild) {
+                    for (uint32_t r : Sp->rows_in_key_order(w.key)) {
+                        if (Sp->row_pp[r] != NO_PAGE)
+                            throw Error{KETO_E_INVALID, "request " + std::to_string(w.i) +
+                                                            " is a wildcard query over a row with a failing page: "
+                                                            "not answered on a migrating partition"};
+                        keto_check_ids x = ids[w.i];
+                        x.row = r;
+                        ids.push_back(x);
+                        parent.push_back(w.i);
+                    }
+                    ids[w.i].row = KETO_NO_ROW;                  // decided by its rows' requests
+                }
+                if ((uint64_t)n + parent.size() >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "too many wildcard rows"};
+                N = n + (uint32_t)parent.size();
+                wild.clear();
+            }
             route();
         });
         // the counts to their owners, each with this rank's status and whether writes left this
@@ -651,7 +677,7 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             if (m >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "more than 2^32 - 1 requests routed to one part"};
             d_recv = c->g.get<keto_check_ids>(std::max<uint64_t>(m, 1));
             d_dec = c->h.get<uint8_t>(std::max<uint64_t>(m, 1));
-            d_back = c->i.get<uint8_t>(std::max<uint32_t>(n, 1));
+            d_back = c->i.get<uint8_t>(std::max<uint32_t>(N, 1));
         });
         agree(*c, mine);
         std::vector<uint64_t> sb(c->n), rb(c->n);
@@ -671,10 +697,17 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         }
         // decisions back to their origins, in the origin's order
         c->t->alltoallv(d_dec, in, d_back, cnt, c->stream);
-        uint8_t* d_out = c->c.get<uint8_t>(std::max<uint64_t>(wb, n));
-        unroute_rows(d_back, d_order, n, d_out, c->stream);
+        uint8_t* d_out = c->c.get<uint8_t>(std::max<uint64_t>(wb, N));
+        unroute_rows(d_back, d_order, N, d_out, c->stream);
+        std::vector<uint8_t> sub(N - n);
         if (n) HIP_OK(hipMemcpyAsync(allowed_out, d_out, n, hipMemcpyDeviceToHost, c->stream));
+        if (N > n) HIP_OK(hipMemcpyAsync(sub.data(), d_out + n, N - n, hipMemcpyDeviceToHost, c->stream));
         sync(*c);
+        for (size_t k = 0; k < parent.size(); ++k) {     // allowed if a row is; undecided if one is, none allowed
+            uint8_t& a = allowed_out[parent[k]];
+            if (sub[k] == 1) a = 1;
+            else if (sub[k] > 1 && a != 1) a = sub[k];
+        }
         for (uint32_t i = 0; i < n; ++i)
             if (allowed_out[i] > 1) {            // KETO_UNDECIDED (and the migrating kernel's unset 255)
                 allowed_out[i] = 0;
