@@ -118,3 +118,44 @@ def test_host_apply_wildcard_sets():
         p.apply([(1, "c", "r", "u")])                                           # n:*#r holds a poisoned page
     assert p.version() == 0
     assert p.apply([(1, "c", "s", "u")]) == 1                                   # no wildcard row matches n:c#s
+
+
+def test_apply_is_not_starved_by_readers():
+    """The snapshot lock lets a waiting write in (RwGate, snapshot.hpp): four threads cloning a
+    host-only snapshot back to back (each clone holds the lock shared) cannot keep keto_snapshot_apply
+    waiting.  With a reader-preferring lock the writes could wait as long as the readers keep
+    overlapping; here 30 transactions must commit while the readers run."""
+    import threading
+    import time
+    ns = [(1, "docs"), (2, "groups")]
+    rows = [(1, f"d{i}", "view", f"u{i % 97}") for i in range(20000)]
+    rows += [(1, f"d{i}", "view", None, 2, f"g{i % 50}", "member") for i in range(0, 20000, 7)]
+    s = keto_amd.Snapshot.build(ns, rows, device=-1)
+    stop = threading.Event()
+    clones = [0] * 4
+    errors = []
+
+    def reader(k):
+        try:
+            while not stop.is_set():
+                s.clone(device=-1).close()
+                clones[k] += 1
+        except Exception as e:          # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=reader, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    t0 = time.time()
+    try:
+        for k in range(30):
+            s.apply([(1, f"w{k}", "view", f"wu{k}")])
+    finally:
+        stop.set()
+        for t in ts:
+            t.join(timeout=60)
+    assert not errors, errors
+    assert s.version() == 30
+    assert time.time() - t0 < 60
+    assert sum(clones) > 0
+    s.close()
