@@ -37,6 +37,10 @@ extern "C" {
 #endif
 
 #define KETO_ABI_VERSION 5
+/* The largest arena one snapshot (a replica) or one partition part takes on a device: handles are
+ * 32-bit counts of 16-byte units.  A graph past it is served as several shared-rows parts, more than
+ * one per device if need be (each part holds the subject-set targets and its share of the root rows). */
+#define KETO_ARENA_MAX_BYTES (64ull << 30)
 
 /* return codes */
 #define KETO_OK 0

@@ -54,6 +54,16 @@ func (s *Snapshot) PartArenaBytes(part, nParts int) (uint64, error) {
 	return uint64(st.arena_bytes), nil
 }
 
+// PartStats is what part `part` of nParts shared-rows parts of this host-only snapshot would take on
+// a device: its arena, and of it the rows every part keeps (the subject-set targets).
+func (s *Snapshot) PartStats(part, nParts int) (arena, shared uint64, err error) {
+	var st C.keto_part_stats
+	if rc := C.keto_snapshot_part_stats_mode(s.h, C.uint32_t(part), C.uint32_t(nParts), C.KETO_PART_SHARED, &st); rc != C.KETO_OK {
+		return 0, 0, lastErr(rc)
+	}
+	return uint64(st.arena_bytes), uint64(st.shared_bytes), nil
+}
+
 // UploadPart uploads this host-only snapshot as part `part` of nParts shared-rows parts on HIP
 // device `device` (keto_snapshot_upload_part_mode, KETO_PART_SHARED): the rows subject sets point at
 // on every part, each root row on the part hash(namespace, object) picks.
@@ -82,9 +92,9 @@ func Fits(arena uint64, devices []int) (bool, error) {
 	return true, nil
 }
 
-// Partition is a graph too large for one GPU, edge-partitioned over the devices of the server
-// process: one shared-rows part per device (subject-set targets on every part, root rows by hash)
-// and one in-process communicator rank per part (keto_comm_init_local).  It answers batches like a
+// Partition is a graph too large for one replica, edge-partitioned over the devices of the server
+// process: shared-rows parts (subject-set targets on every part, root rows by hash), one or more per
+// device (PlanParts), and one in-process communicator rank per part (keto_comm_init_local).  It answers batches like a
 // snapshot does: a batch is split over the ranks and every rank calls the collective routed entry
 // point with its slice -- an empty slice too -- on its own goroutine, so each request travels to
 // the part owning its row and its decision (or tree) comes back.  Batches run one at a time; every
@@ -95,8 +105,9 @@ type Partition struct {
 	comms []*Comm
 }
 
-// NewPartition partitions the host-only snapshot base over devices; base becomes part 0 (the
-// partition owns it), the other parts are host-only clones of it.
+// NewPartition partitions the host-only snapshot base over devices, one part per entry (a device
+// may appear more than once: its parts are separate ranks on it); base becomes part 0 (the partition
+// owns it), the other parts are host-only clones of it.
 func NewPartition(base *Snapshot, devices []int) (*Partition, error) {
 	if len(devices) == 0 {
 		return nil, errors.New("gpu: no device")
@@ -232,9 +243,83 @@ func (p *Partition) Close() {
 	p.comms, p.parts = nil, nil
 }
 
+// arenaCap is the largest arena a replica or a part takes on a device (KETO_ARENA_MAX_BYTES: handles
+// are 32-bit counts of 16-byte units).
+const arenaCap = uint64(C.KETO_ARENA_MAX_BYTES)
+
+// maxParts bounds the partitions PlanParts tries (every part holds all the subject-set targets).
+const maxParts = 64
+
+// PlanParts picks the shared-rows parts of a snapshot that does not fit a replica, and the device of
+// each: the fewest parts -- at least one per device, dealt to the devices in turn, so a device may
+// hold several -- such that every part's arena stays within arenaCap and each device's parts fit its
+// free memory.  Part sizes are estimated from the one-part statistics (every part keeps the targets,
+// the root rows split by hash; an eighth of margin), and the first plan the estimate admits is then
+// checked part by part.  A graph whose root rows pass 64 GiB is so served from one GPU too.
+func PlanParts(base *Snapshot, devices []int) ([]int, error) {
+	if len(devices) == 0 {
+		return nil, errors.New("gpu: no device")
+	}
+	total, shared, err := base.PartStats(0, 1)
+	if err != nil {
+		return nil, err
+	}
+	free := make([]uint64, len(devices))
+	for i, d := range devices {
+		if free[i], _, err = DeviceMemory(d); err != nil {
+			return nil, err
+		}
+	}
+	roots := uint64(0)
+	if total > shared {
+		roots = total - shared
+	}
+	fits := func(P int, arena func(k int) (uint64, error)) (bool, error) {
+		load := make([]uint64, len(devices))
+		for k := 0; k < P; k++ {
+			a, err := arena(k)
+			if err != nil {
+				return false, err
+			}
+			if a > arenaCap {
+				return false, nil
+			}
+			load[k%len(devices)] += a + a/8 + workspaceBytes // + room for the rows writes add
+		}
+		for i := range devices {
+			if load[i] > free[i] {
+				return false, nil
+			}
+		}
+		return true, nil
+	}
+	for P := len(devices); P <= maxParts; P++ {
+		est := func(int) (uint64, error) { return shared + roots/uint64(P) + roots/uint64(8*P), nil }
+		ok, err := fits(P, est)
+		if err != nil {
+			return nil, err
+		}
+		if !ok {
+			continue
+		}
+		if ok, err = fits(P, func(k int) (uint64, error) { return base.PartArenaBytes(k, P) }); err != nil {
+			return nil, err
+		}
+		if ok {
+			plan := make([]int, P)
+			for k := range plan {
+				plan[k] = devices[k%len(devices)]
+			}
+			return plan, nil
+		}
+	}
+	return nil, errors.New("gpu: no partition of the snapshot fits the devices")
+}
+
 // Place builds the engines for a host-only snapshot base (consumed) on devices: replicas -- base
-// cloned to every device -- when the replicated arena fits each of them (mode "" or "auto") or when
-// mode is "replicate"; else (or with mode "partition") one Partition over all of them.
+// cloned to every device -- when the replicated arena is within arenaCap and fits each of them (mode
+// "" or "auto") or when mode is "replicate"; else (or with mode "partition") one Partition over the
+// parts PlanParts picks (one per device, or more when a part would pass arenaCap).
 func Place(base *Snapshot, devices []int, mode string) ([]Engine, error) {
 	if len(devices) == 0 {
 		base.Close()
@@ -251,9 +336,15 @@ func Place(base *Snapshot, devices []int, mode string) ([]Engine, error) {
 			base.Close()
 			return nil, err
 		}
+		replicate = replicate && arena <= arenaCap
 	}
 	if !replicate {
-		p, err := NewPartition(base, devices)
+		plan, err := PlanParts(base, devices)
+		if err != nil {
+			base.Close()
+			return nil, err
+		}
+		p, err := NewPartition(base, plan)
 		if err != nil {
 			return nil, err
 		}

@@ -342,6 +342,7 @@ void check_named(Snapshot& S, const keto_check_req* reqs, uint32_t n, int32_t gl
 extern "C" {
 
 int keto_abi_version(void) { return KETO_ABI_VERSION; }
+static_assert(KETO_ARENA_MAX_BYTES == keto::ARENA_MAX_WORDS * 4, "the header's arena cap is the engine's");
 
 const char* keto_last_error(void) { return g_err.c_str(); }
 

@@ -113,6 +113,13 @@ def test_multi_gpu_server_process():
     part = _code(open(os.path.join(GO, "internal", "gpu", "partition.go")).read())
     assert re.search(r"func Place\(base \*Snapshot, devices \[\]int, mode string\) \(\[\]Engine, error\)", part)
     assert "C.keto_device_memory(" in part and "C.keto_snapshot_part_stats_mode(" in part
+    # past the arena cap a replica cannot take (KETO_ARENA_MAX_BYTES), the snapshot is partitioned
+    # even onto one device: PlanParts deals parts to the devices in turn, several per device if need be
+    assert "C.KETO_ARENA_MAX_BYTES" in part and "arena <= arenaCap" in part
+    assert re.search(r"func PlanParts\(base \*Snapshot, devices \[\]int\) \(\[\]int, error\)", part)
+    assert "plan[k] = devices[k%len(devices)]" in part and "NewPartition(base, plan)" in part
+    hdr = open(os.path.join(ROOT, "include", "keto_mi355x.h")).read()
+    assert re.search(r"#define KETO_ARENA_MAX_BYTES \(64ull << 30\)", hdr)
     bat = _code(open(os.path.join(GO, "internal", "gpu", "batcher.go")).read())
     assert re.search(r"func NewBatcher\(snaps \[\]Engine,", bat)
     assert re.search(r"func NewExpandBatcher\(snaps \[\]Engine,", bat)
