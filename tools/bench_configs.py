@@ -339,9 +339,10 @@ def config5(a, g=None):
             "gpu": {"trees_per_s": round(n / best, 1), "wall_ms": round(best * 1e3, 3),
                     "kernel_ms": round(kern, 3),
                     "what": "keto_expand_batch_ids: H2D roots, one pass (trees counted and staged in per-lane "
-                            "regions), host scan, second pass for trees that did not fit, id-run copies, gather to "
-                            "offsets, handle -> row ids, D2H tree arena; kernel_ms = the passes' tier kernels, the "
-                            "id-run copies and the gather (HIP events; not the handle -> row map)"},
+                            "regions, a tree past its region in an overflow chunk), id-run copies, host scan, gather "
+                            "to offsets with set handles -> row ids on the way (split trees piece by piece), a "
+                            "second pass only for trees that fit neither, D2H tree arena; kernel_ms = the passes' "
+                            "tier kernels, the id-run copies, the gather and the piece copies (HIP events)"},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern, 3),
                          "alg_bytes_per_root": round(per, 1),
