@@ -639,6 +639,8 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
                     std::chrono::duration<double, std::milli>(t2 - t1).count(),
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
         if (version_out) *version_out = S.version;
+        if (xl.owns_lock()) xl.unlock();             // (apply_mu still held: retired is the writer's)
+        S.retired.clear();
         return KETO_OK;
     });
 }

@@ -201,7 +201,8 @@ void pack_strings(uint64_t n, Get get, std::vector<uint64_t>& off, std::vector<c
     });
 }
 
-void unpack_strings(const std::vector<uint64_t>& off, const std::vector<char>& blob, std::vector<std::string>& out,
+template <class Out>   // std::vector<std::string> or Chunked<std::string>
+void unpack_strings(const std::vector<uint64_t>& off, const std::vector<char>& blob, Out& out,
                     unsigned threads, const char* what) {
     if (off.empty()) throw Error{KETO_E_INVALID, std::string("snapshot file: no offsets for ") + what};
     const uint64_t n = off.size() - 1;

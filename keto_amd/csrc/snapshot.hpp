@@ -13,6 +13,7 @@
 // walked edge by edge with full visited semantics.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <functional>
@@ -209,6 +210,46 @@ struct RwGate {
     void unlock_shared() { m.unlock_shared(); }
 };
 
+// A table that grows without moving its elements: fixed chunks of 2^SHIFT, so appending under the
+// snapshot's exclusive lock costs the appended elements (and a new chunk now and then), never a copy
+// of the whole table -- a std::vector of the 1B-tuple graph's ~220M strings moved 7 GB on the first
+// write that added a string, blocking every batch for ~2 s (profiles/r05aj_apply_1b_readers.log).
+template <class T, unsigned SHIFT = 16>
+struct Chunked {
+    static constexpr uint64_t CH = 1ull << SHIFT;
+    Chunked() = default;
+    Chunked(const Chunked& o) { *this = o; }
+    Chunked(Chunked&&) noexcept = default;
+    Chunked& operator=(Chunked&&) noexcept = default;
+    Chunked& operator=(const Chunked& o) {
+        if (this == &o) return *this;
+        resize(0);
+        resize(o.n);
+        for (uint64_t c = 0; c < o.chunks.size(); ++c)
+            std::copy(o.chunks[c].get(), o.chunks[c].get() + std::min(CH, o.n - c * CH), chunks[c].get());
+        return *this;
+    }
+    uint64_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    T& operator[](uint64_t i) { return chunks[i >> SHIFT][i & (CH - 1)]; }
+    const T& operator[](uint64_t i) const { return chunks[i >> SHIFT][i & (CH - 1)]; }
+    void resize(uint64_t m) {
+        for (uint64_t i = m; i < n && (i & (CH - 1)); ++i) (*this)[i] = T();   // the kept chunk's tail
+        chunks.resize((m + CH - 1) >> SHIFT);
+        for (auto& c : chunks)
+            if (!c) c.reset(new T[CH]());
+        n = m;
+    }
+    void push_back(T&& x) {
+        if (n == chunks.size() * CH) chunks.emplace_back(new T[CH]());
+        (*this)[n++] = std::move(x);
+    }
+
+   private:
+    std::vector<std::unique_ptr<T[]>> chunks;
+    uint64_t n = 0;
+};
+
 struct Snapshot {
     const uint64_t uid = next_snapshot_uid();   // never reused (caches keyed by snapshot use it, not its address)
     // ---- config
@@ -219,8 +260,7 @@ struct Snapshot {
     uint32_t page_size = 100;
 
     // ---- strings (byte order == id order)
-    std::vector<std::string> strs;
-    std::unordered_map<std::string_view, uint32_t> str_id;   // views into strs
+    Chunked<std::string> strs;
     uint32_t empty_str = ANY;                                // id of "" if present
 
     // ---- rows
@@ -299,6 +339,7 @@ struct Snapshot {
     std::unordered_map<uint32_t, RowPlace> row_place;
     std::vector<uint32_t> dirty;               // rows the last apply changed (device_apply's work list)
     std::vector<uint32_t> needs_cb;            // of them: rows that became subject-set targets without a filter
+    std::vector<std::shared_ptr<void>> retired;   // tables a commit replaced: freed after the exclusive lock
     // edges of row r in ORDER BY order (row-id encoded), whether or not a write changed it
     std::pair<const uint32_t*, uint64_t> row_edges(uint32_t r) const {
         auto it = row_over.find(r);

@@ -159,3 +159,30 @@ def test_apply_is_not_starved_by_readers():
     assert time.time() - t0 < 60
     assert sum(clones) > 0
     s.close()
+
+
+def test_string_table_grows_across_chunks(tmp_path):
+    """Writes append strings to a chunked table (Chunked, snapshot.hpp: 2^16 strings a chunk, never
+    moved) and rows to per-row tables grown before the exclusive lock (delta.cpp, Grown).  180,000
+    new strings on a 140,003-string build cross two chunk boundaries; every added and built name
+    still resolves and prints back, in the snapshot, a clone and a saved / loaded copy."""
+    ns = [(1, "docs")]
+    s = keto_amd.Snapshot.build(ns, [(1, f"d{i}", "view", f"u{i}") for i in range(70000)], device=-1)
+    for k in range(3):
+        s.apply([(1, f"n{k}_{i}", "view", f"w{k}_{i}") for i in range(30000)])
+    st = s.stats()
+    assert st["n_strings"] == 140003 + 180000 and st["n_rows"] == 160000, st
+    picks = [(k, i) for k in range(3) for i in (0, 1, 21844, 21845, 29999)]
+    reqs = [("docs", f"n{k}_{i}", "view", ("id", f"w{k}_{i}"), 0) for k, i in picks]
+    reqs += [("docs", "d5", "view", ("id", "u5"), 0), ("docs", "zz", "view", ("id", "nope"), 0)]
+    want = [("id", f"w{k}_{i}") for k, i in picks] + [("id", "u5")]
+    path = str(tmp_path / "snap.bin")
+    s.save(path)
+    for snap in (s, s.clone(device=-1), keto_amd.Snapshot.load(path, device=-1)[0]):
+        out, status = snap.resolve_checks(reqs)
+        assert (status == 0).all()
+        assert (out["row"][:-1] != 0xFFFFFFFF).all() and out["row"][-1] == 0xFFFFFFFF
+        assert snap.subject_fields([int(x) for x in out["target"][:-1]]) == want
+        assert snap.stats()["n_strings"] == st["n_strings"]
+    s.apply([(1, "n0_0", "view", "late")])
+    assert s.resolve_checks([("docs", "n0_0", "view", ("id", "late"), 0)])[0]["target"][0] == st["n_strings"]

@@ -7,7 +7,7 @@ the snapshot's shared lock (batches keep running) and commits it under the exclu
 waits for the running batch only to commit, and the next batch waits only for the commit.
 
   python tools/apply_concurrent.py [--k 100] [--gap-ms 20] [--seconds 5]
-  python tools/apply_concurrent.py --graph powerlaw1b --packed [--requests 1000000]
+  python tools/apply_concurrent.py --graph powerlaw1b --packed [--requests 1000000] [--readers 4]
 
 --graph powerlaw1b: the headline graph (config #4, 1B tuples) with its string table (the bench's
 string_form snapshot, keto_snapshot_from_csr + strings); writes add and remove direct
@@ -40,6 +40,11 @@ def main():
                     help="reads through keto_check_batch_packed (GPU resolution, the Go batcher's call)")
     ap.add_argument("--graph", choices=["drive10m", "powerlaw1b"], default="drive10m")
     ap.add_argument("--requests", type=int, default=1_000_000)
+    ap.add_argument("--new-rows", action="store_true",
+                    help="each write's tuples name new objects: every write adds K rows (and strings)")
+    ap.add_argument("--readers", type=int, default=1,
+                    help="reader threads running batches side by side (the snapshot lock is writer-preferring: "
+                         "a waiting write holds new batches back, so readers cannot starve it)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -81,15 +86,23 @@ def main():
             lat.append(time.perf_counter() - t0)
             bad.append(int((out != before).sum()))
 
+    def read_threads(seconds, lat, bad):
+        ts = [threading.Thread(target=reads, args=(seconds, lat, bad)) for _ in range(a.readers)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+
     quiet, quiet_bad = [], []
-    reads(a.seconds / 2, quiet, quiet_bad)
+    read_threads(a.seconds / 2, quiet, quiet_bad)
     stop = threading.Event()
     wlat, serial = [], [0]
 
     def writer():
         while not stop.is_set():
             rows = rng.choice(files_view, size=a.k, replace=False)
-            ins = [(doc_ns, hx(g.row_obj[r]), "view", f"uw{serial[0] + i:08x}") for i, r in enumerate(rows)]
+            ins = [(doc_ns, f"nw{serial[0] + i:08x}" if a.new_rows else hx(g.row_obj[r]), "view",
+                    f"uw{serial[0] + i:08x}") for i, r in enumerate(rows)]
             serial[0] += a.k
             t0 = time.perf_counter()
             snap.apply(inserts=ins)
@@ -100,12 +113,12 @@ def main():
     loaded, loaded_bad = [], []
     w = threading.Thread(target=writer)
     w.start()
-    reads(a.seconds, loaded, loaded_bad)
+    read_threads(a.seconds, loaded, loaded_bad)
     stop.set()
     w.join()
     out = {"graph": label, "tuples": int(g.n_edges), "setup_s": round(t_setup, 1),
            "reads": "keto_check_batch_packed (GPU resolution)" if a.packed else "keto_check_batch (host resolution)",
-           "requests_per_batch": len(q), "write_tuples": a.k, "write_gap_ms": a.gap_ms,
+           "requests_per_batch": len(q), "reader_threads": a.readers, "write_tuples": a.k, "writes_add_rows": a.new_rows, "write_gap_ms": a.gap_ms,
            "batch_ms_quiet": {"p50": pct(quiet, 50), "p99": pct(quiet, 99), "n": len(quiet)},
            "batch_ms_with_writes": {"p50": pct(loaded, 50), "p99": pct(loaded, 99), "n": len(loaded)},
            "write_ms_under_reads": {"p50": pct(wlat, 50), "p99": pct(wlat, 99), "n": len(wlat)},
