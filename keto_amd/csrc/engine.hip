@@ -3354,8 +3354,8 @@ uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint
 // Closure filters after a write (device_apply): rounds of closure_pass over the rows with a filter
 // and subject sets until one changes nothing, then the child signatures of every row with a filter
 // -- as build_closures, on the snapshot's stream, over row lists kept on the device from the last
-// write: they are rebuilt only when this write gave a row a new identity (fresh) or changed whether
-// a row takes part (its first subject set, or its last, or the ordered path)
+// write: they are rebuilt only when this write gave a target row a new identity (fresh) or changed
+// whether a row takes part (its first subject set, or its last, or the ordered path)
 void apply_closures(Snapshot& S, DeviceState& D, bool fresh) {
     const uint32_t R = S.n_rows();
     // only rows some subject set points at carry a filter: a write that changed none of them (e.g.
@@ -3371,10 +3371,14 @@ void apply_closures(Snapshot& S, DeviceState& D, bool fresh) {
     auto in_list = [&](uint32_t r) {
         return S.row_cb[r] && S.present(r) && S.rows[r].n_sets > 0 && !(S.row_flags(r) & ROW_SEQ);
     };
-    bool valid = D.cl_valid && !fresh && D.cl_in.size() == R;
+    // rows past the lists' last build (rows writes added since) are in neither list until a check
+    // here finds one that belongs: every added row is dirty in the write that adds it, so a write of
+    // new root rows keeps the lists (rebuilding them scanned every row: 322 ms a write on the 1B graph,
+    // profiles/r05ak_apply_1b_new_rows.log)
+    bool valid = D.cl_valid && !fresh && D.cl_in.size() <= R;
     for (uint32_t r : S.dirty) {
         if (!valid) break;
-        if (r >= R || (uint8_t)in_list(r) != D.cl_in[r]) valid = false;
+        if (r >= R || (uint8_t)in_list(r) != (r < D.cl_in.size() ? D.cl_in[r] : 0u)) valid = false;
     }
     if (!valid) {
         std::vector<uint32_t> list, all;
@@ -3601,7 +3605,8 @@ bool apply_in_place(Snapshot& S) {
     HIP_OK(hipStreamSynchronize(D.stream));
     lap("copies");
     // 4. closure filters of every row with one (from their own ids up)
-    apply_closures(S, D, !fresh.empty());
+    // (a fresh root row carries no filter and is in no closure list: only fresh targets rebuild them)
+    apply_closures(S, D, std::any_of(fresh.begin(), fresh.end(), [&](uint32_t r) { return S.row_cb[r] != 0; }));
     lap("closures");
     // 5. what the kernels and expand output read next: the collision table when a write added
     // classes or gave a classed row a new identity handle
@@ -3628,49 +3633,64 @@ bool apply_in_place(Snapshot& S) {
         S.layout_units.swap(lu);
         S.rows_by_unit.swap(rbu);
     }
-    // 6. the lazily built maps: the rows with a fresh identity are patched in (row -> handle,
-    // handle -> row) while they fit; past their room, or with no direct handle map, the maps are
-    // rebuilt by the next batch that needs them.  (An old identity keeps its stale entry: only
-    // top-level handles resolved before the write reach it, through its forward.)
-    // rows the write added that got no handle here (another part's root rows) still need their
-    // NO_UNIT entry in the row -> handle map: the map's slack past its rows is uninitialized
+    // 6. the lazily built maps, each on its own: the rows with a fresh identity are patched into
+    // whichever of them exists (row -> handle, handle -> row) while they fit; a map past its room is
+    // dropped and rebuilt by the next batch that needs it.  (Both were dropped when either was missing:
+    // with no expand since the build -- no handle -> row map -- every row-adding write made the next
+    // check re-upload the whole row -> handle map, 1.2 GB and ~12 ms at the 1B graph,
+    // profiles/r05am_apply_rows_lock_trace.log.)  An old identity keeps its stale entry: only top-level
+    // handles resolved before the write reach it, through its forward.  Rows the write added that got
+    // no handle here (another part's root rows) still need their NO_UNIT entry in the row -> handle
+    // map: the map's slack past its rows is uninitialized
     const bool grew = D.row_handle && S.n_rows() > D.row_handle_rows;
-    const bool patch = (!fresh.empty() || grew) && D.row_handle && S.n_rows() <= D.row_handle_cap && D.unit_row &&
-                       S.n_units <= D.unit_row_cap && fresh.size() + (S.n_rows() - D.row_handle_rows) <= (1u << 20);
-    if ((!fresh.empty() || grew) && !patch) {
-        for (uint32_t** p : {&D.row_handle, &D.layout_units, &D.rows_by_unit, &D.unit_row})
-            if (*p) {
-                (void)hipFree(*p);
-                *p = nullptr;
-            }
-        D.row_handle_cap = D.unit_row_cap = D.row_handle_rows = 0;
-    } else if (patch) {
+    if (!fresh.empty() || grew) {
+        const bool rh_ok = D.row_handle && S.n_rows() <= D.row_handle_cap &&
+                           fresh.size() + (S.n_rows() - D.row_handle_rows) <= (1u << 20);
+        const bool ur_ok = D.unit_row && S.n_units <= D.unit_row_cap && fresh.size() <= (1u << 20);
+        if (D.row_handle && !rh_ok) {
+            (void)hipFree(D.row_handle);
+            D.row_handle = nullptr;
+            D.row_handle_cap = D.row_handle_rows = 0;
+        }
+        if (D.unit_row && !ur_ok) {
+            (void)hipFree(D.unit_row);
+            D.unit_row = nullptr;
+            D.unit_row_cap = 0;
+        }
         // (row, handle) for row_handle: the fresh rows and every row the write added; (handle, row)
         // for unit_row: the fresh rows
         std::vector<uint32_t> rh, hr;
         for (uint32_t r : fresh) {
-            rh.push_back(r);
-            rh.push_back(S.unit_of_row[r]);
-            hr.push_back(S.unit_of_row[r]);
-            hr.push_back(r);
+            if (rh_ok) {
+                rh.push_back(r);
+                rh.push_back(S.unit_of_row[r]);
+            }
+            if (ur_ok) {
+                hr.push_back(S.unit_of_row[r]);
+                hr.push_back(r);
+            }
         }
-        for (uint64_t r = D.row_handle_rows; r < S.n_rows(); ++r) {
-            rh.push_back((uint32_t)r);
-            rh.push_back(S.unit_of_row[r]);
+        if (rh_ok) {
+            for (uint64_t r = D.row_handle_rows; r < S.n_rows(); ++r) {
+                rh.push_back((uint32_t)r);
+                rh.push_back(S.unit_of_row[r]);
+            }
+            D.row_handle_rows = S.n_rows();
         }
-        D.row_handle_rows = S.n_rows();
-        std::vector<uint32_t> pr(rh);
-        pr.insert(pr.end(), hr.begin(), hr.end());
-        uint32_t* d_pr = nullptr;
-        HIP_OK(hipMalloc(&d_pr, std::max<size_t>(1, pr.size()) * sizeof(uint32_t)));
-        HIP_OK(hipMemcpyAsync(d_pr, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, D.stream));
-        const uint32_t n1 = (uint32_t)(rh.size() / 2), n2 = (uint32_t)(hr.size() / 2);
-        if (n1) hipLaunchKernelGGL(scatter_pairs, dim3((n1 + 255) / 256), dim3(256), 0, D.stream, D.row_handle, d_pr, n1);
-        if (n2) hipLaunchKernelGGL(scatter_pairs, dim3((n2 + 255) / 256), dim3(256), 0, D.stream, D.unit_row, d_pr + rh.size(), n2);
-        HIP_OK(hipGetLastError());
-        HIP_OK(hipStreamSynchronize(D.stream));
-        (void)hipFree(d_pr);
-        // the device handle lists are used only without the direct map: leave them to a rebuild
+        if (!rh.empty() || !hr.empty()) {
+            std::vector<uint32_t> pr(rh);
+            pr.insert(pr.end(), hr.begin(), hr.end());
+            uint32_t* d_pr = nullptr;
+            HIP_OK(hipMalloc(&d_pr, pr.size() * sizeof(uint32_t)));
+            HIP_OK(hipMemcpyAsync(d_pr, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice, D.stream));
+            const uint32_t n1 = (uint32_t)(rh.size() / 2), n2 = (uint32_t)(hr.size() / 2);
+            if (n1) hipLaunchKernelGGL(scatter_pairs, dim3((n1 + 255) / 256), dim3(256), 0, D.stream, D.row_handle, d_pr, n1);
+            if (n2) hipLaunchKernelGGL(scatter_pairs, dim3((n2 + 255) / 256), dim3(256), 0, D.stream, D.unit_row, d_pr + rh.size(), n2);
+            HIP_OK(hipGetLastError());
+            HIP_OK(hipStreamSynchronize(D.stream));
+            (void)hipFree(d_pr);
+        }
+        // the arena-order handle lists (expand output without the direct map): rebuilt when needed
         for (uint32_t** p : {&D.layout_units, &D.rows_by_unit})
             if (*p) {
                 (void)hipFree(*p);
