@@ -143,6 +143,24 @@ def test_packed_empty_batch_and_bad_offsets():
     packed["off"][0] = 1000
     with pytest.raises(KetoError):
         snap.check_batch_packed(blob, packed, 5)
+    # the bounds are checked on the device (resolve_packed): the first request past the blob is named,
+    # no field of it is read, nothing is written to the outputs, and the snapshot answers afterwards
+    reqs = [("n", "a", "r", ("id", "u"), 0), ("n", "a", "r", ("id", "x"), 0), ("n", "", "r", ("id", "u"), 0),
+            ("n", "a", "r", ("set", "n", "a", "r"), 0)]
+    blob, packed = pack_requests(reqs)
+    for bad, (field, value) in ((1, ("off", len(blob) - 1)), (3, ("len", 0xFFFF))):
+        p = packed.copy()
+        if field == "off":
+            p["off"][bad] = value
+        else:
+            p["len"][bad][5] = value
+        allowed = np.full(len(reqs), 7, dtype=np.uint8)
+        with pytest.raises(KetoError, match=f"request {bad}'s fields lie outside the blob"):
+            snap.check_batch_packed(blob, p, 5, allowed=allowed)
+        assert (allowed == 7).all()
+    got, st = snap.check_batch_packed(blob, packed, 5)                    # (request 2: a wildcard, host)
+    want, want_st = snap.check_batch(reqs, 5)
+    assert (got == want).all() and (st == want_st).all() and got[0] == 1 and got[1] == 0
     snap.close()
 
 
