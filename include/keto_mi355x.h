@@ -367,7 +367,12 @@ int keto_check_batch(keto_snapshot* s, const keto_check_req* reqs, uint32_t n, i
  * internal/check/engine.go:116-123): decisions and statuses equal keto_check_batch's on the same
  * requests.  Requests with an empty namespace, object or relation (wildcard queries, in the subject
  * set too) are resolved on the host as keto_check_batch does.  blob_len < 2^32; fields of up to
- * 65535 bytes (longer ones: keto_check_batch). */
+ * 65535 bytes (longer ones: keto_check_batch).  A request whose fields lie outside the blob fails the
+ * call (KETO_E_INVALID, naming the first such request) before anything is written to the outputs.
+ * Large batches are pipelined (pieces of KETO_PACKED_CHUNK requests, default 2^21, uploaded while
+ * earlier pieces are resolved and checked): fastest when the strings are packed in request order, as
+ * the Go batcher packs them; any other layout gives the same answers after a second pass.  Pinned
+ * blob and records (keto_host_alloc) let the upload run asynchronously. */
 typedef struct {
     uint32_t off;               /* byte offset of the request's first field in blob */
     uint16_t len[6];            /* namespace, object, relation, subject id | set namespace, set object, set relation */

@@ -192,13 +192,17 @@ __device__ int64_t query_row_dev(const ResolveDev& R, const uint8_t* f, uint32_t
 
 // cnt[0]: the first request whose fields lie outside the blob (atomicMin; NO_BAD = none) -- its fields
 // are not read; cnt[1]: how many requests the host resolves (wildcard queries).  Both were host loops
-// over every record before (~20 ms of a 16.7M-request batch's 40.7 ms, profiles/r05ap_*).
+// over every record before (~20 ms of a 16.7M-request batch's 40.7 ms, profiles/r05ap_*).  Requests
+// [i0, i0 + n); the bytes [lo, hi) of the blob are on the device so far (a pipelined batch uploads it
+// piece by piece): a request with a field outside them is counted in cnt[2] and left for a second
+// pass once the whole blob is there.
 __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                      const keto_check_packed* __restrict__ q, uint32_t n,
-                                                      keto_check_ids* __restrict__ out, uint8_t* __restrict__ status,
-                                                      uint32_t* __restrict__ cnt) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+                                                      uint64_t lo, uint64_t hi, const keto_check_packed* __restrict__ q,
+                                                      uint32_t i0, uint32_t n, keto_check_ids* __restrict__ out,
+                                                      uint8_t* __restrict__ status, uint32_t* __restrict__ cnt) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t i = i0 + k;
     const keto_check_packed p = q[i];
     const uint8_t* f = blob + p.off;
     keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0u, p.max_depth};
@@ -208,6 +212,8 @@ __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_
     if ((uint64_t)p.off + len > blob_len) {
         atomicMin(cnt, i);
         st = ST_HOST;                                                      // (the batch fails)
+    } else if (p.off < lo || (uint64_t)p.off + len > hi) {
+        atomicAdd(cnt + 2, 1u);                                            // (the batch is resolved again)
     } else if (!p.len[0] || !p.len[1] || !p.len[2] || (set && (!p.len[3] || !p.len[4] || !p.len[5]))) {
         st = ST_HOST;                                                      // a wildcard query: the host
         atomicAdd(cnt + 1, 1u);
@@ -257,11 +263,15 @@ struct RDevState {
     bool base_ready = false;       // the build's string and row indexes and the namespaces (fixed after the build)
     std::mutex mu;                 // one packed batch at a time per snapshot
     hipStream_t stream = nullptr;
+    hipStream_t copy = nullptr;    // a pipelined batch's uploads
+    std::vector<hipEvent_t> ev;    // piece k's bytes are on the device
     RBuf str_slots, str_bytes, str_off, add_slots, add_bytes, add_off, row_slots, extra_slots, ns_bytes, ns_off, ns_id;
     ResolveDev view{};
     RBuf blob, reqs, ids, status, dec, cnt;
     ~RDevState() {
         (void)hipSetDevice(device);
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -291,6 +301,7 @@ RDevState& rdev_get(Snapshot& S, int device) {
         std::unique_ptr<RDevState, RDevStateDeleter> r(new RDevState);
         r->device = device;
         HIP_OK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking));
         S.rdev = std::move(r);
     }
     return *S.rdev;
@@ -398,6 +409,23 @@ void rdev_refresh(Snapshot& S, RDevState& R) {
 
 }  // namespace
 
+namespace {
+// requests per piece of a pipelined packed batch (KETO_PACKED_CHUNK; 0 = one piece)
+uint64_t packed_chunk() {
+    const char* e = getenv("KETO_PACKED_CHUNK");
+    return e ? (uint64_t)std::max(0ll, atoll(e)) : (1ull << 21);
+}
+}  // namespace
+
+// A batch of 2 pieces or more on an unpartitioned snapshot is pipelined: the blob and the records go
+// up in pieces on R.copy while the compute stream resolves and checks each piece once its bytes are
+// there, so the resolution and the check hide under the upload, which is the floor (821 MB of a
+// 16.7M-request batch: 14.5 ms of its 21.6 ms unpipelined, profiles/r05aq_string_form_trace.txt).
+// Piece k's blob window comes from the records at the piece boundaries, exact for a batch packed in
+// request order (the Go batcher's and the generator's); a request whose fields lie outside its window
+// is counted by resolve_packed, and then the whole batch is resolved and checked again over the whole
+// blob.  The bounds error is raised before anything is written to the outputs, as unpipelined;
+// (a partitioned snapshot is never pipelined: its misrouted-row error must not precede it).
 void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs, uint32_t n,
                          int32_t gmd, uint8_t* allowed, uint8_t* status, std::vector<uint32_t>& host) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
@@ -409,24 +437,83 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
     lock_trace("packed: R.mu");
     rdev_refresh(S, R);
     lock_trace("packed: refreshed");
-    hipStream_t st = R.stream;
-    const uint8_t* d_blob = upload(R.blob, blob, blob_len, st);
-    const keto_check_packed* d_q = upload(R.reqs, reqs, n, st);
+    hipStream_t st = R.stream, cs = R.copy;
+    struct Drain {                       // no copy from the caller's memory outlives the call
+        hipStream_t a, b;
+        ~Drain() {
+            (void)hipStreamSynchronize(a);
+            (void)hipStreamSynchronize(b);
+        }
+    } drain{cs, st};
+    const uint64_t chunk = packed_chunk();
+    uint32_t K = 1;
+    if (chunk && S.n_parts == 1 && n >= 2 * chunk) K = (uint32_t)std::min<uint64_t>(64, (n + chunk - 1) / chunk);
+    std::vector<uint32_t> cb(K + 1);
+    std::vector<uint64_t> wb(K + 1);
+    for (uint32_t k = 0; k <= K; ++k) cb[k] = (uint32_t)((uint64_t)n * k / K);
+    wb[0] = 0;
+    wb[K] = blob_len;
+    for (uint32_t k = 1; k < K; ++k) wb[k] = std::min<uint64_t>(blob_len, std::max<uint64_t>(wb[k - 1], reqs[cb[k]].off));
+    uint8_t* d_blob = R.blob.get<uint8_t>(std::max<uint64_t>(blob_len, 1));
+    keto_check_packed* d_q = R.reqs.get<keto_check_packed>(std::max<uint32_t>(n, 1));
     keto_check_ids* d_ids = R.ids.get<keto_check_ids>(n);
     uint8_t* d_st = R.status.get<uint8_t>(n);
     uint8_t* d_dec = R.dec.get<uint8_t>(n);
-    uint32_t* d_cnt = R.cnt.get<uint32_t>(2);
-    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
-    HIP_OK(hipMemsetAsync(d_cnt + 1, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(resolve_packed, dim3((n + 255) / 256), dim3(256), 0, st, R.view, d_blob, blob_len, d_q, n, d_ids,
-                       d_st, d_cnt);
-    HIP_OK(hipGetLastError());
-    uint32_t cnt[2] = {NO_BAD, 0u};
-    HIP_OK(hipMemcpyAsync(cnt, d_cnt, sizeof cnt, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));                                      // (before the check, as the host loop was)
-    if (cnt[0] != NO_BAD)
-        throw Error{KETO_E_INVALID, "request " + std::to_string(cnt[0]) + "'s fields lie outside the blob"};
-    device_check_rows(S, d_ids, n, gmd, d_dec, st);                        // row ids -> handles, the check
+    uint32_t* d_cnt = R.cnt.get<uint32_t>(3);
+    while (R.ev.size() < K) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        R.ev.push_back(e);
+    }
+    if (K > 1) HIP_OK(hipEventRecord(R.ev[0], st));                        // (the buffers are free: the last
+    for (uint32_t k = 0; k < K; ++k) {                                     //  call's work on st is done)
+        if (k == 0 && K > 1) HIP_OK(hipStreamWaitEvent(cs, R.ev[0], 0));
+        hipStream_t s = K > 1 ? cs : st;
+        if (wb[k + 1] > wb[k])
+            HIP_OK(hipMemcpyAsync(d_blob + wb[k], blob + wb[k], wb[k + 1] - wb[k], hipMemcpyHostToDevice, s));
+        if (cb[k + 1] > cb[k])
+            HIP_OK(hipMemcpyAsync(d_q + cb[k], reqs + cb[k], (uint64_t)(cb[k + 1] - cb[k]) * sizeof(keto_check_packed),
+                                  hipMemcpyHostToDevice, s));
+        if (K > 1) HIP_OK(hipEventRecord(R.ev[k], cs));
+    }
+    auto reset = [&] {
+        HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
+        HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 2 * sizeof(uint32_t), st));
+    };
+    auto resolve = [&](uint32_t i0, uint32_t m, uint64_t hi) {
+        if (!m) return;
+        hipLaunchKernelGGL(resolve_packed, dim3((m + 255) / 256), dim3(256), 0, st, R.view, d_blob, blob_len, 0ull, hi,
+                           d_q, i0, m, d_ids, d_st, d_cnt);
+        HIP_OK(hipGetLastError());
+    };
+    uint32_t cnt[3] = {NO_BAD, 0u, 0u};
+    auto read_cnt = [&] {
+        HIP_OK(hipMemcpyAsync(cnt, d_cnt, sizeof cnt, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+    };
+    reset();
+    if (K == 1) {
+        resolve(0, n, blob_len);
+        read_cnt();                                                        // (before the check, as the host loop was)
+        if (cnt[0] != NO_BAD)
+            throw Error{KETO_E_INVALID, "request " + std::to_string(cnt[0]) + "'s fields lie outside the blob"};
+        device_check_rows(S, d_ids, n, gmd, d_dec, st);                    // row ids -> handles, the check
+    } else {
+        for (uint32_t k = 0; k < K; ++k) {
+            HIP_OK(hipStreamWaitEvent(st, R.ev[k], 0));
+            resolve(cb[k], cb[k + 1] - cb[k], wb[k + 1]);
+            device_check_rows(S, d_ids + cb[k], cb[k + 1] - cb[k], gmd, d_dec + cb[k], st);
+        }
+        read_cnt();
+        if (cnt[0] != NO_BAD)
+            throw Error{KETO_E_INVALID, "request " + std::to_string(cnt[0]) + "'s fields lie outside the blob"};
+        if (cnt[2]) {                                                      // not packed in request order
+            reset();
+            resolve(0, n, blob_len);
+            read_cnt();
+            device_check_rows(S, d_ids, n, gmd, d_dec, st);
+        }
+    }
     lock_trace("packed: checked");
     hipLaunchKernelGGL(fold_undecided, dim3((n + 255) / 256), dim3(256), 0, st, d_dec, d_st, n);
     HIP_OK(hipGetLastError());

@@ -133,6 +133,47 @@ def test_powerlaw_packed_matches_host():
     g.close()
 
 
+@pytest.mark.parametrize("layout", ["in_order", "shuffled"])
+def test_packed_pipelined_pieces(layout, monkeypatch):
+    """A batch of several pieces (KETO_PACKED_CHUNK) is uploaded piece by piece while earlier pieces
+    are resolved and checked (resolve_dev.hip, device_check_packed).  In request order each piece's
+    strings are in its window; shuffled records (fields anywhere in the blob) are found by the kernel
+    and the batch is resolved and checked again over the whole blob.  Both equal keto_check_batch;
+    a bounds error in the last piece still fails the call before any output is written."""
+    from keto_amd.capi import KetoError
+    from tools import synth
+    monkeypatch.setenv("KETO_PACKED_CHUNK", "4096")
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 1024), threads=16)
+    st = g.string_tuples(seed=5)
+    snap, _ = g.snapshot_from_strings(st, device=0)
+    q = g.queries(50_000, seed=13, depth=5)
+    arr = g.string_requests(st, q)
+    want, want_st = snap.check_batch_reqs(arr, len(q), 5)
+    blob, rec, used = g.pack_requests(arr, len(q))
+    b, r = blob.array[:used], rec.array[:len(q)]          # (pinned: the pieces' copies are asynchronous)
+    if layout == "shuffled":                 # the same records, the blob's strings in another order
+        perm = np.random.default_rng(3).permutation(len(q))
+        lens = r["len"].astype(np.int64).sum(axis=1)
+        parts, off, new_off = [], 0, np.zeros(len(q), dtype=np.uint32)
+        for i in perm:
+            parts.append(b[r["off"][i]:r["off"][i] + lens[i]])
+            new_off[i] = off
+            off += lens[i]
+        b = np.concatenate(parts)
+        r = r.copy()
+        r["off"] = new_off
+    got, got_st = snap.check_batch_packed(b, r, 5, n=len(q))
+    assert (got == want).all() and (got_st == want_st).all()
+    bad = r.copy()
+    bad["off"][len(q) - 3] = len(b) - 1
+    out = np.full(len(q), 7, dtype=np.uint8)
+    with pytest.raises(KetoError, match=f"request {len(q) - 3}'s fields lie outside the blob"):
+        snap.check_batch_packed(b, bad, 5, n=len(q), allowed=out)
+    assert (out == 7).all()
+    snap.close()
+    g.close()
+
+
 def test_packed_empty_batch_and_bad_offsets():
     import keto_amd
     from keto_amd.capi import CHECK_PACKED_DTYPE, KetoError, pack_requests
