@@ -8,7 +8,8 @@
 //
 // cgo pointer rules: the C side keeps no pointer after a call returns (keto_mi355x.h), and every
 // array handed to it lives in C memory (one C.malloc'd block of structs plus one of string bytes
-// per call), so no Go pointer is ever passed inside a struct.
+// per call, or a large packed batch's page-locked arena from keto_host_alloc), so no Go pointer is
+// ever passed inside a struct.
 package gpu
 
 /*
@@ -22,6 +23,7 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"sync"
 	"unsafe"
 
 	"github.com/ory/keto/internal/namespace"
@@ -117,6 +119,52 @@ type Row struct {
 type Snapshot struct {
 	h       *C.keto_snapshot
 	Version uint64 // bumped by every Apply (snapshot lifecycle, see apply.go)
+	arena   pinnedArena
+}
+
+// pinnedArena is a snapshot's page-locked buffer for large packed batches (keto_host_alloc), reused
+// from call to call and grown when a batch needs more.  keto_check_batch_packed uploads a batch from
+// it asynchronously, piece by piece under the resolution and check of earlier pieces; from C.malloc'd
+// memory the runtime stages every copy through its own bounce buffers, synchronously.  Pinning maps
+// and locks every page, so it is paid once per size, not per call.
+type pinnedArena struct {
+	mu sync.Mutex
+	p  unsafe.Pointer
+	n  int
+}
+
+// pinMin is the smallest packed batch (bytes of strings, records and outputs) that uses the arena.
+const pinMin = 1 << 20
+
+// get locks the arena and returns it with at least n bytes; ok = false (and unlocked) when pinning
+// failed, and the caller uses C memory instead.
+func (a *pinnedArena) get(n int) (unsafe.Pointer, bool) {
+	a.mu.Lock()
+	if n > a.n {
+		if a.p != nil {
+			C.keto_host_free(a.p)
+			a.p, a.n = nil, 0
+		}
+		grow := n + n/4
+		var p unsafe.Pointer
+		if rc := C.keto_host_alloc(C.uint64_t(grow), &p); rc != C.KETO_OK || p == nil {
+			a.mu.Unlock()
+			return nil, false
+		}
+		a.p, a.n = p, grow
+	}
+	return a.p, true
+}
+
+func (a *pinnedArena) put() { a.mu.Unlock() }
+
+func (a *pinnedArena) free() {
+	a.mu.Lock()
+	if a.p != nil {
+		C.keto_host_free(a.p)
+		a.p, a.n = nil, 0
+	}
+	a.mu.Unlock()
 }
 
 // rowsLen is the string bytes of rows (one arena per call).
@@ -266,6 +314,7 @@ func (s *Snapshot) Close() {
 		C.keto_snapshot_release(s.h)
 		s.h = nil
 	}
+	s.arena.free()
 }
 
 func subjectLen(sub relationtuple.Subject) int {
@@ -343,8 +392,26 @@ func (s *Snapshot) checkPacked(reqs []*relationtuple.InternalRelationTuple, dept
 	}
 	var m cmem
 	defer m.free()
-	m.strings(total)
-	rec := (*C.keto_check_packed)(m.alloc(n * int(C.sizeof_keto_check_packed)))
+	// strings, records (8-B aligned), decisions and statuses: one pinned arena for a large batch
+	strBytes := (total + 7) &^ 7
+	recBytes := n * int(C.sizeof_keto_check_packed)
+	var rec *C.keto_check_packed
+	var allowed, status *C.uint8_t
+	if size := strBytes + recBytes + 2*n; size >= pinMin {
+		if base, ok := s.arena.get(size); ok {
+			defer s.arena.put()
+			m.str = base
+			rec = (*C.keto_check_packed)(unsafe.Add(base, strBytes))
+			allowed = (*C.uint8_t)(unsafe.Add(base, strBytes+recBytes))
+			status = (*C.uint8_t)(unsafe.Add(base, strBytes+recBytes+n))
+		}
+	}
+	if rec == nil {
+		m.strings(total)
+		rec = (*C.keto_check_packed)(m.alloc(recBytes))
+		allowed = (*C.uint8_t)(m.alloc(n))
+		status = (*C.uint8_t)(m.alloc(n))
+	}
 	rs := unsafe.Slice(rec, n)
 	for i, r := range reqs {
 		f, k, kind := packedFields(r)
@@ -355,8 +422,6 @@ func (s *Snapshot) checkPacked(reqs []*relationtuple.InternalRelationTuple, dept
 		}
 		rs[i] = p
 	}
-	allowed := (*C.uint8_t)(m.alloc(n))
-	status := (*C.uint8_t)(m.alloc(n))
 	if rc := C.keto_check_batch_packed(s.h, (*C.char)(m.str), C.uint64_t(m.used), rec, C.uint32_t(n),
 		C.int32_t(globalMax), allowed, status); rc != C.KETO_OK {
 		return nil, nil, true, lastErr(rc)

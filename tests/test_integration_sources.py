@@ -224,3 +224,18 @@ def test_collective_calls_never_skip_an_empty_batch():
     assert len(re.findall(r"checkWith\(reqs, depths, true,", comm)) == 2
     assert "if n == 0 && !collective {" in gpu_go
     assert "C.keto_comm_init_local(" in comm
+
+
+def test_packed_batches_use_a_reused_pinned_arena():
+    """A large packed batch goes up from a page-locked arena (keto_host_alloc) the snapshot keeps
+    from call to call, so keto_check_batch_packed can upload it asynchronously under the resolution
+    and check of earlier pieces; the arena is locked for the call and freed with the snapshot."""
+    src = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
+    body = src[src.index("func (s *Snapshot) checkPacked("):]
+    body = body[:body.index("\nfunc ")]
+    assert "s.arena.get(" in body and "defer s.arena.put()" in body
+    assert body.index("s.arena.get(") < body.index("C.keto_check_batch_packed(")
+    arena = src[src.index("func (a *pinnedArena) get("):]
+    assert "C.keto_host_alloc(" in arena and "C.keto_host_free(" in arena and "a.mu.Lock()" in arena
+    close = src[src.index("func (s *Snapshot) Close()"):]
+    assert "s.arena.free()" in close[:close.index("\n}")]
