@@ -7,6 +7,8 @@ import (
 	"context"
 	"errors"
 	"fmt"
+	"os"
+	"strconv"
 	"sync"
 	"time"
 
@@ -197,10 +199,24 @@ type checkReq struct {
 	depth int
 }
 
+// CheckFlushFromEnv is the check batcher's flush size, KETO_GPU_CHECK_BATCH requests (default 65,536,
+// at most 2^24).  Larger batches trade latency for throughput: on the 1B-tuple graph a packed batch
+// of 65,536 requests takes 0.34 ms (~190 M checks/s per GPU), one of 1M 1.66 ms (~600 M checks/s),
+// profiles/r05as_packed_*.log.
+func CheckFlushFromEnv() int {
+	if v, err := strconv.Atoi(os.Getenv("KETO_GPU_CHECK_BATCH")); err == nil && v > 0 {
+		if v > 1<<24 {
+			v = 1 << 24
+		}
+		return v
+	}
+	return 1 << 16
+}
+
 // NewBatcher starts the flush loop over the engines (one snapshot per GPU, or a partition).
 func NewBatcher(snaps []Engine, globalMax func() int, fb Fallback) *Batcher {
 	b := &Batcher{rep: newReplicas(snaps), GlobalMax: globalMax, Fallback: fb}
-	b.c = newCoalescer(1<<16, 200*time.Microsecond, b.flush, b.fallbackAll)
+	b.c = newCoalescer(CheckFlushFromEnv(), 200*time.Microsecond, b.flush, b.fallbackAll)
 	return b
 }
 

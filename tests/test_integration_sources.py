@@ -239,3 +239,12 @@ def test_packed_batches_use_a_reused_pinned_arena():
     assert "C.keto_host_alloc(" in arena and "C.keto_host_free(" in arena and "a.mu.Lock()" in arena
     close = src[src.index("func (s *Snapshot) Close()"):]
     assert "s.arena.free()" in close[:close.index("\n}")]
+
+
+def test_check_flush_size_from_env():
+    """The check batcher's flush size is KETO_GPU_CHECK_BATCH (default 65,536, capped at 2^24)."""
+    src = _code(open(os.path.join(GO, "internal", "gpu", "batcher.go")).read())
+    fn = src[src.index("func CheckFlushFromEnv() int {"):]
+    fn = fn[:fn.index("\n}\n")]
+    assert 'os.Getenv("KETO_GPU_CHECK_BATCH")' in fn and "return 1 << 16" in fn and "1<<24" in fn
+    assert "newCoalescer(CheckFlushFromEnv()," in src
