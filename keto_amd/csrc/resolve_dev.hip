@@ -196,14 +196,25 @@ __device__ int64_t query_row_dev(const ResolveDev& R, const uint8_t* f, uint32_t
 // [i0, i0 + n); the bytes [lo, hi) of the blob are on the device so far (a pipelined batch uploads it
 // piece by piece): a request with a field outside them is counted in cnt[2] and left for a second
 // pass once the whole blob is there.
+//
+// CLK (KETO_RESOLVE_CLOCKS, tooling): each request's lane records wall_clock64() (100 MHz) at its
+// start, after its record load, after its row query and after its subject lookup into clk[4 i ..].
+template <bool CLK = false>
 __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                       uint64_t lo, uint64_t hi, const keto_check_packed* __restrict__ q,
                                                       uint32_t i0, uint32_t n, keto_check_ids* __restrict__ out,
-                                                      uint8_t* __restrict__ status, uint32_t* __restrict__ cnt) {
+                                                      uint8_t* __restrict__ status, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ clk = nullptr) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t i = i0 + k;
+    uint64_t c0 = 0, c1 = 0, c2 = 0;
+    if constexpr (CLK) c0 = wall_clock64();
     const keto_check_packed p = q[i];
+    if constexpr (CLK) {
+        asm volatile("" ::"v"(p.off), "v"(p.max_depth) : "memory");        // (the record is in)
+        c1 = wall_clock64();
+    }
     const uint8_t* f = blob + p.off;
     keto_check_ids r{KETO_NO_ROW, KETO_NO_TARGET, 0u, p.max_depth};
     uint8_t st = KETO_CHECK_OK;
@@ -219,6 +230,10 @@ __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_
         atomicAdd(cnt + 1, 1u);
     } else {
         const int64_t row = query_row_dev(R, f, p.len[0], p.len[1], p.len[2]);
+        if constexpr (CLK) {
+            asm volatile("" ::"v"((uint32_t)row) : "memory");
+            c2 = wall_clock64();
+        }
         if (row == -2) st = KETO_CHECK_UNKNOWN_NAMESPACE;
         else if (row >= 0) r.row = (uint32_t)row;
         const uint8_t* g = f + p.len[0] + p.len[1] + p.len[2];
@@ -235,6 +250,14 @@ __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_
     }
     out[i] = r;
     status[i] = st;
+    if constexpr (CLK) {
+        asm volatile("" ::"v"(r.target) : "memory");
+        const uint64_t c3 = wall_clock64();
+        clk[4ull * i] = (uint32_t)c0;
+        clk[4ull * i + 1] = (uint32_t)(c1 - c0);
+        clk[4ull * i + 2] = c2 ? (uint32_t)(c2 - c1) : 0u;
+        clk[4ull * i + 3] = c2 ? (uint32_t)(c3 - c2) : 0u;
+    }
 }
 
 // decisions > 1 (KETO_UNDECIDED from the check) become "not allowed" with an undecided status, as
@@ -267,7 +290,7 @@ struct RDevState {
     std::vector<hipEvent_t> ev;    // piece k's bytes are on the device
     RBuf str_slots, str_bytes, str_off, add_slots, add_bytes, add_off, row_slots, extra_slots, ns_bytes, ns_off, ns_id;
     ResolveDev view{};
-    RBuf blob, reqs, ids, status, dec, cnt;
+    RBuf blob, reqs, ids, status, dec, cnt, clk;
     ~RDevState() {
         (void)hipSetDevice(device);
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -480,10 +503,16 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
         HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
         HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 2 * sizeof(uint32_t), st));
     };
+    static const bool clocks = getenv("KETO_RESOLVE_CLOCKS") != nullptr;  // tooling: per-step clocks
+    uint32_t* d_clk = clocks && K == 1 ? R.clk.get<uint32_t>(4ull * n) : nullptr;
     auto resolve = [&](uint32_t i0, uint32_t m, uint64_t hi) {
         if (!m) return;
-        hipLaunchKernelGGL(resolve_packed, dim3((m + 255) / 256), dim3(256), 0, st, R.view, d_blob, blob_len, 0ull, hi,
-                           d_q, i0, m, d_ids, d_st, d_cnt);
+        if (d_clk && i0 == 0 && m == n)
+            hipLaunchKernelGGL(resolve_packed<true>, dim3((m + 255) / 256), dim3(256), 0, st, R.view, d_blob, blob_len, 0ull,
+                               hi, d_q, i0, m, d_ids, d_st, d_cnt, d_clk);
+        else
+            hipLaunchKernelGGL(resolve_packed<false>, dim3((m + 255) / 256), dim3(256), 0, st, R.view, d_blob, blob_len, 0ull,
+                               hi, d_q, i0, m, d_ids, d_st, d_cnt, nullptr);
         HIP_OK(hipGetLastError());
     };
     uint32_t cnt[3] = {NO_BAD, 0u, 0u};
@@ -521,6 +550,24 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
     HIP_OK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     lock_trace("packed: copied back");
+    if (d_clk) {                                   // tooling: percentiles of the per-step clocks (us)
+        std::vector<uint32_t> c(4ull * n);
+        HIP_OK(hipMemcpy(c.data(), d_clk, c.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        uint32_t t0 = c[0];
+        for (uint32_t i = 0; i < n; ++i) t0 = (int32_t)(c[4ull * i] - t0) < 0 ? c[4ull * i] : t0;
+        std::string line = "[resolve clocks] n " + std::to_string(n);
+        const char* names[4] = {"start", "record", "row_query", "subject"};
+        for (int k = 0; k < 4; ++k) {
+            std::vector<double> v(n);
+            for (uint32_t i = 0; i < n; ++i) v[i] = (k ? c[4ull * i + k] : c[4ull * i] - t0) / 100.0;
+            std::sort(v.begin(), v.end());
+            char b[160];
+            snprintf(b, sizeof b, " | %s p50 %.2f p90 %.2f p99 %.2f max %.2f", names[k], v[n / 2], v[n * 9 / 10],
+                     v[(uint64_t)n * 99 / 100], v[n - 1]);
+            line += b;
+        }
+        fprintf(stderr, "%s\n", line.c_str());
+    }
     if (cnt[1])                                                            // the wildcard queries: the host's
         for (uint32_t i = 0; i < n && host.size() < cnt[1]; ++i)
             if (status[i] == ST_HOST) host.push_back(i);
