@@ -5026,7 +5026,7 @@ void host_free(void* p) {
 }
 
 void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
-                       void* stream) {
+                       void* stream, bool rows_valid) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     DeviceState& D = *S.dev;
     // NULL = the default stream, as the header says: ordered after the caller's default-stream work
@@ -5048,11 +5048,13 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
     ensure_lists(D.ws[0], n);
     HIP_OK(hipMemsetAsync(D.ws[0].counters + 4, 0, sizeof(uint32_t), st));
     translate_rows_locked(S, D, d_reqs, D.xlate, n, st, D.ws[0].counters + 4);
-    uint32_t bad = 0;
-    HIP_OK(hipMemcpyAsync(&bad, D.ws[0].counters + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    if (!rows_valid) {
+        uint32_t bad = 0;
+        HIP_OK(hipMemcpyAsync(&bad, D.ws[0].counters + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
+    }
     lock_trace("rows: translated");
-    if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name root rows another part owns"};
     check_locked(S, D, D.xlate, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, false);
     lock_trace("rows: check launched");
 }

@@ -526,12 +526,12 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
         read_cnt();                                                        // (before the check, as the host loop was)
         if (cnt[0] != NO_BAD)
             throw Error{KETO_E_INVALID, "request " + std::to_string(cnt[0]) + "'s fields lie outside the blob"};
-        device_check_rows(S, d_ids, n, gmd, d_dec, st);                    // row ids -> handles, the check
+        device_check_rows(S, d_ids, n, gmd, d_dec, st, S.n_parts == 1);                    // row ids -> handles, the check
     } else {
         for (uint32_t k = 0; k < K; ++k) {
             HIP_OK(hipStreamWaitEvent(st, R.ev[k], 0));
             resolve(cb[k], cb[k + 1] - cb[k], wb[k + 1]);
-            device_check_rows(S, d_ids + cb[k], cb[k + 1] - cb[k], gmd, d_dec + cb[k], st);
+            device_check_rows(S, d_ids + cb[k], cb[k + 1] - cb[k], gmd, d_dec + cb[k], st, true);
         }
         read_cnt();
         if (cnt[0] != NO_BAD)
@@ -540,7 +540,7 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
             reset();
             resolve(0, n, blob_len);
             read_cnt();
-            device_check_rows(S, d_ids, n, gmd, d_dec, st);
+            device_check_rows(S, d_ids, n, gmd, d_dec, st, S.n_parts == 1);
         }
     }
     lock_trace("packed: checked");

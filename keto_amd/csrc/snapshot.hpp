@@ -504,9 +504,11 @@ constexpr int FORM_HANDLES = 0, FORM_ROWS = 1, FORM_PAIRS = 2;
 void device_check_host(Snapshot& s, const void* reqs, uint32_t n, int32_t gmd, uint8_t* allowed, int form,
                        int32_t pair_depth, const Overlay* ov);
 keto_batch_timing device_last_timing(const Snapshot& s);
-// requests with row ids (not handles) resident on the device: translated, then checked
+// requests with row ids (not handles) resident on the device: translated, then checked.  rows_valid:
+// every row id is one this part holds (the packed path's own resolution on an unpartitioned
+// snapshot), so the misrouted-row count is not read back (a host round trip fewer)
 void device_check_rows(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
-                       void* stream);
+                       void* stream, bool rows_valid = false);
 const char* device_check_kernel_name(int32_t gmd);
 // deep batches (reach.hip): requests split into top-level items, items pretested by hop-bounded
 // reachability; engine.hip checks the kept work requests, then reach_merge folds their decisions
