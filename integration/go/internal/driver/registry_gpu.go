@@ -205,7 +205,11 @@ func (g *gpuState) buildFrom(ctx context.Context, rows []gpu.Row) ([]gpu.Engine,
 	if path := GPUSnapshotFileFromEnv(); path != "" {
 		_ = base.Save(path, gpu.Fingerprint(rows))
 	}
-	return gpu.Place(base, g.devices, GPUPlacementFromEnv())
+	// a rebuild places the new set while the outgoing one is still on the devices: credit its memory
+	g.mu.RLock()
+	resident := gpu.FootprintOf(g.engines)
+	g.mu.RUnlock()
+	return gpu.PlaceWith(base, g.devices, GPUPlacementFromEnv(), resident)
 }
 
 // applyLocked runs after a write committed, with wmu held: every replica follows the table one

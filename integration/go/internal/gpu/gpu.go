@@ -119,6 +119,7 @@ type Row struct {
 type Snapshot struct {
 	h       *C.keto_snapshot
 	Version uint64 // bumped by every Apply (snapshot lifecycle, see apply.go)
+	device  int    // HIP device of its arena, -1: host only
 	arena   pinnedArena
 }
 
@@ -228,7 +229,7 @@ func Build(nss []*namespace.Namespace, rows []Row, device int) (*Snapshot, error
 	if rc := C.keto_snapshot_build(cns, C.uint32_t(len(nss)), ct, C.uint64_t(len(rows)), &opts, &h); rc != C.KETO_OK {
 		return nil, lastErr(rc)
 	}
-	return &Snapshot{h: h}, nil
+	return &Snapshot{h: h, device: device}, nil
 }
 
 // Clone makes a replica of the snapshot at its current version on another HIP device
@@ -238,7 +239,7 @@ func (s *Snapshot) Clone(device int) (*Snapshot, error) {
 	if rc := C.keto_snapshot_clone(s.h, C.int32_t(device), &h); rc != C.KETO_OK {
 		return nil, lastErr(rc)
 	}
-	return &Snapshot{h: h, Version: s.Version}, nil
+	return &Snapshot{h: h, Version: s.Version, device: device}, nil
 }
 
 // Save writes the snapshot's host tables at its current version to path (keto_snapshot_save),
@@ -265,7 +266,7 @@ func Load(path string, device int) (*Snapshot, uint64, error) {
 	if rc := C.keto_snapshot_load(cp, C.int32_t(device), &h, &tag); rc != C.KETO_OK {
 		return nil, 0, lastErr(rc)
 	}
-	return &Snapshot{h: h, Version: uint64(C.keto_snapshot_version(h))}, uint64(tag), nil
+	return &Snapshot{h: h, Version: uint64(C.keto_snapshot_version(h)), device: device}, uint64(tag), nil
 }
 
 // BuildReplicas builds one snapshot per device of a node (one server process driving every GPU):

@@ -23,7 +23,42 @@ type Engine interface {
 	CheckBatch(reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error)
 	ExpandBatch(subs []relationtuple.Subject, depths []int, globalMax int) ([][]Node, []error, error)
 	Apply(inserts, deletes []Row) error
+	Footprint() map[int]uint64
 	Close()
+}
+
+// Footprint is the device memory the snapshot's arena and tables hold, by HIP device
+// (keto_snapshot_get_stats; empty for a host-only snapshot).
+func (s *Snapshot) Footprint() map[int]uint64 {
+	out := map[int]uint64{}
+	var st C.keto_snapshot_stats
+	if s.device >= 0 && C.keto_snapshot_get_stats(s.h, &st) == C.KETO_OK {
+		out[s.device] = uint64(st.device_bytes)
+	}
+	return out
+}
+
+// Footprint of a partition: its parts' device memory, by device.
+func (p *Partition) Footprint() map[int]uint64 {
+	out := map[int]uint64{}
+	for _, s := range p.parts {
+		for d, b := range s.Footprint() {
+			out[d] += b
+		}
+	}
+	return out
+}
+
+// FootprintOf sums the device memory an engine set holds, by device: what a rebuild's placement
+// credits back while the outgoing set is still on the devices (PlaceWith).
+func FootprintOf(es []Engine) map[int]uint64 {
+	out := map[int]uint64{}
+	for _, e := range es {
+		for d, b := range e.Footprint() {
+			out[d] += b
+		}
+	}
+	return out
 }
 
 // Engines views a replica set as engines.
@@ -71,6 +106,7 @@ func (s *Snapshot) UploadPart(part, nParts, device int) error {
 	if rc := C.keto_snapshot_upload_part_mode(s.h, C.uint32_t(part), C.uint32_t(nParts), C.int32_t(device), C.KETO_PART_SHARED); rc != C.KETO_OK {
 		return lastErr(rc)
 	}
+	s.device = device
 	return nil
 }
 
@@ -78,10 +114,27 @@ func (s *Snapshot) UploadPart(part, nParts, device int) error {
 // expand staging and request buffers (the deep tiers and the expand staging pool take the most).
 const workspaceBytes = 12 << 30
 
+// placementFree is the memory of device d a placement may count on: what is free now plus what
+// `resident` (an outgoing engine set that a rebuild replaces) holds there, so that the placement
+// depends on the graph and the devices, not on whether the previous set is still loaded.
+func placementFree(d int, resident map[int]uint64) (uint64, error) {
+	free, total, err := DeviceMemory(d)
+	if err != nil {
+		return 0, err
+	}
+	free += resident[d]
+	if free > total {
+		free = total
+	}
+	return free, nil
+}
+
 // Fits reports whether an arena of `arena` bytes and the engine's workspaces fit on every device.
-func Fits(arena uint64, devices []int) (bool, error) {
+func Fits(arena uint64, devices []int) (bool, error) { return fitsWith(arena, devices, nil) }
+
+func fitsWith(arena uint64, devices []int, resident map[int]uint64) (bool, error) {
 	for _, d := range devices {
-		free, _, err := DeviceMemory(d)
+		free, err := placementFree(d, resident)
 		if err != nil {
 			return false, err
 		}
@@ -256,7 +309,9 @@ const maxParts = 64
 // free memory.  Part sizes are estimated from the one-part statistics (every part keeps the targets,
 // the root rows split by hash; an eighth of margin), and the first plan the estimate admits is then
 // checked part by part.  A graph whose root rows pass 64 GiB is so served from one GPU too.
-func PlanParts(base *Snapshot, devices []int) ([]int, error) {
+func PlanParts(base *Snapshot, devices []int) ([]int, error) { return planPartsWith(base, devices, nil) }
+
+func planPartsWith(base *Snapshot, devices []int, resident map[int]uint64) ([]int, error) {
 	if len(devices) == 0 {
 		return nil, errors.New("gpu: no device")
 	}
@@ -266,7 +321,7 @@ func PlanParts(base *Snapshot, devices []int) ([]int, error) {
 	}
 	free := make([]uint64, len(devices))
 	for i, d := range devices {
-		if free[i], _, err = DeviceMemory(d); err != nil {
+		if free[i], err = placementFree(d, resident); err != nil {
 			return nil, err
 		}
 	}
@@ -321,6 +376,13 @@ func PlanParts(base *Snapshot, devices []int) ([]int, error) {
 // "" or "auto") or when mode is "replicate"; else (or with mode "partition") one Partition over the
 // parts PlanParts picks (one per device, or more when a part would pass arenaCap).
 func Place(base *Snapshot, devices []int, mode string) ([]Engine, error) {
+	return PlaceWith(base, devices, mode, nil)
+}
+
+// PlaceWith is Place for a rebuild: resident is the device memory the outgoing engine set still
+// holds (FootprintOf), counted as free, so the new set is placed as the graph requires (replicas or a
+// partition) and not pushed into a partition by the set it replaces.
+func PlaceWith(base *Snapshot, devices []int, mode string, resident map[int]uint64) ([]Engine, error) {
 	if len(devices) == 0 {
 		base.Close()
 		return nil, errors.New("gpu: no device")
@@ -332,14 +394,14 @@ func Place(base *Snapshot, devices []int, mode string) ([]Engine, error) {
 			base.Close()
 			return nil, err
 		}
-		if replicate, err = Fits(arena, devices); err != nil {
+		if replicate, err = fitsWith(arena, devices, resident); err != nil {
 			base.Close()
 			return nil, err
 		}
 		replicate = replicate && arena <= arenaCap
 	}
 	if !replicate {
-		plan, err := PlanParts(base, devices)
+		plan, err := planPartsWith(base, devices, resident)
 		if err != nil {
 			base.Close()
 			return nil, err

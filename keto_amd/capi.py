@@ -16,6 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KETO_LIB") or os.path.join(HERE, "libketo_mi355x.so")   # KETO_LIB: tuning builds
 
+KETO_ABI_VERSION = 5          # include/keto_mi355x.h KETO_ABI_VERSION: load() refuses any other library
 KETO_OK = 0
 E_REBUILD = -6
 CHECK_OK, CHECK_UNKNOWN_NAMESPACE, CHECK_UNDECIDED = 0, 1, 2
@@ -174,9 +175,12 @@ def load():
         raise KetoError(f"{LIB_PATH} is missing: build it with `python keto_amd/build.py` "
                         "(the engine has no non-HIP implementation)")
     lib = C.CDLL(LIB_PATH)
+    # KETO_LIB_PARTIAL=1 (tooling only: a comparison build that predates entry points its run does not
+    # call) skips the export check; the ABI version is checked whatever library KETO_LIB names
+    if not hasattr(lib, "keto_abi_version") or lib.keto_abi_version() != KETO_ABI_VERSION:
+        raise KetoError(f"{LIB_PATH} is not ABI {KETO_ABI_VERSION} (rebuild it with `python keto_amd/build.py`)")
     for name in EXPORTS:
-        # (a KETO_LIB tuning or comparison build may predate entry points its test does not call)
-        if not hasattr(lib, name) and not os.environ.get("KETO_LIB"):
+        if not hasattr(lib, name) and not os.environ.get("KETO_LIB_PARTIAL"):
             raise KetoError(f"{LIB_PATH} does not export {name}")
     lib.keto_last_error.restype = C.c_char_p
     lib.keto_check_kernel_name.restype = C.c_char_p

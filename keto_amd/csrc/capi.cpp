@@ -621,6 +621,16 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
         std::shared_lock<RwGate> rl(S.rw);
         lock_trace("apply: rw shared");
         std::unique_lock<RwGate> xl(S.rw, std::defer_lock);
+        // on every exit (a HIP error or KETO_E_REBUILD after the swap included): release the exclusive
+        // lock, then free the tables the commit replaced -- apply_mu is still held, retired is ours
+        struct Retire {
+            Snapshot& S;
+            std::unique_lock<RwGate>& xl;
+            ~Retire() {
+                if (xl.owns_lock()) xl.unlock();
+                S.retired.clear();
+            }
+        } retire{S, xl};
         const auto t0 = std::chrono::steady_clock::now();
         auto t1 = t0;
         apply_writes(S, inserts, n_inserts, deletes, n_deletes, [&] {
@@ -639,8 +649,6 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
                     std::chrono::duration<double, std::milli>(t2 - t1).count(),
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
         if (version_out) *version_out = S.version;
-        if (xl.owns_lock()) xl.unlock();             // (apply_mu still held: retired is the writer's)
-        S.retired.clear();
         return KETO_OK;
     });
 }

@@ -643,31 +643,57 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             }
             route();
         });
-        // the counts to their owners, each with this rank's status and whether writes left this
-        // (migrating) part's closure filters stale: the exchange is the agreement
+        // the counts to their owners, each with this rank's status, whether writes left this
+        // (migrating) part's closure filters stale, and the snapshot version it is at: the exchange is
+        // the agreement
         const uint64_t stale = mine.code == KETO_OK && Sp->part_mode == PART_MIGRATE && !Sp->mig_ready ? 1u : 0u;
-        std::vector<uint64_t> cw(3ull * c->n);
+        const uint64_t version = mine.code == KETO_OK ? Sp->version : 0;
+        std::vector<uint64_t> cw(4ull * c->n);
         for (int p = 0; p < c->n; ++p) {
-            cw[3 * p] = mine.code == KETO_OK ? cnt[p] : 0;
-            cw[3 * p + 1] = (uint64_t)(int64_t)mine.code;
-            cw[3 * p + 2] = stale;
+            cw[4 * p] = mine.code == KETO_OK ? cnt[p] : 0;
+            cw[4 * p + 1] = (uint64_t)(int64_t)mine.code;
+            cw[4 * p + 2] = stale;
+            cw[4 * p + 3] = version;
         }
-        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 3, c->stream);
+        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 4, c->stream);
         std::vector<int64_t> codes(c->n);
-        std::vector<uint64_t> in(c->n);
+        std::vector<uint64_t> in(c->n), versions(c->n);
         bool any_stale = false;
         for (int p = 0; p < c->n; ++p) {
-            in[p] = inw[3 * p];
-            codes[p] = (int64_t)inw[3 * p + 1];
-            any_stale |= inw[3 * p + 2] != 0;
+            in[p] = inw[4 * p];
+            codes[p] = (int64_t)inw[4 * p + 1];
+            any_stale |= inw[4 * p + 2] != 0;
+            versions[p] = inw[4 * p + 3];
         }
         settle(*c, mine, codes);
+        // Every part must be at the same snapshot version: a migrating part's records name rows by
+        // their owners' handles, which each write lays out afresh, and a shared-rows part routes rows
+        // that a write may have added on one part only.  Every rank saw the same versions, so every
+        // rank refuses the batch here, before anything travels.
+        for (int p = 0; p < c->n; ++p)
+            if (versions[p] != versions[0])
+                throw Error{KETO_E_INVALID, "parts at different snapshot versions (rank 0 at " +
+                                                std::to_string(versions[0]) + ", rank " + std::to_string(p) + " at " +
+                                                std::to_string(versions[p]) +
+                                                "): apply every write to every part before a routed batch"};
         // a write lays a migrating part out afresh (its stubs' filters start empty): every rank saw the
-        // same flags, so all of them run the exchange again before the batch's records travel
+        // same flags, so all of them run the exchange again before the batch's records travel.  The
+        // exchange rewrites filters in the arena, so it runs under the exclusive lock (no other batch
+        // on this part sees half-closed filters); a write that slips in between is caught below.
         if (any_stale) {
-            close_filters(c, h, nullptr);
-            // the exchange used the communicator's scratch buffers: route again (same owners, same counts)
-            if (mine.code == KETO_OK) mine.run(route);
+            lk.unlock();
+            {
+                std::unique_lock<RwGate> xl(Sp->rw);
+                close_filters(c, h, nullptr);
+            }
+            lk.lock();
+            mine.run([&] {
+                if (Sp->version != version)
+                    throw Error{KETO_E_INVALID, "a write was applied to this part during the routed batch"};
+                // the exchange used the communicator's scratch buffers: route again (same owners, same counts)
+                route();
+            });
+            agree(*c, mine);
         }
         Snapshot& S = *Sp;
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
@@ -792,22 +818,30 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
             injected(*c, "expand");
             if (n) expand_named(*Sp, reqs, n, global_max_depth, *local, routed.data());
         });
-        // the roots to their owners, each count with this rank's status (the exchange is the agreement)
-        std::vector<uint64_t> cw(2ull * P);
+        // the roots to their owners, each count with this rank's status and snapshot version (the
+        // exchange is the agreement)
+        const uint64_t version = mine.code == KETO_OK ? Sp->version : 0;
+        std::vector<uint64_t> cw(3ull * P);
         for (int p = 0; p < P; ++p) {
-            cw[2 * p] = mine.code == KETO_OK ? to[p].size() : 0;
-            cw[2 * p + 1] = (uint64_t)(int64_t)mine.code;
+            cw[3 * p] = mine.code == KETO_OK ? to[p].size() : 0;
+            cw[3 * p + 1] = (uint64_t)(int64_t)mine.code;
+            cw[3 * p + 2] = version;
         }
-        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 2, c->stream);
+        const std::vector<uint64_t> inw = c->t->alltoall_u64(cw, 3, c->stream);
         std::vector<int64_t> codes(P);
         std::vector<uint64_t> in(P), sb(P), rb(P);
         for (int p = 0; p < P; ++p) {
-            in[p] = inw[2 * p];
-            codes[p] = (int64_t)inw[2 * p + 1];
+            in[p] = inw[3 * p];
+            codes[p] = (int64_t)inw[3 * p + 1];
             sb[p] = to[p].size() * 8;
             rb[p] = in[p] * 8;
         }
         settle(*c, mine, codes);
+        for (int p = 0; p < P; ++p)           // every rank refuses alike (see keto_check_batch_routed)
+            if (inw[3 * p + 2] != inw[2])
+                throw Error{KETO_E_INVALID, "parts at different snapshot versions (rank 0 at " + std::to_string(inw[2]) +
+                                                ", rank " + std::to_string(p) + " at " + std::to_string(inw[3 * p + 2]) +
+                                                "): apply every write to every part before a routed batch"};
         const uint64_t m = std::accumulate(in.begin(), in.end(), 0ull);
         // the exchange buffers are allocated inside the agreement: a rank whose allocation fails still
         // meets its peers, and every rank returns that rank's code instead of waiting in the all-to-all
@@ -1016,6 +1050,9 @@ int keto_comm_close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out
     return guarded([&] {
         if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
         HIP_OK(hipSetDevice(c->device));
+        // the exchange rewrites this part's filters: no batch on the part runs meanwhile
+        std::unique_lock<RwGate> xl;
+        if (h) xl = std::unique_lock<RwGate>(h->s->rw);
         close_filters(c, h, rounds_out);
         return KETO_OK;
     });

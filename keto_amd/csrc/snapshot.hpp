@@ -311,7 +311,9 @@ struct Snapshot {
     uint64_t hot_bytes = 0;
     uint32_t hot_units = 0;
     uint64_t hot_rows = 0;
-    bool mig_ready = false;   // PART_MIGRATE: closure filters final (part_closure_done, or one part)
+    // PART_MIGRATE: closure filters final (part_closure_done, or one part); atomic: read by batches under
+    // the shared lock while a filter exchange (exclusive lock) or a write resets it
+    std::atomic<bool> mig_ready{false};
     // r is held by this device (owned, or on every part); stubs are not rows of this part
     bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT && (stub.empty() || !stub[r]); }
     bool mapped(uint32_t r) const { return unit_of_row[r] != NO_UNIT; }   // a row or a stub here

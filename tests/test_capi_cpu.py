@@ -22,7 +22,9 @@ def test_exports_match_header():
 
 
 def test_abi_version():
-    assert keto_amd.load().keto_abi_version() == 5
+    hdr = open(os.path.join(ROOT, "include", "keto_mi355x.h")).read()
+    want = int(re.search(r"#define KETO_ABI_VERSION (\d+)", hdr).group(1))
+    assert keto_amd.load().keto_abi_version() == want == capi.KETO_ABI_VERSION
 
 
 def test_host_snapshot_stats():

@@ -294,6 +294,47 @@ def test_local_error_agreement(powerlaw_strings, monkeypatch, point):
         p.close()
 
 
+@pytest.mark.parametrize("mode", ["shared", "migrate"])
+def test_local_parts_at_different_versions_refused(powerlaw_strings, mode):
+    """A write applied to one part but not yet to the other: the routed check and the routed expand
+    refuse the batch on every rank (KETO_E_INVALID, agreed: the version travels with the counts)
+    instead of sending a migrating part's records, which name rows by their owners' handles of
+    another layout.  Once every part has the write, the same batch answers like the replicated
+    snapshot (the write adds a new document only, so no earlier decision changes)."""
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED, KetoError
+    g, st, full, arr, n, want, want_st = powerlaw_strings
+    P = 2
+    m = PART_MIGRATE if mode == "migrate" else PART_SHARED
+    parts = []
+    for r in range(P):
+        part, _ = g.snapshot_from_strings(st, device=-1)
+        parts.append(part.upload_part(r, P, 0, mode=m))
+    comms = _local_comms(P)
+    if m == PART_MIGRATE:
+        _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+    k = 20_000
+    write = [(1, "zz000001", "view", "u00000001")]
+    parts[0].apply(write, [])
+
+    def routed(r):
+        return comms[r].check_batch_routed(parts[r], _slice(arr, r * k, (r + 1) * k), 5, n=k)
+
+    for fn in (routed, lambda r: comms[r].expand_batch_routed(parts[r], [(("set", "docs", "zz000001", "view"), 0)], 5)):
+        res = _ranks(P, fn)
+        for r, (ok, v) in enumerate(res):
+            assert not ok and isinstance(v, KetoError) and "different snapshot versions" in str(v), (mode, r, v)
+    parts[1].apply(write, [])
+    for r, (got, gst) in enumerate(_ok(_ranks(P, routed))):
+        assert (got == want[r * k:(r + 1) * k]).all() and (gst == want_st[r * k:(r + 1) * k]).all(), (mode, r)
+    got, _ = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(
+        parts[r], [("docs", "zz000001", "view", ("id", "u00000001"), 0)] if r == 1 else [], 5)))[1]
+    assert list(got) == [1], mode
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+
+
 def test_local_error_agreement_bad_arguments(powerlaw_strings):
     """Real rank-local errors, no injection: rank 2 passes a NULL request array with n > 0.  Every
     rank returns the code, and the communicator stays usable.  Rank 0 then passes a wildcard query
