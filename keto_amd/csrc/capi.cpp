@@ -653,7 +653,7 @@ int keto_snapshot_apply(keto_snapshot* h, const keto_tuple* inserts, uint64_t n_
     });
 }
 
-uint64_t keto_snapshot_version(const keto_snapshot* h) { return h ? h->s->version : 0; }
+uint64_t keto_snapshot_version(const keto_snapshot* h) { return h ? h->s->version.load() : 0; }
 
 namespace {
 int upload_part(keto_snapshot* h, uint32_t part, uint32_t n_parts, int32_t device, uint32_t mode, uint64_t hot_bytes) {
@@ -697,6 +697,8 @@ int keto_snapshot_part_stats_mode(keto_snapshot* h, uint32_t part, uint32_t n_pa
         if (mode == KETO_PART_MIGRATE && n_parts > KETO_MIG_MAX_PARTS)
             throw Error{KETO_E_INVALID, "a migrating partition has at most 30 parts"};
         Snapshot& S = *h->s;
+        // lays the snapshot out for the part and back: no other call may read the layout meanwhile
+        std::unique_lock<RwGate> xl(S.rw);
         if (S.dev) throw Error{KETO_E_INVALID, "part statistics need a host-only snapshot (device = -1)"};
         const uint32_t p0 = S.part, n0 = S.n_parts;
         const int m0 = S.part_mode;
@@ -735,6 +737,7 @@ int keto_snapshot_part_stats(keto_snapshot* h, uint32_t part, uint32_t n_parts, 
 int64_t keto_part_stubs(const keto_snapshot* h, uint32_t* rows_out, uint64_t cap) {
     return guarded([&]() -> int64_t {
         if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<RwGate> lk(h->s->rw);
         const Snapshot& S = *h->s;
         if (S.part_mode != PART_MIGRATE || S.stub.empty()) return 0;
         uint64_t k = 0;
@@ -750,6 +753,7 @@ int64_t keto_part_stubs(const keto_snapshot* h, uint32_t* rows_out, uint64_t cap
 int keto_part_filters(keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t* filters_out) {
     return guarded([&] {
         if (!h || (n && (!rows || !filters_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<RwGate> lk(h->s->rw);
         part_filters(*h->s, rows, n, filters_out);
         return KETO_OK;
     });
@@ -759,6 +763,7 @@ int keto_part_close(keto_snapshot* h, const uint32_t* stub_rows, uint64_t n, con
                     uint64_t* changed_out) {
     return guarded([&] {
         if (!h || (n && (!stub_rows || !filters))) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::unique_lock<RwGate> xl(h->s->rw);          // rewrites the part's filters
         const uint64_t c = part_close(*h->s, stub_rows, n, filters);
         if (changed_out) *changed_out = c;
         return KETO_OK;
@@ -768,6 +773,7 @@ int keto_part_close(keto_snapshot* h, const uint32_t* stub_rows, uint64_t n, con
 int keto_part_closure_done(keto_snapshot* h, int converged) {
     return guarded([&] {
         if (!h) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::unique_lock<RwGate> xl(h->s->rw);
         if (h->s->part_mode != PART_MIGRATE) throw Error{KETO_E_INVALID, "not a migrating part"};
         part_closure_done(*h->s, converged != 0);
         return KETO_OK;
@@ -793,6 +799,7 @@ int keto_mig_begin(keto_snapshot* h, const keto_check_ids* d_reqs, uint32_t n, i
                    uint8_t* d_allowed_out, void* stream, keto_mig_out* out) {
     return guarded([&] {
         if (!h || !out) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<RwGate> lk(h->s->rw);
         MigOut m{};
         mig_begin(*h->s, d_reqs, n, global_max_depth, d_allowed_out, stream, m);
         copy_out(m, out);
@@ -821,6 +828,7 @@ int keto_mig_round(keto_snapshot* h, const void* d_records, const uint32_t* d_of
                    const uint64_t* in_units, void* stream, keto_mig_out* out) {
     return guarded([&] {
         if (!h || !out || !in_records || !in_units) throw Error{KETO_E_INVALID, "NULL argument"};
+        std::shared_lock<RwGate> lk(h->s->rw);
         MigOut m{};
         mig_round(*h->s, d_records, d_offsets, in_records, in_units, stream, m);
         copy_out(m, out);
@@ -853,6 +861,7 @@ int keto_unroute_device(const uint8_t* d_back, const uint32_t* d_order, uint32_t
 int keto_row_owner(const keto_snapshot* h, const uint32_t* rows, uint64_t n, uint32_t n_parts, int32_t* out) {
     return guarded([&] {
         if (!h || (n && (!rows || !out)) || n_parts == 0) throw Error{KETO_E_INVALID, "bad argument"};
+        std::shared_lock<RwGate> lk(h->s->rw);
         const Snapshot& S = *h->s;
         for (uint64_t i = 0; i < n; ++i) {
             if (rows[i] == KETO_NO_ROW) { out[i] = -1; continue; }

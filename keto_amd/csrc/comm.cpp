@@ -647,7 +647,7 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         // (migrating) part's closure filters stale, and the snapshot version it is at: the exchange is
         // the agreement
         const uint64_t stale = mine.code == KETO_OK && Sp->part_mode == PART_MIGRATE && !Sp->mig_ready ? 1u : 0u;
-        const uint64_t version = mine.code == KETO_OK ? Sp->version : 0;
+        const uint64_t version = mine.code == KETO_OK ? Sp->version.load() : 0;
         std::vector<uint64_t> cw(4ull * c->n);
         for (int p = 0; p < c->n; ++p) {
             cw[4 * p] = mine.code == KETO_OK ? cnt[p] : 0;
@@ -820,7 +820,7 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
         });
         // the roots to their owners, each count with this rank's status and snapshot version (the
         // exchange is the agreement)
-        const uint64_t version = mine.code == KETO_OK ? Sp->version : 0;
+        const uint64_t version = mine.code == KETO_OK ? Sp->version.load() : 0;
         std::vector<uint64_t> cw(3ull * P);
         for (int p = 0; p < P; ++p) {
             cw[3 * p] = mine.code == KETO_OK ? to[p].size() : 0;

@@ -929,7 +929,7 @@ std::unique_ptr<Snapshot> clone_host(const Snapshot& S) {
     C.n_tuples = S.n_tuples;
     C.n_poisoned_rows = S.n_poisoned_rows;
     C.n_seq_rows = S.n_seq_rows;
-    C.version = S.version;
+    C.version = S.version.load();
     C.n_sorted_strs = S.n_sorted_strs;
     C.added_str = S.added_str;
     C.n_base_rows = S.n_base_rows;

@@ -326,7 +326,7 @@ struct Snapshot {
     // ---- lifecycle (delta.cpp): writes applied since the build
     RwGate rw;                                 // calls read the host tables shared; keto_snapshot_apply exclusive
     std::mutex apply_mu;                       // one keto_snapshot_apply at a time (it stages under rw shared)
-    uint64_t version = 0;                      // bumped by every keto_snapshot_apply
+    std::atomic<uint64_t> version{0};          // bumped by every keto_snapshot_apply (read without the lock)
     uint32_t n_sorted_strs = 0;                // strs[0, n) are in byte order (id = rank); later ones were added
     std::unordered_map<std::string, uint32_t> added_str;
     uint32_t n_base_rows = 0;                  // rows of the build; rows >= n_base_rows were added by writes
