@@ -359,6 +359,23 @@ def main():
     strf = None
     if not migrate and not a.partitioned and unified is not None:
         strf = string_form(g, unified, snap, q_gen, a)
+    rows_dev = None
+    if not a.partitioned and not migrate and a.steps > 0:
+        # the same batch resident in HBM by row id (what the resolution produces): keto_check_batch_rows_device,
+        # the row id -> handle translation inside the timed region (detail only; value times the handle form)
+        d_rows = torch.from_numpy(np.ascontiguousarray(q).view(np.uint8)).to(f"cuda:{dev}")
+        d_rout = torch.empty(a.batch, dtype=torch.uint8, device=f"cuda:{dev}")
+        for _ in range(2):
+            snap.check_batch_rows_device(d_rows.data_ptr(), a.batch, d_rout.data_ptr(), a.depth, sp)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            snap.check_batch_rows_device(d_rows.data_ptr(), a.batch, d_rout.data_ptr(), a.depth, sp)
+        torch.cuda.synchronize()
+        t_rows = (time.perf_counter() - t0) / a.steps
+        rows_dev = {"value": round(a.batch / t_rows, 1), "unit": "checks/s", "ms_per_step": round(t_rows * 1e3, 3),
+                    "what": "the batch resident in HBM as 16-B row-id requests through keto_check_batch_rows_device "
+                            "(row id -> handle translation + the check, timed like value)", "_out": d_rout}
     e2e = None
     if not a.partitioned and a.e2e_steps > 0:
         e2e = end_to_end(snap, q, a, d_out)
@@ -486,6 +503,8 @@ def main():
         e2e["frac"] = round(roofline["alg_bytes_per_launch"] / (e2e["ms_per_batch"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if e2e is not None:
         e2e["decisions_equal_device_resident"] = all(bool((o == gpu_out).all()) for o in e2e.pop("_out"))
+    if rows_dev is not None:
+        rows_dev["decisions_equal_device_resident"] = bool((rows_dev.pop("_out").cpu().numpy() == gpu_out).all())
     if strf is not None:
         strf["decisions_equal_device_resident"] = bool((strf.pop("_out") == gpu_out).all())
         hr = strf["host_resolution"]
@@ -513,7 +532,13 @@ def main():
                                    ("migrating partition (every row on one part, searches move between parts as "
                                     f"records, {a.hot_mb} MB of replicated hot rows per part)" if migrate else
                                     "edge-partitioned snapshot, requests routed by all-to-all" if a.partitioned
-                                    else "replicated snapshot"),
+                                    else "replicated snapshot") +
+                                   ("; value = requests resident in HBM by row id, routed and checked per step"
+                                    if a.partitioned else
+                                    "; value = a device-resident batch of pre-resolved requests (row handles in HBM, "
+                                    "keto_check_batch_device; the row id -> handle resolution is untimed); "
+                                    "detail.device_row_ids times the row-id form with its translation, and "
+                                    "end_to_end.value is SURVEY 8(d) t_batch (host entry to decisions on the host)"),
                        "tuples": int(g.n_edges), "set_edge_fraction": round(g.n_set_edges / max(1, g.n_edges), 4),
                        "rows": int(g.n_rows), "checks_per_gpu_per_step": a.batch, "max_depth": a.depth,
                        "global_batch": a.batch * world,
@@ -525,7 +550,7 @@ def main():
             "cpu_baseline": cpu,
             "ref_sql": ref_sql,
             "parity": parity if part_parity is None else part_parity,
-            "detail": {"tier0_ms": round(tier0_ms, 3), "tier1_ms": round(tier1_ms, 3),
+            "detail": {"device_row_ids": rows_dev, "tier0_ms": round(tier0_ms, 3), "tier1_ms": round(tier1_ms, 3),
                        "tier0_overflow_requests": overflow, "allowed_fraction": round(allowed_rate, 4),
                        "gen_s": round(t_gen, 1), "snapshot_upload_s": round(t_snap, 1), "work": work,
                        "host_per_rank": [{"peak_rss_gb": round(r_, 2), "cpu_s": round(c_, 1)} for r_, c_ in host_ranks],

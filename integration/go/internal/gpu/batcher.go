@@ -138,9 +138,10 @@ func (c *coalescer) loop() {
 type Fallback func(ctx context.Context, r *relationtuple.InternalRelationTuple, restDepth int) (bool, error)
 
 // replicas deals batches to the engines of a set: one snapshot replica per GPU (BuildReplicas), or
-// one Partition over all of them (a graph past one GPU's memory).  A batch goes to an engine with no
-// batch in flight, so the GPUs of a node work on consecutive batches at once and the dealing follows
-// their load; when every engine is busy the flush loop waits (back-pressure).
+// one Partition over all of them (a graph past one GPU's memory).  A batch goes to an engine with
+// fewer than InflightFromEnv batches in flight, so the GPUs of a node work on consecutive batches at
+// once, each overlapping two of them, and the dealing follows their load; when every engine is full
+// the flush loop waits (back-pressure).
 type replicas struct {
 	mu  sync.RWMutex // held shared by a running batch (from dealing to its end), exclusively by swap
 	cur *engineSet
@@ -148,13 +149,31 @@ type replicas struct {
 
 type engineSet struct {
 	snaps []Engine
-	idle  chan int // indices of the engines with no batch in flight
+	idle  chan int // one token per batch an engine may take more: InflightFromEnv tokens per engine
+}
+
+// InflightFromEnv is the number of batches the batchers keep in flight per engine,
+// KETO_GPU_INFLIGHT (default 2, at most 8): the library overlaps one packed batch's upload and
+// resolution with another's check on the same device (keto_check_batch_packed keeps that many
+// in flight, KETO_PACKED_SLOTS), so at the 65,536-request flush the GPU is not idle between batches.
+// A Partition serializes its own batches.
+func InflightFromEnv() int {
+	if v, err := strconv.Atoi(os.Getenv("KETO_GPU_INFLIGHT")); err == nil && v > 0 {
+		if v > 8 {
+			v = 8
+		}
+		return v
+	}
+	return 2
 }
 
 func newEngineSet(snaps []Engine) *engineSet {
-	s := &engineSet{snaps: snaps, idle: make(chan int, len(snaps))}
-	for k := range snaps {
-		s.idle <- k
+	per := InflightFromEnv()
+	s := &engineSet{snaps: snaps, idle: make(chan int, per*len(snaps))}
+	for j := 0; j < per; j++ { // engine k's tokens interleaved, so batches spread over the GPUs first
+		for k := range snaps {
+			s.idle <- k
+		}
 	}
 	return s
 }

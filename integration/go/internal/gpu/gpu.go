@@ -120,7 +120,7 @@ type Snapshot struct {
 	h       *C.keto_snapshot
 	Version uint64 // bumped by every Apply (snapshot lifecycle, see apply.go)
 	device  int    // HIP device of its arena, -1: host only
-	arena   pinnedArena
+	arenas  arenaPool
 }
 
 // pinnedArena is a snapshot's page-locked buffer for large packed batches (keto_host_alloc), reused
@@ -158,6 +158,52 @@ func (a *pinnedArena) get(n int) (unsafe.Pointer, bool) {
 }
 
 func (a *pinnedArena) put() { a.mu.Unlock() }
+
+// arenaPool holds one pinned arena per packed batch a snapshot keeps in flight (InflightFromEnv):
+// the library runs one batch's upload and resolution while another's check runs
+// (keto_check_batch_packed, KETO_PACKED_SLOTS), so two batches must not share staging memory.
+type arenaPool struct {
+	once sync.Once
+	free chan *pinnedArena
+	all  []*pinnedArena
+}
+
+func (p *arenaPool) init() {
+	p.once.Do(func() {
+		n := InflightFromEnv()
+		p.free = make(chan *pinnedArena, n)
+		for i := 0; i < n; i++ {
+			a := &pinnedArena{}
+			p.all = append(p.all, a)
+			p.free <- a
+		}
+	})
+}
+
+// get takes a free arena with at least n bytes (waiting for one); ok = false when pinning failed
+// (the arena is returned, and the caller uses C memory instead).
+func (p *arenaPool) get(n int) (*pinnedArena, unsafe.Pointer, bool) {
+	p.init()
+	a := <-p.free
+	base, ok := a.get(n)
+	if !ok {
+		p.free <- a
+		return nil, nil, false
+	}
+	return a, base, true
+}
+
+func (p *arenaPool) put(a *pinnedArena) {
+	a.put()
+	p.free <- a
+}
+
+func (p *arenaPool) freeAll() {
+	p.init()
+	for _, a := range p.all {
+		a.free()
+	}
+}
 
 func (a *pinnedArena) free() {
 	a.mu.Lock()
@@ -315,7 +361,7 @@ func (s *Snapshot) Close() {
 		C.keto_snapshot_release(s.h)
 		s.h = nil
 	}
-	s.arena.free()
+	s.arenas.freeAll()
 }
 
 func subjectLen(sub relationtuple.Subject) int {
@@ -399,8 +445,8 @@ func (s *Snapshot) checkPacked(reqs []*relationtuple.InternalRelationTuple, dept
 	var rec *C.keto_check_packed
 	var allowed, status *C.uint8_t
 	if size := strBytes + recBytes + 2*n; size >= pinMin {
-		if base, ok := s.arena.get(size); ok {
-			defer s.arena.put()
+		if a, base, ok := s.arenas.get(size); ok {
+			defer s.arenas.put(a)
 			m.str = base
 			rec = (*C.keto_check_packed)(unsafe.Add(base, strBytes))
 			allowed = (*C.uint8_t)(unsafe.Add(base, strBytes+recBytes))

@@ -2701,11 +2701,14 @@ struct DeviceState {
     uint32_t n_units = 0;         // main-arena handles are < n_units
     uint32_t n_coll = 0;          // collision classes
     std::mutex mu;                // one batch at a time per snapshot (workspaces are shared)
-    WorkSet ws[2];                // check workspaces (ws[1]: the second compute stream of the pipeline)
+    WorkSet ws[3];                // check workspaces (ws[1]: the second compute stream of the pipeline;
+                                  // ws[2]: packed batches checked without a host round trip, astream)
     WorkSet ews;                  // expand workspaces
     uint32_t v1_lanes[16] = {};   // resident lanes of the tier-0 check kernel, per variant
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;    // the pipeline's second compute stream (ws[1])
+    hipStream_t astream = nullptr;    // device_check_rows_async: every such check in call order (ws[2])
+    std::vector<hipEvent_t> aev;      // its stash timing events (3)
     hipEvent_t ev[6] = {};
     keto_batch_timing last{};
     uint32_t* row_handle = nullptr;   // row id -> handle (NO_UNIT: another part's root row), lazily
@@ -3772,6 +3775,8 @@ void device_release(Snapshot& S) {
     }
     if (D.stream) (void)hipStreamDestroy(D.stream);
     if (D.stream2) (void)hipStreamDestroy(D.stream2);
+    if (D.astream) (void)hipStreamDestroy(D.astream);
+    for (auto& e : D.aev) (void)hipEventDestroy(e);
     if (D.copy_in) (void)hipStreamDestroy(D.copy_in);
     if (D.copy_out) (void)hipStreamDestroy(D.copy_out);
     for (auto& e : D.ev)
@@ -5057,6 +5062,51 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
     lock_trace("rows: translated");
     check_locked(S, D, D.xlate, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, false);
     lock_trace("rows: check launched");
+}
+
+// A batch of row-id requests checked without a host round trip (the packed path's batches in flight,
+// resolve_dev.hip): under the device lock, only enqueued -- on D.astream, after `ready`: the
+// translation into the caller's d_xlate, tiers 0 and 1 on their own workspace (ws[2]) with the
+// tier-1 overflows only counted (d_counts[0]; stash of capacity 0), then `done` recorded.  Another
+// batch's upload and resolution run meanwhile on their own streams, and this call returns before the
+// check ends.  A batch with d_counts[0] > 0 needs tier 2 and is checked again by the caller through
+// device_check_rows.  Deep batches (max-depth > 9) are not taken: false.  Rows must be valid
+// (unpartitioned snapshot); d_counts[2] counts misrouted rows anyway.
+bool device_check_rows_async(Snapshot& S, const keto_check_ids* d_rows, uint32_t n, int32_t gmd, uint8_t* d_allowed,
+                             keto_check_ids* d_xlate, uint32_t* d_counts, void* ready_event, void* done_event) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    hipEvent_t ready = (hipEvent_t)ready_event, done = (hipEvent_t)done_event;
+    if (std::max(1, std::min<int32_t>(gmd, 65535) - 1) > 8 || S.n_parts != 1) return false;
+    DeviceState& D = *S.dev;
+    lock_trace("rows async: waiting for D.mu");
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    if (!D.astream) HIP_OK(hipStreamCreateWithFlags(&D.astream, hipStreamNonBlocking));
+    while (D.aev.size() < 3) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        D.aev.push_back(e);
+    }
+    hipStream_t st = D.astream;
+    HIP_OK(hipStreamWaitEvent(st, ready, 0));
+    HIP_OK(hipMemsetAsync(d_counts, 0, 3 * sizeof(uint32_t), st));
+    translate_rows_locked(S, D, d_rows, d_xlate, n, st, d_counts + 2);
+    PipeStash ps;
+    ps.q = d_xlate;                   // (capacity 0: nothing is stashed, the overflows are counted)
+    ps.idx = nullptr;
+    ps.count = d_counts;
+    ps.cap = 0;
+    ps.base = 0;
+    ps.dq = d_xlate;
+    ps.ev = D.aev;
+    ps.chunk = 0;
+    const keto_batch_timing before = D.last;
+    check_locked(S, D, d_xlate, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, true, nullptr, &ps, 2);
+    D.last = before;
+    D.last.requests[0] = n;
+    HIP_OK(hipEventRecord(done, st));
+    lock_trace("rows async: enqueued");
+    return true;
 }
 
 // Expand output: set nodes carry row handles; map them to row ids on the device (binary search in

@@ -24,7 +24,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 
 #include "parallel.hpp"
@@ -279,20 +281,44 @@ T* upload(RBuf& b, const T* src, uint64_t n, hipStream_t st) {
 
 }  // namespace
 
+// A packed batch in flight (device_check_packed_async): its own stream, device buffers and pinned
+// output staging, so that one batch's upload and resolution run while another's check does.
+struct PSlot {
+    int device = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ready = nullptr, done = nullptr;   // resolved (the check may start) / checked
+    RBuf blob, reqs, ids, status, dec, cnt, xlate;
+    uint8_t* host = nullptr;       // pinned: decisions | statuses | the six counter words
+    uint64_t host_cap = 0;
+    ~PSlot() {
+        (void)hipSetDevice(device);
+        if (st) (void)hipStreamSynchronize(st);
+        if (host) (void)hipHostFree(host);
+        if (ready) (void)hipEventDestroy(ready);
+        if (done) (void)hipEventDestroy(done);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
 // The device copies of the indexes (per snapshot version) and the per-call buffers.
 struct RDevState {
     int device = 0;
     uint64_t version = ~0ull;
     bool base_ready = false;       // the build's string and row indexes and the namespaces (fixed after the build)
-    std::mutex mu;                 // one packed batch at a time per snapshot
+    std::mutex mu;                 // the tables' refresh; a large (or fallback) batch holds it throughout
     hipStream_t stream = nullptr;
     hipStream_t copy = nullptr;    // a pipelined batch's uploads
     std::vector<hipEvent_t> ev;    // piece k's bytes are on the device
     RBuf str_slots, str_bytes, str_off, add_slots, add_bytes, add_off, row_slots, extra_slots, ns_bytes, ns_off, ns_id;
     ResolveDev view{};
     RBuf blob, reqs, ids, status, dec, cnt, clk;
+    std::mutex slot_mu;            // the batches in flight (KETO_PACKED_SLOTS)
+    std::condition_variable slot_cv;
+    std::vector<std::unique_ptr<PSlot>> slots;
+    std::vector<uint8_t> slot_busy;
     ~RDevState() {
         (void)hipSetDevice(device);
+        slots.clear();
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
@@ -438,6 +464,116 @@ uint64_t packed_chunk() {
     const char* e = getenv("KETO_PACKED_CHUNK");
     return e ? (uint64_t)std::max(0ll, atoll(e)) : (1ull << 21);
 }
+
+// packed batches a snapshot keeps in flight at once (KETO_PACKED_SLOTS, default 2; 0 = one batch at
+// a time through the synchronous path)
+uint32_t packed_slots() {
+    const char* e = getenv("KETO_PACKED_SLOTS");
+    return e ? (uint32_t)std::min(16, std::max(0, atoi(e))) : 2u;
+}
+
+// A batch of one piece on an unpartitioned snapshot, with max-depth <= 9, and no host round trip
+// before its results: a free slot takes it; its upload and resolution run on the slot's stream (no
+// lock: another slot's batch may be checking meanwhile), its check is enqueued behind them under the
+// device lock (device_check_rows_async), and the decisions, statuses and every counter come home in
+// one copy.  Only then are the counters looked at: a request outside the blob fails the call before
+// the outputs are written, as on the synchronous path; a batch whose check needs tier 2 (tier-1
+// overflows) returns false, and the caller checks it again synchronously.
+bool device_check_packed_async(Snapshot& S, RDevState& R, const uint8_t* blob, uint64_t blob_len,
+                               const keto_check_packed* reqs, uint32_t n, int32_t gmd, uint8_t* allowed, uint8_t* status,
+                               std::vector<uint32_t>& host) {
+    ResolveDev view;
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        rdev_refresh(S, R);
+        view = R.view;
+    }
+    PSlot* P = nullptr;
+    uint32_t si = 0;
+    {
+        std::unique_lock<std::mutex> lk(R.slot_mu);
+        const uint32_t want = packed_slots();
+        while (R.slots.size() < want) {
+            R.slots.emplace_back(new PSlot);
+            R.slot_busy.push_back(0);
+        }
+        R.slot_cv.wait(lk, [&] {
+            for (si = 0; si < want; ++si)
+                if (!R.slot_busy[si]) return true;
+            return false;
+        });
+        R.slot_busy[si] = 1;
+        P = R.slots[si].get();
+    }
+    struct Free {                    // the slot's work drained (no copy from the caller outlives the call), then freed
+        RDevState& R;
+        PSlot* P;
+        uint32_t si;
+        bool checking = false;       // a check reading the slot's buffers is enqueued on the device's stream
+        ~Free() {
+            if (checking) (void)hipEventSynchronize(P->done);
+            if (P->st) (void)hipStreamSynchronize(P->st);
+            {
+                std::lock_guard<std::mutex> lk(R.slot_mu);
+                R.slot_busy[si] = 0;
+            }
+            R.slot_cv.notify_one();
+        }
+    } free_slot{R, P, si};
+    P->device = R.device;
+    if (!P->st) {
+        HIP_OK(hipStreamCreateWithFlags(&P->st, hipStreamNonBlocking));
+        HIP_OK(hipEventCreateWithFlags(&P->ready, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&P->done, hipEventDisableTiming));
+    }
+    const uint64_t hbytes = 2ull * n + 64;
+    if (P->host_cap < hbytes) {
+        if (P->host) (void)hipHostFree(P->host);
+        P->host = nullptr;
+        P->host_cap = 0;
+        const uint64_t c = std::max<uint64_t>(hbytes + hbytes / 4, 1 << 20);
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&P->host), c, hipHostMallocDefault);
+        if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e)};
+        P->host_cap = c;
+    }
+    hipStream_t st = P->st;
+    uint8_t* d_blob = P->blob.get<uint8_t>(std::max<uint64_t>(blob_len, 1));
+    keto_check_packed* d_q = P->reqs.get<keto_check_packed>(std::max<uint32_t>(n, 1));
+    keto_check_ids* d_ids = P->ids.get<keto_check_ids>(n);
+    uint8_t* d_st = P->status.get<uint8_t>(n);
+    uint8_t* d_dec = P->dec.get<uint8_t>(n);
+    uint32_t* d_cnt = P->cnt.get<uint32_t>(6);          // resolve: bad, host, order | check: overflows, -, misrouted
+    keto_check_ids* d_x = P->xlate.get<keto_check_ids>(n);
+    if (blob_len) HIP_OK(hipMemcpyAsync(d_blob, blob, blob_len, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_q, reqs, (uint64_t)n * sizeof(keto_check_packed), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
+    HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 2 * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(resolve_packed<false>, dim3((n + 255) / 256), dim3(256), 0, st, view, d_blob, blob_len, 0ull,
+                       blob_len, d_q, 0u, n, d_ids, d_st, d_cnt, nullptr);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(P->ready, st));
+    if (!device_check_rows_async(S, d_ids, n, gmd, d_dec, d_x, d_cnt + 3, P->ready, P->done)) return false;
+    free_slot.checking = true;
+    HIP_OK(hipStreamWaitEvent(st, P->done, 0));
+    hipLaunchKernelGGL(fold_undecided, dim3((n + 255) / 256), dim3(256), 0, st, d_dec, d_st, n);
+    HIP_OK(hipGetLastError());
+    uint8_t* h = P->host;
+    uint32_t* hc = reinterpret_cast<uint32_t*>(h + ((2ull * n + 15) & ~15ull));
+    HIP_OK(hipMemcpyAsync(h, d_dec, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h + n, d_st, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(hc, d_cnt, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    lock_trace("packed async: copied back");
+    if (hc[0] != NO_BAD) throw Error{KETO_E_INVALID, "request " + std::to_string(hc[0]) + "'s fields lie outside the blob"};
+    static const bool force_sync = getenv("KETO_TEST_PACKED_FALLBACK") != nullptr;   // test hook
+    if (hc[3] || hc[5] || force_sync) return false;   // tier 2 needed (or a misrouted row): the synchronous path
+    std::memcpy(allowed, h, n);
+    std::memcpy(status, h + n, n);
+    if (hc[1])                                   // the wildcard queries: the host's
+        for (uint32_t i = 0; i < n && host.size() < hc[1]; ++i)
+            if (status[i] == ST_HOST) host.push_back(i);
+    return true;
+}
 }  // namespace
 
 // A batch of 2 pieces or more on an unpartitioned snapshot is pipelined: the blob and the records go
@@ -455,6 +591,15 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
     const DevView dv = device_view(S);
     HIP_OK(hipSetDevice(dv.device));
     RDevState& R = rdev_get(S, dv.device);
+    static const bool clocks = getenv("KETO_RESOLVE_CLOCKS") != nullptr;  // tooling: per-step clocks
+    {
+        const uint64_t chunk = packed_chunk();
+        const bool one_piece = !(chunk && S.n_parts == 1 && n >= 2 * chunk);
+        if (n && one_piece && S.n_parts == 1 && !clocks && packed_slots() > 0 && std::min<int32_t>(gmd, 65535) <= 9 &&
+            device_check_packed_async(S, R, blob, blob_len, reqs, n, gmd, allowed, status, host))
+            return;
+        host.clear();
+    }
     lock_trace("packed: waiting for R.mu");
     std::lock_guard<std::mutex> lk(R.mu);                                   // held through the last copy
     lock_trace("packed: R.mu");
@@ -503,7 +648,6 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
         HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
         HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 2 * sizeof(uint32_t), st));
     };
-    static const bool clocks = getenv("KETO_RESOLVE_CLOCKS") != nullptr;  // tooling: per-step clocks
     uint32_t* d_clk = clocks && K == 1 ? R.clk.get<uint32_t>(4ull * n) : nullptr;
     auto resolve = [&](uint32_t i0, uint32_t m, uint64_t hi) {
         if (!m) return;

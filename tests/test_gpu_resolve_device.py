@@ -259,3 +259,71 @@ def test_packed_batches_concurrent_with_writes():
     got = _same_as_host(snap, wreq, 5)
     assert got.all()
     snap.close()
+
+
+def test_packed_batches_in_flight_equal_sync(monkeypatch):
+    """Packed batches of one piece keep up to KETO_PACKED_SLOTS in flight per snapshot (resolve_dev.hip
+    device_check_packed_async): one batch's upload and resolution run while another's check does, and
+    the check is enqueued without a host round trip.  Eight threads at once with 1, 2 and 4 slots,
+    and the batch redone on the synchronous path when the check needs tier 2 (forced here by the test
+    hook), all decide like keto_check_batch (host resolution) on the power-law graph."""
+    import threading
+    from tools import synth
+    g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 256), threads=16)
+    st = g.string_tuples(seed=5)
+    snap, _ = g.snapshot_from_strings(st, device=0)
+    q = g.queries(65_536, seed=13, depth=5)
+    arr = g.string_requests(st, q)
+    want, want_st = snap.check_batch_reqs(arr, len(q), 5)
+    blob, rec, used = g.pack_requests(arr, len(q))
+    for env in ({"KETO_PACKED_SLOTS": "0"}, {"KETO_PACKED_SLOTS": "1"}, {}, {"KETO_PACKED_SLOTS": "4"},
+                {"KETO_TEST_PACKED_FALLBACK": "1"}):
+        for k in ("KETO_PACKED_SLOTS", "KETO_TEST_PACKED_FALLBACK"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        errors = []
+
+        def reader():
+            try:
+                for _ in range(6):
+                    got, gst = snap.check_batch_packed(blob.array[:used], rec.array, 5, n=len(q))
+                    if not ((got == want).all() and (gst == want_st).all()):
+                        errors.append(int((got != want).sum()))
+            except Exception as e:      # noqa: BLE001 -- reported below
+                errors.append(repr(e))
+
+        ts = [threading.Thread(target=reader) for _ in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in ts)
+        assert not errors, (env, errors[:5])
+    snap.close()
+    g.close()
+
+
+def test_packed_tier_overflow_in_flight_matches_oracle():
+    """The hub graph of tests/test_gpu_overflow.py through packed batches: maps outgrow tier 0, so the
+    in-flight check runs tier 1 behind tier 0 without reading its count back; every global max-depth
+    from 1 to 7 (max-depth > 9 takes the synchronous path) against the SQL oracle."""
+    import keto_amd
+    from tests.test_gpu_overflow import _graph
+    ns, tuples = _graph()
+    snap = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), device=0)
+    store = SQLStore(ns, tuples)
+    rng = random.Random(5)
+    for gmd in range(1, 8):
+        reqs, items = [], []
+        for _ in range(200):
+            obj = rng.choice(["root", "hub", f"x{rng.randrange(150):04d}"])
+            sub = SubjectID(f"u{rng.randrange(2000):05d}") if rng.random() < 0.8 else SubjectSet("n", f"y{rng.randrange(150):04d}", "r")
+            d = rng.choice([0, 1, 2, 3, 5, 8])
+            items.append((RelationTuple("n", obj, "r", sub), d))
+            reqs.append(("n", obj, "r", subj(sub), d))
+        got = _same_as_host(snap, reqs, gmd)
+        eng = CheckEngine(store, gmd)
+        bad = [(t, d) for (t, d), a in zip(items, got) if bool(a) != eng.subject_is_allowed(t, d)]
+        assert not bad, (gmd, bad[:5])
+    snap.close()

@@ -229,16 +229,24 @@ def test_collective_calls_never_skip_an_empty_batch():
 def test_packed_batches_use_a_reused_pinned_arena():
     """A large packed batch goes up from a page-locked arena (keto_host_alloc) the snapshot keeps
     from call to call, so keto_check_batch_packed can upload it asynchronously under the resolution
-    and check of earlier pieces; the arena is locked for the call and freed with the snapshot."""
+    and check of earlier pieces.  The snapshot keeps one arena per batch in flight (a pool of
+    InflightFromEnv arenas, each locked for its call), frees them all with the snapshot, and the
+    batchers deal InflightFromEnv batches to an engine at once (KETO_GPU_INFLIGHT)."""
     src = _code(open(os.path.join(GO, "internal", "gpu", "gpu.go")).read())
     body = src[src.index("func (s *Snapshot) checkPacked("):]
     body = body[:body.index("\nfunc ")]
-    assert "s.arena.get(" in body and "defer s.arena.put()" in body
-    assert body.index("s.arena.get(") < body.index("C.keto_check_batch_packed(")
+    assert "s.arenas.get(" in body and "defer s.arenas.put(a)" in body
+    assert body.index("s.arenas.get(") < body.index("C.keto_check_batch_packed(")
     arena = src[src.index("func (a *pinnedArena) get("):]
     assert "C.keto_host_alloc(" in arena and "C.keto_host_free(" in arena and "a.mu.Lock()" in arena
+    pool = src[src.index("func (p *arenaPool) init("):]
+    assert "InflightFromEnv()" in pool[:pool.index("\n}")]
     close = src[src.index("func (s *Snapshot) Close()"):]
-    assert "s.arena.free()" in close[:close.index("\n}")]
+    assert "s.arenas.freeAll()" in close[:close.index("\n}")]
+    bat = _code(open(os.path.join(GO, "internal", "gpu", "batcher.go")).read())
+    es = bat[bat.index("func newEngineSet("):]
+    es = es[:es.index("\n}")]
+    assert "InflightFromEnv()" in es and "per*len(snaps)" in es
 
 
 def test_check_flush_size_from_env():

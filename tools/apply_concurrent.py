@@ -87,14 +87,18 @@ def main():
             bad.append(int((out != before).sum()))
 
     def read_threads(seconds, lat, bad):
+        """Runs the readers for `seconds`; returns the checks per second of all of them together."""
         ts = [threading.Thread(target=reads, args=(seconds, lat, bad)) for _ in range(a.readers)]
+        n0 = len(lat)
+        t0 = time.perf_counter()
         for t in ts:
             t.start()
         for t in ts:
             t.join()
+        return round((len(lat) - n0) * len(q) / (time.perf_counter() - t0), 1)
 
     quiet, quiet_bad = [], []
-    read_threads(a.seconds / 2, quiet, quiet_bad)
+    rate_quiet = read_threads(a.seconds / 2, quiet, quiet_bad)
     stop = threading.Event()
     wlat, serial = [], [0]
 
@@ -113,7 +117,7 @@ def main():
     loaded, loaded_bad = [], []
     w = threading.Thread(target=writer)
     w.start()
-    read_threads(a.seconds, loaded, loaded_bad)
+    rate_loaded = read_threads(a.seconds, loaded, loaded_bad)
     stop.set()
     w.join()
     out = {"graph": label, "tuples": int(g.n_edges), "setup_s": round(t_setup, 1),
@@ -121,6 +125,8 @@ def main():
            "requests_per_batch": len(q), "reader_threads": a.readers, "write_tuples": a.k, "writes_add_rows": a.new_rows, "write_gap_ms": a.gap_ms,
            "batch_ms_quiet": {"p50": pct(quiet, 50), "p99": pct(quiet, 99), "n": len(quiet)},
            "batch_ms_with_writes": {"p50": pct(loaded, 50), "p99": pct(loaded, 99), "n": len(loaded)},
+           "checks_per_s_quiet": rate_quiet, "checks_per_s_with_writes": rate_loaded,
+           "packed_slots": os.environ.get("KETO_PACKED_SLOTS", "2 (default)") if a.packed else None,
            "write_ms_under_reads": {"p50": pct(wlat, 50), "p99": pct(wlat, 99), "n": len(wlat)},
            "writes_per_s": round(2 * len(wlat) / a.seconds, 1),
            "untouched_decisions_changed": int(sum(quiet_bad) + sum(loaded_bad)), "version": int(snap.version())}
