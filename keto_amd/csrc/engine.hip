@@ -2690,6 +2690,10 @@ struct WorkSet {
     uint64_t pool_words = 0;
 };
 
+// streams (and workspaces) of the packed batches checked without a host round trip: two checks of
+// ~65K requests (a few hundred waves each, latency-bound) run side by side
+constexpr int ASYNC_STREAMS = 2;
+
 struct DeviceState {
     int device = 0;
     uint32_t* arena = nullptr;
@@ -2701,14 +2705,15 @@ struct DeviceState {
     uint32_t n_units = 0;         // main-arena handles are < n_units
     uint32_t n_coll = 0;          // collision classes
     std::mutex mu;                // one batch at a time per snapshot (workspaces are shared)
-    WorkSet ws[3];                // check workspaces (ws[1]: the second compute stream of the pipeline;
-                                  // ws[2]: packed batches checked without a host round trip, astream)
+    WorkSet ws[2 + ASYNC_STREAMS];   // check workspaces (ws[1]: the second compute stream of the pipeline;
+                                     // ws[2 + k]: packed batches checked without a host round trip, astream[k])
     WorkSet ews;                  // expand workspaces
     uint32_t v1_lanes[16] = {};   // resident lanes of the tier-0 check kernel, per variant
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;    // the pipeline's second compute stream (ws[1])
-    hipStream_t astream = nullptr;    // device_check_rows_async: every such check in call order (ws[2])
-    std::vector<hipEvent_t> aev;      // its stash timing events (3)
+    hipStream_t astream[ASYNC_STREAMS] = {};   // device_check_rows_async: the checks, dealt in turn (ws[2 + k])
+    uint32_t amax[ASYNC_STREAMS] = {};         // the largest batch each has checked (its workspace's size)
+    uint32_t anext = 0;
     hipEvent_t ev[6] = {};
     keto_batch_timing last{};
     uint32_t* row_handle = nullptr;   // row id -> handle (NO_UNIT: another part's root row), lazily
@@ -2741,6 +2746,8 @@ struct DeviceState {
     uint64_t* ex_pieces = nullptr;    // copy_stage_pieces' {source, destination, length} triples
     uint64_t ex_pieces_cap = 0;
     hipEvent_t ex_ev[4] = {};         // copy_runs / gather timing (added to tier 0 of the batch timing)
+    uint8_t* ap_buf = nullptr;        // a write's row images and their places, uploaded at once
+    uint64_t ap_cap = 0;
     keto_check_ids* xlate = nullptr;  // requests translated from row ids to handles
     uint64_t xlate_cap = 0;
     // host-buffer calls (device_check_host): a pipeline of chunks over two device slots, H2D on
@@ -3445,6 +3452,17 @@ __global__ void __launch_bounds__(256) scatter_pairs(uint32_t* __restrict__ dst,
 namespace {
 // device_apply in place; false (nothing written to the device yet) when a new subject-set target
 // finds no place below 2^31 units
+// a write's row images into the arena, in order (one block: a later image wins where two meet, as
+// the per-image copies did; seg: arena word, first word in img, words)
+__global__ void __launch_bounds__(256) scatter_images(uint32_t* __restrict__ arena, const uint64_t* __restrict__ seg,
+                                                      const uint32_t* __restrict__ img, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t to = seg[3 * i], from = seg[3 * i + 1], len = seg[3 * i + 2];
+        for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) arena[to + k] = img[from + k];
+        __syncthreads();
+    }
+}
+
 bool apply_in_place(Snapshot& S) {
     DeviceState& D = *S.dev;
     lock_trace("apply: waiting for D.mu");
@@ -3602,9 +3620,39 @@ bool apply_in_place(Snapshot& S) {
         D.arena = na;
         D.arena_words = cap;
     }
-    for (const Write& w : writes)
-        HIP_OK(hipMemcpyAsync(D.arena + w.word, w.img.data(), w.img.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                              D.stream));
+    // every image in one upload, then one kernel writes them into the arena in order (one pageable
+    // copy per image took ~4 us each: 0.42 ms of a 100-row write's exclusive part on the 1B graph)
+    if (!writes.empty()) {
+        uint64_t words = 0;
+        for (const Write& w : writes) words += w.img.size();
+        const uint64_t nw = writes.size(), need_b = words * 4 + nw * 24;
+        if (D.ap_cap < need_b) {
+            if (D.ap_buf) (void)hipFree(D.ap_buf);
+            D.ap_buf = nullptr;
+            D.ap_cap = 0;
+            uint64_t acc = 0;
+            const uint64_t c = std::max<uint64_t>(need_b + need_b / 2, 1 << 20);
+            D.ap_buf = dmalloc<uint8_t>(c, acc);
+            D.ap_cap = c;
+        }
+        std::vector<uint8_t> up(need_b);
+        uint64_t* seg = reinterpret_cast<uint64_t*>(up.data());          // (arena word, first image word, words)
+        uint32_t* img = reinterpret_cast<uint32_t*>(up.data() + nw * 24);
+        uint64_t at = 0;
+        for (uint64_t i = 0; i < nw; ++i) {
+            const Write& w = writes[i];
+            seg[3 * i] = w.word;
+            seg[3 * i + 1] = at;
+            seg[3 * i + 2] = w.img.size();
+            std::memcpy(img + at, w.img.data(), w.img.size() * 4);
+            at += w.img.size();
+        }
+        HIP_OK(hipMemcpyAsync(D.ap_buf, up.data(), need_b, hipMemcpyHostToDevice, D.stream));
+        hipLaunchKernelGGL(scatter_images, dim3(1), dim3(256), 0, D.stream, D.arena,
+                           reinterpret_cast<const uint64_t*>(D.ap_buf),
+                           reinterpret_cast<const uint32_t*>(D.ap_buf + nw * 24), nw);
+        HIP_OK(hipGetLastError());
+    }
     HIP_OK(hipStreamSynchronize(D.stream));
     lap("copies");
     // 4. closure filters of every row with one (from their own ids up)
@@ -3762,6 +3810,7 @@ void device_release(Snapshot& S) {
     for (hipEvent_t e : D.ex_ev)
         if (e) (void)hipEventDestroy(e);
     if (D.xlate) (void)hipFree(D.xlate);
+    if (D.ap_buf) (void)hipFree(D.ap_buf);
     if (D.st_pairs) (void)hipFree(D.st_pairs);
     if (D.st_dec) (void)hipFree(D.st_dec);
     if (D.st_x) (void)hipFree(D.st_x);
@@ -3775,8 +3824,8 @@ void device_release(Snapshot& S) {
     }
     if (D.stream) (void)hipStreamDestroy(D.stream);
     if (D.stream2) (void)hipStreamDestroy(D.stream2);
-    if (D.astream) (void)hipStreamDestroy(D.astream);
-    for (auto& e : D.aev) (void)hipEventDestroy(e);
+    for (hipStream_t& a : D.astream)
+        if (a) (void)hipStreamDestroy(a);
     if (D.copy_in) (void)hipStreamDestroy(D.copy_in);
     if (D.copy_out) (void)hipStreamDestroy(D.copy_out);
     for (auto& e : D.ev)
@@ -3861,6 +3910,9 @@ struct Undecided {
 // overflows (requests that need tier 2) are copied to a batch-wide stash instead, and decided by a
 // full check of the stash once every chunk is done.
 struct PipeStash {
+    // t0_only (device_check_rows_async): tier 0 alone; its overflow count goes to count[0] and the
+    // workset's counters are left zero for the next batch (one small kernel, no memset, no events)
+    bool t0_only = false;
     keto_check_ids* q = nullptr;   // device: stashed requests (handle form)
     uint32_t* idx = nullptr;       // device: their batch indices
     uint32_t* count = nullptr;     // device: how many
@@ -3884,6 +3936,14 @@ __global__ void __launch_bounds__(256) stash_overflow(const keto_check_ids* __re
             sq[at] = q[list[i]];
             sidx[at] = base + list[i];
         }
+    }
+}
+
+// the end of a t0_only batch: tier 0's overflow count out, the workset's tier counters zeroed
+__global__ void t0_tail(uint32_t* __restrict__ counters, uint32_t* __restrict__ out) {
+    if (threadIdx.x == 0) {
+        out[0] = counters[0];
+        for (int i = 0; i < 4; ++i) counters[i] = 0;
     }
 }
 
@@ -3911,6 +3971,12 @@ void run_tiers(DeviceState& D, WorkSet& W, uint32_t n, const Plan& p, hipStream_
             W.pool_words = words;
         }
         HIP_OK(hipMemsetAsync(W.pool_busy, 0, words * sizeof(uint32_t), st));
+    }
+    if (stash && stash->t0_only) {
+        launch(0, set[0], (const uint32_t*)nullptr, (const uint32_t*)nullptr, list0, c0, p.slots[0]);
+        hipLaunchKernelGGL(t0_tail, dim3(1), dim3(64), 0, st, W.counters, stash->count);
+        HIP_OK(hipGetLastError());
+        return;
     }
     HIP_OK(hipMemsetAsync(W.counters, 0, 4 * sizeof(uint32_t), st));
     if (stash) {
@@ -5064,16 +5130,16 @@ void device_check_rows(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, in
     lock_trace("rows: check launched");
 }
 
-// A batch of row-id requests checked without a host round trip (the packed path's batches in flight,
-// resolve_dev.hip): under the device lock, only enqueued -- on D.astream, after `ready`: the
-// translation into the caller's d_xlate, tiers 0 and 1 on their own workspace (ws[2]) with the
-// tier-1 overflows only counted (d_counts[0]; stash of capacity 0), then `done` recorded.  Another
-// batch's upload and resolution run meanwhile on their own streams, and this call returns before the
-// check ends.  A batch with d_counts[0] > 0 needs tier 2 and is checked again by the caller through
-// device_check_rows.  Deep batches (max-depth > 9) are not taken: false.  Rows must be valid
-// (unpartitioned snapshot); d_counts[2] counts misrouted rows anyway.
-bool device_check_rows_async(Snapshot& S, const keto_check_ids* d_rows, uint32_t n, int32_t gmd, uint8_t* d_allowed,
-                             keto_check_ids* d_xlate, uint32_t* d_counts, void* ready_event, void* done_event) {
+// A batch of requests in the handle form checked without a host round trip (the packed path's
+// batches in flight, resolve_dev.hip): under the device lock, only enqueued -- on one of the
+// ASYNC_STREAMS check streams in turn, after `ready`: tier 0 on that stream's workspace (ws[2 + k]),
+// then t0_tail writes tier 0's overflow count to d_counts[0] and `done` is recorded.  Other batches'
+// uploads, resolutions and checks run meanwhile on their own streams, and this call returns before
+// the check ends.  A batch with d_counts[0] > 0 needs the next tiers and is checked again by the
+// caller through device_check_rows.  Deep batches (max-depth > 9) and partitioned snapshots are not
+// taken: false.
+bool device_check_rows_async(Snapshot& S, const keto_check_ids* d_handles, uint32_t n, int32_t gmd,
+                             uint8_t* d_allowed, uint32_t* d_counts, void* ready_event, void* done_event) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
     hipEvent_t ready = (hipEvent_t)ready_event, done = (hipEvent_t)done_event;
     if (std::max(1, std::min<int32_t>(gmd, 65535) - 1) > 8 || S.n_parts != 1) return false;
@@ -5081,32 +5147,45 @@ bool device_check_rows_async(Snapshot& S, const keto_check_ids* d_rows, uint32_t
     lock_trace("rows async: waiting for D.mu");
     std::lock_guard<std::mutex> lk(D.mu);
     HIP_OK(hipSetDevice(D.device));
-    if (!D.astream) HIP_OK(hipStreamCreateWithFlags(&D.astream, hipStreamNonBlocking));
-    while (D.aev.size() < 3) {
-        hipEvent_t e;
-        HIP_OK(hipEventCreate(&e));
-        D.aev.push_back(e);
+    const uint32_t k = D.anext++ % ASYNC_STREAMS;
+    WorkSet& W = D.ws[2 + k];
+    if (!D.astream[k]) {
+        HIP_OK(hipStreamCreateWithFlags(&D.astream[k], hipStreamNonBlocking));
+        ensure_lists(W, n);
+        HIP_OK(hipMemset(W.counters, 0, 8 * sizeof(uint32_t)));      // t0_tail keeps them zero after each batch
     }
-    hipStream_t st = D.astream;
+    hipStream_t st = D.astream[k];
+    if (n > D.amax[k]) {
+        // a larger batch grows the workspace (its lists and tier tables are freed and allocated
+        // again): the stream's earlier checks must be done with them
+        HIP_OK(hipStreamSynchronize(st));
+        D.amax[k] = n;
+    }
     HIP_OK(hipStreamWaitEvent(st, ready, 0));
-    HIP_OK(hipMemsetAsync(d_counts, 0, 3 * sizeof(uint32_t), st));
-    translate_rows_locked(S, D, d_rows, d_xlate, n, st, d_counts + 2);
     PipeStash ps;
-    ps.q = d_xlate;                   // (capacity 0: nothing is stashed, the overflows are counted)
-    ps.idx = nullptr;
+    ps.t0_only = true;
     ps.count = d_counts;
-    ps.cap = 0;
-    ps.base = 0;
-    ps.dq = d_xlate;
-    ps.ev = D.aev;
-    ps.chunk = 0;
+    ps.dq = d_handles;
     const keto_batch_timing before = D.last;
-    check_locked(S, D, d_xlate, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, true, nullptr, &ps, 2);
+    check_locked(S, D, d_handles, n, gmd, d_allowed, st, DevOverlay{nullptr, 0xFFFFFFFFu}, nullptr, true, nullptr, &ps,
+                 2 + (int)k);
     D.last = before;
     D.last.requests[0] = n;
     HIP_OK(hipEventRecord(done, st));
     lock_trace("rows async: enqueued");
     return true;
+}
+
+// The row id -> handle map on the device (built on first use; a write patches it under the
+// exclusive lock): the packed path's resolution writes handles with it.  Call with the snapshot lock
+// held shared; the map stays valid until it is released.
+const uint32_t* device_row_handle_map(Snapshot& S) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    DeviceState& D = *S.dev;
+    std::lock_guard<std::mutex> lk(D.mu);
+    HIP_OK(hipSetDevice(D.device));
+    translate_rows_locked(S, D, nullptr, nullptr, 0, nullptr, nullptr);
+    return D.row_handle;
 }
 
 // Expand output: set nodes carry row handles; map them to row ids on the device (binary search in

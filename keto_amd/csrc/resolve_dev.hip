@@ -76,6 +76,7 @@ using StrSlot = Snapshot::StrSlot;
 using RowSlot = Snapshot::RowSlot;
 constexpr uint32_t INLINE = sizeof(StrSlot::b);
 constexpr uint32_t NO_BAD = 0xFFFFFFFFu;           // no request outside the blob
+constexpr uint32_t NO_UNIT_R = 0xFFFFFFFFu;        // the row -> handle map's "not on this part" (engine.hip NO_UNIT)
 constexpr uint8_t ST_HOST = 0xFF;                   // resolved on the host (wildcards)
 
 // ---- hashing, mirrored bit for bit from parallel.hpp (hash_bytes, mix64) and resolve.cpp (row_hash)
@@ -201,12 +202,15 @@ __device__ int64_t query_row_dev(const ResolveDev& R, const uint8_t* f, uint32_t
 //
 // CLK (KETO_RESOLVE_CLOCKS, tooling): each request's lane records wall_clock64() (100 MHz) at its
 // start, after its record load, after its row query and after its subject lookup into clk[4 i ..].
-template <bool CLK = false>
+// XL (the batches in flight): rows and subject-set targets come out as handles through the device's
+// row id -> handle map (rows_to_handles' rule), a row this part does not hold counted in cnt[3]
+template <bool CLK = false, bool XL = false>
 __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                       uint64_t lo, uint64_t hi, const keto_check_packed* __restrict__ q,
                                                       uint32_t i0, uint32_t n, keto_check_ids* __restrict__ out,
                                                       uint8_t* __restrict__ status, uint32_t* __restrict__ cnt,
-                                                      uint32_t* __restrict__ clk = nullptr) {
+                                                      uint32_t* __restrict__ clk = nullptr,
+                                                      const uint32_t* __restrict__ row_handle = nullptr, uint32_t n_rows = 0) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t i = i0 + k;
@@ -250,6 +254,17 @@ __global__ void __launch_bounds__(256) resolve_packed(ResolveDev R, const uint8_
             }
         }
     }
+    if constexpr (XL) {
+        if (r.row != KETO_NO_ROW) {
+            const uint32_t h = r.row < n_rows ? row_handle[r.row] : NO_UNIT_R;
+            if (h == NO_UNIT_R) atomicAdd(cnt + 3, 1u);
+            r.row = h == NO_UNIT_R ? KETO_NO_ROW : h;
+        }
+        if ((r.flags & 1u) && r.target != KETO_NO_TARGET) {
+            const uint32_t h = r.target < n_rows ? row_handle[r.target] : NO_UNIT_R;
+            r.target = h == NO_UNIT_R ? KETO_NO_TARGET : h;
+        }
+    }
     out[i] = r;
     status[i] = st;
     if constexpr (CLK) {
@@ -272,6 +287,20 @@ __global__ void __launch_bounds__(256) fold_undecided(uint8_t* __restrict__ allo
     if (status[i] == KETO_CHECK_OK) status[i] = KETO_CHECK_UNDECIDED;
 }
 
+// fold_undecided for a batch in flight; its first thread also readies the slot's other counter block
+// for the slot's next batch ({NO_BAD, 0, ...}: that block's batch has completed)
+__global__ void __launch_bounds__(256) fold_and_reset(uint8_t* __restrict__ allowed, uint8_t* __restrict__ status,
+                                                      uint32_t n, uint32_t* __restrict__ next_cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        next_cnt[0] = NO_BAD;
+        for (int k = 1; k < 8; ++k) next_cnt[k] = 0;
+    }
+    if (i >= n || status[i] == ST_HOST || allowed[i] <= 1) return;
+    allowed[i] = 0;
+    if (status[i] == KETO_CHECK_OK) status[i] = KETO_CHECK_UNDECIDED;
+}
+
 template <class T>
 T* upload(RBuf& b, const T* src, uint64_t n, hipStream_t st) {
     T* d = b.get<T>(std::max<uint64_t>(n, 1));
@@ -287,8 +316,11 @@ struct PSlot {
     int device = 0;
     hipStream_t st = nullptr;
     hipEvent_t ready = nullptr, done = nullptr;   // resolved (the check may start) / checked
-    RBuf blob, reqs, ids, status, dec, cnt, xlate;
-    uint8_t* host = nullptr;       // pinned: decisions | statuses | the six counter words
+    RBuf blob, reqs, ids, out;     // out: decisions | statuses | two blocks of 8 counter words
+    uint64_t out_n = 0;            // the batch size out is laid out for
+    uint32_t par = 0;              // the counter block of the next batch
+    bool clean[2] = {false, false};   // that block holds {NO_BAD, 0, ...}
+    uint8_t* host = nullptr;       // pinned: the copy of out
     uint64_t host_cap = 0;
     ~PSlot() {
         (void)hipSetDevice(device);
@@ -473,12 +505,16 @@ uint32_t packed_slots() {
 }
 
 // A batch of one piece on an unpartitioned snapshot, with max-depth <= 9, and no host round trip
-// before its results: a free slot takes it; its upload and resolution run on the slot's stream (no
-// lock: another slot's batch may be checking meanwhile), its check is enqueued behind them under the
-// device lock (device_check_rows_async), and the decisions, statuses and every counter come home in
-// one copy.  Only then are the counters looked at: a request outside the blob fails the call before
-// the outputs are written, as on the synchronous path; a batch whose check needs tier 2 (tier-1
-// overflows) returns false, and the caller checks it again synchronously.
+// before its results: a free slot takes it; its upload and its resolution -- straight to the handle
+// form through the device's row -> handle map -- run on the slot's stream (no lock: other slots'
+// batches may be resolving or checking meanwhile), its tier-0 check is enqueued behind them under the
+// device lock (device_check_rows_async, one of two check streams), and the decisions, statuses and
+// every counter come home in one copy.  Only then are the counters looked at: a request outside the
+// blob fails the call before the outputs are written, as on the synchronous path; a batch some of
+// whose requests tier 0 hands up (rare at max-depth <= 9: none in the 1B graph's 16.7M) returns
+// false, and the caller checks it again synchronously through every tier.  The slot's counters are
+// two blocks used in turn: each batch's last kernel readies the other one, so no batch starts with
+// memsets.
 bool device_check_packed_async(Snapshot& S, RDevState& R, const uint8_t* blob, uint64_t blob_len,
                                const keto_check_packed* reqs, uint32_t n, int32_t gmd, uint8_t* allowed, uint8_t* status,
                                std::vector<uint32_t>& host) {
@@ -488,6 +524,7 @@ bool device_check_packed_async(Snapshot& S, RDevState& R, const uint8_t* blob, u
         rdev_refresh(S, R);
         view = R.view;
     }
+    const uint32_t* row_handle = device_row_handle_map(S);
     PSlot* P = nullptr;
     uint32_t si = 0;
     {
@@ -526,12 +563,13 @@ bool device_check_packed_async(Snapshot& S, RDevState& R, const uint8_t* blob, u
         HIP_OK(hipEventCreateWithFlags(&P->ready, hipEventDisableTiming));
         HIP_OK(hipEventCreateWithFlags(&P->done, hipEventDisableTiming));
     }
-    const uint64_t hbytes = 2ull * n + 64;
-    if (P->host_cap < hbytes) {
+    // out: decisions at 0, statuses at n, the counter blocks 16-B aligned after them
+    const uint64_t coff = (2ull * n + 15) & ~15ull, obytes = coff + 64;
+    if (P->host_cap < obytes) {
         if (P->host) (void)hipHostFree(P->host);
         P->host = nullptr;
         P->host_cap = 0;
-        const uint64_t c = std::max<uint64_t>(hbytes + hbytes / 4, 1 << 20);
+        const uint64_t c = std::max<uint64_t>(obytes + obytes / 4, 1 << 20);
         const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&P->host), c, hipHostMallocDefault);
         if (e != hipSuccess) throw Error{KETO_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e)};
         P->host_cap = c;
@@ -539,34 +577,43 @@ bool device_check_packed_async(Snapshot& S, RDevState& R, const uint8_t* blob, u
     hipStream_t st = P->st;
     uint8_t* d_blob = P->blob.get<uint8_t>(std::max<uint64_t>(blob_len, 1));
     keto_check_packed* d_q = P->reqs.get<keto_check_packed>(std::max<uint32_t>(n, 1));
-    keto_check_ids* d_ids = P->ids.get<keto_check_ids>(n);
-    uint8_t* d_st = P->status.get<uint8_t>(n);
-    uint8_t* d_dec = P->dec.get<uint8_t>(n);
-    uint32_t* d_cnt = P->cnt.get<uint32_t>(6);          // resolve: bad, host, order | check: overflows, -, misrouted
-    keto_check_ids* d_x = P->xlate.get<keto_check_ids>(n);
+    keto_check_ids* d_x = P->ids.get<keto_check_ids>(n);
+    if (P->out_n != n) {                      // the counter blocks move with n: both need setting up
+        P->out_n = n;
+        P->clean[0] = P->clean[1] = false;
+    }
+    uint8_t* d_out = P->out.get<uint8_t>(obytes);
+    uint8_t* d_dec = d_out;
+    uint8_t* d_st = d_out + n;
+    const uint32_t par = P->par;
+    uint32_t* d_cnt = reinterpret_cast<uint32_t*>(d_out + coff) + 8 * par;   // resolve: bad, host, order, misrouted |
+    uint32_t* d_next = reinterpret_cast<uint32_t*>(d_out + coff) + 8 * (par ^ 1u);   // tier-0 overflows
+    if (!P->clean[par]) {
+        HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
+        HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 7 * sizeof(uint32_t), st));
+    }
+    P->clean[par] = false;
+    P->par = par ^ 1u;
     if (blob_len) HIP_OK(hipMemcpyAsync(d_blob, blob, blob_len, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_q, reqs, (uint64_t)n * sizeof(keto_check_packed), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
-    HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 2 * sizeof(uint32_t), st));
-    hipLaunchKernelGGL(resolve_packed<false>, dim3((n + 255) / 256), dim3(256), 0, st, view, d_blob, blob_len, 0ull,
-                       blob_len, d_q, 0u, n, d_ids, d_st, d_cnt, nullptr);
+    hipLaunchKernelGGL((resolve_packed<false, true>), dim3((n + 255) / 256), dim3(256), 0, st, view, d_blob, blob_len, 0ull,
+                       blob_len, d_q, 0u, n, d_x, d_st, d_cnt, nullptr, row_handle, S.n_rows());
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(P->ready, st));
-    if (!device_check_rows_async(S, d_ids, n, gmd, d_dec, d_x, d_cnt + 3, P->ready, P->done)) return false;
+    if (!device_check_rows_async(S, d_x, n, gmd, d_dec, d_cnt + 4, P->ready, P->done)) return false;
     free_slot.checking = true;
     HIP_OK(hipStreamWaitEvent(st, P->done, 0));
-    hipLaunchKernelGGL(fold_undecided, dim3((n + 255) / 256), dim3(256), 0, st, d_dec, d_st, n);
+    hipLaunchKernelGGL(fold_and_reset, dim3((n + 255) / 256), dim3(256), 0, st, d_dec, d_st, n, d_next);
     HIP_OK(hipGetLastError());
     uint8_t* h = P->host;
-    uint32_t* hc = reinterpret_cast<uint32_t*>(h + ((2ull * n + 15) & ~15ull));
-    HIP_OK(hipMemcpyAsync(h, d_dec, n, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(h + n, d_st, n, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(hc, d_cnt, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h, d_out, coff + 8 * (par + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    P->clean[par ^ 1u] = true;
+    const uint32_t* hc = reinterpret_cast<const uint32_t*>(h + coff) + 8 * par;
     lock_trace("packed async: copied back");
     if (hc[0] != NO_BAD) throw Error{KETO_E_INVALID, "request " + std::to_string(hc[0]) + "'s fields lie outside the blob"};
     static const bool force_sync = getenv("KETO_TEST_PACKED_FALLBACK") != nullptr;   // test hook
-    if (hc[3] || hc[5] || force_sync) return false;   // tier 2 needed (or a misrouted row): the synchronous path
+    if (hc[4] || hc[3] || force_sync) return false;   // the next tiers needed (or a misrouted row): the synchronous path
     std::memcpy(allowed, h, n);
     std::memcpy(status, h + n, n);
     if (hc[1])                                   // the wildcard queries: the host's

@@ -511,11 +511,14 @@ keto_batch_timing device_last_timing(const Snapshot& s);
 // snapshot), so the misrouted-row count is not read back (a host round trip fewer)
 void device_check_rows(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed,
                        void* stream, bool rows_valid = false);
-// the same with valid rows, without a host round trip: enqueued after `ready`, `done` recorded when the
-// decisions are in d_allowed; d_counts (3 words): tier-1 overflows (> 0: check the batch again with
-// device_check_rows), -, misrouted rows.  false: not taken (deep batch or a partitioned snapshot)
-bool device_check_rows_async(Snapshot& s, const keto_check_ids* d_rows, uint32_t n, int32_t gmd, uint8_t* d_allowed,
-                             keto_check_ids* d_xlate, uint32_t* d_counts, void* ready_event, void* done_event);
+// requests already in the handle form, checked without a host round trip: enqueued after `ready`,
+// `done` recorded when the decisions are in d_allowed; d_counts[0]: tier-0 overflows (> 0: check the
+// batch again with device_check_rows).  false: not taken (deep batch or a partitioned snapshot)
+bool device_check_rows_async(Snapshot& s, const keto_check_ids* d_handles, uint32_t n, int32_t gmd,
+                             uint8_t* d_allowed, uint32_t* d_counts, void* ready_event, void* done_event);
+// the device row id -> handle map (NO_UNIT: a row this part does not hold); valid while the caller
+// holds the snapshot lock
+const uint32_t* device_row_handle_map(Snapshot& s);
 const char* device_check_kernel_name(int32_t gmd);
 // deep batches (reach.hip): requests split into top-level items, items pretested by hop-bounded
 // reachability; engine.hip checks the kept work requests, then reach_merge folds their decisions
