@@ -143,7 +143,8 @@ def test_partitioned_serving():
     assert ".ExpandBatchRouted(p.parts[k], subs[lo:hi]" in part
     assert "wg.Wait()" in part                                           # the ranks' calls run at once
     apply_at = part.index("func (p *Partition) Apply(")
-    assert "s.Apply(inserts, deletes)" in part[apply_at:apply_at + 400]
+    assert "p.parts[k].Apply(inserts, deletes)" in part[apply_at:apply_at + 400]       # every part, side by side
+    assert "p.ranks(" in part[apply_at:apply_at + 400]
 
 
 def test_persisted_snapshot_at_startup():
