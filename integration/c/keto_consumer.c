@@ -10,7 +10,9 @@
  * does.  tests/test_consumer_c.py compiles it with gcc against the header and runs it: host-only
  * (device -1: compute must fail with KETO_E_HIP) on the CPU, and on the GPU the reference's golden
  * cases (tests/golden/reference_cases.json) and seeded write / check / expand sequences compared with
- * the SQL oracle.
+ * the SQL oracle.  Every check batch also goes through keto_check_batch_packed (the Go shim's call),
+ * once alone and then from four threads at once, three times each (the batcher keeps batches in
+ * flight per engine, KETO_GPU_INFLIGHT): decisions and statuses must equal keto_check_batch's.
  *
  * Several GPUs in the one server process (registry_gpu.go EnableGPU over a device list): with an
  * "R" line the consumer keeps one replica per listed device -- the first built from the table, the
@@ -307,6 +309,38 @@ typedef struct {
     int rc;
 } rank_call_t;
 
+/* one thread's packed batches (keto_check_batch_packed from several threads on one snapshot) */
+#define PACKED_THREADS 4
+typedef struct {
+    keto_snapshot* snap;
+    const char* blob;
+    size_t total;
+    const keto_check_packed* pk;
+    uint32_t m;
+    int32_t gmd;
+    const uint8_t* want_allowed;
+    const uint8_t* want_status;
+    int bad;
+} packed_call_t;
+
+static void* packed_main(void* arg) {
+    packed_call_t* c = (packed_call_t*)arg;
+    uint8_t* a = (uint8_t*)malloc(c->m ? c->m : 1);
+    uint8_t* st = (uint8_t*)malloc(c->m ? c->m : 1);
+    if (!a || !st) exit(3);
+    for (int rep = 0; rep < 3 && !c->bad; ++rep) {
+        if (keto_check_batch_packed(c->snap, c->blob, c->total, c->pk, c->m, c->gmd, a, st) != KETO_OK) {
+            c->bad = 1;
+            break;
+        }
+        for (uint32_t k = 0; k < c->m; ++k)
+            if (a[k] != c->want_allowed[k] || st[k] != c->want_status[k]) c->bad = 1;
+    }
+    free(a);
+    free(st);
+    return NULL;
+}
+
 static void* rank_main(void* arg) {
     rank_call_t* c = (rank_call_t*)arg;
     partition_t* pt = c->pt;
@@ -584,6 +618,20 @@ int main(int argc, char** argv) {
                 if (rc != KETO_OK) fail("keto_check_batch_packed", rc);
                 for (size_t k = 0; k < m; ++k)
                     if (pa[k] != allowed[k] || ps[k] != status[k]) return 13;
+                /* several threads at once, as the Go batcher keeps batches in flight per engine: the
+                   library runs one's upload and resolution under another's check; every thread's
+                   decisions and statuses must equal keto_check_batch's */
+                {
+                    packed_call_t pc[PACKED_THREADS];
+                    pthread_t th[PACKED_THREADS];
+                    for (int t = 0; t < PACKED_THREADS; ++t) {
+                        pc[t] = (packed_call_t){snap, blob, total, pk, (uint32_t)m, gmd, allowed, status, 0};
+                        if (pthread_create(&th[t], NULL, packed_main, &pc[t]) != 0) exit(3);
+                    }
+                    for (int t = 0; t < PACKED_THREADS; ++t) pthread_join(th[t], NULL);
+                    for (int t = 0; t < PACKED_THREADS; ++t)
+                        if (pc[t].bad) return 14;
+                }
                 free(blob);
                 free(pk);
                 free(pa);
