@@ -21,7 +21,10 @@
  * during the call.  The library keeps no caller pointers after a call returns.  A snapshot may be
  * shared by concurrent *_batch calls from any threads; calls on one snapshot run one at a time on its
  * device (a batch's persistent grid fills the whole GPU, so overlapping two would not finish either
- * sooner), each call's host-side work (resolution, staging) runs in the calling thread.
+ * sooner), each call's host-side work (resolution, staging) runs in the calling thread.  The
+ * exception is keto_check_batch_packed with a small batch (below), whose calls from several threads
+ * keep up to KETO_PACKED_SLOTS (default 2) batches in flight: one's upload and resolution run while
+ * another's check does.
  * Every call returns KETO_OK (0) or a negative KETO_E_* code; keto_last_error() then holds a
  * thread-local message.  There is no CPU fallback inside the library: when the HIP runtime or a
  * device is missing, compute calls fail with KETO_E_HIP.
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 5
+#define KETO_ABI_VERSION 6
 /* The largest arena one snapshot (a replica) or one partition part takes on a device: handles are
  * 32-bit counts of 16-byte units.  A graph past it is served as several shared-rows parts, more than
  * one per device if need be (each part holds the subject-set targets and its share of the root rows). */
@@ -461,6 +464,14 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* s, const keto_check_re
  * page.  Every rank returns the same code when any rank fails. */
 int keto_check_batch_routed(keto_comm* c, keto_snapshot* s, const keto_check_req* reqs, uint32_t n,
                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
+/* The same for a packed batch (the keto_check_batch_packed layout: strings back to back in
+ * blob, one keto_check_packed record per request), resolved on this rank's device instead of on
+ * host threads (ABI 6): the partitioned form of the Go shim's CheckBatch
+ * (integration/go/internal/gpu/partition.go).  Decisions, statuses and errors as
+ * keto_check_batch_routed; a request whose fields lie outside the blob fails the call on every rank. */
+int keto_check_batch_routed_packed(keto_comm* c, keto_snapshot* s, const char* blob, uint64_t blob_len,
+                                   const keto_check_packed* reqs, uint32_t n, int32_t global_max_depth,
+                                   uint8_t* allowed_out, uint8_t* status_out);
 /* BuildTree (internal/expand/engine.go:33-102) over an edge-partitioned snapshot of shared-rows
  * parts (KETO_PART_SHARED; this rank's part as above): every rank passes its own roots; a root row
  * another part owns is expanded on that part (one all-to-all of roots, one of trees), every other

@@ -92,6 +92,73 @@ func (c *Comm) CheckBatchRouted(s *Snapshot, reqs []*relationtuple.InternalRelat
 	})
 }
 
+// packedFits reports whether every request of a batch fits a keto_check_packed record (fields of
+// at most 65,535 bytes, strings below 4 GiB): a partitioned batch then goes packed on every rank
+// (CheckBatchRoutedPacked), else by name on every rank -- the ranks of one collective call agree.
+func packedFits(reqs []*relationtuple.InternalRelationTuple) bool {
+	total := 0
+	for _, r := range reqs {
+		f, k, _ := packedFields(r)
+		for j := 0; j < k; j++ {
+			if len(f[j]) > 65535 {
+				return false
+			}
+			total += len(f[j])
+		}
+	}
+	return total < 1<<32
+}
+
+// CheckBatchRoutedPacked is CheckBatchRouted with the batch packed into one string blob and 24-B
+// records and resolved on this rank's device (keto_check_batch_routed_packed) instead of on host
+// threads.  Collective: every rank calls it, with an empty batch too; every request must fit a
+// record (packedFits).
+func (c *Comm) CheckBatchRoutedPacked(s *Snapshot, reqs []*relationtuple.InternalRelationTuple, depths []int, globalMax int) ([]bool, []uint8, error) {
+	n := len(reqs)
+	if len(depths) != n {
+		return nil, nil, fmt.Errorf("gpu: %d requests, %d depths", n, len(depths))
+	}
+	var m cmem
+	defer m.free()
+	total := 0
+	for _, r := range reqs {
+		f, k, _ := packedFields(r)
+		for j := 0; j < k; j++ {
+			total += len(f[j])
+		}
+	}
+	m.strings(total)
+	rec := (*C.keto_check_packed)(m.alloc(n * int(C.sizeof_keto_check_packed)))
+	allowed := (*C.uint8_t)(m.alloc(n))
+	status := (*C.uint8_t)(m.alloc(n))
+	if n > 0 {
+		rs := unsafe.Slice(rec, n)
+		for i, r := range reqs {
+			f, k, kind := packedFields(r)
+			p := C.keto_check_packed{off: C.uint32_t(m.used), kind: C.uint8_t(kind), max_depth: C.int32_t(depths[i])}
+			for j := 0; j < k; j++ {
+				p.len[j] = C.uint16_t(len(f[j]))
+				m.s(f[j])
+			}
+			rs[i] = p
+		}
+	}
+	if rc := C.keto_check_batch_routed_packed(c.h, s.h, (*C.char)(m.str), C.uint64_t(m.used), rec, C.uint32_t(n),
+		C.int32_t(globalMax), allowed, status); rc != C.KETO_OK {
+		return nil, nil, lastErr(rc)
+	}
+	out := make([]bool, n)
+	st := make([]uint8, n)
+	if n > 0 {
+		as, ss := unsafe.Slice(allowed, n), unsafe.Slice(status, n)
+		for i := range out {
+			out[i] = as[i] == 1
+			st[i] = uint8(ss[i])
+		}
+	}
+	return out, st, nil
+}
+
 // ExpandBatchRouted is BuildTree (internal/expand/engine.go:33-102) for this rank's roots over an
 // edge-partitioned snapshot of shared-rows parts (keto_expand_batch_routed): a root row another
 // part owns is expanded there.  Collective: every rank calls it, with an empty batch too.

@@ -232,9 +232,16 @@ func (p *Partition) CheckBatch(reqs []*relationtuple.InternalRelationTuple, dept
 	defer p.mu.Unlock()
 	allowed := make([]bool, len(reqs))
 	status := make([]uint8, len(reqs))
+	// resolved on every rank's device when every request fits a packed record (the same choice on
+	// every rank: one collective call), else on host threads by name
+	packed := packedFits(reqs)
 	errs := p.ranks(func(k int) error {
 		lo, hi := share(len(reqs), k, len(p.parts))
-		a, st, err := p.comms[k].CheckBatchRouted(p.parts[k], reqs[lo:hi], depths[lo:hi], globalMax)
+		call := p.comms[k].CheckBatchRouted
+		if packed {
+			call = p.comms[k].CheckBatchRoutedPacked
+		}
+		a, st, err := call(p.parts[k], reqs[lo:hi], depths[lo:hi], globalMax)
 		if err != nil {
 			return err
 		}

@@ -16,7 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KETO_LIB") or os.path.join(HERE, "libketo_mi355x.so")   # KETO_LIB: tuning builds
 
-KETO_ABI_VERSION = 5          # include/keto_mi355x.h KETO_ABI_VERSION: load() refuses any other library
+KETO_ABI_VERSION = 6          # include/keto_mi355x.h KETO_ABI_VERSION: load() refuses any other library
 KETO_OK = 0
 E_REBUILD = -6
 CHECK_OK, CHECK_UNKNOWN_NAMESPACE, CHECK_UNDECIDED = 0, 1, 2
@@ -39,6 +39,7 @@ EXPORTS = [
     "keto_part_close", "keto_part_closure_done", "keto_mig_begin", "keto_mig_round", "keto_device_copy", "keto_device_memory", "keto_snapshot_upload_part_migrate",
     "keto_tree_proto_all_device", "keto_tree_json_all", "keto_subject_fields",
     "keto_comm_id", "keto_comm_init", "keto_comm_free", "keto_check_batch_sharded", "keto_check_batch_routed",
+    "keto_check_batch_routed_packed",
     "keto_comm_close_filters", "keto_comm_init_local", "keto_snapshot_clone", "keto_check_batch_packed",
     "keto_snapshot_save", "keto_snapshot_load", "keto_expand_batch_routed",
 ]
@@ -498,11 +499,7 @@ class Snapshot:
         uint8 array or a HostBuffer array) and CHECK_PACKED_DTYPE records.  Returns (allowed, status)."""
         n = len(packed) if n is None else n
         packed = np.ascontiguousarray(packed, dtype=CHECK_PACKED_DTYPE)
-        if isinstance(blob, (bytes, bytearray)):
-            blob = np.frombuffer(blob, dtype=np.uint8) if len(blob) else np.zeros(1, dtype=np.uint8)
-            blen = len(blob) if blob.size else 0
-        else:
-            blen = blob.nbytes
+        blob, blen = _blob_array(blob)
         if allowed is None:
             allowed = np.zeros(max(1, n), dtype=np.uint8)
         if status is None:
@@ -810,6 +807,14 @@ class Snapshot:
         return out
 
 
+def _blob_array(blob):
+    """A packed batch's string blob (bytes, a numpy uint8 array or a HostBuffer array) -> (array, bytes used)."""
+    if isinstance(blob, (bytes, bytearray)):
+        blen = len(blob)
+        return (np.frombuffer(blob, dtype=np.uint8) if blen else np.zeros(1, dtype=np.uint8)), blen
+    return blob, blob.nbytes
+
+
 class Comm:
     """A keto_comm: multi-GPU batches over RCCL behind the C-ABI (keto_amd/csrc/comm.cpp), one process
     per GPU.  Every rank builds it with the id one rank made (Comm.make_id) and distributed."""
@@ -861,6 +866,20 @@ class Comm:
     def check_batch_routed(self, snap, reqs, global_max_depth=5, n=None):
         """keto_check_batch_routed (this rank's part of an edge-partitioned snapshot)."""
         return self._batch(self.lib.keto_check_batch_routed, snap, reqs, global_max_depth, n)
+
+    def check_batch_routed_packed(self, snap, blob, packed: np.ndarray, global_max_depth=5, n=None):
+        """keto_check_batch_routed_packed: a packed batch (as Snapshot.check_batch_packed takes it),
+        resolved on this rank's device and routed to the parts owning its rows."""
+        n = len(packed) if n is None else n
+        packed = np.ascontiguousarray(packed, dtype=CHECK_PACKED_DTYPE)
+        blob, blen = _blob_array(blob)
+        allowed = np.zeros(max(1, n), dtype=np.uint8)
+        status = np.zeros(max(1, n), dtype=np.uint8)
+        _check(self.lib.keto_check_batch_routed_packed(self.h, snap.h, blob.ctypes.data_as(C.c_void_p), C.c_uint64(blen),
+                                                       packed.ctypes.data_as(C.c_void_p), C.c_uint32(n),
+                                                       C.c_int32(global_max_depth), allowed.ctypes.data_as(C.c_void_p),
+                                                       status.ctypes.data_as(C.c_void_p)))
+        return allowed[:n], status[:n]
 
     def expand_batch_routed(self, snap, reqs, global_max_depth=5, **kw):
         """keto_expand_batch_routed (this rank's shared-rows or migrating part): reqs and results as

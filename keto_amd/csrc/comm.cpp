@@ -39,6 +39,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <unordered_map>
 #include <map>
 #include <mutex>
 #include <numeric>
@@ -300,7 +301,7 @@ struct keto_comm {
     // device buffers, kept across calls: a requests, b their order, c routing workspace / output,
     // d routed requests out, g routed requests in, h their decisions, i decisions back, k / l the
     // migrating rounds' records and offsets
-    DBuf a, b, c, d, g, h, i, k, l;
+    DBuf a, b, c, d, e, g, h, i, k, l, p;   // e: a packed batch's host-resolved requests; p: its device-resolved ones
     // owner part per row id (int16, -1 = every part) of the last routed snapshot (its uid, version,
     // partitioning: a snapshot freed and another allocated at its address is not mistaken for it)
     uint64_t owner_uid = 0, owner_version = ~0ull, owner_layout = ~0ull;
@@ -572,8 +573,22 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* h, const keto_check_re
 
 void close_filters(keto_comm* c, keto_snapshot* h, uint32_t* rounds_out);
 
-int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, uint32_t n,
-                            int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
+}  // extern "C"
+
+namespace {
+
+// A packed batch (keto_check_batch_routed_packed): the requests' strings back to back in one blob
+// and 24-B records, resolved on the device.
+struct PackedIn {
+    const char* blob;
+    uint64_t blob_len;
+    const keto_check_packed* reqs;
+};
+
+// keto_check_batch_routed's body, for named requests (reqs: resolved on host threads) or a packed
+// batch (pk: resolved on the device, the wildcard queries it leaves to the host resolved here).
+int routed_check(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, const PackedIn* pk, uint32_t n,
+                 int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
     return guarded([&] {
         if (!c) throw Error{KETO_E_INVALID, "NULL communicator"};
         HIP_OK(hipSetDevice(c->device));
@@ -585,16 +600,41 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         keto_check_ids* d_send = nullptr;
         uint32_t* d_order = nullptr;
         uint64_t wb = 0;
+        // named requests: every request's row-id form; a packed batch: the requests the device left to
+        // the host (wildcard queries), in hidx order, the others in d_pk on the device
         std::vector<keto_check_ids> ids;
+        std::vector<uint32_t> hidx;
+        std::unordered_map<uint32_t, uint32_t> hpos;     // packed: batch index -> position in ids / wr
+        std::vector<keto_check_req> wr;                  // packed: those requests by name (into the blob)
+        keto_check_ids* d_pk = nullptr;
+        auto idref = [&](uint32_t i) -> keto_check_ids& { return pk ? ids[hpos.at(i)] : ids[i]; };
         // a migrating part's wildcard queries: one request per matching row after the batch's own
         // (parent = the query's index), their decisions OR-ed into the query's below
         std::vector<uint32_t> parent;
+        std::vector<keto_check_ids> extra;               // those requests
         uint32_t N = n;                                  // requests routed: the batch's + those
         // row-id requests to the device, grouped by owner (d_send, d_order); counts per part
         auto route = [&] {
             keto_check_ids* d_reqs = c->a.get<keto_check_ids>(N);
-            HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)N * sizeof(keto_check_ids), hipMemcpyHostToDevice,
-                                  c->stream));
+            if (!pk) {
+                HIP_OK(hipMemcpyAsync(d_reqs, ids.data(), (uint64_t)n * sizeof(keto_check_ids), hipMemcpyHostToDevice,
+                                      c->stream));
+            } else {
+                if (n) HIP_OK(hipMemcpyAsync(d_reqs, d_pk, (uint64_t)n * sizeof(keto_check_ids), hipMemcpyDeviceToDevice,
+                                             c->stream));
+                if (!hidx.empty()) {                     // the host-resolved requests into their places
+                    const uint64_t m = hidx.size();
+                    uint8_t* tmp = c->e.get<uint8_t>(m * (sizeof(keto_check_ids) + 4));
+                    HIP_OK(hipMemcpyAsync(tmp, ids.data(), m * sizeof(keto_check_ids), hipMemcpyHostToDevice, c->stream));
+                    HIP_OK(hipMemcpyAsync(tmp + m * sizeof(keto_check_ids), hidx.data(), m * 4, hipMemcpyHostToDevice,
+                                          c->stream));
+                    scatter_ids(d_reqs, reinterpret_cast<const uint32_t*>(tmp + m * sizeof(keto_check_ids)),
+                                reinterpret_cast<const keto_check_ids*>(tmp), (uint32_t)m, c->stream);
+                }
+            }
+            if (!extra.empty())
+                HIP_OK(hipMemcpyAsync(d_reqs + n, extra.data(), extra.size() * sizeof(keto_check_ids),
+                                      hipMemcpyHostToDevice, c->stream));
             const int16_t* d_owner = owner_table(*c, *Sp);
             wb = route_work_bytes(N, c->n);
             uint8_t* work = c->c.get<uint8_t>(std::max<uint64_t>(wb, N));
@@ -605,7 +645,9 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
             cnt.assign(cs.begin(), cs.end());
         };
         mine.run([&] {
-            if (!h || (n && (!reqs || !allowed_out || !status_out))) throw Error{KETO_E_INVALID, "NULL argument"};
+            if (!h || (n && ((!reqs && !pk) || (pk && (!pk->reqs || (pk->blob_len && !pk->blob))) || !allowed_out ||
+                             !status_out)))
+                throw Error{KETO_E_INVALID, "NULL argument"};
             Sp = h->s.get();
             lk = std::shared_lock<RwGate>(Sp->rw);
             if ((int)Sp->n_parts != c->n || (int)Sp->part != c->rank)
@@ -613,8 +655,48 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
                                             "part = rank and n_parts = ranks)"};
             injected(*c, "resolve");
             // names -> row ids (routing needs rows, not this part's handles)
-            ids.resize(std::max<uint32_t>(n, 1));
-            wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
+            if (!pk) {
+                ids.resize(std::max<uint32_t>(n, 1));
+                wild = resolve_all(*Sp, reqs, n, ids.data(), status_out, true);
+            } else {
+                // on the device: whereQuery per request against this part's copy of the indexes (every
+                // part's host tables are the whole graph's), then the wildcard queries it leaves to
+                // the host, by name, exactly as the named form resolves them
+                d_pk = c->p.get<keto_check_ids>(std::max<uint32_t>(n, 1));
+                device_resolve_packed_rows(*Sp, reinterpret_cast<const uint8_t*>(pk->blob), pk->blob_len, pk->reqs, n,
+                                           d_pk, status_out, hidx, c->stream);
+                const uint32_t m = (uint32_t)hidx.size();
+                wr.resize(m);
+                for (uint32_t k = 0; k < m; ++k) {
+                    const keto_check_packed& p = pk->reqs[hidx[k]];
+                    const char* f = pk->blob + p.off;
+                    keto_str fs[6];
+                    for (int j = 0; j < 6; ++j) {
+                        fs[j] = keto_str{f, (uint32_t)(p.kind || j < 4 ? p.len[j] : 0u)};
+                        f += fs[j].n;
+                    }
+                    keto_check_req& q = wr[k];
+                    std::memset(&q, 0, sizeof q);
+                    q.namespace_ = fs[0];
+                    q.object = fs[1];
+                    q.relation = fs[2];
+                    q.subject.kind = p.kind;
+                    if (p.kind == 0) {
+                        q.subject.id = fs[3];
+                    } else {
+                        q.subject.set_namespace = fs[3];
+                        q.subject.set_object = fs[4];
+                        q.subject.set_relation = fs[5];
+                    }
+                    q.max_depth = p.max_depth;
+                    hpos[hidx[k]] = k;
+                }
+                ids.resize(std::max<uint32_t>(m, 1));
+                std::vector<uint8_t> hst(std::max<uint32_t>(m, 1));
+                for (const WildReq& w : resolve_all(*Sp, wr.data(), m, ids.data(), hst.data(), true))
+                    wild.push_back(WildReq{hidx[w.i], w.key});
+                for (uint32_t k = 0; k < m; ++k) status_out[hidx[k]] = hst[k];
+            }
             if (!wild.empty() && Sp->part_mode == PART_MIGRATE) {
                 // A wildcard query that no stored subject set uses has no row here, and its
                 // batch-local row would hold other parts' subject sets.  Its tuples are every
@@ -630,12 +712,12 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
                             throw Error{KETO_E_INVALID, "request " + std::to_string(w.i) +
                                                             " is a wildcard query over a row with a failing page: "
                                                             "not answered on a migrating partition"};
-                        keto_check_ids x = ids[w.i];
+                        keto_check_ids x = idref(w.i);
                         x.row = r;
-                        ids.push_back(x);
+                        extra.push_back(x);
                         parent.push_back(w.i);
                     }
-                    ids[w.i].row = KETO_NO_ROW;                  // decided by its rows' requests
+                    idref(w.i).row = KETO_NO_ROW;                // decided by its rows' requests
                 }
                 if ((uint64_t)n + parent.size() >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "too many wildcard rows"};
                 N = n + (uint32_t)parent.size();
@@ -746,7 +828,7 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         // it: below its top level a search only enters subject-set targets, which every part holds.
         if (!wild.empty()) {
             std::vector<keto_check_req> wq(wild.size());
-            for (size_t k = 0; k < wild.size(); ++k) wq[k] = reqs[wild[k].i];
+            for (size_t k = 0; k < wild.size(); ++k) wq[k] = pk ? wr[hpos.at(wild[k].i)] : reqs[wild[k].i];
             std::vector<uint8_t> wa(wild.size()), ws(wild.size());
             check_named(S, wq.data(), (uint32_t)wq.size(), global_max_depth, wa.data(), ws.data());
             for (size_t k = 0; k < wild.size(); ++k) {
@@ -756,6 +838,22 @@ int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req
         }
         return KETO_OK;
     });
+}
+
+}  // namespace
+
+extern "C" {
+
+int keto_check_batch_routed(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, uint32_t n,
+                            int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out) {
+    return routed_check(c, h, reqs, nullptr, n, global_max_depth, allowed_out, status_out);
+}
+
+int keto_check_batch_routed_packed(keto_comm* c, keto_snapshot* h, const char* blob, uint64_t blob_len,
+                                   const keto_check_packed* reqs, uint32_t n, int32_t global_max_depth,
+                                   uint8_t* allowed_out, uint8_t* status_out) {
+    const PackedIn pk{blob, blob_len, reqs};
+    return routed_check(c, h, nullptr, &pk, n, global_max_depth, allowed_out, status_out);
 }
 
 // BuildTree (internal/expand/engine.go:33-102) for every rank's own roots over an edge-partitioned

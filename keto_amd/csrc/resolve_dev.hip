@@ -764,6 +764,47 @@ void device_check_packed(Snapshot& S, const uint8_t* blob, uint64_t blob_len, co
             if (status[i] == ST_HOST) host.push_back(i);
 }
 
+// A packed batch resolved on the device into the row-id form the routed path sends between parts
+// (keto_check_batch_routed_packed, comm.cpp): the snapshot's device indexes as for
+// keto_check_batch_packed, the requests' row ids and subject targets into d_out (n entries), their
+// statuses into status_out (host).  Requests the device leaves to the host (wildcard queries) are
+// listed in host_idx, with d_out holding {no row, no target} for them.  A request whose fields lie
+// outside the blob fails the call (KETO_E_INVALID) before anything is written to status_out.
+void device_resolve_packed_rows(Snapshot& S, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs,
+                                uint32_t n, keto_check_ids* d_out, uint8_t* status_out, std::vector<uint32_t>& host_idx,
+                                void* stream) {
+    if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    host_idx.clear();
+    if (!n) return;
+    const DevView dv = device_view(S);
+    HIP_OK(hipSetDevice(dv.device));
+    RDevState& R = rdev_get(S, dv.device);
+    std::lock_guard<std::mutex> lk(R.mu);
+    rdev_refresh(S, R);
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* d_blob = R.blob.get<uint8_t>(std::max<uint64_t>(blob_len, 1));
+    keto_check_packed* d_q = R.reqs.get<keto_check_packed>(n);
+    uint8_t* d_st = R.status.get<uint8_t>(n);
+    uint32_t* d_cnt = R.cnt.get<uint32_t>(4);
+    if (blob_len) HIP_OK(hipMemcpyAsync(d_blob, blob, blob_len, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_q, reqs, (uint64_t)n * sizeof(keto_check_packed), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_cnt), NO_BAD, 1, st));
+    HIP_OK(hipMemsetAsync(d_cnt + 1, 0, 3 * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(resolve_packed<false>, dim3((n + 255) / 256), dim3(256), 0, st, R.view, d_blob, blob_len, 0ull,
+                       blob_len, d_q, 0u, n, d_out, d_st, d_cnt, nullptr);
+    HIP_OK(hipGetLastError());
+    uint32_t cnt[3] = {NO_BAD, 0u, 0u};
+    std::vector<uint8_t> stv(n);
+    HIP_OK(hipMemcpyAsync(cnt, d_cnt, sizeof cnt, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(stv.data(), d_st, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (cnt[0] != NO_BAD) throw Error{KETO_E_INVALID, "request " + std::to_string(cnt[0]) + "'s fields lie outside the blob"};
+    std::memcpy(status_out, stv.data(), n);
+    if (cnt[1])
+        for (uint32_t i = 0; i < n && host_idx.size() < cnt[1]; ++i)
+            if (stv[i] == ST_HOST) host_idx.push_back(i);
+}
+
 void rdev_release(Snapshot& S) { S.rdev.reset(); }
 
 }  // namespace keto

@@ -179,6 +179,18 @@ void route_rows(const keto_check_ids* d_reqs, uint32_t n, const int16_t* d_owner
     for (uint32_t b = 0; b < n_parts; ++b) counts_out[b] = starts[b + 1] - starts[b];
 }
 
+__global__ void __launch_bounds__(256) scatter_ids_kernel(keto_check_ids* __restrict__ d, const uint32_t* __restrict__ idx,
+                                                          const keto_check_ids* __restrict__ vals, uint32_t m) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) d[idx[k]] = vals[k];
+}
+
+void scatter_ids(keto_check_ids* d, const uint32_t* d_idx, const keto_check_ids* d_vals, uint32_t m, void* stream) {
+    if (!m) return;
+    hipLaunchKernelGGL(scatter_ids_kernel, dim3((m + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, d_idx, d_vals, m);
+    HIP_OK(hipGetLastError());
+}
+
 void unroute_rows(const uint8_t* d_back, const uint32_t* d_order, uint32_t n, uint8_t* d_out, void* stream) {
     if (n == 0) return;
     hipLaunchKernelGGL(unroute, dim3((n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), d_back, d_order,

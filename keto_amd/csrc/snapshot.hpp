@@ -591,6 +591,13 @@ void device_memory(int device, uint64_t& free_bytes, uint64_t& total_bytes);
 void device_check_packed(Snapshot& s, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs, uint32_t n,
                          int32_t gmd, uint8_t* allowed, uint8_t* status, std::vector<uint32_t>& host);
 void rdev_release(Snapshot& s);
+// a packed batch resolved on the device into row-id requests (the routed path, comm.cpp): d_out on
+// the device, statuses to the host; host_idx = the requests left to the host (wildcard queries)
+void device_resolve_packed_rows(Snapshot& s, const uint8_t* blob, uint64_t blob_len, const keto_check_packed* reqs,
+                                uint32_t n, keto_check_ids* d_out, uint8_t* status_out, std::vector<uint32_t>& host_idx,
+                                void* stream);
+// d[idx[k]] = vals[k] for k < m (device arrays)
+void scatter_ids(keto_check_ids* d, const uint32_t* d_idx, const keto_check_ids* d_vals, uint32_t m, void* stream);
 // An allocator whose resize() leaves new elements default-initialized (no zero fill): the expand
 // node arena is sized, then overwritten by one D2H copy.
 template <class T>

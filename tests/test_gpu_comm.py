@@ -185,6 +185,48 @@ def test_local_ranks_match_oracle(P, seed):
     full.close()
 
 
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("seed", range(4300, 4316))
+def test_local_routed_packed_equals_named(P, seed):
+    """keto_check_batch_routed_packed (each rank's batch packed and resolved on its device) against
+    keto_check_batch_routed (resolved on host threads) on quirk-heavy random graphs, shared-rows and
+    migrating parts: the same decisions and statuses for every request -- unknown namespaces and
+    strings, subject sets, wildcard queries (left to the host by the device) -- or the same agreed
+    error (a migrating part refuses a wildcard query over a row with a failing page), and both equal
+    the SQL oracle (internal/check/engine.go:36-123, relationtuples.go:178-198)."""
+    import keto_amd
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED, pack_requests
+    store, ns, tuples, raw, ps, alph = random_store(seed)
+    rows = rows_from_tuples(ns, tuples, raw)
+    reqs, checks = _reqs(seed, alph)
+    g = 5
+    mine = [list(range(r, len(reqs), P)) for r in range(P)]
+    if seed % 2:
+        mine[-1] = []                                   # the last rank passes no request
+    packed = [pack_requests([reqs[i] for i in m]) for m in mine]
+    comms = _local_comms(P)
+    for mode in (PART_SHARED, PART_MIGRATE):
+        parts = _parts(ns, rows, ps, P, mode)
+        if mode == PART_MIGRATE:
+            _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+        named = _ranks(P, lambda r: comms[r].check_batch_routed(parts[r], [reqs[i] for i in mine[r]], g))
+        pk = _ranks(P, lambda r: comms[r].check_batch_routed_packed(parts[r], packed[r][0], packed[r][1], g))
+        if not all(ok for ok, _ in named):
+            assert mode == PART_MIGRATE and any("failing page" in str(v) for ok, v in named if not ok), named
+            assert not any(ok for ok, _ in pk) and any("failing page" in str(v) for ok, v in pk if not ok), pk
+        else:
+            for r, ((_, (a, st)), (okp, vp)) in enumerate(zip(named, pk)):
+                assert okp, (seed, mode, r, vp)
+                assert (vp[0] == a).all() and (vp[1] == st).all(), (seed, mode, r)
+                for k, i in enumerate(mine[r]):
+                    t, d, _ = checks[i]
+                    assert bool(a[k]) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, mode, t, d)
+        for p in parts:
+            p.close()
+    for c in comms:
+        c.close()
+
+
 @pytest.fixture(scope="module")
 def powerlaw_strings():
     from tools import synth
@@ -233,6 +275,45 @@ def test_local_routed_powerlaw_matches_replicated(powerlaw_strings, P, mode):
     res = _ok(_ranks(P, lambda r: comms[r].check_batch_sharded(full, arr, 5, n=n)))
     for got, gst in res:
         assert (got == want).all() and (gst == want_st).all()
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("mode", ["shared", "migrate"])
+def test_local_routed_packed_powerlaw_matches_replicated(powerlaw_strings, P, mode):
+    """The power-law graph (1/256 scale) on P parts: every rank's 240,000 / P requests packed by the
+    generator's packer and resolved on its device (keto_check_batch_routed_packed), decisions equal
+    the replicated snapshot's; a request whose fields lie outside its blob on one rank fails every
+    rank alike, and the next call answers exactly."""
+    from keto_amd.capi import PART_MIGRATE, PART_SHARED
+    g, st, full, arr, n, want, want_st = powerlaw_strings
+    m = PART_MIGRATE if mode == "migrate" else PART_SHARED
+    parts = []
+    for r in range(P):
+        part, _ = g.snapshot_from_strings(st, device=-1)
+        parts.append(part.upload_part(r, P, 0, mode=m))
+    comms = _local_comms(P)
+    if m == PART_MIGRATE:
+        _ok(_ranks(P, lambda r: comms[r].close_filters(parts[r])))
+    bounds = [(r * n // P, (r + 1) * n // P) for r in range(P)]
+    packs = [g.pack_requests(_slice(arr, lo, hi), hi - lo) for lo, hi in bounds]
+    res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed_packed(parts[r], packs[r][0].array[:packs[r][2]],
+                                                                     packs[r][1].array, 5, n=bounds[r][1] - bounds[r][0])))
+    for r, (got, gst) in enumerate(res):
+        lo, hi = bounds[r]
+        assert (got == want[lo:hi]).all() and (gst == want_st[lo:hi]).all(), (mode, P, r)
+    bad = packs[1][1].array.copy()
+    bad["off"][5] = packs[1][2]                         # request 5's fields past rank 1's blob
+    _agreed_failure(_ranks(P, lambda r: comms[r].check_batch_routed_packed(
+        parts[r], packs[r][0].array[:packs[r][2]], bad if r == 1 else packs[r][1].array, 5,
+        n=bounds[r][1] - bounds[r][0])), 1, "outside the blob")
+    res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed_packed(parts[r], packs[r][0].array[:packs[r][2]],
+                                                                     packs[r][1].array, 5, n=bounds[r][1] - bounds[r][0])))
+    for r, (got, _) in enumerate(res):
+        assert (got == want[bounds[r][0]:bounds[r][1]]).all()
     for c in comms:
         c.close()
     for p in parts:

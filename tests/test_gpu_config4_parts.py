@@ -8,9 +8,11 @@ rank of the in-process transport (keto_comm_init_local) on device 0, as the Go s
 past one GPU's memory (integration/go/internal/gpu/partition.go).  For each form:
 
 * the bench's 16,777,216-request batch (docs:d#view@u at max-depth 5, tools/synth.py queries seed
-  1000) goes through keto_check_batch_routed, each rank passing its own slice (most requests belong to
-  other parts): every decision equals the replicated snapshot's, whose first 1,000,000 decisions equal
-  oracle/keto_oracle.c (internal/check/engine.go:36-123);
+  1000) goes through keto_check_batch_routed (named, resolved on host threads) and
+  keto_check_batch_routed_packed (packed, resolved on each rank's device: the Go Partition's call),
+  each rank passing its own slice (most requests belong to other parts): every decision equals the
+  replicated snapshot's, whose first 1,000,000 decisions equal oracle/keto_oracle.c
+  (internal/check/engine.go:36-123);
 * 5,000 expand roots (request rows owned by every part, and subject-set targets) go through
   keto_expand_batch_routed: every tree equals the replicated snapshot's node for node
   (internal/expand/engine.go:33-102);
@@ -188,6 +190,20 @@ def _check_form(b, P, mode, label):
         rec["routed_batch_ms"] = round(dt * 1e3, 1)
         rec["routed_checks_per_s"] = round(BATCH / dt, 1)
         assert (got == b.want).all()
+        # the same batch packed (the Go Partition's call): every rank's slice resolved on its device
+        bounds = [(r * BATCH // P, (r + 1) * BATCH // P) for r in range(P)]
+        packs = [g.pack_requests(_slice(b.arr, lo, hi), hi - lo) for lo, hi in bounds]
+        for rep in range(2):                             # the first call uploads each part's indexes
+            t0 = time.perf_counter()
+            res = _ranks(P, lambda r: comms[r].check_batch_routed_packed(
+                parts[r], packs[r][0].array[:packs[r][2]], packs[r][1].array, 5, n=bounds[r][1] - bounds[r][0]))
+            dt = time.perf_counter() - t0
+            got = np.concatenate([x for x, _ in res])
+            assert (got == b.want).all(), f"{label} packed: {int((got != b.want).sum())} mismatches"
+            assert all((s_ == 0).all() for _, s_ in res)
+        rec["routed_packed_batch_ms"] = round(dt * 1e3, 1)
+        rec["routed_packed_checks_per_s"] = round(BATCH / dt, 1)
+        del packs
         # expand: each rank its share of the roots
         shares = [list(range(r, N_ROOTS, P)) for r in range(P)]
         t0 = time.perf_counter()

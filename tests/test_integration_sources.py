@@ -139,7 +139,10 @@ def test_partitioned_serving():
     part = _code(open(os.path.join(GO, "internal", "gpu", "partition.go")).read())
     assert "C.keto_snapshot_upload_part_mode(" in part and "C.KETO_PART_SHARED" in part
     assert "NewLocalComm(" in part
-    assert ".CheckBatchRouted(p.parts[k], reqs[lo:hi]" in part          # every rank, its slice
+    assert "call(p.parts[k], reqs[lo:hi]" in part                       # every rank, its slice
+    assert "call = p.comms[k].CheckBatchRoutedPacked" in part and "packedFits(reqs)" in part   # resolved on the device
+    comm = _code(open(os.path.join(GO, "internal", "gpu", "comm.go")).read())
+    assert "C.keto_check_batch_routed_packed(" in comm
     assert ".ExpandBatchRouted(p.parts[k], subs[lo:hi]" in part
     assert "wg.Wait()" in part                                           # the ranks' calls run at once
     apply_at = part.index("func (p *Partition) Apply(")
