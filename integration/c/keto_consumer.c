@@ -24,7 +24,8 @@
  * not fit a device): the table is built once host-only, cloned host-only per part, and each clone is
  * uploaded as one shared-rows part (keto_snapshot_upload_part_mode, KETO_PART_SHARED) on its device;
  * one keto_comm_init_local rank per part, each driven by its own thread.  A check batch is split over
- * the ranks and every rank calls keto_check_batch_routed with its slice (an empty slice too); an
+ * the ranks and every rank calls keto_check_batch_routed with its slice (an empty slice too), then
+ * keto_check_batch_routed_packed with the slice packed (the Go Partition's call; both must agree); an
  * expand batch the same way through keto_expand_batch_routed; every write transaction is applied to
  * every part.  A restart in this mode builds a host-only snapshot from the table, saves it, loads the
  * file host-only and partitions it again (the Go server's persisted-file path).
@@ -294,12 +295,51 @@ typedef struct {
     uint8_t id[KETO_COMM_ID_BYTES];
 } partition_t;
 
+/* a check batch packed as the Go shim packs it (keto_check_batch_packed's layout): every request's
+   strings back to back in *blob, one record per request */
+static void pack_batch(const keto_check_req* q, size_t m, char** blob, size_t* total, keto_check_packed** pk) {
+    size_t t = 0;
+    for (size_t k = 0; k < m; ++k) {
+        const keto_check_req* r = &q[k];
+        t += r->namespace_.n + r->object.n + r->relation.n;
+        t += r->subject.kind == 0 ? r->subject.id.n
+                                  : r->subject.set_namespace.n + r->subject.set_object.n + r->subject.set_relation.n;
+    }
+    *blob = (char*)xrealloc(NULL, t ? t : 1);
+    *pk = (keto_check_packed*)calloc(m ? m : 1, sizeof(keto_check_packed));
+    if (!*pk) exit(3);
+    size_t at = 0;
+    for (size_t k = 0; k < m; ++k) {
+        const keto_check_req* r = &q[k];
+        keto_str f[6] = {r->namespace_, r->object, r->relation, r->subject.id, {NULL, 0}, {NULL, 0}};
+        int nf = 4;
+        if (r->subject.kind == 1) {
+            f[3] = r->subject.set_namespace;
+            f[4] = r->subject.set_object;
+            f[5] = r->subject.set_relation;
+            nf = 6;
+        }
+        (*pk)[k].off = (uint32_t)at;
+        (*pk)[k].kind = r->subject.kind;
+        (*pk)[k].max_depth = r->max_depth;
+        for (int j = 0; j < nf; ++j) {
+            (*pk)[k].len[j] = (uint16_t)f[j].n;
+            if (f[j].n) memcpy(*blob + at, f[j].p, f[j].n);
+            at += f[j].n;
+        }
+    }
+    *total = t;
+}
+
 /* one rank's share of a collective call, run on its own thread */
 typedef struct {
     partition_t* pt;
     int rank;
-    int op;                                   /* 0 init, 1 check, 2 expand */
+    int op;                                   /* 0 init, 1 check, 2 expand, 3 packed check */
     const keto_check_req* q;
+    const char* blob;                         /* op 3: the rank's slice packed */
+    size_t blob_len;
+    const keto_check_packed* pk;
     const keto_expand_req* e;
     uint32_t n;
     int32_t gmd;
@@ -348,6 +388,9 @@ static void* rank_main(void* arg) {
         c->rc = keto_comm_init_local(pt->id, pt->n, c->rank, pt->devices[c->rank], &pt->comms[c->rank]);
     else if (c->op == 1)
         c->rc = keto_check_batch_routed(pt->comms[c->rank], pt->parts[c->rank], c->q, c->n, c->gmd, c->allowed, c->status);
+    else if (c->op == 3)
+        c->rc = keto_check_batch_routed_packed(pt->comms[c->rank], pt->parts[c->rank], c->blob, c->blob_len, c->pk, c->n,
+                                               c->gmd, c->allowed, c->status);
     else
         c->rc = keto_expand_batch_routed(pt->comms[c->rank], pt->parts[c->rank], c->e, c->n, c->gmd, &c->ar);
     return NULL;
@@ -565,6 +608,33 @@ int main(int argc, char** argv) {
                 }
                 rc = ranks_run(&part, calls);
                 if (rc != KETO_OK) fail("keto_check_batch_routed", rc);
+                {
+                    /* the Go Partition's call: every rank's slice packed and resolved on its device
+                       (keto_check_batch_routed_packed); decisions and statuses must equal the named form's */
+                    uint8_t* pa = (uint8_t*)malloc(m ? m : 1);
+                    uint8_t* ps = (uint8_t*)malloc(m ? m : 1);
+                    char* blobs[MAX_REPLICAS];
+                    keto_check_packed* pks[MAX_REPLICAS];
+                    if (!pa || !ps) return 3;
+                    for (int k = 0; k < part.n; ++k) {
+                        pack_batch(calls[k].q, calls[k].n, &blobs[k], &calls[k].blob_len, &pks[k]);
+                        calls[k].op = 3;
+                        calls[k].blob = blobs[k];
+                        calls[k].pk = pks[k];
+                        calls[k].allowed = pa + (calls[k].q - q);
+                        calls[k].status = ps + (calls[k].q - q);
+                    }
+                    rc = ranks_run(&part, calls);
+                    if (rc != KETO_OK) fail("keto_check_batch_routed_packed", rc);
+                    for (size_t k = 0; k < m; ++k)
+                        if (pa[k] != allowed[k] || ps[k] != status[k]) return 15;
+                    for (int k = 0; k < part.n; ++k) {
+                        free(blobs[k]);
+                        free(pks[k]);
+                    }
+                    free(pa);
+                    free(ps);
+                }
                 for (size_t k = 0; k < m; ++k) printf("check\t%d\t%u\t%u\n", checks++, allowed[k], status[k]);
                 free(q);
                 free(allowed);
@@ -583,37 +653,12 @@ int main(int argc, char** argv) {
                 /* the Go shim's path: the same batch packed in one string blob, resolved on the GPU
                    (keto_check_batch_packed); decisions and statuses must equal keto_check_batch's */
                 size_t total = 0;
-                for (size_t k = 0; k < m; ++k) {
-                    const keto_check_req* r = &q[k];
-                    total += r->namespace_.n + r->object.n + r->relation.n;
-                    total += r->subject.kind == 0 ? r->subject.id.n
-                                                  : r->subject.set_namespace.n + r->subject.set_object.n + r->subject.set_relation.n;
-                }
-                char* blob = (char*)xrealloc(NULL, total);
-                keto_check_packed* pk = (keto_check_packed*)calloc(m, sizeof(keto_check_packed));
+                char* blob = NULL;
+                keto_check_packed* pk = NULL;
+                pack_batch(q, m, &blob, &total, &pk);
                 uint8_t* pa = (uint8_t*)malloc(m);
                 uint8_t* ps = (uint8_t*)malloc(m);
-                if (!pk || !pa || !ps) return 3;
-                size_t at = 0;
-                for (size_t k = 0; k < m; ++k) {
-                    const keto_check_req* r = &q[k];
-                    keto_str f[6] = {r->namespace_, r->object, r->relation, r->subject.id, {NULL, 0}, {NULL, 0}};
-                    int nf = 4;
-                    if (r->subject.kind == 1) {
-                        f[3] = r->subject.set_namespace;
-                        f[4] = r->subject.set_object;
-                        f[5] = r->subject.set_relation;
-                        nf = 6;
-                    }
-                    pk[k].off = (uint32_t)at;
-                    pk[k].kind = r->subject.kind;
-                    pk[k].max_depth = r->max_depth;
-                    for (int j = 0; j < nf; ++j) {
-                        pk[k].len[j] = (uint16_t)f[j].n;
-                        if (f[j].n) memcpy(blob + at, f[j].p, f[j].n);
-                        at += f[j].n;
-                    }
-                }
+                if (!pa || !ps) return 3;
                 rc = keto_check_batch_packed(snap, blob, total, pk, (uint32_t)m, gmd, pa, ps);
                 if (rc != KETO_OK) fail("keto_check_batch_packed", rc);
                 for (size_t k = 0; k < m; ++k)
