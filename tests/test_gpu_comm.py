@@ -186,7 +186,7 @@ def test_local_ranks_match_oracle(P, seed):
 
 
 @pytest.mark.parametrize("P", [2, 3])
-@pytest.mark.parametrize("seed", range(4300, 4316))
+@pytest.mark.parametrize("seed", range(4300, 4308))
 def test_local_routed_packed_equals_named(P, seed):
     """keto_check_batch_routed_packed (each rank's batch packed and resolved on its device) against
     keto_check_batch_routed (resolved on host threads) on quirk-heavy random graphs, shared-rows and
