@@ -987,6 +987,12 @@ __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_
     return (c & ~m) | ((v << off) & m);
 }
 
+// request prefetch slots per lane of the tier-0 kernels (2: the next pair; 1: the next request only,
+// 4 KB less LDS per block -- room for a 7th wave per SIMD at 20 KB)
+#ifndef KETO_NQ_SLOTS
+#define KETO_NQ_SLOTS 2
+#endif
+
 // requests j and j + 1 (if in the run) straight into the wave's LDS prefetch slots (global_load_lds:
 // no VGPR destination; lane L's 16 B land at wave_base + 16 L, i.e. lds_nq[tid] and
 // lds_nq[LDS_STRIDE + tid]); retired by the iteration's vmcnt(0)
@@ -1089,7 +1095,8 @@ __device__ __forceinline__ void
     __shared__ uint32_t lds_vis[(LV > 0 ? LV : 1) * LDS_STRIDE];
     __shared__ uint2 sf_pk[F * LDS_STRIDE];
     __shared__ uint4 sf_win[(WIN ? F : 1) * LDS_STRIDE];
-    __shared__ uint4 lds_nq[2 * LDS_STRIDE];                   // the lane's prefetched request pair
+    // the lane's prefetched requests (STREAM: one slot holds a pair of 8-B requests)
+    __shared__ uint4 lds_nq[(STREAM ? 1 : KETO_NQ_SLOTS) * LDS_STRIDE];
     uint32_t* const vcol = lds_vis + tid;
     LaneVisited<RV, LV> V;
     V.fresh();
@@ -1181,9 +1188,11 @@ __device__ __forceinline__ void
                 c = P_XLT | ((uint32_t)d << C_K) | ((nq.y & EDGE_SET) ? C_TSET : 0u) | keep;
                 return;
             }
-            if (c & C_NQ2) {
-                lds_nq[tid] = lds_nq[LDS_STRIDE + tid];
-                keep = C_NQ;
+            if constexpr (KETO_NQ_SLOTS == 2) {
+                if (c & C_NQ2) {
+                    lds_nq[tid] = lds_nq[LDS_STRIDE + tid];
+                    keep = C_NQ;
+                }
             }
             int d = (int)nq.w;
             if (d <= 0 || gmd < d) d = gmd;                       // engine.go:118-120
@@ -1269,11 +1278,15 @@ __device__ __forceinline__ void
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ta.pairs + j),
                                                  reinterpret_cast<void*>(lds_nq + (__builtin_amdgcn_readfirstlane(tid) & ~63u)),
                                                  16, 0, KETO_STREAM_CPOL);
+            } else if constexpr (KETO_NQ_SLOTS == 1) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q + j),
+                                                 reinterpret_cast<void*>(lds_nq + (__builtin_amdgcn_readfirstlane(tid) & ~63u)),
+                                                 16, 0, 0);
             } else {
                 // (the wave's LDS base from a scalar: a vector copy of it was spilled to scratch)
                 prefetch_pair(q, j, j_end, lds_nq + (__builtin_amdgcn_readfirstlane(tid) & ~63u));
             }
-            c |= C_NQ | (j + 1u < j_end ? C_NQ2 : 0u);
+            c |= C_NQ | ((STREAM || KETO_NQ_SLOTS == 2) && j + 1u < j_end ? C_NQ2 : 0u);
             w.request();
         }
         uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
