@@ -988,7 +988,8 @@ __device__ inline uint32_t bf_set(uint32_t c, uint32_t off, uint32_t wd, uint32_
 }
 
 // request prefetch slots per lane of the tier-0 kernels (2: the next pair; 1: the next request only,
-// 4 KB less LDS per block -- room for a 7th wave per SIMD at 20 KB)
+// 4 KB less LDS per block -- room for a 7th wave per SIMD at 20 KB -- measured slower at 6 and at 7
+// waves, 2.81 / 2.61-2.65 ms against 2.49-2.54, profiles/r06l_tier0_one_prefetch_slot_rejected.log)
 #ifndef KETO_NQ_SLOTS
 #define KETO_NQ_SLOTS 2
 #endif
