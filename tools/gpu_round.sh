@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 step() { echo "== $(date +%T) $1"; }
 if [ -z "$PROFILE_ONLY" ]; then
 step pytest
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -30 $out/pytest_gpu.log; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread --durations=30 > $out/pytest_gpu.log 2>&1 || { tail -30 $out/pytest_gpu.log; exit 1; }
 tail -3 $out/pytest_gpu.log
 step smoke
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail -30 $out/smoke.log; exit 1; }
