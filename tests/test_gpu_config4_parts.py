@@ -167,11 +167,9 @@ def _check_form(b, P, mode, label):
     g, u = b.g, b.u
     rec = {"form": label, "parts": P}
     t0 = time.perf_counter()
-    parts = []
-    for r in range(P):
-        s = Snapshot.from_csr(g.namespaces, g.row_ns, u.row_obj, u.row_rel, g.row_ptr, u.edges,
-                              kstrs=(u.strs, u.n_strings), device=-1)
-        parts.append(s.upload_part(r, P, 0, mode=mode))
+    # the parts side by side (each a host-only snapshot of the whole graph, then its part uploaded)
+    parts = _ranks(P, lambda r: Snapshot.from_csr(g.namespaces, g.row_ns, u.row_obj, u.row_rel, g.row_ptr, u.edges,
+                                                  kstrs=(u.strs, u.n_strings), device=-1).upload_part(r, P, 0, mode=mode))
     rec["build_upload_s"] = round(time.perf_counter() - t0, 1)
     rec["part_gib"] = [round(p.stats()["device_bytes"] / 2**30, 2) for p in parts]
     cid = os.urandom(32)
