@@ -397,7 +397,7 @@ void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_
     const int P = c.n;
     mine.run([&] {
         injected(c, "mig_begin");
-        mig_begin(S, d_reqs, n, gmd, d_dec, c.stream, out);
+        mig_begin(S, d_reqs, n, gmd, d_dec, c.stream, out, true);
     });
     for (uint32_t rounds = 0;; ++rounds) {
         // one all-gather per round: every rank's status and the records it emitted
@@ -612,6 +612,7 @@ int routed_check(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, con
         // (parent = the query's index), their decisions OR-ed into the query's below
         std::vector<uint32_t> parent;
         std::vector<keto_check_ids> extra;               // those requests
+        std::vector<uint32_t> decided;                   // queries a top-level tuple allows outright
         uint32_t N = n;                                  // requests routed: the batch's + those
         // row-id requests to the device, grouped by owner (d_send, d_order); counts per part
         auto route = [&] {
@@ -703,20 +704,67 @@ int routed_check(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, con
                 // matching row's, and each top-level tuple is searched with a fresh visited map
                 // (the shadowed ctx, internal/check/engine.go:47-48), so the query is allowed iff
                 // one of the matching rows is, checked as a request of its own at the same depth:
-                // those requests travel like any other.  A poisoned page would cut the query's
-                // ORDER BY sequence elsewhere than the rows' own (relationtuples.go:200-223): such
-                // queries are refused.
+                // those requests travel like any other.
+                //
+                // The query's ORDER BY sequence is its rows' tuples one after another, read a page at a
+                // time until a page fails toInternal (relationtuples.go:64-71, 250-277): the search sees
+                // the first L tuples, L = the failing page's start (engine.go:98-100 then answers
+                // false).  Rows wholly before L go as above (none holds a failing tuple, so each is
+                // whole in its owner's arena).  The row L cuts is taken a tuple at a time, each with the
+                // fresh map of a top-level tuple: a subject id or the requested set itself decides here;
+                // any other set is a request that enters its row as the walk would after the hop
+                // (remaining depth d - 1, the map holding the set's visit key; migrate.hip mig_start).
+                const int32_t g = std::min<int32_t>(global_max_depth, 65535);
                 for (const WildReq& w : wild) {
-                    for (uint32_t r : Sp->rows_in_key_order(w.key)) {
-                        if (Sp->row_pp[r] != NO_PAGE)
-                            throw Error{KETO_E_INVALID, "request " + std::to_string(w.i) +
-                                                            " is a wildcard query over a row with a failing page: "
-                                                            "not answered on a migrating partition"};
-                        keto_check_ids x = idref(w.i);
-                        x.row = r;
-                        extra.push_back(x);
-                        parent.push_back(w.i);
+                    const keto_check_ids q = idref(w.i);
+                    const std::vector<uint32_t> rows = Sp->rows_in_key_order(w.key);
+                    uint64_t L = UINT64_MAX, at = 0;
+                    for (uint32_t r : rows) {
+                        const auto e = Sp->row_edges(r);
+                        if (Sp->row_pp[r] != NO_PAGE) {
+                            uint64_t i = 0;
+                            while (i < e.second && e.first[i] != EDGE_POISON) ++i;
+                            L = (at + i) / Sp->page_size * Sp->page_size;
+                            break;
+                        }
+                        at += e.second;
                     }
+                    int32_t d = q.max_depth;
+                    if (d <= 0 || g < d) d = g;
+                    if (d <= 0) L = 0;                           // engine.go:88-91: nothing is read
+                    bool yes = false;
+                    at = 0;
+                    for (uint32_t r : rows) {
+                        if (at >= L || yes) break;
+                        const auto e = Sp->row_edges(r);
+                        if (at + e.second <= L) {
+                            keto_check_ids x = q;
+                            x.row = r;
+                            extra.push_back(x);
+                            parent.push_back(w.i);
+                        } else {
+                            for (uint64_t i = 0; i < L - at && !yes; ++i) {
+                                const uint32_t v = e.first[i];
+                                const bool set = (v & EDGE_SET) != 0;
+                                if (set != ((q.flags & 1u) != 0) || (v & EDGE_VAL) != q.target) {
+                                    if (!set || d < 2 || q.target == KETO_NO_TARGET) continue;
+                                    uint32_t cls = 0;                // the set's visit key: its class if it collides
+                                    if (auto it = Sp->coll.find(v); it != Sp->coll.end()) cls = (it->second & ~VID_CLASS) + 1u;
+                                    if (cls >= (1u << 24)) throw Error{KETO_E_RANGE, "collision class past 2^24"};
+                                    keto_check_ids x = q;
+                                    x.row = v & EDGE_VAL;
+                                    x.flags = (q.flags & 1u) | KETO_CHILD_FLAG | (cls << 8);
+                                    x.max_depth = d - 1;
+                                    extra.push_back(x);
+                                    parent.push_back(w.i);
+                                } else {
+                                    yes = true;                      // engine.go:54-57 on a top-level tuple
+                                }
+                            }
+                        }
+                        at += e.second;
+                    }
+                    if (yes) decided.push_back(w.i);
                     idref(w.i).row = KETO_NO_ROW;                // decided by its rows' requests
                 }
                 if ((uint64_t)n + parent.size() >= 0xFFFFFFFFull) throw Error{KETO_E_RANGE, "too many wildcard rows"};
@@ -811,6 +859,7 @@ int routed_check(keto_comm* c, keto_snapshot* h, const keto_check_req* reqs, con
         if (n) HIP_OK(hipMemcpyAsync(allowed_out, d_out, n, hipMemcpyDeviceToHost, c->stream));
         if (N > n) HIP_OK(hipMemcpyAsync(sub.data(), d_out + n, N - n, hipMemcpyDeviceToHost, c->stream));
         sync(*c);
+        for (uint32_t i : decided) allowed_out[i] = 1;
         for (size_t k = 0; k < parent.size(); ++k) {     // allowed if a row is; undecided if one is, none allowed
             uint8_t& a = allowed_out[parent[k]];
             if (sub[k] == 1) a = 1;

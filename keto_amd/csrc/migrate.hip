@@ -51,6 +51,7 @@ namespace {
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint64_t MAX_ROUND_RECORDS = 1ull << 28;   // record counts are 28-bit fields of the grouping cursors
 constexpr uint32_t HEAD_WORDS = 8;
+constexpr uint32_t START_UNITS = 3;                 // a START record: the head and one visit id
 constexpr uint32_t K_ENTER = 0, K_RESUME = 1, K_DECISION = 2;
 constexpr uint32_t F_SEQ = 1, F_TOP = 2;            // frame flags
 constexpr uint32_t MIG_FRAMES = 64;                 // saved frames of one search (max-depth <= 65)
@@ -522,11 +523,14 @@ __global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
 
 // START records of a routed batch (row-id requests of this part): the depth clamp
 // (engine.go:118-120), the row's handle, a set target's global identity.  Trivial requests become
-// DECISION records for this part.
+// DECISION records for this part.  Each record takes START_UNITS units: the head, and room for one
+// visit id -- a request for one top-level tuple of a wildcard query (KETO_CHILD_FLAG, when
+// `child_entries`) enters its row below the top, the map holding the tuple's visit key, as
+// run_record does after the hop from a top-level frame.
 __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restrict__ q, uint32_t n, int32_t gmd,
                                                  const uint32_t* __restrict__ g_handle,
                                                  const uint8_t* __restrict__ owner, uint32_t n_rows, uint32_t self,
-                                                 uint32_t hot_units,
+                                                 uint32_t hot_units, uint32_t child_entries,
                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ off,
                                                  uint32_t* misrouted) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -534,7 +538,8 @@ __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restric
     const keto_check_ids r = q[i];
     int d = r.max_depth;
     if (d <= 0 || gmd < d) d = gmd;
-    uint32_t info = K_ENTER | (F_TOP << 5) | (self << 8);
+    const bool child = child_entries && (r.flags & KETO_CHILD_FLAG);
+    uint32_t info = K_ENTER | ((child ? 0u : F_TOP) << 5) | (self << 8);
     uint32_t t_lo = r.target, t_hi = 0, enter = NONE;
     bool trivial = r.row == KETO_NO_ROW || d <= 0 || r.target == KETO_NO_TARGET;
     if (!trivial) {
@@ -555,10 +560,18 @@ __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restric
         }
     }
     if (trivial) info = K_DECISION | (self << 8);              // denied (decision 0)
-    uint32_t* o = out + (uint64_t)i * 8;
+    uint32_t nv = 0;
+    uint64_t vid = 0;
+    if (!trivial && child) {
+        const uint32_t cls = r.flags >> 8;
+        vid = cls ? vid_class(cls - 1u) : vid_row(enter < hot_units ? VID_HOT_PART : self, enter);
+        nv = 1;
+    }
+    uint32_t* o = out + (uint64_t)i * 4 * START_UNITS;
     *reinterpret_cast<uint4*>(o) = make_uint4(i, info, t_lo, t_hi);
-    *reinterpret_cast<uint4*>(o + 4) = make_uint4(enter, (uint32_t)d, 0u, 0u);
-    off[i] = 2 * i;
+    *reinterpret_cast<uint4*>(o + 4) = make_uint4(enter, (uint32_t)d, 0u, nv);
+    *reinterpret_cast<uint4*>(o + 8) = make_uint4((uint32_t)vid, (uint32_t)(vid >> 32), 0u, 0u);
+    off[i] = START_UNITS * i;
 }
 
 // group the round's output records by destination part: counts, then a scatter in which every
@@ -953,7 +966,7 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
 }  // namespace
 
 void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
-               MigOut& out) {
+               MigOut& out, bool child_entries) {
     std::lock_guard<std::mutex> lk(S.mu);
     MigState& M = mig_state(S);
     HIP_OK(hipSetDevice(M.device));
@@ -973,13 +986,13 @@ void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gm
         dfree(M.start);
         dfree(M.start_off);
         M.start_cap = std::max<uint64_t>(n, 4096);
-        M.start = dalloc<uint32_t>(M.start_cap * 8);
+        M.start = dalloc<uint32_t>(M.start_cap * 4 * START_UNITS);
         M.start_off = dalloc<uint32_t>(M.start_cap);
     }
     HIP_OK(hipMemsetAsync(M.ctr, 0, 4, st));
     if (n) {
         hipLaunchKernelGGL(mig_start, dim3((n + 255) / 256), dim3(256), 0, st, d_reqs, n, gmd, M.g_handle, M.owner,
-                           M.n_rows, S.part, S.hot_units, M.start, M.start_off, M.ctr);
+                           M.n_rows, S.part, S.hot_units, child_entries ? 1u : 0u, M.start, M.start_off, M.ctr);
         HIP_OK(hipGetLastError());
     }
     uint32_t bad = 0;
@@ -987,7 +1000,7 @@ void mig_begin(Snapshot& S, const keto_check_ids* d_reqs, uint32_t n, int32_t gm
     HIP_OK(hipStreamSynchronize(st));
     if (bad) throw Error{KETO_E_INVALID, std::to_string(bad) + " requests name rows another part owns"};
     const uint32_t recs = n;
-    const uint64_t units = 2ull * n;
+    const uint64_t units = (uint64_t)START_UNITS * n;
     run_round(S, M, M.start, M.start_off, n, &recs, &units, 1, st, out);
 }
 

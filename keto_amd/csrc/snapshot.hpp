@@ -49,6 +49,11 @@ constexpr uint32_t VID_CLASS = 0x80000000u;     // visit ids of colliding keys l
 // keto_check_ids.flags bit of the engine's own top-level items (reach.hip; not part of the C-ABI,
 // honoured only for the work arrays reach.hip builds)
 constexpr uint32_t KETO_ITEM_FLAG = 2u;
+// keto_check_ids.flags bit of a migrating batch's requests for one top-level tuple of a wildcard
+// query (comm.cpp routed_check): enter `row` as the walk does after the hop from that tuple, the map
+// holding the tuple's visit key (bits 8..31: its collision class + 1, or 0 for the row's own key).
+// Honoured only where comm.cpp builds them (mig_begin(..., child_entries = true)).
+constexpr uint32_t KETO_CHILD_FLAG = 4u;
 
 // Device arena (one u32 array per device).  Row r occupies
 //   [subject-id table, 2^hlog2 words of 16-B buckets, for rows whose ids do not all fit in the
@@ -575,7 +580,7 @@ struct MigOut {
     uint32_t decided, undecided, processed, reruns;
 };
 void mig_begin(Snapshot& s, const keto_check_ids* d_reqs, uint32_t n, int32_t gmd, uint8_t* d_allowed, void* stream,
-               MigOut& out);
+               MigOut& out, bool child_entries = false);
 void mig_round(Snapshot& s, const void* d_in, const uint32_t* d_in_off, const uint32_t* in_records,
                const uint64_t* in_units, void* stream, MigOut& out);
 void mig_release(Snapshot& s);

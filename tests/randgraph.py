@@ -87,3 +87,35 @@ def random_expands(seed, alph, k=6):
                              rng.choice(rels))
         out.append((sub, rng.choice([0, 1, 2, 3, 4, 6]), rng.choice([1, 2, 3, 5])))
     return out
+
+
+def poisoned_wildcard_case(seed):
+    """A random graph with 1-3 failing tuples (subject sets of a namespace id the config lacks),
+    page sizes 1-5, and wildcard queries over every (namespace, relation) and (namespace, object)
+    pair of its alphabet at depths 1-7, subject ids and sets, plus random checks.  Returns
+    (store, namespaces, tuples, raw, page size, request tuples, [(RelationTuple, depth)])."""
+    rng = random.Random(seed * 31 + 7)
+    ns, tuples, raw, _, alph = random_graph(seed, n_tuples=rng.randint(20, 60), allow_poison=False)
+    names, objs, rels, users = alph
+    nsid = dict((n_, i) for i, n_ in ns)
+    for _ in range(rng.randint(1, 3)):
+        raw.append((nsid[rng.choice(names)], rng.choice(objs), rng.choice(rels), None, 99, rng.choice(objs),
+                    rng.choice(rels)))
+    ps = rng.choice([1, 2, 3, 5])
+    store = SQLStore(ns, tuples, page_size=ps, raw_rows=raw)
+    checks = []
+    for n_ in names:
+        for o, r in [("", r) for r in rels] + [(o, "") for o in objs]:
+            for _ in range(2):
+                if rng.random() < 0.6:
+                    sub = SubjectID(rng.choice(users))
+                else:
+                    sub = SubjectSet(rng.choice(names), rng.choice(objs), rng.choice(rels))
+                checks.append((RelationTuple(n_, o, r, sub), rng.choice([1, 2, 3, 5, 7])))
+    checks += [(t, d) for t, d, _ in random_checks(seed, alph, k=24)]
+    reqs = [(t.namespace, t.object, t.relation, _subj(t.subject), d) for t, d in checks]
+    return store, ns, tuples, raw, ps, reqs, checks
+
+
+def _subj(s):
+    return ("id", s.id) if isinstance(s, SubjectID) else ("set", s.namespace, s.object, s.relation)
