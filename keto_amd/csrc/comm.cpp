@@ -93,6 +93,13 @@ struct Transport {
     // bytes: send[sdisp(p), +scount[p]) to rank p; recv[rdisp(p), +rcount[p]) from rank p (device)
     virtual void alltoallv(const void* send, const std::vector<uint64_t>& scount, void* recv,
                            const std::vector<uint64_t>& rcount, hipStream_t st) = 0;
+    // two all-to-alls of one step (a migrating round's records and their offsets)
+    virtual void alltoallv2(const void* s1, const std::vector<uint64_t>& sc1, void* r1, const std::vector<uint64_t>& rc1,
+                            const void* s2, const std::vector<uint64_t>& sc2, void* r2, const std::vector<uint64_t>& rc2,
+                            hipStream_t st) {
+        alltoallv(s1, sc1, r1, rc1, st);
+        alltoallv(s2, sc2, r2, rc2, st);
+    }
     // every rank's `bytes` at send -> recv + p * bytes (device)
     virtual void allgather(const void* send, void* recv, uint64_t bytes, hipStream_t st) = 0;
     // host words: in[p * k + j] goes to rank p, arriving as out[src * k + j]
@@ -165,9 +172,9 @@ struct LocalHub {
     bool broken = false;
     std::string why;
     struct Post {
-        const void* dsend = nullptr;
+        const void* dsend[2] = {nullptr, nullptr};
         int device = 0;
-        std::vector<uint64_t> sdisp, scount, host;
+        std::vector<uint64_t> sdisp[2], scount[2], host;
     };
     std::vector<Post> post;
 };
@@ -219,54 +226,87 @@ struct LocalTransport final : Transport {
         }
         if (hub->gen == g) throw Error{KETO_E_HIP, "local communicator broken: " + hub->why};
     }
-    void put(const void* dsend, const std::vector<uint64_t>& scount, std::vector<uint64_t> host) {
+    void put(const void* d0, const std::vector<uint64_t>& c0, const void* d1, const std::vector<uint64_t>* c1,
+             std::vector<uint64_t> host) {
         std::lock_guard<std::mutex> lk(hub->mu);
         LocalHub::Post& p = hub->post[rank];
-        p.dsend = dsend;
         p.device = device;
-        p.scount = scount;
-        p.sdisp.assign(scount.size(), 0);
-        for (size_t q = 1; q < scount.size(); ++q) p.sdisp[q] = p.sdisp[q - 1] + scount[q - 1];
+        for (int a = 0; a < 2; ++a) {
+            const std::vector<uint64_t>& c = a == 0 ? c0 : c1 ? *c1 : c0;
+            p.dsend[a] = a == 0 ? d0 : d1;
+            p.scount[a] = a == 0 || c1 ? c : std::vector<uint64_t>(c.size(), 0);
+            p.sdisp[a].assign(c.size(), 0);
+            for (size_t q = 1; q < c.size(); ++q) p.sdisp[a][q] = p.sdisp[a][q - 1] + p.scount[a][q - 1];
+        }
         p.host = std::move(host);
     }
-    void alltoallv(const void* send, const std::vector<uint64_t>& scount, void* recv, const std::vector<uint64_t>& rcount,
-                   hipStream_t st) override {
+    // One exchange step of one or two arrays.  The peers' segments for this rank are copied by one
+    // launch (copy_segments) when they lie on this device, instead of one runtime copy per peer and
+    // array: a migrating round on 8 parts had spent most of its copy time in ~2.7K blit launches per
+    // batch (profiles/r06p_migrate_local.log).
+    void exchange(const void* s1, const std::vector<uint64_t>& sc1, void* r1, const std::vector<uint64_t>& rc1,
+                  const void* s2, const std::vector<uint64_t>* sc2, void* r2, const std::vector<uint64_t>* rc2,
+                  hipStream_t st) {
         HIP_OK(hipStreamSynchronize(st));            // this rank's send data is complete
-        put(send, scount, {});
+        put(s1, sc1, s2, sc2, {});
         barrier();
-        uint64_t ro = 0;
-        for (int p = 0; p < n; ++p) {
-            const LocalHub::Post& src = hub->post[p];
-            if (src.scount[rank] != rcount[p])
-                fail("rank " + std::to_string(rank) + " expected " + std::to_string(rcount[p]) + " bytes from rank " +
-                     std::to_string(p) + ", which sends " + std::to_string(src.scount[rank]));
-            if (rcount[p]) {
-                const void* from = static_cast<const uint8_t*>(src.dsend) + src.sdisp[rank];
-                void* to = static_cast<uint8_t*>(recv) + ro;
-                if (src.device == device) HIP_OK(hipMemcpyAsync(to, from, rcount[p], hipMemcpyDeviceToDevice, st));
-                else HIP_OK(hipMemcpyPeerAsync(to, device, from, src.device, rcount[p], st));
+        CopySegments cs{};
+        for (int a = 0; a < (sc2 ? 2 : 1); ++a) {
+            const std::vector<uint64_t>& rcount = a == 0 ? rc1 : *rc2;
+            void* recv = a == 0 ? r1 : r2;
+            uint64_t ro = 0;
+            for (int p = 0; p < n; ++p) {
+                const LocalHub::Post& src = hub->post[p];
+                if (src.scount[a][rank] != rcount[p])
+                    fail("rank " + std::to_string(rank) + " expected " + std::to_string(rcount[p]) + " bytes from rank " +
+                         std::to_string(p) + ", which sends " + std::to_string(src.scount[a][rank]));
+                if (rcount[p]) {
+                    const void* from = static_cast<const uint8_t*>(src.dsend[a]) + src.sdisp[a][rank];
+                    void* to = static_cast<uint8_t*>(recv) + ro;
+                    if (src.device != device) {
+                        HIP_OK(hipMemcpyPeerAsync(to, device, from, src.device, rcount[p], st));
+                    } else {
+                        if (cs.n == COPY_SEGMENTS) {
+                            copy_segments(cs, st);
+                            cs.n = 0;
+                        }
+                        cs.src[cs.n] = from;
+                        cs.dst[cs.n] = to;
+                        cs.bytes[cs.n++] = rcount[p];
+                    }
+                }
+                ro += rcount[p];
             }
-            ro += rcount[p];
         }
+        if (cs.n) copy_segments(cs, st);
         HIP_OK(hipStreamSynchronize(st));
         barrier();                                  // every copy out of the send buffers is done
     }
+    void alltoallv(const void* send, const std::vector<uint64_t>& scount, void* recv, const std::vector<uint64_t>& rcount,
+                   hipStream_t st) override {
+        exchange(send, scount, recv, rcount, nullptr, nullptr, nullptr, nullptr, st);
+    }
+    void alltoallv2(const void* s1, const std::vector<uint64_t>& sc1, void* r1, const std::vector<uint64_t>& rc1,
+                    const void* s2, const std::vector<uint64_t>& sc2, void* r2, const std::vector<uint64_t>& rc2,
+                    hipStream_t st) override {
+        exchange(s1, sc1, r1, rc1, s2, &sc2, r2, &rc2, st);
+    }
     void allgather(const void* send, void* recv, uint64_t bytes, hipStream_t st) override {
         HIP_OK(hipStreamSynchronize(st));
-        put(send, std::vector<uint64_t>(n, 0), {});
+        put(send, std::vector<uint64_t>(n, 0), nullptr, nullptr, {});
         barrier();
         for (int p = 0; p < n; ++p) {
             const LocalHub::Post& src = hub->post[p];
             void* to = static_cast<uint8_t*>(recv) + (uint64_t)p * bytes;
             if (!bytes) continue;
-            if (src.device == device) HIP_OK(hipMemcpyAsync(to, src.dsend, bytes, hipMemcpyDeviceToDevice, st));
-            else HIP_OK(hipMemcpyPeerAsync(to, device, src.dsend, src.device, bytes, st));
+            if (src.device == device) HIP_OK(hipMemcpyAsync(to, src.dsend[0], bytes, hipMemcpyDeviceToDevice, st));
+            else HIP_OK(hipMemcpyPeerAsync(to, device, src.dsend[0], src.device, bytes, st));
         }
         HIP_OK(hipStreamSynchronize(st));
         barrier();
     }
     std::vector<uint64_t> alltoall_u64(const std::vector<uint64_t>& in, int k, hipStream_t) override {
-        put(nullptr, std::vector<uint64_t>(n, 0), in);
+        put(nullptr, std::vector<uint64_t>(n, 0), nullptr, nullptr, in);
         barrier();
         std::vector<uint64_t> out((uint64_t)n * k);
         for (int p = 0; p < n; ++p) {
@@ -278,7 +318,7 @@ struct LocalTransport final : Transport {
         return out;
     }
     std::vector<uint64_t> allgather_u64(const std::vector<uint64_t>& in, hipStream_t) override {
-        put(nullptr, std::vector<uint64_t>(n, 0), in);
+        put(nullptr, std::vector<uint64_t>(n, 0), nullptr, nullptr, in);
         barrier();
         std::vector<uint64_t> out;
         out.reserve(in.size() * n);
@@ -400,26 +440,29 @@ void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_
         mig_begin(S, d_reqs, n, gmd, d_dec, c.stream, out, true);
     });
     for (uint32_t rounds = 0;; ++rounds) {
-        // one all-gather per round: every rank's status and the records it emitted
+        // one all-to-all of words per round: to every rank, this rank's status, the records it emitted
+        // in all, and the units and records it sends that rank
         uint64_t emitted = 0;
         if (mine.code == KETO_OK)
             for (int q = 0; q < P; ++q) emitted += out.records[q];
-        const std::vector<uint64_t> all = c.t->allgather_u64({(uint64_t)(int64_t)mine.code, emitted}, c.stream);
+        std::vector<uint64_t> cnt((uint64_t)P * 4);
+        for (int q = 0; q < P; ++q) {
+            const bool ok = mine.code == KETO_OK;
+            cnt[4 * q] = (uint64_t)(int64_t)mine.code;
+            cnt[4 * q + 1] = emitted;
+            cnt[4 * q + 2] = ok ? out.units[q] : 0;
+            cnt[4 * q + 3] = ok ? out.records[q] : 0;
+        }
+        const std::vector<uint64_t> in = c.t->alltoall_u64(cnt, 4, c.stream);
         std::vector<int64_t> codes(P);
         uint64_t total = 0;
         for (int p = 0; p < P; ++p) {
-            codes[p] = (int64_t)all[2 * p];
-            total += all[2 * p + 1];
+            codes[p] = (int64_t)in[4 * p];
+            total += in[4 * p + 1];
         }
         settle(c, mine, codes);
         if (total == 0) return;
         if (rounds >= (1u << 20)) throw Error{KETO_E_RANGE, "migrating check did not finish in 2^20 rounds"};
-        std::vector<uint64_t> cnt((uint64_t)P * 2);
-        for (int q = 0; q < P; ++q) {
-            cnt[2 * q] = out.units[q];
-            cnt[2 * q + 1] = out.records[q];
-        }
-        const std::vector<uint64_t> in = c.t->alltoall_u64(cnt, 2, c.stream);
         std::vector<uint64_t> su(P), sr(P), ru(P), rr(P);
         std::vector<uint32_t> in_recs(MIG_MAX_PARTS, 0);
         std::vector<uint64_t> in_units(MIG_MAX_PARTS, 0);
@@ -427,12 +470,12 @@ void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_
         for (int q = 0; q < P; ++q) {
             su[q] = out.units[q] * 16;
             sr[q] = (uint64_t)out.records[q] * 4;
-            ru[q] = in[2 * q] * 16;
-            rr[q] = in[2 * q + 1] * 4;
-            in_units[q] = in[2 * q];
-            in_recs[q] = (uint32_t)in[2 * q + 1];
-            tu += in[2 * q];
-            tr += in[2 * q + 1];
+            ru[q] = in[4 * q + 2] * 16;
+            rr[q] = in[4 * q + 3] * 4;
+            in_units[q] = in[4 * q + 2];
+            in_recs[q] = (uint32_t)in[4 * q + 3];
+            tu += in[4 * q + 2];
+            tr += in[4 * q + 3];
         }
         uint8_t* rbuf = nullptr;
         uint32_t* roff = nullptr;
@@ -441,8 +484,7 @@ void mig_rounds(keto_comm& c, Snapshot& S, const keto_check_ids* d_reqs, uint32_
             roff = c.l.get<uint32_t>(tr);
         });
         agree(c, mine);
-        c.t->alltoallv(out.d_buf, su, rbuf, ru, c.stream);
-        c.t->alltoallv(out.d_off, sr, roff, rr, c.stream);
+        c.t->alltoallv2(out.d_buf, su, rbuf, ru, out.d_off, sr, roff, rr, c.stream);
         out = MigOut{};
         mine.run([&] {
             injected(c, "mig_round");

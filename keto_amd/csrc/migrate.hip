@@ -574,57 +574,120 @@ __global__ void __launch_bounds__(256) mig_start(const keto_check_ids* __restric
     off[i] = START_UNITS * i;
 }
 
-// group the round's output records by destination part: counts, then a scatter in which every
-// record takes its place; per wave and destination one 64-bit atomic (records << 36 | units) on the
-// destination's cursor, the wave's records placed by prefix sums (a same-address atomic per record
-// would serialize the whole round on one or two addresses)
+// group the round's output records by destination part, without a global atomic: each block takes
+// a chunk of GROUP_CHUNK records and counts them per destination in LDS (mig_group_count), one block
+// per destination turns the per-block counts into exclusive prefixes and the destination's total
+// (mig_group_scan), and each block then places its chunk's records in input order after its prefix
+// (mig_group_scatter).  (One 64-bit atomic per wave and destination on P cursors had serialized at
+// the L2: 0.3-0.7 ms per round at 200K records, profiles/r06p_migrate_local.log.)  Counts are
+// records << 36 | units.
+constexpr uint32_t GROUP_CHUNK = 2048;               // records per block: 256 threads x 8
 __device__ inline uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     return v;
 }
-__global__ void __launch_bounds__(256) mig_count(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ len,
-                                                 const uint32_t* __restrict__ n, uint32_t n_parts,
-                                                 unsigned long long* __restrict__ cnt) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = i < *n;
-    const uint32_t d = valid ? dest[i] : NONE, l = valid ? len[i] : 0u;
-    for (uint32_t p = 0; p < n_parts; ++p) {
-        const uint64_t m = __ballot(d == p);
-        if (!m) continue;
-        const uint32_t units = wave_sum(d == p ? l : 0u);
-        if (lane_id() == 0) atomicAdd(cnt + p, ((unsigned long long)__popcll(m) << 36) | units);
+__global__ void __launch_bounds__(256) mig_group_count(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ len,
+                                                       uint32_t n, uint32_t n_parts, uint32_t n_blocks,
+                                                       unsigned long long* __restrict__ bcnt) {
+    __shared__ unsigned long long c[MIG_MAX_PARTS];
+    if (threadIdx.x < n_parts) c[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * GROUP_CHUNK;
+    for (uint32_t k = 0; k < GROUP_CHUNK / 256; ++k) {
+        const uint32_t i = base + k * 256 + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t d = valid ? dest[i] : NONE, l = valid ? len[i] : 0u;
+        for (uint32_t p = 0; p < n_parts; ++p) {
+            const uint64_t m = __ballot(d == p);
+            if (!m) continue;
+            const uint32_t units = wave_sum(d == p ? l : 0u);
+            if (lane_id() == 0) atomicAdd(&c[p], ((unsigned long long)__popcll(m) << 36) | units);
+        }
     }
+    __syncthreads();
+    if (threadIdx.x < n_parts) bcnt[(uint64_t)threadIdx.x * n_blocks + blockIdx.x] = c[threadIdx.x];
 }
-__global__ void __launch_bounds__(256) mig_scatter(const uint32_t* __restrict__ dest, const uint32_t* __restrict__ unit,
-                                                   const uint32_t* __restrict__ len, const uint32_t* __restrict__ n,
-                                                   uint32_t n_parts, const uint32_t* __restrict__ pool,
-                                                   unsigned long long* __restrict__ cursor,
-                                                   const uint64_t* __restrict__ unit_base,
-                                                   const uint32_t* __restrict__ rec_base, uint32_t* __restrict__ send,
-                                                   uint32_t* __restrict__ send_off) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = lane_id();
-    const bool valid = i < *n;
-    const uint32_t d = valid ? dest[i] : NONE, l = valid ? len[i] : 0u;
-    for (uint32_t p = 0; p < n_parts; ++p) {
-        const uint64_t m = __ballot(d == p);
-        if (!m) continue;
-        const uint32_t incl = wave_scan(d == p ? l : 0u);
-        const uint32_t tot = __shfl(incl, 63);
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(cursor + p, ((unsigned long long)__popcll(m) << 36) | tot);
-        base = __shfl(base, 0);
-        if (d != p) continue;
-        const uint64_t u_in = (base & ((1ull << 36) - 1)) + incl - l;
-        const uint64_t r_in = (base >> 36) + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
-        const uint4* src = reinterpret_cast<const uint4*>(pool) + unit[i];
-        uint4* dst = reinterpret_cast<uint4*>(send) + unit_base[p] + u_in;
-        for (uint32_t k = 0; k < l; ++k) dst[k] = src[k];
-        send_off[rec_base[p] + r_in] = (uint32_t)u_in;
+// one block per destination: its column of per-block counts -> exclusive prefixes; total[p]
+__global__ void __launch_bounds__(256) mig_group_scan(unsigned long long* __restrict__ bcnt, uint32_t n_blocks,
+                                                      unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long s[256];
+    unsigned long long* col = bcnt + (uint64_t)blockIdx.x * n_blocks;
+    unsigned long long carry = 0;
+    for (uint32_t at = 0; at < n_blocks; at += 256) {
+        const uint32_t i = at + threadIdx.x;
+        const unsigned long long v = i < n_blocks ? col[i] : 0ull;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (uint32_t d = 1; d < 256; d <<= 1) {
+            const unsigned long long t = threadIdx.x >= d ? s[threadIdx.x - d] : 0ull;
+            __syncthreads();
+            s[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < n_blocks) col[i] = carry + s[threadIdx.x] - v;
+        carry += s[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) total[blockIdx.x] = carry;
+}
+struct GroupBases {
+    uint64_t unit[MIG_MAX_PARTS];     // first unit of each destination's segment of the send buffer
+    uint32_t rec[MIG_MAX_PARTS];      // first record of each destination's segment
+};
+__global__ void __launch_bounds__(256) mig_group_scatter(const uint32_t* __restrict__ dest,
+                                                         const uint32_t* __restrict__ unit,
+                                                         const uint32_t* __restrict__ len, uint32_t n,
+                                                         uint32_t n_parts, uint32_t n_blocks,
+                                                         const unsigned long long* __restrict__ bcnt,
+                                                         const uint32_t* __restrict__ pool, GroupBases gb,
+                                                         uint32_t* __restrict__ send, uint32_t* __restrict__ send_off) {
+    __shared__ unsigned long long run[MIG_MAX_PARTS];
+    __shared__ unsigned long long wt[4][MIG_MAX_PARTS];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x < n_parts) run[threadIdx.x] = bcnt[(uint64_t)threadIdx.x * n_blocks + blockIdx.x];
+    __syncthreads();
+    const uint32_t base = blockIdx.x * GROUP_CHUNK;
+    for (uint32_t k = 0; k < GROUP_CHUNK / 256; ++k) {
+        const uint32_t i = base + k * 256 + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t d = valid ? dest[i] : NONE, l = valid ? len[i] : 0u;
+        uint32_t my_u = 0, my_r = 0;
+        for (uint32_t p = 0; p < n_parts; ++p) {
+            const uint64_t m = __ballot(d == p);
+            if (!m) {
+                if (lane == 0) wt[w][p] = 0;
+                continue;
+            }
+            const uint32_t incl = wave_scan(d == p ? l : 0u);
+            if (lane == 63) wt[w][p] = ((unsigned long long)__popcll(m) << 36) | incl;
+            if (d == p) {
+                my_u = incl - l;
+                my_r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            }
+        }
+        __syncthreads();
+        if (d < n_parts) {
+            unsigned long long off = run[d];
+            for (uint32_t v = 0; v < w; ++v) off += wt[v][d];
+            const uint64_t u_in = (off & ((1ull << 36) - 1)) + my_u;
+            const uint64_t r_in = (off >> 36) + my_r;
+            const uint4* src = reinterpret_cast<const uint4*>(pool) + unit[i];
+            uint4* dst = reinterpret_cast<uint4*>(send) + gb.unit[d] + u_in;
+            for (uint32_t x = 0; x < l; ++x) dst[x] = src[x];
+            send_off[gb.rec[d] + r_in] = (uint32_t)u_in;
+        }
+        __syncthreads();
+        if (threadIdx.x < n_parts) run[threadIdx.x] += wt[0][threadIdx.x] + wt[1][threadIdx.x] + wt[2][threadIdx.x] + wt[3][threadIdx.x];
+        __syncthreads();
     }
 }
 
+inline uint32_t pow2_floor(uint32_t v) {
+    uint32_t p = 1;
+    while (p * 2 <= v) p *= 2;
+    return p;
+}
 template <class T>
 T* dalloc(uint64_t n) {
     void* p = nullptr;
@@ -692,11 +755,11 @@ struct MigState {
     uint64_t out_cap = 0;
     uint32_t* ctr = nullptr;           // [0] out_count [1] n_spill [2] n_big [3] scratch [4..7] stats [8..11] err
     unsigned long long* pool_used = nullptr;
-    unsigned long long* cursor = nullptr;   // [MIG_MAX_PARTS]
+    unsigned long long* cursor = nullptr;   // [MIG_MAX_PARTS] records << 36 | units per destination
+    unsigned long long* bcnt = nullptr;     // per block and destination (mig_group_*)
+    uint64_t bcnt_cap = 0;
     uint64_t* unit_base = nullptr;          // [MIG_MAX_PARTS] source / destination unit bases
     uint32_t* rec_base = nullptr;           // [MIG_MAX_PARTS + 1]
-    uint64_t* dunit_base = nullptr;
-    uint32_t* drec_base = nullptr;
     uint32_t* send = nullptr;
     uint64_t send_cap = 0;
     uint32_t* send_off = nullptr;
@@ -720,10 +783,9 @@ struct MigState {
         dfree(ctr);
         dfree(pool_used);
         dfree(cursor);
+        dfree(bcnt);
         dfree(unit_base);
         dfree(rec_base);
-        dfree(dunit_base);
-        dfree(drec_base);
         dfree(send);
         dfree(send_off);
     }
@@ -756,8 +818,6 @@ MigState& mig_state(Snapshot& S) {
         M->cursor = dalloc<unsigned long long>(MIG_MAX_PARTS);
         M->unit_base = dalloc<uint64_t>(MIG_MAX_PARTS);
         M->rec_base = dalloc<uint32_t>(MIG_MAX_PARTS + 1);
-        M->dunit_base = dalloc<uint64_t>(MIG_MAX_PARTS);
-        M->drec_base = dalloc<uint32_t>(MIG_MAX_PARTS + 1);
         S.mig.reset(M.release());
     }
     return *S.mig;
@@ -804,7 +864,13 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
         if (const char* e = getenv("KETO_MIG_POOL_UNITS")) want = std::max<uint64_t>(64, strtoull(e, nullptr, 0));
         grow_pool(M, want, st);
     }
-    if (!M.small.vtab) M.small.alloc(LANES_SMALL, VCAP_SMALL);
+    if (!M.small.vtab) {
+        // KETO_MIG_LANES / KETO_MIG_VCAP: the small tier's lanes and table entries (measurement knobs)
+        uint32_t lanes = LANES_SMALL, vcap = VCAP_SMALL;
+        if (const char* e = getenv("KETO_MIG_LANES")) lanes = std::max<uint32_t>(256, (uint32_t)strtoul(e, nullptr, 0) / 256 * 256);
+        if (const char* e = getenv("KETO_MIG_VCAP")) vcap = pow2_floor(std::max<uint32_t>(16, std::min<uint32_t>(VCAP_BIG, (uint32_t)strtoul(e, nullptr, 0))));
+        M.small.alloc(lanes, vcap);
+    }
     if (!M.bigl.vtab) M.bigl.alloc(LANES_BIG, VCAP_BIG);
     // source segments
     uint32_t rb[MIG_MAX_PARTS + 1];
@@ -907,30 +973,42 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
     if (getenv("KETO_MIG_DEBUG"))
         fprintf(stderr, "mig part %u: in %u big %u out %u decided %u undecided %u pool %llu spilled %u\n", S.part, n_in,
                 n_big, n_out, cnt[4], cnt[5], (unsigned long long)M.pool_cap, spilled);
-    // group by destination
-    HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
-    if (n_out) {
-        hipLaunchKernelGGL(mig_count, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_len, M.ctr + 0, P,
-                           M.cursor);
-        HIP_OK(hipGetLastError());
+    if (cnt[8])
+        throw Error{KETO_E_INVALID, std::to_string(cnt[8]) + " malformed continuation records or handles (first: code " +
+                                        std::to_string(cnt[9]) + ", input record " + std::to_string(cnt[10]) +
+                                        ", value " + std::to_string(cnt[11]) + ")"};
+    // group by destination (mig_group_*): per-block counts, their prefixes, then the records in place
+    const uint32_t nb = (uint32_t)(((uint64_t)n_out + GROUP_CHUNK - 1) / GROUP_CHUNK);
+    if (M.bcnt_cap < (uint64_t)nb * P || !M.bcnt) {
+        dfree(M.bcnt);
+        M.bcnt_cap = std::max<uint64_t>((uint64_t)nb * P * 2, 1024);
+        M.bcnt = dalloc<unsigned long long>(M.bcnt_cap);
     }
-    unsigned long long c[MIG_MAX_PARTS];
-    HIP_OK(hipMemcpyAsync(c, M.cursor, MIG_MAX_PARTS * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    uint64_t dub[MIG_MAX_PARTS], total_units = 0;
-    uint32_t drb[MIG_MAX_PARTS + 1];
-    drb[0] = 0;
+    unsigned long long c[MIG_MAX_PARTS] = {};
+    if (n_out) {
+        hipLaunchKernelGGL(mig_group_count, dim3(nb), dim3(256), 0, st, M.out_dest, M.out_len, n_out, P, nb, M.bcnt);
+        HIP_OK(hipGetLastError());
+        hipLaunchKernelGGL(mig_group_scan, dim3(P), dim3(256), 0, st, M.bcnt, nb, M.cursor);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(c, M.cursor, P * 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    GroupBases gb{};
+    uint64_t total_units = 0;
+    uint32_t total_recs = 0;
     for (uint32_t p = 0; p < P; ++p) {
         out.units[p] = c[p] & ((1ull << 36) - 1);
         out.records[p] = (uint32_t)(c[p] >> 36);
-        dub[p] = total_units;
+        gb.unit[p] = total_units;
+        gb.rec[p] = total_recs;
         total_units += out.units[p];
-        drb[p + 1] = drb[p] + out.records[p];
+        total_recs += out.records[p];
     }
     for (uint32_t p = P; p < MIG_MAX_PARTS; ++p) {
         out.units[p] = 0;
         out.records[p] = 0;
     }
+    if (total_recs != n_out) throw Error{KETO_E_INVALID, "continuation records with a bad destination part"};
     if (M.send_cap < total_units || !M.send) {
         dfree(M.send);
         M.send_cap = std::max<uint64_t>(total_units * 2, 1ull << 16);
@@ -942,19 +1020,11 @@ void run_round(Snapshot& S, MigState& M, const uint32_t* d_in, const uint32_t* d
         M.send_off = dalloc<uint32_t>(M.send_off_cap);
     }
     if (n_out) {
-        HIP_OK(hipMemcpyAsync(M.dunit_base, dub, P * 8, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(M.drec_base, drb, (P + 1) * 4, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemsetAsync(M.cursor, 0, MIG_MAX_PARTS * 8, st));
-        hipLaunchKernelGGL(mig_scatter, dim3((n_out + 255) / 256), dim3(256), 0, st, M.out_dest, M.out_unit, M.out_len,
-                           M.ctr + 0, P, M.pool, M.cursor, M.dunit_base, M.drec_base, M.send, M.send_off);
+        hipLaunchKernelGGL(mig_group_scatter, dim3(nb), dim3(256), 0, st, M.out_dest, M.out_unit, M.out_len, n_out, P,
+                           nb, M.bcnt, M.pool, gb, M.send, M.send_off);
         HIP_OK(hipGetLastError());
+        HIP_OK(hipStreamSynchronize(st));
     }
-    HIP_OK(hipMemcpyAsync(cnt, M.ctr, 16 * 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (cnt[8])
-        throw Error{KETO_E_INVALID, std::to_string(cnt[8]) + " malformed continuation records or handles (first: code " +
-                                        std::to_string(cnt[9]) + ", input record " + std::to_string(cnt[10]) +
-                                        ", value " + std::to_string(cnt[11]) + ")"};
     out.d_buf = M.send;
     out.d_off = M.send_off;
     out.decided = cnt[4];

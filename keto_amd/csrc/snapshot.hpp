@@ -603,6 +603,15 @@ void device_resolve_packed_rows(Snapshot& s, const uint8_t* blob, uint64_t blob_
                                 void* stream);
 // d[idx[k]] = vals[k] for k < m (device arrays)
 void scatter_ids(keto_check_ids* d, const uint32_t* d_idx, const keto_check_ids* d_vals, uint32_t m, void* stream);
+// up to COPY_SEGMENTS device-to-device copies in one launch (route.hip)
+constexpr uint32_t COPY_SEGMENTS = 64;
+struct CopySegments {
+    const void* src[COPY_SEGMENTS];
+    void* dst[COPY_SEGMENTS];
+    uint64_t bytes[COPY_SEGMENTS];
+    uint32_t n;
+};
+void copy_segments(const CopySegments& s, void* stream);
 // An allocator whose resize() leaves new elements default-initialized (no zero fill): the expand
 // node arena is sized, then overwritten by one D2H copy.
 template <class T>
