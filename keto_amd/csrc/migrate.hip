@@ -93,22 +93,27 @@ __device__ inline uint32_t coll_find(const uint64_t* coll, uint32_t mask, uint32
     }
 }
 
-// A visited map in the lane's HBM table (epoch-tagged: entry = epoch << 36 | visit id), with an
-// insertion log so the whole map can travel in a record.
+// A visited map: its first MIG_LDS_VIDS ids in the lane's LDS column, behind a 64-bit filter in
+// registers (a test the filter rules out, and an insert, touch no memory; a filter hit scans the
+// column); past that, the lane's HBM table (epoch-tagged: entry = epoch << 36 | visit id) takes every
+// id, as before round 6.  The insertion log (LDS column, then the HBM log) lets the whole map travel
+// in a record.  (Every test had been a dependent HBM probe: profiles/r06y_migrate_lds_map.log.)
+constexpr uint32_t MIG_LDS_VIDS = 16;
 struct MigVisited {
     uint64_t* tab;
     uint64_t* log;
     uint32_t mask, cap;      // cap = ids a map may hold (half the table)
     uint32_t epoch, n;
+    uint64_t* lv;            // the lane's LDS column: entry k at lv[k * 256]
+    uint64_t filt;
+    bool big;                // the map lives in the HBM table
+    __device__ inline uint64_t at(uint32_t k) const { return big ? log[k] : lv[(uint64_t)k * 256]; }
     __device__ inline void fresh() {
-        if (++epoch > EPOCH_MAX) {
-            for (uint32_t i = 0; i <= mask; ++i) tab[i] = 0;
-            epoch = 1;
-        }
         n = 0;
+        filt = 0;
+        big = false;
     }
-    // 0 = new, 1 = present, 2 = the map is full
-    __device__ inline int test_add(uint64_t vid) {
+    __device__ inline int tab_add(uint64_t vid) {
         uint32_t i = mixv(vid) & mask;
         const uint64_t want = ((uint64_t)epoch << 36) | vid;
         for (;;) {
@@ -122,6 +127,32 @@ struct MigVisited {
             if (e == want) return 1;
             i = (i + 1) & mask;
         }
+    }
+    // 0 = new, 1 = present, 2 = the map is full
+    __device__ inline int test_add(uint64_t vid) {
+        if (!big) {
+            const uint64_t b = 1ull << (mixv(vid) & 63u);
+            if (filt & b)
+                for (uint32_t k = 0; k < n; ++k)
+                    if (lv[(uint64_t)k * 256] == vid) return 1;
+            if (n < MIG_LDS_VIDS && n < cap) {
+                lv[(uint64_t)n * 256] = vid;
+                ++n;
+                filt |= b;
+                return 0;
+            }
+            // the column is full: the map moves to the HBM table (a fresh epoch), then takes vid there
+            if (++epoch > EPOCH_MAX) {
+                for (uint32_t i = 0; i <= mask; ++i) tab[i] = 0;
+                epoch = 1;
+            }
+            const uint32_t m = n;
+            n = 0;
+            big = true;
+            for (uint32_t k = 0; k < m; ++k)
+                if (tab_add(lv[(uint64_t)k * 256]) == 2) return 2;
+        }
+        return tab_add(vid);
     }
 };
 
@@ -461,8 +492,9 @@ __global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t stride = gridDim.x * blockDim.x;
+    __shared__ uint64_t s_vids[MIG_LDS_VIDS * 256];
     MigVisited V{a.vtab + (uint64_t)slot * a.vcap, a.vlog + (uint64_t)slot * (a.vcap / 2), a.vcap - 1u, a.vcap / 2,
-                 a.lane_epoch[slot], 0};
+                 a.lane_epoch[slot], 0, s_vids + threadIdx.x, 0, false};
     uint4* const fr = a.frames + (uint64_t)slot * MIG_FRAMES;
     const uint32_t total = a.list ? *a.n_list : a.n_in;
     uint32_t n_dec = 0, n_und = 0, n_in = 0;
@@ -505,7 +537,7 @@ __global__ void __launch_bounds__(256) mig_kernel(MigArgs a) {
         *reinterpret_cast<uint4*>(ow + 4) = make_uint4(o.enter, o.k, nso, nvo);
         for (uint32_t i = 0; i < nso; ++i) *reinterpret_cast<uint4*>(ow + HEAD_WORDS + 4ull * i) = fr[i];
         uint64_t* ov = reinterpret_cast<uint64_t*>(ow + HEAD_WORDS + 4ull * nso);
-        for (uint32_t i = 0; i < nvo; ++i) ov[i] = V.log[i];
+        for (uint32_t i = 0; i < nvo; ++i) ov[i] = V.at(i);
         if (nvo & 1u) ov[nvo] = 0;
         a.out_dest[at] = o.dest;
         a.out_unit[at] = (uint32_t)u;
