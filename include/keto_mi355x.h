@@ -460,8 +460,9 @@ int keto_check_batch_sharded(keto_comm* c, keto_snapshot* s, const keto_check_re
  * wildcard query that no stored subject set uses has no row to route by: a shared-rows part answers
  * it itself (its batch-local row from the whole graph's host tables); a migrating part sends one
  * request per matching row (each top-level tuple is searched with a fresh visited map, so the query
- * is allowed iff one of those rows is) and returns KETO_E_INVALID only when one of them has a failing
- * page.  Every rank returns the same code when any rank fails. */
+ * is allowed iff one of those rows is); when a page of the query's ORDER BY sequence fails, the rows
+ * before that page go whole and the row it cuts one top-level tuple at a time (relationtuples.go:
+ * 64-71; engine.go:98-100).  Every rank returns the same code when any rank fails. */
 int keto_check_batch_routed(keto_comm* c, keto_snapshot* s, const keto_check_req* reqs, uint32_t n,
                             int32_t global_max_depth, uint8_t* allowed_out, uint8_t* status_out);
 /* The same for a packed batch (the keto_check_batch_packed layout: strings back to back in
