@@ -41,9 +41,12 @@ extern "C" {
 
 #define KETO_ABI_VERSION 6
 /* The largest arena one snapshot (a replica) or one partition part takes on a device: handles are
- * 32-bit counts of 16-byte units.  A graph past it is served as several shared-rows parts, more than
- * one per device if need be (each part holds the subject-set targets and its share of the root rows). */
-#define KETO_ARENA_MAX_BYTES (64ull << 30)
+ * 32-bit; below 2^31 a count of 16-byte units (subject-set targets, and the root rows of the first
+ * 32 GiB), above it a count of 32-, 64- or 128-byte units of the root rows past 32 GiB (arenas past
+ * 64 GiB, whatever unit gives every root row a handle).  A graph past it is served as several
+ * shared-rows parts, more than one per device if need be (each part holds the subject-set targets and
+ * its share of the root rows).  Targets alone are capped at 32 GiB. */
+#define KETO_ARENA_MAX_BYTES (288ull << 30)
 
 /* return codes */
 #define KETO_OK 0

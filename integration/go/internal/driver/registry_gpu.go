@@ -29,7 +29,7 @@ import (
 // The server stays one process (internal/driver/daemon.go:62-69) and drives every GPU of the node
 // itself: EnableGPU builds the snapshot from one full scan of the table (sorted once, host-only) and
 // places it (gpu.Place): one replica per device while the replicated arena fits each of them (and the
-// 64 GiB arena cap), else one edge-partitioned snapshot over all of them (gpu.Partition: shared-rows
+// 288 GiB arena cap), else one edge-partitioned snapshot over all of them (gpu.Partition: shared-rows
 // parts, one in-process communicator rank per part, several parts per device when a part would pass
 // the cap), so a table of any size is served from this one process, as the
 // reference serves it.  It starts the check and expand batchers, which deal each batch to an engine

@@ -301,7 +301,7 @@ func (p *Partition) Close() {
 }
 
 // arenaCap is the largest arena a replica or a part takes on a device (KETO_ARENA_MAX_BYTES: handles
-// are 32-bit counts of 16-byte units).
+// are 32-bit counts of 16-byte units, or of up to 128-byte units for the root rows past 32 GiB).
 const arenaCap = uint64(C.KETO_ARENA_MAX_BYTES)
 
 // maxParts bounds the partitions PlanParts tries (every part holds all the subject-set targets).
@@ -312,7 +312,7 @@ const maxParts = 64
 // hold several -- such that every part's arena stays within arenaCap and each device's parts fit its
 // free memory.  Part sizes are estimated from the one-part statistics (every part keeps the targets,
 // the root rows split by hash; an eighth of margin), and the first plan the estimate admits is then
-// checked part by part.  A graph whose root rows pass 64 GiB is so served from one GPU too.
+// checked part by part.  A graph whose arena passes 288 GiB is so served from one GPU too.
 func PlanParts(base *Snapshot, devices []int) ([]int, error) { return planPartsWith(base, devices, nil) }
 
 func planPartsWith(base *Snapshot, devices []int, resident map[int]uint64) ([]int, error) {

@@ -706,7 +706,7 @@ int keto_snapshot_part_stats_mode(keto_snapshot* h, uint32_t part, uint32_t n_pa
         S.n_parts = n_parts;
         S.part_mode = (int)mode;
         compute_layout(S);
-        out->arena_bytes = S.n_units * HDR_WORDS * 4;
+        out->arena_bytes = S.n_words * 4;
         out->shared_bytes = mode == KETO_PART_SHARED ? S.shared_words * 4 : 0;
         out->rows = 0;
         out->shared_rows = 0;

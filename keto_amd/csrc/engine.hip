@@ -67,6 +67,7 @@ struct DevSnap {
     const uint64_t* coll;     // (edge value << 32) | visit id ; empty = ~0
     uint32_t coll_mask;       // 0 = no collisions
     uint32_t n_units;         // handles of the main arena are < n_units (DirectVisited's class base)
+    uint32_t root_g;          // wide arenas: root handles past 2^31 count 16 << root_g bytes (hword)
 };
 
 struct DevOverlay {           // batch-local wildcard rows (top-level / root only)
@@ -129,11 +130,11 @@ __device__ inline RowView load_row(const DevSnap& s, const DevOverlay& ov, uint3
         w = (uint64_t)(h - ov.base) * HDR_WORDS;
     } else {
         rv.a = s.arena;
-        w = (uint64_t)h * HDR_WORDS;
+        w = hword(h, s.root_g);
     }
     uint4 v = *reinterpret_cast<const uint4*>(rv.a + w);
     while (v.z & HDR_FWD) {                        // a row a write moved (delta.cpp): its current place
-        w = (uint64_t)v.x * HDR_WORDS;
+        w = hword(v.x, s.root_g);
         v = *reinterpret_cast<const uint4*>(rv.a + w);
     }
     rv.beg = w + HDR_WORDS;
@@ -795,7 +796,7 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
                 ea = ov.arena;
                 hw = (uint64_t)(enter - ov.base) * HDR_WORDS;
             } else {
-                hw = (uint64_t)enter * HDR_WORDS;
+                hw = hword(enter, s.root_g);
             }
             h0 = *reinterpret_cast<const uint4*>(ea + hw);
             h1 = *reinterpret_cast<const uint4*>(ea + hw + HDR_WORDS);
@@ -871,15 +872,15 @@ __global__ void __launch_bounds__(256, KETO_CHECK_WAVES) check_kernel(DevSnap s,
             uint32_t at = enter;
             while (h0.z & HDR_FWD) {
                 at = h0.x;
-                h0 = *reinterpret_cast<const uint4*>(ea + (uint64_t)at * HDR_WORDS);
-                h1 = *reinterpret_cast<const uint4*>(ea + (uint64_t)at * HDR_WORDS + HDR_WORDS);
+                h0 = *reinterpret_cast<const uint4*>(ea + hword(at, s.root_g));
+                h1 = *reinterpret_cast<const uint4*>(ea + hword(at, s.root_g) + HDR_WORDS);
             }
             const uint32_t n_sets = h0.x, n_ids = h0.y;
             const bool seq = (h0.z & HDR_SEQ) != 0;
             const uint32_t hl = (h0.z >> 8) & 31u;
             const bool cb = pruned_cb;
             const bool tcb = (h0.z & HDR_CLOSURE) != 0;       // the id table sits below a filter
-            const uint64_t beg = (at >= ov.base ? (uint64_t)(at - ov.base) : (uint64_t)at) * HDR_WORDS + HDR_WORDS;
+            const uint64_t beg = (at >= ov.base ? (uint64_t)(at - ov.base) * HDR_WORDS : hword(at, s.root_g)) + HDR_WORDS;
             w.row();
             w.header(ea + beg - HDR_WORDS);
             if (cb && !tset && !(enter_fl & FR_TOP) && !((cbw >> (cwb & 31u)) & 1u)) {
@@ -1086,7 +1087,11 @@ __device__ inline bool chunk_wait(const uint32_t* p, uint64_t ticks) {
 #endif
 constexpr uint32_t P_XLT = 5;          // streamed: the request's row id (and set target) -> handles
 
-template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM>
+// WIDE: an arena past 64 GiB (snapshot.hpp hword).  Root rows may lie in any of its up to 18
+// segments, targets only in segments 0 and 1; only a search's top frame is ever a root row, so the
+// segment field of the control word and of saved frames keeps 0 and 1 as they are and 2 for "the
+// lane's root segment", held in one register (rseg) set when the request's row is entered.
+template <int F, bool WIN, int LV, int RV, bool COUNT, bool STREAM, bool WIDE = false>
 __device__ __forceinline__ void
     check_wave_body(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
                     uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
@@ -1150,6 +1155,7 @@ __device__ __forceinline__ void
     uint32_t pos = 0, left = 0;                                // current frame (k, fl in c)
     uint4 win = make_uint4(0, 0, 0, 0);
     uint32_t eh = 0;                                           // row to enter (P_HDR) / bucket (P_IDQ)
+    uint32_t rseg = 0;                                         // WIDE: the segment of the request's row
     // record request qi's decision: whole groups of 4 are stored as one word, a run's partial last
     // group byte by byte
     auto decide = [&](uint32_t qi, uint32_t r) {
@@ -1253,10 +1259,19 @@ __device__ __forceinline__ void
         // next request pair's prefetch
         const bool hdr = ph == P_HDR;
         const bool in_ov = hdr ? eh >= ov.base : (bf(c, C_FL, 4) & FR_OV) != 0;
-        const uint32_t seg = in_ov ? 0u : hdr ? (eh >> SEG_SHIFT) : c_seg(c);
+        uint32_t seg, hdr_w;                                      // a header's segment and word in it
+        if constexpr (WIDE) {
+            const uint64_t hw = hword(eh, s.root_g);
+            const uint32_t f = c_seg(c);
+            seg = in_ov ? 0u : hdr ? (uint32_t)(hw >> 32) : f == 2u ? rseg : f;
+            hdr_w = in_ov ? (eh - ov.base) * HDR_WORDS : (uint32_t)hw;
+        } else {
+            seg = in_ov ? 0u : hdr ? (eh >> SEG_SHIFT) : c_seg(c);
+            hdr_w = (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS;
+        }
         const uint32_t* const ar = (in_ov ? ov.arena : s.arena) + ((uint64_t)seg << 32);
         const uint32_t hl = bf(c, C_HL, 5);
-        const uint32_t word = hdr ? (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS
+        const uint32_t word = hdr ? hdr_w
                                   : ph == P_IDQ ? pos - HDR_WORDS - ((c & C_CB) ? CB_WORDS : 0u) - (1u << hl) +
                                                       eh * BUCKET_WORDS
                                                 : (pos & ~3u);
@@ -1378,12 +1393,19 @@ __device__ __forceinline__ void
                 const uint32_t hl = (v0.z >> 8) & 31u;
                 const uint32_t k = have ? bf(c, C_K, 5) - 1u : bf(c, C_K, 5);
                 const uint32_t fl = (have ? 0u : (uint32_t)FR_TOP) | (seq ? FR_SEQ : 0u) | (is_ov ? FR_OV : 0u) | FR_WV;
-                pos = (is_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS + HDR_WORDS;
                 left = v0.x;
                 win = v1;
                 c = bf_set(bf_set(bf_set(bf_set(c, C_K, 5, k), C_FL, 4, fl), C_HL, 5, hl), C_PH, 3, P_WALK) | C_HAVE;
                 c = (v0.z & HDR_CLOSURE) ? (c | C_CB) : (c & ~C_CB);
-                c = c_with_seg(c, is_ov ? 0u : eh >> SEG_SHIFT);
+                if constexpr (WIDE) {
+                    // (seg / hdr_w are this iteration's header: eh has not changed since)
+                    pos = hdr_w + HDR_WORDS;
+                    if (seg >= 2u) rseg = seg;
+                    c = c_with_seg(c, min(seg, 2u));
+                } else {
+                    pos = (is_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS + HDR_WORDS;
+                    c = c_with_seg(c, is_ov ? 0u : eh >> SEG_SHIFT);
+                }
                 // window slots whose subject set cannot reach T (child signatures, read entering a
                 // subject set; never for a subject-set request)
                 const uint32_t skip = (have && !tset && (v0.z & HDR_CLOSURE)) ? ~(sgw >> ((cbit & 7u) * 4u)) & 15u : 0u;
@@ -1538,6 +1560,13 @@ __global__ void __launch_bounds__(256, 8)
     check_wave_kernel_w8(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
                          uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
     check_wave_body<F, false, LV, RV, false, false>(s, ov, q, n, gmd, allowed, ta, work);
+}
+// tier 0 of a wide arena (past 64 GiB): the default geometry, root rows in any segment
+template <int F, bool STREAM>
+__global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
+    check_wave_kernel_wide(DevSnap s, DevOverlay ov, const keto_check_ids* __restrict__ q, uint32_t n, int gmd,
+                           uint8_t* __restrict__ allowed, TierArgs ta, unsigned long long* __restrict__ work) {
+    check_wave_body<F, false, 8, 8, false, STREAM, true>(s, ov, q, n, gmd, allowed, ta, work);
 }
 
 // ------------------------------------------------------------------ check, deep requests
@@ -2084,11 +2113,11 @@ __device__ int expand_one(const DevSnap& s, const DevOverlay& ov, uint32_t root,
             if (hl >= ov.base) {
                 rv = load_row(s, ov, hl);
             } else {
-                uint64_t w = (uint64_t)hl * HDR_WORDS;
+                uint64_t w = hword(hl, s.root_g);
                 uint4 v = *reinterpret_cast<const uint4*>(s.arena + w);
                 w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
                 while (v.z & HDR_FWD) {                     // a row a write moved (delta.cpp)
-                    w = (uint64_t)v.x * HDR_WORDS;
+                    w = hword(v.x, s.root_g);
                     v = *reinterpret_cast<const uint4*>(s.arena + w);
                     w4 = *reinterpret_cast<const uint4*>(s.arena + w + HDR_WORDS);
                 }
@@ -2308,7 +2337,7 @@ __device__ int expand_sm(const DevSnap& s, const DevOverlay& ov, uint32_t root, 
         uint4 v = make_uint4(0, 0, 0, 0), w4 = make_uint4(0, 0, 0, 0);
         const bool in_ov = ol >= ov.base;
         const uint32_t* const ha = in_ov ? ov.arena : s.arena;
-        const uint64_t hw = (uint64_t)(in_ov ? ol - ov.base : ol) * HDR_WORDS;
+        const uint64_t hw = in_ov ? (uint64_t)(ol - ov.base) * HDR_WORDS : hword(ol, s.root_g);
         if (opening) {
             v = *reinterpret_cast<const uint4*>(ha + hw);
             if (!in_ov) w4 = *reinterpret_cast<const uint4*>(ha + hw + HDR_WORDS);   // (the arena has slack)
@@ -2789,7 +2818,8 @@ struct DeviceState {
     uint32_t* st_ready = nullptr;
     uint64_t st_cap = 0;
 
-    DevSnap view() const { return DevSnap{arena, coll, coll_mask, n_units}; }
+    uint32_t root_g = 0;          // wide arenas (snapshot.hpp hword)
+    DevSnap view() const { return DevSnap{arena, coll, coll_mask, n_units, root_g}; }
 };
 
 namespace {
@@ -2930,10 +2960,10 @@ void host_parallel_for(uint64_t n, F f) {
 // Write one row (table, closure filter seed, header, edges) into an arena at its handle.  The
 // closure filter starts as the row's own ids (all bits for a ROW_SEQ row); closure_pass adds the
 // closures of its subject sets on the device, then sig_pass its child signatures.
-void put_row(uint32_t* arena, uint32_t unit, const RowRec& rec, uint32_t pp, uint32_t hlog2, const uint32_t* edges,
+void put_row(uint32_t* arena, uint64_t hdr_word, const RowRec& rec, uint32_t pp, uint32_t hlog2, const uint32_t* edges,
              uint64_t n_stored, const std::vector<uint32_t>& unit_of_row, bool closure, uint64_t base = 0) {
     // `arena` holds the arena's words from `base` on
-    uint64_t h = (uint64_t)unit * HDR_WORDS - base;
+    uint64_t h = hdr_word - base;
     const bool seq = ((rec.hi_flags >> 8) & ROW_SEQ) != 0;
     arena[h + 0] = rec.n_sets;
     arena[h + 1] = rec.n_ids;
@@ -3193,8 +3223,8 @@ void device_upload(Snapshot& S, int device) {
     auto D = std::make_unique<DeviceState>();
     D->device = device;
     uint64_t acc = 0;
-    const uint64_t words = S.n_units * HDR_WORDS;
-    if (words > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
+    const uint64_t words = S.n_words;
+    if (words > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 288 GiB"};
     // a split layout's reserve [tgt_tail, roots_at) is not built on the host: the targets below it
     // and the roots above it are two host pieces
     const bool split = S.tgt_end > 0;
@@ -3215,8 +3245,8 @@ void device_upload(Snapshot& S, int device) {
             return;
         }
         const auto ed = S.row_edges((uint32_t)r);
-        const bool hi = split && (uint64_t)S.unit_of_row[r] * HDR_WORDS >= hi_base;
-        put_row(hi ? arena_hi.data() : arena.data(), S.unit_of_row[r], S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r),
+        const bool hi = split && S.hdr_word(S.unit_of_row[r]) >= hi_base;
+        put_row(hi ? arena_hi.data() : arena.data(), S.hdr_word(S.unit_of_row[r]), S.rows[r], S.row_pp[r], S.row_hlog2((uint32_t)r),
                 ed.first, ed.second, S.unit_of_row, S.row_cb[r] != 0, hi ? hi_base : 0);
     });
     // room at the tail for rows writes move (keto_snapshot_apply; grown on demand)
@@ -3236,6 +3266,7 @@ void device_upload(Snapshot& S, int device) {
     // a map holds at most one id per row / collision class (+ an expand root outside the rows)
     D->vid_bound = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)S.n_rows() + S.n_coll_keys + 2);
     D->n_units = (uint32_t)S.n_units;
+    D->root_g = S.root_g;
     D->n_coll = S.n_coll_keys;
     // the compute stream and the two copy streams; the pipeline's optional second compute stream is
     // created on first use (KETO_PIPE_STREAMS=2): a process gets few hardware queues
@@ -3353,24 +3384,28 @@ namespace {
 // A tail place for a row (the same line and segment rules as compute_layout): returns its header
 // unit.  A subject-set target (cb) needs a handle below 2^31: in a split layout it goes into the
 // target reserve, else to the tail while that is low enough; without room the caller must rebuild
-// (compute_layout places it among the targets).
-uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint64_t& total_words) {
+// (compute_layout places it among the targets).  `low`: the new content of a target a write moved
+// (its identity keeps the closure block) in a wide layout, whose tier 0 holds the segment of the
+// search's top row only (check_wave_kernel_wide): it goes into the target reserve too.
+uint32_t tail_place(Snapshot& S, uint32_t hlog2, bool cb, uint64_t n_edges, uint64_t& total_words, bool low = false) {
     const uint64_t table = hlog2 ? (1ull << hlog2) : 0;
     const uint64_t c = cb ? CB_WORDS : 0;
-    if (cb && S.tgt_end) {
+    if ((cb || low) && S.tgt_end) {
         const uint64_t w = arena_fit(S.tgt_tail, table, c, n_edges, total_words);
         if (w + total_words > S.tgt_end)
             throw Error{KETO_E_REBUILD, "the arena's reserve for new subject-set targets is full: rebuild the snapshot"};
         S.tgt_tail = w + total_words;
         return (uint32_t)((w + table + c) / HDR_WORDS);
     }
-    const uint64_t w = arena_fit(S.n_units * HDR_WORDS, table, c, n_edges, total_words);
-    const uint64_t unit = (w + table + c) / HDR_WORDS;
+    const uint64_t w = arena_fit_g(S.n_words, table, c, n_edges, total_words, S.root_g);
+    const uint64_t unit = handle_at_word(w + table + c, S.root_g);
     if (cb && unit >= (uint64_t)EDGE_VAL)
         throw Error{KETO_E_REBUILD, "a new subject-set target would lie past 2^31 16-byte units: rebuild the snapshot"};
-    if (w + total_words > ARENA_MAX_WORDS || unit >= HANDLE_MAX)
-        throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
-    S.n_units = (w + total_words) / HDR_WORDS;
+    // past the narrow layout's 64 GiB, or out of handles: laid out afresh (wide, or a coarser root unit)
+    if (w + total_words > (S.root_g ? ARENA_MAX_WORDS : NARROW_MAX_WORDS) || unit >= HANDLE_MAX - 0x1000u)
+        throw Error{KETO_E_REBUILD, "the arena's tail is out of handles: rebuild the snapshot"};
+    S.n_words = w + total_words;
+    S.n_units = handle_end(S.n_words, S.root_g);
     return (uint32_t)unit;
 }
 }  // namespace
@@ -3505,19 +3540,19 @@ bool apply_in_place(Snapshot& S) {
         const uint32_t hl = S.row_hlog2(r);
         const uint64_t table = hl ? (1ull << hl) : 0, c = cb ? CB_WORDS : 0;
         Write w;
-        w.word = (uint64_t)unit * HDR_WORDS - table - c;
+        w.word = S.hdr_word(unit) - table - c;
         w.img.assign(table + c + HDR_WORDS + ((ed.second + 3) & ~3ull), 0);
         // put_row writes relative to the header: lay it out in a scratch arena starting at word 0
         const uint32_t u0 = (uint32_t)((table + c + HDR_WORDS - 1) / HDR_WORDS);
         std::vector<uint32_t> scratch((uint64_t)u0 * HDR_WORDS + HDR_WORDS + ((ed.second + 3) & ~3ull) + 8, 0);
-        put_row(scratch.data(), u0, S.rows[r], S.row_pp[r], hl, ed.first, ed.second, S.unit_of_row, cb);
+        put_row(scratch.data(), (uint64_t)u0 * HDR_WORDS, S.rows[r], S.row_pp[r], hl, ed.first, ed.second, S.unit_of_row, cb);
         const uint64_t from = (uint64_t)u0 * HDR_WORDS - table - c;
         std::copy(scratch.begin() + from, scratch.begin() + from + w.img.size(), w.img.begin());
         writes.push_back(std::move(w));
     };
     auto forward = [&](uint32_t at, uint32_t to, bool cb) {
         Write w;
-        w.word = (uint64_t)at * HDR_WORDS;
+        w.word = S.hdr_word(at);
         w.img = {to, 0u, HDR_FWD | (cb ? HDR_CLOSURE : 0u), 0u};
         writes.push_back(std::move(w));
     };
@@ -3580,7 +3615,7 @@ bool apply_in_place(Snapshot& S) {
             image(r, pl.unit, pl.cb);                         // fits where it is
             if (pl.unit != id && S.row_cb[r]) {               // a forwarded row: re-seed the identity filter
                 Write w;
-                w.word = (uint64_t)id * HDR_WORDS - CB_WORDS;
+                w.word = S.hdr_word(id) - CB_WORDS;
                 w.img.assign(CF_WORDS, 0);
                 const auto ed = S.row_edges(r);
                 const bool seq = (S.row_flags(r) & ROW_SEQ) != 0;
@@ -3596,13 +3631,19 @@ bool apply_in_place(Snapshot& S) {
             }
         } else {
             uint64_t tw = 0;
-            const uint32_t u = tail_place(S, hl, false, S.row_edges(r).second, tw);
+            uint32_t u = 0;
+            try {
+                u = tail_place(S, hl, false, S.row_edges(r).second, tw, S.root_g && S.row_cb[r]);
+            } catch (const Error& e) {
+                if (e.code == KETO_E_REBUILD) return false;       // (nothing written to the device yet)
+                throw;
+            }
             pl = Snapshot::RowPlace{u, hl, cap, false};
             image(r, u, false);
             forward(id, u, S.row_cb[r] != 0);
             if (S.row_cb[r]) {                                // the identity's filter, re-seeded
                 Write w;
-                w.word = (uint64_t)id * HDR_WORDS - CB_WORDS;
+                w.word = S.hdr_word(id) - CB_WORDS;
                 w.img.assign(CF_WORDS, 0);
                 const auto ed = S.row_edges(r);
                 const bool seq = (S.row_flags(r) & ROW_SEQ) != 0;
@@ -3621,8 +3662,7 @@ bool apply_in_place(Snapshot& S) {
     for (auto& m : moved) forward(m.second, S.unit_of_row[m.first], false);   // stale top-level handles
     lap("images");
     // 3. room: grow the arena if the tail outgrew it (handles are word offsets: copied as is)
-    const uint64_t need = S.n_units * HDR_WORDS;
-    if (need > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
+    const uint64_t need = S.n_words;
     if (need > D.arena_words) {
         // (slack past the last row: the kernels read a header's 32-B slot, window included)
         const uint64_t cap = std::min<uint64_t>(ARENA_MAX_WORDS, std::max<uint64_t>(need + 1024, D.arena_words + D.arena_words / 4));
@@ -4064,7 +4104,7 @@ struct OverlayBuf {
             const uint64_t e = i + 1 < ov->rows.size()
                                    ? ((uint64_t)ov->rows[i + 1].edge_lo | ((uint64_t)(ov->rows[i + 1].hi_flags & 0xFFu) << 32))
                                    : ov->edges.size();
-            put_row(arena.data(), ov->unit[i], rec, ov->pp[i], 0, ov->edges.data() + b, e - b, S.unit_of_row, false);
+            put_row(arena.data(), (uint64_t)ov->unit[i] * HDR_WORDS, rec, ov->pp[i], 0, ov->edges.data() + b, e - b, S.unit_of_row, false);
         }
         uint64_t acc = 0;
         uint32_t* a = dmalloc<uint32_t>(arena.size(), acc);
@@ -4171,14 +4211,14 @@ struct PullSet {
         };
         for (size_t i = 0; i < n_wild; ++i) {
             const auto ed = wild_edges(i);
-            put_row(arena.data(), wild->unit[i], wild->rows[i], wild->pp[i], 0, ed.first, ed.second, S.unit_of_row, false);
+            put_row(arena.data(), (uint64_t)wild->unit[i] * HDR_WORDS, wild->rows[i], wild->pp[i], 0, ed.first, ed.second, S.unit_of_row, false);
             patch(wild->unit[i], ed.first, ed.second);
         }
         for (size_t k = 0; k < id_row.size(); ++k) arena[(slots_at + k) * HDR_WORDS + 2] = HDR_REMOTE;
         for (size_t k = 0; k < pulled.size(); ++k) {
             const uint32_t r = pulled[k];
             const auto ed = S.row_edges(r);
-            put_row(arena.data(), (uint32_t)at[k], S.rows[r], S.row_pp[r], 0, ed.first, ed.second, S.unit_of_row, false);
+            put_row(arena.data(), (uint64_t)at[k] * HDR_WORDS, S.rows[r], S.row_pp[r], 0, ed.first, ed.second, S.unit_of_row, false);
             patch(at[k], ed.first, ed.second);
         }
         for (void* q : bufs.p)
@@ -4413,14 +4453,16 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
         p.slots[2] = s2;
     }
     // (deep_wave_kernel keeps one segment bit: arenas of up to 2 segments)
-    const bool dw = kind == 2 && deep_wave(gmd) && (uint64_t)D.n_units <= (1ull << 31);
+    const bool dw = kind == 2 && deep_wave(gmd) && (uint64_t)D.n_units <= (1ull << 31) && D.root_g == 0;
     if (ss && kind != 0) throw Error{KETO_E_INVALID, "streamed batches need max-depth <= 5"};
     int var = ss ? T0_VARIANTS + 3 + (t0_stream_v0() ? 1 : 0)
                  : kind == 0 ? t0_variant() : kind == 1 ? T0_VARIANTS : dw ? T0_VARIANTS + 2 : T0_VARIANTS + 1;
     // batches of fewer than 16 requests per lane of the 8-wave build take check_wave_kernel_w8
     // (variant 0's geometry at 8 waves per SIMD); KETO_T0 (tuning) or KETO_T0_W8=0 keep the variant
     constexpr int VAR_W8 = T0_VARIANTS + 5;
-    if (kind == 0 && !ss && !work_out && !getenv("KETO_T0") && !(getenv("KETO_T0_W8") && atoi(getenv("KETO_T0_W8")) == 0)) {
+    // a wide arena (past 64 GiB) takes check_wave_kernel_wide as tier 0, whatever the variant
+    const bool wide = D.root_g != 0;
+    if (kind == 0 && !ss && !work_out && !wide && !getenv("KETO_T0") && !(getenv("KETO_T0_W8") && atoi(getenv("KETO_T0_W8")) == 0)) {
         if (!D.v1_lanes[VAR_W8]) {
             int per_cu = 0, cus = 0;
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_wave_kernel_w8<4, 4, 16>, 256, 0));
@@ -4432,8 +4474,13 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
     if (!D.v1_lanes[var]) {
         // persistent grid = what is resident at the kernel's register / LDS budget (KETO_SLOTS overrides)
         int per_cu = 0, cus = 0;
-        if (ss)
+        if (ss && wide)
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, check_wave_kernel_wide<4, true>, 256, 0));
+        else if (ss)
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t0_stream_kernel(), 256, 0));
+        else if (wide && kind < 2)
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, kind == 0 ? check_wave_kernel_wide<4, false> : check_wave_kernel_wide<8, false>, 256, 0));
         else if (dw)
             HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, deep_wave_kernel<8, 8, false>, 256, 0));
         else if (kind == 2)
@@ -4576,7 +4623,8 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
                       }
                       HIP_OK(hipMemsetAsync(W.heads, 0, KETO_HEAD_WORDS * sizeof(uint32_t), st));
                       a.heads = W.heads;
-                      go(t0_stream_kernel());
+                      if (wide) go(check_wave_kernel_wide<4, true>);
+                      else go(t0_stream_kernel());
                   }
                   else if (level == 0 && kind < 2) {
                       a.dyn = t0_dyn(n, slots);
@@ -4591,6 +4639,7 @@ void check_core(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_t 
                           a.heads = W.heads;
                       }
                       if (var == VAR_W8) go(check_wave_kernel_w8<4, 4, 16>);
+                      else if (wide) kind == 0 ? go(check_wave_kernel_wide<4, false>) : go(check_wave_kernel_wide<8, false>);
                       else go(t0_kernel(var, dwork != nullptr));
                   }
                   else if (level == 0 && dw) {
@@ -4643,7 +4692,8 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
     const int32_t g = std::min<int32_t>(gmd, 65535);
     // (the reachability pretest's indexes keep handles in 31 bits: arenas whose roots lie past 2^31
     // units check deep batches without it)
-    const bool deep = n > 0 && g - 1 > 8 && S.part_mode != PART_MIGRATE && (uint64_t)D.n_units <= (uint64_t)EDGE_VAL;
+    const bool deep = n > 0 && g - 1 > 8 && S.part_mode != PART_MIGRATE && (uint64_t)D.n_units <= (uint64_t)EDGE_VAL &&
+                      D.root_g == 0;
     ItemWork iw;
     if (!deep || !reach_split(S, dq, n, gmd, da, dov.base, st, d_steps != nullptr, iw)) {
         check_core(S, D, dq, n, gmd, da, st, dov, work_out, accumulate, d_steps, stash, wsi, nullptr);

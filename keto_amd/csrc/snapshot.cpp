@@ -363,13 +363,29 @@ uint64_t arena_fit(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, ui
     return w;
 }
 
+uint64_t arena_fit_g(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, uint64_t& total, uint32_t g) {
+    // wide layouts: a header past word 2^33 sits on a multiple of 4 << g words from there (its handle
+    // counts such units, hword).  That alignment (>= 8 words, and 2^33 is line-aligned) already keeps
+    // header + window inside one line; the rest of the line rule gives way to it, the segment rule
+    // does not
+    const uint64_t x = arena_fit(w, table, cb, n_edges, total);
+    if (g == 0 || x + table + cb < TARGET_MAX_WORDS) return x;
+    const uint64_t a = 4ull << g, pre = table + cb;
+    const uint64_t fit = std::max(total, pre + HDR_WORDS + WINDOW_WORDS);
+    auto up = [&](uint64_t h) { return TARGET_MAX_WORDS + (std::max(h, TARGET_MAX_WORDS) - TARGET_MAX_WORDS + a - 1) / a * a; };
+    uint64_t h = up(w + pre);
+    if (((h - pre) >> 32) != ((h - pre + fit - 1) >> 32)) h = up(((((h - pre) >> 32) + 1) << 32) + pre);   // stay in a segment
+    return h - pre;
+}
+
 namespace {
 // The arena layout of one part: which rows it holds, where, and (PART_MIGRATE) its stubs.
 struct PartLayout {
     std::vector<uint32_t> unit_of_row, rows_by_unit, layout_units;
     std::vector<uint8_t> stub;
-    uint64_t n_units = 0, shared_words = 0, n_stubs = 0, hot_words = 0, hot_rows = 0;
+    uint64_t n_units = 0, n_words = 0, shared_words = 0, n_stubs = 0, hot_words = 0, hot_rows = 0;
     uint64_t tgt_tail = 0, tgt_end = 0, roots_at = 0;
+    uint32_t root_g = 0;
 };
 
 // hot_band (PART_MIGRATE): rows of in-degree band >= hot_band are kept on every part; sorted
@@ -450,6 +466,7 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
     uint64_t root_words = 0;
     for (uint64_t v : root_part) root_words += v;
     L.tgt_tail = L.tgt_end = L.roots_at = 0;
+    L.root_g = 0;
     // test hook: the target reserve's size in words (a small one fills after a few writes)
     const char* reserve_words = getenv("KETO_TEST_TGT_RESERVE");
     bool in_roots = false;
@@ -467,16 +484,30 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
                 L.tgt_end = std::min<uint64_t>(TARGET_MAX_WORDS, w + reserve);
                 L.roots_at = std::max<uint64_t>(L.tgt_end, root_base ? strtoull(root_base, nullptr, 0) & ~(uint64_t)(LINE_WORDS - 1) : 0);
                 w = L.roots_at;
+                // wide: the roots run past 64 GiB, so those past word 2^33 take handles in units of
+                // 16 << g bytes, the smallest g leaving an eighth of the handles for writes and
+                // overlays (root_words allows a line of alignment per root, >= 4 << g words)
+                // (test hook KETO_TEST_ROOT_G: at least this g, whatever the size)
+                const char* force_g = getenv("KETO_TEST_ROOT_G");
+                const uint64_t end = w + root_words;
+                if (end > NARROW_MAX_WORDS || force_g) {
+                    L.root_g = force_g ? std::max<uint32_t>(1, std::min<uint32_t>(ROOT_G_MAX, (uint32_t)atoi(force_g))) : 1;
+                    auto fits = [&](uint32_t g) {
+                        const uint64_t hu = end <= TARGET_MAX_WORDS ? 0 : (end - TARGET_MAX_WORDS + (4ull << g) - 1) >> (2 + g);
+                        return 0x80000000ull + hu + hu / 8 < HANDLE_MAX;
+                    };
+                    while (L.root_g < ROOT_G_MAX && !fits(L.root_g)) ++L.root_g;
+                }
             }
         }
         const uint32_t h = (uint32_t)(p >> 40) & 63u;
         const uint64_t table = h ? (1ull << h) : 0;
         const uint64_t cb = (p & P_CB) ? CB_WORDS : 0;              // closure filter
         uint64_t total = 0;
-        w = arena_fit(w, table, cb, p & ((1ull << 40) - 1), total);
-        const uint64_t unit = (w + table + cb) / HDR_WORDS;
+        w = arena_fit_g(w, table, cb, p & ((1ull << 40) - 1), total, L.root_g);
+        const uint64_t unit = handle_at_word(w + table + cb, L.root_g);
         if (!root || stub ? unit >= (uint64_t)EDGE_VAL : unit >= HANDLE_MAX)
-            throw Error{KETO_E_RANGE, root && !stub ? "device arena exceeds 2^32 16-byte units"
+            throw Error{KETO_E_RANGE, root && !stub ? "device arena exceeds the 2^32 handles (288 GiB)"
                                                     : "subject-set targets exceed 2^31 16-byte units"};
         L.layout_units[x] = (uint32_t)unit;
         if (!root && !stub) L.shared_words += total;
@@ -489,10 +520,12 @@ void layout_part(const Snapshot& S, const std::vector<uint8_t>& band, uint32_t p
     par_chunks(kept, th, 1 << 16, [&](uint64_t b, uint64_t e, unsigned) {
         for (uint64_t x = b; x < e; ++x) L.unit_of_row[L.rows_by_unit[x]] = L.layout_units[x];
     });
-    if (w > ARENA_MAX_WORDS) throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB)"};
+    if (w > (L.root_g ? ARENA_MAX_WORDS : NARROW_MAX_WORDS))
+        throw Error{KETO_E_RANGE, "device arena exceeds 2^34 words (64 GiB) in 16-byte handles"};
     if (mode == PART_MIGRATE && w > TARGET_MAX_WORDS)
         throw Error{KETO_E_RANGE, "a migrating part's arena exceeds 2^31 16-byte units"};
-    L.n_units = w / HDR_WORDS;
+    L.n_words = w;
+    L.n_units = handle_end(w, L.root_g);
 }
 }  // namespace
 
@@ -549,6 +582,8 @@ void compute_layout(Snapshot& S) {
     S.stub = std::move(L.stub);
     S.n_stubs = L.n_stubs;
     S.n_units = L.n_units;
+    S.n_words = L.n_words;
+    S.root_g = L.root_g;
     S.tgt_tail = L.tgt_tail;
     S.tgt_end = L.tgt_end;
     S.roots_at = L.roots_at;

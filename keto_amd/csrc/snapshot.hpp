@@ -70,9 +70,10 @@ constexpr uint32_t HDR_WORDS = 4;
 constexpr uint32_t WINDOW_WORDS = 4;            // edge words read together with the header
 constexpr uint32_t LINE_WORDS = 32;             // 128-B cache line
 constexpr uint32_t BUCKET_WORDS = 4;            // id tables are probed one 16-B bucket at a time
-// The arena is up to four segments of 2^32 words (16 GiB each, 64 GiB in all); no row (id table to
-// last edge) crosses from one to the next, so a position inside a row is a 32-bit word index within
-// its segment.  A handle (a 16-B unit, 32 bits) lies in segment handle >> SEG_SHIFT.
+// The arena is segments of 2^32 words (16 GiB each, up to four in a narrow layout, 64 GiB in all); no
+// row (id table to last edge) crosses from one to the next, so a position inside a row is a 32-bit
+// word index within its segment.  A narrow handle (a 16-B unit, 32 bits) lies in segment
+// handle >> SEG_SHIFT; a wide one in segment hword(handle, g) >> 32.
 //
 // Edges hold a subject set's handle in 31 bits, so every row some subject set points at (a
 // target) has a handle below 2^31 (the first 32 GiB); root rows -- rows no subject set points at,
@@ -82,9 +83,30 @@ constexpr uint32_t BUCKET_WORDS = 4;            // id tables are probed one 16-B
 // [0, tgt_tail) targets, [tgt_tail, tgt_end) reserve, [roots_at >= tgt_end, ...) roots).
 constexpr uint32_t SEG_SHIFT = 30;
 constexpr uint32_t SEG_MASK = (1u << SEG_SHIFT) - 1u;
-constexpr uint64_t ARENA_MAX_WORDS = 1ull << 34;
+constexpr uint64_t NARROW_MAX_WORDS = 1ull << 34;     // every handle a 16-B unit: up to 64 GiB
 constexpr uint64_t TARGET_MAX_WORDS = 1ull << 33;     // target rows' headers lie below this word
 constexpr uint32_t HANDLE_MAX = 0xFFFFFFF0u;          // handles (and overlay handles) stay below
+// Wide arenas (past 64 GiB, round 6): a handle below 2^31 is still a 16-B unit (every target, and the
+// roots laid out below word 2^33), but a handle h >= 2^31 names a root row whose header lies at word
+// 2^33 + ((h - 2^31) << (2 + g)): root rows past 32 GiB are addressed in units of 16 << g bytes (their
+// headers aligned so), g = Snapshot::root_g in 1..ROOT_G_MAX, the smallest that gives every root a
+// handle.  Only a request's own row (the top frame of a search, or a tree's root) is ever a root, so
+// only the request start decodes such a handle; g = 0 is the narrow layout (hword(h, 0) = 4 h).
+// Segments stay 2^32 words (no row crosses one); up to 18 of them.
+constexpr uint32_t ROOT_G_MAX = 3;
+constexpr uint64_t ARENA_MAX_WORDS = TARGET_MAX_WORDS + (1ull << (33 + ROOT_G_MAX));   // 288 GiB
+KETO_HD inline uint64_t hword(uint32_t h, uint32_t g) {
+    return h < 0x80000000u ? (uint64_t)h * 4u : TARGET_MAX_WORDS + ((uint64_t)(h - 0x80000000u) << (2u + g));
+}
+// the handle of a header at word w (w a multiple of 4 below 2^33, else of 4 << g past it)
+KETO_HD inline uint64_t handle_at_word(uint64_t w, uint32_t g) {
+    return w < TARGET_MAX_WORDS || g == 0 ? w / 4u : 0x80000000ull + ((w - TARGET_MAX_WORDS) >> (2u + g));
+}
+// the first handle past an arena of w words (every header of it has a smaller one)
+KETO_HD inline uint64_t handle_end(uint64_t w, uint32_t g) {
+    return w <= TARGET_MAX_WORDS || g == 0 ? (w + 3u) / 4u
+                                           : 0x80000000ull + ((w - TARGET_MAX_WORDS + (4ull << g) - 1u) >> (2u + g));
+}
 // header word 2: bits 0..7 flags, 8..12 hlog2, 13..31 bloom bits 32..50; word 3: bloom bits 0..31.
 // The 51-bit bloom filter (2 bits per subject id) summarizes the ids of a row with an id table,
 // so most absent ids are rejected with the header and the table is never probed for them.
@@ -322,7 +344,10 @@ struct Snapshot {
     // r is held by this device (owned, or on every part); stubs are not rows of this part
     bool present(uint32_t r) const { return unit_of_row[r] != NO_UNIT && (stub.empty() || !stub[r]); }
     bool mapped(uint32_t r) const { return unit_of_row[r] != NO_UNIT; }   // a row or a stub here
-    uint64_t n_units = 0;
+    uint64_t n_units = 0;                 // handle end: every row's handle is below (overlay handles start here)
+    uint64_t n_words = 0;                 // arena words laid out (== 4 n_units in a narrow layout)
+    uint32_t root_g = 0;                  // wide layouts: root handles past 2^31 count 16 << root_g bytes (hword)
+    uint64_t hdr_word(uint32_t h) const { return hword(h, root_g); }
     uint64_t shared_words = 0;            // arena words of the rows every part keeps (non-root rows)
     uint32_t handle(uint32_t row) const { return unit_of_row[row]; }
     int64_t row_of_handle(uint32_t unit) const;   // -1 if not a row header
@@ -487,6 +512,8 @@ void compute_layout(Snapshot& s);
 // row of `table` id-table words, `cb` closure-block words and n_edges edges keeps the line and
 // segment rules; total = the row's words from there
 uint64_t arena_fit(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, uint64_t& total);
+// the same, with a wide layout's header alignment past word 2^33 (root_g = g, see hword)
+uint64_t arena_fit_g(uint64_t w, uint64_t table, uint64_t cb, uint64_t n_edges, uint64_t& total, uint32_t g);
 // snapshot lifecycle (delta.cpp): apply an insert / delete transaction to the host tables
 // (TransactRelationTuples, internal/persistence/sql/relationtuples.go:289-297); throws KETO_E_REBUILD
 // for writes outside the delta path; device_apply then patches the device arena

@@ -4,6 +4,12 @@ roots from just below 3 x 2^32 words on, a ~48 GiB arena on the device whose gap
 the host); KETO_TEST_TGT_RESERVE shrinks the reserve for targets later writes add, so that a write
 overflows it and the snapshot lays its arena out afresh inside keto_snapshot_apply.
 
+Wide arenas (past 64 GiB, snapshot.hpp hword; round 6): the roots past word 2^33 take handles in
+units of 32, 64 or 128 B, and tier 0 keeps a root's segment (any of up to 18) in a register
+(check_wave_kernel_wide).  The same tests run on a wide layout at ~80 GiB (32-B units, roots in
+segments 4 and 5), at ~100 GiB (64-B units, segments 6 and 7) and at 48 GiB forced to 128-B units
+(KETO_TEST_ROOT_G), each a real device allocation of that size.
+
 Every decision and tree is compared with the oracle (or with the same graph in an ordinary layout):
 checks at max-depth 5 (tier 0), 9 (the 8-frame tier 0) and 16 (check_kernel; the reachability
 pretest is off past 2^31 units), subject-set requests naming root rows (handles past 2^31, never
@@ -18,30 +24,63 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT_BASE = 3 * (1 << 32) - (1 << 16)        # words: roots straddle segments 2 and 3
+# layout -> (KETO_TEST_ROOT_BASE in words, KETO_TEST_ROOT_G or None, root unit g, root segments)
+LAYOUTS = {
+    "split48": (ROOT_BASE, None, 0, (2, 3)),
+    "wide48_g3": (ROOT_BASE, 3, 3, (2, 3)),
+    "wide80": ((1 << 34) + (1 << 32) - (1 << 16), None, 1, (4, 5)),
+    "wide100": ((7 << 32) - (1 << 16), None, 2, (6, 7)),
+}
+
+
+def _env(layout):
+    base, force_g, _, _ = LAYOUTS[layout]
+    env = {"KETO_TEST_ROOT_BASE": str(base)}
+    if force_g is not None:
+        env["KETO_TEST_ROOT_G"] = str(force_g)
+    return env
+
+
+def hword(h, g):
+    h = np.asarray(h, dtype=np.uint64)
+    return np.where(h < (1 << 31), h * np.uint64(4), np.uint64(1 << 33) + ((h - np.uint64(1 << 31)) << np.uint64(2 + g)))
 
 
 @pytest.fixture(scope="module")
-def split():
+def graph():
     from tools import synth
     g = synth.SynthGraph(synth.scaled(synth.POWERLAW_1B, 1 / 4096), threads=16)
     plain = g.snapshot(device=0)
-    os.environ["KETO_TEST_ROOT_BASE"] = str(ROOT_BASE)
-    try:
-        snap = g.snapshot(device=0)
-    finally:
-        del os.environ["KETO_TEST_ROOT_BASE"]
-    yield g, snap, plain
-    snap.close()
+    yield g, plain
     plain.close()
     g.close()
 
 
+@pytest.fixture(scope="module", params=list(LAYOUTS))
+def split(request, graph):
+    g, plain = graph
+    env = _env(request.param)
+    os.environ.update(env)
+    try:
+        snap = g.snapshot(device=0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    snap.layout = request.param
+    yield g, snap, plain
+    snap.close()
+
+
 def test_split_layout_places_roots_high(split):
     g, snap, _ = split
+    _, _, rg, segs = LAYOUTS[snap.layout]
     h = snap.row_handles(np.arange(g.n_rows, dtype=np.uint32)).astype(np.int64)
     assert (h < (1 << 31)).any()                               # the targets
     assert (h >= (1 << 31)).mean() > 0.5                       # the roots
-    assert (h >= 3 << 30).any() and ((h >= 1 << 31) & (h < 3 << 30)).any()   # both segments 2 and 3
+    seg = hword(h[h >= (1 << 31)], rg) >> np.uint64(32)
+    assert set(np.unique(seg).tolist()) == set(segs)           # both segments
+    if rg:
+        assert snap.stats()["device_bytes"] > (LAYOUTS[snap.layout][0] * 4)
 
 
 @pytest.mark.parametrize("gmd", [5, 9, 16])
@@ -103,17 +142,20 @@ def test_split_expand_trees_equal_plain_layout(split):
         assert (np.asarray(x) == np.asarray(y)).all()
 
 
-@pytest.mark.parametrize("seed", range(10))
-def test_split_writes_interleaved_with_checks(seed, monkeypatch):
+@pytest.mark.parametrize("layout,seed", [(lay, s) for lay in ("split48", "wide48_g3", "wide80") for s in range(10)])
+def test_split_writes_interleaved_with_checks(layout, seed, monkeypatch):
     """Writes on a split layout whose target reserve holds a few rows: new targets fill it, then a
     write lays the arena out afresh (no KETO_E_REBUILD reaches the caller); every check and tree
-    after every write equals the SQL oracle's."""
+    after every write equals the SQL oracle's.  On a wide layout a target a write moves keeps its
+    content in the target reserve (tier 0 holds only the top row's segment): wide48_g3 seed 9 read
+    a moved target in a root segment through the top row's before that."""
     import keto_amd
     from oracle.oracle_sql import CheckEngine, ExpandEngine, NotFoundError, SQLStore
     from tests.engine_util import rows_from_tuples, subj
     from tests.randgraph import random_checks, random_expands, random_graph
     from tests.test_gpu_lifecycle import _random_write, _row
-    monkeypatch.setenv("KETO_TEST_ROOT_BASE", str(ROOT_BASE))
+    for k, v in _env(layout).items():
+        monkeypatch.setenv(k, v)
     monkeypatch.setenv("KETO_TEST_TGT_RESERVE", "256")
     ns, tuples, raw, ps, alph = random_graph(seed + 900, wide=seed % 3 == 2, allow_poison=False,
                                              allow_collisions=seed % 2 == 0)

@@ -119,7 +119,7 @@ def test_multi_gpu_server_process():
     assert re.search(r"func PlanParts\(base \*Snapshot, devices \[\]int\) \(\[\]int, error\)", part)
     assert "plan[k] = devices[k%len(devices)]" in part and "NewPartition(base, plan)" in part
     hdr = open(os.path.join(ROOT, "include", "keto_mi355x.h")).read()
-    assert re.search(r"#define KETO_ARENA_MAX_BYTES \(64ull << 30\)", hdr)
+    assert re.search(r"#define KETO_ARENA_MAX_BYTES \(288ull << 30\)", hdr)
     bat = _code(open(os.path.join(GO, "internal", "gpu", "batcher.go")).read())
     assert re.search(r"func NewBatcher\(snaps \[\]Engine,", bat)
     assert re.search(r"func NewExpandBatcher\(snaps \[\]Engine,", bat)
