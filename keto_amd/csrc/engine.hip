@@ -1267,11 +1267,11 @@ __device__ __forceinline__ void
             hdr_w = in_ov ? (eh - ov.base) * HDR_WORDS : (uint32_t)hw;
         } else {
             seg = in_ov ? 0u : hdr ? (eh >> SEG_SHIFT) : c_seg(c);
-            hdr_w = (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS;
+            hdr_w = 0;                                            // (the narrow form below, as before)
         }
         const uint32_t* const ar = (in_ov ? ov.arena : s.arena) + ((uint64_t)seg << 32);
         const uint32_t hl = bf(c, C_HL, 5);
-        const uint32_t word = hdr ? hdr_w
+        const uint32_t word = hdr ? (WIDE ? hdr_w : (in_ov ? eh - ov.base : eh & SEG_MASK) * HDR_WORDS)
                                   : ph == P_IDQ ? pos - HDR_WORDS - ((c & C_CB) ? CB_WORDS : 0u) - (1u << hl) +
                                                       eh * BUCKET_WORDS
                                                 : (pos & ~3u);
