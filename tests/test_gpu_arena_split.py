@@ -195,3 +195,44 @@ def test_split_writes_interleaved_with_checks(layout, seed, monkeypatch):
                     want = ("error", None)
                 assert ({0: "tree", 1: "nil", 2: "error"}[st], js) == want, (seed, step, s, d, gm)
     snap.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("seed", range(4100, 4106))
+def test_wide_shared_parts_routed(P, seed, monkeypatch):
+    """Shared-rows parts whose arenas are wide (32 GiB, 128-B root units), P ranks of the local
+    transport on the one GPU: each rank's named batch is routed to the parts owning its rows and
+    checked on their wide arenas; every decision equals the replicated snapshot's and the SQL
+    oracle's (internal/check/engine.go:36-123)."""
+    import keto_amd
+    from keto_amd.capi import PART_SHARED
+    from oracle.oracle_sql import CheckEngine
+    from tests.test_gpu_comm import _local_comms, _ok, _ranks, _reqs
+    from tests.engine_util import rows_from_tuples
+    from tests.randgraph import random_store
+    monkeypatch.setenv("KETO_COMM_TIMEOUT_MS", "60000")
+    store, ns, tuples, raw, ps, alph = random_store(seed)
+    rows = rows_from_tuples(ns, tuples, raw)
+    full = keto_amd.Snapshot.build(ns, rows, page_size=ps, device=0)
+    reqs, checks = _reqs(seed, alph)
+    g = 5
+    want, want_st = full.check_batch(reqs, g)
+    for (t, d, _), a in zip(checks, want):
+        assert bool(a) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, t, d)
+    # roots from just past word 2^33 in 128-B units: ~32 GiB per part (the module's wide100 arena may
+    # still be held)
+    monkeypatch.setenv("KETO_TEST_ROOT_BASE", str((1 << 33) + (1 << 20)))
+    monkeypatch.setenv("KETO_TEST_ROOT_G", "3")
+    parts = [keto_amd.Snapshot.build(ns, rows, page_size=ps, device=-1).upload_part(r, P, 0, mode=PART_SHARED)
+             for r in range(P)]
+    comms = _local_comms(P)
+    mine = [list(range(r, len(reqs), P)) for r in range(P)]
+    res = _ok(_ranks(P, lambda r: comms[r].check_batch_routed(parts[r], [reqs[i] for i in mine[r]], g)))
+    for r, (got, st) in enumerate(res):
+        for k, i in enumerate(mine[r]):
+            assert got[k] == want[i] and st[k] == want_st[i], (seed, P, r, reqs[i])
+    for c in comms:
+        c.close()
+    for p in parts:
+        p.close()
+    full.close()
