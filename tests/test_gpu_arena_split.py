@@ -236,3 +236,44 @@ def test_wide_shared_parts_routed(P, seed, monkeypatch):
     for p in parts:
         p.close()
     full.close()
+
+
+@pytest.mark.parametrize("layout", ["wide48_g3", "wide80"])
+@pytest.mark.parametrize("seed", range(4600, 4606))
+def test_wide_packed_and_device_proto(layout, seed, monkeypatch):
+    """The Go shim's calls on a wide arena: packed string batches resolved on the GPU (the in-flight
+    path that enqueues tier 0 alone on its own stream, check_wave_kernel_wide), named batches, and
+    expand trees with their SubjectTree bytes encoded on the device -- each equal to the same graph
+    in the narrow layout and to the SQL oracle (internal/check/engine.go:36-123,
+    internal/expand/engine.go:33-102)."""
+    import keto_amd
+    from keto_amd.capi import pack_requests
+    from oracle.oracle_sql import CheckEngine
+    from tests.engine_util import rows_from_tuples, subj
+    from tests.randgraph import random_expands, random_store
+    from tests.test_gpu_comm import _reqs
+    store, ns, tuples, raw, ps, alph = random_store(seed)
+    rows = rows_from_tuples(ns, tuples, raw)
+    plain = keto_amd.Snapshot.build(ns, rows, page_size=ps, device=0)
+    for k, v in _env(layout).items():
+        monkeypatch.setenv(k, v)
+    wide = keto_amd.Snapshot.build(ns, rows, page_size=ps, device=0)
+    reqs, checks = _reqs(seed, alph)
+    for g in (3, 5, 12):
+        want, want_st = plain.check_batch(reqs, g)
+        got, st = wide.check_batch(reqs, g)
+        assert (got == want).all() and (st == want_st).all(), (seed, g)
+        blob, pk = pack_requests(reqs)
+        got_p, st_p = wide.check_batch_packed(blob, pk, g)
+        assert (got_p == want).all() and (st_p == want_st).all(), (seed, g)
+        if g == 5:
+            for (t, d, _), a in zip(checks, got):
+                assert bool(a) == CheckEngine(store, g).subject_is_allowed(t, d), (seed, t, d)
+    exps = random_expands(seed, alph, k=24)
+    er = [(subj(s), d) for s, d, _ in exps]
+    a, pa = plain.expand_batch(er, 5, proto_all="host")
+    b, pb = wide.expand_batch(er, 5, proto_all="device")
+    assert [x[:2] for x in a] == [x[:2] for x in b]
+    assert pa == pb
+    wide.close()
+    plain.close()
