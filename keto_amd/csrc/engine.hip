@@ -2611,12 +2611,14 @@ __global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict_
                                                      const keto_tree_node* __restrict__ stage,
                                                      const uint64_t* __restrict__ stage_pos,
                                                      const uint64_t* __restrict__ offset, uint32_t n,
-                                                     const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
+                                                     const uint32_t* __restrict__ unit_row, uint32_t ov_units_base,
+                                                     uint64_t big) {
     const uint32_t gl = threadIdx.x & 15u;
     const uint32_t groups = gridDim.x * (blockDim.x >> 4);
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; i < n; i += groups) {
         const uint64_t sp = stage_pos[i], b = offset[i], e = offset[i + 1];
-        if (sp >= SPLIT_POS) continue;                      // not staged, or in two pieces (copy_stage_pieces)
+        // not staged, in two pieces, or bigger than `big` nodes: copy_stage_pieces, a wave per piece
+        if (sp >= SPLIT_POS || e - b > big) continue;
         for (uint64_t k = gl; k < e - b; k += 16) {
             keto_tree_node v = stage[sp + k];
             if (unit_row && (v.subject & EDGE_SET) && (v.subject & EDGE_VAL) < ov_units_base)
@@ -2626,7 +2628,8 @@ __global__ void __launch_bounds__(256) gather_staged(keto_tree_node* __restrict_
     }
 }
 
-// The staged trees in two pieces (StageSeg): each piece of at most 2048 nodes {source in the staging
+// The staged trees in two pieces (StageSeg), and the single-piece ones past the gather's size bound:
+// each piece of at most GPIECE (512) nodes {source in the staging
 // pool, destination in the node arena, length} copied by one wave, set handles turned into row ids on
 // the way as in gather_staged (unit_row != NULL)
 __global__ void __launch_bounds__(256) copy_stage_pieces(keto_tree_node* __restrict__ nodes,
@@ -2673,21 +2676,34 @@ __global__ void __launch_bounds__(256) copy_lane_runs(const CopyRun* __restrict_
         const uint32_t total = __shfl(incl, G - 1, G);
         const uint32_t excl = incl - len;
         const uint64_t src = (uint64_t)c.src, dst = (uint64_t)c.dst;
-        for (uint32_t base = 0; base < total; base += G) {      // every thread takes part in the shuffles
-            const uint32_t f = base + (uint32_t)t;
-            int j = 0;
-            for (int step = G / 2; step > 0; step >>= 1) {
-                const uint32_t ev = __shfl(excl, j + step < G ? j + step : G - 1, G);
-                if ((uint32_t)(j + step) < m && ev <= f) j += step;
+        // U ids per thread per round, their loads in flight together (a lane's runs of up to 32K ids
+        // are copied in rounds of U x 32, not 32)
+        constexpr int U = 4;
+        for (uint32_t base = 0; base < total; base += U * G) {  // every thread takes part in the shuffles
+            uint32_t val[U];
+            keto_tree_node* dps[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t f = base + (uint32_t)(u * G + t);
+                int j = 0;
+                for (int step = G / 2; step > 0; step >>= 1) {
+                    const uint32_t ev = __shfl(excl, j + step < G ? j + step : G - 1, G);
+                    if ((uint32_t)(j + step) < m && ev <= f) j += step;
+                }
+                const uint32_t ej = __shfl(excl, j, G);
+                const uint32_t slo = __shfl((uint32_t)src, j, G), shi = __shfl((uint32_t)(src >> 32), j, G);
+                const uint32_t dlo = __shfl((uint32_t)dst, j, G), dhi = __shfl((uint32_t)(dst >> 32), j, G);
+                dps[u] = nullptr;
+                val[u] = 0;
+                if (f < total) {
+                    const uint32_t* sp = reinterpret_cast<const uint32_t*>(((uint64_t)shi << 32) | slo);
+                    dps[u] = reinterpret_cast<keto_tree_node*>(((uint64_t)dhi << 32) | dlo) + (f - ej);
+                    val[u] = sp[f - ej];
+                }
             }
-            const uint32_t ej = __shfl(excl, j, G);
-            const uint32_t slo = __shfl((uint32_t)src, j, G), shi = __shfl((uint32_t)(src >> 32), j, G);
-            const uint32_t dlo = __shfl((uint32_t)dst, j, G), dhi = __shfl((uint32_t)(dst >> 32), j, G);
-            if (f < total) {
-                const uint32_t* sp = reinterpret_cast<const uint32_t*>(((uint64_t)shi << 32) | slo);
-                keto_tree_node* dp = reinterpret_cast<keto_tree_node*>(((uint64_t)dhi << 32) | dlo);
-                dp[f - ej] = keto_tree_node{sp[f - ej], 0x80000000u};
-            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (dps[u]) *dps[u] = keto_tree_node{val[u], 0x80000000u};
         }
     }
 }
@@ -5771,9 +5787,16 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std:
     // the translation over just their ranges.  (Round 3's fused version, a wave per tree, waited its
     // lanes' map loads one after another: 2.5x slower than a pass of its own.)
     const bool fuse = staged && D.unit_row;
+    // a staged tree of more than `gbig` nodes goes to copy_stage_pieces in pieces of at most GPIECE
+    // (a wave each) instead of one 16-lane group, whose copy of the biggest trees set the gather's
+    // time (KETO_EXPAND_GATHER_BIG: the threshold, 0 = every single-piece tree in the gather)
+    constexpr uint64_t GPIECE = 512;
+    const char* gbe = getenv("KETO_EXPAND_GATHER_BIG");
+    const uint64_t gbig = gbe ? (atoll(gbe) > 0 ? (uint64_t)atoll(gbe) : ~0ull) : 256u;
     if (staged)
         hipLaunchKernelGGL(gather_staged, dim3(copy_blocks((n + 15) / 16)), dim3(256), 0, st,
-                           D.ex_nodes, D.ex_stage, dstage, doff, n, fuse ? D.unit_row : nullptr, (uint32_t)S.n_units);
+                           D.ex_nodes, D.ex_stage, dstage, doff, n, fuse ? D.unit_row : nullptr, (uint32_t)S.n_units,
+                           gbig);
     HIP_OK(hipGetLastError());
     // staged trees in two pieces (a region, then an overflow chunk): copied piece by piece
     std::vector<uint64_t> pc;                          // (alive until the stream is synchronized below)
@@ -5784,12 +5807,17 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std:
         n_split = std::min<uint32_t>(ns_, D.ex_seg_cap);
         const StageSeg* sgs = reinterpret_cast<const StageSeg*>(segbuf.data() + 16);
         auto piece = [&](uint64_t src, uint64_t dst, uint64_t len) {
-            for (uint64_t b = 0; b < len; b += 2048) {
+            for (uint64_t b = 0; b < len; b += GPIECE) {
                 pc.push_back(src + b);
                 pc.push_back(dst + b);
-                pc.push_back(std::min<uint64_t>(2048, len - b));
+                pc.push_back(std::min<uint64_t>(GPIECE, len - b));
             }
         };
+        if (gbig != ~0ull)
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint64_t b = out.offset[i], len = out.offset[i + 1] - b;
+                if (spos[i] < SPLIT_POS && len > gbig) piece(spos[i], b, len);
+            }
         for (uint32_t k = 0; k < n_split; ++k) {
             const StageSeg& g = sgs[k];
             if (g.root >= n || spos[g.root] != (SPLIT_POS | k)) continue;   // (a record of another call)
