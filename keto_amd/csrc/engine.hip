@@ -1993,8 +1993,13 @@ __global__ void __launch_bounds__(256, KETO_WAVE_WAVES)
 constexpr uint32_t RUN_INLINE_DEFAULT = 0;
 constexpr uint32_t RUNS_PER_LANE = 32;
 // a run longer than BIG_RUN ids goes to a shared queue instead, cut into BIG_RUN-id pieces that
-// different waves copy (one atomic per big run: rare, and small next to the copy it saves)
-constexpr uint32_t BIG_RUN = 1024;
+// different waves copy (one atomic per big run: rare, and small next to the copy it saves).  256
+// instead of 1024 made config #5's stage pass 178 -> 612 us (the queue's claims contend),
+// profiles/r06zg_expand_big_run_256_rejected.log
+#ifndef KETO_BIG_RUN
+#define KETO_BIG_RUN 1024
+#endif
+constexpr uint32_t BIG_RUN = KETO_BIG_RUN;
 struct CopyRun {
     const uint32_t* src;     // the ids
     keto_tree_node* dst;     // their leaf nodes
