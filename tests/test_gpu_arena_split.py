@@ -277,3 +277,59 @@ def test_wide_packed_and_device_proto(layout, seed, monkeypatch):
     assert pa == pb
     wide.close()
     plain.close()
+
+
+@pytest.mark.parametrize("seed", range(4700, 4704))
+def test_wide_after_writes_clone_and_persist(seed, monkeypatch, tmp_path):
+    """A wide snapshot (32 GiB, 128-B root units) after writes, then cloned and saved / loaded (both
+    lay the arena out afresh, wide again): every copy decides and expands like the narrow snapshot at
+    the same version and like the SQL oracle."""
+    import keto_amd
+    from oracle.oracle_sql import CheckEngine, SQLStore
+    from tests.engine_util import rows_from_tuples, subj
+    from tests.randgraph import random_expands, random_graph
+    from tests.test_gpu_comm import _reqs
+    from tests.test_gpu_lifecycle import _random_write, _row
+    ns, tuples, raw, ps, alph = random_graph(seed, allow_poison=False, allow_collisions=seed % 2 == 0)
+    names, objs, rels, users = alph
+    names = [n for n in names if n]
+    if not names:
+        pytest.skip("only a namespace named ''")
+    store = SQLStore(ns, tuples, page_size=ps)
+    plain = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), page_size=ps, device=0)
+    # roots from just past word 2^33 in 128-B units: three ~32 GiB copies (the module's wide100 arena
+    # may still be held)
+    monkeypatch.setenv("KETO_TEST_ROOT_BASE", str((1 << 33) + (1 << 20)))
+    monkeypatch.setenv("KETO_TEST_ROOT_G", "3")
+    wide = keto_amd.Snapshot.build(ns, rows_from_tuples(ns, tuples), page_size=ps, device=0)
+    rng = random.Random(seed)
+    for _ in range(4):
+        ins = [_random_write(rng, names, objs, rels, users) for _ in range(rng.randint(1, 10))]
+        cur = store.tuples()
+        dels = [rng.choice(cur) for _ in range(rng.randint(0, 2))] if cur else []
+        for snap in (plain, wide):
+            snap.apply([_row(ns, t) for t in ins], [_row(ns, t) for t in dels])
+        for t in ins:
+            store.insert(t)
+        for t in dels:
+            store.delete(t)
+    clone = wide.clone(0)
+    path = str(tmp_path / "wide.snap")
+    wide.save(path, tag=seed)
+    loaded, tag = keto_amd.Snapshot.load(path, device=0)
+    assert tag == seed
+    reqs, checks = _reqs(seed, (names, objs, rels, users))
+    want, want_st = plain.check_batch(reqs, 5)
+    for (t, d, _), a in zip(checks, want):
+        assert bool(a) == CheckEngine(store, 5).subject_is_allowed(t, d), (seed, t, d)
+    exps = random_expands(seed, (names, objs, rels, users), k=16)
+    er = [(subj(s), d) for s, d, _ in exps]
+    want_t = [x[:2] for x in plain.expand_batch(er, 5)]
+    for name, snap in (("wide", wide), ("clone", clone), ("loaded", loaded)):
+        got, st = snap.check_batch(reqs, 5)
+        assert (got == want).all() and (st == want_st).all(), (seed, name)
+        assert [x[:2] for x in snap.expand_batch(er, 5)] == want_t, (seed, name)
+    h = loaded.row_handles(np.arange(loaded.stats()["n_rows"], dtype=np.uint32)).astype(np.int64)
+    assert (h >= (1 << 31)).any()                              # laid out wide again
+    for snap in (loaded, clone, wide, plain):
+        snap.close()
