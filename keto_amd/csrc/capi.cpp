@@ -904,7 +904,7 @@ void expand_named(Snapshot& S, const keto_expand_req* reqs, uint32_t n, int32_t 
     ov.base = S.n_rows();
     a->ov_base = ov.base;
     a->extra_base = (uint32_t)S.strs.size();
-    std::vector<uint32_t> root(n), flags(n), vid(n, 0);
+    std::vector<uint32_t> root(n), flags(n), vid(n, 0), rrow(n, KETO_NO_ROW);
     std::vector<int32_t> depth(n);
     std::vector<uint8_t> not_found(n, 0);
     std::vector<std::pair<uint32_t, uint32_t>> remote;                  // (request, row) of other parts
@@ -949,10 +949,11 @@ void expand_named(Snapshot& S, const keto_expand_req* reqs, uint32_t n, int32_t 
         } else {
             root[i] = S.handle((uint32_t)r);
             vid[i] = S.vid_of_row((uint32_t)r);
+            rrow[i] = (uint32_t)r;
         }
     }
     a->ov_keys = ov.keys;
-    device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r, &remote);
+    device_expand(S, root, flags, vid, depth, global_max_depth, &ov, a->r, &remote, &rrow);
     for (uint32_t i = 0; i < n; ++i)
         if (not_found[i]) a->r.status[i] = KETO_EXPAND_NOT_FOUND;
 }
@@ -981,7 +982,7 @@ int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t
         Snapshot& S = *h->s;
         auto a = std::make_unique<keto_tree_arena>();
         a->extra_base = (uint32_t)S.strs.size();
-        std::vector<uint32_t> root(n), flags(n), vid(n, 0);
+        std::vector<uint32_t> root(n), flags(n), vid(n, 0), rrow(n, KETO_NO_ROW);
         std::vector<int32_t> depth(max_depth, max_depth + n);
         for (uint32_t i = 0; i < n; ++i) {
             const bool set = (roots[i] & EDGE_SET) != 0;
@@ -991,10 +992,11 @@ int keto_expand_batch_ids(keto_snapshot* h, const uint32_t* roots, const int32_t
                 if (root[i] >= S.n_rows()) throw Error{KETO_E_INVALID, "root row out of range"};
                 if (!S.present(root[i])) throw Error{KETO_E_INVALID, "expand root is owned by another part"};
                 vid[i] = S.vid_of_row(root[i]);
+                rrow[i] = root[i];
                 root[i] = S.handle(root[i]);
             }
         }
-        device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, a->r);
+        device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, a->r, nullptr, &rrow);
         *out = a.release();
         return KETO_OK;
     });

@@ -1053,17 +1053,18 @@ int keto_expand_batch_routed(keto_comm* c, keto_snapshot* h, const keto_expand_r
             if (!m) return;
             injected(*c, "owner");
             Snapshot& S = *Sp;
-            std::vector<uint32_t> root(m), flags(m, 1u), vid(m);
+            std::vector<uint32_t> root(m), flags(m, 1u), vid(m), rrow(m);
             std::vector<int32_t> depth(m);
             for (uint64_t k = 0; k < m; ++k) {
                 const uint32_t r = (uint32_t)got[k];
                 if (r >= S.n_rows() || !S.present(r)) throw Error{KETO_E_INVALID, "a routed expand root is not on its owner part"};
                 root[k] = S.handle(r);
                 vid[k] = S.vid_of_row(r);
+                rrow[k] = r;
                 depth[k] = (int32_t)(uint32_t)(got[k] >> 32);
             }
             ExpandResult er;
-            device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, er);
+            device_expand(S, root, flags, vid, depth, global_max_depth, nullptr, er, nullptr, &rrow);
             uint64_t k = 0;
             for (int p = 0; p < P; ++p) {
                 const uint64_t w0 = pack.size();

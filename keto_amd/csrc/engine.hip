@@ -2783,7 +2783,7 @@ struct DeviceState {
     uint32_t* row_handle = nullptr;   // row id -> handle (NO_UNIT: another part's root row), lazily
     uint32_t* layout_units = nullptr; // handles in arena order (increasing) and their rows, lazily:
     uint32_t* rows_by_unit = nullptr; //   expand output handle -> row id on the device
-    uint32_t* unit_row = nullptr;     // handle -> row id, direct (n_units entries; lazily, when <= 8 GiB)
+    uint32_t* unit_row = nullptr;     // handle -> row id, direct (handles below min(n_units, 2^31); lazily)
     uint64_t row_handle_cap = 0;      // entries allocated (a write patches the maps in place while its rows fit)
     uint64_t row_handle_rows = 0;     // entries written (rows below it hold their handle or NO_UNIT)
     uint64_t unit_row_cap = 0;
@@ -3772,7 +3772,8 @@ bool apply_in_place(Snapshot& S) {
     if (!fresh.empty() || grew) {
         const bool rh_ok = D.row_handle && S.n_rows() <= D.row_handle_cap &&
                            fresh.size() + (S.n_rows() - D.row_handle_rows) <= (1u << 20);
-        const bool ur_ok = D.unit_row && S.n_units <= D.unit_row_cap && fresh.size() <= (1u << 20);
+        const bool ur_ok = D.unit_row && std::min<uint64_t>(S.n_units, 1ull << 31) <= D.unit_row_cap &&
+                           fresh.size() <= (1u << 20);
         if (D.row_handle && !rh_ok) {
             (void)hipFree(D.row_handle);
             D.row_handle = nullptr;
@@ -3791,7 +3792,7 @@ bool apply_in_place(Snapshot& S) {
                 rh.push_back(r);
                 rh.push_back(S.unit_of_row[r]);
             }
-            if (ur_ok) {
+            if (ur_ok && S.unit_of_row[r] < D.unit_row_cap) {     // (a root past 2^31: never translated)
                 hr.push_back(S.unit_of_row[r]);
                 hr.push_back(r);
             }
@@ -5277,9 +5278,9 @@ const uint32_t* device_row_handle_map(Snapshot& S) {
 // the arena-order handle list; overlay handles >= ov_units_base are left for the host).
 // the direct handle -> row map: every row header's unit gets its row (other units are never looked up)
 __global__ void __launch_bounds__(256) scatter_unit_rows(uint32_t* __restrict__ unit_row, const uint32_t* __restrict__ units,
-                                                         const uint32_t* __restrict__ rows, uint32_t n) {
+                                                         const uint32_t* __restrict__ rows, uint32_t n, uint32_t cap) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) unit_row[units[i]] = rows[i];
+    if (i < n && units[i] < cap) unit_row[units[i]] = rows[i];
 }
 __global__ void __launch_bounds__(256) handles_to_rows_direct(keto_tree_node* __restrict__ nodes, uint64_t n,
                                                               const uint32_t* __restrict__ unit_row, uint32_t ov_units_base) {
@@ -5305,15 +5306,6 @@ __global__ void __launch_bounds__(256) handles_to_rows_ranges(keto_tree_node* __
             if ((x & EDGE_SET) && (x & EDGE_VAL) < ov_units_base) nodes[i].subject = EDGE_SET | unit_row[x & EDGE_VAL];
         }
     }
-}
-// arenas with root rows past 2^31 units: a tree's root node lost its handle's bit 31 to EDGE_SET, so
-// it takes its row from the request (overlay roots: the host, below)
-__global__ void __launch_bounds__(256) root_rows_of_trees(keto_tree_node* __restrict__ nodes, const uint64_t* __restrict__ off,
-                                                          const ExpandReq* __restrict__ q, const uint32_t* __restrict__ unit_row,
-                                                          uint32_t n, uint32_t n_units) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !(q[i].flags & 1u) || off[i + 1] == off[i] || q[i].root >= n_units) return;
-    nodes[off[i]].subject = EDGE_SET | unit_row[q[i].root];
 }
 __global__ void __launch_bounds__(256) handles_to_rows(keto_tree_node* __restrict__ nodes, uint64_t n,
                                                        const uint32_t* __restrict__ units, const uint32_t* __restrict__ rows,
@@ -5399,8 +5391,11 @@ void pinned_give(void* p) noexcept {
 void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std::vector<uint32_t>& root_flags,
                    const std::vector<uint32_t>& root_vid_in, const std::vector<int32_t>& depth, int32_t gmd,
                    const Overlay* ovh, ExpandResult& out,
-                   const std::vector<std::pair<uint32_t, uint32_t>>* remote_roots) {
+                   const std::vector<std::pair<uint32_t, uint32_t>>* remote_roots,
+                   const std::vector<uint32_t>* root_rows) {
     if (!S.dev) throw Error{KETO_E_HIP, "snapshot has no device copy"};
+    if (S.n_units > (uint64_t)EDGE_VAL && (!root_rows || root_rows->size() != root_in.size()))
+        throw Error{KETO_E_INVALID, "expand over an arena whose roots lie past 2^31 units needs the roots' row ids"};
     // a migrating part holds its own rows and stubs for the others' rows it points at: the rows a
     // tree needs from other parts are copied into the call's overlay (PullSet) from the host tables,
     // which every part holds whole
@@ -5765,15 +5760,17 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std:
                          hipMemcpyHostToDevice));
         // the direct map (one word per arena unit) when it is small next to the arena; else the
         // handle -> row translation binary-searches the handle list
-        if (S.n_units && S.n_units <= (1ull << 32)) {
-            D.unit_row_cap = std::min<uint64_t>(1ull << 32, S.n_units + S.n_units / 64 + 4096);
+        // (only handles below 2^31 are translated -- a set node keeps 31 bits, and a tree's root past
+        // them takes its row from the request -- so the map stops there: <= 8 GiB)
+        if (S.n_units) {
+            D.unit_row_cap = std::min<uint64_t>(1ull << 31, S.n_units + S.n_units / 64 + 4096);
             D.unit_row = dmalloc<uint32_t>(D.unit_row_cap, acc);
             // units that start no row (and the slack) read NO_UNIT, never a stale row id
             HIP_OK(hipMemsetAsync(D.unit_row, 0xFF, D.unit_row_cap * sizeof(uint32_t), st));
             const uint32_t m32 = (uint32_t)S.layout_units.size();
             if (m32)
                 hipLaunchKernelGGL(scatter_unit_rows, dim3((m32 + 255) / 256), dim3(256), 0, st, D.unit_row,
-                                   D.layout_units, D.rows_by_unit, m32);
+                                   D.layout_units, D.rows_by_unit, m32, (uint32_t)D.unit_row_cap);
             HIP_OK(hipGetLastError());
         }
     }
@@ -5876,16 +5873,16 @@ void device_expand(Snapshot& S, const std::vector<uint32_t>& root_in, const std:
                            D.layout_units, D.rows_by_unit, (uint32_t)S.layout_units.size(), (uint32_t)S.n_units);
     HIP_OK(hipGetLastError());
     const bool high_roots = S.n_units > (uint64_t)EDGE_VAL;
-    if (high_roots) {
-        if (!D.unit_row) throw Error{KETO_E_RANGE, "expand over an arena past 2^31 units needs the direct unit map"};
-        hipLaunchKernelGGL(root_rows_of_trees, dim3((n + 255) / 256), dim3(256), 0, st, D.ex_nodes, doff, dq, D.unit_row,
-                           n, (uint32_t)S.n_units);
-        HIP_OK(hipGetLastError());
-    }
     lap("h2rows");
     HIP_OK(hipMemcpyAsync(out.nodes.data(), D.ex_nodes, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     lap("d2h");
+    // arenas with root rows past 2^31 units: a tree's root node lost its handle's bit 31 to EDGE_SET,
+    // so it takes its row from the request (overlay roots: below)
+    if (high_roots)
+        for (uint32_t i = 0; i < n; ++i)
+            if (root_flags[i] && out.offset[i + 1] > out.offset[i] && root[i] >= EDGE_VAL && root[i] < S.n_units)
+                out.nodes[out.offset[i]].subject = EDGE_SET | (*root_rows)[i];
     {
         float ms = 0;
         if (hipEventElapsedTime(&ms, D.ex_ev[2], D.ex_ev[3]) == hipSuccess) extra_ms += ms;

@@ -693,10 +693,13 @@ struct ExpandResult {
 };
 // roots: row handles (root_flags bit0 = subject set) or string ids; out.nodes carry row ids.  On a
 // migrating part, remote_roots lists the roots (index, row id) whose rows this part does not hold
-// (their root / vid entries are ignored)
+// (their root / vid entries are ignored).  root_rows: each subject-set root's row id (any other
+// entry ignored), which an arena whose roots lie past 2^31 units needs: such a root's handle does
+// not fit a tree node, so its node takes the row from here
 void device_expand(Snapshot& s, const std::vector<uint32_t>& root, const std::vector<uint32_t>& root_flags,
                    const std::vector<uint32_t>& root_vid, const std::vector<int32_t>& depth, int32_t gmd,
                    const Overlay* ov, ExpandResult& out,
-                   const std::vector<std::pair<uint32_t, uint32_t>>* remote_roots = nullptr);
+                   const std::vector<std::pair<uint32_t, uint32_t>>* remote_roots = nullptr,
+                   const std::vector<uint32_t>* root_rows = nullptr);
 
 }  // namespace keto
