@@ -142,7 +142,10 @@ def test_split_expand_trees_equal_plain_layout(split):
         assert (np.asarray(x) == np.asarray(y)).all()
 
 
-@pytest.mark.parametrize("layout,seed", [(lay, s) for lay in ("split48", "wide48_g3", "wide80") for s in range(10)])
+# (the wide layouts' seeds are fewer: each build allocates their full arena; wide48_g3 seed 9 is the
+# moved-target case below)
+@pytest.mark.parametrize("layout,seed", [("split48", s) for s in range(10)] + [("wide48_g3", s) for s in (5, 7, 9)] +
+                         [("wide80", s) for s in (0, 4, 8)])
 def test_split_writes_interleaved_with_checks(layout, seed, monkeypatch):
     """Writes on a split layout whose target reserve holds a few rows: new targets fill it, then a
     write lays the arena out afresh (no KETO_E_REBUILD reaches the caller); every check and tree
@@ -198,7 +201,7 @@ def test_split_writes_interleaved_with_checks(layout, seed, monkeypatch):
 
 
 @pytest.mark.parametrize("P", [2, 3])
-@pytest.mark.parametrize("seed", range(4100, 4106))
+@pytest.mark.parametrize("seed", range(4100, 4103))
 def test_wide_shared_parts_routed(P, seed, monkeypatch):
     """Shared-rows parts whose arenas are wide (32 GiB, 128-B root units), P ranks of the local
     transport on the one GPU: each rank's named batch is routed to the parts owning its rows and
@@ -238,8 +241,7 @@ def test_wide_shared_parts_routed(P, seed, monkeypatch):
     full.close()
 
 
-@pytest.mark.parametrize("layout", ["wide48_g3", "wide80"])
-@pytest.mark.parametrize("seed", range(4600, 4606))
+@pytest.mark.parametrize("layout,seed", [("wide48_g3", s) for s in range(4600, 4604)] + [("wide80", 4604)])
 def test_wide_packed_and_device_proto(layout, seed, monkeypatch):
     """The Go shim's calls on a wide arena: packed string batches resolved on the GPU (the in-flight
     path that enqueues tier 0 alone on its own stream, check_wave_kernel_wide), named batches, and
@@ -279,7 +281,7 @@ def test_wide_packed_and_device_proto(layout, seed, monkeypatch):
     plain.close()
 
 
-@pytest.mark.parametrize("seed", range(4700, 4704))
+@pytest.mark.parametrize("seed", range(4700, 4703))
 def test_wide_after_writes_clone_and_persist(seed, monkeypatch, tmp_path):
     """A wide snapshot (32 GiB, 128-B root units) after writes, then cloned and saved / loaded (both
     lay the arena out afresh, wide again): every copy decides and expands like the narrow snapshot at
