@@ -4712,10 +4712,9 @@ void check_locked(Snapshot& S, DeviceState& D, const keto_check_ids* dq, uint32_
                   hipStream_t st, const DevOverlay& dov, uint64_t* work_out, bool accumulate,
                   uint32_t* d_steps = nullptr, PipeStash* stash = nullptr, int wsi = 0) {
     const int32_t g = std::min<int32_t>(gmd, 65535);
-    // (the reachability pretest's indexes keep handles in 31 bits: arenas whose roots lie past 2^31
-    // units check deep batches without it)
-    const bool deep = n > 0 && g - 1 > 8 && S.part_mode != PART_MIGRATE && (uint64_t)D.n_units <= (uint64_t)EDGE_VAL &&
-                      D.root_g == 0;
+    // (the reachability pretest's indexes hold target handles only, below 2^31 in every layout; the
+    // split reads a request's row by hword, so split and wide arenas take it too)
+    const bool deep = n > 0 && g - 1 > 8 && S.part_mode != PART_MIGRATE;
     ItemWork iw;
     if (!deep || !reach_split(S, dq, n, gmd, da, dov.base, st, d_steps != nullptr, iw)) {
         check_core(S, D, dq, n, gmd, da, st, dov, work_out, accumulate, d_steps, stash, wsi, nullptr);

@@ -144,6 +144,7 @@ struct ReachDev {
     const uint32_t* post;
     uint32_t pn;              // pdir entries
     uint32_t ov_base;         // handles >= ov_base are batch-local overlay rows (never items)
+    uint32_t root_g;          // wide arenas: root handles past 2^31 (snapshot.hpp hword)
 };
 
 __device__ inline uint32_t win(const uint4& w, uint32_t i) {
@@ -152,12 +153,13 @@ __device__ inline uint32_t win(const uint4& w, uint32_t i) {
     return (i & 2u) ? hi : lo;
 }
 
-// a row's header (forwards followed) and window; beg = word index of its first edge
-__device__ inline void row_at(const uint32_t* a, uint32_t h, uint4& h0, uint4& h1, uint64_t& beg) {
-    uint64_t w = (uint64_t)h * HDR_WORDS;
+// a row's header (forwards followed) and window; beg = word index of its first edge (g: the arena's
+// root unit, hword; only a request's own row can be a root)
+__device__ inline void row_at(const uint32_t* a, uint32_t h, uint32_t g, uint4& h0, uint4& h1, uint64_t& beg) {
+    uint64_t w = hword(h, g);
     h0 = *reinterpret_cast<const uint4*>(a + w);
     while (h0.z & HDR_FWD) {
-        w = (uint64_t)h0.x * HDR_WORDS;
+        w = hword(h0.x, g);
         h0 = *reinterpret_cast<const uint4*>(a + w);
     }
     h1 = *reinterpret_cast<const uint4*>(a + w + HDR_WORDS);
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(256) split_count(ReachDev r, const keto_check_
     } else {
         uint4 h0, h1;
         uint64_t beg;
-        row_at(r.arena, qq.row, h0, h1, beg);
+        row_at(r.arena, qq.row, r.root_g, h0, h1, beg);
         if (h0.z & HDR_SEQ) {
             c = 1u | PASS;                                             // ordered walk of colliding keys
         } else if (holds_id(r.arena, h0, h1, beg, qq.target)) {
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(256) split_fill(ReachDev r, const keto_check_i
     if (d <= 0 || gmd < d) d = gmd;
     uint4 h0, h1;
     uint64_t beg;
-    row_at(r.arena, qq.row, h0, h1, beg);
+    row_at(r.arena, qq.row, r.root_g, h0, h1, beg);
     for (uint32_t j = 0; j < c; ++j) {
         const uint32_t e = j < WINDOW_WORDS ? win(h1, j) : r.arena[beg + j];
         work[o + j] = keto_check_ids{e & EDGE_VAL, qq.target, KETO_ITEM_FLAG, d - 1};
@@ -302,7 +304,7 @@ __device__ bool within(const ReachDev& r, const Pretest& P, uint64_t* M, uint32_
             for (uint32_t x = f0; x < f1; ++x) {
                 uint4 h0, h1;
                 uint64_t beg;
-                row_at(r.arena, F[x], h0, h1, beg);
+                row_at(r.arena, F[x], r.root_g, h0, h1, beg);
                 const uint32_t ns = h0.x;                // ROW_SEQ: every edge, sets and ids mixed
                 work += ns;
                 if (work > P.work_cap) return true;
@@ -468,7 +470,7 @@ __global__ void __launch_bounds__(64) pretest_wave_kernel(ReachDev r, const keto
                 };
                 auto gather = [&](Pf& p, uint32_t x) {
                     p.rl = RevList{RD_NONE, 0};
-                    if (x < nfw) row_at(r.arena, F[f0 + x], p.h0, p.h1, p.beg);
+                    if (x < nfw) row_at(r.arena, F[f0 + x], r.root_g, p.h0, p.h1, p.beg);
                     else if (x < nfw + nbw) p.rl.e = rdir_at(r.rdir, r.rn, Bat(b0 + x - nfw));
                 };
                 auto count = [&](Pf& p) {               // counts of reverse lists of 3+ parents
@@ -668,13 +670,25 @@ void build_index(const Snapshot& S, ReachState& R) {
     const uint32_t NR = S.n_rows();
     // every stored edge of every row on this device (a superset of the effective edges)
     auto edges_of = [&](uint32_t r) { return S.row_edges(r); };
+    // Only rows some subject set points at (row_cb: a target identity, kept while the row is one) go
+    // into the index, as parents and as rows holding an id.  An item's forward search reaches only
+    // targets (its own set is one), and a root row has no parent, so a backward path through a root
+    // ends there without meeting the forward side: leaving roots out drops no meeting, i.e. changes no
+    // kept item (and a T held by roots only now drops every item at once, as it should: no entered
+    // row can hold it).  It keeps every handle in the index below 2^31 (targets), so arenas whose
+    // roots lie past 2^31 units (split and wide layouts) take the pretest too, and it leaves out the
+    // postings of the documents, most of the index on the power-law graphs.
+    // (KETO_REACH_ROOTS=1, A/B tooling: roots too, as before round 6 -- arenas below 2^31 units only)
+    const char* er = getenv("KETO_REACH_ROOTS");
+    const bool roots_too = er && atoi(er) == 1 && S.n_units <= (uint64_t)EDGE_VAL;
+    auto kept = [&](uint32_t r) { return S.present(r) && (roots_too || (r < S.row_cb.size() && S.row_cb[r])); };
     uint32_t max_id = 0;
     {
         std::vector<uint32_t> mx(th, 0);
         par_chunks(NR, th, 1 << 14, [&](uint64_t b, uint64_t e, unsigned t) {
             uint32_t m = mx[t];
             for (uint64_t r = b; r < e; ++r) {
-                if (!S.present((uint32_t)r)) continue;
+                if (!kept((uint32_t)r)) continue;
                 const auto ed = edges_of((uint32_t)r);
                 for (uint64_t k = 0; k < ed.second; ++k) {
                     const uint32_t v = ed.first[k];
@@ -688,7 +702,7 @@ void build_index(const Snapshot& S, ReachState& R) {
     std::vector<uint32_t> indeg(NR, 0), idc((uint64_t)max_id + 1, 0);
     par_chunks(NR, th, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
         for (uint64_t r = b; r < e; ++r) {
-            if (!S.present((uint32_t)r)) continue;
+            if (!kept((uint32_t)r)) continue;
             const auto ed = edges_of((uint32_t)r);
             for (uint64_t k = 0; k < ed.second; ++k) {
                 const uint32_t v = ed.first[k];
@@ -724,7 +738,7 @@ void build_index(const Snapshot& S, ReachState& R) {
     std::vector<uint32_t> rev(std::max<uint64_t>(rw, 1)), post(std::max<uint64_t>(pw, 1));
     par_chunks(NR, th, 1 << 14, [&](uint64_t b, uint64_t e, unsigned) {
         for (uint64_t r = b; r < e; ++r) {
-            if (!S.present((uint32_t)r)) continue;
+            if (!kept((uint32_t)r)) continue;
             const uint32_t h = S.unit_of_row[r];
             const auto ed = edges_of((uint32_t)r);
             for (uint64_t k = 0; k < ed.second; ++k) {
@@ -821,7 +835,7 @@ bool reach_split(Snapshot& S, const keto_check_ids* dq, uint32_t n, int32_t gmd,
     HIP_OK(hipEventCreate(&ea));
     HIP_OK(hipEventCreate(&eb));
     HIP_OK(hipEventRecord(e0, st));
-    const ReachDev rd{V.arena, R.rdir, R.rev, R.rn, R.pdir, R.post, R.pn, ov_base};
+    const ReachDev rd{V.arena, R.rdir, R.rev, R.rn, R.pdir, R.post, R.pn, ov_base, S.root_g};
     uint32_t* acc = R.acc.get<uint32_t>(n);
     uint32_t* cnt = R.cnt.get<uint32_t>((uint64_t)n + 1);
     uint32_t* off = R.off.get<uint32_t>((uint64_t)n + 1);

@@ -11,8 +11,8 @@ segments 4 and 5), at ~100 GiB (64-B units, segments 6 and 7) and at 48 GiB forc
 (KETO_TEST_ROOT_G), each a real device allocation of that size.
 
 Every decision and tree is compared with the oracle (or with the same graph in an ordinary layout):
-checks at max-depth 5 (tier 0), 9 (the 8-frame tier 0) and 16 (check_kernel; the reachability
-pretest is off past 2^31 units), subject-set requests naming root rows (handles past 2^31, never
+checks at max-depth 5 (tier 0), 9 (the 8-frame tier 0), 16 and 32 (top-level items, the reachability
+pretest -- whose index holds target handles only, below 2^31 in every layout -- and check_kernel), subject-set requests naming root rows (handles past 2^31, never
 allowed: no tuple has them as subject), expand trees rooted at high rows, the streamed pair form, and
 writes interleaved with checks and expands against the SQL oracle."""
 import os
@@ -83,7 +83,7 @@ def test_split_layout_places_roots_high(split):
         assert snap.stats()["device_bytes"] > (LAYOUTS[snap.layout][0] * 4)
 
 
-@pytest.mark.parametrize("gmd", [5, 9, 16])
+@pytest.mark.parametrize("gmd", [5, 9, 16, 32])
 def test_split_checks_match_oracle(split, gmd):
     g, snap, _ = split
     q = g.queries(20000, seed=700 + gmd, depth=gmd)
