@@ -50,14 +50,20 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def _engine_build_id():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_keto_build", os.path.join(ROOT, "keto_amd", "build.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.engine_build_id()
+
+
 def pmc_traffic(kernel_name, workload):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC passes
     (profiles/*_traffic.json, written by tools/traffic.py from tools/gpu_round.sh), used only when
-    they were measured on this engine.hip and this workload; else None."""
+    they were measured on this engine.hip, built with these flags, and this workload; else None."""
     import glob
-    import hashlib
-    with open(os.path.join(ROOT, "keto_amd", "csrc", "engine.hip"), "rb") as f:
-        sha = hashlib.sha256(f.read()).hexdigest()
+    sha = _engine_build_id()
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         try:
             j = json.load(open(p))

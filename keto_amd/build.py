@@ -11,6 +11,21 @@ ARCH = "gfx950"
 SOURCES = ["snapshot.cpp", "resolve.cpp", "delta.cpp", "persist.cpp", "capi.cpp", "engine.hip", "route.hip", "migrate.hip", "proto.hip", "reach.hip", "resolve_dev.hip", "comm.cpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 HOST_HIP = ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]   # host-only sources using the HIP / RCCL APIs
+# engine.hip (tier 0, the deep tier, expand) is scheduled for memory clauses: the latency-bound deep
+# tier's independent loads issue back to back (config #3 126-128 -> 121 ms, tier 0 and config #5
+# unchanged, A/B on one box: profiles/r06zzc_configs_compiler_flags.txt, r06zzb_*)
+SOURCE_FLAGS = {"engine.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+
+
+def engine_build_id():
+    """sha256 of engine.hip and its compile flags: keys the committed PMC traffic profiles
+    (tools/traffic.py writes it, bench.py matches it)."""
+    import hashlib
+    h = hashlib.sha256(open(os.path.join(CSRC, "engine.hip"), "rb").read())
+    flags = SOURCE_FLAGS.get("engine.hip", [])
+    if flags:
+        h.update(b"\0" + " ".join(flags).encode())
+    return h.hexdigest()
 
 
 def _stale(target, deps):
@@ -22,7 +37,7 @@ def _stale(target, deps):
 
 def build(verbose=False, force=False):
     deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "parallel.hpp"), os.path.join(CSRC, "snapshot.hpp"), os.path.join(CSRC, "capi_internal.hpp"),
-                                                        os.path.join(HERE, "..", "include", "keto_mi355x.h")]
+                                                        os.path.join(HERE, "..", "include", "keto_mi355x.h"), os.path.abspath(__file__)]
     if not force and not _stale(OUT, deps):
         return OUT
     objs = []
@@ -32,7 +47,7 @@ def build(verbose=False, force=False):
         objs.append(obj)
         if not force and not _stale(obj, [path] + deps[len(SOURCES):]):
             continue
-        cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, "-c", path, "-o", obj]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, *SOURCE_FLAGS.get(src, []), "-c", path, "-o", obj]
         if src.endswith(".cpp"):
             cmd = [HIPCC, *CXXFLAGS, *HOST_HIP, "-x", "c++", "-c", path, "-o", obj]
         if verbose:
@@ -61,7 +76,7 @@ def build_variant(name, defines):
         if src.endswith(".cpp"):
             cmd = [HIPCC, *CXXFLAGS, *HOST_HIP, *flags, "-x", "c++", "-c", path, "-o", obj]
         else:
-            cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, *flags, "-c", path, "-o", obj]
+            cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, *SOURCE_FLAGS.get(src, []), *flags, "-c", path, "-o", obj]
         subprocess.check_call(cmd)
         objs.append(obj)
     out = os.path.join(vdir, f"lib_{name}.so")

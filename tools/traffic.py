@@ -9,11 +9,10 @@ PMC passes).  Correction (calibrated with tools/calib.hip on an MI355X, profiles
 FETCH_SIZE tallies 64 B per L2 miss while every miss is a 128-B DRAM read (TCC_EA0_RDREQ_128B =
 TCC_EA0_RDREQ), for streaming reads and for random 4-16 B gathers alike, so read bytes =
 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 is taken as is.
-The json carries the sha256 of engine.hip, so bench.py only uses it for the kernel it was measured on.
+The json carries the sha256 of engine.hip and its compile flags, so bench.py only uses it for the kernel it was measured on.
 """
 import collections
 import csv
-import hashlib
 import json
 import os
 import sys
@@ -22,8 +21,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def engine_sha():
-    with open(os.path.join(ROOT, "keto_amd", "csrc", "engine.hip"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_keto_build", os.path.join(ROOT, "keto_amd", "build.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.engine_build_id()   # engine.hip and its compile flags
 
 
 def pmc(path, counter, kernel):
