@@ -188,3 +188,18 @@ def test_string_table_grows_across_chunks(tmp_path):
         assert snap.stats()["n_strings"] == st["n_strings"]
     s.apply([(1, "n0_0", "view", "late")])
     assert s.resolve_checks([("docs", "n0_0", "view", ("id", "late"), 0)])[0]["target"][0] == st["n_strings"]
+
+
+def test_engine_build_id_keys_traffic_profiles():
+    """The PMC traffic profiles bench.py reports as `roofline.traffic` are keyed on engine.hip and its
+    compile flags (keto_amd/build.py SOURCE_FLAGS): the key changes with the flags, and a committed
+    profile exists for the build as it stands, so the round's bench line carries measured traffic."""
+    import glob
+    import hashlib
+    import json
+    from keto_amd import build
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(build.CSRC, "engine.hip"), "rb").read()
+    assert build.engine_build_id() != hashlib.sha256(src).hexdigest() or not build.SOURCE_FLAGS.get("engine.hip")
+    keys = [json.load(open(p)).get("engine_sha256") for p in glob.glob(os.path.join(root, "profiles", "*_traffic.json"))]
+    assert build.engine_build_id() in keys
