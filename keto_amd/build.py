@@ -11,10 +11,12 @@ ARCH = "gfx950"
 SOURCES = ["snapshot.cpp", "resolve.cpp", "delta.cpp", "persist.cpp", "capi.cpp", "engine.hip", "route.hip", "migrate.hip", "proto.hip", "reach.hip", "resolve_dev.hip", "comm.cpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 HOST_HIP = ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]   # host-only sources using the HIP / RCCL APIs
-# engine.hip (tier 0, the deep tier, expand) is scheduled for memory clauses: the latency-bound deep
-# tier's independent loads issue back to back (config #3 126-128 -> 121 ms, tier 0 and config #5
-# unchanged, A/B on one box: profiles/r06zzc_configs_compiler_flags.txt, r06zzb_*)
-SOURCE_FLAGS = {"engine.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+# engine.hip (tier 0, the deep tier, expand) and migrate.hip (the migrating walk) are scheduled for
+# memory clauses: the latency-bound walks' independent loads issue back to back (config #3 126-128 ->
+# 121 ms, P = 8 migrating parts 18.1-19.2 -> 17.3-18.1 ms; tier 0 and config #5 unchanged; A/B on one
+# box: profiles/r06zzc_configs_compiler_flags.txt, r06zze_migrate_compiler_flags.txt, r06zzb_*)
+_MEM_CLAUSE = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
+SOURCE_FLAGS = {"engine.hip": _MEM_CLAUSE, "migrate.hip": _MEM_CLAUSE}
 
 
 def engine_build_id():
